@@ -1,0 +1,421 @@
+// ref_harness.cpp — golden-vector generator that runs the REFERENCE's arithmetic on LibTorch CPU.
+//
+// TEST INFRASTRUCTURE ONLY: built by oracle/Makefile into oracle/_ref/ (git-ignored), run once to
+// write tests/golden/*. Nothing in the product links or loads it.
+//
+// What is the reference here:
+//   * include/rl_utils.h (Normal / Dirichlet / Beta) is compiled AS-IS from /root/reference
+//     (-I/root/reference/include) — the distributions are the reference's own code.
+//   * The agents and the loss/update arithmetic live inline in the reference's main() functions,
+//     which cannot be compiled here (boost, MPI, MuJoCo, protobuf are absent). They are replayed
+//     with the same LibTorch calls, in the same order, as:
+//       ppo_continuous_action.cpp:120-157 (AgentImpl), :447-467 (GAE), :489-540 (update)
+//       ac_ppo_continuous_action.cpp:150-249 (AgentImpl), :803-888 (update, distributed adv norm)
+//   * LibTorch is the pip wheel's 2.10 CPU build (reference pins 2.4.1); ATen formulas for addmm,
+//     tanh, layer_norm, softplus, lgamma/digamma, clip_grad_norm_ and Adam are unchanged across
+//     those versions. RNG streams are not used: every random input is injected.
+#include <rl_utils.h>
+#include <torch/torch.h>
+
+#include <cstdio>
+#include <filesystem>
+#include <fstream>
+#include <random>
+#include <sstream>
+#include <string>
+#include <vector>
+
+using torch::Tensor;
+namespace nn = torch::nn;
+
+static std::string g_out;
+static std::ostringstream g_manifest;
+static bool g_first_case = true;
+static bool g_first_entry = true;
+
+static void begin_case(const std::string& name, const std::string& meta_json) {
+  g_manifest << (g_first_case ? "" : ",\n") << "  \"" << name << "\": {\"meta\": " << meta_json << ", \"arrays\": {";
+  g_first_case = false;
+  g_first_entry = true;
+  std::filesystem::create_directories(g_out + "/" + name);
+}
+static void end_case() { g_manifest << "}}"; }
+
+static void dump(const std::string& cname, const std::string& name, const Tensor& t0) {
+  Tensor t = t0.detach().contiguous();
+  std::string dt;
+  if (t.scalar_type() == torch::kFloat32) dt = "f32";
+  else if (t.scalar_type() == torch::kInt64) dt = "i64";
+  else { t = t.to(torch::kFloat32); dt = "f32"; }
+  std::string path = g_out + "/" + cname + "/" + name + "." + dt;
+  std::ofstream f(path, std::ios::binary);
+  f.write(reinterpret_cast<const char*>(t.data_ptr()), t.numel() * t.element_size());
+  g_manifest << (g_first_entry ? "" : ", ") << "\"" << name << "\": {\"dtype\": \"" << dt << "\", \"shape\": [";
+  for (int64_t i = 0; i < t.dim(); ++i) g_manifest << (i ? ", " : "") << t.size(i);
+  g_manifest << "]}";
+  g_first_entry = false;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Agents (same module structure / registration order as the reference, so named_parameters()
+// order equals the reference's flat order).
+// ---------------------------------------------------------------------------------------------
+struct PPOAgentImpl : nn::Module {  // ppo_continuous_action.cpp:120-157
+  nn::Sequential critic{nullptr}, actor_mean{nullptr};
+  Tensor actor_logstd;
+  PPOAgentImpl(int O, int A, int H) {
+    critic = register_module("critic", nn::Sequential(nn::Linear(O, H), nn::Tanh(), nn::Linear(H, H), nn::Tanh(),
+                                                      nn::Linear(H, 1)));
+    actor_mean = register_module("actor_mean", nn::Sequential(nn::Linear(O, H), nn::Tanh(), nn::Linear(H, H),
+                                                              nn::Tanh(), nn::Linear(H, A)));
+    actor_logstd = register_parameter("actor_logstd", torch::zeros({1, A}, torch::kFloat32));
+  }
+  Tensor get_value(const Tensor& x) { return critic->forward(x); }
+  std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> get_action_and_value(const Tensor& x, const Tensor& action) {
+    const Tensor action_mean = actor_mean->forward(x);
+    const Tensor action_logstd = actor_logstd.expand_as(action_mean);
+    const Tensor action_std = torch::exp(action_logstd);
+    const Normal probs(action_mean, action_std);
+    Tensor logprob = probs.log_prob(action).sum(1);
+    Tensor entropy = probs.entropy().sum(1);
+    Tensor value = critic->forward(x);
+    return {action, logprob, entropy, value, action_mean};
+  }
+};
+TORCH_MODULE(PPOAgent);
+
+struct ACAgentImpl : nn::Module {  // ac_ppo_continuous_action.cpp:150-249
+  nn::Sequential critic{nullptr}, actor_encoder{nullptr}, dist_alpha{nullptr}, dist_beta{nullptr};
+  Tensor action_space_high, action_space_low, mean_, std_;
+  ACAgentImpl(int O, int A, int H, float high, float low, Tensor mean, Tensor std) {
+    action_space_high = register_parameter("action_space_high", torch::tensor(high), false);
+    action_space_low = register_parameter("action_space_low", torch::tensor(low), false);
+    mean_ = register_parameter("mean_", mean.unsqueeze(0), false);
+    std_ = register_parameter("std_", std.unsqueeze(0), false);
+    critic = register_module("critic", nn::Sequential(nn::Linear(O, H), nn::LayerNorm(nn::LayerNormOptions({H})),
+                                                      nn::ReLU(), nn::Linear(H, H),
+                                                      nn::LayerNorm(nn::LayerNormOptions({H})), nn::ReLU(),
+                                                      nn::Linear(H, 1)));
+    actor_encoder = register_module(
+        "actor_mean", nn::Sequential(nn::Linear(O, H), nn::LayerNorm(nn::LayerNormOptions({H})), nn::ReLU(),
+                                     nn::Linear(H, H), nn::LayerNorm(nn::LayerNormOptions({H})), nn::ReLU()));
+    dist_alpha = register_module("dist_alpha", nn::Sequential(nn::Linear(H, A)));
+    dist_beta = register_module("dist_beta", nn::Sequential(nn::Linear(H, A)));
+  }
+  Tensor scale_action(const Tensor& action) const {
+    constexpr float d_low = 0.0f, d_high = 1.0f, eps = 1e-7;
+    Tensor s = (action - action_space_low) / (action_space_high - action_space_low) * (d_high - d_low) + d_low;
+    return torch::clamp(s, d_low + eps, d_high + eps);
+  }
+  Tensor unscale_action(const Tensor& action) const {
+    constexpr float d_low = 0.0f, d_high = 1.0f;
+    return (action - d_low) / (d_high - d_low) * (action_space_high - action_space_low) + action_space_low;
+  }
+  // mode: "given" (update path) or "mean" (eval path)
+  std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> get_action_and_value(const Tensor& x, Tensor action,
+                                                                                  const std::string& mode) {
+    Tensor xn = (x - mean_) / std_;
+    Tensor feat = actor_encoder->forward(xn);
+    Tensor alpha = nn::functional::softplus(dist_alpha->forward(feat)) + 1.0f;
+    Tensor beta = nn::functional::softplus(dist_beta->forward(feat)) + 1.0f;
+    const Beta probs(alpha, beta);
+    if (mode == "mean") action = probs.mean();
+    else action = scale_action(action);
+    Tensor logprob = probs.log_prob(action).sum(1);
+    action = unscale_action(action);
+    Tensor entropy = probs.entropy().sum(1);
+    Tensor value = critic->forward(xn);
+    return {action, logprob, entropy, value, alpha, beta};
+  }
+};
+TORCH_MODULE(ACAgent);
+
+// ---------------------------------------------------------------------------------------------
+// Deterministic inputs
+// ---------------------------------------------------------------------------------------------
+static std::mt19937 g_rng(1234);
+static Tensor randn(std::vector<int64_t> shape, float scale = 1.0f) {
+  std::normal_distribution<float> d(0.0f, 1.0f);
+  Tensor t = torch::empty(shape, torch::kFloat32);
+  float* p = t.data_ptr<float>();
+  for (int64_t i = 0; i < t.numel(); ++i) p[i] = d(g_rng) * scale;
+  return t;
+}
+static Tensor randu(std::vector<int64_t> shape, float lo, float hi) {
+  std::uniform_real_distribution<float> d(lo, hi);
+  Tensor t = torch::empty(shape, torch::kFloat32);
+  float* p = t.data_ptr<float>();
+  for (int64_t i = 0; i < t.numel(); ++i) p[i] = d(g_rng);
+  return t;
+}
+
+// Fill every parameter with deterministic values of a sensible scale and return the flat vector
+// in named_parameters() order (and the names, for the manifest).
+static Tensor set_params(nn::Module& m, std::string& names_json) {
+  torch::NoGradGuard ng;
+  std::vector<Tensor> flat;
+  names_json = "[";
+  bool first = true;
+  for (auto& kv : m.named_parameters()) {
+    Tensor p = kv.value();
+    const std::string& n = kv.key();
+    Tensor v;
+    if (n == "action_space_high") v = torch::tensor(1.0f);
+    else if (n == "action_space_low") v = torch::tensor(-1.0f);
+    else if (n == "mean_") v = randn(p.sizes().vec(), 0.1f);
+    else if (n == "std_") v = randu(p.sizes().vec(), 0.8f, 1.5f);
+    else if (n == "actor_logstd") v = randu(p.sizes().vec(), -0.7f, -0.3f);
+    else if (n.find("weight") != std::string::npos && p.dim() == 1) v = randu(p.sizes().vec(), 0.8f, 1.2f);  // LN gamma
+    else if (n.find("weight") != std::string::npos) v = randn(p.sizes().vec(), 1.0f / std::sqrt((float)p.size(1)));
+    else v = randn(p.sizes().vec(), 0.1f);  // biases / LN beta
+    p.copy_(v.reshape(p.sizes()));
+    flat.push_back(p.detach().reshape({-1}).clone());
+    names_json += std::string(first ? "" : ", ") + "[\"" + n + "\", " + std::to_string(p.numel()) + ", " +
+                  (p.requires_grad() ? "1" : "0") + "]";
+    first = false;
+  }
+  names_json += "]";
+  return torch::cat(flat);
+}
+
+static Tensor flat_grads(nn::Module& m) {
+  std::vector<Tensor> g;
+  for (auto& p : m.parameters()) {
+    if (p.grad().defined()) g.push_back(p.grad().detach().reshape({-1}).clone());
+    else g.push_back(torch::zeros({p.numel()}));
+  }
+  return torch::cat(g);
+}
+static Tensor flat_params(nn::Module& m) {
+  std::vector<Tensor> g;
+  for (auto& p : m.parameters()) g.push_back(p.detach().reshape({-1}).clone());
+  return torch::cat(g);
+}
+static Tensor flat_state(torch::optim::Adam& opt, bool sq) {
+  std::vector<Tensor> out;
+  for (auto& p : opt.param_groups()[0].params()) {
+    auto it = opt.state().find(p.unsafeGetTensorImpl());
+    if (it == opt.state().end()) { out.push_back(torch::zeros({p.numel()})); continue; }
+    auto& st = static_cast<torch::optim::AdamParamState&>(*it->second);
+    out.push_back((sq ? st.exp_avg_sq() : st.exp_avg()).reshape({-1}).clone());
+  }
+  return torch::cat(out);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Losses (ppo:497-535 ; ac:817-872 with world_size = G emulated by row shards)
+// ---------------------------------------------------------------------------------------------
+struct LossCfg { float clip_coef, ent_coef, vf_coef; bool clip_vloss, norm_adv; };
+
+static std::tuple<Tensor, std::vector<float>> ppo_loss(const Tensor& newlogprob, const Tensor& entropy,
+                                                       Tensor newvalue, const Tensor& old_logp, Tensor mb_adv,
+                                                       const Tensor& ret, const Tensor& old_v, const LossCfg& c,
+                                                       const Tensor* adv_mean, const Tensor* adv_std) {
+  Tensor logratio = newlogprob - old_logp;
+  Tensor ratio = logratio.exp();
+  Tensor old_approx_kl, approx_kl;
+  float clipfrac;
+  {
+    torch::NoGradGuard ng;
+    old_approx_kl = (-logratio).mean();
+    approx_kl = ((ratio - 1.0f) - logratio).mean();
+    clipfrac = ((ratio - 1.0f).abs() > c.clip_coef).to(torch::kFloat).mean().item<float>();
+  }
+  if (c.norm_adv) {
+    if (adv_mean) mb_adv = (mb_adv - *adv_mean) / (*adv_std + 1e-8);  // distributed form (ac:848)
+    else mb_adv = (mb_adv - mb_adv.mean()) / (mb_adv.std() + 1e-8);   // ppo:511
+  }
+  Tensor pg_loss1 = -mb_adv * ratio;
+  Tensor pg_loss2 = -mb_adv * torch::clamp(ratio, 1.0f - c.clip_coef, 1.0f + c.clip_coef);
+  Tensor pg_loss = torch::max(pg_loss1, pg_loss2).mean();
+  newvalue = newvalue.view(-1);
+  Tensor v_loss;
+  if (c.clip_vloss) {
+    Tensor v_loss_unclipped = torch::pow(newvalue - ret, 2);
+    Tensor v_clipped = old_v + torch::clamp(newvalue - old_v, -c.clip_coef, c.clip_coef);
+    Tensor v_loss_clipped = torch::pow(v_clipped - ret, 2);
+    v_loss = 0.5f * torch::max(v_loss_unclipped, v_loss_clipped).mean();
+  } else {
+    v_loss = 0.5 * torch::pow(newvalue - ret, 2).mean();
+  }
+  Tensor entropy_loss = entropy.mean();
+  Tensor loss = pg_loss - c.ent_coef * entropy_loss + v_loss * c.vf_coef;
+  std::vector<float> st = {pg_loss.item<float>(),      v_loss.item<float>(),   entropy_loss.item<float>(),
+                           old_approx_kl.item<float>(), approx_kl.item<float>(), clipfrac, loss.item<float>()};
+  return {loss, st};
+}
+
+// ---------------------------------------------------------------------------------------------
+int main(int argc, char** argv) {
+  torch::set_num_threads(1);
+  g_out = argc > 1 ? argv[1] : "tests/golden";
+  std::filesystem::create_directories(g_out);
+  g_manifest << "{\n";
+  const int O = 17, A = 6, H = 64, M = 64;
+
+  // ---- PPO agent: act + update ----------------------------------------------------------
+  {
+    PPOAgent agent(O, A, H);
+    std::string names;
+    Tensor p0 = set_params(*agent, names);
+    Tensor x = randn({M, O});
+    Tensor act = randn({M, A}, 0.8f);
+    begin_case("ppo_act", "{\"kind\": 0, \"O\": 17, \"A\": 6, \"H\": 64, \"n\": 64, \"params\": " + names + "}");
+    {
+      torch::NoGradGuard ng;
+      auto [a, lp, ent, v, mu] = agent->get_action_and_value(x, act);
+      dump("ppo_act", "params", p0); dump("ppo_act", "x", x); dump("ppo_act", "action", act);
+      dump("ppo_act", "logprob", lp); dump("ppo_act", "entropy", ent); dump("ppo_act", "value", v.view(-1));
+      dump("ppo_act", "mean", mu);
+    }
+    end_case();
+
+    LossCfg c{0.2f, 0.01f, 0.5f, true, true};
+    Tensor old_logp, adv = randn({M}), ret = randn({M}), old_v;
+    {
+      torch::NoGradGuard ng;
+      auto [a, lp, ent, v, mu] = agent->get_action_and_value(x, act);
+      old_logp = lp + randn({M}, 0.15f);
+      old_v = v.view(-1) + randn({M}, 0.15f);
+    }
+    torch::optim::Adam opt(agent->parameters(), torch::optim::AdamOptions(3e-4).eps(1e-5));
+    begin_case("ppo_update", "{\"kind\": 0, \"O\": 17, \"A\": 6, \"H\": 64, \"M\": 64, \"clip_coef\": 0.2, "
+                             "\"ent_coef\": 0.01, \"vf_coef\": 0.5, \"clip_vloss\": 1, \"norm_adv\": 1, "
+                             "\"max_grad_norm\": 0.5, \"lr\": 0.0003, \"adam_eps\": 1e-05}");
+    dump("ppo_update", "params", p0); dump("ppo_update", "x", x); dump("ppo_update", "action", act);
+    dump("ppo_update", "old_logp", old_logp); dump("ppo_update", "adv", adv); dump("ppo_update", "ret", ret);
+    dump("ppo_update", "old_v", old_v);
+    for (int s = 1; s <= 3; ++s) {
+      auto [a, lp, ent, v, mu] = agent->get_action_and_value(x, act);
+      auto [loss, st] = ppo_loss(lp, ent, v, old_logp, adv, ret, old_v, c, nullptr, nullptr);
+      opt.zero_grad();
+      loss.backward();
+      if (s == 1) { dump("ppo_update", "grad_raw", flat_grads(*agent)); dump("ppo_update", "stats", torch::tensor(st)); }
+      double tn = torch::nn::utils::clip_grad_norm_(agent->parameters(), 0.5);
+      if (s == 1) { dump("ppo_update", "grad_clipped", flat_grads(*agent)); dump("ppo_update", "total_norm", torch::tensor({(float)tn})); }
+      opt.step();
+      if (s == 1) dump("ppo_update", "params_step1", flat_params(*agent));
+    }
+    dump("ppo_update", "params_step3", flat_params(*agent));
+    dump("ppo_update", "adam_m_step3", flat_state(opt, false));
+    dump("ppo_update", "adam_v_step3", flat_state(opt, true));
+    end_case();
+  }
+
+  // ---- AC agent: act (given + mean) + update + distributed equivalence ---------------------
+  {
+    Tensor mean = randn({O}, 0.1f), stdv = randu({O}, 0.8f, 1.5f);
+    ACAgent agent(O, A, H, 1.0f, -1.0f, mean, stdv);
+    std::string names;
+    Tensor p0 = set_params(*agent, names);
+    Tensor x = randn({M, O});
+    Tensor act = randu({M, A}, -0.98f, 0.98f);
+    begin_case("ac_act", "{\"kind\": 1, \"O\": 17, \"A\": 6, \"H\": 64, \"n\": 64, \"params\": " + names + "}");
+    {
+      torch::NoGradGuard ng;
+      auto [a, lp, ent, v, al, be] = agent->get_action_and_value(x, act, "given");
+      dump("ac_act", "params", p0); dump("ac_act", "x", x); dump("ac_act", "action", act);
+      dump("ac_act", "logprob", lp); dump("ac_act", "entropy", ent); dump("ac_act", "value", v.view(-1));
+      dump("ac_act", "alpha", al); dump("ac_act", "beta", be); dump("ac_act", "action_roundtrip", a);
+      auto [am, lpm, entm, vm, alm, bem] = agent->get_action_and_value(x, Tensor(), "mean");
+      dump("ac_act", "mean_action", am); dump("ac_act", "mean_logprob", lpm);
+    }
+    end_case();
+
+    LossCfg c{0.1f, 0.01f, 0.5f, true, true};
+    Tensor old_logp, adv = randn({M}), ret = randn({M}), old_v;
+    {
+      torch::NoGradGuard ng;
+      auto [a, lp, ent, v, al, be] = agent->get_action_and_value(x, act, "given");
+      old_logp = lp + randn({M}, 0.1f);
+      old_v = v.view(-1) + randn({M}, 0.1f);
+    }
+    torch::optim::Adam opt(agent->parameters(), torch::optim::AdamOptions(2.5e-4).eps(1e-5));
+    begin_case("ac_update", "{\"kind\": 1, \"O\": 17, \"A\": 6, \"H\": 64, \"M\": 64, \"clip_coef\": 0.1, "
+                            "\"ent_coef\": 0.01, \"vf_coef\": 0.5, \"clip_vloss\": 1, \"norm_adv\": 1, "
+                            "\"max_grad_norm\": 0.5, \"lr\": 0.00025, \"adam_eps\": 1e-05}");
+    dump("ac_update", "params", p0); dump("ac_update", "x", x); dump("ac_update", "action", act);
+    dump("ac_update", "old_logp", old_logp); dump("ac_update", "adv", adv); dump("ac_update", "ret", ret);
+    dump("ac_update", "old_v", old_v);
+    // G = 2 equivalence (ac:830-849, :877-885): two row shards, distributed adv stats, avg grads
+    {
+      Tensor gsum;
+      const int G = 2, Md = M / G;
+      std::vector<Tensor> means;
+      for (int r = 0; r < G; ++r) means.push_back(adv.slice(0, r * Md, (r + 1) * Md).mean());
+      Tensor amean = (means[0] + means[1]) / 2.0f;  // ncclAvg
+      Tensor ssum = torch::zeros({});
+      for (int r = 0; r < G; ++r) ssum = ssum + torch::sum(torch::square(adv.slice(0, r * Md, (r + 1) * Md) - amean));
+      Tensor astd = torch::sqrt(ssum / static_cast<float>(G * Md - 1));
+      for (int r = 0; r < G; ++r) {
+        auto sl = [&](const Tensor& t) { return t.slice(0, r * Md, (r + 1) * Md); };
+        auto [a, lp, ent, v, al, be] = agent->get_action_and_value(sl(x), sl(act), "given");
+        auto [loss, st] = ppo_loss(lp, ent, v, sl(old_logp), sl(adv), sl(ret), sl(old_v), c, &amean, &astd);
+        opt.zero_grad();
+        loss.backward();
+        Tensor g = flat_grads(*agent);
+        gsum = gsum.defined() ? gsum + g : g;
+      }
+      dump("ac_update", "grad_dist2_avg", gsum / 2.0f);
+      dump("ac_update", "dist2_adv_stats", torch::stack({amean, astd}));
+    }
+    for (int s = 1; s <= 3; ++s) {
+      auto [a, lp, ent, v, al, be] = agent->get_action_and_value(x, act, "given");
+      auto [loss, st] = ppo_loss(lp, ent, v, old_logp, adv, ret, old_v, c, nullptr, nullptr);
+      opt.zero_grad();
+      loss.backward();
+      if (s == 1) { dump("ac_update", "grad_raw", flat_grads(*agent)); dump("ac_update", "stats", torch::tensor(st)); }
+      double tn = torch::nn::utils::clip_grad_norm_(agent->parameters(), 0.5);
+      if (s == 1) { dump("ac_update", "grad_clipped", flat_grads(*agent)); dump("ac_update", "total_norm", torch::tensor({(float)tn})); }
+      opt.step();
+      if (s == 1) dump("ac_update", "params_step1", flat_params(*agent));
+    }
+    dump("ac_update", "params_step3", flat_params(*agent));
+    end_case();
+  }
+
+  // ---- GAE (ppo:447-467) -------------------------------------------------------------------
+  {
+    const int T = 64, E = 16;
+    const float gamma = 0.99f, gae_lambda = 0.95f;
+    Tensor rewards = randn({T, E}), values = randn({T, E});
+    Tensor dones = (randu({T, E}, 0.0f, 1.0f) < 0.05f).to(torch::kFloat32);
+    dones.index_put_({0}, 1.0f);
+    dones.index_put_({T - 1, torch::indexing::Slice(0, E / 2)}, 1.0f);
+    Tensor next_value = randn({E});
+    Tensor next_done = (randu({E}, 0.0f, 1.0f) < 0.5f).to(torch::kFloat32);
+    Tensor advantages = torch::zeros({T, E});
+    Tensor lastgaelam = torch::zeros({E});
+    Tensor nextnonterminal, nextvalues;
+    for (int t = T - 1; t >= 0; --t) {
+      if (t == T - 1) { nextnonterminal = 1.0f - next_done; nextvalues = next_value; }
+      else { nextnonterminal = 1.0 - dones.index({t + 1}); nextvalues = values.index({t + 1}); }
+      Tensor delta = rewards.index({t}) + gamma * nextvalues * nextnonterminal - values.index({t});
+      advantages.index({t}) = delta + gamma * gae_lambda * nextnonterminal * lastgaelam;
+      lastgaelam = advantages.index({t});
+    }
+    Tensor returns = advantages + values;
+    begin_case("gae", "{\"T\": 64, \"E\": 16, \"gamma\": 0.99, \"gae_lambda\": 0.95}");
+    dump("gae", "rewards", rewards); dump("gae", "values", values); dump("gae", "dones", dones);
+    dump("gae", "next_value", next_value); dump("gae", "next_done", next_done);
+    dump("gae", "advantages", advantages); dump("gae", "returns", returns);
+    end_case();
+  }
+
+  // ---- Distribution spot values straight from rl_utils.h ------------------------------------
+  {
+    torch::NoGradGuard ng;
+    Tensor al = randu({256}, 1.0f, 8.0f), be = randu({256}, 1.0f, 8.0f), xs = randu({256}, 0.01f, 0.99f);
+    const Beta b(al, be);
+    begin_case("beta_dist", "{\"n\": 256}");
+    dump("beta_dist", "alpha", al); dump("beta_dist", "beta", be); dump("beta_dist", "x", xs);
+    dump("beta_dist", "log_prob", b.log_prob(xs)); dump("beta_dist", "entropy", b.entropy());
+    dump("beta_dist", "mean", b.mean());
+    end_case();
+  }
+
+  g_manifest << "\n}\n";
+  std::ofstream(g_out + "/manifest.json") << g_manifest.str();
+  std::printf("golden fixtures written to %s\n", g_out.c_str());
+  return 0;
+}

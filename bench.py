@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""bench.py — env steps/s of the MI355X-native AC-PPO hot path (BASELINE.json metric).
+
+One "step" = one full PPO iteration of ac_ppo_continuous_action on HalfCheetah-v5 shapes
+(src/ac_ppo_continuous_action.cpp defaults: num_envs=4096, num_steps=128, num_minibatches=4,
+update_epochs=4): rollout of T steps (agent act + env step for every env), GAE, and 16 optimizer
+steps (gather, forward, loss, backward, grad all-reduce, clip_grad_norm_, Adam). The env is the
+device-resident synthetic HalfCheetah-shaped env (MuJoCo is not available), so inputs are resident
+in HBM when the timed region starts. value = env steps of all ranks / max-over-ranks wall time.
+
+Multi-GPU: one process per GPU (torch.distributed.run); the reference shards num_envs over ranks
+(num_envs_per_device = num_envs / world_size, ac:399), gradients are averaged with RCCL every
+minibatch — strong scaling by default, --scaling weak keeps num_envs per GPU.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ppo.cpp_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+
+import ppo_amd  # noqa: E402  (loads libppo_hip.so before torch, so one HIP runtime serves both)
+
+PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector peak (spec)
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "env steps/sec (SPS), HalfCheetah-v5 num_envs=4096 at 1/2/4/8 MI355X"
+
+
+def algorithmic_work(O, A, H, E, T, MB, nh):
+    """Algorithmic FLOPs / bytes per launch of each kernel (DESIGN.md 'Roofline accounting')."""
+    M = E * T // MB
+    fwd_row = (2 * O * H + 2 * H * H + 2 * H) + (2 * O * H + 2 * H * H + 2 * nh * H)
+    bwd_row = (2 * H + 2 * H * H + 2 * H) + (2 * nh * H + 2 * H * H + 2 * nh * H)  # dh, dW3, dh1 (dW1/dW2: k_dw)
+    return {
+        "fwdbwd": ("flop", M * (fwd_row + bwd_row)),
+        "dw_l2": ("flop", 2 * (2 * H * H * M)),
+        "dw_l1": ("flop", 2 * (2 * H * O * M)),
+        "act": ("flop", E * fwd_row),
+        "gae": ("byte", E * T * 4 * 5),  # reads r, v, d; writes adv, ret
+    }
+
+
+def cpu_baseline(E, T, MB, EP):
+    """The reference's CPU arithmetic on this host (1 intra-op thread, as ac:288 sets), bounded sample."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if os.path.exists(harness):
+        try:
+            out = subprocess.run([harness, "--bench", str(E), str(T), str(MB), str(EP), "2000"], capture_output=True,
+                                 text=True, timeout=300, check=True).stdout.strip().splitlines()[-1]
+            r = json.loads(out)
+            return {"value": round(r["sps"], 2), "unit": "env_steps/s", "cores": 1, "kind": "reference",
+                    "sample": (f"LibTorch CPU replay of the reference AC-PPO arithmetic (rl_utils.h Beta, 1 thread): "
+                               f"{r['n_act']} batch-1 get_action_and_value calls ({r['t_act_batch1_s']*1e3:.3f} ms each) "
+                               f"+ 1 optimizer step on M={r['M']} rows ({r['t_opt_step_s']:.2f} s) + GAE "
+                               f"({r['t_gae_s']*1e3:.1f} ms), extrapolated to one iteration ({E*T} acts, {EP*MB} "
+                               f"optimizer steps); env physics excluded")}
+        except Exception as e:  # noqa: BLE001
+            print(f"[bench] reference harness failed: {e}", file=sys.stderr)
+    # C restatement (oracle) — port baseline
+    import oracle_lib as O
+    L = O.layout_init(1, 17, 6, 256)
+    rng = np.random.default_rng(0)
+    p = (rng.standard_normal(L.P) * 0.05).astype(np.float32)
+    p[L.hi], p[L.lo] = 1.0, -1.0
+    p[L.ostd:L.ostd + 17] = 1.0
+    Ms = 2048
+    x = rng.standard_normal((Ms, 17)).astype(np.float32)
+    a = rng.uniform(-0.9, 0.9, (Ms, 6)).astype(np.float32)
+    cfg = O.LossCfg(0.1, 0.01, 0.5, 1, 1)
+    t0 = time.perf_counter()
+    O.minibatch_grad(L, p, x, a, np.zeros(Ms), rng.standard_normal(Ms), rng.standard_normal(Ms), np.zeros(Ms), cfg)
+    t_row = (time.perf_counter() - t0) / Ms
+    t0 = time.perf_counter()
+    O.get_action_and_value(L, p, x[:512], 0)
+    t_act = (time.perf_counter() - t0) / 512
+    B = E * T
+    t_iter = t_act * B + t_row * B * EP
+    return {"value": round(B / t_iter, 2), "unit": "env_steps/s", "cores": 1, "kind": "port",
+            "sample": f"C oracle: {Ms}-row minibatch gradient + 512 sampled acts, extrapolated to one iteration"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--num-envs", type=int, default=4096)
+    ap.add_argument("--num-steps", type=int, default=128)
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-all", action="store_true", help="HIP-event time every kernel class")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo (CPU) only for rendezvous, barriers and timing max
+        dist.init_process_group("gloo")
+    ppo_amd.set_device(local_rank)
+
+    E_total = args.num_envs if args.scaling == "strong" else args.num_envs * world
+    E = E_total // world
+    T = args.num_steps
+    cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=E_total, num_steps=T,
+                              total_timesteps=E_total * T * (args.steps + args.warmup + 1))
+    tr = ppo_amd.Trainer(cfg, num_envs_per_device=E, rank=rank, world_size=world)
+    if world > 1:
+        uid = [ppo_amd.Agent.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        tr.agent.comm_init(uid[0], rank, world)
+        tr.agent.comm_broadcast_params(0)
+
+    for _ in range(args.warmup):
+        tr.iterate()
+    tr.agent.sync()
+    # per-kernel HIP events on the context stream over the timed region (dominant kernel always)
+    mask = 0xFFFF if args.profile_all else (1 << 1)
+    tr.agent.profile_reset()
+    tr.agent.profile(mask)
+    if dist:
+        dist.barrier()
+    tr.agent.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.iterate()
+    tr.agent.sync()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tr.agent.profile(0)
+    prof = tr.agent.profile_read()
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    units = E_total * T * args.steps
+    value = units / elapsed
+    if rank == 0:
+        H, O_, A = 256, 17, 6
+        work = algorithmic_work(O_, A, H, E, T, cfg.num_minibatches, 2 * A)
+        roof = None
+        if prof:
+            name = max(prof, key=lambda k: prof[k][0])
+            ms, cnt = prof[name]
+            avg_s = ms / 1e3 / cnt
+            kind, amount = work.get(name, ("flop", 0))
+            if kind == "flop":
+                achieved = amount / avg_s / 1e12
+                roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F32_MFMA_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4), "traffic": None,
+                        "kernel": name, "avg_launch_ms": round(ms / cnt, 4), "launches": cnt,
+                        "algorithmic_per_launch": amount}
+            else:
+                achieved = amount / avg_s / 1e9
+                roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None, "kernel": name,
+                        "avg_launch_ms": round(ms / cnt, 4), "launches": cnt, "algorithmic_per_launch": amount}
+            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                try:
+                    tj = json.load(open(pmc))
+                    if name in tj and tj[name].get("config") == f"E={E},T={T}":
+                        roof["traffic"] = tj[name]["hbm_bytes_per_launch"]
+                except Exception:  # noqa: BLE001
+                    pass
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: device-resident HalfCheetah-shaped env (O=17, A=6), random-init AC agent",
+            "config": {"workload": f"ac_ppo_continuous_action HalfCheetah-v5 num_envs={E_total} num_steps={T} "
+                                   f"num_minibatches={cfg.num_minibatches} update_epochs={cfg.update_epochs}",
+                       "num_envs": E_total, "num_envs_per_device": E, "num_steps": T,
+                       "minibatch_per_device": E * T // cfg.num_minibatches, "parallelism": f"dp{world}"},
+            "roofline": roof,
+        }
+        if args.profile_all:
+            out["kernels_ms_per_step"] = {k: round(v[0] / args.steps, 3) for k, v in prof.items()}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(E, T, cfg.num_minibatches, cfg.update_epochs)
+        print(json.dumps(out), flush=True)
+    tr.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,144 @@
+/*
+ * ppo_hip.h — C-ABI of libppo_hip.so: the MI355X-native rollout -> GAE -> PPO-update hot path.
+ *
+ * Plain C: opaque handles, plain pointers and sizes, int status codes (0 = OK; on error
+ * ppo_last_error() returns a thread-local message). All `*_dev` pointers are HIP device pointers
+ * (allocate with ppo_dev_malloc or hipMalloc); `stream` arguments are hipStream_t passed as
+ * void* (NULL = the context's own stream). No LibTorch / torch types cross this boundary.
+ *
+ * What each entry point replaces in the reference (autonomousvision/ppo.cpp):
+ *   ppo_create / ppo_destroy         AgentImpl ctor + optim::Adam ctor + storage zeros
+ *                                    (ppo_continuous_action.cpp:338-364, ac_ppo_continuous_action.cpp:542-596)
+ *   ppo_load_params / ppo_save_params  torch::save(agent) / parameter broadcast source (ppo:173-180, ac:551-553)
+ *   ppo_get_action_and_value         Agent::get_action_and_value (ppo:145-157, ac:212-249) + Normal/Beta
+ *                                    (include/rl_utils.h:20-132)
+ *   ppo_get_value                    Agent::get_value (ppo:140-143, ac:188-192)
+ *   ppo_rollout_act                  one rollout step's agent half: obs/dones/actions/logprobs/values stores
+ *                                    (ppo:387-400, ac:649-660) for envs [env_begin, env_end)
+ *   ppo_rollout_reward               rewards[step] store (ppo:406, ac:668)
+ *   ppo_compute_gae                  next_value + GAE(lambda) + returns (ppo:447-467, ac:759-779)
+ *   ppo_update                       epochs x minibatches: randperm, gather, loss, backward, grad all-reduce,
+ *                                    clip_grad_norm_, Adam (ppo:489-542, ac:803-889)
+ *   ppo_comm_*                       torchfort::Comm (include/distributed.h:41-60, src/distributed.cpp:81-224)
+ *                                    re-designed as one RCCL communicator over xGMI
+ */
+#ifndef PPO_HIP_H
+#define PPO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ppo_layout.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ppo_ctx ppo_t;
+
+typedef struct ppo_hip_config {
+  int net_kind;         /* PPO_NET_TANH_NORMAL (ppo_continuous_action) / PPO_NET_LN_BETA (ac_ppo_...) */
+  int obs_dim, act_dim; /* environment observation / action space */
+  int hidden;           /* 64 (PPO agent) or 256 (AC agent) */
+  int num_envs;         /* envs on THIS device (num_envs_per_device, ac:399) */
+  int num_steps;        /* T (rollout length) */
+  int num_minibatches;  /* minibatch_per_device = T*num_envs / num_minibatches (ac:407) */
+  int update_epochs;
+  float gamma, gae_lambda;
+  float clip_coef, ent_coef, vf_coef, max_grad_norm, adam_eps;
+  int norm_adv, clip_vloss;
+  uint64_t seed;        /* Philox key for action sampling and minibatch permutations */
+  int rank, world_size; /* data-parallel position (envs sharded per rank, ac:398-407) */
+} ppo_hip_config;
+
+typedef struct ppo_update_stats {
+  float pg_loss, v_loss, entropy, old_approx_kl, approx_kl, clipfrac; /* last minibatch; clipfrac = mean */
+  float grad_norm;    /* total norm of the last minibatch (pre-clip) */
+  int minibatches;
+} ppo_update_stats;
+
+/* sample types for ppo_get_action_and_value (ac:225-238) */
+enum { PPO_SAMPLE = 0, PPO_MEAN = 1, PPO_GIVEN = 2 };
+
+/* storage buffers, all [T, E, *] row-major fp32 (ppo:357-364) */
+enum { PPO_BUF_OBS = 0, PPO_BUF_ACTIONS, PPO_BUF_LOGPROBS, PPO_BUF_REWARDS, PPO_BUF_DONES, PPO_BUF_VALUES,
+       PPO_BUF_ADVANTAGES, PPO_BUF_RETURNS, PPO_BUF_COUNT };
+
+const char* ppo_last_error(void);
+const char* ppo_version(void);
+
+int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
+int ppo_destroy(ppo_t* ctx);
+int ppo_get_layout(const ppo_t* ctx, ppo_layout* out);
+void* ppo_stream(ppo_t* ctx);
+
+/* parameters in the reference's flat named_parameters() order (ppo_layout.h); loading also
+ * resets the Adam state (fresh optimizer, as after the reference's ctor). */
+int ppo_load_params(ppo_t* ctx, const float* host, long n);
+int ppo_save_params(ppo_t* ctx, float* host, long n);
+/* Adam state in the same flat order (exp_avg, exp_avg_sq) and its step count */
+int ppo_save_adam(ppo_t* ctx, float* m_host, float* v_host, long n, long* step);
+int ppo_load_adam(ppo_t* ctx, const float* m_host, const float* v_host, long n, long step);
+
+int ppo_get_action_and_value(ppo_t* ctx, int n, const float* x_dev, int sample_type,
+                             const float* action_in_dev, long env_base, long step_id,
+                             float* action_dev, float* logprob_dev, float* entropy_dev, float* value_dev,
+                             void* stream);
+int ppo_get_value(ppo_t* ctx, int n, const float* x_dev, float* value_dev, void* stream);
+
+/* rollout step `step` for envs [env_begin, env_end): stores obs/dones, samples actions with the
+ * Philox key (seed, rank, env, iteration*T + step), writes actions into storage and (if non-NULL)
+ * into action_out_dev[e - env_begin]. Several host threads may call it concurrently on distinct
+ * env ranges and streams (AC-PPO async collection, ac:641-698). */
+int ppo_rollout_act(ppo_t* ctx, int step, int env_begin, int env_end, const float* next_obs_dev,
+                    const float* next_done_dev, float* action_out_dev, void* stream);
+int ppo_rollout_reward(ppo_t* ctx, int step, int env_begin, int env_end, const float* reward_dev, void* stream);
+/* GAE over steps [0, num_steps_collected) using next_obs/next_done after the last step. */
+int ppo_compute_gae(ppo_t* ctx, const float* next_obs_dev, const float* next_done_dev, int num_steps_collected,
+                    void* stream);
+/* GAE with a caller-supplied bootstrap value next_value[E] (skips the critic call). */
+int ppo_gae_from_values(ppo_t* ctx, const float* next_value_dev, const float* next_done_dev, int num_steps_collected,
+                        void* stream);
+/* Runs update_epochs x num_minibatches optimizer steps with learning rate lr. Asynchronous on the
+ * context stream; stats (if non-NULL) are copied back after a stream sync. Advances the iteration
+ * counter used by the rollout RNG. perms_dev (optional, int32 [epochs][T*E]) overrides the
+ * Philox/Feistel minibatch permutation (tests inject the reference's randperm). */
+int ppo_update(ppo_t* ctx, float lr, const int32_t* perms_dev, ppo_update_stats* stats);
+int ppo_sync(ppo_t* ctx);
+/* test hook: raw (pre-clip, post all-reduce) gradient of the last minibatch, flat reference order */
+int ppo_debug_last_grad(ppo_t* ctx, float* host, long n);
+long ppo_iteration(const ppo_t* ctx);
+int ppo_set_iteration(ppo_t* ctx, long iteration);
+float* ppo_buffer(ppo_t* ctx, int which);
+
+/* ---- data-parallel communicator (RCCL over xGMI) ---- */
+#define PPO_COMM_ID_BYTES 128
+int ppo_comm_unique_id(char id_out[PPO_COMM_ID_BYTES]);
+/* attaches a communicator for (rank, world) to the context; subsequent ppo_update calls average
+ * gradients and advantage statistics over ranks. */
+int ppo_comm_init(ppo_t* ctx, const char id[PPO_COMM_ID_BYTES], int rank, int world);
+int ppo_comm_broadcast_params(ppo_t* ctx, int root);
+int ppo_comm_allreduce(ppo_t* ctx, float* buf_dev, long n, int average);
+
+/* ---- device memory helpers (so C / ctypes callers need no HIP headers) ---- */
+int ppo_set_device(int device);
+int ppo_device_count(int* n);
+int ppo_dev_malloc(void** p, size_t bytes);
+int ppo_dev_free(void* p);
+int ppo_memcpy_h2d(void* dst_dev, const void* src_host, size_t bytes);
+int ppo_memcpy_d2h(void* dst_host, const void* src_dev, size_t bytes);
+int ppo_memset_dev(void* dst_dev, int value, size_t bytes);
+int ppo_device_sync(void);
+
+/* ---- profiling hooks: per-kernel HIP-event timing of the context's launches ---- */
+int ppo_profile_enable(ppo_t* ctx, int on);
+/* returns (into host arrays of length cap) accumulated ms and launch counts per kernel id; names
+ * via ppo_profile_name(). Returns the number of kernel ids. */
+int ppo_profile_read(ppo_t* ctx, double* ms, long* count, int cap);
+const char* ppo_profile_name(int id);
+int ppo_profile_reset(ppo_t* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPO_HIP_H */

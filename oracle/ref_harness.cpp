@@ -17,7 +17,9 @@
 #include <rl_utils.h>
 #include <torch/torch.h>
 
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <filesystem>
 #include <fstream>
 #include <random>
@@ -246,8 +248,95 @@ static std::tuple<Tensor, std::vector<float>> ppo_loss(const Tensor& newlogprob,
 }
 
 // ---------------------------------------------------------------------------------------------
+// --bench: times the reference's CPU arithmetic for one AC-PPO iteration on a bounded sample
+// (1 intra-op thread, as ac_ppo_continuous_action.cpp:288-289 sets):
+//   * n_act batch-1 Agent::get_action_and_value calls with a per-env generator ("sample", ac:655)
+//   * one full optimizer step on a minibatch of M rows (ac:815-888: forward, loss, backward,
+//     clip_grad_norm_, Adam)
+//   * the GAE loop over [T, E] (ac:759-779)
+// and prints a JSON line; bench.py extrapolates it to one iteration (E*T acts, EP*MB steps).
+// ---------------------------------------------------------------------------------------------
+static int bench_main(int E, int T, int MB, int EP, int n_act) {
+  using clk = std::chrono::steady_clock;
+  const int O = 17, A = 6, H = 256;
+  const long B = (long)E * T, M = B / MB;
+  ACAgent agent(O, A, H, 1.0f, -1.0f, torch::zeros({O}), torch::ones({O}));
+  std::string names;
+  set_params(*agent, names);
+  torch::optim::Adam opt(agent->parameters(), torch::optim::AdamOptions(2.5e-4).eps(1e-5));
+  // batch-1 rollout inference
+  auto gen = at::make_generator<at::CPUGeneratorImpl>(1);
+  Tensor x1 = randn({1, O});
+  double t_act;
+  {
+    torch::NoGradGuard ng;
+    Tensor xn, feat, al, be;
+    auto t0 = clk::now();
+    for (int i = 0; i < n_act; ++i) {
+      Tensor xx = (x1 - agent->mean_) / agent->std_;
+      feat = agent->actor_encoder->forward(xx);
+      al = nn::functional::softplus(agent->dist_alpha->forward(feat)) + 1.0f;
+      be = nn::functional::softplus(agent->dist_beta->forward(feat)) + 1.0f;
+      const Beta probs(al, be);
+      Tensor a = probs.sample(gen);
+      Tensor lp = probs.log_prob(a).sum(1);
+      a = agent->unscale_action(a);
+      Tensor ent = probs.entropy().sum(1);
+      Tensor v = agent->critic->forward(xx);
+      (void)lp; (void)ent; (void)v;
+    }
+    t_act = std::chrono::duration<double>(clk::now() - t0).count() / n_act;
+  }
+  // one optimizer step on M rows
+  Tensor bx = randn({M, O}), ba = randu({M, A}, -0.99f, 0.99f), blp = randn({M}, 0.1f) - 5.0f;
+  Tensor badv = randn({M}), bret = randn({M}), bval = randn({M});
+  LossCfg c{0.1f, 0.01f, 0.5f, true, true};
+  double t_opt;
+  {
+    auto t0 = clk::now();
+    auto [a, lp, ent, v, al, be] = agent->get_action_and_value(bx, ba, "given");
+    Tensor amean = badv.mean();
+    Tensor astd = torch::sqrt(torch::sum(torch::square(badv - amean)) / static_cast<float>(M - 1));
+    auto [loss, st] = ppo_loss(lp, ent, v, blp, badv, bret, bval, c, &amean, &astd);
+    opt.zero_grad();
+    loss.backward();
+    torch::nn::utils::clip_grad_norm_(agent->parameters(), 0.5);
+    opt.step();
+    t_opt = std::chrono::duration<double>(clk::now() - t0).count();
+  }
+  // GAE over [T, E]
+  double t_gae;
+  {
+    torch::NoGradGuard ng;
+    Tensor rewards = randn({T, E}), values = randn({T, E}), dones = torch::zeros({T, E});
+    Tensor next_value = randn({E}), next_done = torch::zeros({E}), advantages = torch::zeros({T, E});
+    auto t0 = clk::now();
+    Tensor lastgaelam = torch::zeros({E}), nnt, nv;
+    for (int t = T - 1; t >= 0; --t) {
+      if (t == T - 1) { nnt = 1.0f - next_done; nv = next_value; }
+      else { nnt = 1.0 - dones.index({t + 1}); nv = values.index({t + 1}); }
+      Tensor delta = rewards.index({t}) + 0.99f * nv * nnt - values.index({t});
+      advantages.index({t}) = delta + 0.99f * 0.95f * nnt * lastgaelam;
+      lastgaelam = advantages.index({t});
+    }
+    Tensor returns = advantages + values;
+    t_gae = std::chrono::duration<double>(clk::now() - t0).count();
+  }
+  const double t_iter = t_act * (double)B + t_opt * (double)(EP * MB) + t_gae;
+  std::printf("{\"t_act_batch1_s\": %.9g, \"t_opt_step_s\": %.9g, \"t_gae_s\": %.9g, \"n_act\": %d, \"M\": %ld, "
+              "\"t_iter_s\": %.9g, \"sps\": %.9g, \"threads\": 1}\n",
+              t_act, t_opt, t_gae, n_act, M, t_iter, (double)B / t_iter);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   torch::set_num_threads(1);
+  if (argc > 1 && std::string(argv[1]) == "--bench") {
+    int E = argc > 2 ? std::atoi(argv[2]) : 4096, T = argc > 3 ? std::atoi(argv[3]) : 128;
+    int MB = argc > 4 ? std::atoi(argv[4]) : 4, EP = argc > 5 ? std::atoi(argv[5]) : 4;
+    int n_act = argc > 6 ? std::atoi(argv[6]) : 2000;
+    return bench_main(E, T, MB, EP, n_act);
+  }
   g_out = argc > 1 ? argv[1] : "tests/golden";
   std::filesystem::create_directories(g_out);
   g_manifest << "{\n";

@@ -1,0 +1,170 @@
+// ppo_agent.hpp — the agent (actor + critic trunks) in the batch-on-lanes MFMA layout.
+//
+// Layout recap (ppo_device.hpp): a wave owns 16 batch rows; lane = (j = row, g = lane >> 4);
+// a width-H activation is NT = H/16 f4 registers per lane: register t holds features
+// 16t + 4g + {0,1,2,3}. A Linear layer Z^T = W . H^T runs as NT_OUT x NT_IN x 4 MFMAs
+// v_mfma_f32_16x16x4_f32: A = four consecutive input columns of a weight row (one 16-byte load
+// per lane), B = the activation register itself — no LDS, no transposes between layers.
+// LayerNorm over features = in-lane sum + two cross-lane adds (row_allreduce).
+#pragma once
+
+#include "ppo_device.hpp"
+#include "ppo_packed.hpp"
+
+// Buffer-resource loads (T8): a wave-uniform 128-bit descriptor + one 32-bit per-lane offset; the
+// per-(tile, out-tile) displacement goes in the scalar soffset, so an unrolled layer needs no
+// 64-bit VGPR address pairs (hipcc otherwise hoists and spills hundreds of them).
+struct PBuf {
+  __amdgpu_buffer_rsrc_t r;
+};
+PPO_DEV PBuf make_pbuf(const float* base, int nfloats) {
+  return PBuf{__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nfloats * 4, 0x00020000)};
+}
+// f4 at float offset (lane_floats + uni_floats); lane part per lane, uniform part in soffset
+PPO_DEV f4 pld4(PBuf b, int lane_floats, int uni_floats) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(b.r, lane_floats * 4, uni_floats * 4, 0));
+}
+
+// Z^T tile chain: out = W . in (+ bias), W row-major [NT_OUT*16][LDW].
+template <int NT_OUT, int NT_IN, int LDW, bool BIAS>
+PPO_DEV void mm_layer(f4 (&out)[NT_OUT], const f4 (&in)[NT_IN], const float* __restrict__ W,
+                      const float* __restrict__ bias, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const PBuf wb = make_pbuf(W, NT_OUT * 16 * LDW);
+  const int lo = i * LDW + 4 * g;
+  if constexpr (BIAS) {
+    const PBuf bb = make_pbuf(bias, NT_OUT * 16);
+#pragma unroll
+    for (int ot = 0; ot < NT_OUT; ++ot) out[ot] = pld4(bb, 4 * g, 16 * ot);
+  } else {
+#pragma unroll
+    for (int ot = 0; ot < NT_OUT; ++ot) out[ot] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int t = 0; t < NT_IN; ++t) {
+#pragma unroll
+    for (int ot = 0; ot < NT_OUT; ++ot) {
+      const f4 w = pld4(wb, lo, 16 * ot * LDW + 16 * t);
+      out[ot] = mfma16(w.x, in[t].x, out[ot]);
+      out[ot] = mfma16(w.y, in[t].y, out[ot]);
+      out[ot] = mfma16(w.z, in[t].z, out[ot]);
+      out[ot] = mfma16(w.w, in[t].w, out[ot]);
+    }
+  }
+}
+
+// normalized agent input (AC: (x - mean_) / std_, ac:189 / :215), zero padded to NTO*16 features
+template <int NTO, int KIND>
+PPO_DEV void load_input(f4 (&xin)[NTO], const float* __restrict__ xrow, int O, const float* __restrict__ omean,
+                        const float* __restrict__ ostd, int g) {
+#pragma unroll
+  for (int t = 0; t < NTO; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * t + 4 * g + r;
+      float v = 0.0f;
+      if (xrow && f < O) {
+        v = xrow[f];
+        if constexpr (KIND == PPO_NET_LN_BETA) v = (v - omean[f]) / ostd[f];
+      }
+      xin[t][r] = v;
+    }
+  }
+}
+
+template <int NT>
+PPO_DEV void ln_stats(const f4 (&z)[NT], float& mu, float& rs) {
+  constexpr float invH = 1.0f / (16 * NT);
+  float s = 0.0f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) s += (z[t].x + z[t].y) + (z[t].z + z[t].w);
+  s = row_allreduce(s);
+  mu = s * invH;
+  float q = 0.0f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = z[t][r] - mu;
+      q += d * d;
+    }
+  }
+  q = row_allreduce(q);
+  rs = 1.0f / sqrtf(q * invH + 1e-5f);
+}
+
+// in place: z -> x_hat = (z - mu) * rs
+template <int NT>
+PPO_DEV void ln_normalize(f4 (&z)[NT], float mu, float rs) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) z[t] = (z[t] - mu) * rs;
+}
+
+// h = relu(gamma * x_hat + beta)
+template <int NT>
+PPO_DEV void affine_relu(f4 (&h)[NT], const f4 (&xh)[NT], PBuf pb, int gam, int bet, int g) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const f4 gm = pld4(pb, 4 * g, gam + 16 * t), bt = pld4(pb, 4 * g, bet + 16 * t);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float y = __fmaf_rn(gm[r], xh[t][r], bt[r]);
+      h[t][r] = y > 0.0f ? y : 0.0f;
+    }
+  }
+}
+
+template <int NT>
+PPO_DEV void tanh_inplace(f4 (&z)[NT]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) z[t][r] = tanhf(z[t][r]);
+}
+
+// one output of a Linear(H, k) head for this lane's row: sum_f w[f] h[f] + b (all 4 g-lanes get it)
+template <int NT>
+PPO_DEV float head_dot(const f4 (&h)[NT], PBuf pb, int w, float b, int g) {
+  float p = 0.0f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const f4 wv = pld4(pb, 4 * g, w + 16 * t);
+    p += (wv.x * h[t].x + wv.y * h[t].y) + (wv.z * h[t].z + wv.w * h[t].w);
+  }
+  return row_allreduce(p) + b;
+}
+
+// Full trunk forward: returns the last hidden activation in h (width H). For the LN net, also
+// returns the layer-1/2 statistics (needed by the fused backward).
+template <int H, int KIND, int NTO>
+PPO_DEV void trunk_forward(const TrunkDev& T, const float* __restrict__ P, PBuf pb, const f4 (&xin)[NTO],
+                           f4 (&h)[H / 16], int lane) {
+  constexpr int NT = H / 16;
+  const int g = lane >> 4;
+  f4 a[NT];
+  mm_layer<NT, NTO, NTO * 16, true>(a, xin, P + T.W1, P + T.b1, lane);
+  if constexpr (KIND == PPO_NET_LN_BETA) {
+    float mu, rs;
+    ln_stats<NT>(a, mu, rs);
+    ln_normalize<NT>(a, mu, rs);
+    affine_relu<NT>(a, a, pb, T.g1, T.be1, g);
+  } else {
+    tanh_inplace<NT>(a);
+  }
+  mm_layer<NT, NT, H, true>(h, a, P + T.W2, P + T.b2, lane);
+  if constexpr (KIND == PPO_NET_LN_BETA) {
+    float mu, rs;
+    ln_stats<NT>(h, mu, rs);
+    ln_normalize<NT>(h, mu, rs);
+    affine_relu<NT>(h, h, pb, T.g2, T.be2, g);
+  } else {
+    tanh_inplace<NT>(h);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-row distribution math. Every g-lane of a row computes the same per-row values; action
+// dimensions are distributed over the 4 g-lanes (a = g, g+4, ...) and summed with row_allreduce.
+// ---------------------------------------------------------------------------------------------
+static constexpr float kLz = 0.91893853320467274178f;   // log(sqrt(2 pi))  (rl_utils.h:20)
+static constexpr float kEntC = 1.4189385332046727418f;  // 0.5 + 0.5 log(2 pi) (rl_utils.h:44)

@@ -1,0 +1,884 @@
+// ppo_capi.hip — C-ABI of libppo_hip.so (include/ppo_hip.h, include/ppo_synth_env.h).
+//
+// Host runtime around the gfx950 kernels: device memory for the agent (packed params, grads,
+// Adam moments), the [T, E, *] rollout storage, minibatch scratch, the per-minibatch launch
+// sequence of the PPO update, and the RCCL communicator that replaces torchfort::Comm
+// (reference src/distributed.cpp). Everything runs asynchronously on the context stream; the only
+// host synchronisation in an update is the optional stats read-back at its end.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ppo_hip.h"
+#include "../../include/ppo_synth_env.h"
+#include "ppo_kernels.hpp"
+
+// ------------------------------------------------------------------------------------------
+// errors
+// ------------------------------------------------------------------------------------------
+static thread_local std::string g_err;
+static int fail(const std::string& msg, int code = -1) {
+  g_err = msg;
+  return code;
+}
+#define HIP_TRY(expr)                                                                           \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess) return fail(std::string(#expr) + ": " + hipGetErrorString(e_), -2);   \
+  } while (0)
+#define NCCL_TRY(expr)                                                                          \
+  do {                                                                                          \
+    ncclResult_t r_ = (expr);                                                                   \
+    if (r_ != ncclSuccess) return fail(std::string(#expr) + ": " + ncclGetErrorString(r_), -3); \
+  } while (0)
+
+extern "C" const char* ppo_last_error(void) { return g_err.c_str(); }
+extern "C" const char* ppo_version(void) { return "ppo_hip 0.1 (gfx950)"; }
+
+// ------------------------------------------------------------------------------------------
+// profiling (HIP events around the context's launches)
+// ------------------------------------------------------------------------------------------
+enum {
+  PK_ACT = 0, PK_FWDBWD, PK_DW2, PK_DW1, PK_COLSUM, PK_GRADNORM, PK_ADAM, PK_GAE, PK_PERM, PK_ADV, PK_ALLREDUCE,
+  PK_SYNTH, PK_COUNT
+};
+static const char* kProfNames[PK_COUNT] = {"act", "fwdbwd", "dw_l2", "dw_l1", "colsum", "gradnorm",
+                                           "adam", "gae", "perm", "adv_stats", "allreduce", "synth_env"};
+
+struct ProfEvent {
+  int id;
+  hipEvent_t a, b;
+};
+
+struct ppo_ctx {
+  ppo_hip_config cfg;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  ppo_layout L;
+  PackedLayout K;
+  SmallGradLayout sg[2];
+  long B = 0;
+  int M = 0, nmb = 0;
+  float *P = nullptr, *G = nullptr, *Am = nullptr, *Av = nullptr, *W2T[2] = {nullptr, nullptr};
+  float* buf[PPO_BUF_COUNT] = {};
+  float* next_value = nullptr;
+  int32_t* perms = nullptr;
+  float *advstats = nullptr, *advsq = nullptr;
+  float *Xn = nullptr, *H1[2] = {}, *DZ1[2] = {}, *DZ2[2] = {};
+  float* slab[2] = {};
+  int tiles_per_block = 1, nblk = 1;
+  size_t lds_bytes = 0;
+  float* dwslab[4] = {};
+  int nchunks = 1, rows_per_chunk = 64;
+  float* normout = nullptr;
+  float* mbstats = nullptr;  // [EP*MB][8]
+  long adam_step = 0;
+  long iteration = 0;
+  ncclComm_t comm = nullptr;
+  int world = 1, rank = 0;
+  // profiling
+  unsigned prof_mask = 0;
+  std::mutex prof_mu;
+  std::vector<ProfEvent> pending;
+  std::vector<hipEvent_t> free_events;
+  double prof_ms[PK_COUNT] = {};
+  long prof_cnt[PK_COUNT] = {};
+};
+
+static hipEvent_t prof_event(ppo_t* c) {
+  if (!c->free_events.empty()) {
+    hipEvent_t e = c->free_events.back();
+    c->free_events.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  return e;
+}
+struct ProfScope {
+  ppo_t* c;
+  int id;
+  hipStream_t s;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(ppo_t* c_, int id_, hipStream_t s_) : c(c_), id(id_), s(s_) {
+    if (c->prof_mask & (1u << id)) {
+      std::lock_guard<std::mutex> lk(c->prof_mu);
+      a = prof_event(c);
+      b = prof_event(c);
+      (void)hipEventRecord(a, s);
+    }
+  }
+  ~ProfScope() {
+    if (a) {
+      (void)hipEventRecord(b, s);
+      std::lock_guard<std::mutex> lk(c->prof_mu);
+      c->pending.push_back({id, a, b});
+    }
+  }
+};
+static void prof_drain(ppo_t* c) {
+  std::lock_guard<std::mutex> lk(c->prof_mu);
+  for (auto& p : c->pending) {
+    (void)hipEventSynchronize(p.b);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, p.a, p.b);
+    c->prof_ms[p.id] += ms;
+    c->prof_cnt[p.id] += 1;
+    c->free_events.push_back(p.a);
+    c->free_events.push_back(p.b);
+  }
+  c->pending.clear();
+}
+
+static hipStream_t S(ppo_t* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+
+// ------------------------------------------------------------------------------------------
+// create / destroy
+// ------------------------------------------------------------------------------------------
+template <typename T>
+static int dmalloc(T** p, size_t n) {
+  if (n == 0) n = 1;
+  hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+  if (e != hipSuccess) return fail(std::string("hipMalloc: ") + hipGetErrorString(e), -2);
+  (void)hipMemset(*p, 0, n * sizeof(T));
+  return 0;
+}
+
+extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
+  if (!cfg || !out) return fail("ppo_create: null argument");
+  ppo_layout L;
+  if (ppo_layout_init(&L, cfg->net_kind, cfg->obs_dim, cfg->act_dim, cfg->hidden) != 0)
+    return fail("ppo_create: bad net kind / dims");
+  if (cfg->hidden != 64 && cfg->hidden != 256) return fail("ppo_create: hidden must be 64 or 256");
+  if (cfg->act_dim > 20) return fail("ppo_create: act_dim > 20 not supported");
+  if (cfg->num_envs <= 0 || cfg->num_steps <= 0 || cfg->num_minibatches <= 0 || cfg->update_epochs <= 0)
+    return fail("ppo_create: sizes must be positive");
+  const long B = (long)cfg->num_envs * cfg->num_steps;
+  if (B % cfg->num_minibatches) return fail("ppo_create: num_steps*num_envs must divide by num_minibatches");
+  if (B >= (1L << 31)) return fail("ppo_create: batch too large");
+  HIP_TRY(hipSetDevice(device));
+  ppo_t* c = new ppo_t();
+  c->cfg = *cfg;
+  c->device = device;
+  c->L = L;
+  c->K = make_packed(L);
+  {
+    int nto = c->K.OP / 16;
+    bool ok = false;
+    const int H = cfg->hidden, kind = cfg->net_kind;
+    const int sup[][3] = {{256, 1, 1}, {256, 1, 2}, {256, 1, 7}, {256, 1, 24}, {64, 0, 1}, {64, 0, 2},
+                          {64, 0, 7}, {64, 0, 24}, {64, 1, 2}, {256, 0, 2}};
+    for (auto& s3 : sup)
+      if (s3[0] == H && s3[1] == kind && s3[2] == nto) ok = true;
+    if (!ok) {
+      delete c;
+      return fail("ppo_create: no kernel instantiation for this (hidden, net_kind, obs_dim)");
+    }
+  }
+  c->B = B;
+  c->nmb = cfg->num_minibatches;
+  c->M = (int)(B / cfg->num_minibatches);
+  c->rank = cfg->rank;
+  c->world = cfg->world_size > 0 ? cfg->world_size : 1;
+  const int H = cfg->hidden, A = cfg->act_dim, O = cfg->obs_dim, OP = c->K.OP;
+  c->sg[0] = make_sg(H, 1, A);
+  c->sg[1] = make_sg(H, cfg->net_kind == PPO_NET_LN_BETA ? 2 * A : A, A);
+  int rc = 0;
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  const size_t PS = c->K.size;
+  rc |= dmalloc(&c->P, PS); rc |= dmalloc(&c->G, PS); rc |= dmalloc(&c->Am, PS); rc |= dmalloc(&c->Av, PS);
+  for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->W2T[k], (size_t)H * H);
+  const size_t E = cfg->num_envs, T = cfg->num_steps;
+  rc |= dmalloc(&c->buf[PPO_BUF_OBS], T * E * O);
+  rc |= dmalloc(&c->buf[PPO_BUF_ACTIONS], T * E * A);
+  for (int b = PPO_BUF_LOGPROBS; b < PPO_BUF_COUNT; ++b)
+    if (b != PPO_BUF_ACTIONS) rc |= dmalloc(&c->buf[b], T * E);
+  rc |= dmalloc(&c->next_value, E);
+  const int EP = cfg->update_epochs;
+  rc |= dmalloc(&c->perms, (size_t)EP * B);
+  rc |= dmalloc(&c->advstats, (size_t)2 * EP * c->nmb);
+  rc |= dmalloc(&c->advsq, (size_t)EP * c->nmb);
+  const size_t Mr = ((size_t)c->M + 63) / 64 * 64;
+  rc |= dmalloc(&c->Xn, Mr * OP + 64);
+  for (int k = 0; k < 2; ++k) {
+    rc |= dmalloc(&c->H1[k], Mr * H);
+    rc |= dmalloc(&c->DZ1[k], Mr * H);
+    rc |= dmalloc(&c->DZ2[k], Mr * H);
+  }
+  const int tiles = (int)(Mr / 64);
+  c->tiles_per_block = std::max(1, (tiles + 255) / 256);
+  c->nblk = (tiles + c->tiles_per_block - 1) / c->tiles_per_block;
+  for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->slab[k], (size_t)c->nblk * c->sg[k].size);
+  c->lds_bytes = (size_t)4 * std::max(c->sg[0].size, c->sg[1].size) * sizeof(float);
+  c->rows_per_chunk = std::max(64, (int)(((c->M + 63) / 64 + 1) & ~1));
+  c->nchunks = (c->M + c->rows_per_chunk - 1) / c->rows_per_chunk;
+  for (int k = 0; k < 2; ++k) {
+    rc |= dmalloc(&c->dwslab[k], (size_t)c->nchunks * H * H);
+    rc |= dmalloc(&c->dwslab[2 + k], (size_t)c->nchunks * H * OP);
+  }
+  rc |= dmalloc(&c->normout, 4);
+  rc |= dmalloc(&c->mbstats, (size_t)8 * EP * c->nmb);
+  if (rc) {
+    ppo_destroy(c);
+    return -2;
+  }
+  if (fwdbwd_set_lds(c->K, c->lds_bytes) != 0) {
+    ppo_destroy(c);
+    return fail("ppo_create: cannot set LDS size for the fused update kernel");
+  }
+  HIP_TRY(hipDeviceSynchronize());
+  *out = c;
+  return 0;
+}
+
+extern "C" int ppo_destroy(ppo_t* c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  prof_drain(c);
+  for (auto e : c->free_events) (void)hipEventDestroy(e);
+  float* ptrs[] = {c->P, c->G, c->Am, c->Av, c->W2T[0], c->W2T[1], c->next_value, c->advstats, c->advsq, c->Xn,
+                   c->normout, c->mbstats};
+  for (float* p : ptrs)
+    if (p) (void)hipFree(p);
+  for (int b = 0; b < PPO_BUF_COUNT; ++b)
+    if (c->buf[b]) (void)hipFree(c->buf[b]);
+  for (int k = 0; k < 2; ++k) {
+    float* q[] = {c->H1[k], c->DZ1[k], c->DZ2[k], c->slab[k]};
+    for (float* p : q)
+      if (p) (void)hipFree(p);
+  }
+  for (int k = 0; k < 4; ++k)
+    if (c->dwslab[k]) (void)hipFree(c->dwslab[k]);
+  if (c->perms) (void)hipFree(c->perms);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+extern "C" int ppo_get_layout(const ppo_t* c, ppo_layout* out) {
+  if (!c || !out) return fail("ppo_get_layout: null argument");
+  *out = c->L;
+  return 0;
+}
+extern "C" void* ppo_stream(ppo_t* c) { return c ? (void*)c->stream : nullptr; }
+extern "C" long ppo_iteration(const ppo_t* c) { return c ? c->iteration : -1; }
+extern "C" int ppo_set_iteration(ppo_t* c, long it) {
+  if (!c) return fail("null ctx");
+  c->iteration = it;
+  return 0;
+}
+extern "C" float* ppo_buffer(ppo_t* c, int which) {
+  if (!c || which < 0 || which >= PPO_BUF_COUNT) return nullptr;
+  return c->buf[which];
+}
+
+// ------------------------------------------------------------------------------------------
+// parameters / optimizer state
+// ------------------------------------------------------------------------------------------
+static int refresh_w2t(ppo_t* c) {
+  for (int k = 0; k < 2; ++k) launch_transpose(c->P + c->K.tr[k].W2, c->W2T[k], c->K.H, c->stream);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+extern "C" int ppo_load_params(ppo_t* c, const float* host, long n) {
+  if (!c || !host) return fail("ppo_load_params: null argument");
+  if (n != c->L.P) return fail("ppo_load_params: expected " + std::to_string(c->L.P) + " floats");
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<float> packed(c->K.size);
+  pack_params(c->K, c->L, host, packed.data());
+  HIP_TRY(hipMemcpyAsync(c->P, packed.data(), sizeof(float) * c->K.size, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemsetAsync(c->Am, 0, sizeof(float) * c->K.size, c->stream));
+  HIP_TRY(hipMemsetAsync(c->Av, 0, sizeof(float) * c->K.size, c->stream));
+  c->adam_step = 0;
+  if (refresh_w2t(c)) return -2;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+extern "C" int ppo_save_params(ppo_t* c, float* host, long n) {
+  if (!c || !host) return fail("ppo_save_params: null argument");
+  if (n != c->L.P) return fail("ppo_save_params: expected " + std::to_string(c->L.P) + " floats");
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<float> packed(c->K.size);
+  HIP_TRY(hipMemcpyAsync(packed.data(), c->P, sizeof(float) * c->K.size, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  unpack_params(c->K, c->L, packed.data(), host);
+  return 0;
+}
+
+extern "C" int ppo_save_adam(ppo_t* c, float* m_host, float* v_host, long n, long* step) {
+  if (!c) return fail("null ctx");
+  if (n != c->L.P) return fail("ppo_save_adam: size mismatch");
+  std::vector<float> pm(c->K.size), pv(c->K.size);
+  HIP_TRY(hipMemcpyAsync(pm.data(), c->Am, sizeof(float) * c->K.size, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(pv.data(), c->Av, sizeof(float) * c->K.size, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (m_host) unpack_params(c->K, c->L, pm.data(), m_host);
+  if (v_host) unpack_params(c->K, c->L, pv.data(), v_host);
+  if (step) *step = c->adam_step;
+  return 0;
+}
+
+extern "C" int ppo_load_adam(ppo_t* c, const float* m_host, const float* v_host, long n, long step) {
+  if (!c || !m_host || !v_host) return fail("ppo_load_adam: null argument");
+  if (n != c->L.P) return fail("ppo_load_adam: size mismatch");
+  std::vector<float> pm(c->K.size), pv(c->K.size);
+  pack_params(c->K, c->L, m_host, pm.data());
+  pack_params(c->K, c->L, v_host, pv.data());
+  HIP_TRY(hipMemcpyAsync(c->Am, pm.data(), sizeof(float) * c->K.size, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->Av, pv.data(), sizeof(float) * c->K.size, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->adam_step = step;
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// agent calls
+// ------------------------------------------------------------------------------------------
+static ActArgs base_act(ppo_t* c) {
+  ActArgs a;
+  memset(&a, 0, sizeof(a));
+  a.P = c->P;
+  a.K = c->K;
+  a.seed = c->cfg.seed;
+  a.rank = c->rank;
+  a.store_step = -1;
+  a.E = c->cfg.num_envs;
+  return a;
+}
+
+extern "C" int ppo_get_action_and_value(ppo_t* c, int n, const float* x, int sample_type, const float* action_in,
+                                        long env_base, long step_id, float* action, float* logprob, float* entropy,
+                                        float* value, void* stream) {
+  if (!c || !x) return fail("ppo_get_action_and_value: null argument");
+  if (n <= 0) return 0;
+  if (sample_type == PPO_GIVEN && !action_in) return fail("ppo_get_action_and_value: GIVEN needs action_in");
+  if (sample_type < 0 || sample_type > 2) return fail("Unsupported sample type used. Sample type: " + std::to_string(sample_type));
+  ActArgs a = base_act(c);
+  a.n = n;
+  a.x = x;
+  a.ldx = c->K.O;
+  a.mode = sample_type;
+  a.need_actor = (action || logprob || entropy) ? 1 : 0;
+  a.action_in = action_in;
+  a.env_base = env_base;
+  a.step_id = step_id;
+  a.action_out = action;
+  a.logprob_out = logprob;
+  a.entropy_out = entropy;
+  a.value_out = value;
+  hipStream_t s = S(c, stream);
+  ProfScope ps(c, PK_ACT, s);
+  if (launch_act(a, s) != 0) return fail("no act kernel for this configuration");
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+extern "C" int ppo_get_value(ppo_t* c, int n, const float* x, float* value, void* stream) {
+  return ppo_get_action_and_value(c, n, x, PPO_MEAN, nullptr, 0, 0, nullptr, nullptr, nullptr, value, stream);
+}
+
+extern "C" int ppo_rollout_act(ppo_t* c, int step, int e0, int e1, const float* next_obs, const float* next_done,
+                               float* action_out, void* stream) {
+  if (!c || !next_obs) return fail("ppo_rollout_act: null argument");
+  if (step < 0 || step >= c->cfg.num_steps || e0 < 0 || e1 > c->cfg.num_envs || e0 >= e1)
+    return fail("ppo_rollout_act: step / env range out of bounds");
+  ActArgs a = base_act(c);
+  a.n = e1 - e0;
+  a.x = next_obs;
+  a.ldx = c->K.O;
+  a.mode = PPO_SAMPLE;
+  a.need_actor = 1;
+  a.env_base = e0;
+  a.step_id = c->iteration * (long)c->cfg.num_steps + step;
+  a.action_out = action_out;
+  a.store_step = step;
+  a.next_done = next_done;
+  a.s_obs = c->buf[PPO_BUF_OBS];
+  a.s_actions = c->buf[PPO_BUF_ACTIONS];
+  a.s_logp = c->buf[PPO_BUF_LOGPROBS];
+  a.s_dones = c->buf[PPO_BUF_DONES];
+  a.s_values = c->buf[PPO_BUF_VALUES];
+  hipStream_t s = S(c, stream);
+  ProfScope ps(c, PK_ACT, s);
+  if (launch_act(a, s) != 0) return fail("no act kernel for this configuration");
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+extern "C" int ppo_rollout_reward(ppo_t* c, int step, int e0, int e1, const float* reward, void* stream) {
+  if (!c || !reward) return fail("ppo_rollout_reward: null argument");
+  if (step < 0 || step >= c->cfg.num_steps || e0 < 0 || e1 > c->cfg.num_envs || e0 >= e1)
+    return fail("ppo_rollout_reward: step / env range out of bounds");
+  HIP_TRY(hipMemcpyAsync(c->buf[PPO_BUF_REWARDS] + (size_t)step * c->cfg.num_envs + e0, reward,
+                         sizeof(float) * (e1 - e0), hipMemcpyDeviceToDevice, S(c, stream)));
+  return 0;
+}
+
+static int gae_launch(ppo_t* c, const float* next_value, const float* next_done, int nsteps, hipStream_t s);
+
+extern "C" int ppo_compute_gae(ppo_t* c, const float* next_obs, const float* next_done, int nsteps, void* stream) {
+  if (!c || !next_obs || !next_done) return fail("ppo_compute_gae: null argument");
+  if (nsteps <= 0 || nsteps > c->cfg.num_steps) return fail("ppo_compute_gae: bad step count");
+  hipStream_t s = S(c, stream);
+  int rc = ppo_get_value(c, c->cfg.num_envs, next_obs, c->next_value, s);
+  if (rc) return rc;
+  return gae_launch(c, c->next_value, next_done, nsteps, s);
+}
+
+extern "C" int ppo_gae_from_values(ppo_t* c, const float* next_value, const float* next_done, int nsteps,
+                                   void* stream) {
+  if (!c || !next_value || !next_done) return fail("ppo_gae_from_values: null argument");
+  if (nsteps <= 0 || nsteps > c->cfg.num_steps) return fail("ppo_gae_from_values: bad step count");
+  return gae_launch(c, next_value, next_done, nsteps, S(c, stream));
+}
+
+static int gae_launch(ppo_t* c, const float* next_value, const float* next_done, int nsteps, hipStream_t s) {
+  GaeArgs g;
+  g.rewards = c->buf[PPO_BUF_REWARDS];
+  g.values = c->buf[PPO_BUF_VALUES];
+  g.dones = c->buf[PPO_BUF_DONES];
+  g.next_value = next_value;
+  g.next_done = next_done;
+  g.adv = c->buf[PPO_BUF_ADVANTAGES];
+  g.ret = c->buf[PPO_BUF_RETURNS];
+  g.T = nsteps;
+  g.E = c->cfg.num_envs;
+  g.gamma = c->cfg.gamma;
+  g.lam = c->cfg.gae_lambda;
+  ProfScope ps(c, PK_GAE, s);
+  launch_gae(g, s);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// update
+// ------------------------------------------------------------------------------------------
+static int allreduce(ppo_t* c, float* buf, long n, int average, hipStream_t s) {
+  if (!c->comm || c->world <= 1) return 0;
+  ProfScope ps(c, PK_ALLREDUCE, s);
+  NCCL_TRY(ncclAllReduce(buf, buf, (size_t)n, ncclFloat, average ? ncclAvg : ncclSum, c->comm, s));
+  return 0;
+}
+
+extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_update_stats* out) {
+  if (!c) return fail("ppo_update: null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const ppo_hip_config& cfg = c->cfg;
+  const int EP = cfg.update_epochs, MB = c->nmb, M = c->M, H = c->K.H, OP = c->K.OP, A = c->K.A;
+  const long B = c->B;
+  // ---- permutations (torch::randperm per epoch, ppo:490 / ac:804) ----
+  const int32_t* perms = perms_dev;
+  if (!perms) {
+    ProfScope ps(c, PK_PERM, s);
+    for (int e = 0; e < EP; ++e)
+      launch_perm(c->perms + (size_t)e * B, (uint32_t)B,
+                  make_perm_key(cfg.seed, c->rank, c->iteration * (long)EP + e, B), s);
+    perms = c->perms;
+  }
+  // ---- advantage statistics of every minibatch (ppo:511; distributed ac:833-846) ----
+  AdvArgs aa;
+  aa.perm = perms;
+  aa.adv = c->buf[PPO_BUF_ADVANTAGES];
+  aa.stats = c->advstats;
+  aa.sq = c->advsq;
+  aa.M = M;
+  aa.nmb = EP * MB;
+  aa.world = c->world;
+  if (cfg.norm_adv) {
+    ProfScope ps(c, PK_ADV, s);
+    launch_adv_sum(aa, s);
+    if (allreduce(c, c->advstats, 2L * EP * MB, 1, s)) return -3;
+    launch_adv_sq(aa, s);
+    if (allreduce(c, c->advsq, (long)EP * MB, 0, s)) return -3;
+    launch_adv_finalize(aa, s);
+  }
+  // ---- per-minibatch launch sequence ----
+  UpdArgs u;
+  memset(&u, 0, sizeof(u));
+  u.P = c->P;
+  u.W2T[0] = c->W2T[0];
+  u.W2T[1] = c->W2T[1];
+  u.K = c->K;
+  u.sg[0] = c->sg[0];
+  u.sg[1] = c->sg[1];
+  u.M = M;
+  u.tiles_per_block = c->tiles_per_block;
+  u.obs = c->buf[PPO_BUF_OBS];
+  u.actions = c->buf[PPO_BUF_ACTIONS];
+  u.logp = c->buf[PPO_BUF_LOGPROBS];
+  u.adv = c->buf[PPO_BUF_ADVANTAGES];
+  u.ret = c->buf[PPO_BUF_RETURNS];
+  u.val = c->buf[PPO_BUF_VALUES];
+  u.clip_coef = cfg.clip_coef;
+  u.ent_coef = cfg.ent_coef;
+  u.vf_coef = cfg.vf_coef;
+  u.inv_m = 1.0f / (float)M;
+  u.clip_vloss = cfg.clip_vloss;
+  u.norm_adv = cfg.norm_adv;
+  u.Xn = c->Xn;
+  for (int k = 0; k < 2; ++k) {
+    u.H1[k] = c->H1[k];
+    u.DZ1[k] = c->DZ1[k];
+    u.DZ2[k] = c->DZ2[k];
+    u.slab[k] = c->slab[k];
+  }
+  DwArgs d2, d1;
+  memset(&d2, 0, sizeof(d2));
+  memset(&d1, 0, sizeof(d1));
+  d2.M = d1.M = M;
+  d2.rows_per_chunk = d1.rows_per_chunk = c->rows_per_chunk;
+  for (int k = 0; k < 2; ++k) {
+    d2.job[k] = DwJob{c->DZ2[k], c->H1[k], H, H, c->dwslab[k], (long)H * H, H, H, H};
+    d1.job[k] = DwJob{c->DZ1[k], c->Xn, H, OP, c->dwslab[2 + k], (long)H * OP, OP, H, OP};
+  }
+  // slab -> packed gradient segments
+  ColsumArgs cs;
+  memset(&cs, 0, sizeof(cs));
+  int ns = 0;
+  long maxlen = 0;
+  auto seg = [&](const float* src, long stride, int count, int len, float* dst, float scale) {
+    cs.seg[ns++] = ColsumSeg{src, dst, stride, count, len, scale};
+    maxlen = std::max(maxlen, (long)len);
+  };
+  const bool ln = cfg.net_kind == PPO_NET_LN_BETA;
+  for (int k = 0; k < 2; ++k) {
+    const TrunkDev& T = c->K.tr[k];
+    seg(c->dwslab[k], (long)H * H, c->nchunks, H * H, c->G + T.W2, 1.f);
+    seg(c->dwslab[2 + k], (long)H * OP, c->nchunks, H * OP, c->G + T.W1, 1.f);
+    const SmallGradLayout& g = c->sg[k];
+    const float* sl = c->slab[k];
+    seg(sl + g.b1, g.size, c->nblk, H, c->G + T.b1, 1.f);
+    seg(sl + g.b2, g.size, c->nblk, H, c->G + T.b2, 1.f);
+    if (ln) {
+      seg(sl + g.g1, g.size, c->nblk, H, c->G + T.g1, 1.f);
+      seg(sl + g.be1, g.size, c->nblk, H, c->G + T.be1, 1.f);
+      seg(sl + g.g2, g.size, c->nblk, H, c->G + T.g2, 1.f);
+      seg(sl + g.be2, g.size, c->nblk, H, c->G + T.be2, 1.f);
+    }
+    if (k == 0) {
+      seg(sl + g.hW, g.size, c->nblk, H, c->G + c->K.cW3, 1.f);
+      seg(sl + g.hb, g.size, c->nblk, 1, c->G + c->K.cb3, 1.f);
+    } else if (!ln) {
+      seg(sl + g.hW, g.size, c->nblk, A * H, c->G + c->K.aW3, 1.f);
+      seg(sl + g.hb, g.size, c->nblk, A, c->G + c->K.ab3, 1.f);
+      seg(sl + g.ls, g.size, c->nblk, A, c->G + c->K.logstd, 1.f);
+    } else {
+      seg(sl + g.hW, g.size, c->nblk, A * H, c->G + c->K.aW3, 1.f);
+      seg(sl + g.hW + A * H, g.size, c->nblk, A * H, c->G + c->K.bW3, 1.f);
+      seg(sl + g.hb, g.size, c->nblk, A, c->G + c->K.ab3, 1.f);
+      seg(sl + g.hb + A, g.size, c->nblk, A, c->G + c->K.bb3, 1.f);
+    }
+  }
+  const int stats_seg0 = ns;  // filled per minibatch below
+  ns += 3;
+  NormArgs na;
+  memset(&na, 0, sizeof(na));
+  na.grad = c->G;
+  na.max_norm = cfg.max_grad_norm;
+  na.out = c->normout;
+  for (int t = 0; t < c->K.nt; ++t)
+    if (c->K.grad[t]) {
+      na.off[na.nt] = c->K.poff[t];
+      na.len[na.nt] = c->K.rows[t] * c->K.ld[t];
+      na.nt++;
+    }
+  int tb = -1;
+  for (int t = 0; t < c->K.nt; ++t)
+    if (c->K.grad[t]) { tb = c->K.poff[t]; break; }
+  AdamArgs ad;
+  memset(&ad, 0, sizeof(ad));
+  ad.param = c->P;
+  ad.grad = c->G;
+  ad.m = c->Am;
+  ad.v = c->Av;
+  ad.begin = tb;
+  ad.n = c->K.size - tb;
+  ad.norm_out = c->normout;
+  ad.eps = cfg.adam_eps;
+  ad.H = H;
+  for (int k = 0; k < 2; ++k) {
+    ad.w2_off[k] = c->K.tr[k].W2;
+    ad.w2t[k] = c->W2T[k];
+  }
+  const long trainable_n = c->K.size - tb;
+
+  for (int e = 0; e < EP; ++e) {
+    for (int mb = 0; mb < MB; ++mb) {
+      const int gi = e * MB + mb;
+      u.perm = perms + (size_t)e * B + (size_t)mb * M;
+      u.adv_stats = c->advstats + 2 * gi;
+      {
+        ProfScope ps(c, PK_FWDBWD, s);
+        if (launch_fwdbwd(u, c->nblk, c->lds_bytes, s) != 0) return fail("no update kernel for this configuration");
+      }
+      {
+        ProfScope ps(c, PK_DW2, s);
+        if (launch_dw(d2, 1, H, OP, c->nchunks, 2, s) != 0) return fail("no dW kernel (layer 2)");
+      }
+      {
+        ProfScope ps(c, PK_DW1, s);
+        if (launch_dw(d1, 0, H, OP, c->nchunks, 2, s) != 0) return fail("no dW kernel (layer 1)");
+      }
+      float* st = c->mbstats + 8 * gi;
+      cs.seg[stats_seg0 + 0] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_PG, st + ST_PG, c->sg[1].size, c->nblk, 1, 1.f / M};
+      cs.seg[stats_seg0 + 1] = ColsumSeg{c->slab[0] + c->sg[0].stats + ST_V, st + ST_V, c->sg[0].size, c->nblk, 1, 0.5f / M};
+      cs.seg[stats_seg0 + 2] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_ENT, st + ST_ENT, c->sg[1].size, c->nblk, 4, 1.f / M};
+      {
+        ProfScope ps(c, PK_COLSUM, s);
+        launch_colsum(cs, ns, maxlen, s);
+      }
+      if (allreduce(c, c->G + tb, trainable_n, 1, s)) return -3;
+      {
+        ProfScope ps(c, PK_GRADNORM, s);
+        launch_gradnorm(na, s);
+      }
+      c->adam_step += 1;
+      const double bc1 = 1.0 - std::pow(0.9, (double)c->adam_step);
+      const double bc2 = 1.0 - std::pow(0.999, (double)c->adam_step);
+      ad.step_size = (float)((double)lr / bc1);
+      ad.sbc2 = (float)std::sqrt(bc2);
+      {
+        ProfScope ps(c, PK_ADAM, s);
+        launch_adam(ad, s);
+      }
+      // keep the total norm of this minibatch next to its loss stats
+      HIP_TRY(hipMemcpyAsync(st + 6, c->normout, sizeof(float), hipMemcpyDeviceToDevice, s));
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  c->iteration += 1;
+  if (out) {
+    std::vector<float> h((size_t)8 * EP * MB);
+    if (c->world > 1 && allreduce(c, c->mbstats, 8L * EP * MB, 1, s)) return -3;
+    HIP_TRY(hipMemcpyAsync(h.data(), c->mbstats, sizeof(float) * h.size(), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const float* last = h.data() + 8 * (EP * MB - 1);
+    out->pg_loss = last[ST_PG];
+    out->v_loss = last[ST_V];
+    out->entropy = last[ST_ENT];
+    out->old_approx_kl = last[ST_OKL];
+    out->approx_kl = last[ST_KL];
+    double cf = 0;
+    for (int i = 0; i < EP * MB; ++i) cf += h[8 * i + ST_CF];
+    out->clipfrac = (float)(cf / (EP * MB));
+    out->grad_norm = last[6];
+    out->minibatches = EP * MB;
+  }
+  return 0;
+}
+
+extern "C" int ppo_debug_last_grad(ppo_t* c, float* host, long n) {
+  if (!c || !host) return fail("ppo_debug_last_grad: null argument");
+  if (n != c->L.P) return fail("ppo_debug_last_grad: size mismatch");
+  std::vector<float> packed(c->K.size);
+  HIP_TRY(hipMemcpyAsync(packed.data(), c->G, sizeof(float) * c->K.size, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  unpack_params(c->K, c->L, packed.data(), host);
+  return 0;
+}
+
+extern "C" int ppo_sync(ppo_t* c) {
+  if (!c) return fail("null ctx");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// communicator (RCCL)
+// ------------------------------------------------------------------------------------------
+extern "C" int ppo_comm_unique_id(char id_out[PPO_COMM_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) <= PPO_COMM_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  memset(id_out, 0, PPO_COMM_ID_BYTES);
+  memcpy(id_out, &id, sizeof(id));
+  return 0;
+}
+
+extern "C" int ppo_comm_init(ppo_t* c, const char id[PPO_COMM_ID_BYTES], int rank, int world) {
+  if (!c || !id) return fail("ppo_comm_init: null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  if (c->comm) {
+    (void)ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  if (world > 1) NCCL_TRY(ncclCommInitRank(&c->comm, world, uid, rank));
+  c->rank = rank;
+  c->world = world;
+  return 0;
+}
+
+extern "C" int ppo_comm_broadcast_params(ppo_t* c, int root) {
+  if (!c) return fail("null ctx");
+  if (!c->comm || c->world <= 1) return 0;
+  NCCL_TRY(ncclBroadcast(c->P, c->P, (size_t)c->K.size, ncclFloat, root, c->comm, c->stream));
+  if (refresh_w2t(c)) return -2;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+extern "C" int ppo_comm_allreduce(ppo_t* c, float* buf, long n, int average) {
+  if (!c || !buf) return fail("null argument");
+  return allreduce(c, buf, n, average, c->stream);
+}
+
+// ------------------------------------------------------------------------------------------
+// device helpers
+// ------------------------------------------------------------------------------------------
+extern "C" int ppo_set_device(int d) { HIP_TRY(hipSetDevice(d)); return 0; }
+extern "C" int ppo_device_count(int* n) { HIP_TRY(hipGetDeviceCount(n)); return 0; }
+extern "C" int ppo_dev_malloc(void** p, size_t bytes) {
+  HIP_TRY(hipMalloc(p, bytes ? bytes : 1));
+  HIP_TRY(hipMemset(*p, 0, bytes ? bytes : 1));
+  return 0;
+}
+extern "C" int ppo_dev_free(void* p) { HIP_TRY(hipFree(p)); return 0; }
+extern "C" int ppo_memcpy_h2d(void* d, const void* h, size_t n) { HIP_TRY(hipMemcpy(d, h, n, hipMemcpyHostToDevice)); return 0; }
+extern "C" int ppo_memcpy_d2h(void* h, const void* d, size_t n) { HIP_TRY(hipMemcpy(h, d, n, hipMemcpyDeviceToHost)); return 0; }
+extern "C" int ppo_memset_dev(void* d, int v, size_t n) { HIP_TRY(hipMemset(d, v, n)); return 0; }
+extern "C" int ppo_device_sync(void) { HIP_TRY(hipDeviceSynchronize()); return 0; }
+
+// ------------------------------------------------------------------------------------------
+// profiling API
+// ------------------------------------------------------------------------------------------
+extern "C" int ppo_profile_enable(ppo_t* c, int mask) {
+  if (!c) return fail("null ctx");
+  c->prof_mask = (unsigned)mask;
+  return 0;
+}
+extern "C" int ppo_profile_read(ppo_t* c, double* ms, long* count, int cap) {
+  if (!c) return fail("null ctx");
+  prof_drain(c);
+  for (int i = 0; i < PK_COUNT && i < cap; ++i) {
+    if (ms) ms[i] = c->prof_ms[i];
+    if (count) count[i] = c->prof_cnt[i];
+  }
+  return PK_COUNT;
+}
+extern "C" const char* ppo_profile_name(int id) { return (id >= 0 && id < PK_COUNT) ? kProfNames[id] : ""; }
+extern "C" int ppo_profile_reset(ppo_t* c) {
+  if (!c) return fail("null ctx");
+  prof_drain(c);
+  for (int i = 0; i < PK_COUNT; ++i) {
+    c->prof_ms[i] = 0;
+    c->prof_cnt[i] = 0;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// synthetic device env
+// ------------------------------------------------------------------------------------------
+struct psyn_env {
+  SynthArgs a;
+  int device;
+};
+
+extern "C" int psyn_create(int E, int O, int A, psyn_t** out) {
+  if (!out || E <= 0 || O <= 0 || A <= 0) return fail("psyn_create: bad arguments");
+  psyn_t* env = new psyn_t();
+  memset(&env->a, 0, sizeof(env->a));
+  (void)hipGetDevice(&env->device);
+  SynthArgs& a = env->a;
+  a.E = E; a.O = O; a.A = A;
+  int rc = 0;
+  rc |= dmalloc(&a.q, (size_t)E * O);
+  rc |= dmalloc(&a.t, E);
+  rc |= dmalloc(&a.autoreset, E);
+  rc |= dmalloc(&a.rseed, E);
+  rc |= dmalloc(&a.rcount, E);
+  rc |= dmalloc(&a.ep_ret, E);
+  rc |= dmalloc(&a.ep_len, E);
+  rc |= dmalloc(&a.fin_ret, E);
+  rc |= dmalloc(&a.fin_len, E);
+  rc |= dmalloc(&a.fin_cnt, E);
+  if (rc) {
+    psyn_destroy(env);
+    return -2;
+  }
+  *out = env;
+  return 0;
+}
+
+extern "C" int psyn_destroy(psyn_t* env) {
+  if (!env) return 0;
+  SynthArgs& a = env->a;
+  void* ptrs[] = {a.q, a.t, a.autoreset, a.rseed, a.rcount, a.ep_ret, a.ep_len, a.fin_ret, a.fin_len, a.fin_cnt};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  delete env;
+  return 0;
+}
+
+extern "C" int psyn_reset(psyn_t* env, int seed, float* obs, float* done, void* stream) {
+  if (!env || !obs) return fail("psyn_reset: null argument");
+  launch_synth_reset(env->a, seed, obs, done, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+extern "C" int psyn_step(psyn_t* env, int e0, int e1, const float* act, float lo, float hi, float* obs, float* reward,
+                         float* done, void* stream) {
+  if (!env || !act || !obs || !reward || !done) return fail("psyn_step: null argument");
+  if (e0 < 0 || e1 > env->a.E || e0 >= e1) return fail("psyn_step: env range out of bounds");
+  launch_synth_step(env->a, e0, e1, act, lo, hi, obs, reward, done, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+// One full device-resident rollout (ppo:387-434 with the env behind the gymcpp boundary replaced by
+// the synthetic device env): T x {agent act + store, env step, reward store}. next_obs / next_done
+// carry the env state across iterations exactly like the reference's next_obs / next_done tensors.
+extern "C" int ppo_rollout_synth(ppo_t* c, psyn_t* env, float* next_obs, float* next_done, float* act_scratch,
+                                 float* rew_scratch) {
+  if (!c || !env || !next_obs || !next_done || !act_scratch || !rew_scratch) return fail("ppo_rollout_synth: null argument");
+  const int E = c->cfg.num_envs;
+  if (env->a.E != E || env->a.O != c->K.O || env->a.A != c->K.A) return fail("ppo_rollout_synth: env shape mismatch");
+  const float lo = -1.0f, hi = 1.0f;
+  for (int t = 0; t < c->cfg.num_steps; ++t) {
+    int rc = ppo_rollout_act(c, t, 0, E, next_obs, next_done, act_scratch, nullptr);
+    if (rc) return rc;
+    {
+      ProfScope ps(c, PK_SYNTH, c->stream);
+      launch_synth_step(env->a, 0, E, act_scratch, lo, hi, next_obs, rew_scratch, next_done, c->stream);
+    }
+    rc = ppo_rollout_reward(c, t, 0, E, rew_scratch, nullptr);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+extern "C" int psyn_episode_stats(psyn_t* env, float* sr, float* sl, float* sc) {
+  if (!env) return fail("null env");
+  const int E = env->a.E;
+  std::vector<float> r(E), l(E), n(E);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(r.data(), env->a.fin_ret, sizeof(float) * E, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(l.data(), env->a.fin_len, sizeof(float) * E, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(n.data(), env->a.fin_cnt, sizeof(float) * E, hipMemcpyDeviceToHost));
+  double R = 0, Lsum = 0, N = 0;
+  for (int i = 0; i < E; ++i) { R += r[i]; Lsum += l[i]; N += n[i]; }
+  HIP_TRY(hipMemset(env->a.fin_ret, 0, sizeof(float) * E));
+  HIP_TRY(hipMemset(env->a.fin_len, 0, sizeof(float) * E));
+  HIP_TRY(hipMemset(env->a.fin_cnt, 0, sizeof(float) * E));
+  if (sr) *sr = (float)R;
+  if (sl) *sl = (float)Lsum;
+  if (sc) *sc = (float)N;
+  return 0;
+}

@@ -1,0 +1,880 @@
+// ppo_kernels.hip — hand-written gfx950 kernels of the rollout -> GAE -> PPO-update hot path.
+//
+//   k_act        Agent::get_action_and_value / get_value + rollout stores (ppo:145-157, :387-400;
+//                ac:212-249, :649-660). One wave = 16 env rows x one trunk, MFMA 16x16x4 f32.
+//   k_fwdbwd     fused minibatch gather + forward + PPO loss + backward of one trunk
+//                (ppo:495-538, ac:815-875); emits H1/DZ1/DZ2/Xn for the dW GEMMs and the
+//                per-block "small gradient" slab (biases, LayerNorm affine, heads, logstd).
+//   k_dw         dW = DZ^T . IN split-K partial GEMM (MFMA 32x32x2 f32) for the two Linear
+//                weight matrices of each trunk.
+//   k_colsum     deterministic slab reductions -> packed gradient
+//   k_gradnorm   clip_grad_norm_ (norm of per-tensor norms, torch/nn/utils/clip_grad.h)
+//   k_adam       clip scale + optim::Adam step (torch/optim/adam.cpp) + W2^T refresh
+//   k_gae        GAE(lambda) (ppo:447-467) — op-for-op fp32, bit-exact with the reference formula
+//   k_perm / k_adv_*  minibatch permutation and (distributed) advantage statistics (ac:830-849)
+//   k_synth_*    synthetic HalfCheetah-shaped device env (bench/test env; not the hot path)
+#include "ppo_agent.hpp"
+#include "ppo_kernels.hpp"
+
+#include <type_traits>
+
+// =============================================================================================
+// k_act
+// =============================================================================================
+template <int H, int KIND, int NTO>
+__global__ __launch_bounds__(64) void k_act(ActArgs a) {
+  constexpr int NT = H / 16;
+  const int lane = threadIdx.x, j = lane & 15, g = lane >> 4;
+  const int trunk = blockIdx.y;
+  const int row = blockIdx.x * 16 + j;
+  const bool valid = row < a.n;
+  const PackedLayout& K = a.K;
+  const float* __restrict__ P = a.P;
+  const float* xrow = valid ? a.x + (size_t)row * a.ldx : nullptr;
+  const long env = a.env_base + row;
+  const long srow = (long)a.store_step * a.E + env;  // storage row when storing
+
+  f4 xin[NTO];
+  load_input<NTO, KIND>(xin, xrow, K.O, P + (K.omean >= 0 ? K.omean : 0), P + (K.ostd >= 0 ? K.ostd : 0), g);
+  const PBuf pbuf = make_pbuf(P, K.size);
+  f4 h[NT];
+  trunk_forward<H, KIND, NTO>(K.tr[trunk], P, pbuf, xin, h, lane);
+
+  if (trunk == 0) {
+    const float v = head_dot<NT>(h, pbuf, K.cW3, P[K.cb3], g);
+    if (valid && g == 0) {
+      if (a.value_out) a.value_out[row] = v;
+      if (a.store_step >= 0) {
+        a.s_values[srow] = v;
+        a.s_dones[srow] = a.next_done ? a.next_done[row] : 0.0f;
+      }
+    }
+    if (valid && a.store_step >= 0)
+      for (int f = g; f < K.O; f += 4) a.s_obs[srow * K.O + f] = xrow[f];
+    return;
+  }
+  if (!a.need_actor) return;
+
+  const int A = K.A;
+  const SampleKey key = sample_key(a.seed, a.rank);
+  float lp = 0.0f, ent = 0.0f;
+  if constexpr (KIND == PPO_NET_TANH_NORMAL) {
+    for (int ai = 0; ai < A; ++ai) {
+      const float mu = head_dot<NT>(h, pbuf, K.aW3 + ai * H, P[K.ab3 + ai], g);
+      if ((ai & 3) == g) {
+        const float sd = expf(P[K.logstd + ai]);
+        const float var = sd * sd, lsd = logf(sd);
+        float act;
+        if (a.mode == PPO_GIVEN) {
+          act = valid ? a.action_in[(size_t)row * A + ai] : 0.0f;
+        } else if (a.mode == PPO_MEAN) {
+          act = mu;
+        } else {
+          uint32_t rr[4];
+          philox_draw(key, env, a.step_id, (uint32_t)(ai >> 1), rr);
+          float z0, z1;
+          box_muller(rr[0], rr[1], z0, z1);
+          act = mu + ((ai & 1) ? z1 : z0) * sd;
+        }
+        const float d = act - mu;
+        lp += -(d * d) / (2.0f * var) - lsd - kLz;
+        ent += kEntC + lsd;
+        if (valid) {
+          if (a.action_out) a.action_out[(size_t)row * A + ai] = act;
+          if (a.store_step >= 0) a.s_actions[srow * A + ai] = act;
+        }
+      }
+    }
+  } else {
+    const float hi = P[K.hi], lo = P[K.lo];
+    for (int ai = 0; ai < A; ++ai) {
+      const float pa = head_dot<NT>(h, pbuf, K.aW3 + ai * H, P[K.ab3 + ai], g);
+      const float pb = head_dot<NT>(h, pbuf, K.bW3 + ai * H, P[K.bb3 + ai], g);
+      if ((ai & 3) == g) {
+        const float al = softplusf_(pa) + 1.0f, be = softplusf_(pb) + 1.0f;
+        float s;
+        if (a.mode == PPO_GIVEN) {
+          const float av = valid ? a.action_in[(size_t)row * A + ai] : 0.5f * (hi + lo);
+          s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+          s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
+        } else if (a.mode == PPO_MEAN) {
+          s = al / (al + be);
+        } else {
+          const float ga = gamma_mt(al, key, env, a.step_id, 0x10000u + (uint32_t)(ai * 2 + 0) * 64u);
+          const float gb = gamma_mt(be, key, env, a.step_id, 0x10000u + (uint32_t)(ai * 2 + 1) * 64u);
+          s = ga / (ga + gb);
+        }
+        const float ab = al + be;
+        const float lga = lgammaf(al), lgb = lgammaf(be), lgab = lgammaf(ab);
+        lp += xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
+        ent += (lga + lgb) - lgab - (2.0f - ab) * digammaf_(ab) -
+               ((al - 1.0f) * digammaf_(al) + (be - 1.0f) * digammaf_(be));
+        const float act = (s - 0.0f) / (1.0f - 0.0f) * (hi - lo) + lo;
+        if (valid) {
+          if (a.action_out) a.action_out[(size_t)row * A + ai] = act;
+          if (a.store_step >= 0) a.s_actions[srow * A + ai] = act;
+        }
+      }
+    }
+  }
+  lp = row_allreduce(lp);
+  ent = row_allreduce(ent);
+  if (valid && g == 0) {
+    if (a.logprob_out) a.logprob_out[row] = lp;
+    if (a.entropy_out) a.entropy_out[row] = ent;
+    if (a.store_step >= 0) a.s_logp[srow] = lp;
+  }
+}
+
+// =============================================================================================
+// k_fwdbwd — fused gather + forward + loss + backward of one trunk for 16 rows per wave
+// =============================================================================================
+
+// Butterfly reduce-scatter of a per-lane feature vector over the 16 rows of a wave (lanes with the
+// same g). On return lane j holds V/16 sums: slots [(V/16) j, (V/16)(j+1)), slot s <-> feature
+// 16 (s >> 2) + 4 g + (s & 3). Adds them into the wave's LDS accumulator at `acc` (feature index).
+template <int NT, typename Fn>
+PPO_DEV void rows_reduce_fn(Fn f, float* acc, int lane) {
+  constexpr int V = 4 * NT;
+  const int j = lane & 15, g = lane >> 4;
+  float v[V / 2];
+  {
+    const bool bit = (j & 8) != 0;
+#pragma unroll
+    for (int i = 0; i < V / 2; ++i) {
+      const float lo = f(i), hi = f(i + V / 2);
+      const float keep = bit ? hi : lo, send = bit ? lo : hi;
+      v[i] = keep + shfl_xor(send, 8);
+    }
+  }
+#pragma unroll
+  for (int m = 4, len = V / 2; m >= 1; m >>= 1, len >>= 1) {
+    const bool bit = (j & m) != 0;
+#pragma unroll
+    for (int i = 0; i < len / 2; ++i) {
+      const float lo = v[i], hi = v[i + len / 2];
+      const float keep = bit ? hi : lo, send = bit ? lo : hi;
+      v[i] = keep + shfl_xor(send, m);
+    }
+  }
+  constexpr int PER = V / 16;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int s = PER * j + q;
+    const int f2 = 16 * (s >> 2) + 4 * g + (s & 3);
+    acc[f2] += v[q];
+  }
+}
+#define SLOT(arr, s) (arr)[(s) >> 2][(s) & 3]
+
+// per-row scalar -> sum over the 16 rows of lane group g; lane j == 0 of the group gets the sum
+PPO_DEV float rows_sum16(float v) {
+  v += shfl_xor(v, 1);
+  v += shfl_xor(v, 2);
+  v += shfl_xor(v, 4);
+  v += shfl_xor(v, 8);
+  return v;
+}
+
+template <int NT>
+PPO_DEV void store_rows(float* __restrict__ dst, int ld, const f4 (&v)[NT], bool valid, int g) {
+  if (!valid) return;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) st4(dst + 16 * t + 4 * g, v[t]);
+}
+
+template <int H, int KIND, int NTO>
+__global__ __launch_bounds__(256) void k_fwdbwd(UpdArgs a) {
+  constexpr int NT = H / 16;
+  constexpr int V = 4 * NT;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 15, g = lane >> 4;
+  const int trunk = blockIdx.y;
+  const PackedLayout& K = a.K;
+  const TrunkDev& T = K.tr[trunk];
+  const float* __restrict__ P = a.P;
+  const PBuf pbuf = make_pbuf(P, K.size);
+  const SmallGradLayout sg = a.sg[trunk];
+  float* acc = lds + wave * sg.size;
+  for (int i = lane; i < sg.size; i += 64) acc[i] = 0.0f;
+
+  const int O = K.O, A = K.A, OP = K.OP;
+  const float c = a.clip_coef;
+  const float adv_mean = a.adv_stats[0], adv_std = a.adv_stats[1];
+
+  for (int tile = 0; tile < a.tiles_per_block; ++tile) {
+    const int m = (blockIdx.x * a.tiles_per_block + tile) * 64 + wave * 16 + j;
+    const bool valid = m < a.M;
+    const long b = valid ? (long)a.perm[m] : 0;
+    const float* xrow = valid ? a.obs + b * O : nullptr;
+    f4 xin[NTO];
+    load_input<NTO, KIND>(xin, xrow, O, P + (K.omean >= 0 ? K.omean : 0), P + (K.ostd >= 0 ? K.ostd : 0), g);
+    if (trunk == 0) store_rows<NTO>(a.Xn + (size_t)m * OP, OP, xin, valid, g);
+
+    // ---------------- forward ----------------
+    f4 hA[NT];   // layer-1 output; later dh1 accumulator
+    f4 hC[NT];   // layer-2: x_hat2 (LN) or h2 (tanh); later dz2
+    float mu1 = 0.f, rs1 = 0.f, mu2 = 0.f, rs2 = 0.f;
+    mm_layer<NT, NTO, NTO * 16, true>(hA, xin, P + T.W1, P + T.b1, lane);
+    if constexpr (KIND == PPO_NET_LN_BETA) {
+      ln_stats<NT>(hA, mu1, rs1);
+      ln_normalize<NT>(hA, mu1, rs1);
+      affine_relu<NT>(hA, hA, pbuf, T.g1, T.be1, g);
+    } else {
+      tanh_inplace<NT>(hA);
+    }
+    store_rows<NT>(a.H1[trunk] + (size_t)m * H, H, hA, valid, g);
+    mm_layer<NT, NT, H, true>(hC, hA, P + T.W2, P + T.b2, lane);
+    if constexpr (KIND == PPO_NET_LN_BETA) {
+      ln_stats<NT>(hC, mu2, rs2);
+      ln_normalize<NT>(hC, mu2, rs2);  // hC = x_hat2
+    } else {
+      tanh_inplace<NT>(hC);  // hC = h2
+    }
+    // h2 view (recomputed from x_hat2 for the LN net)
+    auto h2_tile = [&](int t) -> f4 {
+      if constexpr (KIND == PPO_NET_LN_BETA) {
+        const f4 gm = pld4(pbuf, 4 * g, T.g2 + 16 * t), bt = pld4(pbuf, 4 * g, T.be2 + 16 * t);
+        f4 r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float y = __fmaf_rn(gm[q], hC[t][q], bt[q]);
+          r[q] = y > 0.0f ? y : 0.0f;
+        }
+        return r;
+      } else {
+        return hC[t];
+      }
+    };
+    // f4 h2[NT] materialised once (needed by several head loops)
+    f4 h2[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) h2[t] = h2_tile(t);
+
+    // ---------------- heads + loss (per row) + head backward ----------------
+    f4 dh[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) dh[t] = f4{0.f, 0.f, 0.f, 0.f};
+    float st_pg = 0.f, st_v = 0.f, st_ent = 0.f, st_okl = 0.f, st_kl = 0.f, st_cf = 0.f;
+
+    if (trunk == 0) {
+      const float v = head_dot<NT>(h2, pbuf, K.cW3, P[K.cb3], g);
+      const float rt = valid ? a.ret[b] : 0.f, ov = valid ? a.val[b] : 0.f;
+      float gv;
+      if (a.clip_vloss) {
+        const float vu = (v - rt) * (v - rt);
+        const float dv = v - ov;
+        const float vcl = ov + fminf(fmaxf(dv, -c), c);
+        const float vc = (vcl - rt) * (vcl - rt);
+        st_v = fmaxf(vu, vc);
+        const float w1 = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
+        const float inr = (dv >= -c && dv <= c) ? 1.0f : 0.0f;
+        gv = 0.5f * a.vf_coef * a.inv_m * (w1 * 2.0f * (v - rt) + (1.0f - w1) * 2.0f * (vcl - rt) * inr);
+      } else {
+        st_v = (v - rt) * (v - rt);
+        gv = 0.5f * a.vf_coef * a.inv_m * 2.0f * (v - rt);
+      }
+      if (!valid) { gv = 0.f; st_v = 0.f; }
+      // head weight / bias grads and dh2
+#pragma unroll
+      for (int t = 0; t < NT; ++t) dh[t] = pld4(pbuf, 4 * g, K.cW3 + 16 * t) * gv;
+      rows_reduce_fn<NT>([&](int sI) { return gv * SLOT(h2, sI); }, acc + sg.hW, lane);
+      const float gsum = rows_sum16(gv);
+      if (lane == 0) acc[sg.hb] += gsum;
+    } else {
+      // ---- actor: pass 1 (log-prob, entropy of the stored action) ----
+      float lp = 0.f, ent = 0.f;
+      float own_x[5], own_p[5], own_q[5];  // per owned action dim (a = g + 4k): action / head pre-acts
+#pragma unroll
+      for (int k = 0; k < 5; ++k) { own_x[k] = 0.f; own_p[k] = 0.f; own_q[k] = 0.f; }
+      if constexpr (KIND == PPO_NET_TANH_NORMAL) {
+        for (int ai = 0; ai < A; ++ai) {
+          const float mu = head_dot<NT>(h2, pbuf, K.aW3 + ai * H, P[K.ab3 + ai], g);
+          if ((ai & 3) == g) {
+            const float sd = expf(P[K.logstd + ai]);
+            const float var = sd * sd, lsd = logf(sd);
+            const float act = valid ? a.actions[b * A + ai] : mu;
+            const float d = act - mu;
+            lp += -(d * d) / (2.0f * var) - lsd - kLz;
+            ent += kEntC + lsd;
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+              if ((ai >> 2) == k) { own_x[k] = act; own_p[k] = mu; }
+          }
+        }
+      } else {
+        const float hi = P[K.hi], lo = P[K.lo];
+        for (int ai = 0; ai < A; ++ai) {
+          const float pa = head_dot<NT>(h2, pbuf, K.aW3 + ai * H, P[K.ab3 + ai], g);
+          const float pb = head_dot<NT>(h2, pbuf, K.bW3 + ai * H, P[K.bb3 + ai], g);
+          if ((ai & 3) == g) {
+            const float al = softplusf_(pa) + 1.0f, be = softplusf_(pb) + 1.0f;
+            const float av = valid ? a.actions[b * A + ai] : 0.5f * (hi + lo);
+            float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+            s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
+            const float ab = al + be;
+            const float lga = lgammaf(al), lgb = lgammaf(be), lgab = lgammaf(ab);
+            lp += xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
+            ent += (lga + lgb) - lgab - (2.0f - ab) * digammaf_(ab) -
+                   ((al - 1.0f) * digammaf_(al) + (be - 1.0f) * digammaf_(be));
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+              if ((ai >> 2) == k) { own_x[k] = s; own_p[k] = pa; own_q[k] = pb; }
+          }
+        }
+      }
+      lp = row_allreduce(lp);
+      ent = row_allreduce(ent);
+      // ---- PPO clipped surrogate (per row) ----
+      const float oldlp = valid ? a.logp[b] : lp;
+      const float logratio = lp - oldlp;
+      const float ratio = expf(logratio);
+      st_okl = -logratio;
+      st_kl = (ratio - 1.0f) - logratio;
+      st_cf = fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
+      st_ent = ent;
+      float an = valid ? a.adv[b] : 0.f;
+      if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
+      const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
+      const float pg1 = -an * ratio, pg2 = -an * rc;
+      st_pg = fmaxf(pg1, pg2);
+      const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+      const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
+      float g_logp = a.inv_m * (w1 * (-an) + (1.0f - w1) * (-an) * inr) * ratio;
+      float g_ent = -a.ent_coef * a.inv_m;
+      if (!valid) { g_logp = 0.f; g_ent = 0.f; st_pg = st_okl = st_kl = st_cf = st_ent = 0.f; }
+
+      // ---- pass 2: per owned action dim gradients wrt head pre-activations ----
+      float own_ga[5], own_gb[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        own_ga[k] = 0.f; own_gb[k] = 0.f;
+        const int ai = g + 4 * k;
+        if (ai < A) {
+          if constexpr (KIND == PPO_NET_TANH_NORMAL) {
+            const float sd = expf(P[K.logstd + ai]);
+            const float var = sd * sd;
+            const float d = own_x[k] - own_p[k];
+            own_ga[k] = g_logp * d / var;                                 // d loss / d mu
+            own_gb[k] = g_logp * (d * d / var - 1.0f) + g_ent;            // d loss / d logstd
+          } else {
+            const float al = softplusf_(own_p[k]) + 1.0f, be = softplusf_(own_q[k]) + 1.0f;
+            const float ab = al + be, s = own_x[k];
+            const float psab = digammaf_(ab), tab = trigammaf_(ab);
+            const float dla = ((al - 1.0f) != 0.0f ? logf(s) : 0.0f) + psab - digammaf_(al);
+            const float dlb = ((be - 1.0f) != 0.0f ? logf(1.0f - s) : 0.0f) + psab - digammaf_(be);
+            const float dea = (ab - 2.0f) * tab - (al - 1.0f) * trigammaf_(al);
+            const float deb = (ab - 2.0f) * tab - (be - 1.0f) * trigammaf_(be);
+            own_ga[k] = (g_logp * dla + g_ent * dea) * softplus_d(own_p[k]);
+            own_gb[k] = (g_logp * dlb + g_ent * deb) * softplus_d(own_q[k]);
+          }
+        }
+      }
+      // scalar grads: head biases (and logstd) summed over the wave's rows
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const float sa = rows_sum16(own_ga[k]);
+        const float sb = rows_sum16(own_gb[k]);
+        const int ai = g + 4 * k;
+        if (j == 0 && ai < A) {
+          acc[sg.hb + ai] += sa;
+          if constexpr (KIND == PPO_NET_TANH_NORMAL) acc[sg.ls + ai] += sb;
+          else acc[sg.hb + A + ai] += sb;
+        }
+      }
+      // head weight grads + dh2: every lane needs every head's per-row gradient
+      const int nh = (KIND == PPO_NET_TANH_NORMAL) ? A : 2 * A;
+      for (int hk = 0; hk < nh; ++hk) {
+        const int ai = hk % A;
+        const bool second = hk >= A;
+        float mine = 0.f;
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+          if ((ai >> 2) == k) mine = second ? own_gb[k] : own_ga[k];
+        const float gk = __shfl(mine, j + 16 * (ai & 3), 64);
+        const int wrow = (KIND == PPO_NET_TANH_NORMAL) ? K.aW3 + ai * H : (second ? K.bW3 + ai * H : K.aW3 + ai * H);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) dh[t] += pld4(pbuf, 4 * g, wrow + 16 * t) * gk;
+        rows_reduce_fn<NT>([&](int sI) { return gk * SLOT(h2, sI); }, acc + sg.hW + hk * H, lane);
+      }
+    }
+    // loss statistics (one lane group per row)
+    {
+      const float s0 = rows_sum16(g == 0 ? st_pg : 0.f), s1 = rows_sum16(g == 0 ? st_v : 0.f);
+      const float s2 = rows_sum16(g == 0 ? st_ent : 0.f), s3 = rows_sum16(g == 0 ? st_okl : 0.f);
+      const float s4 = rows_sum16(g == 0 ? st_kl : 0.f), s5 = rows_sum16(g == 0 ? st_cf : 0.f);
+      if (lane == 0) {
+        acc[sg.stats + ST_PG] += s0; acc[sg.stats + ST_V] += s1; acc[sg.stats + ST_ENT] += s2;
+        acc[sg.stats + ST_OKL] += s3; acc[sg.stats + ST_KL] += s4; acc[sg.stats + ST_CF] += s5;
+      }
+    }
+
+    // ---------------- layer-2 backward: dh2 -> dz2 (in hC) ----------------
+    {
+      if constexpr (KIND == PPO_NET_LN_BETA) {
+        // dy2 = dh2 * relu'(y2); dgamma2, dbeta2; LN backward
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const f4 gm = pld4(pbuf, 4 * g, T.g2 + 16 * t);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float dy = h2[t][q] > 0.0f ? dh[t][q] : 0.0f;  // y2 > 0 <=> relu output > 0
+            dh[t][q] = dy;
+            const float dx = dy * gm[q];
+            s1 += dx;
+            s2 += dx * hC[t][q];
+          }
+        }
+        s1 = row_allreduce(s1) * (1.0f / H);
+        s2 = row_allreduce(s2) * (1.0f / H);
+        rows_reduce_fn<NT>([&](int sI) { return SLOT(dh, sI); }, acc + sg.be2, lane);
+        rows_reduce_fn<NT>([&](int sI) { return SLOT(dh, sI) * SLOT(hC, sI); }, acc + sg.g2, lane);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const f4 gm = pld4(pbuf, 4 * g, T.g2 + 16 * t);
+          hC[t] = rs2 * (dh[t] * gm - s1 - hC[t] * s2);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) hC[t] = dh[t] * (1.0f - hC[t] * hC[t]);
+      }
+      rows_reduce_fn<NT>([&](int sI) { return SLOT(hC, sI); }, acc + sg.b2, lane);
+      store_rows<NT>(a.DZ2[trunk] + (size_t)m * H, H, hC, valid, g);
+    }
+    // ---------------- dh1 = W2^T dz2 ----------------
+    mm_layer<NT, NT, H, false>(dh, hC, a.W2T[trunk], nullptr, lane);
+    // ---------------- recompute layer 1, layer-1 backward ----------------
+    mm_layer<NT, NTO, NTO * 16, true>(hA, xin, P + T.W1, P + T.b1, lane);
+    {
+      if constexpr (KIND == PPO_NET_LN_BETA) {
+        ln_normalize<NT>(hA, mu1, rs1);  // x_hat1 (bit-identical recompute)
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const f4 gm = pld4(pbuf, 4 * g, T.g1 + 16 * t), bt = pld4(pbuf, 4 * g, T.be1 + 16 * t);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float y = __fmaf_rn(gm[q], hA[t][q], bt[q]);
+            const float dy = y > 0.0f ? dh[t][q] : 0.0f;
+            dh[t][q] = dy;
+            const float dx = dy * gm[q];
+            s1 += dx;
+            s2 += dx * hA[t][q];
+          }
+        }
+        s1 = row_allreduce(s1) * (1.0f / H);
+        s2 = row_allreduce(s2) * (1.0f / H);
+        rows_reduce_fn<NT>([&](int sI) { return SLOT(dh, sI); }, acc + sg.be1, lane);
+        rows_reduce_fn<NT>([&](int sI) { return SLOT(dh, sI) * SLOT(hA, sI); }, acc + sg.g1, lane);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const f4 gm = pld4(pbuf, 4 * g, T.g1 + 16 * t);
+          hA[t] = rs1 * (dh[t] * gm - s1 - hA[t] * s2);
+        }
+      } else {
+        tanh_inplace<NT>(hA);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) hA[t] = dh[t] * (1.0f - hA[t] * hA[t]);
+      }
+      rows_reduce_fn<NT>([&](int sI) { return SLOT(hA, sI); }, acc + sg.b1, lane);
+      store_rows<NT>(a.DZ1[trunk] + (size_t)m * H, H, hA, valid, g);
+    }
+  }
+  // ---------------- block reduction of the 4 wave accumulators (fixed order) ----------------
+  __syncthreads();
+  float* out = a.slab[trunk] + (size_t)blockIdx.x * sg.size;
+  for (int i = threadIdx.x; i < sg.size; i += blockDim.x)
+    out[i] = ((lds[i] + lds[sg.size + i]) + lds[2 * sg.size + i]) + lds[3 * sg.size + i];
+}
+
+// =============================================================================================
+// k_dw — partial dW[o][i] = sum_{m in chunk} DZ[m][o] * IN[m][i]   (MFMA 32x32x2 f32)
+//   block = WAVES waves; wave w owns o-tiles [w*TOW, (w+1)*TOW) of the block's o range and all
+//   TI i-tiles. Operands straight from HBM/L2: A lane (o, h) = DZ[m0+2s+h][o], B = IN[m0+2s+h][i].
+// =============================================================================================
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+template <int WAVES, int TOW, int TI>
+__global__ __launch_bounds__(WAVES * 64) void k_dw(DwArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l32 = lane & 31, hsel = lane >> 5;
+  const int job = blockIdx.z;
+  const DwJob& J = a.job[job];
+  const int chunk = blockIdx.x;
+  const int obase = blockIdx.y * (WAVES * TOW * 32) + wave * TOW * 32;
+  const long m0 = (long)chunk * a.rows_per_chunk;
+  const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
+  f16v acc[TOW][TI];
+#pragma unroll
+  for (int u = 0; u < TOW; ++u)
+#pragma unroll
+    for (int v = 0; v < TI; ++v)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[u][v][r] = 0.0f;
+  const float* __restrict__ DZ = J.dz;
+  const float* __restrict__ IN = J.in;
+#pragma unroll 4
+  for (long m = m0; m < m1; m += 2) {
+    const long mr = m + hsel;
+    const bool ok = mr < m1;
+    float av[TOW], bv[TI];
+#pragma unroll
+    for (int u = 0; u < TOW; ++u) av[u] = ok ? DZ[mr * J.ld_dz + obase + u * 32 + l32] : 0.0f;
+#pragma unroll
+    for (int v = 0; v < TI; ++v) bv[v] = (ok && v * 32 + l32 < J.n_in_store) ? IN[mr * J.ld_in + v * 32 + l32] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < TOW; ++u)
+#pragma unroll
+      for (int v = 0; v < TI; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[v], acc[u][v], 0, 0, 0);
+  }
+  float* out = J.out + (size_t)chunk * J.slab_stride;
+#pragma unroll
+  for (int u = 0; u < TOW; ++u)
+#pragma unroll
+    for (int v = 0; v < TI; ++v)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = obase + u * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
+        const int i = v * 32 + l32;
+        if (o < J.n_out && i < J.n_in_store) out[(size_t)o * J.ld_out + i] = acc[u][v][r];
+      }
+}
+
+// =============================================================================================
+// k_colsum — dst[seg] = sum_{c < C} src[c * stride + seg]   (fixed order => deterministic)
+// =============================================================================================
+__global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
+  const int s = blockIdx.y;
+  const ColsumSeg& S = a.seg[s];
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= S.len) return;
+  const float* src = S.src + i;
+  float acc = 0.0f;
+  for (int cI = 0; cI < S.count; ++cI) acc += src[(size_t)cI * S.stride];
+  S.dst[i] = acc * S.scale;
+}
+
+// =============================================================================================
+// k_gradnorm — clip_grad_norm_: per-tensor L2 norms (fp32 tensors), norm of norms, clip coef
+// =============================================================================================
+__global__ __launch_bounds__(1024) void k_gradnorm(NormArgs a) {
+  __shared__ float red[32];
+  __shared__ float norms[PPO_LAYOUT_MAX_TENSORS];
+  const int tid = threadIdx.x;
+  for (int t = 0; t < a.nt; ++t) {
+    float s = 0.0f;
+    for (int i = tid; i < a.len[t]; i += 1024) {
+      const float gv = a.grad[a.off[t] + i];
+      s += gv * gv;
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = s;
+    __syncthreads();
+    if (tid == 0) {
+      float tot = 0.0f;
+      for (int w = 0; w < 16; ++w) tot += red[w];
+      norms[t] = sqrtf(tot);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    float tot = 0.0f;
+    for (int t = 0; t < a.nt; ++t) tot += norms[t] * norms[t];
+    const float total = sqrtf(tot);
+    float coef = a.max_norm / (total + 1e-6f);
+    coef = coef > 1.0f ? 1.0f : coef;
+    a.out[0] = total;
+    a.out[1] = coef;
+  }
+}
+
+// =============================================================================================
+// k_adam — grad *= clip coef; Adam (bias-corrected, torch::optim::Adam); refresh W2^T copies
+// =============================================================================================
+__global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const long p = a.begin + i;
+  const float coef = a.norm_out ? a.norm_out[1] : 1.0f;
+  const float gv = a.grad[p] * coef;
+  const float m = a.m[p] * 0.9f + gv * 0.1f;
+  const float v = a.v[p] * 0.999f + gv * gv * 0.001f;
+  a.m[p] = m;
+  a.v[p] = v;
+  const float denom = sqrtf(v) / a.sbc2 + a.eps;
+  const float np = a.param[p] - a.step_size * (m / denom);
+  a.param[p] = np;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const long o = p - a.w2_off[k];
+    if (o >= 0 && o < (long)a.H * a.H) {
+      const int r = (int)(o / a.H), cI = (int)(o % a.H);
+      a.w2t[k][(size_t)cI * a.H + r] = np;
+    }
+  }
+}
+
+__global__ void k_transpose(const float* __restrict__ src, float* __restrict__ dst, int H) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= H * H) return;
+  const int r = i / H, c = i % H;
+  dst[(size_t)c * H + r] = src[i];
+}
+
+// =============================================================================================
+// k_gae — one thread per env, t = T-1 .. 0; op-for-op fp32 (no contraction), ppo:447-467
+// =============================================================================================
+__global__ __launch_bounds__(256) void k_gae(GaeArgs a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.E) return;
+  const long E = a.E;
+  const float gl = __fmul_rn(a.gamma, a.lam);
+  float last = 0.0f;
+  float nnt = __fsub_rn(1.0f, a.next_done[e]);
+  float nv = a.next_value[e];
+  for (int t = a.T - 1; t >= 0; --t) {
+    const long idx = (long)t * E + e;
+    const float r = a.rewards[idx], v = a.values[idx];
+    const float gnv = __fmul_rn(a.gamma, nv);
+    const float delta = __fsub_rn(__fadd_rn(r, __fmul_rn(gnv, nnt)), v);
+    const float adv = __fadd_rn(delta, __fmul_rn(__fmul_rn(gl, nnt), last));
+    a.adv[idx] = adv;
+    a.ret[idx] = __fadd_rn(adv, v);
+    last = adv;
+    nnt = __fsub_rn(1.0f, a.dones[idx]);
+    nv = v;
+  }
+}
+
+// =============================================================================================
+// minibatch permutations and advantage statistics
+// =============================================================================================
+__global__ __launch_bounds__(256) void k_perm(int32_t* __restrict__ out, uint32_t B, PermKey pk) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < B) out[i] = (int32_t)perm_index(i, B, pk);
+}
+
+// per minibatch (blockIdx.x): sum of gathered advantages (double) -> local mean
+__global__ __launch_bounds__(1024) void k_adv_sum(AdvArgs a) {
+  __shared__ double red[16];
+  const int mb = blockIdx.x;
+  const int32_t* perm = a.perm + (long)mb * a.M;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < a.M; i += 1024) s += (double)a.adv[perm[i]];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < 16; ++w) t += red[w];
+    a.stats[2 * mb + 0] = (float)(t / a.M);  // local mean (all-reduced with ncclAvg when G > 1)
+  }
+}
+// per minibatch: sum (adv - mean)^2 with the (global) mean -> stats[2mb+1] = local sum of squares
+__global__ __launch_bounds__(1024) void k_adv_sq(AdvArgs a) {
+  __shared__ double red[16];
+  const int mb = blockIdx.x;
+  const int32_t* perm = a.perm + (long)mb * a.M;
+  const float mu = a.stats[2 * mb + 0];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < a.M; i += 1024) {
+    const double d = (double)(a.adv[perm[i]] - mu);
+    s += d * d;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < 16; ++w) t += red[w];
+    a.sq[mb] = (float)t;
+  }
+}
+// std = sqrt(sum_sq_global / (G * M - 1))  (ac:845-846; ppo's Tensor::std() for G = 1)
+__global__ void k_adv_finalize(AdvArgs a) {
+  const int mb = threadIdx.x;
+  if (mb < a.nmb) a.stats[2 * mb + 1] = sqrtf((float)((double)a.sq[mb] / (double)(a.world * (long)a.M - 1)));
+}
+
+// =============================================================================================
+// synthetic device env (SeqVectorEnv + RecordEpisodeStatistics semantics; bit-identical to the
+// host SyntheticCheetah and the oracle)
+// =============================================================================================
+PPO_DEV void synth_reset_one(SynthArgs& a, int e, int seed, float* obs) {
+  if (seed > 0) { a.rseed[e] = (uint32_t)seed; a.rcount[e] = 0; }
+  const uint32_t rs = a.rseed[e], rc = a.rcount[e];
+  for (int i = 0; i < a.O; ++i) {
+    uint32_t r[4];
+    philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, r);
+    const float q = __fmul_rn(0.1f, __fsub_rn(__fmul_rn(2.0f, u01(r[0])), 1.0f));
+    a.q[(long)e * a.O + i] = q;
+    obs[(long)e * a.O + i] = q;
+  }
+  a.rcount[e] = rc + 1;
+  a.t[e] = 0;
+  a.ep_ret[e] = 0.0f;
+  a.ep_len[e] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_synth_reset(SynthArgs a, int seed, float* obs, float* done) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.E) return;
+  synth_reset_one(a, e, seed + e, obs);
+  a.autoreset[e] = 0;
+  if (done) done[e] = 0.0f;
+}
+
+__global__ __launch_bounds__(256) void k_synth_step(SynthArgs a, int e0, int e1, const float* __restrict__ act,
+                                                    float lo, float hi, float* obs, float* reward, float* done) {
+  const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= e1) return;
+  const int O = a.O, A = a.A;
+  if (a.autoreset[e]) {
+    synth_reset_one(a, e, -1, obs);
+    reward[e] = 0.0f;
+    done[e] = 0.0f;
+    a.autoreset[e] = 0;
+    return;
+  }
+  float* q = a.q + (long)e * O;
+  const float* ar = act + (long)(e - e0) * A;
+  const float xb = q[0];
+  float q0 = q[0];
+  float nq_prev = 0.0f;
+  // q'_i depends on q_{i+1} (old) — walk i ascending keeping the old q_0 for the wrap-around
+  for (int i = 0; i < O; ++i) {
+    const float ai = fminf(fmaxf(ar[i % A], lo), hi);
+    const float qn = (i + 1 < O) ? q[i + 1] : q0;
+    const float nq = __fmaf_rn(0.9f, q[i], __fmaf_rn(0.1f, ai, __fmul_rn(0.05f, qn)));
+    if (i > 0) q[i - 1] = nq_prev;
+    nq_prev = nq;
+  }
+  q[O - 1] = nq_prev;
+  const float vel = __fdiv_rn(__fsub_rn(q[0], xb), 0.05f);
+  float ctrl = 0.0f;
+  for (int k = 0; k < A; ++k) {
+    const float ak = fminf(fmaxf(ar[k], lo), hi);
+    ctrl = __fadd_rn(ctrl, __fmul_rn(__fmul_rn(0.1f, ak), ak));
+  }
+  const float r = __fsub_rn(vel, ctrl);
+  const int t = a.t[e] + 1;
+  a.t[e] = t;
+  const bool tr = t >= 1000;
+  for (int i = 0; i < O; ++i) obs[(long)e * O + i] = q[i];
+  reward[e] = r;
+  done[e] = tr ? 1.0f : 0.0f;
+  a.ep_ret[e] = __fadd_rn(a.ep_ret[e], r);
+  a.ep_len[e] += 1;
+  if (tr) {
+    a.fin_ret[e] += a.ep_ret[e];
+    a.fin_len[e] += (float)a.ep_len[e];
+    a.fin_cnt[e] += 1.0f;
+  }
+  a.autoreset[e] = tr ? 1 : 0;
+}
+
+// =============================================================================================
+// explicit instantiations / launch wrappers
+// =============================================================================================
+// supported (H, kind, OP/16) instantiations: AC agent H=256, PPO agent H=64; inputs up to 384
+template <typename F>
+static int dispatch_net(const PackedLayout& K, F&& f) {
+  const int nto = K.OP / 16;
+#define PPO_NET_CASE(H_, KIND_, NTO_) \
+  if (K.H == H_ && K.kind == KIND_ && nto == NTO_) return f(std::integral_constant<int, H_>{}, std::integral_constant<int, KIND_>{}, std::integral_constant<int, NTO_>{});
+  PPO_NET_CASE(256, PPO_NET_LN_BETA, 1) PPO_NET_CASE(256, PPO_NET_LN_BETA, 2) PPO_NET_CASE(256, PPO_NET_LN_BETA, 7)
+  PPO_NET_CASE(256, PPO_NET_LN_BETA, 24) PPO_NET_CASE(64, PPO_NET_TANH_NORMAL, 1) PPO_NET_CASE(64, PPO_NET_TANH_NORMAL, 2)
+  PPO_NET_CASE(64, PPO_NET_TANH_NORMAL, 7) PPO_NET_CASE(64, PPO_NET_TANH_NORMAL, 24) PPO_NET_CASE(64, PPO_NET_LN_BETA, 2)
+  PPO_NET_CASE(256, PPO_NET_TANH_NORMAL, 2)
+#undef PPO_NET_CASE
+  return -1;
+}
+
+int launch_act(const ActArgs& a, hipStream_t s) {
+  dim3 grid((a.n + 15) / 16, a.need_actor ? 2 : 1);
+  return dispatch_net(a.K, [&](auto H_, auto KIND_, auto NTO_) {
+    hipLaunchKernelGGL((k_act<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value>), grid, dim3(64), 0,
+                       s, a);
+    return 0;
+  });
+}
+
+int launch_fwdbwd(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s) {
+  dim3 grid(nblocks, 2);
+  return dispatch_net(a.K, [&](auto H_, auto KIND_, auto NTO_) {
+    hipLaunchKernelGGL((k_fwdbwd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value>), grid,
+                       dim3(256), lds_bytes, s, a);
+    return 0;
+  });
+}
+
+int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes) {
+  return dispatch_net(K, [&](auto H_, auto KIND_, auto NTO_) {
+    return hipFuncSetAttribute(
+               (const void*)k_fwdbwd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value>,
+               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes) == hipSuccess
+               ? 0
+               : -2;
+  });
+}
+
+// dW jobs: layer-2 (H x H) and layer-1 (H x OP) of each trunk
+int launch_dw(const DwArgs& a, int kind_l2, int H, int OP, int nchunks, int njobs, hipStream_t s) {
+  if (kind_l2) {
+    if (H == 256) {  // 2 blocks of 128 o-rows, 4 waves x 1 o-tile x 8 i-tiles
+      hipLaunchKernelGGL((k_dw<4, 1, 8>), dim3(nchunks, 2, njobs), dim3(256), 0, s, a);
+      return 0;
+    }
+    if (H == 64) {
+      hipLaunchKernelGGL((k_dw<2, 1, 2>), dim3(nchunks, 1, njobs), dim3(128), 0, s, a);
+      return 0;
+    }
+    return -1;
+  }
+  const int TI = OP / 32 + (OP % 32 ? 1 : 0);
+  if (H == 256) {
+    if (TI == 1) { hipLaunchKernelGGL((k_dw<4, 2, 1>), dim3(nchunks, 1, njobs), dim3(256), 0, s, a); return 0; }
+    if (TI == 4) { hipLaunchKernelGGL((k_dw<4, 2, 4>), dim3(nchunks, 1, njobs), dim3(256), 0, s, a); return 0; }
+    if (TI == 12) { hipLaunchKernelGGL((k_dw<4, 2, 12>), dim3(nchunks, 1, njobs), dim3(256), 0, s, a); return 0; }
+  }
+  if (H == 64) {
+    if (TI == 1) { hipLaunchKernelGGL((k_dw<2, 1, 1>), dim3(nchunks, 1, njobs), dim3(128), 0, s, a); return 0; }
+    if (TI == 4) { hipLaunchKernelGGL((k_dw<2, 1, 4>), dim3(nchunks, 1, njobs), dim3(128), 0, s, a); return 0; }
+    if (TI == 12) { hipLaunchKernelGGL((k_dw<2, 1, 12>), dim3(nchunks, 1, njobs), dim3(128), 0, s, a); return 0; }
+  }
+  return -1;
+}
+
+void launch_colsum(const ColsumArgs& a, int nseg, long maxlen, hipStream_t s) {
+  hipLaunchKernelGGL(k_colsum, dim3((unsigned)((maxlen + 255) / 256), nseg), dim3(256), 0, s, a);
+}
+void launch_gradnorm(const NormArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_gradnorm, dim3(1), dim3(1024), 0, s, a); }
+void launch_adam(const AdamArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
+}
+void launch_transpose(const float* src, float* dst, int H, hipStream_t s) {
+  hipLaunchKernelGGL(k_transpose, dim3((H * H + 255) / 256), dim3(256), 0, s, src, dst, H);
+}
+void launch_gae(const GaeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_gae, dim3((a.E + 255) / 256), dim3(256), 0, s, a);
+}
+void launch_perm(int32_t* out, uint32_t B, const PermKey& pk, hipStream_t s) {
+  hipLaunchKernelGGL(k_perm, dim3((B + 255) / 256), dim3(256), 0, s, out, B, pk);
+}
+void launch_adv_sum(const AdvArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_adv_sum, dim3(a.nmb), dim3(1024), 0, s, a); }
+void launch_adv_sq(const AdvArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_adv_sq, dim3(a.nmb), dim3(1024), 0, s, a); }
+void launch_adv_finalize(const AdvArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_adv_finalize, dim3(1), dim3(((a.nmb + 63) / 64) * 64), 0, s, a);
+}
+void launch_synth_reset(const SynthArgs& a, int seed, float* obs, float* done, hipStream_t s) {
+  hipLaunchKernelGGL(k_synth_reset, dim3((a.E + 255) / 256), dim3(256), 0, s, a, seed, obs, done);
+}
+void launch_synth_step(const SynthArgs& a, int e0, int e1, const float* act, float lo, float hi, float* obs,
+                       float* reward, float* done, hipStream_t s) {
+  hipLaunchKernelGGL(k_synth_step, dim3((e1 - e0 + 255) / 256), dim3(256), 0, s, a, e0, e1, act, lo, hi, obs, reward,
+                     done);
+}

@@ -1,0 +1,146 @@
+// ppo_kernels.hpp — kernel argument blocks and launch wrappers (host <-> device contract).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ppo_device.hpp"
+#include "ppo_packed.hpp"
+
+#include "../../include/ppo_hip.h"
+
+struct ActArgs {
+  const float* P;
+  PackedLayout K;
+  int n;
+  const float* x;
+  int ldx;
+  int mode;
+  int need_actor;
+  const float* action_in;
+  uint64_t seed;
+  int rank;
+  long env_base;
+  long step_id;
+  float* action_out;
+  float* logprob_out;
+  float* entropy_out;
+  float* value_out;
+  int store_step;  // < 0: no rollout stores
+  int E;
+  const float* next_done;
+  float *s_obs, *s_actions, *s_logp, *s_dones, *s_values;
+};
+
+struct UpdArgs {
+  const float* P;
+  const float* W2T[2];
+  PackedLayout K;
+  SmallGradLayout sg[2];
+  int M;
+  int tiles_per_block;
+  const int32_t* perm;
+  const float *obs, *actions, *logp, *adv, *ret, *val;
+  const float* adv_stats;  // [2] mean, std of this minibatch
+  float clip_coef, ent_coef, vf_coef, inv_m;
+  int clip_vloss, norm_adv;
+  float* Xn;
+  float* H1[2];
+  float* DZ1[2];
+  float* DZ2[2];
+  float* slab[2];
+};
+
+struct DwJob {
+  const float* dz;
+  const float* in;
+  int ld_dz, ld_in;
+  float* out;
+  long slab_stride;
+  int ld_out, n_out, n_in_store;
+};
+struct DwArgs {
+  DwJob job[4];
+  int M;
+  int rows_per_chunk;
+};
+
+struct ColsumSeg {
+  const float* src;
+  float* dst;
+  long stride;
+  int count;
+  int len;
+  float scale;
+};
+#define PPO_MAX_SEGS 40
+struct ColsumArgs {
+  ColsumSeg seg[PPO_MAX_SEGS];
+};
+
+struct NormArgs {
+  const float* grad;
+  int nt;
+  int off[PPO_LAYOUT_MAX_TENSORS];
+  int len[PPO_LAYOUT_MAX_TENSORS];
+  float max_norm;
+  float* out;  // [0] total norm, [1] clip coefficient
+};
+
+struct AdamArgs {
+  float* param;
+  const float* grad;
+  float *m, *v;
+  long begin, n;
+  const float* norm_out;
+  float step_size, sbc2, eps;
+  long w2_off[2];
+  float* w2t[2];
+  int H;
+};
+
+struct GaeArgs {
+  const float *rewards, *values, *dones, *next_value, *next_done;
+  float *adv, *ret;
+  int T, E;
+  float gamma, lam;
+};
+
+struct AdvArgs {
+  const int32_t* perm;  // [nmb][M]
+  const float* adv;
+  float* stats;         // [nmb][2]
+  float* sq;            // [nmb]
+  int M, nmb, world;
+};
+
+struct SynthArgs {
+  int E, O, A;
+  float* q;
+  int* t;
+  int* autoreset;
+  uint32_t* rseed;
+  uint32_t* rcount;
+  float* ep_ret;
+  int* ep_len;
+  float* fin_ret;
+  float* fin_len;
+  float* fin_cnt;
+};
+
+int launch_act(const ActArgs& a, hipStream_t s);
+int launch_fwdbwd(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s);
+int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes);
+int launch_dw(const DwArgs& a, int kind_l2, int H, int OP, int nchunks, int njobs, hipStream_t s);
+void launch_colsum(const ColsumArgs& a, int nseg, long maxlen, hipStream_t s);
+void launch_gradnorm(const NormArgs& a, hipStream_t s);
+void launch_adam(const AdamArgs& a, hipStream_t s);
+void launch_transpose(const float* src, float* dst, int H, hipStream_t s);
+void launch_gae(const GaeArgs& a, hipStream_t s);
+void launch_perm(int32_t* out, uint32_t B, const PermKey& pk, hipStream_t s);
+void launch_adv_sum(const AdvArgs& a, hipStream_t s);
+void launch_adv_sq(const AdvArgs& a, hipStream_t s);
+void launch_adv_finalize(const AdvArgs& a, hipStream_t s);
+void launch_synth_reset(const SynthArgs& a, int seed, float* obs, float* done, hipStream_t s);
+void launch_synth_step(const SynthArgs& a, int e0, int e1, const float* act, float lo, float hi, float* obs,
+                       float* reward, float* done, hipStream_t s);

@@ -1,0 +1,364 @@
+"""GPU parity of the HIP hot path (through the C-ABI) against the reference-arithmetic golden
+vectors (tests/golden) and the CPU oracle (oracle/ppo_oracle.c) on the same seeded inputs.
+
+Tolerances (fp32 throughout, MFMA f32 = exact fp32 FMA chains, oracle accumulates in double):
+  forward values / log-probs / entropies   rtol 2e-5 .. 1e-4 (sums of O(10) terms)
+  raw gradients                            relative L2 error < 2e-4 overall, < 2e-3 per tensor
+  parameters after Adam                     atol 2e-6 per step (lr = 2.5e-4 .. 3e-4)
+  GAE, env dynamics, permutations           bit-exact
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from golden_io import load_case
+
+pytestmark = pytest.mark.gpu
+
+ppo_amd = pytest.importorskip("ppo_amd")
+from ppo_amd import DeviceArray  # noqa: E402
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def make_agent(kind, O_, A, H, E, T=1, MB=1, EP=1, clip=0.2, ent=0.01, vf=0.5, max_grad_norm=0.5, adam_eps=1e-5,
+               seed=1, norm_adv=1, clip_vloss=1):
+    hc = ppo_amd.HipConfig(kind, O_, A, H, E, T, MB, EP, 0.99, 0.95, clip, ent, vf, max_grad_norm, adam_eps,
+                           norm_adv, clip_vloss, seed, 0, 1)
+    return ppo_amd.Agent(hc)
+
+
+def fill_storage(ag, T, E, obs, act, logp, adv, ret, val):
+    ag.buffer(ppo_amd.BUF_OBS, (T, E, ag.O)).upload(obs.reshape(T, E, ag.O))
+    ag.buffer(ppo_amd.BUF_ACTIONS, (T, E, ag.A)).upload(act.reshape(T, E, ag.A))
+    ag.buffer(ppo_amd.BUF_LOGPROBS, (T, E)).upload(logp.reshape(T, E))
+    ag.buffer(ppo_amd.BUF_ADVANTAGES, (T, E)).upload(adv.reshape(T, E))
+    ag.buffer(ppo_amd.BUF_RETURNS, (T, E)).upload(ret.reshape(T, E))
+    ag.buffer(ppo_amd.BUF_VALUES, (T, E)).upload(val.reshape(T, E))
+
+
+def random_params(L, rng, scale=1.0):
+    p = np.zeros(L.P, np.float32)
+    for t in range(L.ntensors):
+        o, n = L.t_off[t], L.t_len[t]
+        p[o:o + n] = rng.standard_normal(n).astype(np.float32) * 0.1
+    if L.kind == 1:
+        p[L.hi], p[L.lo] = 1.0, -1.0
+        p[L.ostd:L.ostd + L.O] = rng.uniform(0.8, 1.5, L.O)
+        for tr in (L.critic, L.actor):
+            p[tr[2]:tr[2] + L.H] = rng.uniform(0.8, 1.2, L.H)  # LN gamma
+            p[tr[6]:tr[6] + L.H] = rng.uniform(0.8, 1.2, L.H)
+    for tr in (L.critic, L.actor):
+        p[tr[0]:tr[0] + L.H * L.O] = rng.standard_normal(L.H * L.O) / np.sqrt(L.O)
+        p[tr[4]:tr[4] + L.H * L.H] = rng.standard_normal(L.H * L.H) / np.sqrt(L.H)
+    return (p * 1.0).astype(np.float32)
+
+
+# ------------------------------------------------------------------------------------------------
+# act (Agent::get_action_and_value) vs golden and oracle
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("case,kind", [("ppo_act", 0), ("ac_act", 1)])
+def test_act_given_action_vs_golden(case, kind):
+    meta, d = load_case(case)
+    n = d["x"].shape[0]
+    ag = make_agent(kind, meta["O"], meta["A"], meta["H"], n)
+    ag.load_params(d["params"])
+    np.testing.assert_array_equal(ag.params(), d["params"])  # pack/unpack round trip
+    x = DeviceArray.from_numpy(d["x"])
+    a = DeviceArray.from_numpy(d["action"])
+    act, lp, ent, v = ag.get_action_and_value(x, ppo_amd.PPO_GIVEN, a)
+    np.testing.assert_allclose(lp.numpy(), d["logprob"], rtol=2e-5, atol=5e-5)
+    np.testing.assert_allclose(ent.numpy(), d["entropy"], rtol=2e-5, atol=5e-5)
+    np.testing.assert_allclose(v.numpy(), d["value"], rtol=2e-5, atol=2e-5)
+    if kind == 1:
+        np.testing.assert_allclose(act.numpy(), d["action_roundtrip"], rtol=0, atol=2e-7)
+        am, lpm, _, _ = ag.get_action_and_value(x, ppo_amd.PPO_MEAN)
+        np.testing.assert_allclose(am.numpy(), d["mean_action"], rtol=1e-5, atol=2e-6)
+        np.testing.assert_allclose(lpm.numpy(), d["mean_logprob"], rtol=2e-5, atol=5e-5)
+    else:
+        am, _, _, _ = ag.get_action_and_value(x, ppo_amd.PPO_MEAN)
+        np.testing.assert_allclose(am.numpy(), d["mean"], rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("kind,O_,A,H,n", [(1, 17, 6, 256, 1000), (0, 17, 6, 64, 777), (0, 376, 17, 64, 300),
+                                           (1, 105, 8, 256, 200)])
+def test_act_vs_oracle_given_mean_sample(kind, O_, A, H, n):
+    rng = np.random.default_rng(7)
+    ag = make_agent(kind, O_, A, H, n)
+    L = O.layout_init(kind, O_, A, H)
+    p = random_params(L, rng)
+    ag.load_params(p)
+    x = rng.standard_normal((n, O_)).astype(np.float32)
+    act = rng.uniform(-0.95, 0.95, (n, A)).astype(np.float32)
+    if kind == 0:
+        act = rng.standard_normal((n, A)).astype(np.float32)
+    xd, ad = DeviceArray.from_numpy(x), DeviceArray.from_numpy(act)
+    # given action
+    _, lp, ent, v = ag.get_action_and_value(xd, ppo_amd.PPO_GIVEN, ad)
+    _, olp, oent, ov = O.get_action_and_value(L, p, x, 1, act)
+    np.testing.assert_allclose(v.numpy(), ov, rtol=1e-4, atol=5e-5)
+    np.testing.assert_allclose(lp.numpy(), olp, rtol=1e-4, atol=2e-4)
+    np.testing.assert_allclose(ent.numpy(), oent, rtol=1e-4, atol=2e-4)
+    # deterministic mean action
+    am, lpm, _, _ = ag.get_action_and_value(xd, ppo_amd.PPO_MEAN)
+    oam, olpm, _, _ = O.get_action_and_value(L, p, x, 2)
+    np.testing.assert_allclose(am.numpy(), oam, rtol=1e-4, atol=2e-5)
+    # sampled actions: same Philox counters; differences only from libm vs ocml ulps
+    sa, slp, _, _ = ag.get_action_and_value(xd, ppo_amd.PPO_SAMPLE, env_base=5, step_id=123)
+    osa, oslp, _, _ = O.get_action_and_value(L, p, x, 0, seed=1, rank=0, env_base=5, step_id=123)
+    sa = sa.numpy()
+    close = np.isclose(sa, osa, rtol=1e-4, atol=5e-5)
+    assert close.mean() > 0.999, close.mean()   # a rare Marsaglia-Tsang accept flip is allowed
+    rows = close.all(axis=1)
+    np.testing.assert_allclose(slp.numpy()[rows], oslp[rows], rtol=1e-3, atol=1e-3)
+    if kind == 1:
+        assert np.all(sa > -1.0) and np.all(sa < 1.0)
+
+
+def test_beta_sampler_moments():
+    """Marsaglia-Tsang Beta samples have the right mean/variance (replaces at::_sample_dirichlet)."""
+    n, O_, A, H = 8192, 17, 6, 64
+    ag = make_agent(1, O_, A, H, n)
+    L = O.layout_init(1, O_, A, H)
+    p = np.zeros(L.P, np.float32)
+    p[L.hi], p[L.lo] = 1.0, -1.0
+    p[L.ostd:L.ostd + O_] = 1.0
+    for tr in (L.critic, L.actor):
+        p[tr[2]:tr[2] + H] = 1.0; p[tr[6]:tr[6] + H] = 1.0
+    # heads: constant pre-activations -> alpha = softplus(1.5)+1, beta = softplus(-0.5)+1
+    p[L.ab3:L.ab3 + A] = 1.5
+    p[L.bb3:L.bb3 + A] = -0.5
+    ag.load_params(p)
+    x = DeviceArray.from_numpy(np.zeros((n, O_), np.float32))
+    a, _, _, _ = ag.get_action_and_value(x, ppo_amd.PPO_SAMPLE, step_id=99)
+    s = (a.numpy() + 1.0) / 2.0
+    al = np.log1p(np.exp(1.5)) + 1; be = np.log1p(np.exp(-0.5)) + 1
+    mean = al / (al + be); var = al * be / ((al + be) ** 2 * (al + be + 1))
+    assert abs(s.mean() - mean) < 4 * np.sqrt(var / s.size)
+    assert abs(s.var() - var) / var < 0.02
+
+
+# ------------------------------------------------------------------------------------------------
+# GAE
+# ------------------------------------------------------------------------------------------------
+def test_gae_bit_exact_vs_golden():
+    meta, d = load_case("gae")
+    T, E = d["rewards"].shape
+    ag = make_agent(0, 17, 6, 64, E, T=T)
+    ag.buffer(ppo_amd.BUF_REWARDS, (T, E)).upload(d["rewards"])
+    ag.buffer(ppo_amd.BUF_VALUES, (T, E)).upload(d["values"])
+    ag.buffer(ppo_amd.BUF_DONES, (T, E)).upload(d["dones"])
+    ag.gae_from_values(DeviceArray.from_numpy(d["next_value"]), DeviceArray.from_numpy(d["next_done"]))
+    np.testing.assert_array_equal(ag.buffer(ppo_amd.BUF_ADVANTAGES, (T, E)).numpy(), d["advantages"])
+    np.testing.assert_array_equal(ag.buffer(ppo_amd.BUF_RETURNS, (T, E)).numpy(), d["returns"])
+
+
+def test_gae_full_size_bit_exact_vs_oracle():
+    T, E = 128, 4096
+    rng = np.random.default_rng(3)
+    r = rng.standard_normal((T, E)).astype(np.float32)
+    v = rng.standard_normal((T, E)).astype(np.float32)
+    dn = (rng.random((T, E)) < 0.001).astype(np.float32)
+    dn[0] = 1.0
+    nv = rng.standard_normal(E).astype(np.float32)
+    nd = (rng.random(E) < 0.5).astype(np.float32)
+    ag = make_agent(1, 17, 6, 256, E, T=T, MB=4, EP=1)
+    ag.buffer(ppo_amd.BUF_REWARDS, (T, E)).upload(r)
+    ag.buffer(ppo_amd.BUF_VALUES, (T, E)).upload(v)
+    ag.buffer(ppo_amd.BUF_DONES, (T, E)).upload(dn)
+    ag.gae_from_values(DeviceArray.from_numpy(nv), DeviceArray.from_numpy(nd))
+    oa, orr = O.gae(r, v, dn, nv, nd, 0.99, 0.95)
+    np.testing.assert_array_equal(ag.buffer(ppo_amd.BUF_ADVANTAGES, (T, E)).numpy(), oa)
+    np.testing.assert_array_equal(ag.buffer(ppo_amd.BUF_RETURNS, (T, E)).numpy(), orr)
+
+
+# ------------------------------------------------------------------------------------------------
+# minibatch update (loss, backward, clip_grad_norm_, Adam) vs golden
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("case,kind", [("ppo_update", 0), ("ac_update", 1)])
+def test_update_vs_golden(case, kind):
+    meta, d = load_case(case)
+    M = meta["M"]
+    ag = make_agent(kind, meta["O"], meta["A"], meta["H"], M, T=1, MB=1, EP=1, clip=meta["clip_coef"],
+                    ent=meta["ent_coef"], vf=meta["vf_coef"], max_grad_norm=meta["max_grad_norm"],
+                    adam_eps=meta["adam_eps"])
+    ag.load_params(d["params"])
+    fill_storage(ag, 1, M, d["x"], d["action"], d["old_logp"], d["adv"], d["ret"], d["old_v"])
+    perm = DeviceArray.from_numpy(np.arange(M, dtype=np.int32))
+    st = ag.update(meta["lr"], perms=perm)
+    g = ag.last_grad()
+    assert rel(g, d["grad_raw"]) < 2e-4
+    L = ag.layout
+    for t in range(L.ntensors):
+        o, n = L.t_off[t], L.t_len[t]
+        if L.t_grad[t]:
+            assert rel(g[o:o + n], d["grad_raw"][o:o + n]) < 2e-3, t
+    gs = d["stats"]
+    np.testing.assert_allclose([st["pg_loss"], st["v_loss"], st["entropy"], st["old_approx_kl"], st["approx_kl"],
+                                st["clipfrac"]], gs[:6], rtol=2e-4, atol=2e-5)
+    np.testing.assert_allclose(st["grad_norm"], d["total_norm"][0], rtol=2e-4)
+    np.testing.assert_allclose(ag.params(), d["params_step1"], rtol=0, atol=2e-6)
+    ag.update(meta["lr"], perms=perm)
+    ag.update(meta["lr"], perms=perm)
+    np.testing.assert_allclose(ag.params(), d["params_step3"], rtol=0, atol=6e-6)
+
+
+@pytest.mark.parametrize("kind,O_,A,H,E,T,MB", [(1, 17, 6, 256, 256, 4, 1), (1, 17, 6, 256, 200, 3, 2),
+                                               (0, 376, 17, 64, 96, 4, 2), (1, 105, 8, 256, 64, 4, 1)])
+def test_minibatch_grad_vs_oracle(kind, O_, A, H, E, T, MB):
+    rng = np.random.default_rng(11)
+    L = O.layout_init(kind, O_, A, H)
+    p = random_params(L, rng)
+    B = T * E
+    x = rng.standard_normal((B, O_)).astype(np.float32)
+    act = (rng.uniform(-0.95, 0.95, (B, A)) if kind else rng.standard_normal((B, A))).astype(np.float32)
+    _, lp0, _, v0 = O.get_action_and_value(L, p, x, 1, act)
+    olp = (lp0 + rng.standard_normal(B) * 0.1).astype(np.float32)
+    ov = (v0 + rng.standard_normal(B) * 0.1).astype(np.float32)
+    adv = rng.standard_normal(B).astype(np.float32)
+    ret = rng.standard_normal(B).astype(np.float32)
+    clip = 0.1 if kind else 0.2
+    ag = make_agent(kind, O_, A, H, E, T=T, MB=MB, EP=1, clip=clip)
+    ag.load_params(p)
+    fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
+    perm = rng.permutation(B).astype(np.int32)
+    ag.update(2.5e-4, perms=DeviceArray.from_numpy(perm))
+    g = ag.last_grad()
+    M = B // MB
+    sl = perm[(MB - 1) * M:]  # last minibatch
+    cfg = O.LossCfg(clip, 0.01, 0.5, 1, 1)
+    if MB == 1:
+        og, _ = O.minibatch_grad(L, p, x[sl], act[sl], olp[sl], adv[sl], ret[sl], ov[sl], cfg)
+        assert rel(g, og) < 5e-4
+        for t in range(L.ntensors):
+            o, n = L.t_off[t], L.t_len[t]
+            if L.t_grad[t]:
+                assert rel(g[o:o + n], og[o:o + n]) < 5e-3, (t, rel(g[o:o + n], og[o:o + n]))
+    # whole update (all minibatches, clip + Adam) vs the oracle's update loop
+    ag2 = make_agent(kind, O_, A, H, E, T=T, MB=MB, EP=1, clip=clip)
+    ag2.load_params(p)
+    fill_storage(ag2, T, E, x, act, olp, adv, ret, ov)
+    ag2.update(2.5e-4, perms=DeviceArray.from_numpy(perm))
+    op, _, _, _, _ = O.update(L, p, np.zeros(L.P), np.zeros(L.P), 0, x, act, olp, adv, ret, ov, 1, MB, 2.5e-4, 0.5,
+                              1e-5, cfg, perms=perm.astype(np.int64)[None, :])
+    np.testing.assert_allclose(ag2.params(), op, rtol=0, atol=2e-6 * MB)
+
+
+def test_permutation_matches_oracle_and_is_a_permutation():
+    """Feistel minibatch permutation (replaces torch::randperm) — bit-exact with the oracle."""
+    E, T, MB, EP = 64, 8, 2, 2
+    rng = np.random.default_rng(5)
+    L = O.layout_init(0, 17, 6, 64)
+    p = random_params(L, rng)
+    B = E * T
+    x = rng.standard_normal((B, 17)).astype(np.float32)
+    act = rng.standard_normal((B, 6)).astype(np.float32)
+    _, lp0, _, v0 = O.get_action_and_value(L, p, x, 1, act)
+    adv = rng.standard_normal(B).astype(np.float32)
+    ret = rng.standard_normal(B).astype(np.float32)
+    ag = make_agent(0, 17, 6, 64, E, T=T, MB=MB, EP=EP)
+    ag.load_params(p)
+    fill_storage(ag, T, E, x, act, lp0, adv, ret, v0)
+    ag.set_iteration(3)
+    ag.update(3e-4)
+    cfg = O.LossCfg(0.2, 0.01, 0.5, 1, 1)
+    op, _, _, _, _ = O.update(L, p, np.zeros(L.P), np.zeros(L.P), 0, x, act, lp0, adv, ret, v0, EP, MB, 3e-4, 0.5,
+                              1e-5, cfg, seed=1, rank=0, epoch_counter0=3 * EP)
+    np.testing.assert_allclose(ag.params(), op, rtol=0, atol=1e-5)
+    for B_ in (1, 7, 64, 1000, 524288):
+        pr = O.perm(B_, 1, 0, 5)
+        assert np.array_equal(np.sort(pr), np.arange(B_))
+
+
+# ------------------------------------------------------------------------------------------------
+# synthetic device env vs oracle env (bit-exact) and a full small iteration vs the oracle
+# ------------------------------------------------------------------------------------------------
+def test_synth_env_bit_exact_vs_oracle():
+    E, O_, A = 300, 17, 6
+    env = ppo_amd.SynthEnv(E, O_, A)
+    oenv = O.SynthEnv(E, O_, A)
+    obs = DeviceArray((E, O_)); done = DeviceArray(E); rew = DeviceArray(E)
+    env.reset(7, obs, done)
+    o_obs = oenv.reset(7)
+    np.testing.assert_array_equal(obs.numpy(), o_obs)
+    rng = np.random.default_rng(0)
+    for t in range(1005):
+        a = rng.uniform(-1.3, 1.3, (E, A)).astype(np.float32)
+        env.step(DeviceArray.from_numpy(a), obs, rew, done)
+        o_obs, o_r, o_te, o_tr, _, _ = oenv.step(a)
+        if t % 97 == 0 or t >= 998:
+            np.testing.assert_array_equal(obs.numpy(), o_obs)
+            np.testing.assert_array_equal(rew.numpy(), o_r)
+            np.testing.assert_array_equal(done.numpy(), np.maximum(o_te, o_tr))
+    sr, sl, n = env.episode_stats()
+    assert n == E and abs(sl - 1000 * E) < 1e-3
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_full_iteration_vs_oracle(kind):
+    """rollout (act + env) -> GAE -> update for E=64, T=16, MB=2, EP=2, against the oracle doing
+    the same with the same Philox counters and Feistel permutations."""
+    E, T, MB, EP = 64, 16, 2, 2
+    O_, A, H = 17, 6, (64 if kind == 0 else 256)
+    rng = np.random.default_rng(21)
+    L = O.layout_init(kind, O_, A, H)
+    p = random_params(L, rng)
+    if kind == 0:
+        p[L.logstd:L.logstd + A] = -0.5
+    clip = 0.2 if kind == 0 else 0.1
+    cfg = ppo_amd.PPOConfig(num_envs=E, num_steps=T, num_minibatches=MB, update_epochs=EP, env_id="HalfCheetah-v5",
+                            net_kind=kind, hidden=H, clip_coef=clip, ent_coef=0.01, total_timesteps=E * T * 4)
+    tr = ppo_amd.Trainer(cfg, params=p)
+    tr.iterate()
+    gpu_p = tr.agent.params()
+    gpu_obs = tr.agent.buffer(ppo_amd.BUF_OBS, (T, E, O_)).numpy()
+    gpu_adv = tr.agent.buffer(ppo_amd.BUF_ADVANTAGES, (T, E)).numpy()
+    # oracle replay
+    oenv = O.SynthEnv(E, O_, A)
+    nobs = oenv.reset(cfg.seed)
+    ndone = np.zeros(E, np.float32)
+    bo = np.zeros((T, E, O_), np.float32); ba = np.zeros((T, E, A), np.float32)
+    bl = np.zeros((T, E), np.float32); br = np.zeros((T, E), np.float32)
+    bd = np.zeros((T, E), np.float32); bv = np.zeros((T, E), np.float32)
+    for t in range(T):
+        bo[t] = nobs; bd[t] = ndone
+        a, lp, _, v = O.get_action_and_value(L, p, nobs, 0, seed=cfg.seed, rank=0, env_base=0, step_id=t)
+        ba[t] = a; bl[t] = lp; bv[t] = v
+        nobs, r, te, trn, _, _ = oenv.step(a)
+        br[t] = r
+        ndone = np.maximum(te, trn)
+    _, _, _, nv = O.get_action_and_value(L, p, nobs, 2)
+    adv, ret = O.gae(br, bv, bd, nv, ndone, 0.99, 0.95)
+    np.testing.assert_allclose(gpu_obs, bo, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(gpu_adv, adv, rtol=1e-3, atol=1e-3)
+    lcfg = O.LossCfg(clip, 0.01, 0.5, 1, 1)
+    lr = float(np.float32(1.0) * np.float32(cfg.learning_rate))
+    op, _, _, _, _ = O.update(L, p, np.zeros(L.P), np.zeros(L.P), 0, bo.reshape(-1, O_), ba.reshape(-1, A),
+                              bl.reshape(-1), adv.reshape(-1), ret.reshape(-1), bv.reshape(-1), EP, MB, lr, 0.5, 1e-5,
+                              lcfg, seed=cfg.seed, rank=0, epoch_counter0=0)
+    np.testing.assert_allclose(gpu_p, op, rtol=0, atol=2e-5)
+
+
+# ------------------------------------------------------------------------------------------------
+# metric configuration (AC-PPO HalfCheetah, E=4096, T=128, MB=4, EP=4): size-independent checks
+# ------------------------------------------------------------------------------------------------
+def test_metric_config_iteration_properties_and_determinism():
+    cfg = ppo_amd.ACPPOConfig(num_envs=4096, env_id="HalfCheetah-v5", total_timesteps=4096 * 128 * 10)
+    res = []
+    for rep in range(2):
+        tr = ppo_amd.Trainer(cfg)
+        st = tr.iterate(want_stats=True)
+        res.append((tr.agent.params(), st))
+        tr.close()
+    (p0, s0), (p1, s1) = res
+    assert np.isfinite(p0).all()
+    np.testing.assert_array_equal(p0, p1)          # bitwise deterministic (no atomics anywhere)
+    assert s0 == s1
+    assert s0["minibatches"] == 16
+    for k in ("pg_loss", "v_loss", "entropy", "approx_kl", "clipfrac", "grad_norm"):
+        assert np.isfinite(s0[k]), k
+    assert 0.0 <= s0["clipfrac"] <= 1.0
+    assert s0["grad_norm"] > 0

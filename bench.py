@@ -39,8 +39,7 @@ def algorithmic_work(O, A, H, E, T, MB, nh):
     bwd_row = (2 * H + 2 * H * H + 2 * H) + (2 * nh * H + 2 * H * H + 2 * nh * H)  # dh, dW3, dh1 (dW1/dW2: k_dw)
     return {
         "fwdbwd": ("flop", M * (fwd_row + bwd_row)),
-        "dw_l2": ("flop", 2 * (2 * H * H * M)),
-        "dw_l1": ("flop", 2 * (2 * H * O * M)),
+        "dw": ("flop", 2 * (2 * H * H * M + 2 * H * O * M)),
         "act": ("flop", E * fwd_row),
         "gae": ("byte", E * T * 4 * 5),  # reads r, v, d; writes adv, ret
     }

@@ -53,6 +53,67 @@ PPO_DEV void mm_layer(f4 (&out)[NT_OUT], const f4 (&in)[NT_IN], const float* __r
   }
 }
 
+// Workgroup barrier that orders LDS traffic only: waits for this wave's LDS ops (lgkmcnt) and
+// leaves global loads/stores in flight (a plain __syncthreads() may also drain vmcnt).
+PPO_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Block-cooperative layer for 256-thread (4-wave) workgroups whose waves all need the same W:
+// W is streamed k-tile by k-tile (16 input columns x NT_OUT*16 rows) through a double-buffered
+// LDS slab, register-staged one tile ahead (load t+2 after the barrier, write it after computing t),
+// so every weight byte leaves L2 once per workgroup instead of once per wave.
+// wlds: 2 * NT_OUT * 256 floats. Every thread of the block must call it (uniform control flow).
+template <int NT_OUT, int NT_IN, int LDW, bool BIAS>
+PPO_DEV void mm_layer_lds(f4 (&out)[NT_OUT], const f4 (&in)[NT_IN], const float* __restrict__ W,
+                          const float* __restrict__ bias, float* wlds, int lane, int tid) {
+  constexpr int ROWS = NT_OUT * 16;
+  constexpr int SLAB = ROWS * 16;
+  constexpr int F4PT = (SLAB / 4 + 255) / 256;
+  const PBuf wb = make_pbuf(W, ROWS * LDW);
+  const int i = lane & 15, g = lane >> 4;
+  f4 st[F4PT];
+  auto load = [&](int t) {
+#pragma unroll
+    for (int u = 0; u < F4PT; ++u) {
+      const int c = tid + 256 * u;
+      st[u] = (c < SLAB / 4) ? pld4(wb, (c >> 2) * LDW + 4 * (c & 3), 16 * t) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < F4PT; ++u) {
+      const int c = tid + 256 * u;
+      if (c < SLAB / 4) *reinterpret_cast<f4*>(wlds + buf * SLAB + 4 * c) = st[u];
+    }
+  };
+  if constexpr (BIAS) {
+    const PBuf bb = make_pbuf(bias, ROWS);
+#pragma unroll
+    for (int ot = 0; ot < NT_OUT; ++ot) out[ot] = pld4(bb, 4 * g, 16 * ot);
+  } else {
+#pragma unroll
+    for (int ot = 0; ot < NT_OUT; ++ot) out[ot] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  load(0);
+  store(0);
+  lds_barrier();
+  if constexpr (NT_IN > 1) load(1);
+#pragma unroll
+  for (int t = 0; t < NT_IN; ++t) {
+    const float* sb = wlds + (t & 1) * SLAB + i * 16 + 4 * g;
+#pragma unroll
+    for (int ot = 0; ot < NT_OUT; ++ot) {
+      const f4 w = *reinterpret_cast<const f4*>(sb + ot * 256);
+      out[ot] = mfma16(w.x, in[t].x, out[ot]);
+      out[ot] = mfma16(w.y, in[t].y, out[ot]);
+      out[ot] = mfma16(w.z, in[t].z, out[ot]);
+      out[ot] = mfma16(w.w, in[t].w, out[ot]);
+    }
+    if (t + 1 < NT_IN) store((t + 1) & 1);
+    lds_barrier();
+    if (t + 2 < NT_IN) load(t + 2);
+  }
+}
+
 // normalized agent input (AC: (x - mean_) / std_, ac:189 / :215), zero padded to NTO*16 features
 template <int NTO, int KIND>
 PPO_DEV void load_input(f4 (&xin)[NTO], const float* __restrict__ xrow, int O, const float* __restrict__ omean,

@@ -49,7 +49,7 @@ enum {
   PK_ACT = 0, PK_FWDBWD, PK_DW2, PK_DW1, PK_COLSUM, PK_GRADNORM, PK_ADAM, PK_GAE, PK_PERM, PK_ADV, PK_ALLREDUCE,
   PK_SYNTH, PK_COUNT
 };
-static const char* kProfNames[PK_COUNT] = {"act", "fwdbwd", "dw_l2", "dw_l1", "colsum", "gradnorm",
+static const char* kProfNames[PK_COUNT] = {"act", "fwdbwd", "dw", "dw_l1", "colsum", "gradnorm",
                                            "adam", "gae", "perm", "adv_stats", "allreduce", "synth_env"};
 
 struct ProfEvent {
@@ -75,6 +75,7 @@ struct ppo_ctx {
   float* slab[2] = {};
   int tiles_per_block = 1, nblk = 1;
   size_t lds_bytes = 0;
+  int wlds_off = 0;
   float* dwslab[4] = {};
   int nchunks = 1, rows_per_chunk = 64;
   float* normout = nullptr;
@@ -216,13 +217,13 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   c->tiles_per_block = std::max(1, (tiles + 255) / 256);
   c->nblk = (tiles + c->tiles_per_block - 1) / c->tiles_per_block;
   for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->slab[k], (size_t)c->nblk * c->sg[k].size);
-  c->lds_bytes = (size_t)4 * std::max(c->sg[0].size, c->sg[1].size) * sizeof(float);
-  c->rows_per_chunk = std::max(64, (int)(((c->M + 63) / 64 + 1) & ~1));
+  c->wlds_off = 4 * std::max(c->sg[0].size, c->sg[1].size);
+  c->wlds_off = (c->wlds_off + 63) & ~63;
+  c->lds_bytes = ((size_t)c->wlds_off + 2 * (size_t)H * 16) * sizeof(float);
+  // dW split-K: ~128 row chunks per trunk (256 workgroups for the two trunks), 16-row multiples
+  c->rows_per_chunk = std::max(64, (((c->M + 127) / 128) + 15) & ~15);
   c->nchunks = (c->M + c->rows_per_chunk - 1) / c->rows_per_chunk;
-  for (int k = 0; k < 2; ++k) {
-    rc |= dmalloc(&c->dwslab[k], (size_t)c->nchunks * H * H);
-    rc |= dmalloc(&c->dwslab[2 + k], (size_t)c->nchunks * H * OP);
-  }
+  for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->dwslab[k], (size_t)c->nchunks * (H * H + H * OP));
   rc |= dmalloc(&c->normout, 4);
   rc |= dmalloc(&c->mbstats, (size_t)8 * EP * c->nmb);
   if (rc) {
@@ -516,6 +517,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   u.sg[1] = c->sg[1];
   u.M = M;
   u.tiles_per_block = c->tiles_per_block;
+  u.wlds_off = c->wlds_off;
   u.obs = c->buf[PPO_BUF_OBS];
   u.actions = c->buf[PPO_BUF_ACTIONS];
   u.logp = c->buf[PPO_BUF_LOGPROBS];
@@ -535,14 +537,17 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
     u.DZ2[k] = c->DZ2[k];
     u.slab[k] = c->slab[k];
   }
-  DwArgs d2, d1;
-  memset(&d2, 0, sizeof(d2));
-  memset(&d1, 0, sizeof(d1));
-  d2.M = d1.M = M;
-  d2.rows_per_chunk = d1.rows_per_chunk = c->rows_per_chunk;
+  DwArgs dw;
+  memset(&dw, 0, sizeof(dw));
+  dw.M = M;
+  dw.rows_per_chunk = c->rows_per_chunk;
+  dw.xn = c->Xn;
+  dw.slab_stride = (long)H * H + (long)H * OP;
   for (int k = 0; k < 2; ++k) {
-    d2.job[k] = DwJob{c->DZ2[k], c->H1[k], H, H, c->dwslab[k], (long)H * H, H, H, H};
-    d1.job[k] = DwJob{c->DZ1[k], c->Xn, H, OP, c->dwslab[2 + k], (long)H * OP, OP, H, OP};
+    dw.dz2[k] = c->DZ2[k];
+    dw.h1[k] = c->H1[k];
+    dw.dz1[k] = c->DZ1[k];
+    dw.slab[k] = c->dwslab[k];
   }
   // slab -> packed gradient segments
   ColsumArgs cs;
@@ -556,8 +561,8 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   const bool ln = cfg.net_kind == PPO_NET_LN_BETA;
   for (int k = 0; k < 2; ++k) {
     const TrunkDev& T = c->K.tr[k];
-    seg(c->dwslab[k], (long)H * H, c->nchunks, H * H, c->G + T.W2, 1.f);
-    seg(c->dwslab[2 + k], (long)H * OP, c->nchunks, H * OP, c->G + T.W1, 1.f);
+    seg(c->dwslab[k], dw.slab_stride, c->nchunks, H * H, c->G + T.W2, 1.f);
+    seg(c->dwslab[k] + (long)H * H, dw.slab_stride, c->nchunks, H * OP, c->G + T.W1, 1.f);
     const SmallGradLayout& g = c->sg[k];
     const float* sl = c->slab[k];
     seg(sl + g.b1, g.size, c->nblk, H, c->G + T.b1, 1.f);
@@ -626,11 +631,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
       }
       {
         ProfScope ps(c, PK_DW2, s);
-        if (launch_dw(d2, 1, H, OP, c->nchunks, 2, s) != 0) return fail("no dW kernel (layer 2)");
-      }
-      {
-        ProfScope ps(c, PK_DW1, s);
-        if (launch_dw(d1, 0, H, OP, c->nchunks, 2, s) != 0) return fail("no dW kernel (layer 1)");
+        if (launch_dw(dw, H, OP, c->nchunks, s) != 0) return fail("no dW kernel for this configuration");
       }
       float* st = c->mbstats + 8 * gi;
       cs.seg[stats_seg0 + 0] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_PG, st + ST_PG, c->sg[1].size, c->nblk, 1, 1.f / M};
@@ -742,15 +743,36 @@ extern "C" int ppo_comm_allreduce(ppo_t* c, float* buf, long n, int average) {
 // ------------------------------------------------------------------------------------------
 extern "C" int ppo_set_device(int d) { HIP_TRY(hipSetDevice(d)); return 0; }
 extern "C" int ppo_device_count(int* n) { HIP_TRY(hipGetDeviceCount(n)); return 0; }
+// The helpers are host-synchronous and device-wide ordered: contexts run on non-blocking streams,
+// which are NOT ordered against the legacy null stream that plain hipMemcpy/hipMemset use.
 extern "C" int ppo_dev_malloc(void** p, size_t bytes) {
   HIP_TRY(hipMalloc(p, bytes ? bytes : 1));
   HIP_TRY(hipMemset(*p, 0, bytes ? bytes : 1));
+  HIP_TRY(hipDeviceSynchronize());
   return 0;
 }
-extern "C" int ppo_dev_free(void* p) { HIP_TRY(hipFree(p)); return 0; }
-extern "C" int ppo_memcpy_h2d(void* d, const void* h, size_t n) { HIP_TRY(hipMemcpy(d, h, n, hipMemcpyHostToDevice)); return 0; }
-extern "C" int ppo_memcpy_d2h(void* h, const void* d, size_t n) { HIP_TRY(hipMemcpy(h, d, n, hipMemcpyDeviceToHost)); return 0; }
-extern "C" int ppo_memset_dev(void* d, int v, size_t n) { HIP_TRY(hipMemset(d, v, n)); return 0; }
+extern "C" int ppo_dev_free(void* p) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipFree(p));
+  return 0;
+}
+extern "C" int ppo_memcpy_h2d(void* d, const void* h, size_t n) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(d, h, n, hipMemcpyHostToDevice));
+  HIP_TRY(hipDeviceSynchronize());
+  return 0;
+}
+extern "C" int ppo_memcpy_d2h(void* h, const void* d, size_t n) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(h, d, n, hipMemcpyDeviceToHost));
+  return 0;
+}
+extern "C" int ppo_memset_dev(void* d, int v, size_t n) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemset(d, v, n));
+  HIP_TRY(hipDeviceSynchronize());
+  return 0;
+}
 extern "C" int ppo_device_sync(void) { HIP_TRY(hipDeviceSynchronize()); return 0; }
 
 // ------------------------------------------------------------------------------------------
@@ -811,6 +833,7 @@ extern "C" int psyn_create(int E, int O, int A, psyn_t** out) {
     psyn_destroy(env);
     return -2;
   }
+  HIP_TRY(hipDeviceSynchronize());
   *out = env;
   return 0;
 }
@@ -877,6 +900,7 @@ extern "C" int psyn_episode_stats(psyn_t* env, float* sr, float* sl, float* sc) 
   HIP_TRY(hipMemset(env->a.fin_ret, 0, sizeof(float) * E));
   HIP_TRY(hipMemset(env->a.fin_len, 0, sizeof(float) * E));
   HIP_TRY(hipMemset(env->a.fin_cnt, 0, sizeof(float) * E));
+  HIP_TRY(hipDeviceSynchronize());
   if (sr) *sr = (float)R;
   if (sl) *sl = (float)Lsum;
   if (sc) *sc = (float)N;

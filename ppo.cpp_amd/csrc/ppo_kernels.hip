@@ -16,6 +16,7 @@
 #include "ppo_agent.hpp"
 #include "ppo_kernels.hpp"
 
+#include <algorithm>
 #include <type_traits>
 
 // =============================================================================================
@@ -196,6 +197,7 @@ __global__ __launch_bounds__(256) void k_fwdbwd(UpdArgs a) {
   const PBuf pbuf = make_pbuf(P, K.size);
   const SmallGradLayout sg = a.sg[trunk];
   float* acc = lds + wave * sg.size;
+  float* wlds = lds + a.wlds_off;  // 2 x H*16 floats: weight k-tile double buffer
   for (int i = lane; i < sg.size; i += 64) acc[i] = 0.0f;
 
   const int O = K.O, A = K.A, OP = K.OP;
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(256) void k_fwdbwd(UpdArgs a) {
     f4 hA[NT];   // layer-1 output; later dh1 accumulator
     f4 hC[NT];   // layer-2: x_hat2 (LN) or h2 (tanh); later dz2
     float mu1 = 0.f, rs1 = 0.f, mu2 = 0.f, rs2 = 0.f;
-    mm_layer<NT, NTO, NTO * 16, true>(hA, xin, P + T.W1, P + T.b1, lane);
+    mm_layer_lds<NT, NTO, NTO * 16, true>(hA, xin, P + T.W1, P + T.b1, wlds, lane, threadIdx.x);
     if constexpr (KIND == PPO_NET_LN_BETA) {
       ln_stats<NT>(hA, mu1, rs1);
       ln_normalize<NT>(hA, mu1, rs1);
@@ -224,7 +226,7 @@ __global__ __launch_bounds__(256) void k_fwdbwd(UpdArgs a) {
       tanh_inplace<NT>(hA);
     }
     store_rows<NT>(a.H1[trunk] + (size_t)m * H, H, hA, valid, g);
-    mm_layer<NT, NT, H, true>(hC, hA, P + T.W2, P + T.b2, lane);
+    mm_layer_lds<NT, NT, H, true>(hC, hA, P + T.W2, P + T.b2, wlds, lane, threadIdx.x);
     if constexpr (KIND == PPO_NET_LN_BETA) {
       ln_stats<NT>(hC, mu2, rs2);
       ln_normalize<NT>(hC, mu2, rs2);  // hC = x_hat2
@@ -443,9 +445,9 @@ __global__ __launch_bounds__(256) void k_fwdbwd(UpdArgs a) {
       store_rows<NT>(a.DZ2[trunk] + (size_t)m * H, H, hC, valid, g);
     }
     // ---------------- dh1 = W2^T dz2 ----------------
-    mm_layer<NT, NT, H, false>(dh, hC, a.W2T[trunk], nullptr, lane);
+    mm_layer_lds<NT, NT, H, false>(dh, hC, a.W2T[trunk], nullptr, wlds, lane, threadIdx.x);
     // ---------------- recompute layer 1, layer-1 backward ----------------
-    mm_layer<NT, NTO, NTO * 16, true>(hA, xin, P + T.W1, P + T.b1, lane);
+    mm_layer_lds<NT, NTO, NTO * 16, true>(hA, xin, P + T.W1, P + T.b1, wlds, lane, threadIdx.x);
     {
       if constexpr (KIND == PPO_NET_LN_BETA) {
         ln_normalize<NT>(hA, mu1, rs1);  // x_hat1 (bit-identical recompute)
@@ -489,56 +491,113 @@ __global__ __launch_bounds__(256) void k_fwdbwd(UpdArgs a) {
 }
 
 // =============================================================================================
-// k_dw — partial dW[o][i] = sum_{m in chunk} DZ[m][o] * IN[m][i]   (MFMA 32x32x2 f32)
-//   block = WAVES waves; wave w owns o-tiles [w*TOW, (w+1)*TOW) of the block's o range and all
-//   TI i-tiles. Operands straight from HBM/L2: A lane (o, h) = DZ[m0+2s+h][o], B = IN[m0+2s+h][i].
+// k_dw — split-K weight gradients of one trunk for one chunk of minibatch rows:
+//   phase 2: dW2[o][i] = sum_m DZ2[m][o] * H1[m][i]     (H x H)
+//   phase 1: dW1[o][i] = sum_m DZ1[m][o] * Xn[m][i]     (H x OP)
+// 4 waves; MFMA 32x32x2 f32; rows staged 16 at a time through a double-buffered LDS tile
+// (register-staged, one sub-chunk ahead); wave (wo, wi) owns o-tiles [wo*TOW, ..) x i-tiles
+// [wi*TIW, ..). Partial sums go to a per-chunk slab (deterministic reduction in k_colsum).
 // =============================================================================================
 typedef float f16v __attribute__((ext_vector_type(16)));
 
-template <int WAVES, int TOW, int TI>
-__global__ __launch_bounds__(WAVES * 64) void k_dw(DwArgs a) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int l32 = lane & 31, hsel = lane >> 5;
-  const int job = blockIdx.z;
-  const DwJob& J = a.job[job];
-  const int chunk = blockIdx.x;
-  const int obase = blockIdx.y * (WAVES * TOW * 32) + wave * TOW * 32;
-  const long m0 = (long)chunk * a.rows_per_chunk;
-  const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
-  f16v acc[TOW][TI];
+template <int NO, int NI, int LDI, int WO, int WI>
+PPO_DEV void dw_phase(const float* __restrict__ DZ, const float* __restrict__ IN, long m0, long m1,
+                      float* __restrict__ out, float* lds, int tid) {
+  constexpr int TO = NO / 32, TI = (NI + 31) / 32;
+  constexpr int TOW = TO / WO, TIW = (TI + WI - 1) / WI;
+  constexpr int KS = 16;                       // rows per stage
+  constexpr int ADZ = KS * NO, AIN = KS * LDI; // floats per stage
+  constexpr int STG = ADZ + AIN;
+  constexpr int NF4 = STG / 4;
+  constexpr int F4PT = (NF4 + 255) / 256;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wo = wave % WO, wi = wave / WO;
+  const int l32 = lane & 31, hs = lane >> 5;
+  f16v acc[TOW][TIW];
 #pragma unroll
   for (int u = 0; u < TOW; ++u)
 #pragma unroll
-    for (int v = 0; v < TI; ++v)
+    for (int v = 0; v < TIW; ++v)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[u][v][r] = 0.0f;
-  const float* __restrict__ DZ = J.dz;
-  const float* __restrict__ IN = J.in;
-#pragma unroll 4
-  for (long m = m0; m < m1; m += 2) {
-    const long mr = m + hsel;
-    const bool ok = mr < m1;
-    float av[TOW], bv[TI];
+  f4 st[F4PT];
+  auto load = [&](long mb) {
 #pragma unroll
-    for (int u = 0; u < TOW; ++u) av[u] = ok ? DZ[mr * J.ld_dz + obase + u * 32 + l32] : 0.0f;
+    for (int u = 0; u < F4PT; ++u) {
+      const int c = tid + 256 * u;
+      f4 v = f4{0.f, 0.f, 0.f, 0.f};
+      if (c < NF4) {
+        const int fl = 4 * c;
+        if (fl < ADZ) {
+          const long row = mb + fl / NO;
+          if (row < m1) v = ld4(DZ + row * NO + (fl % NO));
+        } else {
+          const int f2 = fl - ADZ;
+          const long row = mb + f2 / LDI;
+          if (row < m1) v = ld4(IN + row * LDI + (f2 % LDI));
+        }
+      }
+      st[u] = v;
+    }
+  };
+  auto store = [&](int buf) {
 #pragma unroll
-    for (int v = 0; v < TI; ++v) bv[v] = (ok && v * 32 + l32 < J.n_in_store) ? IN[mr * J.ld_in + v * 32 + l32] : 0.0f;
+    for (int u = 0; u < F4PT; ++u) {
+      const int c = tid + 256 * u;
+      if (c < NF4) *reinterpret_cast<f4*>(lds + buf * STG + 4 * c) = st[u];
+    }
+  };
+  const int nst = (int)((m1 - m0 + KS - 1) / KS);
+  load(m0);
+  store(0);
+  lds_barrier();
+  if (nst > 1) load(m0 + KS);
+  for (int sI = 0; sI < nst; ++sI) {
+    const float* sdz = lds + (sI & 1) * STG;
+    const float* sin = sdz + ADZ;
 #pragma unroll
-    for (int u = 0; u < TOW; ++u)
+    for (int k = 0; k < KS; k += 2) {
+      float av[TOW], bv[TIW];
 #pragma unroll
-      for (int v = 0; v < TI; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[v], acc[u][v], 0, 0, 0);
+      for (int u = 0; u < TOW; ++u) av[u] = sdz[(k + hs) * NO + (wo * TOW + u) * 32 + l32];
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) {
+        const int col = (wi * TIW + v) * 32 + l32;
+        bv[v] = (col < LDI) ? sin[(k + hs) * LDI + col] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < TOW; ++u)
+#pragma unroll
+        for (int v = 0; v < TIW; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[v], acc[u][v], 0, 0, 0);
+    }
+    if (sI + 1 < nst) store((sI + 1) & 1);
+    lds_barrier();
+    if (sI + 2 < nst) load(m0 + (long)(sI + 2) * KS);
   }
-  float* out = J.out + (size_t)chunk * J.slab_stride;
 #pragma unroll
   for (int u = 0; u < TOW; ++u)
 #pragma unroll
-    for (int v = 0; v < TI; ++v)
+    for (int v = 0; v < TIW; ++v)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int o = obase + u * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
-        const int i = v * 32 + l32;
-        if (o < J.n_out && i < J.n_in_store) out[(size_t)o * J.ld_out + i] = acc[u][v][r];
+        const int o = (wo * TOW + u) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hs;
+        const int i = (wi * TIW + v) * 32 + l32;
+        if (i < LDI) out[(size_t)o * LDI + i] = acc[u][v][r];
       }
+}
+
+template <int H, int OP, int WO2, int WI2, int WO1, int WI1>
+__global__ __launch_bounds__(256) void k_dw(DwArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int trunk = blockIdx.y;
+  const long m0 = (long)blockIdx.x * a.rows_per_chunk;
+  const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
+  float* out = a.slab[trunk] + (size_t)blockIdx.x * a.slab_stride;
+  if (m0 < m1) {
+    dw_phase<H, H, H, WO2, WI2>(a.dz2[trunk], a.h1[trunk], m0, m1, out, lds, threadIdx.x);
+    lds_barrier();
+    dw_phase<H, OP, OP, WO1, WI1>(a.dz1[trunk], a.xn, m0, m1, out + H * H, lds, threadIdx.x);
+  }
 }
 
 // =============================================================================================
@@ -627,23 +686,24 @@ __global__ void k_transpose(const float* __restrict__ src, float* __restrict__ d
 // k_gae — one thread per env, t = T-1 .. 0; op-for-op fp32 (no contraction), ppo:447-467
 // =============================================================================================
 __global__ __launch_bounds__(256) void k_gae(GaeArgs a) {
+#pragma clang fp contract(off)
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= a.E) return;
   const long E = a.E;
-  const float gl = __fmul_rn(a.gamma, a.lam);
+  const float gl = (a.gamma * a.lam);
   float last = 0.0f;
-  float nnt = __fsub_rn(1.0f, a.next_done[e]);
+  float nnt = (1.0f - a.next_done[e]);
   float nv = a.next_value[e];
   for (int t = a.T - 1; t >= 0; --t) {
     const long idx = (long)t * E + e;
     const float r = a.rewards[idx], v = a.values[idx];
-    const float gnv = __fmul_rn(a.gamma, nv);
-    const float delta = __fsub_rn(__fadd_rn(r, __fmul_rn(gnv, nnt)), v);
-    const float adv = __fadd_rn(delta, __fmul_rn(__fmul_rn(gl, nnt), last));
+    const float gnv = (a.gamma * nv);
+    const float delta = ((r + (gnv * nnt)) - v);
+    const float adv = (delta + ((gl * nnt) * last));
     a.adv[idx] = adv;
-    a.ret[idx] = __fadd_rn(adv, v);
+    a.ret[idx] = (adv + v);
     last = adv;
-    nnt = __fsub_rn(1.0f, a.dones[idx]);
+    nnt = (1.0f - a.dones[idx]);
     nv = v;
   }
 }
@@ -705,12 +765,13 @@ __global__ void k_adv_finalize(AdvArgs a) {
 // host SyntheticCheetah and the oracle)
 // =============================================================================================
 PPO_DEV void synth_reset_one(SynthArgs& a, int e, int seed, float* obs) {
+#pragma clang fp contract(off)
   if (seed > 0) { a.rseed[e] = (uint32_t)seed; a.rcount[e] = 0; }
   const uint32_t rs = a.rseed[e], rc = a.rcount[e];
   for (int i = 0; i < a.O; ++i) {
     uint32_t r[4];
     philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, r);
-    const float q = __fmul_rn(0.1f, __fsub_rn(__fmul_rn(2.0f, u01(r[0])), 1.0f));
+    const float q = (0.1f * ((2.0f * u01(r[0])) - 1.0f));
     a.q[(long)e * a.O + i] = q;
     obs[(long)e * a.O + i] = q;
   }
@@ -730,6 +791,7 @@ __global__ __launch_bounds__(256) void k_synth_reset(SynthArgs a, int seed, floa
 
 __global__ __launch_bounds__(256) void k_synth_step(SynthArgs a, int e0, int e1, const float* __restrict__ act,
                                                     float lo, float hi, float* obs, float* reward, float* done) {
+#pragma clang fp contract(off)
   const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= e1) return;
   const int O = a.O, A = a.A;
@@ -749,25 +811,25 @@ __global__ __launch_bounds__(256) void k_synth_step(SynthArgs a, int e0, int e1,
   for (int i = 0; i < O; ++i) {
     const float ai = fminf(fmaxf(ar[i % A], lo), hi);
     const float qn = (i + 1 < O) ? q[i + 1] : q0;
-    const float nq = __fmaf_rn(0.9f, q[i], __fmaf_rn(0.1f, ai, __fmul_rn(0.05f, qn)));
+    const float nq = __fmaf_rn(0.9f, q[i], __fmaf_rn(0.1f, ai, (0.05f * qn)));
     if (i > 0) q[i - 1] = nq_prev;
     nq_prev = nq;
   }
   q[O - 1] = nq_prev;
-  const float vel = __fdiv_rn(__fsub_rn(q[0], xb), 0.05f);
+  const float vel = ((q[0] - xb) / 0.05f);
   float ctrl = 0.0f;
   for (int k = 0; k < A; ++k) {
     const float ak = fminf(fmaxf(ar[k], lo), hi);
-    ctrl = __fadd_rn(ctrl, __fmul_rn(__fmul_rn(0.1f, ak), ak));
+    ctrl = (ctrl + ((0.1f * ak) * ak));
   }
-  const float r = __fsub_rn(vel, ctrl);
+  const float r = (vel - ctrl);
   const int t = a.t[e] + 1;
   a.t[e] = t;
   const bool tr = t >= 1000;
   for (int i = 0; i < O; ++i) obs[(long)e * O + i] = q[i];
   reward[e] = r;
   done[e] = tr ? 1.0f : 0.0f;
-  a.ep_ret[e] = __fadd_rn(a.ep_ret[e], r);
+  a.ep_ret[e] = (a.ep_ret[e] + r);
   a.ep_len[e] += 1;
   if (tr) {
     a.fin_ret[e] += a.ep_ret[e];
@@ -822,30 +884,38 @@ int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes) {
   });
 }
 
-// dW jobs: layer-2 (H x H) and layer-1 (H x OP) of each trunk
-int launch_dw(const DwArgs& a, int kind_l2, int H, int OP, int nchunks, int njobs, hipStream_t s) {
-  if (kind_l2) {
-    if (H == 256) {  // 2 blocks of 128 o-rows, 4 waves x 1 o-tile x 8 i-tiles
-      hipLaunchKernelGGL((k_dw<4, 1, 8>), dim3(nchunks, 2, njobs), dim3(256), 0, s, a);
-      return 0;
-    }
-    if (H == 64) {
-      hipLaunchKernelGGL((k_dw<2, 1, 2>), dim3(nchunks, 1, njobs), dim3(128), 0, s, a);
-      return 0;
-    }
-    return -1;
+// dW of both Linear weight matrices of both trunks, grid = (chunks, 2 trunks)
+template <int H, int OP>
+static int launch_dw_t(const DwArgs& a, int nchunks, size_t lds, hipStream_t s) {
+  constexpr int TO = H / 32, TI1 = (OP + 31) / 32;
+  constexpr int WO2 = TO >= 4 ? 4 : TO, WI2 = 4 / WO2;
+  constexpr int WO1 = TO >= 4 ? 4 : TO, WI1 = 4 / WO1;
+  (void)TI1;
+  auto k = k_dw<H, OP, WO2, WI2, WO1, WI1>;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
+    attr = true;
   }
-  const int TI = OP / 32 + (OP % 32 ? 1 : 0);
-  if (H == 256) {
-    if (TI == 1) { hipLaunchKernelGGL((k_dw<4, 2, 1>), dim3(nchunks, 1, njobs), dim3(256), 0, s, a); return 0; }
-    if (TI == 4) { hipLaunchKernelGGL((k_dw<4, 2, 4>), dim3(nchunks, 1, njobs), dim3(256), 0, s, a); return 0; }
-    if (TI == 12) { hipLaunchKernelGGL((k_dw<4, 2, 12>), dim3(nchunks, 1, njobs), dim3(256), 0, s, a); return 0; }
-  }
-  if (H == 64) {
-    if (TI == 1) { hipLaunchKernelGGL((k_dw<2, 1, 1>), dim3(nchunks, 1, njobs), dim3(128), 0, s, a); return 0; }
-    if (TI == 4) { hipLaunchKernelGGL((k_dw<2, 1, 4>), dim3(nchunks, 1, njobs), dim3(128), 0, s, a); return 0; }
-    if (TI == 12) { hipLaunchKernelGGL((k_dw<2, 1, 12>), dim3(nchunks, 1, njobs), dim3(128), 0, s, a); return 0; }
-  }
+  hipLaunchKernelGGL(k, dim3(nchunks, 2), dim3(256), lds, s, a);
+  return 0;
+}
+
+size_t dw_lds_bytes(int H, int OP) {
+  const int KS = 16;
+  return (size_t)2 * (KS * H + KS * std::max(H, OP)) * sizeof(float);
+}
+
+int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s) {
+  const size_t lds = dw_lds_bytes(H, OP);
+  if (H == 256 && OP == 16) return launch_dw_t<256, 16>(a, nchunks, lds, s);
+  if (H == 256 && OP == 32) return launch_dw_t<256, 32>(a, nchunks, lds, s);
+  if (H == 256 && OP == 112) return launch_dw_t<256, 112>(a, nchunks, lds, s);
+  if (H == 256 && OP == 384) return launch_dw_t<256, 384>(a, nchunks, lds, s);
+  if (H == 64 && OP == 16) return launch_dw_t<64, 16>(a, nchunks, lds, s);
+  if (H == 64 && OP == 32) return launch_dw_t<64, 32>(a, nchunks, lds, s);
+  if (H == 64 && OP == 112) return launch_dw_t<64, 112>(a, nchunks, lds, s);
+  if (H == 64 && OP == 384) return launch_dw_t<64, 384>(a, nchunks, lds, s);
   return -1;
 }
 

@@ -39,6 +39,7 @@ struct UpdArgs {
   SmallGradLayout sg[2];
   int M;
   int tiles_per_block;
+  int wlds_off;  // float offset of the weight staging buffers in dynamic LDS
   const int32_t* perm;
   const float *obs, *actions, *logp, *adv, *ret, *val;
   const float* adv_stats;  // [2] mean, std of this minibatch
@@ -51,16 +52,13 @@ struct UpdArgs {
   float* slab[2];
 };
 
-struct DwJob {
-  const float* dz;
-  const float* in;
-  int ld_dz, ld_in;
-  float* out;
-  long slab_stride;
-  int ld_out, n_out, n_in_store;
-};
 struct DwArgs {
-  DwJob job[4];
+  const float* dz2[2];
+  const float* h1[2];
+  const float* dz1[2];
+  const float* xn;
+  float* slab[2];     // [nchunks][H*H + H*OP] per trunk
+  long slab_stride;
   int M;
   int rows_per_chunk;
 };
@@ -131,7 +129,8 @@ struct SynthArgs {
 int launch_act(const ActArgs& a, hipStream_t s);
 int launch_fwdbwd(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s);
 int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes);
-int launch_dw(const DwArgs& a, int kind_l2, int H, int OP, int nchunks, int njobs, hipStream_t s);
+int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s);
+size_t dw_lds_bytes(int H, int OP);
 void launch_colsum(const ColsumArgs& a, int nseg, long maxlen, hipStream_t s);
 void launch_gradnorm(const NormArgs& a, hipStream_t s);
 void launch_adam(const AdamArgs& a, hipStream_t s);

@@ -224,7 +224,7 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   c->rows_per_chunk = std::max(64, (((c->M + 127) / 128) + 15) & ~15);
   c->nchunks = (c->M + c->rows_per_chunk - 1) / c->rows_per_chunk;
   for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->dwslab[k], (size_t)c->nchunks * (H * H + H * OP));
-  rc |= dmalloc(&c->normout, 4);
+  rc |= dmalloc(&c->normout, 2 + PPO_LAYOUT_MAX_TENSORS + 2);
   rc |= dmalloc(&c->mbstats, (size_t)8 * EP * c->nmb);
   if (rc) {
     ppo_destroy(c);
@@ -612,6 +612,8 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   ad.begin = tb;
   ad.n = c->K.size - tb;
   ad.norm_out = c->normout;
+  ad.nt = na.nt;
+  ad.max_norm = cfg.max_grad_norm;
   ad.eps = cfg.adam_eps;
   ad.H = H;
   for (int k = 0; k < 2; ++k) {
@@ -878,10 +880,10 @@ extern "C" int ppo_rollout_synth(ppo_t* c, psyn_t* env, float* next_obs, float* 
     if (rc) return rc;
     {
       ProfScope ps(c, PK_SYNTH, c->stream);
-      launch_synth_step(env->a, 0, E, act_scratch, lo, hi, next_obs, rew_scratch, next_done, c->stream);
+      // the env's reward output IS rewards[t] of the rollout storage (ppo:406) — no extra copy
+      launch_synth_step(env->a, 0, E, act_scratch, lo, hi, next_obs, c->buf[PPO_BUF_REWARDS] + (size_t)t * E,
+                        next_done, c->stream);
     }
-    rc = ppo_rollout_reward(c, t, 0, E, rew_scratch, nullptr);
-    if (rc) return rc;
   }
   HIP_TRY(hipGetLastError());
   return 0;

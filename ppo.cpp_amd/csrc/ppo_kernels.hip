@@ -128,6 +128,251 @@ __global__ __launch_bounds__(64) void k_act(ActArgs a) {
 }
 
 // =============================================================================================
+// k_act2 — the same agent forward as k_act, block-cooperative: a 256-thread workgroup owns
+// ROWS = 16*RG env rows of one trunk and its 4 waves SPLIT THE OUTPUT FEATURES (wave w computes
+// feature tiles [w*NT/4, (w+1)*NT/4) of every layer), so a rollout step of 4096 envs runs on
+// 2 x 4096/ROWS workgroups with 4x less serial MFMA work per wave than k_act. Activations are
+// exchanged through LDS (one [ROWS][H] buffer); LayerNorm row moments are reduced over the four
+// waves through LDS; head outputs are reduced per row; the per-(row, action-dim) distribution math
+// runs one item per thread. Every weight byte is read once per workgroup.
+// =============================================================================================
+template <int H, int KIND, int NTO, int RG>
+__global__ __launch_bounds__(256) void k_act2(ActArgs a) {
+  constexpr int NT = H / 16, NTW = NT / 4;
+  constexpr int ROWS = 16 * RG;
+  constexpr int MAXNH = 40;
+  __shared__ __attribute__((aligned(16))) float hbuf[ROWS * H];
+  __shared__ float red[4][ROWS];
+  __shared__ float headp[4][ROWS][MAXNH + 1];
+  __shared__ float itm[ROWS][MAXNH / 2 + 1][2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int trunk = blockIdx.y;
+  const PackedLayout& K = a.K;
+  const TrunkDev& T = K.tr[trunk];
+  const float* __restrict__ P = a.P;
+  const PBuf pbuf = make_pbuf(P, K.size);
+  const int row0 = blockIdx.x * ROWS;
+  const int O = K.O, A = K.A;
+  const int nh = trunk == 0 ? 1 : (KIND == PPO_NET_LN_BETA ? 2 * A : A);
+  if (trunk == 1 && !a.need_actor) return;
+
+  // ---- inputs (every wave loads its rows' inputs; batch-on-lanes layout) ----
+  f4 xin[RG][NTO];
+#pragma unroll
+  for (int rg = 0; rg < RG; ++rg) {
+    const int row = row0 + 16 * rg + j;
+    load_input<NTO, KIND>(xin[rg], row < a.n ? a.x + (size_t)row * a.ldx : nullptr, O,
+                          P + (K.omean >= 0 ? K.omean : 0), P + (K.ostd >= 0 ? K.ostd : 0), g);
+  }
+  // own output tiles: [wave*NTW, (wave+1)*NTW)
+  auto layer = [&](f4 (&acc)[RG][NTW], auto&& bfrag, int NTIN, const float* W, int ldw, int boff) {
+    const PBuf wb = make_pbuf(W, H * ldw);
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+      for (int u = 0; u < NTW; ++u) acc[rg][u] = pld4(pbuf, 4 * g, boff + 16 * (wave * NTW + u));
+    for (int t = 0; t < NTIN; ++t) {
+      f4 w[NTW];
+#pragma unroll
+      for (int u = 0; u < NTW; ++u) w[u] = pld4(wb, (16 * (wave * NTW + u) + j) * ldw + 4 * g, 16 * t);
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) {
+        const f4 b = bfrag(rg, t);
+#pragma unroll
+        for (int u = 0; u < NTW; ++u) {
+          acc[rg][u] = mfma16(w[u].x, b.x, acc[rg][u]);
+          acc[rg][u] = mfma16(w[u].y, b.y, acc[rg][u]);
+          acc[rg][u] = mfma16(w[u].z, b.z, acc[rg][u]);
+          acc[rg][u] = mfma16(w[u].w, b.w, acc[rg][u]);
+        }
+      }
+    }
+  };
+  // LayerNorm (+ReLU) or tanh over the full H features of each row, own tiles in registers
+  auto activate = [&](f4 (&acc)[RG][NTW], int gam, int bet) {
+    if constexpr (KIND == PPO_NET_LN_BETA) {
+      float mu[RG], rs[RG];
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) {
+        float sm = 0.f;
+#pragma unroll
+        for (int u = 0; u < NTW; ++u) sm += (acc[rg][u].x + acc[rg][u].y) + (acc[rg][u].z + acc[rg][u].w);
+        sm = row_allreduce(sm);
+        if (g == 0) red[wave][16 * rg + j] = sm;
+      }
+      lds_barrier();
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) {
+        const int r = 16 * rg + j;
+        mu[rg] = (((red[0][r] + red[1][r]) + red[2][r]) + red[3][r]) * (1.0f / H);
+      }
+      lds_barrier();
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) {
+        float q = 0.f;
+#pragma unroll
+        for (int u = 0; u < NTW; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = acc[rg][u][r] - mu[rg];
+            q += d * d;
+          }
+        q = row_allreduce(q);
+        if (g == 0) red[wave][16 * rg + j] = q;
+      }
+      lds_barrier();
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) {
+        const int r = 16 * rg + j;
+        const float q = (((red[0][r] + red[1][r]) + red[2][r]) + red[3][r]) * (1.0f / H);
+        rs[rg] = 1.0f / sqrtf(q + 1e-5f);
+      }
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+        for (int u = 0; u < NTW; ++u) {
+          const int ft = wave * NTW + u;
+          const f4 gm = pld4(pbuf, 4 * g, gam + 16 * ft), bt = pld4(pbuf, 4 * g, bet + 16 * ft);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float y = __fmaf_rn(gm[r], (acc[rg][u][r] - mu[rg]) * rs[rg], bt[r]);
+            acc[rg][u][r] = y > 0.0f ? y : 0.0f;
+          }
+        }
+    } else {
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+        for (int u = 0; u < NTW; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[rg][u][r] = tanhf(acc[rg][u][r]);
+    }
+  };
+
+  f4 acc[RG][NTW];
+  layer(acc, [&](int rg, int t) { return xin[rg][t]; }, NTO, P + T.W1, NTO * 16, T.b1);
+  activate(acc, T.g1, T.be1);
+  // h1 -> LDS (row-major [ROWS][H]) for the layer-2 B operands
+#pragma unroll
+  for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+    for (int u = 0; u < NTW; ++u)
+      *reinterpret_cast<f4*>(hbuf + (16 * rg + j) * H + 16 * (wave * NTW + u) + 4 * g) = acc[rg][u];
+  lds_barrier();
+  layer(acc, [&](int rg, int t) { return *reinterpret_cast<const f4*>(hbuf + (16 * rg + j) * H + 16 * t + 4 * g); },
+        NT, P + T.W2, H, T.b2);
+  activate(acc, T.g2, T.be2);
+  // ---- heads: partial dots over this wave's features, reduced over waves through LDS ----
+  const int hW = trunk == 0 ? K.cW3 : K.aW3;
+  for (int k = 0; k < nh; ++k) {
+    const int wrow = (KIND == PPO_NET_LN_BETA && trunk == 1 && k >= A) ? K.bW3 + (k - A) * H : hW + k * H;
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) {
+      float p = 0.f;
+#pragma unroll
+      for (int u = 0; u < NTW; ++u) {
+        const f4 w = pld4(pbuf, 4 * g, wrow + 16 * (wave * NTW + u));
+        p += (w.x * acc[rg][u].x + w.y * acc[rg][u].y) + (w.z * acc[rg][u].z + w.w * acc[rg][u].w);
+      }
+      p = row_allreduce(p);
+      if (g == 0) headp[wave][16 * rg + j][k] = p;
+    }
+  }
+  lds_barrier();
+  auto head_out = [&](int r, int k) {
+    const int bo = (trunk == 0) ? K.cb3 : ((KIND == PPO_NET_LN_BETA && k >= A) ? K.bb3 + (k - A) : K.ab3 + k);
+    return (((headp[0][r][k] + headp[1][r][k]) + headp[2][r][k]) + headp[3][r][k]) + P[bo];
+  };
+  if (trunk == 0) {
+    if (tid < ROWS) {
+      const int row = row0 + tid;
+      if (row < a.n) {
+        const float v = head_out(tid, 0);
+        const long env = a.env_base + row;
+        if (a.value_out) a.value_out[row] = v;
+        if (a.store_step >= 0) {
+          const long srow = (long)a.store_step * a.E + env;
+          a.s_values[srow] = v;
+          a.s_dones[srow] = a.next_done ? a.next_done[row] : 0.0f;
+        }
+      }
+    }
+    if (a.store_step >= 0) {
+      for (int idx = tid; idx < ROWS * O; idx += 256) {
+        const int r = idx / O, f = idx % O, row = row0 + r;
+        if (row < a.n) a.s_obs[((long)a.store_step * a.E + a.env_base + row) * O + f] = a.x[(size_t)row * a.ldx + f];
+      }
+    }
+    return;
+  }
+  // ---- actor: one (row, action-dim) item per thread ----
+  const SampleKey key = sample_key(a.seed, a.rank);
+  for (int idx = tid; idx < ROWS * A; idx += 256) {
+    const int r = idx / A, ai = idx % A, row = row0 + r;
+    const long env = a.env_base + row;
+    const bool valid = row < a.n;
+    float lp = 0.f, ent = 0.f, act = 0.f;
+    if constexpr (KIND == PPO_NET_TANH_NORMAL) {
+      const float mu = head_out(r, ai);
+      const float sd = expf(P[K.logstd + ai]);
+      const float var = sd * sd, lsd = logf(sd);
+      if (a.mode == PPO_GIVEN) {
+        act = valid ? a.action_in[(size_t)row * A + ai] : 0.0f;
+      } else if (a.mode == PPO_MEAN) {
+        act = mu;
+      } else {
+        uint32_t rr[4];
+        philox_draw(key, env, a.step_id, (uint32_t)(ai >> 1), rr);
+        float z0, z1;
+        box_muller(rr[0], rr[1], z0, z1);
+        act = mu + ((ai & 1) ? z1 : z0) * sd;
+      }
+      const float d = act - mu;
+      lp = -(d * d) / (2.0f * var) - lsd - kLz;
+      ent = kEntC + lsd;
+    } else {
+      const float hi = P[K.hi], lo = P[K.lo];
+      const float al = softplusf_(head_out(r, ai)) + 1.0f, be = softplusf_(head_out(r, A + ai)) + 1.0f;
+      float sv;
+      if (a.mode == PPO_GIVEN) {
+        const float av = valid ? a.action_in[(size_t)row * A + ai] : 0.5f * (hi + lo);
+        sv = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+        sv = fminf(fmaxf(sv, 1e-7f), 1.0f + 1e-7f);
+      } else if (a.mode == PPO_MEAN) {
+        sv = al / (al + be);
+      } else {
+        const float ga = gamma_mt(al, key, env, a.step_id, 0x10000u + (uint32_t)(ai * 2 + 0) * 64u);
+        const float gb = gamma_mt(be, key, env, a.step_id, 0x10000u + (uint32_t)(ai * 2 + 1) * 64u);
+        sv = ga / (ga + gb);
+      }
+      const float ab = al + be;
+      const float lga = lgammaf(al), lgb = lgammaf(be), lgab = lgammaf(ab);
+      lp = xlogyf_(al - 1.0f, sv) + xlogyf_(be - 1.0f, 1.0f - sv) + (lgab - (lga + lgb));
+      ent = (lga + lgb) - lgab - (2.0f - ab) * digammaf_(ab) -
+            ((al - 1.0f) * digammaf_(al) + (be - 1.0f) * digammaf_(be));
+      act = (sv - 0.0f) / (1.0f - 0.0f) * (hi - lo) + lo;
+    }
+    itm[r][ai][0] = lp;
+    itm[r][ai][1] = ent;
+    if (valid) {
+      if (a.action_out) a.action_out[(size_t)row * A + ai] = act;
+      if (a.store_step >= 0) a.s_actions[((long)a.store_step * a.E + env) * A + ai] = act;
+    }
+  }
+  lds_barrier();
+  if (tid < ROWS) {
+    const int row = row0 + tid;
+    if (row < a.n) {
+      float lp = 0.f, ent = 0.f;
+      for (int ai = 0; ai < A; ++ai) { lp += itm[tid][ai][0]; ent += itm[tid][ai][1]; }
+      if (a.logprob_out) a.logprob_out[row] = lp;
+      if (a.entropy_out) a.entropy_out[row] = ent;
+      if (a.store_step >= 0) a.s_logp[(long)a.store_step * a.E + a.env_base + row] = lp;
+    }
+  }
+}
+
+// =============================================================================================
 // k_fwdbwd — fused gather + forward + loss + backward of one trunk for 16 rows per wave
 // =============================================================================================
 
@@ -604,8 +849,32 @@ __global__ __launch_bounds__(256) void k_dw(DwArgs a) {
 // k_colsum — dst[seg] = sum_{c < C} src[c * stride + seg]   (fixed order => deterministic)
 // =============================================================================================
 __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
-  const int s = blockIdx.y;
-  const ColsumSeg& S = a.seg[s];
+  const ColsumSeg& S = a.seg[blockIdx.y];
+  const bool vec = ((((uintptr_t)S.src) | ((uintptr_t)S.dst)) & 15) == 0 && (S.stride & 3) == 0;
+  if (vec) {
+    const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i >= S.len) return;
+    if (i + 4 <= S.len) {
+      const float* src = S.src + i;
+      f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+      int c = 0;
+      for (; c + 4 <= S.count; c += 4) {
+        a0 += ld4(src + (size_t)(c + 0) * S.stride);
+        a1 += ld4(src + (size_t)(c + 1) * S.stride);
+        a2 += ld4(src + (size_t)(c + 2) * S.stride);
+        a3 += ld4(src + (size_t)(c + 3) * S.stride);
+      }
+      for (; c < S.count; ++c) a0 += ld4(src + (size_t)c * S.stride);
+      st4(S.dst + i, ((a0 + a1) + (a2 + a3)) * S.scale);
+      return;
+    }
+    for (long k = i; k < S.len; ++k) {
+      float acc = 0.f;
+      for (int c = 0; c < S.count; ++c) acc += S.src[(size_t)c * S.stride + k];
+      S.dst[k] = acc * S.scale;
+    }
+    return;
+  }
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= S.len) return;
   const float* src = S.src + i;
@@ -618,34 +887,21 @@ __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
 // k_gradnorm — clip_grad_norm_: per-tensor L2 norms (fp32 tensors), norm of norms, clip coef
 // =============================================================================================
 __global__ __launch_bounds__(1024) void k_gradnorm(NormArgs a) {
-  __shared__ float red[32];
-  __shared__ float norms[PPO_LAYOUT_MAX_TENSORS];
-  const int tid = threadIdx.x;
-  for (int t = 0; t < a.nt; ++t) {
-    float s = 0.0f;
-    for (int i = tid; i < a.len[t]; i += 1024) {
-      const float gv = a.grad[a.off[t] + i];
-      s += gv * gv;
-    }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
-    if ((tid & 63) == 0) red[tid >> 6] = s;
-    __syncthreads();
-    if (tid == 0) {
-      float tot = 0.0f;
-      for (int w = 0; w < 16; ++w) tot += red[w];
-      norms[t] = sqrtf(tot);
-    }
-    __syncthreads();
+  __shared__ float red[16];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  float s = 0.0f;
+  for (int i = tid; i < a.len[t]; i += 1024) {
+    const float gv = a.grad[a.off[t] + i];
+    s += gv * gv;
   }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
   if (tid == 0) {
     float tot = 0.0f;
-    for (int t = 0; t < a.nt; ++t) tot += norms[t] * norms[t];
-    const float total = sqrtf(tot);
-    float coef = a.max_norm / (total + 1e-6f);
-    coef = coef > 1.0f ? 1.0f : coef;
-    a.out[0] = total;
-    a.out[1] = coef;
+    for (int w = 0; w < 16; ++w) tot += red[w];
+    a.out[2 + t] = sqrtf(tot);  // per-tensor L2 norm (an fp32 tensor, clip_grad.h: grad.norm())
   }
 }
 
@@ -653,10 +909,22 @@ __global__ __launch_bounds__(1024) void k_gradnorm(NormArgs a) {
 // k_adam — grad *= clip coef; Adam (bias-corrected, torch::optim::Adam); refresh W2^T copies
 // =============================================================================================
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
+  __shared__ float s_coef;
+  if (threadIdx.x == 0) {
+    // clip_grad_norm_: total = ||(||g_t||)_t||, coef = clamp(max_norm / (total + 1e-6), max = 1)
+    float tot = 0.0f;
+    for (int t = 0; t < a.nt; ++t) tot += a.norm_out[2 + t] * a.norm_out[2 + t];
+    const float total = sqrtf(tot);
+    float coef = a.max_norm / (total + 1e-6f);
+    coef = coef > 1.0f ? 1.0f : coef;
+    s_coef = coef;
+    if (blockIdx.x == 0) { a.norm_out[0] = total; a.norm_out[1] = coef; }
+  }
+  __syncthreads();
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
   const long p = a.begin + i;
-  const float coef = a.norm_out ? a.norm_out[1] : 1.0f;
+  const float coef = s_coef;
   const float gv = a.grad[p] * coef;
   const float m = a.m[p] * 0.9f + gv * 0.1f;
   const float v = a.v[p] * 0.999f + gv * gv * 0.001f;
@@ -857,6 +1125,17 @@ static int dispatch_net(const PackedLayout& K, F&& f) {
 }
 
 int launch_act(const ActArgs& a, hipStream_t s) {
+  return dispatch_net(a.K, [&](auto H_, auto KIND_, auto NTO_) {
+    constexpr int H = decltype(H_)::value, KIND = decltype(KIND_)::value, NTO = decltype(NTO_)::value;
+    if (a.K.A > 20) return -1;
+    constexpr int RG = 2;  // 32 rows per workgroup
+    dim3 grid((a.n + 16 * RG - 1) / (16 * RG), a.need_actor ? 2 : 1);
+    hipLaunchKernelGGL((k_act2<H, KIND, NTO, RG>), grid, dim3(256), 0, s, a);
+    return 0;
+  });
+}
+
+int launch_act_wave(const ActArgs& a, hipStream_t s) {
   dim3 grid((a.n + 15) / 16, a.need_actor ? 2 : 1);
   return dispatch_net(a.K, [&](auto H_, auto KIND_, auto NTO_) {
     hipLaunchKernelGGL((k_act<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value>), grid, dim3(64), 0,
@@ -920,9 +1199,9 @@ int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s) {
 }
 
 void launch_colsum(const ColsumArgs& a, int nseg, long maxlen, hipStream_t s) {
-  hipLaunchKernelGGL(k_colsum, dim3((unsigned)((maxlen + 255) / 256), nseg), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_colsum, dim3((unsigned)((maxlen + 255) / 256), nseg), dim3(256), 0, s, a);  // (vector path uses 1/4)
 }
-void launch_gradnorm(const NormArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_gradnorm, dim3(1), dim3(1024), 0, s, a); }
+void launch_gradnorm(const NormArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_gradnorm, dim3(a.nt), dim3(1024), 0, s, a); }
 void launch_adam(const AdamArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_adam, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
 }

@@ -82,7 +82,7 @@ struct NormArgs {
   int off[PPO_LAYOUT_MAX_TENSORS];
   int len[PPO_LAYOUT_MAX_TENSORS];
   float max_norm;
-  float* out;  // [0] total norm, [1] clip coefficient
+  float* out;  // [0] total norm, [1] clip coefficient, [2 + t] per-tensor norms
 };
 
 struct AdamArgs {
@@ -90,7 +90,9 @@ struct AdamArgs {
   const float* grad;
   float *m, *v;
   long begin, n;
-  const float* norm_out;
+  float* norm_out;
+  int nt;
+  float max_norm;
   float step_size, sbc2, eps;
   long w2_off[2];
   float* w2t[2];

@@ -1,0 +1,400 @@
+// ac_ppo_continuous_action — drop-in for the reference executable of the same name
+// (src/ac_ppo_continuous_action.cpp): same flags and defaults, one process per GPU, envs sharded
+// per rank (num_envs_per_device = num_envs / world_size, ac:398-407), gradients averaged over ranks
+// every minibatch — here with one RCCL communicator (replacing torchfort::Comm's MPI + NCCL) inside
+// ppo_update.
+//
+// Asynchronous collection (ac:641-698): the reference runs one host thread + one CUDA stream +
+// batch-1 inference per env. Here the per-device envs are split into --num_collect_groups groups;
+// each group has a host thread and a HIP stream and runs the batched act kernel for its env slice,
+// copies the actions back, steps its envs on the CPU and copies obs/reward/done up — so the GPU
+// inference of one group overlaps the CPU env stepping of the others. Per-env trajectories are
+// identical to the reference's per-env threads (counter-based Philox sampling is independent of
+// grouping). --env_backend device runs the device-resident synthetic env instead (no PCIe).
+//
+// Launch: one process per GPU with RANK / WORLD_SIZE / LOCAL_RANK (torchrun or any launcher) or
+// OMPI_COMM_WORLD_{RANK,SIZE,LOCAL_RANK} (mpirun); the RCCL id is exchanged through --rdzv_file.
+#include "trainer_common.h"
+
+#include <atomic>
+#include <iomanip>
+#include <thread>
+
+using namespace app;
+namespace fs = std::filesystem;
+
+struct GlobalConfig {  // ac_ppo_continuous_action.cpp:55-148
+  int seed = 1;
+  int eval_seed = 2;
+  unsigned total_timesteps = 10'000'000;
+  float learning_rate = 2.5e-4f;
+  unsigned num_envs = 8;
+  unsigned num_steps = 128;
+  float gamma = 0.99f;
+  float gae_lambda = 0.95f;
+  unsigned num_minibatches = 4;
+  unsigned update_epochs = 4;
+  bool norm_adv = true;
+  float clip_coef = 0.1f;
+  bool clip_vloss = true;
+  float ent_coef = 0.01f;
+  float vf_coef = 0.5f;
+  float max_grad_norm = 0.5f;
+  float adam_eps = 1e-5f;
+  bool anneal_lr = true;
+  unsigned num_eval_runs = 128;
+  bool clip_actions = true;
+  bool torch_deterministic = true;
+  std::string exp_name_stem = "Ant-v5_AC_PPO_Atari";
+  std::string env_id = "Ant-v5";
+  std::string render = "rgb_array";
+  std::vector<int> gpu_ids = {0};
+  std::string collect_device = "cpu";
+  std::string train_device = "cpu";
+  std::string rdzv_addr = "localhost";
+  int tcp_store_port = 29500;
+  int use_dd_ppo_preempt = 0;
+  float dd_ppo_min_perc = 0.25f;
+  float dd_ppo_preempt_threshold = 0.6f;
+  bool estimate_mean_std = false;
+  // MI355X build additions
+  std::string env_backend = "host";  // host | device
+  int num_collect_groups = 8;
+  std::string rdzv_file = "";
+  unsigned num_devices = 1, num_envs_per_device = 0, batch_size = 0, minibatch_size = 0, num_iterations = 0;
+  unsigned batch_size_per_device = 0, minibatch_per_device = 0;
+  std::string exp_name;
+};
+
+static int env_int(const char* a, const char* b, int def) {
+  if (const char* v = std::getenv(a)) return std::atoi(v);
+  if (const char* v = std::getenv(b)) return std::atoi(v);
+  return def;
+}
+
+int main(int argc, const char** argv) {
+  std::ios_base::sync_with_stdio(false);
+  const int rank = env_int("RANK", "OMPI_COMM_WORLD_RANK", 0);
+  const int world_size = env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", 1);
+  const int local_rank = env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", rank);
+
+  GlobalConfig config;
+  Flags flags;
+  flags.add("seed", "Training seed", &config.seed);
+  flags.add("eval_seed", "Seed of final evaluation run", &config.eval_seed);
+  flags.add("total_timesteps", "Number of environment steps", &config.total_timesteps);
+  flags.add("learning_rate", "Adam learning rate", &config.learning_rate);
+  flags.add("num_steps", "Num environment steps per iteration", &config.num_steps);
+  flags.add("gamma", "Discount factor", &config.gamma);
+  flags.add("gae_lambda", "Lambda of generalized advantage estimation", &config.gae_lambda);
+  flags.add("num_minibatches", "Number of training iterations per epoch", &config.num_minibatches);
+  flags.add("update_epochs", "Number of training epochs per iteration", &config.update_epochs);
+  flags.add("norm_adv", "Whether to normalize the advantage", &config.norm_adv);
+  flags.add("clip_coef", "PPO clip coefficient", &config.clip_coef);
+  flags.add("clip_vloss", "Whether to apply clipping to the value loss", &config.clip_vloss);
+  flags.add("ent_coef", "Weigth of entropy loss.", &config.ent_coef);
+  flags.add("vf_coef", "Weigth of value loss.", &config.vf_coef);
+  flags.add("max_grad_norm", "Factor for gradient clipping.", &config.max_grad_norm);
+  flags.add("adam_eps", "Epsilon of adam.", &config.adam_eps);
+  flags.add("anneal_lr", "Whether to anneal the learning rate linearly.", &config.anneal_lr);
+  flags.add("num_eval_runs", "How many environments to evaluate", &config.num_eval_runs);
+  flags.add("clip_actions", "Whether to clip action into the valid range.", &config.clip_actions);
+  flags.add("torch_deterministic", "Whether to use deterministic algorithms (always deterministic here)",
+            &config.torch_deterministic);
+  flags.add("exp_name_stem", "Name of the experiment.", &config.exp_name_stem);
+  flags.add("env_id", "Name of the env to be executed.", &config.env_id);
+  flags.add("render", "rgb_array (human rendering needs MuJoCo/GLFW)", &config.render);
+  flags.add("num_envs", "Number of environments to be used.", &config.num_envs);
+  flags.add_list("gpu_ids", "The ids of the GPUs used for training. Usage: --gpu_ids 0 --gpu_ids 1 ...", &config.gpu_ids);
+  flags.add("collect_device", "Whether to collect data on gpu or cpu. Options: cpu, gpu", &config.collect_device);
+  flags.add("train_device", "Whether to train on gpu or cpu. Options: cpu, gpu", &config.train_device);
+  flags.add("rdzv_addr", "IP adress of master node. Default: localhost", &config.rdzv_addr);
+  flags.add("tcp_store_port", "Port for the TCP store. Default: 29500", &config.tcp_store_port);
+  flags.add("use_dd_ppo_preempt", "Flag to toggle the dd_ppo pre-emption trick", &config.use_dd_ppo_preempt);
+  flags.add("dd_ppo_min_perc", "Percentage of envs that need to finish before preemtion.", &config.dd_ppo_min_perc);
+  flags.add("dd_ppo_preempt_threshold", "Percentage of envs that need to finish before preemtion.",
+            &config.dd_ppo_preempt_threshold);
+  flags.add("estimate_mean_std", "Estimate obs mean/std of env 0 (no-op here)", &config.estimate_mean_std);
+  flags.add("env_backend", "host (gymcpp envs on the CPU) or device (synthetic env in HBM)", &config.env_backend);
+  flags.add("num_collect_groups", "host envs: number of async collection groups (threads + HIP streams)",
+            &config.num_collect_groups);
+  flags.add("rdzv_file", "file used to exchange the RCCL id between ranks", &config.rdzv_file);
+  try {
+    flags.parse(argc, argv);
+  } catch (const HelpRequested&) {
+    flags.print_help(std::cout);
+    return 0;
+  } catch (const ParseError& e) {
+    std::cerr << e.what() << std::endl;
+    flags.print_help(std::cerr);
+    return 1;
+  }
+  if (config.use_dd_ppo_preempt) {
+    std::cerr << "use_dd_ppo_preempt is not supported by this build (disabled in every reference config)\n";
+    return 1;
+  }
+  // derived fields (ac:398-407)
+  config.num_devices = world_size;
+  config.num_envs_per_device = config.num_envs / config.num_devices;
+  if (config.num_envs % config.num_devices != 0) {
+    std::cerr << "num_envs must be a multiple of num_devices.\n";
+    return 1;
+  }
+  config.exp_name = config.exp_name_stem + "_" + std::to_string(config.seed);
+  config.batch_size = config.num_steps * config.num_envs;
+  config.minibatch_size = config.batch_size / config.num_minibatches;
+  config.num_iterations = config.total_timesteps / config.batch_size;
+  config.batch_size_per_device = config.batch_size / config.num_devices;
+  config.minibatch_per_device = config.minibatch_size / config.num_devices;
+  std::cout << "world_size: " << world_size << "\nrank: " << rank << "\nlocal_rank: " << local_rank << std::endl;
+  if (config.collect_device != "cpu" && config.collect_device != "gpu") {
+    std::cerr << "Unsupported Collect device selected. Options: cpu, gpu. Selected Device: " << config.collect_device << std::endl;
+    return 2;
+  }
+  if (config.train_device != "cpu" && config.train_device != "gpu") {
+    std::cerr << "Unsupported train device selected. Options: cpu, gpu. Selected device: " << config.train_device << std::endl;
+    return 3;
+  }
+  // The agent always runs on the MI355X (the reference's cpu options exist for LibTorch CPU runs).
+  const int device = config.gpu_ids.at((size_t)local_rank % config.gpu_ids.size());
+
+  const fs::path exe = fs::canonical(argv[0]);
+  const fs::path exp_folder = exe.parent_path() / ".." / "models" / config.exp_name;
+  fs::create_directories(exp_folder);
+  ScalarLog logger(exp_folder / ("scalars_" + std::to_string(rank) + ".jsonl"));
+
+  const int E = (int)config.num_envs_per_device, T = (int)config.num_steps;
+  const bool device_env = config.env_backend == "device";
+  int O = 17, A = 6;
+  float act_lo = -1.f, act_hi = 1.f;
+  std::vector<std::shared_ptr<gymcpp::SeqVectorEnv>> envs;  // one SeqVectorEnv per env, as the reference
+  if (!device_env) {
+    try {
+      for (int i = 0; i < E; ++i) {
+        std::vector<std::shared_ptr<gymcpp::EnvironmentWrapper>> arr{
+            std::make_shared<gymcpp::RecordEpisodeStatistics>(make_base_env(config.env_id))};
+        envs.push_back(std::make_shared<gymcpp::SeqVectorEnv>(arr, config.clip_actions));
+      }
+    } catch (const std::invalid_argument& e) {
+      std::cerr << e.what() << std::endl;
+      return 1;
+    }
+    O = envs[0]->get_observation_space();
+    A = envs[0]->get_action_space();
+    act_lo = envs[0]->get_action_space_min();
+    act_hi = envs[0]->get_action_space_max();
+  } else if (config.env_id != "SyntheticCheetah-v0" && config.env_id != "HalfCheetah-v5") {
+    std::cerr << "env_backend device provides the HalfCheetah-shaped synthetic env only\n";
+    return 1;
+  }
+
+  ppo_hip_config hc{};
+  hc.net_kind = PPO_NET_LN_BETA; hc.obs_dim = O; hc.act_dim = A; hc.hidden = 256;
+  hc.num_envs = E; hc.num_steps = T; hc.num_minibatches = (int)config.num_minibatches;
+  hc.update_epochs = (int)config.update_epochs; hc.gamma = config.gamma; hc.gae_lambda = config.gae_lambda;
+  hc.clip_coef = config.clip_coef; hc.ent_coef = config.ent_coef; hc.vf_coef = config.vf_coef;
+  hc.max_grad_norm = config.max_grad_norm; hc.adam_eps = config.adam_eps; hc.norm_adv = config.norm_adv;
+  hc.clip_vloss = config.clip_vloss; hc.seed = (uint64_t)config.seed; hc.rank = rank; hc.world_size = world_size;
+  ppo_t* agent = nullptr;
+  psyn_t* denv = nullptr;
+  try {
+    check(ppo_create(&hc, device, &agent), "ppo_create");
+    ppo_layout L;
+    check(ppo_get_layout(agent, &L), "ppo_get_layout");
+    auto p0 = init_params(L, config.seed, act_hi, act_lo, {}, {});
+    check(ppo_load_params(agent, p0.data(), L.P), "ppo_load_params");
+    if (world_size > 1) {  // ncclUniqueId exchange through a file (no MPI in this build)
+      const std::string path = config.rdzv_file.empty()
+                                   ? "/tmp/ppo_rdzv_" + std::to_string(config.tcp_store_port) + ".id"
+                                   : config.rdzv_file;
+      char id[PPO_COMM_ID_BYTES];
+      if (rank == 0) {
+        check(ppo_comm_unique_id(id), "ppo_comm_unique_id");
+        std::ofstream(path + ".tmp", std::ios::binary).write(id, PPO_COMM_ID_BYTES);
+        fs::rename(path + ".tmp", path);
+      } else {
+        for (int tries = 0; !fs::exists(path); ++tries) {
+          if (tries > 6000) throw std::runtime_error("timed out waiting for " + path);
+          std::this_thread::sleep_for(std::chrono::milliseconds(10));
+        }
+        std::ifstream(path, std::ios::binary).read(id, PPO_COMM_ID_BYTES);
+      }
+      check(ppo_comm_init(agent, id, rank, world_size), "ppo_comm_init");
+      check(ppo_comm_broadcast_params(agent, 0), "ppo_comm_broadcast_params");  // ac:551-553
+    }
+    if (rank == 0) std::cout << "Number of parameters in model: " << (L.P - L.train_begin) << std::endl;
+
+    hipStream_t s = (hipStream_t)ppo_stream(agent);
+    float *d_obs, *d_done, *d_act, *d_rew;
+    HIPCHECK(hipMalloc(&d_obs, sizeof(float) * E * O));
+    HIPCHECK(hipMalloc(&d_done, sizeof(float) * E));
+    HIPCHECK(hipMalloc(&d_act, sizeof(float) * E * A));
+    HIPCHECK(hipMalloc(&d_rew, sizeof(float) * E));
+    HIPCHECK(hipMemset(d_done, 0, sizeof(float) * E));
+    float *h_obs = nullptr, *h_act = nullptr, *h_rew = nullptr, *h_done = nullptr;
+    const int G = std::max(1, std::min(config.num_collect_groups, E));
+    std::vector<hipStream_t> gstreams(G);
+    if (device_env) {
+      check(psyn_create(E, O, A, &denv), "psyn_create");
+      check(psyn_reset(denv, config.seed, d_obs, d_done, s), "psyn_reset");
+    } else {
+      HIPCHECK(hipHostMalloc(&h_obs, sizeof(float) * E * O));
+      HIPCHECK(hipHostMalloc(&h_act, sizeof(float) * E * A));
+      HIPCHECK(hipHostMalloc(&h_rew, sizeof(float) * E));
+      HIPCHECK(hipHostMalloc(&h_done, sizeof(float) * E));
+      for (int i = 0; i < E; ++i) {  // env i reset with seed + i (ac:606)
+        const float* o = envs[i]->reset(config.seed + i);
+        std::copy(o, o + O, h_obs + (size_t)i * O);
+      }
+      HIPCHECK(hipMemcpy(d_obs, h_obs, sizeof(float) * E * O, hipMemcpyHostToDevice));
+      for (auto& gs : gstreams) HIPCHECK(hipStreamCreateWithFlags(&gs, hipStreamNonBlocking));
+    }
+    HIPCHECK(hipDeviceSynchronize());
+
+    long global_step = 0;
+    const auto start_time = std::chrono::high_resolution_clock::now();
+    ppo_update_stats st{};
+    for (unsigned iteration = 0; iteration < config.num_iterations; ++iteration) {
+      float lrnow = config.learning_rate;
+      if (config.anneal_lr) {  // ac:634-639
+        const float frac = 1.0f - static_cast<float>(iteration) / static_cast<float>(config.num_iterations);
+        lrnow = frac * config.learning_rate;
+      }
+      double sum_r = 0, sum_l = 0, n_ep = 0;
+      if (device_env) {
+        check(ppo_rollout_synth(agent, denv, d_obs, d_done, d_act, d_rew), "ppo_rollout_synth");
+        float r, l, n;
+        check(psyn_episode_stats(denv, &r, &l, &n), "psyn_episode_stats");
+        sum_r = r; sum_l = l; n_ep = n;
+      } else {
+        // asynchronous collection: one host thread + HIP stream per env group
+        std::vector<std::thread> th;
+        std::vector<double> gr(G, 0), gl(G, 0), gn(G, 0);
+        std::atomic<int> failed{0};
+        for (int gi = 0; gi < G; ++gi) {
+          th.emplace_back([&, gi] {
+            const int e0 = E * gi / G, e1 = E * (gi + 1) / G, n = e1 - e0;
+            hipStream_t gs = gstreams[gi];
+            try {
+              for (int step = 0; step < T; ++step) {
+                check(ppo_rollout_act(agent, step, e0, e1, d_obs + (size_t)e0 * O, d_done + e0, d_act + (size_t)e0 * A, gs),
+                      "ppo_rollout_act");
+                HIPCHECK(hipMemcpyAsync(h_act + (size_t)e0 * A, d_act + (size_t)e0 * A, sizeof(float) * n * A,
+                                        hipMemcpyDeviceToHost, gs));
+                HIPCHECK(hipStreamSynchronize(gs));
+                for (int i = e0; i < e1; ++i) {
+                  gymcpp::VecStep r = envs[i]->step(h_act + (size_t)i * A);
+                  std::copy(r.obs, r.obs + O, h_obs + (size_t)i * O);
+                  h_rew[i] = r.rewards[0];
+                  h_done[i] = (r.terminations[0] != 0.f || r.truncations[0] != 0.f) ? 1.f : 0.f;
+                  if ((*r.infos)[0].has_value()) {
+                    gr[gi] += (*r.infos)[0]->r;
+                    gl[gi] += (*r.infos)[0]->l;
+                    gn[gi] += 1;
+                  }
+                }
+                HIPCHECK(hipMemcpyAsync(d_rew + e0, h_rew + e0, sizeof(float) * n, hipMemcpyHostToDevice, gs));
+                check(ppo_rollout_reward(agent, step, e0, e1, d_rew + e0, gs), "ppo_rollout_reward");
+                HIPCHECK(hipMemcpyAsync(d_obs + (size_t)e0 * O, h_obs + (size_t)e0 * O, sizeof(float) * n * O,
+                                        hipMemcpyHostToDevice, gs));
+                HIPCHECK(hipMemcpyAsync(d_done + e0, h_done + e0, sizeof(float) * n, hipMemcpyHostToDevice, gs));
+              }
+              HIPCHECK(hipStreamSynchronize(gs));
+            } catch (const std::exception& e) {
+              std::cerr << e.what() << std::endl;
+              failed = 1;
+            }
+          });
+        }
+        for (auto& t : th) t.join();
+        if (failed) throw std::runtime_error("collection failed");
+        for (int gi = 0; gi < G; ++gi) { sum_r += gr[gi]; sum_l += gl[gi]; n_ep += gn[gi]; }
+      }
+      global_step += (long)config.num_envs * config.num_steps;  // ac:730
+      // episode statistics summed over ranks (ac:700-727), through the RCCL communicator
+      float h_stats[3] = {(float)sum_r, (float)sum_l, (float)n_ep};
+      if (world_size > 1) {
+        float* d_stats;
+        HIPCHECK(hipMalloc(&d_stats, sizeof(h_stats)));
+        HIPCHECK(hipMemcpy(d_stats, h_stats, sizeof(h_stats), hipMemcpyHostToDevice));
+        check(ppo_comm_allreduce(agent, d_stats, 3, 0), "ppo_comm_allreduce");
+        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(hipMemcpy(h_stats, d_stats, sizeof(h_stats), hipMemcpyDeviceToHost));
+        (void)hipFree(d_stats);
+      }
+      if (rank == 0 && h_stats[2] > 0) {
+        const float avg_return = h_stats[0] / h_stats[2], avg_length = h_stats[1] / h_stats[2];
+        logger.add_scalar("charts/episodic_return", global_step, avg_return);
+        logger.add_scalar("charts/episodic_length", global_step, avg_length);
+        std::cout << "global_step=" << global_step << ", avg_episodic_return=" << std::fixed << std::setprecision(2)
+                  << avg_return << " \n";
+        logger.add_scalar("charts/episodic_return_per_sec", std::lround(seconds_since(start_time)), avg_return);
+      }
+      check(ppo_compute_gae(agent, d_obs, d_done, T, s), "ppo_compute_gae");
+      check(ppo_update(agent, lrnow, nullptr, &st), "ppo_update");  // stats are rank-averaged inside
+      if (rank == 0) {
+        char mf[64], of[64];
+        std::snprintf(mf, sizeof mf, "model_latest_%09u.bin", iteration);
+        std::snprintf(of, sizeof of, "optimizer_latest_%09u.bin", iteration);
+        save_state(agent, exp_folder, mf, of);
+        cleanup_checkpoints(exp_folder, iteration);
+        const double secs = seconds_since(start_time);
+        float sps = 0.f;
+        if (secs > 0) {
+          sps = (float)(global_step / secs);
+          std::cout << std::fixed << std::setprecision(0) << "SPS: " << sps << std::endl;
+        }
+        logger.add_scalar("charts/learning_rate", global_step, lrnow);
+        logger.add_scalar("losses/value_loss", global_step, st.v_loss);
+        logger.add_scalar("losses/policy_loss", global_step, st.pg_loss);
+        logger.add_scalar("losses/entropy", global_step, st.entropy);
+        logger.add_scalar("losses/old_approx_kl", global_step, st.old_approx_kl);
+        logger.add_scalar("losses/approx_kl", global_step, st.approx_kl);
+        logger.add_scalar("losses/clipfrac", global_step, st.clipfrac);
+        logger.add_scalar("charts/SPS", global_step, sps);
+      }
+      std::cout << std::flush;
+    }
+    if (rank == 0) save_state(agent, exp_folder, "model_final.bin", "optimizer_final.bin");
+    // rank 0 evaluation with the Beta mean action on env 0 (ac:965-1001)
+    if (rank == 0 && !device_env) {
+      std::vector<float> episodic_returns;
+      const float* o = envs[0]->reset(config.eval_seed);
+      std::copy(o, o + O, h_obs);
+      long guard = 0;
+      while (episodic_returns.size() < config.num_eval_runs && guard++ < 100000000L) {
+        HIPCHECK(hipMemcpy(d_obs, h_obs, sizeof(float) * O, hipMemcpyHostToDevice));
+        check(ppo_get_action_and_value(agent, 1, d_obs, PPO_MEAN, nullptr, 0, 0, d_act, nullptr, nullptr, nullptr, s),
+              "ppo_get_action_and_value");
+        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(hipMemcpy(h_act, d_act, sizeof(float) * A, hipMemcpyDeviceToHost));
+        gymcpp::VecStep r = envs[0]->step(h_act);
+        std::copy(r.obs, r.obs + O, h_obs);
+        if ((*r.infos)[0].has_value()) {
+          std::cout << "Evaluation result: episode=" << episodic_returns.size() << " episodic_return=" << std::fixed
+                    << std::setprecision(2) << (*r.infos)[0]->r << " \n";
+          episodic_returns.push_back((*r.infos)[0]->r);
+        }
+      }
+      for (size_t i = 0; i < episodic_returns.size(); ++i) logger.add_scalar("eval/episodic_return", (long)i, episodic_returns[i]);
+      double avg = 0;
+      for (float x : episodic_returns) avg += x;
+      avg /= std::max<size_t>(1, episodic_returns.size());
+      logger.add_scalar("eval/avg_return", (long)episodic_returns.size(), avg);
+      std::cout << "Average evaluation return=" << std::fixed << std::setprecision(2) << avg << " over "
+                << episodic_returns.size() << " episodes" << std::endl;
+    }
+    for (auto gs : gstreams)
+      if (gs) (void)hipStreamDestroy(gs);
+    if (denv) psyn_destroy(denv);
+    (void)hipFree(d_obs); (void)hipFree(d_done); (void)hipFree(d_act); (void)hipFree(d_rew);
+    if (h_obs) { (void)hipHostFree(h_obs); (void)hipHostFree(h_act); (void)hipHostFree(h_rew); (void)hipHostFree(h_done); }
+    ppo_destroy(agent);
+  } catch (const std::exception& e) {
+    std::cerr << e.what() << std::endl;
+    if (denv) psyn_destroy(denv);
+    if (agent) ppo_destroy(agent);
+    return 6;
+  }
+  return 0;
+}

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts 64 B per memory-side read
+request while wide coalesced reads issue 128-B requests, so it reports half the bytes: it is
+doubled here. WRITE_SIZE is exact for 16-B-per-lane stores. Both counters are in KB (1024 B).
+Usage: pmc_traffic.py <rocprof out dir> <config tag>  -> JSON on stdout."""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+CLASSES = [("k_fwdbwd", "fwdbwd"), ("k_dw", "dw"), ("k_act", "act"), ("k_colsum", "colsum"),
+           ("k_gradnorm", "gradnorm"), ("k_adam", "adam"), ("k_gae", "gae"), ("k_perm", "perm"),
+           ("k_adv_", "adv_stats"), ("k_synth_step", "synth_env")]
+
+
+def klass(name):
+    for pat, k in CLASSES:
+        if re.search(r"\b" + pat, name):
+            return k
+    return None
+
+
+def per_kernel(path, counter):
+    acc = {}
+    for fn in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") != counter:
+                    continue
+                k = klass(row.get("Kernel_Name", ""))
+                if k is None:
+                    continue
+                key = (row.get("Dispatch_Id") or row.get("Correlation_Id"), k)
+                acc.setdefault(k, {}).setdefault(key, 0.0)
+                acc[k][key] += float(row["Counter_Value"])
+    return {k: (sum(v.values()), len(v)) for k, v in acc.items()}
+
+
+def main():
+    path, tag = sys.argv[1], sys.argv[2]
+    fetch = per_kernel(os.path.join(path), "FETCH_SIZE")
+    write = per_kernel(os.path.join(path), "WRITE_SIZE")
+    out = {"_note": "bytes per launch; FETCH_SIZE doubled (gfx950 correction), KB = 1024 B; config = bench workload"}
+    for k in sorted(set(fetch) | set(write)):
+        fsum, fn = fetch.get(k, (0.0, 0))
+        wsum, wn = write.get(k, (0.0, 0))
+        if fn == 0 or wn == 0:
+            continue
+        rd = 2.0 * fsum * 1024 / fn
+        wr = wsum * 1024 / wn
+        out[k] = {"config": tag, "read_bytes_per_launch": round(rd), "write_bytes_per_launch": round(wr),
+                  "hbm_bytes_per_launch": round(rd + wr), "launches_fetch": fn, "launches_write": wn}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -74,6 +75,9 @@ struct ppo_ctx {
   float *Xn = nullptr, *H1[2] = {}, *DZ1[2] = {}, *DZ2[2] = {};
   float* slab[2] = {};
   int tiles_per_block = 1, nblk = 1;
+  bool use_upd = false;  // feature-split k_upd (ppo_update.hip) instead of k_fwdbwd
+  UpdGeoOut upd = {};
+  int upd_nblk = 0;
   size_t lds_bytes = 0;
   int wlds_off = 0;
   float* dwslab[4] = {};
@@ -216,7 +220,17 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   const int tiles = (int)(Mr / 64);
   c->tiles_per_block = std::max(1, (tiles + 255) / 256);
   c->nblk = (tiles + c->tiles_per_block - 1) / c->tiles_per_block;
-  for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->slab[k], (size_t)c->nblk * c->sg[k].size);
+  {
+    const char* ev = getenv("PPO_UPD_KERNEL");  // "0": force the wave-per-16-rows k_fwdbwd
+    const int sgmax = std::max(c->sg[0].size, c->sg[1].size);
+    if (!(ev && ev[0] == '0') && upd_supported(c->K, c->sg[1].nh, sgmax, &c->upd) == 0) {
+      c->use_upd = true;
+      const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
+      c->upd_nblk = std::min(ut, 256);  // 2 workgroups per CU x 256 CUs over the two trunks
+    }
+  }
+  for (int k = 0; k < 2; ++k)
+    rc |= dmalloc(&c->slab[k], (size_t)std::max(c->nblk, c->upd_nblk) * c->sg[k].size);
   c->wlds_off = 4 * std::max(c->sg[0].size, c->sg[1].size);
   c->wlds_off = (c->wlds_off + 63) & ~63;
   c->lds_bytes = ((size_t)c->wlds_off + 2 * (size_t)H * 16) * sizeof(float);
@@ -531,6 +545,9 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   u.clip_vloss = cfg.clip_vloss;
   u.norm_adv = cfg.norm_adv;
   u.Xn = c->Xn;
+  u.actn_off = c->upd.actn_off;
+  u.acc_off = c->upd.acc_off;
+  const int nblk = c->use_upd ? c->upd_nblk : c->nblk;  // workgroups that wrote a slab row
   for (int k = 0; k < 2; ++k) {
     u.H1[k] = c->H1[k];
     u.DZ1[k] = c->DZ1[k];
@@ -565,26 +582,26 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
     seg(c->dwslab[k] + (long)H * H, dw.slab_stride, c->nchunks, H * OP, c->G + T.W1, 1.f);
     const SmallGradLayout& g = c->sg[k];
     const float* sl = c->slab[k];
-    seg(sl + g.b1, g.size, c->nblk, H, c->G + T.b1, 1.f);
-    seg(sl + g.b2, g.size, c->nblk, H, c->G + T.b2, 1.f);
+    seg(sl + g.b1, g.size, nblk, H, c->G + T.b1, 1.f);
+    seg(sl + g.b2, g.size, nblk, H, c->G + T.b2, 1.f);
     if (ln) {
-      seg(sl + g.g1, g.size, c->nblk, H, c->G + T.g1, 1.f);
-      seg(sl + g.be1, g.size, c->nblk, H, c->G + T.be1, 1.f);
-      seg(sl + g.g2, g.size, c->nblk, H, c->G + T.g2, 1.f);
-      seg(sl + g.be2, g.size, c->nblk, H, c->G + T.be2, 1.f);
+      seg(sl + g.g1, g.size, nblk, H, c->G + T.g1, 1.f);
+      seg(sl + g.be1, g.size, nblk, H, c->G + T.be1, 1.f);
+      seg(sl + g.g2, g.size, nblk, H, c->G + T.g2, 1.f);
+      seg(sl + g.be2, g.size, nblk, H, c->G + T.be2, 1.f);
     }
     if (k == 0) {
-      seg(sl + g.hW, g.size, c->nblk, H, c->G + c->K.cW3, 1.f);
-      seg(sl + g.hb, g.size, c->nblk, 1, c->G + c->K.cb3, 1.f);
+      seg(sl + g.hW, g.size, nblk, H, c->G + c->K.cW3, 1.f);
+      seg(sl + g.hb, g.size, nblk, 1, c->G + c->K.cb3, 1.f);
     } else if (!ln) {
-      seg(sl + g.hW, g.size, c->nblk, A * H, c->G + c->K.aW3, 1.f);
-      seg(sl + g.hb, g.size, c->nblk, A, c->G + c->K.ab3, 1.f);
-      seg(sl + g.ls, g.size, c->nblk, A, c->G + c->K.logstd, 1.f);
+      seg(sl + g.hW, g.size, nblk, A * H, c->G + c->K.aW3, 1.f);
+      seg(sl + g.hb, g.size, nblk, A, c->G + c->K.ab3, 1.f);
+      seg(sl + g.ls, g.size, nblk, A, c->G + c->K.logstd, 1.f);
     } else {
-      seg(sl + g.hW, g.size, c->nblk, A * H, c->G + c->K.aW3, 1.f);
-      seg(sl + g.hW + A * H, g.size, c->nblk, A * H, c->G + c->K.bW3, 1.f);
-      seg(sl + g.hb, g.size, c->nblk, A, c->G + c->K.ab3, 1.f);
-      seg(sl + g.hb + A, g.size, c->nblk, A, c->G + c->K.bb3, 1.f);
+      seg(sl + g.hW, g.size, nblk, A * H, c->G + c->K.aW3, 1.f);
+      seg(sl + g.hW + A * H, g.size, nblk, A * H, c->G + c->K.bW3, 1.f);
+      seg(sl + g.hb, g.size, nblk, A, c->G + c->K.ab3, 1.f);
+      seg(sl + g.hb + A, g.size, nblk, A, c->G + c->K.bb3, 1.f);
     }
   }
   const int stats_seg0 = ns;  // filled per minibatch below
@@ -629,16 +646,18 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
       u.adv_stats = c->advstats + 2 * gi;
       {
         ProfScope ps(c, PK_FWDBWD, s);
-        if (launch_fwdbwd(u, c->nblk, c->lds_bytes, s) != 0) return fail("no update kernel for this configuration");
+        const int rc_ = c->use_upd ? launch_upd(u, c->sg[1].nh, c->upd_nblk, c->upd.lds_bytes, s)
+                                   : launch_fwdbwd(u, nblk, c->lds_bytes, s);
+        if (rc_ != 0) return fail("no update kernel for this configuration");
       }
       {
         ProfScope ps(c, PK_DW2, s);
         if (launch_dw(dw, H, OP, c->nchunks, s) != 0) return fail("no dW kernel for this configuration");
       }
       float* st = c->mbstats + 8 * gi;
-      cs.seg[stats_seg0 + 0] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_PG, st + ST_PG, c->sg[1].size, c->nblk, 1, 1.f / M};
-      cs.seg[stats_seg0 + 1] = ColsumSeg{c->slab[0] + c->sg[0].stats + ST_V, st + ST_V, c->sg[0].size, c->nblk, 1, 0.5f / M};
-      cs.seg[stats_seg0 + 2] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_ENT, st + ST_ENT, c->sg[1].size, c->nblk, 4, 1.f / M};
+      cs.seg[stats_seg0 + 0] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_PG, st + ST_PG, c->sg[1].size, nblk, 1, 1.f / M};
+      cs.seg[stats_seg0 + 1] = ColsumSeg{c->slab[0] + c->sg[0].stats + ST_V, st + ST_V, c->sg[0].size, nblk, 1, 0.5f / M};
+      cs.seg[stats_seg0 + 2] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_ENT, st + ST_ENT, c->sg[1].size, nblk, 4, 1.f / M};
       {
         ProfScope ps(c, PK_COLSUM, s);
         launch_colsum(cs, ns, maxlen, s);

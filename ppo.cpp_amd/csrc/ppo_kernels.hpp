@@ -50,6 +50,13 @@ struct UpdArgs {
   float* DZ1[2];
   float* DZ2[2];
   float* slab[2];
+  int actn_off, acc_off;  // k_upd: runtime LDS offsets (floats)
+};
+
+// k_upd geometry (ppo_update.hip)
+struct UpdGeoOut {
+  size_t lds_bytes;
+  int actn_off, acc_off, rows;
 };
 
 struct DwArgs {
@@ -131,6 +138,8 @@ struct SynthArgs {
 int launch_act(const ActArgs& a, hipStream_t s);
 int launch_fwdbwd(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s);
 int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes);
+int upd_supported(const PackedLayout& K, int nh_actor, int sg_size, UpdGeoOut* g);
+int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s);
 int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s);
 size_t dw_lds_bytes(int H, int OP);
 void launch_colsum(const ColsumArgs& a, int nseg, long maxlen, hipStream_t s);

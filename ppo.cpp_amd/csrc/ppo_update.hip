@@ -1,0 +1,805 @@
+// ppo_update.hip — k_upd: the fused minibatch forward / PPO loss / backward kernel, feature-split.
+//
+// Same contract as k_fwdbwd (ppo_kernels.hip) — gather through the permutation, forward of one
+// trunk, heads, clipped-surrogate / value / entropy loss and its gradient, backward to dz2 / dz1,
+// the "small gradient" slab (biases, LayerNorm affine, head weights and biases, logstd, loss
+// stats) and the Xn / H1 / DZ1 / DZ2 activations the dW GEMM reads — but laid out so that the
+// VALU work stays small next to the MFMA work (reference: ppo:495-538, ac:815-875):
+//
+//  * a workgroup (4 waves) owns R rows per iteration; the rows' activations live in LDS
+//    ([R][H+4] fp32, row stride = 4 mod 64 banks so every ds_read_b128 B-operand load is
+//    conflict-free); each wave owns FT 16-feature output tiles x RT 16-row tiles, so a 256-wide
+//    layer needs 64 accumulator registers per wave instead of 256;
+//  * weight A-operands stream from L2 with buffer loads, double-buffered one k-block ahead;
+//  * heads are MFMAs (split-K over the waves' features, partials reduced through LDS), the head
+//    backward dh2 = W3^T G^T and the head weight gradient G^T h2 are MFMAs too;
+//  * LayerNorm row statistics: in-lane sums + 2 lane shuffles + a cross-wave LDS exchange;
+//    column sums (bias / LN-affine gradients) are a 15-shuffle reduce-scatter per vector per
+//    iteration instead of per 16 rows;
+//  * R = 32 rows keep LDS under 80 KB, so two workgroups (8 waves) share a CU and one's VALU /
+//    barrier phases overlap the other's MFMA phases.
+// Everything is reduced in a fixed order: results are bitwise reproducible run to run.
+#include "ppo_agent.hpp"
+#include "ppo_kernels.hpp"
+
+namespace {
+
+template <int H_, int NTO_, int NHT_>
+struct Geo {
+  static constexpr int H = H_, NT = H / 16;
+  static constexpr int WF = (H >= 256) ? 4 : 1;  // wave feature groups
+  static constexpr int WR = 4 / WF;              // wave row groups
+  static constexpr int FT = NT / WF;             // 16-feature tiles per wave
+  static constexpr int RT = (WF == 4) ? 2 : 1;   // 16-row tiles per wave
+  static constexpr int R = 16 * RT * WR;         // rows per workgroup iteration
+  static constexpr int NTO = NTO_, OP = NTO * 16;
+  static constexpr int NHT = NHT_, NHP = 16 * NHT;
+  static constexpr int LDX = ((OP + 63) / 64) * 64 + 4;
+  static constexpr int LDA = ((H + 63) / 64) * 64 + 4;
+  static constexpr int LDG = NHP + 4;
+  static constexpr int ITS = 10;  // floats per (row, action) item
+  // static part of the LDS carve (floats); the runtime part (items, rows, accumulators) follows
+  static constexpr int oXN = 0;
+  static constexpr int oACT = oXN + R * LDX;
+  static constexpr int oRED = oACT + R * LDA;        // 4 slots x WF x R
+  static constexpr int oPRE = oRED + 4 * WF * R;     // R x LDG head pre-activations
+  static constexpr int oG = oPRE + R * LDG;          // R x LDG head gradients
+  static constexpr int oROW = oG + R * LDG;          // R x 8 per-row scalars
+  static constexpr int oSCR = oROW + R * 8;          // head partials (WF x NHP x R) / items (R x A x ITS)
+};
+
+PPO_DEV float lds_f(const float* p) { return *p; }
+PPO_DEV f4 lds_f4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+PPO_DEV void lds_st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+PPO_DEV float bld1(PBuf b, int lane_floats, int uni_floats) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b.r, lane_floats * 4, uni_floats * 4, 0));
+}
+
+// out[ft][rt] (+)= sum_k W[fbase + 16 ft + i][k] * IN[rbase + 16 rt + j][k], k in [0, 16 NKB)
+//   wlane = (fbase + i) * LDW + 4 g (per lane), in = IN + (rbase + j) * LDI + 4 g (LDS, per lane)
+// A (weights) double-buffered one 16-wide k-block ahead; B (activations) one ds_read_b128 per row tile.
+template <int FT, int RT, int NKB, int LDW, int LDI>
+PPO_DEV void mm_fr(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* in) {
+  f4 w0[FT], w1[FT];
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft) w0[ft] = pld4(wb, wlane, 16 * ft * LDW);
+#pragma unroll
+  for (int kb = 0; kb < NKB; kb += 2) {
+    if (kb + 1 < NKB) {
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) w1[ft] = pld4(wb, wlane, 16 * ft * LDW + 16 * (kb + 1));
+    }
+    {
+      f4 b[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) b[rt] = lds_f4(in + 16 * rt * LDI + 16 * kb);
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          out[ft][rt] = mfma16(w0[ft].x, b[rt].x, out[ft][rt]);
+          out[ft][rt] = mfma16(w0[ft].y, b[rt].y, out[ft][rt]);
+          out[ft][rt] = mfma16(w0[ft].z, b[rt].z, out[ft][rt]);
+          out[ft][rt] = mfma16(w0[ft].w, b[rt].w, out[ft][rt]);
+        }
+    }
+    if (kb + 1 < NKB) {
+      if (kb + 2 < NKB) {
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft) w0[ft] = pld4(wb, wlane, 16 * ft * LDW + 16 * (kb + 2));
+      }
+      f4 b[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) b[rt] = lds_f4(in + 16 * rt * LDI + 16 * (kb + 1));
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          out[ft][rt] = mfma16(w1[ft].x, b[rt].x, out[ft][rt]);
+          out[ft][rt] = mfma16(w1[ft].y, b[rt].y, out[ft][rt]);
+          out[ft][rt] = mfma16(w1[ft].z, b[rt].z, out[ft][rt]);
+          out[ft][rt] = mfma16(w1[ft].w, b[rt].w, out[ft][rt]);
+        }
+    }
+  }
+}
+
+// bias init: out[ft][rt] = b[fbase + 16 ft + 4 g + r]
+template <int FT, int RT>
+PPO_DEV void init_bias(f4 (&out)[FT][RT], PBuf pb, int boff_lane) {
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft) {
+    const f4 bv = pld4(pb, boff_lane, 16 * ft);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) out[ft][rt] = bv;
+  }
+}
+template <int FT, int RT>
+PPO_DEV void zero(f4 (&out)[FT][RT]) {
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) out[ft][rt] = f4{0.f, 0.f, 0.f, 0.f};
+}
+
+// per-row sums over all H features of (row tile rt, lane's row j): in-lane over the wave's
+// FT x 4 features, then the 4 lane groups, then (WF > 1) the WF feature-group waves via LDS.
+// red: a [WF][R] LDS slot. Must be called by every thread (contains a barrier when WF > 1).
+template <int WF, int RT, int R>
+PPO_DEV void rows_total(float (&s)[RT], float* red, int wf, int rbase, int j, int g) {
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) s[rt] = row_allreduce(s[rt]);
+  if constexpr (WF > 1) {
+    if (g == 0) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) red[wf * R + rbase + 16 * rt + j] = s[rt];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WF; ++w) t += red[w * R + rbase + 16 * rt + j];
+      s[rt] = t;
+    }
+  }
+}
+// two row sums at once (one barrier)
+template <int WF, int RT, int R>
+PPO_DEV void rows_total2(float (&s)[RT], float (&q)[RT], float* red0, float* red1, int wf, int rbase, int j, int g) {
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    s[rt] = row_allreduce(s[rt]);
+    q[rt] = row_allreduce(q[rt]);
+  }
+  if constexpr (WF > 1) {
+    if (g == 0) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        red0[wf * R + rbase + 16 * rt + j] = s[rt];
+        red1[wf * R + rbase + 16 * rt + j] = q[rt];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float t = 0.f, u = 0.f;
+#pragma unroll
+      for (int w = 0; w < WF; ++w) {
+        t += red0[w * R + rbase + 16 * rt + j];
+        u += red1[w * R + rbase + 16 * rt + j];
+      }
+      s[rt] = t;
+      q[rt] = u;
+    }
+  }
+}
+
+// LayerNorm statistics of z (two-pass, eps 1e-5, biased variance as torch::layer_norm)
+template <int FT, int RT, int WF, int R, int H>
+PPO_DEV void ln_rows(const f4 (&z)[FT][RT], float (&mu)[RT], float (&rs)[RT], float* red0, float* red1, int wf,
+                     int rbase, int j, int g) {
+  constexpr float invH = 1.0f / H;
+  float s[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    float t = 0.f;
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) t += (z[ft][rt].x + z[ft][rt].y) + (z[ft][rt].z + z[ft][rt].w);
+    s[rt] = t;
+  }
+  rows_total<WF, RT, R>(s, red0, wf, rbase, j, g);
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    mu[rt] = s[rt] * invH;
+    float t = 0.f;
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = z[ft][rt][r] - mu[rt];
+        t += d * d;
+      }
+    s[rt] = t;
+  }
+  rows_total<WF, RT, R>(s, red1, wf, rbase, j, g);
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) rs[rt] = 1.0f / sqrtf(s[rt] * invH + 1e-5f);
+}
+
+// column sums over this wave's rows of v(ft, rt, r), added to acc[fbase + feature]:
+// sum over rt in lane, then a 16-lane reduce-scatter (lane j ends with slot j).
+template <int FT, int RT, typename Fn>
+PPO_DEV void col_sums(Fn v, float* acc, int fbase, int j, int g) {
+  static_assert(FT == 4, "col_sums assumes 16 slots per lane");
+  float x[16];
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float t = v(ft, 0, r);
+#pragma unroll
+      for (int rt = 1; rt < RT; ++rt) t += v(ft, rt, r);
+      x[4 * ft + r] = t;
+    }
+#pragma unroll
+  for (int m = 8, len = 16; m >= 1; m >>= 1, len >>= 1) {
+    const bool bit = (j & m) != 0;
+#pragma unroll
+    for (int i = 0; i < len / 2; ++i) {
+      const float lo = x[i], hi = x[i + len / 2];
+      const float keep = bit ? hi : lo, send = bit ? lo : hi;
+      x[i] = keep + shfl_xor(send, m);
+    }
+  }
+  // slot j <-> feature 16 (j >> 2) + 4 g + (j & 3)
+  acc[fbase + 16 * (j >> 2) + 4 * g + (j & 3)] += x[0];
+}
+
+template <int FT, int RT>
+PPO_DEV void store_tile_rows(float* __restrict__ dst, int ld, const f4 (&v)[FT][RT], int m0, int M, int rbase,
+                             int fbase, int j, int g) {
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int m = m0 + rbase + 16 * rt + j;
+    if (m < M) {
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) st4(dst + (size_t)m * ld + fbase + 16 * ft + 4 * g, v[ft][rt]);
+    }
+  }
+}
+template <int FT, int RT, int LDA>
+PPO_DEV void lds_store_tile(float* act, const f4 (&v)[FT][RT], int rbase, int fbase, int j, int g) {
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) lds_st4(act + (rbase + 16 * rt + j) * LDA + fbase + 16 * ft + 4 * g, v[ft][rt]);
+}
+
+// packed offset of head h's weight row / bias, -1 if h is padding
+PPO_DEV int head_row(const PackedLayout& K, int trunk, int h, int H) {
+  if (trunk == 0) return h == 0 ? K.cW3 : -1;
+  if (K.kind == PPO_NET_LN_BETA) {
+    if (h < K.A) return K.aW3 + h * H;
+    if (h < 2 * K.A) return K.bW3 + (h - K.A) * H;
+    return -1;
+  }
+  return h < K.A ? K.aW3 + h * H : -1;
+}
+PPO_DEV int head_bias(const PackedLayout& K, int trunk, int h) {
+  if (trunk == 0) return K.cb3;
+  if (K.kind == PPO_NET_LN_BETA) return h < K.A ? K.ab3 + h : K.bb3 + (h - K.A);
+  return K.ab3 + h;
+}
+
+}  // namespace
+
+template <int H, int KIND, int NTO, int NHT>
+__global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
+  using GE = Geo<H, NTO, NHT>;
+  constexpr int FT = GE::FT, RT = GE::RT, WF = GE::WF, R = GE::R, NT = GE::NT, OP = GE::OP;
+  constexpr int LDX = GE::LDX, LDA = GE::LDA, LDG = GE::LDG, NHP = GE::NHP, ITS = GE::ITS;
+  constexpr bool LN = KIND == PPO_NET_LN_BETA;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* XN = lds + GE::oXN;
+  float* ACT = lds + GE::oACT;
+  float* RED = lds + GE::oRED;
+  float* PRE = lds + GE::oPRE;
+  float* GG = lds + GE::oG;
+  float* ROWS = lds + GE::oROW;
+  float* SCR = lds + GE::oSCR;   // head partials, then per-item scratch
+  float* ACTN = lds + a.actn_off;  // R x A stored actions
+  float* ACC = lds + a.acc_off;    // WR x sg.size accumulators
+  float* RED0 = RED;
+  float* RED1 = RED + WF * R;
+  float* RED2 = RED + 2 * WF * R;
+  float* RED3 = RED + 3 * WF * R;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int wf = wave % WF, wr = wave / WF;
+  const int fbase = wf * FT * 16, rbase = wr * RT * 16;
+  const int trunk = blockIdx.y;
+  const PackedLayout& K = a.K;
+  const TrunkDev& T = K.tr[trunk];
+  const float* __restrict__ P = a.P;
+  const PBuf pb = make_pbuf(P, K.size);
+  const PBuf w2t = make_pbuf(a.W2T[trunk], H * H);
+  const SmallGradLayout sg = a.sg[trunk];
+  const int O = K.O, A = K.A, nh = sg.nh;
+  const float c = a.clip_coef;
+  const float adv_mean = a.adv_stats[0], adv_std = a.adv_stats[1];
+  float* acc = ACC + wr * sg.size;
+  for (int i = tid; i < GE::WR * sg.size; i += 256) ACC[i] = 0.f;
+  for (int i = tid; i < R * LDG; i += 256) GG[i] = 0.f;  // padding heads stay exactly 0
+
+  // per-lane A-operand offsets
+  const int w1lane = T.W1 + (fbase + j) * OP + 4 * g;
+  const int w2lane = T.W2 + (fbase + j) * H + 4 * g;
+  const int w2tlane = (fbase + j) * H + 4 * g;
+  const float* xn_in = XN + (rbase + j) * LDX + 4 * g;
+  const float* act_in = ACT + (rbase + j) * LDA + 4 * g;
+  // head rows for the forward (A = W3[16 ht + i][..]) and the backward (A = W3^T: heads 16 ht + 4 g + r)
+  int hrow_f[NHT], hrow_b[NHT][4];
+#pragma unroll
+  for (int ht = 0; ht < NHT; ++ht) {
+    hrow_f[ht] = head_row(K, trunk, 16 * ht + j, H);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) hrow_b[ht][r] = head_row(K, trunk, 16 * ht + 4 * g + r, H);
+  }
+  const int ntiles = (a.M + R - 1) / R;
+
+  for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
+    const int m0 = it * R;
+    __syncthreads();  // the previous iteration's LDS readers are done
+    // ---------------- gather (minibatch rows through the permutation) ----------------
+    for (int idx = tid; idx < R * OP; idx += 256) {
+      const int row = idx / OP, f = idx - row * OP;
+      const int m = m0 + row;
+      float v = 0.f;
+      if (m < a.M && f < O) {
+        const long b = a.perm[m];
+        v = a.obs[b * O + f];
+        if constexpr (LN) v = (v - P[K.omean + f]) / P[K.ostd + f];
+      }
+      XN[row * LDX + f] = v;
+      if (trunk == 0 && m < a.M) a.Xn[(size_t)m * OP + f] = v;
+    }
+    if (tid < R) {
+      const int m = m0 + tid;
+      float r1 = 0.f, r2 = 0.f;
+      if (m < a.M) {
+        const long b = a.perm[m];
+        if (trunk == 0) { r1 = a.ret[b]; r2 = a.val[b]; }
+        else { r1 = a.logp[b]; r2 = a.adv[b]; }
+      }
+      ROWS[tid * 8 + 1] = r1;
+      ROWS[tid * 8 + 2] = r2;
+    }
+    if (trunk == 1) {
+      for (int idx = tid; idx < R * A; idx += 256) {
+        const int row = idx / A, ai = idx - row * A;
+        const int m = m0 + row;
+        ACTN[idx] = m < a.M ? a.actions[(long)a.perm[m] * A + ai] : 0.f;
+      }
+    }
+    __syncthreads();
+
+    // ---------------- layer 1 ----------------
+    f4 z[FT][RT];
+    init_bias<FT, RT>(z, pb, T.b1 + fbase + 4 * g);
+    mm_fr<FT, RT, NTO, OP, LDX>(z, pb, w1lane, xn_in);
+    float mu1[RT], rs1[RT];
+    if constexpr (LN) {
+      ln_rows<FT, RT, WF, R, H>(z, mu1, rs1, RED0, RED1, wf, rbase, j, g);
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+        const f4 gm = pld4(pb, T.g1 + fbase + 4 * g, 16 * ft), bt = pld4(pb, T.be1 + fbase + 4 * g, 16 * ft);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float xh = (z[ft][rt][r] - mu1[rt]) * rs1[rt];
+            const float y = __fmaf_rn(gm[r], xh, bt[r]);
+            z[ft][rt][r] = y > 0.0f ? y : 0.0f;
+          }
+      }
+    } else {
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z[ft][rt][r] = tanhf(z[ft][rt][r]);
+    }
+    store_tile_rows<FT, RT>(a.H1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
+    lds_store_tile<FT, RT, LDA>(ACT, z, rbase, fbase, j, g);
+    __syncthreads();
+
+    // ---------------- layer 2 ----------------
+    f4 x2[FT][RT];  // LN: x_hat2; tanh: h2
+    init_bias<FT, RT>(x2, pb, T.b2 + fbase + 4 * g);
+    mm_fr<FT, RT, NT, H, LDA>(x2, pb, w2lane, act_in);
+    float rs2[RT];
+    if constexpr (LN) {
+      float mu2[RT];
+      ln_rows<FT, RT, WF, R, H>(x2, mu2, rs2, RED2, RED3, wf, rbase, j, g);
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) x2[ft][rt] = (x2[ft][rt] - mu2[rt]) * rs2[rt];
+    } else {
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x2[ft][rt][r] = tanhf(x2[ft][rt][r]);
+    }
+    auto h2_of = [&](int ft, int rt) -> f4 {
+      if constexpr (LN) {
+        const f4 gm = pld4(pb, T.g2 + fbase + 4 * g, 16 * ft), bt = pld4(pb, T.be2 + fbase + 4 * g, 16 * ft);
+        f4 y;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = __fmaf_rn(gm[r], x2[ft][rt][r], bt[r]);
+          y[r] = v > 0.0f ? v : 0.0f;
+        }
+        return y;
+      } else {
+        return x2[ft][rt];
+      }
+    };
+    // ---------------- heads (split-K over this wave's features) ----------------
+    f4 hp[NHT][RT];
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) hp[ht][rt] = f4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();  // every wave is done reading h1 from ACT
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      f4 wv[NHT];
+#pragma unroll
+      for (int ht = 0; ht < NHT; ++ht) {
+        wv[ht] = hrow_f[ht] >= 0 ? pld4(pb, hrow_f[ht] + fbase + 4 * g, 16 * ft) : f4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const f4 h2 = h2_of(ft, rt);
+        lds_st4(ACT + (rbase + 16 * rt + j) * LDA + fbase + 16 * ft + 4 * g, h2);
+#pragma unroll
+        for (int ht = 0; ht < NHT; ++ht) {
+          hp[ht][rt] = mfma16(wv[ht].x, h2.x, hp[ht][rt]);
+          hp[ht][rt] = mfma16(wv[ht].y, h2.y, hp[ht][rt]);
+          hp[ht][rt] = mfma16(wv[ht].z, h2.z, hp[ht][rt]);
+          hp[ht][rt] = mfma16(wv[ht].w, h2.w, hp[ht][rt]);
+        }
+      }
+    }
+    // partial head sums -> SCR[wf][head][row]
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) SCR[(wf * NHP + 16 * ht + 4 * g + r) * R + rbase + 16 * rt + j] = hp[ht][rt][r];
+    __syncthreads();
+    for (int idx = tid; idx < R * nh; idx += 256) {
+      const int row = idx / nh, h = idx - row * nh;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WF; ++w) s += SCR[(w * NHP + h) * R + row];
+      PRE[row * LDG + h] = s + P[head_bias(K, trunk, h)];
+    }
+    __syncthreads();
+
+    // ---------------- loss and its gradient wrt the head pre-activations ----------------
+    float* ITM = SCR;  // R x A x ITS (head partials are consumed)
+    float st_a = 0.f, st_b = 0.f, st_c = 0.f, st_d = 0.f, st_e = 0.f, st_f = 0.f;  // per-row stats (tid < R)
+    if (trunk == 0) {
+      if (tid < R) {
+        const bool valid = m0 + tid < a.M;
+        const float v = PRE[tid * LDG];
+        const float rt_ = ROWS[tid * 8 + 1], ov = ROWS[tid * 8 + 2];
+        float gv, sv;
+        if (a.clip_vloss) {
+          const float vu = (v - rt_) * (v - rt_);
+          const float dv = v - ov;
+          const float vcl = ov + fminf(fmaxf(dv, -c), c);
+          const float vc = (vcl - rt_) * (vcl - rt_);
+          sv = fmaxf(vu, vc);
+          const float w1 = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
+          const float inr = (dv >= -c && dv <= c) ? 1.0f : 0.0f;
+          gv = 0.5f * a.vf_coef * a.inv_m * (w1 * 2.0f * (v - rt_) + (1.0f - w1) * 2.0f * (vcl - rt_) * inr);
+        } else {
+          sv = (v - rt_) * (v - rt_);
+          gv = 0.5f * a.vf_coef * a.inv_m * 2.0f * (v - rt_);
+        }
+        if (!valid) { gv = 0.f; sv = 0.f; }
+        GG[tid * LDG] = gv;
+        st_b = sv;
+      }
+    } else {
+      // pass 1: per (row, action) log-prob / entropy terms and derivative pieces
+      for (int idx = tid; idx < R * A; idx += 256) {
+        const int row = idx / A, ai = idx - row * A;
+        const bool valid = m0 + row < a.M;
+        float* it_ = ITM + idx * ITS;
+        if constexpr (LN) {
+          const float hi = P[K.hi], lo = P[K.lo];
+          const float pa = PRE[row * LDG + ai], pbv = PRE[row * LDG + A + ai];
+          const float al = softplusf_(pa) + 1.0f, be = softplusf_(pbv) + 1.0f;
+          const float av = valid ? ACTN[idx] : 0.5f * (hi + lo);
+          float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+          s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
+          const float ab = al + be;
+          const float lga = lgammaf(al), lgb = lgammaf(be), lgab = lgammaf(ab);
+          const float psa = digammaf_(al), psb = digammaf_(be), psab = digammaf_(ab);
+          it_[0] = xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
+          it_[1] = (lga + lgb) - lgab - (2.0f - ab) * psab - ((al - 1.0f) * psa + (be - 1.0f) * psb);
+          const float tab = trigammaf_(ab);
+          it_[2] = ((al - 1.0f) != 0.0f ? logf(s) : 0.0f) + psab - psa;            // d lp / d alpha
+          it_[3] = (ab - 2.0f) * tab - (al - 1.0f) * trigammaf_(al);                // d ent / d alpha
+          it_[4] = softplus_d(pa);
+          it_[5] = ((be - 1.0f) != 0.0f ? logf(1.0f - s) : 0.0f) + psab - psb;     // d lp / d beta
+          it_[6] = (ab - 2.0f) * tab - (be - 1.0f) * trigammaf_(be);                // d ent / d beta
+          it_[7] = softplus_d(pbv);
+        } else {
+          const float mu = PRE[row * LDG + ai];
+          const float sd = expf(P[K.logstd + ai]);
+          const float var = sd * sd, lsd = logf(sd);
+          const float act = valid ? ACTN[idx] : mu;
+          const float d = act - mu;
+          it_[0] = -(d * d) / (2.0f * var) - lsd - kLz;
+          it_[1] = kEntC + lsd;
+          it_[2] = d / var;
+          it_[3] = d * d / var - 1.0f;
+        }
+      }
+      __syncthreads();
+      // per row: log-prob / entropy sums, clipped surrogate, d loss / d logp, d loss / d ent
+      if (tid < R) {
+        const bool valid = m0 + tid < a.M;
+        float lp = 0.f, ent = 0.f;
+        for (int ai = 0; ai < A; ++ai) {
+          lp += ITM[(tid * A + ai) * ITS + 0];
+          ent += ITM[(tid * A + ai) * ITS + 1];
+        }
+        const float oldlp = valid ? ROWS[tid * 8 + 1] : lp;
+        const float logratio = lp - oldlp;
+        const float ratio = expf(logratio);
+        float an = valid ? ROWS[tid * 8 + 2] : 0.f;
+        if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
+        const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
+        const float pg1 = -an * ratio, pg2 = -an * rc;
+        const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+        const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
+        float g_logp = a.inv_m * (w1 * (-an) + (1.0f - w1) * (-an) * inr) * ratio;
+        float g_ent = -a.ent_coef * a.inv_m;
+        st_a = fmaxf(pg1, pg2);
+        st_c = ent;
+        st_d = -logratio;
+        st_e = (ratio - 1.0f) - logratio;
+        st_f = fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
+        if (!valid) { g_logp = 0.f; g_ent = 0.f; st_a = st_c = st_d = st_e = st_f = 0.f; }
+        ROWS[tid * 8 + 3] = g_logp;
+        ROWS[tid * 8 + 4] = g_ent;
+      }
+      __syncthreads();
+      // pass 2: head gradients
+      for (int idx = tid; idx < R * A; idx += 256) {
+        const int row = idx / A, ai = idx - row * A;
+        const float g_logp = ROWS[row * 8 + 3], g_ent = ROWS[row * 8 + 4];
+        float* it_ = ITM + idx * ITS;
+        if constexpr (LN) {
+          GG[row * LDG + ai] = (g_logp * it_[2] + g_ent * it_[3]) * it_[4];
+          GG[row * LDG + A + ai] = (g_logp * it_[5] + g_ent * it_[6]) * it_[7];
+        } else {
+          GG[row * LDG + ai] = g_logp * it_[2];
+          it_[4] = g_logp * it_[3] + g_ent;  // d loss / d logstd (per row)
+        }
+      }
+    }
+    // loss statistics: rows live in wave 0 (R <= 64)
+    if (wave == 0) {
+      float s0 = st_a, s1 = st_b, s2 = st_c, s3 = st_d, s4 = st_e, s5 = st_f;
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) {
+        s0 += shfl_xor(s0, m); s1 += shfl_xor(s1, m); s2 += shfl_xor(s2, m);
+        s3 += shfl_xor(s3, m); s4 += shfl_xor(s4, m); s5 += shfl_xor(s5, m);
+      }
+      if (lane == 0) {
+        float* st = ACC + sg.stats;  // row group 0's accumulator
+        st[ST_PG] += s0; st[ST_V] += s1; st[ST_ENT] += s2; st[ST_OKL] += s3; st[ST_KL] += s4; st[ST_CF] += s5;
+      }
+    }
+    __syncthreads();
+    // head bias (and logstd) gradients: fixed-order sums over the workgroup's rows
+    if (tid < nh) {
+      float s = 0.f;
+      for (int row = 0; row < R; ++row) s += GG[row * LDG + tid];
+      ACC[sg.hb + tid] += s;
+    }
+    if (!LN && trunk == 1 && tid >= 64 && tid < 64 + A) {
+      const int ai = tid - 64;
+      float s = 0.f;
+      for (int row = 0; row < R; ++row) s += ITM[(row * A + ai) * ITS + 4];
+      ACC[sg.ls + ai] += s;
+    }
+
+    // ---------------- head backward: dh2 = W3^T G^T, dW3 += G^T h2 ----------------
+    f4 dh[FT][RT];
+    zero<FT, RT>(dh);
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht) {
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+        f4 wT;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          wT[r] = hrow_b[ht][r] >= 0 ? bld1(pb, hrow_b[ht][r] + fbase + j, 16 * ft) : 0.0f;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const f4 gv = lds_f4(GG + (rbase + 16 * rt + j) * LDG + 16 * ht + 4 * g);
+          dh[ft][rt] = mfma16(wT.x, gv.x, dh[ft][rt]);
+          dh[ft][rt] = mfma16(wT.y, gv.y, dh[ft][rt]);
+          dh[ft][rt] = mfma16(wT.z, gv.z, dh[ft][rt]);
+          dh[ft][rt] = mfma16(wT.w, gv.w, dh[ft][rt]);
+        }
+        // dW3 tile (heads 16 ht.., features fbase + 16 ft ..): contract over this wave's rows
+        f4 d3 = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = rbase + 16 * rt + 4 * g + r;
+            d3 = mfma16(lds_f(GG + row * LDG + 16 * ht + j), lds_f(ACT + row * LDA + fbase + 16 * ft + j), d3);
+          }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = 16 * ht + 4 * g + r;
+          if (h < nh) acc[sg.hW + h * H + fbase + 16 * ft + j] += d3[r];
+        }
+      }
+    }
+
+    // ---------------- layer-2 backward: dz2 ----------------
+    if constexpr (LN) {
+      float s1[RT], s2[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) { s1[rt] = 0.f; s2[rt] = 0.f; }
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+        const f4 gm = pld4(pb, T.g2 + fbase + 4 * g, 16 * ft), bt = pld4(pb, T.be2 + fbase + 4 * g, 16 * ft);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float y = __fmaf_rn(gm[r], x2[ft][rt][r], bt[r]);
+            const float dy = y > 0.0f ? dh[ft][rt][r] : 0.0f;
+            dh[ft][rt][r] = dy;
+            const float dx = dy * gm[r];
+            s1[rt] += dx;
+            s2[rt] += dx * x2[ft][rt][r];
+          }
+      }
+      rows_total2<WF, RT, R>(s1, s2, RED0, RED1, wf, rbase, j, g);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) { s1[rt] *= (1.0f / H); s2[rt] *= (1.0f / H); }
+      col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r]; }, acc + sg.be2, fbase, j, g);
+      col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r] * x2[ft][rt][r]; }, acc + sg.g2, fbase, j, g);
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+        const f4 gm = pld4(pb, T.g2 + fbase + 4 * g, 16 * ft);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) x2[ft][rt] = rs2[rt] * (dh[ft][rt] * gm - s1[rt] - x2[ft][rt] * s2[rt]);
+      }
+    } else {
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) x2[ft][rt] = dh[ft][rt] * (1.0f - x2[ft][rt] * x2[ft][rt]);
+    }
+    // x2 = dz2
+    col_sums<FT, RT>([&](int ft, int rt, int r) { return x2[ft][rt][r]; }, acc + sg.b2, fbase, j, g);
+    store_tile_rows<FT, RT>(a.DZ2[trunk], H, x2, m0, a.M, rbase, fbase, j, g);
+    __syncthreads();  // dW3 readers of h2 are done
+    lds_store_tile<FT, RT, LDA>(ACT, x2, rbase, fbase, j, g);
+    __syncthreads();
+
+    // ---------------- dh1 = W2^T dz2 ----------------
+    zero<FT, RT>(dh);
+    mm_fr<FT, RT, NT, H, LDA>(dh, w2t, w2tlane, act_in);
+    // ---------------- recompute layer 1, layer-1 backward ----------------
+    init_bias<FT, RT>(z, pb, T.b1 + fbase + 4 * g);
+    mm_fr<FT, RT, NTO, OP, LDX>(z, pb, w1lane, xn_in);
+    if constexpr (LN) {
+      float s1[RT], s2[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) { s1[rt] = 0.f; s2[rt] = 0.f; }
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+        const f4 gm = pld4(pb, T.g1 + fbase + 4 * g, 16 * ft), bt = pld4(pb, T.be1 + fbase + 4 * g, 16 * ft);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float xh = (z[ft][rt][r] - mu1[rt]) * rs1[rt];
+            z[ft][rt][r] = xh;
+            const float y = __fmaf_rn(gm[r], xh, bt[r]);
+            const float dy = y > 0.0f ? dh[ft][rt][r] : 0.0f;
+            dh[ft][rt][r] = dy;
+            const float dx = dy * gm[r];
+            s1[rt] += dx;
+            s2[rt] += dx * xh;
+          }
+      }
+      rows_total2<WF, RT, R>(s1, s2, RED2, RED3, wf, rbase, j, g);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) { s1[rt] *= (1.0f / H); s2[rt] *= (1.0f / H); }
+      col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r]; }, acc + sg.be1, fbase, j, g);
+      col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r] * z[ft][rt][r]; }, acc + sg.g1, fbase, j, g);
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+        const f4 gm = pld4(pb, T.g1 + fbase + 4 * g, 16 * ft);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) z[ft][rt] = rs1[rt] * (dh[ft][rt] * gm - s1[rt] - z[ft][rt] * s2[rt]);
+      }
+    } else {
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float h1 = tanhf(z[ft][rt][r]);
+            z[ft][rt][r] = dh[ft][rt][r] * (1.0f - h1 * h1);
+          }
+    }
+    // z = dz1
+    col_sums<FT, RT>([&](int ft, int rt, int r) { return z[ft][rt][r]; }, acc + sg.b1, fbase, j, g);
+    store_tile_rows<FT, RT>(a.DZ1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
+  }
+  // ---------------- workgroup result (row groups summed in a fixed order) ----------------
+  __syncthreads();
+  float* out = a.slab[trunk] + (size_t)blockIdx.x * sg.size;
+  for (int i = tid; i < sg.size; i += 256) {
+    float s = ACC[i];
+#pragma unroll
+    for (int w = 1; w < GE::WR; ++w) s += ACC[w * sg.size + i];
+    out[i] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side: geometry, LDS size, dispatch
+// ---------------------------------------------------------------------------------------------
+template <int H, int NTO, int NHT>
+static void upd_geo(const PackedLayout& K, int sg_size, UpdGeoOut* g) {
+  using GE = Geo<H, NTO, NHT>;
+  const int scr = std::max(GE::WF * GE::NHP * GE::R, GE::R * K.A * GE::ITS);
+  int off = GE::oSCR + scr;
+  g->actn_off = off;
+  off += GE::R * K.A;
+  off = (off + 3) & ~3;
+  g->acc_off = off;
+  off += GE::WR * sg_size;
+  g->lds_bytes = (size_t)off * sizeof(float);
+  g->rows = GE::R;
+}
+
+template <typename F>
+static int dispatch_upd(const PackedLayout& K, int nh, F&& f) {
+  const int nto = K.OP / 16, nht = (nh + 15) / 16;
+#define PPO_UPD_CASE(H_, KIND_, NTO_, NHT_)                                                                   \
+  if (K.H == H_ && K.kind == KIND_ && nto == NTO_ && nht == NHT_)                                             \
+    return f(std::integral_constant<int, H_>{}, std::integral_constant<int, KIND_>{},                        \
+             std::integral_constant<int, NTO_>{}, std::integral_constant<int, NHT_>{});
+  PPO_UPD_CASE(256, PPO_NET_LN_BETA, 1, 1) PPO_UPD_CASE(256, PPO_NET_LN_BETA, 2, 1)
+  PPO_UPD_CASE(256, PPO_NET_LN_BETA, 7, 1) PPO_UPD_CASE(256, PPO_NET_LN_BETA, 24, 3)
+  PPO_UPD_CASE(256, PPO_NET_LN_BETA, 2, 3) PPO_UPD_CASE(256, PPO_NET_TANH_NORMAL, 2, 1)
+#undef PPO_UPD_CASE
+  return -1;
+}
+
+int upd_supported(const PackedLayout& K, int nh_actor, int sg_size, UpdGeoOut* g) {
+  // both trunks run in one launch: the geometry must cover the actor's head count (critic: 1)
+  return dispatch_upd(K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_) {
+    (void)KIND_;
+    upd_geo<decltype(H_)::value, decltype(NTO_)::value, decltype(NHT_)::value>(K, sg_size, g);
+    const auto k = k_upd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value, decltype(NHT_)::value>;
+    return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) ==
+                   hipSuccess
+               ? 0
+               : -2;
+  });
+}
+
+int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s) {
+  return dispatch_upd(a.K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_) {
+    hipLaunchKernelGGL((k_upd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value,
+                              decltype(NHT_)::value>),
+                       dim3(nblocks, 2), dim3(256), lds_bytes, s, a);
+    return 0;
+  });
+}

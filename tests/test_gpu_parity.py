@@ -362,3 +362,41 @@ def test_metric_config_iteration_properties_and_determinism():
         assert np.isfinite(s0[k]), k
     assert 0.0 <= s0["clipfrac"] <= 1.0
     assert s0["grad_norm"] > 0
+
+
+@pytest.mark.parametrize("kind,O_,A,H", [(1, 17, 6, 256), (0, 17, 6, 256)])
+def test_update_kernels_agree(kind, O_, A, H, monkeypatch):
+    """The feature-split k_upd and the wave-per-16-rows k_fwdbwd compute the same minibatch
+    gradient (different summation orders only) at a size where every workgroup loops several
+    times (M = 12 800 rows, ragged last tile)."""
+    rng = np.random.default_rng(5)
+    L = O.layout_init(kind, O_, A, H)
+    p = random_params(L, rng)
+    if kind == 0:
+        p[L.logstd:L.logstd + A] = -0.5
+    E, T = 1600, 8
+    B = T * E
+    x = rng.standard_normal((B, O_)).astype(np.float32)
+    act = (rng.uniform(-0.95, 0.95, (B, A)) if kind else rng.standard_normal((B, A))).astype(np.float32)
+    _, lp0, _, v0 = O.get_action_and_value(L, p, x[:256], 1, act[:256])
+    olp = (np.resize(lp0, B) + rng.standard_normal(B) * 0.1).astype(np.float32)
+    ov = (np.resize(v0, B) + rng.standard_normal(B) * 0.1).astype(np.float32)
+    adv = rng.standard_normal(B).astype(np.float32)
+    ret = rng.standard_normal(B).astype(np.float32)
+    perm = rng.permutation(B).astype(np.int32)
+    grads, stats = [], []
+    for env in ("0", "1"):
+        monkeypatch.setenv("PPO_UPD_KERNEL", env)
+        ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.1)
+        ag.load_params(p)
+        fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
+        st = ag.update(2.5e-4, perms=DeviceArray.from_numpy(perm), want_stats=True)
+        grads.append(ag.last_grad())
+        stats.append([st[k] for k in ("pg_loss", "v_loss", "entropy", "approx_kl", "clipfrac", "grad_norm")])
+        ag.close()
+    assert rel(grads[1], grads[0]) < 2e-5
+    for t in range(L.ntensors):
+        o, n = L.t_off[t], L.t_len[t]
+        if L.t_grad[t]:
+            assert rel(grads[1][o:o + n], grads[0][o:o + n]) < 2e-4, t
+    np.testing.assert_allclose(stats[1], stats[0], rtol=2e-5, atol=1e-7)

@@ -17,6 +17,7 @@
 #include "ppo_kernels.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 // =============================================================================================
@@ -141,7 +142,8 @@ __global__ __launch_bounds__(256) void k_act2(ActArgs a) {
   constexpr int NT = H / 16, NTW = NT / 4;
   constexpr int ROWS = 16 * RG;
   constexpr int MAXNH = 40;
-  __shared__ __attribute__((aligned(16))) float hbuf[ROWS * H];
+  constexpr int LDH = H + 4;  // row stride = 4 mod 64 banks: conflict-free ds_read_b128 B operands
+  __shared__ __attribute__((aligned(16))) float hbuf[ROWS * LDH];
   __shared__ float red[4][ROWS];
   __shared__ float headp[4][ROWS][MAXNH + 1];
   __shared__ float itm[ROWS][MAXNH / 2 + 1][2];
@@ -171,22 +173,38 @@ __global__ __launch_bounds__(256) void k_act2(ActArgs a) {
     for (int rg = 0; rg < RG; ++rg)
 #pragma unroll
       for (int u = 0; u < NTW; ++u) acc[rg][u] = pld4(pbuf, 4 * g, boff + 16 * (wave * NTW + u));
-    for (int t = 0; t < NTIN; ++t) {
-      f4 w[NTW];
+    // weight k-blocks prefetched two ahead (the L2 latency is otherwise exposed every k-block)
+    f4 w[3][NTW];
+    auto wload = [&](f4 (&dst)[NTW], int t) {
 #pragma unroll
-      for (int u = 0; u < NTW; ++u) w[u] = pld4(wb, (16 * (wave * NTW + u) + j) * ldw + 4 * g, 16 * t);
+      for (int u = 0; u < NTW; ++u) dst[u] = pld4(wb, (16 * (wave * NTW + u) + j) * ldw + 4 * g, 16 * t);
+    };
+    auto step = [&](const f4 (&wt)[NTW], int t) {
 #pragma unroll
       for (int rg = 0; rg < RG; ++rg) {
         const f4 b = bfrag(rg, t);
 #pragma unroll
         for (int u = 0; u < NTW; ++u) {
-          acc[rg][u] = mfma16(w[u].x, b.x, acc[rg][u]);
-          acc[rg][u] = mfma16(w[u].y, b.y, acc[rg][u]);
-          acc[rg][u] = mfma16(w[u].z, b.z, acc[rg][u]);
-          acc[rg][u] = mfma16(w[u].w, b.w, acc[rg][u]);
+          acc[rg][u] = mfma16(wt[u].x, b.x, acc[rg][u]);
+          acc[rg][u] = mfma16(wt[u].y, b.y, acc[rg][u]);
+          acc[rg][u] = mfma16(wt[u].z, b.z, acc[rg][u]);
+          acc[rg][u] = mfma16(wt[u].w, b.w, acc[rg][u]);
         }
       }
+    };
+    wload(w[0], 0);
+    if (NTIN > 1) wload(w[1], 1);
+    int t = 0;
+    for (; t + 3 <= NTIN; t += 3) {
+      if (t + 2 < NTIN) wload(w[2], t + 2);
+      step(w[0], t);
+      if (t + 3 < NTIN) wload(w[0], t + 3);
+      step(w[1], t + 1);
+      if (t + 4 < NTIN) wload(w[1], t + 4);
+      step(w[2], t + 2);
     }
+    if (t < NTIN) step(w[0], t);
+    if (t + 1 < NTIN) step(w[1], t + 1);
   };
   // LayerNorm (+ReLU) or tanh over the full H features of each row, own tiles in registers
   auto activate = [&](f4 (&acc)[RG][NTW], int gam, int bet) {
@@ -257,9 +275,9 @@ __global__ __launch_bounds__(256) void k_act2(ActArgs a) {
   for (int rg = 0; rg < RG; ++rg)
 #pragma unroll
     for (int u = 0; u < NTW; ++u)
-      *reinterpret_cast<f4*>(hbuf + (16 * rg + j) * H + 16 * (wave * NTW + u) + 4 * g) = acc[rg][u];
+      *reinterpret_cast<f4*>(hbuf + (16 * rg + j) * LDH + 16 * (wave * NTW + u) + 4 * g) = acc[rg][u];
   lds_barrier();
-  layer(acc, [&](int rg, int t) { return *reinterpret_cast<const f4*>(hbuf + (16 * rg + j) * H + 16 * t + 4 * g); },
+  layer(acc, [&](int rg, int t) { return *reinterpret_cast<const f4*>(hbuf + (16 * rg + j) * LDH + 16 * t + 4 * g); },
         NT, P + T.W2, H, T.b2);
   activate(acc, T.g2, T.be2);
   // ---- heads: partial dots over this wave's features, reduced over waves through LDS ----
@@ -1058,8 +1076,10 @@ __global__ __launch_bounds__(256) void k_synth_reset(SynthArgs a, int seed, floa
 }
 
 __global__ __launch_bounds__(256) void k_synth_step(SynthArgs a, int e0, int e1, const float* __restrict__ act,
-                                                    float lo, float hi, float* obs, float* reward, float* done) {
+                                                    float lo, float hi, float* __restrict__ obs,
+                                                    float* __restrict__ reward, float* __restrict__ done) {
 #pragma clang fp contract(off)
+  constexpr int MO = PSYN_MAXO;
   const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= e1) return;
   const int O = a.O, A = a.A;
@@ -1070,21 +1090,32 @@ __global__ __launch_bounds__(256) void k_synth_step(SynthArgs a, int e0, int e1,
     a.autoreset[e] = 0;
     return;
   }
-  float* q = a.q + (long)e * O;
-  const float* ar = act + (long)(e - e0) * A;
-  const float xb = q[0];
-  float q0 = q[0];
-  float nq_prev = 0.0f;
-  // q'_i depends on q_{i+1} (old) — walk i ascending keeping the old q_0 for the wrap-around
-  for (int i = 0; i < O; ++i) {
-    const float ai = fminf(fmaxf(ar[i % A], lo), hi);
-    const float qn = (i + 1 < O) ? q[i + 1] : q0;
-    const float nq = __fmaf_rn(0.9f, q[i], __fmaf_rn(0.1f, ai, (0.05f * qn)));
-    if (i > 0) q[i - 1] = nq_prev;
-    nq_prev = nq;
+  float* __restrict__ q = a.q + (long)e * O;
+  const float* __restrict__ ar = act + (long)(e - e0) * A;
+  float qv[MO];
+#pragma unroll
+  for (int i = 0; i < MO; ++i) qv[i] = i < O ? q[i] : 0.0f;
+  const float xb = qv[0];
+  float nq[MO];
+  // q'_i = 0.9 q_i + (0.1 a_(i mod A) + 0.05 q_(i+1 mod O))  (fmaf, no contraction: bit-exact)
+#pragma unroll
+  for (int i = 0; i < MO; ++i) {
+    if (i < O) {
+      const float qn = (i + 1 < O) ? qv[(i + 1) % MO] : qv[0];
+      const float ai = fminf(fmaxf(ar[i % A], lo), hi);
+      nq[i] = __fmaf_rn(0.9f, qv[i], __fmaf_rn(0.1f, ai, (0.05f * qn)));
+    } else {
+      nq[i] = 0.0f;
+    }
   }
-  q[O - 1] = nq_prev;
-  const float vel = ((q[0] - xb) / 0.05f);
+#pragma unroll
+  for (int i = 0; i < MO; ++i) {
+    if (i < O) {
+      q[i] = nq[i];
+      obs[(long)e * O + i] = nq[i];
+    }
+  }
+  const float vel = ((nq[0] - xb) / 0.05f);
   float ctrl = 0.0f;
   for (int k = 0; k < A; ++k) {
     const float ak = fminf(fmaxf(ar[k], lo), hi);
@@ -1094,7 +1125,6 @@ __global__ __launch_bounds__(256) void k_synth_step(SynthArgs a, int e0, int e1,
   const int t = a.t[e] + 1;
   a.t[e] = t;
   const bool tr = t >= 1000;
-  for (int i = 0; i < O; ++i) obs[(long)e * O + i] = q[i];
   reward[e] = r;
   done[e] = tr ? 1.0f : 0.0f;
   a.ep_ret[e] = (a.ep_ret[e] + r);
@@ -1128,9 +1158,15 @@ int launch_act(const ActArgs& a, hipStream_t s) {
   return dispatch_net(a.K, [&](auto H_, auto KIND_, auto NTO_) {
     constexpr int H = decltype(H_)::value, KIND = decltype(KIND_)::value, NTO = decltype(NTO_)::value;
     if (a.K.A > 20) return -1;
-    constexpr int RG = 2;  // 32 rows per workgroup
-    dim3 grid((a.n + 16 * RG - 1) / (16 * RG), a.need_actor ? 2 : 1);
-    hipLaunchKernelGGL((k_act2<H, KIND, NTO, RG>), grid, dim3(256), 0, s, a);
+    // 16 rows per workgroup unless that still leaves > 2 workgroups per CU (then 32)
+    static const int force_rg = [] { const char* e = getenv("PPO_ACT_RG"); return e ? atoi(e) : 0; }();
+    if (force_rg == 1 || (force_rg == 0 && (a.n + 15) / 16 <= 512)) {
+      dim3 grid((a.n + 15) / 16, a.need_actor ? 2 : 1);
+      hipLaunchKernelGGL((k_act2<H, KIND, NTO, 1>), grid, dim3(256), 0, s, a);
+    } else {
+      dim3 grid((a.n + 31) / 32, a.need_actor ? 2 : 1);
+      hipLaunchKernelGGL((k_act2<H, KIND, NTO, 2>), grid, dim3(256), 0, s, a);
+    }
     return 0;
   });
 }

@@ -54,6 +54,7 @@ struct UpdArgs {
 };
 
 // k_upd geometry (ppo_update.hip)
+#define PPO_UPD_MAXA 24
 struct UpdGeoOut {
   size_t lds_bytes;
   int actn_off, acc_off, rows;
@@ -121,6 +122,7 @@ struct AdvArgs {
   int M, nmb, world;
 };
 
+#define PSYN_MAXO 32  // device synthetic env: max observation width
 struct SynthArgs {
   int E, O, A;
   float* q;

@@ -134,7 +134,7 @@ PPO_DEV void rows_total(float (&s)[RT], float* red, int wf, int rbase, int j, in
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) red[wf * R + rbase + 16 * rt + j] = s[rt];
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       float t = 0.f;
@@ -160,7 +160,7 @@ PPO_DEV void rows_total2(float (&s)[RT], float (&q)[RT], float* red0, float* red
         red1[wf * R + rbase + 16 * rt + j] = q[rt];
       }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       float t = 0.f, u = 0.f;
@@ -328,24 +328,85 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
   }
   const int ntiles = (a.M + R - 1) / R;
 
-  for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
-    const int m0 = it * R;
-    __syncthreads();  // the previous iteration's LDS readers are done
-    // ---------------- gather (minibatch rows through the permutation) ----------------
+  // Gather prefetch, two stages one tile ahead: permutation indices at the top of a tile, the
+  // rows' data after its forward pass; committed to LDS at the top of the next tile.
+  // (register-staged only for narrow inputs; wide ones (O > 32) gather synchronously)
+  constexpr bool PREF = (R * OP + 255) / 256 <= 4;
+  constexpr int NG = PREF ? (R * OP + 255) / 256 : 1;   // gather items per thread
+  constexpr int NAI = PREF ? (R * PPO_UPD_MAXA + 255) / 256 : 1;  // action items per thread
+  int pg[NG], pra, pac[NAI];
+  float vg[NG], vr1 = 0.f, vr2 = 0.f, vac[NAI];
+  auto pref_idx = [&](int itn) {
+    const int mb = itn * R;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int idx = tid + 256 * k, row = idx / OP, f = idx - row * OP, m = mb + row;
+      pg[k] = (itn < ntiles && idx < R * OP && m < a.M && f < O) ? a.perm[m] : -1;
+    }
+    pra = (itn < ntiles && tid < R && mb + tid < a.M) ? a.perm[mb + tid] : -1;
+#pragma unroll
+    for (int k = 0; k < NAI; ++k) {
+      const int idx = tid + 256 * k, row = idx / (A > 0 ? A : 1), m = mb + row;
+      pac[k] = (trunk == 1 && itn < ntiles && idx < R * A && m < a.M) ? a.perm[m] : -1;
+    }
+  };
+  auto pref_data = [&](int itn) {
+    const int mb = itn * R;
+    (void)mb;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int idx = tid + 256 * k, row = idx / OP, f = idx - row * OP;
+      (void)row;
+      vg[k] = pg[k] >= 0 ? a.obs[(long)pg[k] * O + f] : 0.f;
+    }
+    if (pra >= 0) {
+      if (trunk == 0) { vr1 = a.ret[pra]; vr2 = a.val[pra]; }
+      else { vr1 = a.logp[pra]; vr2 = a.adv[pra]; }
+    } else {
+      vr1 = 0.f; vr2 = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NAI; ++k) {
+      const int idx = tid + 256 * k, ai = idx - (idx / (A > 0 ? A : 1)) * A;
+      vac[k] = pac[k] >= 0 ? a.actions[(long)pac[k] * A + ai] : 0.f;
+    }
+  };
+  auto commit = [&](int itc) {
+    const int mb = itc * R;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int idx = tid + 256 * k, row = idx / OP, f = idx - row * OP, m = mb + row;
+      if (idx < R * OP) {
+        float v = vg[k];
+        if (LN && pg[k] >= 0) v = (v - P[K.omean + f]) / P[K.ostd + f];
+        XN[row * LDX + f] = v;
+        if (trunk == 0 && m < a.M) a.Xn[(size_t)m * OP + f] = v;
+      }
+    }
+    if (tid < R) {
+      ROWS[tid * 8 + 1] = vr1;
+      ROWS[tid * 8 + 2] = vr2;
+    }
+#pragma unroll
+    for (int k = 0; k < NAI; ++k) {
+      const int idx = tid + 256 * k;
+      if (trunk == 1 && idx < R * A) ACTN[idx] = vac[k];
+    }
+  };
+  auto gather_sync = [&](int itc) {
+    const int mb = itc * R;
     for (int idx = tid; idx < R * OP; idx += 256) {
-      const int row = idx / OP, f = idx - row * OP;
-      const int m = m0 + row;
+      const int row = idx / OP, f = idx - row * OP, m = mb + row;
       float v = 0.f;
       if (m < a.M && f < O) {
-        const long b = a.perm[m];
-        v = a.obs[b * O + f];
+        v = a.obs[(long)a.perm[m] * O + f];
         if constexpr (LN) v = (v - P[K.omean + f]) / P[K.ostd + f];
       }
       XN[row * LDX + f] = v;
       if (trunk == 0 && m < a.M) a.Xn[(size_t)m * OP + f] = v;
     }
     if (tid < R) {
-      const int m = m0 + tid;
+      const int m = mb + tid;
       float r1 = 0.f, r2 = 0.f;
       if (m < a.M) {
         const long b = a.perm[m];
@@ -357,12 +418,26 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     }
     if (trunk == 1) {
       for (int idx = tid; idx < R * A; idx += 256) {
-        const int row = idx / A, ai = idx - row * A;
-        const int m = m0 + row;
+        const int row = idx / A, ai = idx - row * A, m = mb + row;
         ACTN[idx] = m < a.M ? a.actions[(long)a.perm[m] * A + ai] : 0.f;
       }
     }
-    __syncthreads();
+  };
+  if constexpr (PREF) {
+    pref_idx(blockIdx.x);
+    pref_data(blockIdx.x);
+  }
+
+  for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
+    const int m0 = it * R;
+    lds_barrier();  // the previous iteration's LDS readers are done
+    if constexpr (PREF) {
+      commit(it);
+      pref_idx(it + gridDim.x);
+    } else {
+      gather_sync(it);
+    }
+    lds_barrier();
 
     // ---------------- layer 1 ----------------
     f4 z[FT][RT];
@@ -393,12 +468,13 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     }
     store_tile_rows<FT, RT>(a.H1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
     lds_store_tile<FT, RT, LDA>(ACT, z, rbase, fbase, j, g);
-    __syncthreads();
+    lds_barrier();
 
     // ---------------- layer 2 ----------------
     f4 x2[FT][RT];  // LN: x_hat2; tanh: h2
     init_bias<FT, RT>(x2, pb, T.b2 + fbase + 4 * g);
     mm_fr<FT, RT, NT, H, LDA>(x2, pb, w2lane, act_in);
+    if constexpr (PREF) pref_data(it + gridDim.x);
     float rs2[RT];
     if constexpr (LN) {
       float mu2[RT];
@@ -435,7 +511,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     for (int ht = 0; ht < NHT; ++ht)
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) hp[ht][rt] = f4{0.f, 0.f, 0.f, 0.f};
-    __syncthreads();  // every wave is done reading h1 from ACT
+    lds_barrier();  // every wave is done reading h1 from ACT
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft) {
       f4 wv[NHT];
@@ -463,7 +539,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) SCR[(wf * NHP + 16 * ht + 4 * g + r) * R + rbase + 16 * rt + j] = hp[ht][rt][r];
-    __syncthreads();
+    lds_barrier();
     for (int idx = tid; idx < R * nh; idx += 256) {
       const int row = idx / nh, h = idx - row * nh;
       float s = 0.f;
@@ -471,7 +547,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       for (int w = 0; w < WF; ++w) s += SCR[(w * NHP + h) * R + row];
       PRE[row * LDG + h] = s + P[head_bias(K, trunk, h)];
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---------------- loss and its gradient wrt the head pre-activations ----------------
     float* ITM = SCR;  // R x A x ITS (head partials are consumed)
@@ -536,7 +612,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
           it_[3] = d * d / var - 1.0f;
         }
       }
-      __syncthreads();
+      lds_barrier();
       // per row: log-prob / entropy sums, clipped surrogate, d loss / d logp, d loss / d ent
       if (tid < R) {
         const bool valid = m0 + tid < a.M;
@@ -565,7 +641,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
         ROWS[tid * 8 + 3] = g_logp;
         ROWS[tid * 8 + 4] = g_ent;
       }
-      __syncthreads();
+      lds_barrier();
       // pass 2: head gradients
       for (int idx = tid; idx < R * A; idx += 256) {
         const int row = idx / A, ai = idx - row * A;
@@ -593,7 +669,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
         st[ST_PG] += s0; st[ST_V] += s1; st[ST_ENT] += s2; st[ST_OKL] += s3; st[ST_KL] += s4; st[ST_CF] += s5;
       }
     }
-    __syncthreads();
+    lds_barrier();
     // head bias (and logstd) gradients: fixed-order sums over the workgroup's rows
     if (tid < nh) {
       float s = 0.f;
@@ -683,9 +759,9 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     // x2 = dz2
     col_sums<FT, RT>([&](int ft, int rt, int r) { return x2[ft][rt][r]; }, acc + sg.b2, fbase, j, g);
     store_tile_rows<FT, RT>(a.DZ2[trunk], H, x2, m0, a.M, rbase, fbase, j, g);
-    __syncthreads();  // dW3 readers of h2 are done
+    lds_barrier();  // dW3 readers of h2 are done
     lds_store_tile<FT, RT, LDA>(ACT, x2, rbase, fbase, j, g);
-    __syncthreads();
+    lds_barrier();
 
     // ---------------- dh1 = W2^T dz2 ----------------
     zero<FT, RT>(dh);
@@ -741,7 +817,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     store_tile_rows<FT, RT>(a.DZ1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
   }
   // ---------------- workgroup result (row groups summed in a fixed order) ----------------
-  __syncthreads();
+  lds_barrier();
   float* out = a.slab[trunk] + (size_t)blockIdx.x * sg.size;
   for (int i = tid; i < sg.size; i += 256) {
     float s = ACC[i];

@@ -1,0 +1,459 @@
+// ppo_act.hip — k_act3: Agent::get_action_and_value / get_value + rollout stores for the 256-wide
+// agents (ac:212-249, :649-660; ppo:145-157, :387-400), latency-first.
+//
+// A rollout step is a single pass over E rows, so every launch starts with cold weights (the
+// per-XCD L2 is not kept across kernel boundaries): the time of one launch is one workgroup's
+// critical path of ~1 us memory round trips, not its MFMA work. The layout below removes the
+// serial round trips instead of adding parallel work:
+//  * 16 rows x 8 waves per workgroup; wave w owns output features [32 w, 32 w + 32) (2 MFMA tiles);
+//  * every small parameter the workgroup needs later (biases, LayerNorm affine, head weights and
+//    biases) is fetched at kernel start, in the same latency window as the inputs and W1, and
+//    parked in LDS;
+//  * the 256 x 256 layer streams its weight A-operands through an 8-deep register ring (8 of the
+//    16 k-blocks in flight), so the layer costs ~2 round trips instead of 16;
+//  * heads are MFMAs (split-K over the waves' features, partials reduced through LDS);
+//  * Beta sampling runs one (row, action, alpha|beta) item per thread, so the two Marsaglia-Tsang
+//    gamma draws and their lgamma/digamma chains run side by side.
+// The per-(row, action) arithmetic and the Philox counters are the ones of k_act / k_act2, so
+// samples are identical for any batching.
+#include "ppo_agent.hpp"
+#include "ppo_kernels.hpp"
+
+#include <cstdlib>
+
+namespace {
+
+constexpr int kActThreads = 512, kActWaves = 8;
+
+template <int NTO, int NHT, int RT>
+struct ActGeo {
+  static constexpr int kActRows = 16 * RT;
+  static constexpr int H = 256, OP = NTO * 16, NHP = 16 * NHT;
+  static constexpr int LDX = ((OP + 63) / 64) * 64 + 4;
+  static constexpr int LDH = H + 4;
+  static constexpr int LDP = NHP + 4;
+  static constexpr int NSP = 6 * H + NHP * H;  // staged params: b1 g1 be1 b2 g2 be2, head rows
+  static constexpr int oXS = 0;
+  static constexpr int oHB = oXS + kActRows * LDX;
+  static constexpr int oSP = oHB + kActRows * LDH;
+  static constexpr int oHBIAS = oSP + NSP;                    // NHP head biases
+  static constexpr int oRED = oHBIAS + NHP;                   // 2 x 8 x 16
+  static constexpr int oHP = oRED + 2 * kActWaves * kActRows;  // 8 x NHP x 16 head partials
+  static constexpr int oPRE = oHP + kActWaves * NHP * kActRows;  // 16 x LDP
+  static constexpr int total = oPRE + kActRows * LDP;
+  // distribution scratch reuses the input / hidden-activation region (dead after layer 2)
+  static constexpr int oITM = 0;                               // R x A x 2 x 4 (A <= 24)
+  static constexpr int oLP = oITM + kActRows * 24 * 2 * 4;    // R x A x 2
+  static_assert(oLP + kActRows * 24 * 2 <= oSP, "distribution scratch must fit in the XS/HB region");
+  // staged param vectors inside SP
+  static constexpr int sB1 = 0, sG1 = H, sBE1 = 2 * H, sB2 = 3 * H, sG2 = 4 * H, sBE2 = 5 * H, sW3 = 6 * H;
+};
+
+// one Linear layer for this wave's 2 output tiles x RT row tiles:
+// acc[u][rt] (+)= W[32 w + 16 u + i][:] . IN[16 rt + j][:], A-operands streamed through a PD-deep
+// register ring; bfrag(t, rt) = this lane's B f4 for k-block t of row tile rt
+template <int NKB, int PD, int LDW, int RT, typename BF>
+PPO_DEV void act_layer(f4 (&acc)[2][RT], PBuf wb, int wlane, BF bfrag) {
+  constexpr int D = PD < NKB ? PD : NKB;
+  f4 w[D][2];
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) w[p][u] = pld4(wb, wlane, 16 * u * LDW + 16 * p);
+  // keep the scheduler from sinking the ring loads towards their uses (it otherwise re-issues
+  // them two k-blocks ahead and waits vmcnt(0) every block)
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int t = 0; t < NKB; ++t) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const f4 b = bfrag(t, rt);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        acc[u][rt] = mfma16(w[t % D][u].x, b.x, acc[u][rt]);
+        acc[u][rt] = mfma16(w[t % D][u].y, b.y, acc[u][rt]);
+        acc[u][rt] = mfma16(w[t % D][u].z, b.z, acc[u][rt]);
+        acc[u][rt] = mfma16(w[t % D][u].w, b.w, acc[u][rt]);
+      }
+    }
+    if (t + D < NKB) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) w[t % D][u] = pld4(wb, wlane, 16 * u * LDW + 16 * (t + D));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// LayerNorm + ReLU (LN net) or tanh over the 256 features of each row; 8 waves exchange row sums
+template <int KIND, int RT>
+PPO_DEV void act_activate(f4 (&acc)[2][RT], const float* sp_g, const float* sp_b, float* red, int wave, int j, int g) {
+  constexpr int R = 16 * RT;
+  if constexpr (KIND == PPO_NET_LN_BETA) {
+    float mu[RT], rs[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float s = (acc[0][rt].x + acc[0][rt].y) + (acc[0][rt].z + acc[0][rt].w) +
+                ((acc[1][rt].x + acc[1][rt].y) + (acc[1][rt].z + acc[1][rt].w));
+      s = row_allreduce(s);
+      if (g == 0) red[wave * R + 16 * rt + j] = s;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < kActWaves; ++w) t += red[w * R + 16 * rt + j];
+      mu[rt] = t * (1.0f / 256);
+      float q = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = acc[u][rt][r] - mu[rt];
+          q += d * d;
+        }
+      q = row_allreduce(q);
+      if (g == 0) red[(kActWaves + wave) * R + 16 * rt + j] = q;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < kActWaves; ++w) v += red[(kActWaves + w) * R + 16 * rt + j];
+      rs[rt] = 1.0f / sqrtf(v * (1.0f / 256) + 1e-5f);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int f = 32 * wave + 16 * u + 4 * g;
+      const f4 gm = *reinterpret_cast<const f4*>(sp_g + f), bt = *reinterpret_cast<const f4*>(sp_b + f);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float y = __fmaf_rn(gm[r], (acc[u][rt][r] - mu[rt]) * rs[rt], bt[r]);
+          acc[u][rt][r] = y > 0.0f ? y : 0.0f;
+        }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[u][rt][r] = tanhf(acc[u][rt][r]);
+  }
+}
+
+PPO_DEV int act_head_row(const PackedLayout& K, int trunk, int h) {
+  if (trunk == 0) return h == 0 ? K.cW3 : -1;
+  if (K.kind == PPO_NET_LN_BETA) {
+    if (h < K.A) return K.aW3 + h * K.H;
+    if (h < 2 * K.A) return K.bW3 + (h - K.A) * K.H;
+    return -1;
+  }
+  return h < K.A ? K.aW3 + h * K.H : -1;
+}
+PPO_DEV int act_head_bias(const PackedLayout& K, int trunk, int h) {
+  if (trunk == 0) return h == 0 ? K.cb3 : -1;
+  if (K.kind == PPO_NET_LN_BETA) {
+    if (h < K.A) return K.ab3 + h;
+    if (h < 2 * K.A) return K.bb3 + (h - K.A);
+    return -1;
+  }
+  return h < K.A ? K.ab3 + h : -1;
+}
+
+}  // namespace
+
+template <int KIND, int NTO, int NHT, int RT>
+__global__ __launch_bounds__(512) void k_act3(ActArgs a) {
+  using GE = ActGeo<NTO, NHT, RT>;
+  constexpr int H = 256, OP = GE::OP, NHP = GE::NHP, LDX = GE::LDX, LDH = GE::LDH, LDP = GE::LDP, R = GE::kActRows;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* XS = lds + GE::oXS;
+  float* HB = lds + GE::oHB;
+  float* SP = lds + GE::oSP;
+  float* HBIAS = lds + GE::oHBIAS;
+  float* RED = lds + GE::oRED;
+  float* HP = lds + GE::oHP;
+  float* PRE = lds + GE::oPRE;
+  float* ITM = lds + GE::oITM;
+  float* LPE = lds + GE::oLP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int trunk = blockIdx.y;
+  if (trunk == 1 && !a.need_actor) return;
+  const PackedLayout& K = a.K;
+  const TrunkDev& T = K.tr[trunk];
+  const float* __restrict__ P = a.P;
+  const PBuf pb = make_pbuf(P, K.size);
+  const int row0 = blockIdx.x * R;
+  const int O = K.O, A = K.A;
+  const int nh = trunk == 0 ? 1 : (KIND == PPO_NET_LN_BETA ? 2 * A : A);
+
+  // ---- kernel start: issue every independent load (inputs, W1 ring, staged params) ----
+  constexpr int NX = (R * OP + kActThreads - 1) / kActThreads;
+  float xv[NX];
+#pragma unroll
+  for (int k = 0; k < NX; ++k) {
+    const int idx = tid + kActThreads * k, r = idx / OP, f = idx - r * OP, row = row0 + r;
+    xv[k] = (idx < R * OP && row < a.n && f < O) ? a.x[(size_t)row * a.ldx + f] : 0.0f;
+  }
+  constexpr int NSP4 = GE::NSP / 4;
+  constexpr int NSPT = (NSP4 + kActThreads - 1) / kActThreads;
+  f4 spv[NSPT];
+#pragma unroll
+  for (int k = 0; k < NSPT; ++k) {
+    const int q = tid + kActThreads * k;  // f4 index into SP
+    f4 v = f4{0.f, 0.f, 0.f, 0.f};
+    if (q < NSP4) {
+      const int fl = 4 * q, vec = fl / H, off = fl - vec * H;
+      int src = -1;
+      if (vec < 6) {
+        const int base = vec == 0 ? T.b1 : vec == 1 ? T.g1 : vec == 2 ? T.be1 : vec == 3 ? T.b2 : vec == 4 ? T.g2 : T.be2;
+        src = base >= 0 ? base + off : -1;
+      } else {
+        const int hr = act_head_row(K, trunk, vec - 6);
+        src = hr >= 0 ? hr + off : -1;
+      }
+      if (src >= 0) v = pld4(pb, src, 0);
+    }
+    spv[k] = v;
+  }
+  float hbias = 0.f;
+  if (tid < NHP) {
+    const int bo = act_head_bias(K, trunk, tid);
+    hbias = bo >= 0 ? P[bo] : 0.f;
+  }
+  // ---- inputs -> LDS (normalized for the LN agent) ----
+#pragma unroll
+  for (int k = 0; k < NX; ++k) {
+    const int idx = tid + kActThreads * k, r = idx / OP, f = idx - r * OP;
+    if (idx < R * OP) {
+      float v = xv[k];
+      if constexpr (KIND == PPO_NET_LN_BETA)
+        if (row0 + r < a.n && f < O) v = (v - P[K.omean + f]) / P[K.ostd + f];
+      XS[r * LDX + f] = v;
+    }
+  }
+  lds_barrier();
+  // ---- layer 1 ----
+  f4 acc[2][RT];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const f4 bv = pld4(pb, T.b1 + 32 * wave + 16 * u + 4 * g, 0);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[u][rt] = bv;
+  }
+  const float* xin = XS + j * LDX + 4 * g;
+  act_layer<NTO, 8, OP, RT>(acc, pb, T.W1 + (32 * wave + j) * OP + 4 * g,
+                            [&](int t, int rt) { return *reinterpret_cast<const f4*>(xin + 16 * rt * LDX + 16 * t); });
+  // staged params land in LDS (visible after the next barrier)
+#pragma unroll
+  for (int k = 0; k < NSPT; ++k) {
+    const int q = tid + kActThreads * k;
+    if (q < NSP4) *reinterpret_cast<f4*>(SP + 4 * q) = spv[k];
+  }
+  if (tid < NHP) HBIAS[tid] = hbias;
+  act_activate<KIND, RT>(acc, SP + GE::sG1, SP + GE::sBE1, RED, wave, j, g);
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+      *reinterpret_cast<f4*>(HB + (16 * rt + j) * LDH + 32 * wave + 16 * u + 4 * g) = acc[u][rt];
+  lds_barrier();
+  // ---- layer 2 ----
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const f4 bv = *reinterpret_cast<const f4*>(SP + GE::sB2 + 32 * wave + 16 * u + 4 * g);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[u][rt] = bv;
+  }
+  const float* hin = HB + j * LDH + 4 * g;
+  act_layer<16, 8, H, RT>(acc, pb, T.W2 + (32 * wave + j) * H + 4 * g,
+                          [&](int t, int rt) { return *reinterpret_cast<const f4*>(hin + 16 * rt * LDH + 16 * t); });
+  act_activate<KIND, RT>(acc, SP + GE::sG2, SP + GE::sBE2, RED, wave, j, g);
+  // ---- heads: split-K partials over this wave's 32 features ----
+#pragma unroll
+  for (int ht = 0; ht < NHT; ++ht) {
+    f4 hp[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) hp[rt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const f4 wv = *reinterpret_cast<const f4*>(SP + GE::sW3 + (16 * ht + j) * H + 32 * wave + 16 * u + 4 * g);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        hp[rt] = mfma16(wv.x, acc[u][rt].x, hp[rt]);
+        hp[rt] = mfma16(wv.y, acc[u][rt].y, hp[rt]);
+        hp[rt] = mfma16(wv.z, acc[u][rt].z, hp[rt]);
+        hp[rt] = mfma16(wv.w, acc[u][rt].w, hp[rt]);
+      }
+    }
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) HP[(wave * NHP + 16 * ht + 4 * g + r) * R + 16 * rt + j] = hp[rt][r];
+  }
+  lds_barrier();
+  for (int idx = tid; idx < R * nh; idx += kActThreads) {
+    const int r = idx / nh, h = idx - r * nh;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < kActWaves; ++w) s += HP[(w * NHP + h) * R + r];
+    PRE[r * LDP + h] = s + HBIAS[h];
+  }
+  lds_barrier();
+
+  if (trunk == 0) {
+    if (tid < R) {
+      const int row = row0 + tid;
+      if (row < a.n) {
+        const float v = PRE[tid * LDP];
+        if (a.value_out) a.value_out[row] = v;
+        if (a.store_step >= 0) {
+          const long srow = (long)a.store_step * a.E + a.env_base + row;
+          a.s_values[srow] = v;
+          a.s_dones[srow] = a.next_done ? a.next_done[row] : 0.0f;
+        }
+      }
+    }
+    if (a.store_step >= 0) {
+      for (int idx = tid; idx < R * O; idx += kActThreads) {
+        const int r = idx / O, f = idx - r * O, row = row0 + r;
+        if (row < a.n) a.s_obs[((long)a.store_step * a.E + a.env_base + row) * O + f] = a.x[(size_t)row * a.ldx + f];
+      }
+    }
+    return;
+  }
+
+  // ---- actor distribution ----
+  const SampleKey key = sample_key(a.seed, a.rank);
+  if constexpr (KIND == PPO_NET_LN_BETA) {
+    // stage 1: one (row, action, alpha|beta) item per thread
+    for (int idx = tid; idx < R * A * 2; idx += kActThreads) {
+      const int which = idx & 1, ra = idx >> 1, r = ra / A, ai = ra - r * A;
+      const long env = a.env_base + row0 + r;
+      const float c = softplusf_(PRE[r * LDP + ai + which * A]) + 1.0f;
+      float gs = 0.f;
+      if (a.mode == PPO_SAMPLE) gs = gamma_mt(c, key, env, a.step_id, 0x10000u + (uint32_t)(ai * 2 + which) * 64u);
+      float* it = ITM + ((r * A + ai) * 2 + which) * 4;
+      it[0] = c;
+      it[1] = gs;
+      it[2] = lgammaf(c);
+      it[3] = digammaf_(c);
+    }
+    lds_barrier();
+    // stage 2: combine per (row, action)
+    for (int idx = tid; idx < R * A; idx += kActThreads) {
+      const int r = idx / A, ai = idx - r * A, row = row0 + r;
+      const long env = a.env_base + row;
+      const bool valid = row < a.n;
+      const float* ia = ITM + (idx * 2 + 0) * 4;
+      const float* ib = ITM + (idx * 2 + 1) * 4;
+      const float al = ia[0], be = ib[0];
+      const float hi = P[K.hi], lo = P[K.lo];
+      float sv;
+      if (a.mode == PPO_GIVEN) {
+        const float av = valid ? a.action_in[(size_t)row * A + ai] : 0.5f * (hi + lo);
+        sv = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+        sv = fminf(fmaxf(sv, 1e-7f), 1.0f + 1e-7f);
+      } else if (a.mode == PPO_MEAN) {
+        sv = al / (al + be);
+      } else {
+        sv = ia[1] / (ia[1] + ib[1]);
+      }
+      const float ab = al + be;
+      const float lga = ia[2], lgb = ib[2], lgab = lgammaf(ab);
+      const float lp = xlogyf_(al - 1.0f, sv) + xlogyf_(be - 1.0f, 1.0f - sv) + (lgab - (lga + lgb));
+      const float ent = (lga + lgb) - lgab - (2.0f - ab) * digammaf_(ab) - ((al - 1.0f) * ia[3] + (be - 1.0f) * ib[3]);
+      const float act = (sv - 0.0f) / (1.0f - 0.0f) * (hi - lo) + lo;
+      LPE[idx * 2 + 0] = lp;
+      LPE[idx * 2 + 1] = ent;
+      if (valid) {
+        if (a.action_out) a.action_out[(size_t)row * A + ai] = act;
+        if (a.store_step >= 0) a.s_actions[((long)a.store_step * a.E + env) * A + ai] = act;
+      }
+    }
+  } else {
+    for (int idx = tid; idx < R * A; idx += kActThreads) {
+      const int r = idx / A, ai = idx - r * A, row = row0 + r;
+      const long env = a.env_base + row;
+      const bool valid = row < a.n;
+      const float mu = PRE[r * LDP + ai];
+      const float sd = expf(P[K.logstd + ai]);
+      const float var = sd * sd, lsd = logf(sd);
+      float act;
+      if (a.mode == PPO_GIVEN) {
+        act = valid ? a.action_in[(size_t)row * A + ai] : 0.0f;
+      } else if (a.mode == PPO_MEAN) {
+        act = mu;
+      } else {
+        uint32_t rr[4];
+        philox_draw(key, env, a.step_id, (uint32_t)(ai >> 1), rr);
+        float z0, z1;
+        box_muller(rr[0], rr[1], z0, z1);
+        act = mu + ((ai & 1) ? z1 : z0) * sd;
+      }
+      const float d = act - mu;
+      LPE[idx * 2 + 0] = -(d * d) / (2.0f * var) - lsd - kLz;
+      LPE[idx * 2 + 1] = kEntC + lsd;
+      if (valid) {
+        if (a.action_out) a.action_out[(size_t)row * A + ai] = act;
+        if (a.store_step >= 0) a.s_actions[((long)a.store_step * a.E + env) * A + ai] = act;
+      }
+    }
+  }
+  lds_barrier();
+  if (tid < R) {
+    const int row = row0 + tid;
+    if (row < a.n) {
+      float lp = 0.f, ent = 0.f;
+      for (int ai = 0; ai < A; ++ai) { lp += LPE[(tid * A + ai) * 2]; ent += LPE[(tid * A + ai) * 2 + 1]; }
+      if (a.logprob_out) a.logprob_out[row] = lp;
+      if (a.entropy_out) a.entropy_out[row] = ent;
+      if (a.store_step >= 0) a.s_logp[(long)a.store_step * a.E + a.env_base + row] = lp;
+    }
+  }
+}
+
+template <int KIND, int NTO, int NHT, int RT>
+static int launch_act3_rt(const ActArgs& a, hipStream_t s) {
+  using GE = ActGeo<NTO, NHT, RT>;
+  const size_t lds = (size_t)GE::total * sizeof(float);
+  static const bool ok = hipFuncSetAttribute((const void*)k_act3<KIND, NTO, NHT, RT>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+  if (!ok) return -2;
+  dim3 grid((a.n + GE::kActRows - 1) / GE::kActRows, a.need_actor ? 2 : 1);
+  hipLaunchKernelGGL((k_act3<KIND, NTO, NHT, RT>), grid, dim3(kActThreads), lds, s, a);
+  return 0;
+}
+// rows per workgroup: every workgroup re-reads the 256 KB layer-2 weights from the memory side
+// (cold L2 per launch), so wide batches use 32 rows (128 workgroups per trunk at E = 4096)
+template <int KIND, int NTO, int NHT>
+static int launch_act3_t(const ActArgs& a, hipStream_t s) {
+  static const int force = [] { const char* e = getenv("PPO_ACT_RT"); return e ? atoi(e) : 0; }();
+  const int rt = force ? force : (a.n >= 2048 ? 2 : 1);
+  if (rt == 4) return launch_act3_rt<KIND, NTO, NHT, 4>(a, s);
+  if (rt == 2) return launch_act3_rt<KIND, NTO, NHT, 2>(a, s);
+  return launch_act3_rt<KIND, NTO, NHT, 1>(a, s);
+}
+
+// 256-wide agents; returns -1 when the shape is not covered (the caller falls back to k_act2)
+int launch_act3(const ActArgs& a, hipStream_t s) {
+  static const bool off = [] { const char* e = getenv("PPO_ACT3"); return e && e[0] == '0'; }();
+  if (off || a.K.H != 256 || a.K.A > 24) return -1;
+  const int nto = a.K.OP / 16;
+  const int nh = a.K.kind == PPO_NET_LN_BETA ? 2 * a.K.A : a.K.A;
+  const int nht = (nh + 15) / 16;
+  if (a.K.kind == PPO_NET_LN_BETA) {
+    if (nto == 1 && nht == 1) return launch_act3_t<PPO_NET_LN_BETA, 1, 1>(a, s);
+    if (nto == 2 && nht == 1) return launch_act3_t<PPO_NET_LN_BETA, 2, 1>(a, s);
+    if (nto == 7 && nht == 1) return launch_act3_t<PPO_NET_LN_BETA, 7, 1>(a, s);
+    if (nto == 24 && nht == 3) return launch_act3_t<PPO_NET_LN_BETA, 24, 3>(a, s);
+    if (nto == 2 && nht == 3) return launch_act3_t<PPO_NET_LN_BETA, 2, 3>(a, s);
+  } else {
+    if (nto == 2 && nht == 1) return launch_act3_t<PPO_NET_TANH_NORMAL, 2, 1>(a, s);
+  }
+  return -1;
+}

@@ -138,6 +138,7 @@ struct SynthArgs {
 };
 
 int launch_act(const ActArgs& a, hipStream_t s);
+int launch_act3(const ActArgs& a, hipStream_t s);
 int launch_fwdbwd(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s);
 int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes);
 int upd_supported(const PackedLayout& K, int nh_actor, int sg_size, UpdGeoOut* g);

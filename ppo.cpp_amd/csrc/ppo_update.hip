@@ -60,47 +60,29 @@ PPO_DEV float bld1(PBuf b, int lane_floats, int uni_floats) {
 // A (weights) double-buffered one 16-wide k-block ahead; B (activations) one ds_read_b128 per row tile.
 template <int FT, int RT, int NKB, int LDW, int LDI>
 PPO_DEV void mm_fr(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* in) {
-  f4 w0[FT], w1[FT];
+  f4 w[2][FT];
 #pragma unroll
-  for (int ft = 0; ft < FT; ++ft) w0[ft] = pld4(wb, wlane, 16 * ft * LDW);
+  for (int ft = 0; ft < FT; ++ft) w[0][ft] = pld4(wb, wlane, 16 * ft * LDW);
 #pragma unroll
-  for (int kb = 0; kb < NKB; kb += 2) {
+  for (int kb = 0; kb < NKB; ++kb) {
     if (kb + 1 < NKB) {
 #pragma unroll
-      for (int ft = 0; ft < FT; ++ft) w1[ft] = pld4(wb, wlane, 16 * ft * LDW + 16 * (kb + 1));
+      for (int ft = 0; ft < FT; ++ft) w[(kb + 1) & 1][ft] = pld4(wb, wlane, 16 * ft * LDW + 16 * (kb + 1));
     }
-    {
-      f4 b[RT];
+    // pin the prefetch here: the scheduler otherwise sinks it next to its use (vmcnt(0) per block)
+    __builtin_amdgcn_sched_barrier(0);
+    f4 b[RT];
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) b[rt] = lds_f4(in + 16 * rt * LDI + 16 * kb);
+    for (int rt = 0; rt < RT; ++rt) b[rt] = lds_f4(in + 16 * rt * LDI + 16 * kb);
 #pragma unroll
-      for (int ft = 0; ft < FT; ++ft)
+    for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          out[ft][rt] = mfma16(w0[ft].x, b[rt].x, out[ft][rt]);
-          out[ft][rt] = mfma16(w0[ft].y, b[rt].y, out[ft][rt]);
-          out[ft][rt] = mfma16(w0[ft].z, b[rt].z, out[ft][rt]);
-          out[ft][rt] = mfma16(w0[ft].w, b[rt].w, out[ft][rt]);
-        }
-    }
-    if (kb + 1 < NKB) {
-      if (kb + 2 < NKB) {
-#pragma unroll
-        for (int ft = 0; ft < FT; ++ft) w0[ft] = pld4(wb, wlane, 16 * ft * LDW + 16 * (kb + 2));
+      for (int rt = 0; rt < RT; ++rt) {
+        out[ft][rt] = mfma16(w[kb & 1][ft].x, b[rt].x, out[ft][rt]);
+        out[ft][rt] = mfma16(w[kb & 1][ft].y, b[rt].y, out[ft][rt]);
+        out[ft][rt] = mfma16(w[kb & 1][ft].z, b[rt].z, out[ft][rt]);
+        out[ft][rt] = mfma16(w[kb & 1][ft].w, b[rt].w, out[ft][rt]);
       }
-      f4 b[RT];
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) b[rt] = lds_f4(in + 16 * rt * LDI + 16 * (kb + 1));
-#pragma unroll
-      for (int ft = 0; ft < FT; ++ft)
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          out[ft][rt] = mfma16(w1[ft].x, b[rt].x, out[ft][rt]);
-          out[ft][rt] = mfma16(w1[ft].y, b[rt].y, out[ft][rt]);
-          out[ft][rt] = mfma16(w1[ft].z, b[rt].z, out[ft][rt]);
-          out[ft][rt] = mfma16(w1[ft].w, b[rt].w, out[ft][rt]);
-        }
-    }
   }
 }
 

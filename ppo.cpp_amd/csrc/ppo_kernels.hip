@@ -866,39 +866,42 @@ __global__ __launch_bounds__(256) void k_dw(DwArgs a) {
 // =============================================================================================
 // k_colsum — dst[seg] = sum_{c < C} src[c * stride + seg]   (fixed order => deterministic)
 // =============================================================================================
+// Each workgroup reduces a 256-float column tile over all `count` slab rows: thread (c, q) sums the
+// float4 column c over rows q, q + 4, q + 8, ... (four accumulators in flight), then the four row
+// phases are added in a fixed order through LDS — deterministic, ~4x the memory parallelism of a
+// thread-per-column loop.
 __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
+  __shared__ f4 part[4][64];
   const ColsumSeg& S = a.seg[blockIdx.y];
-  const bool vec = ((((uintptr_t)S.src) | ((uintptr_t)S.dst)) & 15) == 0 && (S.stride & 3) == 0;
+  const int tid = threadIdx.x, c = tid & 63, q = tid >> 6;
+  const long col0 = (long)blockIdx.x * 256;
+  if (col0 >= S.len) return;
+  const bool vec = ((((uintptr_t)S.src) | ((uintptr_t)S.dst)) & 15) == 0 && (S.stride & 3) == 0 && (S.len & 3) == 0;
   if (vec) {
-    const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
-    if (i >= S.len) return;
-    if (i + 4 <= S.len) {
+    const long i = col0 + 4 * c;
+    f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+    if (i < S.len) {
       const float* src = S.src + i;
-      f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
-      int c = 0;
-      for (; c + 4 <= S.count; c += 4) {
-        a0 += ld4(src + (size_t)(c + 0) * S.stride);
-        a1 += ld4(src + (size_t)(c + 1) * S.stride);
-        a2 += ld4(src + (size_t)(c + 2) * S.stride);
-        a3 += ld4(src + (size_t)(c + 3) * S.stride);
+      int r = q;
+      for (; r + 12 < S.count; r += 16) {
+        acc0 += ld4(src + (size_t)r * S.stride);
+        acc1 += ld4(src + (size_t)(r + 4) * S.stride);
+        acc2 += ld4(src + (size_t)(r + 8) * S.stride);
+        acc3 += ld4(src + (size_t)(r + 12) * S.stride);
       }
-      for (; c < S.count; ++c) a0 += ld4(src + (size_t)c * S.stride);
-      st4(S.dst + i, ((a0 + a1) + (a2 + a3)) * S.scale);
-      return;
+      for (; r < S.count; r += 4) acc0 += ld4(src + (size_t)r * S.stride);
     }
-    for (long k = i; k < S.len; ++k) {
-      float acc = 0.f;
-      for (int c = 0; c < S.count; ++c) acc += S.src[(size_t)c * S.stride + k];
-      S.dst[k] = acc * S.scale;
-    }
+    part[q][c] = (acc0 + acc1) + (acc2 + acc3);
+    __syncthreads();
+    if (q == 0 && i < S.len) st4(S.dst + i, ((part[0][c] + part[1][c]) + (part[2][c] + part[3][c])) * S.scale);
     return;
   }
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= S.len) return;
-  const float* src = S.src + i;
-  float acc = 0.0f;
-  for (int cI = 0; cI < S.count; ++cI) acc += src[(size_t)cI * S.stride];
-  S.dst[i] = acc * S.scale;
+  // unaligned / ragged segments (tiny): one thread per column
+  for (long i = col0 + tid; i < S.len && i < col0 + 256; i += 256) {
+    float acc = 0.0f;
+    for (int r = 0; r < S.count; ++r) acc += S.src[(size_t)r * S.stride + i];
+    S.dst[i] = acc * S.scale;
+  }
 }
 
 // =============================================================================================
@@ -1075,47 +1078,52 @@ __global__ __launch_bounds__(256) void k_synth_reset(SynthArgs a, int seed, floa
   if (done) done[e] = 0.0f;
 }
 
+// One thread per (env, observation dim): 32 lanes per env (2 envs per wave), q_(i+1) comes from the
+// neighbouring lane, so all reads of the old state happen before any write; lane 0 of each env does
+// the per-env reward / time limit / episode statistics. Same fp32 ops as synth_reset_one and the
+// oracle (no contraction): bit-exact.
 __global__ __launch_bounds__(256) void k_synth_step(SynthArgs a, int e0, int e1, const float* __restrict__ act,
                                                     float lo, float hi, float* __restrict__ obs,
                                                     float* __restrict__ reward, float* __restrict__ done) {
 #pragma clang fp contract(off)
-  constexpr int MO = PSYN_MAXO;
-  const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= e1) return;
+  const int i = threadIdx.x & 31;
+  const int e = e0 + blockIdx.x * 8 + (threadIdx.x >> 5);
+  const bool live = e < e1;
   const int O = a.O, A = a.A;
-  if (a.autoreset[e]) {
-    synth_reset_one(a, e, -1, obs);
-    reward[e] = 0.0f;
-    done[e] = 0.0f;
-    a.autoreset[e] = 0;
+  const int ec = live ? e : e0;
+  const bool reset = a.autoreset[ec] != 0;
+  float* __restrict__ q = a.q + (long)ec * O;
+  const float* __restrict__ ar = act + (long)(ec - e0) * A;
+  const float qi = (live && i < O) ? q[i] : 0.0f;
+  // old q_(i+1 mod O) from the neighbouring lane (lane - i is this env's i = 0)
+  const int lane = threadIdx.x & 63;
+  const float qn = __shfl(qi, (i + 1 < O) ? lane + 1 : lane - i, 64);
+  if (!live || i >= O) return;
+  if (reset) {
+    const uint32_t rs = a.rseed[e], rc = a.rcount[e];
+    uint32_t r[4];
+    philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, r);
+    const float v = (0.1f * ((2.0f * u01(r[0])) - 1.0f));
+    q[i] = v;
+    obs[(long)e * O + i] = v;
+    if (i == 0) {
+      a.rcount[e] = rc + 1;
+      a.t[e] = 0;
+      a.ep_ret[e] = 0.0f;
+      a.ep_len[e] = 0;
+      reward[e] = 0.0f;
+      done[e] = 0.0f;
+      a.autoreset[e] = 0;
+    }
     return;
   }
-  float* __restrict__ q = a.q + (long)e * O;
-  const float* __restrict__ ar = act + (long)(e - e0) * A;
-  float qv[MO];
-#pragma unroll
-  for (int i = 0; i < MO; ++i) qv[i] = i < O ? q[i] : 0.0f;
-  const float xb = qv[0];
-  float nq[MO];
-  // q'_i = 0.9 q_i + (0.1 a_(i mod A) + 0.05 q_(i+1 mod O))  (fmaf, no contraction: bit-exact)
-#pragma unroll
-  for (int i = 0; i < MO; ++i) {
-    if (i < O) {
-      const float qn = (i + 1 < O) ? qv[(i + 1) % MO] : qv[0];
-      const float ai = fminf(fmaxf(ar[i % A], lo), hi);
-      nq[i] = __fmaf_rn(0.9f, qv[i], __fmaf_rn(0.1f, ai, (0.05f * qn)));
-    } else {
-      nq[i] = 0.0f;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < MO; ++i) {
-    if (i < O) {
-      q[i] = nq[i];
-      obs[(long)e * O + i] = nq[i];
-    }
-  }
-  const float vel = ((nq[0] - xb) / 0.05f);
+  // q'_i = 0.9 q_i + (0.1 a_(i mod A) + 0.05 q_(i+1 mod O))  (fmaf, no contraction)
+  const float ai = fminf(fmaxf(ar[i % A], lo), hi);
+  const float nq = __fmaf_rn(0.9f, qi, __fmaf_rn(0.1f, ai, (0.05f * qn)));
+  q[i] = nq;
+  obs[(long)e * O + i] = nq;
+  if (i != 0) return;
+  const float vel = ((nq - qi) / 0.05f);
   float ctrl = 0.0f;
   for (int k = 0; k < A; ++k) {
     const float ak = fminf(fmaxf(ar[k], lo), hi);
@@ -1236,7 +1244,7 @@ int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s) {
 }
 
 void launch_colsum(const ColsumArgs& a, int nseg, long maxlen, hipStream_t s) {
-  hipLaunchKernelGGL(k_colsum, dim3((unsigned)((maxlen + 255) / 256), nseg), dim3(256), 0, s, a);  // (vector path uses 1/4)
+  hipLaunchKernelGGL(k_colsum, dim3((unsigned)((maxlen + 255) / 256), nseg), dim3(256), 0, s, a);
 }
 void launch_gradnorm(const NormArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_gradnorm, dim3(a.nt), dim3(1024), 0, s, a); }
 void launch_adam(const AdamArgs& a, hipStream_t s) {
@@ -1261,6 +1269,6 @@ void launch_synth_reset(const SynthArgs& a, int seed, float* obs, float* done, h
 }
 void launch_synth_step(const SynthArgs& a, int e0, int e1, const float* act, float lo, float hi, float* obs,
                        float* reward, float* done, hipStream_t s) {
-  hipLaunchKernelGGL(k_synth_step, dim3((e1 - e0 + 255) / 256), dim3(256), 0, s, a, e0, e1, act, lo, hi, obs, reward,
+  hipLaunchKernelGGL(k_synth_step, dim3((e1 - e0 + 7) / 8), dim3(256), 0, s, a, e0, e1, act, lo, hi, obs, reward,
                      done);
 }

@@ -763,16 +763,17 @@ __global__ __launch_bounds__(256) void k_fwdbwd(UpdArgs a) {
 // =============================================================================================
 typedef float f16v __attribute__((ext_vector_type(16)));
 
-template <int NO, int NI, int LDI, int WO, int WI>
+template <int NO, int NI, int LDI, int WO, int WI, int NTH>
 PPO_DEV void dw_phase(const float* __restrict__ DZ, const float* __restrict__ IN, long m0, long m1,
                       float* __restrict__ out, float* lds, int tid) {
   constexpr int TO = NO / 32, TI = (NI + 31) / 32;
   constexpr int TOW = TO / WO, TIW = (TI + WI - 1) / WI;
   constexpr int KS = 16;                       // rows per stage
-  constexpr int ADZ = KS * NO, AIN = KS * LDI; // floats per stage
+  constexpr int LDZ = NO + 4, LDN = LDI + 4;   // padded LDS rows (the two half-waves read rows k, k+1)
+  constexpr int ADZ = KS * LDZ, AIN = KS * LDN; // floats per stage
   constexpr int STG = ADZ + AIN;
-  constexpr int NF4 = STG / 4;
-  constexpr int F4PT = (NF4 + 255) / 256;
+  constexpr int NF4Z = KS * NO / 4, NF4 = NF4Z + KS * LDI / 4;
+  constexpr int F4PT = (NF4 + NTH - 1) / NTH;
   const int lane = tid & 63, wave = tid >> 6;
   const int wo = wave % WO, wi = wave / WO;
   const int l32 = lane & 31, hs = lane >> 5;
@@ -787,18 +788,15 @@ PPO_DEV void dw_phase(const float* __restrict__ DZ, const float* __restrict__ IN
   auto load = [&](long mb) {
 #pragma unroll
     for (int u = 0; u < F4PT; ++u) {
-      const int c = tid + 256 * u;
+      const int c = tid + NTH * u;
       f4 v = f4{0.f, 0.f, 0.f, 0.f};
-      if (c < NF4) {
-        const int fl = 4 * c;
-        if (fl < ADZ) {
-          const long row = mb + fl / NO;
-          if (row < m1) v = ld4(DZ + row * NO + (fl % NO));
-        } else {
-          const int f2 = fl - ADZ;
-          const long row = mb + f2 / LDI;
-          if (row < m1) v = ld4(IN + row * LDI + (f2 % LDI));
-        }
+      if (c < NF4Z) {
+        const long row = mb + (4 * c) / NO;
+        if (row < m1) v = ld4(DZ + row * NO + (4 * c) % NO);
+      } else if (c < NF4) {
+        const int f2 = 4 * (c - NF4Z);
+        const long row = mb + f2 / LDI;
+        if (row < m1) v = ld4(IN + row * LDI + f2 % LDI);
       }
       st[u] = v;
     }
@@ -806,8 +804,14 @@ PPO_DEV void dw_phase(const float* __restrict__ DZ, const float* __restrict__ IN
   auto store = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < F4PT; ++u) {
-      const int c = tid + 256 * u;
-      if (c < NF4) *reinterpret_cast<f4*>(lds + buf * STG + 4 * c) = st[u];
+      const int c = tid + NTH * u;
+      if (c < NF4Z) {
+        const int fl = 4 * c;
+        *reinterpret_cast<f4*>(lds + buf * STG + (fl / NO) * LDZ + fl % NO) = st[u];
+      } else if (c < NF4) {
+        const int f2 = 4 * (c - NF4Z);
+        *reinterpret_cast<f4*>(lds + buf * STG + ADZ + (f2 / LDI) * LDN + f2 % LDI) = st[u];
+      }
     }
   };
   const int nst = (int)((m1 - m0 + KS - 1) / KS);
@@ -822,11 +826,11 @@ PPO_DEV void dw_phase(const float* __restrict__ DZ, const float* __restrict__ IN
     for (int k = 0; k < KS; k += 2) {
       float av[TOW], bv[TIW];
 #pragma unroll
-      for (int u = 0; u < TOW; ++u) av[u] = sdz[(k + hs) * NO + (wo * TOW + u) * 32 + l32];
+      for (int u = 0; u < TOW; ++u) av[u] = sdz[(k + hs) * LDZ + (wo * TOW + u) * 32 + l32];
 #pragma unroll
       for (int v = 0; v < TIW; ++v) {
         const int col = (wi * TIW + v) * 32 + l32;
-        bv[v] = (col < LDI) ? sin[(k + hs) * LDI + col] : 0.0f;
+        bv[v] = (col < LDI) ? sin[(k + hs) * LDN + col] : 0.0f;
       }
 #pragma unroll
       for (int u = 0; u < TOW; ++u)
@@ -836,6 +840,7 @@ PPO_DEV void dw_phase(const float* __restrict__ DZ, const float* __restrict__ IN
     if (sI + 1 < nst) store((sI + 1) & 1);
     lds_barrier();
     if (sI + 2 < nst) load(m0 + (long)(sI + 2) * KS);
+    __builtin_amdgcn_sched_barrier(0);  // keep the next-next stage's loads issued here
   }
 #pragma unroll
   for (int u = 0; u < TOW; ++u)
@@ -849,17 +854,22 @@ PPO_DEV void dw_phase(const float* __restrict__ DZ, const float* __restrict__ IN
       }
 }
 
-template <int H, int OP, int WO2, int WI2, int WO1, int WI1>
-__global__ __launch_bounds__(256) void k_dw(DwArgs a) {
+// 8 waves (two per SIMD): dW2 as a 4 x 2 grid of 64 x 128 wave tiles (128 accumulator registers
+// per wave), then dW1 (H x OP) with the waves split over the output rows.
+template <int H, int OP>
+__global__ __launch_bounds__(512) void k_dw(DwArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int TO = H / 32;
+  constexpr int WO2 = TO >= 4 ? 4 : TO, WI2 = 8 / WO2;
+  constexpr int WO1 = TO >= 8 ? 8 : TO, WI1 = 8 / WO1;
   const int trunk = blockIdx.y;
   const long m0 = (long)blockIdx.x * a.rows_per_chunk;
   const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
   float* out = a.slab[trunk] + (size_t)blockIdx.x * a.slab_stride;
   if (m0 < m1) {
-    dw_phase<H, H, H, WO2, WI2>(a.dz2[trunk], a.h1[trunk], m0, m1, out, lds, threadIdx.x);
+    dw_phase<H, H, H, WO2, WI2, 512>(a.dz2[trunk], a.h1[trunk], m0, m1, out, lds, threadIdx.x);
     lds_barrier();
-    dw_phase<H, OP, OP, WO1, WI1>(a.dz1[trunk], a.xn, m0, m1, out + H * H, lds, threadIdx.x);
+    dw_phase<H, OP, OP, WO1, WI1, 512>(a.dz1[trunk], a.xn, m0, m1, out + H * H, lds, threadIdx.x);
   }
 }
 
@@ -1211,23 +1221,20 @@ int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes) {
 // dW of both Linear weight matrices of both trunks, grid = (chunks, 2 trunks)
 template <int H, int OP>
 static int launch_dw_t(const DwArgs& a, int nchunks, size_t lds, hipStream_t s) {
-  constexpr int TO = H / 32, TI1 = (OP + 31) / 32;
-  constexpr int WO2 = TO >= 4 ? 4 : TO, WI2 = 4 / WO2;
-  constexpr int WO1 = TO >= 4 ? 4 : TO, WI1 = 4 / WO1;
-  (void)TI1;
-  auto k = k_dw<H, OP, WO2, WI2, WO1, WI1>;
+  auto k = k_dw<H, OP>;
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(nchunks, 2), dim3(256), lds, s, a);
+  hipLaunchKernelGGL(k, dim3(nchunks, 2), dim3(512), lds, s, a);
   return 0;
 }
 
 size_t dw_lds_bytes(int H, int OP) {
   const int KS = 16;
-  return (size_t)2 * (KS * H + KS * std::max(H, OP)) * sizeof(float);
+  const int m = std::max(H, OP) + 4;
+  return (size_t)2 * (KS * (H + 4) + KS * m) * sizeof(float);
 }
 
 int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s) {

@@ -873,6 +873,113 @@ __global__ __launch_bounds__(512) void k_dw(DwArgs a) {
   }
 }
 
+// k_dwf — the same two products of one trunk in ONE pass over the chunk's rows (H = 256, OP <= 32).
+// Every 16-row stage carries DZ2, H1, DZ1 and Xn rows, so the memory-bound dW1 product (K = OP,
+// one 32x32 MFMA per wave and row pair) rides under the MFMA-bound dW2 product (eight per wave)
+// instead of running as a second, load-bound phase. 8 waves: dW2 as a 4 x 2 grid of 64 x 128
+// wave tiles, dW1 as one 32-row o-tile per wave. Slab layout as k_dw.
+template <int H, int OP>
+__global__ __launch_bounds__(512) void k_dwf(DwArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int KS = 16, NTH = 512;
+  constexpr int LDH = H + 4, LDX = OP + 4;
+  constexpr int oH1 = KS * LDH, oDZ1 = 2 * KS * LDH, oXN = 3 * KS * LDH;
+  constexpr int STG = 3 * KS * LDH + KS * LDX;
+  constexpr int N2 = KS * H / 4, NX = KS * OP / 4;  // f4 per stage of a width-H / width-OP source
+  static_assert(H == 256 && OP <= 32 && N2 % NTH == 0, "k_dwf geometry");
+  constexpr int PW = N2 / NTH;                      // f4 per thread per width-H source
+  constexpr int NXT = (NX + NTH - 1) / NTH;
+  constexpr int TOW = 2, TIW = 4;                   // dW2 wave tile: 2 x 4 32x32 tiles
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hs = lane >> 5;
+  const int wo = wave & 3, wi = wave >> 2;
+  const int trunk = blockIdx.y;
+  const long m0 = (long)blockIdx.x * a.rows_per_chunk;
+  const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
+  if (m0 >= m1) return;
+  const float* __restrict__ src3[3] = {a.dz2[trunk], a.h1[trunk], a.dz1[trunk]};
+  const float* __restrict__ XN = a.xn;
+  f16v acc[TOW][TIW], acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc1[r] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < TOW; ++u)
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) acc[u][v][r] = 0.0f;
+  }
+  f4 st[3 * PW], sx[NXT];
+  auto load = [&](long mb) {
+#pragma unroll
+    for (int s3 = 0; s3 < 3; ++s3)
+#pragma unroll
+      for (int p = 0; p < PW; ++p) {
+        const int fl = 4 * (tid + NTH * p);
+        const long row = mb + fl / H;
+        st[s3 * PW + p] = row < m1 ? ld4(src3[s3] + row * H + fl % H) : f4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int p = 0; p < NXT; ++p) {
+      const int fl = 4 * (tid + NTH * p);
+      const long row = mb + fl / OP;
+      sx[p] = (fl < KS * OP && row < m1) ? ld4(XN + row * OP + fl % OP) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store = [&](int buf) {
+    float* b = lds + buf * STG;
+#pragma unroll
+    for (int s3 = 0; s3 < 3; ++s3)
+#pragma unroll
+      for (int p = 0; p < PW; ++p) {
+        const int fl = 4 * (tid + NTH * p);
+        *reinterpret_cast<f4*>(b + s3 * KS * LDH + (fl / H) * LDH + fl % H) = st[s3 * PW + p];
+      }
+#pragma unroll
+    for (int p = 0; p < NXT; ++p) {
+      const int fl = 4 * (tid + NTH * p);
+      if (fl < KS * OP) *reinterpret_cast<f4*>(b + oXN + (fl / OP) * LDX + fl % OP) = sx[p];
+    }
+  };
+  const int nst = (int)((m1 - m0 + KS - 1) / KS);
+  load(m0);
+  store(0);
+  lds_barrier();
+  if (nst > 1) load(m0 + KS);
+  for (int sI = 0; sI < nst; ++sI) {
+    const float* sb = lds + (sI & 1) * STG;
+#pragma unroll
+    for (int k = 0; k < KS; k += 2) {
+      const float* rowp = sb + (k + hs) * LDH;
+      float av[TOW], bv[TIW];
+#pragma unroll
+      for (int u = 0; u < TOW; ++u) av[u] = rowp[(wo * TOW + u) * 32 + l32];
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) bv[v] = rowp[oH1 + (wi * TIW + v) * 32 + l32];
+      const float a1 = rowp[oDZ1 + wave * 32 + l32];
+      const float b1 = l32 < OP ? sb[oXN + (k + hs) * LDX + l32] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < TOW; ++u)
+#pragma unroll
+        for (int v = 0; v < TIW; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[v], acc[u][v], 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc1, 0, 0, 0);
+    }
+    if (sI + 1 < nst) store((sI + 1) & 1);
+    lds_barrier();
+    if (sI + 2 < nst) load(m0 + (long)(sI + 2) * KS);
+    __builtin_amdgcn_sched_barrier(0);  // keep the next-next stage's loads issued here
+  }
+  float* out = a.slab[trunk] + (size_t)blockIdx.x * a.slab_stride;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int orow = (r & 3) + 8 * (r >> 2) + 4 * hs;
+#pragma unroll
+    for (int u = 0; u < TOW; ++u)
+#pragma unroll
+      for (int v = 0; v < TIW; ++v)
+        out[(size_t)((wo * TOW + u) * 32 + orow) * H + (wi * TIW + v) * 32 + l32] = acc[u][v][r];
+    if (l32 < OP) out[(size_t)H * H + (size_t)(wave * 32 + orow) * OP + l32] = acc1[r];
+  }
+}
+
 // =============================================================================================
 // k_colsum — dst[seg] = sum_{c < C} src[c * stride + seg]   (fixed order => deterministic)
 // =============================================================================================
@@ -1237,7 +1344,30 @@ size_t dw_lds_bytes(int H, int OP) {
   return (size_t)2 * (KS * (H + 4) + KS * m) * sizeof(float);
 }
 
+template <int H, int OP>
+static int launch_dwf_t(const DwArgs& a, int nchunks, hipStream_t s) {
+  auto k = k_dwf<H, OP>;
+  constexpr size_t lds = (size_t)2 * (3 * 16 * (H + 4) + 16 * (OP + 4)) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3(nchunks, 2), dim3(512), lds, s, a);
+  return 0;
+}
+
+// "PPO_DW_FUSED=0" forces the two-phase k_dw where k_dwf applies (tests compare the two)
+static bool dw_fused_enabled() {
+  const char* ev = getenv("PPO_DW_FUSED");
+  return !(ev && ev[0] == '0');
+}
+
 int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s) {
+  if (H == 256 && dw_fused_enabled()) {
+    if (OP == 16) return launch_dwf_t<256, 16>(a, nchunks, s);
+    if (OP == 32) return launch_dwf_t<256, 32>(a, nchunks, s);
+  }
   const size_t lds = dw_lds_bytes(H, OP);
   if (H == 256 && OP == 16) return launch_dw_t<256, 16>(a, nchunks, lds, s);
   if (H == 256 && OP == 32) return launch_dw_t<256, 32>(a, nchunks, lds, s);

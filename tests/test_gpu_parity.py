@@ -400,3 +400,35 @@ def test_update_kernels_agree(kind, O_, A, H, monkeypatch):
         if L.t_grad[t]:
             assert rel(grads[1][o:o + n], grads[0][o:o + n]) < 2e-4, t
     np.testing.assert_allclose(stats[1], stats[0], rtol=2e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("kind,O_,A,H", [(1, 17, 6, 256), (0, 17, 6, 256), (1, 9, 3, 256)])
+def test_fused_dw_matches_two_phase_dw(kind, O_, A, H, monkeypatch):
+    """k_dwf (dW2 and dW1 in one pass over the rows) and the two-phase k_dw run the same MFMA
+    chains over the same rows in the same order: the gradients are bitwise equal (ragged last
+    chunk and stage: M = 12 800 - 8 rows)."""
+    rng = np.random.default_rng(7)
+    L = O.layout_init(kind, O_, A, H)
+    p = random_params(L, rng)
+    if kind == 0:
+        p[L.logstd:L.logstd + A] = -0.5
+    E, T = 1599, 8
+    B = T * E
+    x = rng.standard_normal((B, O_)).astype(np.float32)
+    act = (rng.uniform(-0.95, 0.95, (B, A)) if kind else rng.standard_normal((B, A))).astype(np.float32)
+    olp = rng.standard_normal(B).astype(np.float32)
+    ov = rng.standard_normal(B).astype(np.float32)
+    adv = rng.standard_normal(B).astype(np.float32)
+    ret = rng.standard_normal(B).astype(np.float32)
+    perm = rng.permutation(B).astype(np.int32)
+    grads = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("PPO_DW_FUSED", env)
+        ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.1)
+        ag.load_params(p)
+        fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
+        ag.update(2.5e-4, perms=DeviceArray.from_numpy(perm), want_stats=True)
+        grads.append(ag.last_grad())
+        ag.close()
+    assert np.isfinite(grads[0]).all()
+    np.testing.assert_array_equal(grads[1], grads[0])

@@ -72,6 +72,7 @@ struct ppo_ctx {
   float* next_value = nullptr;
   int32_t* perms = nullptr;
   float *advstats = nullptr, *advsq = nullptr;
+  double* advpart = nullptr;
   float *Xn = nullptr, *H1[2] = {}, *DZ1[2] = {}, *DZ2[2] = {};
   float* slab[2] = {};
   int tiles_per_block = 1, nblk = 1;
@@ -83,6 +84,7 @@ struct ppo_ctx {
   float* dwslab[4] = {};
   int nchunks = 1, rows_per_chunk = 64;
   float* normout = nullptr;
+  float* gnpart = nullptr;
   float* mbstats = nullptr;  // [EP*MB][8]
   long adam_step = 0;
   long iteration = 0;
@@ -210,6 +212,7 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   rc |= dmalloc(&c->perms, (size_t)EP * B);
   rc |= dmalloc(&c->advstats, (size_t)2 * EP * c->nmb);
   rc |= dmalloc(&c->advsq, (size_t)EP * c->nmb);
+  rc |= dmalloc(&c->advpart, (size_t)EP * c->nmb * PPO_ADV_SPLIT);
   const size_t Mr = ((size_t)c->M + 63) / 64 * 64;
   rc |= dmalloc(&c->Xn, Mr * OP + 64);
   for (int k = 0; k < 2; ++k) {
@@ -230,7 +233,7 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
     }
   }
   for (int k = 0; k < 2; ++k)
-    rc |= dmalloc(&c->slab[k], (size_t)std::max(c->nblk, c->upd_nblk) * c->sg[k].size);
+    rc |= dmalloc(&c->slab[k], (size_t)std::max(c->nblk, 2 * c->upd_nblk) * c->sg[k].size);  // 2x: PPO_UPD_TRUNK
   c->wlds_off = 4 * std::max(c->sg[0].size, c->sg[1].size);
   c->wlds_off = (c->wlds_off + 63) & ~63;
   c->lds_bytes = ((size_t)c->wlds_off + 2 * (size_t)H * 16) * sizeof(float);
@@ -239,6 +242,7 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   c->nchunks = (c->M + c->rows_per_chunk - 1) / c->rows_per_chunk;
   for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->dwslab[k], (size_t)c->nchunks * (H * H + H * OP));
   rc |= dmalloc(&c->normout, 2 + PPO_LAYOUT_MAX_TENSORS + 2);
+  rc |= dmalloc(&c->gnpart, (size_t)PPO_LAYOUT_MAX_TENSORS * PPO_GN_SPLIT);
   rc |= dmalloc(&c->mbstats, (size_t)8 * EP * c->nmb);
   if (rc) {
     ppo_destroy(c);
@@ -260,7 +264,7 @@ extern "C" int ppo_destroy(ppo_t* c) {
   prof_drain(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   float* ptrs[] = {c->P, c->G, c->Am, c->Av, c->W2T[0], c->W2T[1], c->next_value, c->advstats, c->advsq, c->Xn,
-                   c->normout, c->mbstats};
+                   c->normout, c->gnpart, c->mbstats};
   for (float* p : ptrs)
     if (p) (void)hipFree(p);
   for (int b = 0; b < PPO_BUF_COUNT; ++b)
@@ -273,6 +277,7 @@ extern "C" int ppo_destroy(ppo_t* c) {
   for (int k = 0; k < 4; ++k)
     if (c->dwslab[k]) (void)hipFree(c->dwslab[k]);
   if (c->perms) (void)hipFree(c->perms);
+  if (c->advpart) (void)hipFree(c->advpart);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -509,6 +514,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   aa.adv = c->buf[PPO_BUF_ADVANTAGES];
   aa.stats = c->advstats;
   aa.sq = c->advsq;
+  aa.part = c->advpart;
   aa.M = M;
   aa.nmb = EP * MB;
   aa.world = c->world;
@@ -516,9 +522,12 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
     ProfScope ps(c, PK_ADV, s);
     launch_adv_sum(aa, s);
     if (allreduce(c, c->advstats, 2L * EP * MB, 1, s)) return -3;
-    launch_adv_sq(aa, s);
-    if (allreduce(c, c->advsq, (long)EP * MB, 0, s)) return -3;
-    launch_adv_finalize(aa, s);
+    const bool multi = c->comm && c->world > 1;
+    launch_adv_sq(aa, multi ? 0 : 1, s);
+    if (multi) {
+      if (allreduce(c, c->advsq, (long)EP * MB, 0, s)) return -3;
+      launch_adv_finalize(aa, s);
+    }
   }
   // ---- per-minibatch launch sequence ----
   UpdArgs u;
@@ -611,6 +620,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   na.grad = c->G;
   na.max_norm = cfg.max_grad_norm;
   na.out = c->normout;
+  na.part = c->gnpart;
   for (int t = 0; t < c->K.nt; ++t)
     if (c->K.grad[t]) {
       na.off[na.nt] = c->K.poff[t];
@@ -629,6 +639,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   ad.begin = tb;
   ad.n = c->K.size - tb;
   ad.norm_out = c->normout;
+  ad.part = c->gnpart;
   ad.nt = na.nt;
   ad.max_norm = cfg.max_grad_norm;
   ad.eps = cfg.adam_eps;
@@ -672,12 +683,11 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
       const double bc2 = 1.0 - std::pow(0.999, (double)c->adam_step);
       ad.step_size = (float)((double)lr / bc1);
       ad.sbc2 = (float)std::sqrt(bc2);
+      ad.stat_out = st + 6;  // the total norm of this minibatch next to its loss stats
       {
         ProfScope ps(c, PK_ADAM, s);
         launch_adam(ad, s);
       }
-      // keep the total norm of this minibatch next to its loss stats
-      HIP_TRY(hipMemcpyAsync(st + 6, c->normout, sizeof(float), hipMemcpyDeviceToDevice, s));
     }
   }
   HIP_TRY(hipGetLastError());

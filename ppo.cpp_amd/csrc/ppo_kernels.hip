@@ -983,16 +983,18 @@ __global__ __launch_bounds__(512) void k_dwf(DwArgs a) {
 // =============================================================================================
 // k_colsum — dst[seg] = sum_{c < C} src[c * stride + seg]   (fixed order => deterministic)
 // =============================================================================================
-// Each workgroup reduces a 256-float column tile over all `count` slab rows: thread (c, q) sums the
-// float4 column c over rows q, q + 4, q + 8, ... (four accumulators in flight), then the four row
-// phases are added in a fixed order through LDS — deterministic, ~4x the memory parallelism of a
-// thread-per-column loop.
+// The segments are cut into 64-float column tiles, numbered consecutively over all segments
+// (ColsumArgs::tile0 = first tile of each segment). A workgroup owns one tile: thread (c, q) sums
+// float4 column c over rows q, q + 16, q + 32, ... (four loads in flight), and the 16 row phases
+// are added in a fixed order through LDS — deterministic, and every workgroup has work.
 __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
-  __shared__ f4 part[4][64];
-  const ColsumSeg& S = a.seg[blockIdx.y];
-  const int tid = threadIdx.x, c = tid & 63, q = tid >> 6;
-  const long col0 = (long)blockIdx.x * 256;
-  if (col0 >= S.len) return;
+  __shared__ f4 part[16][16];
+  const int b = blockIdx.x;
+  int sgi = 0;
+  while (sgi + 1 < a.nseg && b >= a.tile0[sgi + 1]) ++sgi;
+  const ColsumSeg& S = a.seg[sgi];
+  const int tid = threadIdx.x, c = tid & 15, q = tid >> 4;
+  const long col0 = (long)(b - a.tile0[sgi]) * 64;
   const bool vec = ((((uintptr_t)S.src) | ((uintptr_t)S.dst)) & 15) == 0 && (S.stride & 3) == 0 && (S.len & 3) == 0;
   if (vec) {
     const long i = col0 + 4 * c;
@@ -1000,64 +1002,112 @@ __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
     if (i < S.len) {
       const float* src = S.src + i;
       int r = q;
-      for (; r + 12 < S.count; r += 16) {
+      for (; r + 48 < S.count; r += 64) {
         acc0 += ld4(src + (size_t)r * S.stride);
-        acc1 += ld4(src + (size_t)(r + 4) * S.stride);
-        acc2 += ld4(src + (size_t)(r + 8) * S.stride);
-        acc3 += ld4(src + (size_t)(r + 12) * S.stride);
+        acc1 += ld4(src + (size_t)(r + 16) * S.stride);
+        acc2 += ld4(src + (size_t)(r + 32) * S.stride);
+        acc3 += ld4(src + (size_t)(r + 48) * S.stride);
       }
-      for (; r < S.count; r += 4) acc0 += ld4(src + (size_t)r * S.stride);
+      for (; r < S.count; r += 16) acc0 += ld4(src + (size_t)r * S.stride);
     }
     part[q][c] = (acc0 + acc1) + (acc2 + acc3);
     __syncthreads();
-    if (q == 0 && i < S.len) st4(S.dst + i, ((part[0][c] + part[1][c]) + (part[2][c] + part[3][c])) * S.scale);
+    if (q == 0 && i < S.len) {
+      f4 t = part[0][c];
+#pragma unroll
+      for (int p = 1; p < 16; ++p) t += part[p][c];
+      st4(S.dst + i, t * S.scale);
+    }
     return;
   }
-  // unaligned / ragged segments (tiny): one thread per column
-  for (long i = col0 + tid; i < S.len && i < col0 + 256; i += 256) {
-    float acc = 0.0f;
-    for (int r = 0; r < S.count; ++r) acc += S.src[(size_t)r * S.stride + i];
-    S.dst[i] = acc * S.scale;
+  // unaligned / ragged segments (biases of width 1..A, loss stats): same 16 row phases, scalar,
+  // 16 columns at a time
+  float* sp = reinterpret_cast<float*>(part);
+  for (int cb = 0; cb < 64 && col0 + cb < S.len; cb += 16) {
+    const long i = col0 + cb + c;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (i < S.len) {
+      const float* src = S.src + i;
+      int r = q;
+      for (; r + 48 < S.count; r += 64) {
+        a0 += src[(size_t)r * S.stride];
+        a1 += src[(size_t)(r + 16) * S.stride];
+        a2 += src[(size_t)(r + 32) * S.stride];
+        a3 += src[(size_t)(r + 48) * S.stride];
+      }
+      for (; r < S.count; r += 16) a0 += src[(size_t)r * S.stride];
+    }
+    sp[q * 16 + c] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (q == 0 && i < S.len) {
+      float t = sp[c];
+#pragma unroll
+      for (int p = 1; p < 16; ++p) t += sp[p * 16 + c];
+      S.dst[i] = t * S.scale;
+    }
+    __syncthreads();
   }
 }
 
 // =============================================================================================
 // k_gradnorm — clip_grad_norm_: per-tensor L2 norms (fp32 tensors), norm of norms, clip coef
 // =============================================================================================
-__global__ __launch_bounds__(1024) void k_gradnorm(NormArgs a) {
-  __shared__ float red[16];
-  const int t = blockIdx.x, tid = threadIdx.x;
+// pass 1 (k_gradnorm): grid (tensor, PPO_GN_SPLIT slices) -> partial sums of squares;
+// pass 2 (head of k_adam, every block): per-tensor norms from the slices in order, total, coef.
+__global__ __launch_bounds__(256) void k_gradnorm(NormArgs a) {
+  __shared__ float red[4];
+  const int t = blockIdx.x, sp = blockIdx.y, tid = threadIdx.x;
+  const int len = a.len[t], sl = (((len + PPO_GN_SPLIT - 1) / PPO_GN_SPLIT) + 3) & ~3;
+  const int i0 = sp * sl, i1 = min(len, i0 + sl);
+  const float* g = a.grad + a.off[t];
   float s = 0.0f;
-  for (int i = tid; i < a.len[t]; i += 1024) {
-    const float gv = a.grad[a.off[t] + i];
-    s += gv * gv;
+  if (((a.off[t] | sl) & 3) == 0) {
+    for (int i = i0 + 4 * tid; i < i1; i += 1024) {
+      if (i + 3 < i1) {
+        const f4 v = ld4(g + i);
+        s += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+      } else {
+        for (int k = i; k < i1; ++k) s += g[k] * g[k];
+      }
+    }
+  } else {
+    for (int i = i0 + tid; i < i1; i += 256) s += g[i] * g[i];
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
   if ((tid & 63) == 0) red[tid >> 6] = s;
   __syncthreads();
-  if (tid == 0) {
-    float tot = 0.0f;
-    for (int w = 0; w < 16; ++w) tot += red[w];
-    a.out[2 + t] = sqrtf(tot);  // per-tensor L2 norm (an fp32 tensor, clip_grad.h: grad.norm())
-  }
+  if (tid == 0) a.part[t * PPO_GN_SPLIT + sp] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // =============================================================================================
 // k_adam — grad *= clip coef; Adam (bias-corrected, torch::optim::Adam); refresh W2^T copies
 // =============================================================================================
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
+  __shared__ float s_norm[PPO_LAYOUT_MAX_TENSORS];
   __shared__ float s_coef;
+  if (threadIdx.x < a.nt) {
+    float q = 0.0f;
+#pragma unroll
+    for (int sp = 0; sp < PPO_GN_SPLIT; ++sp) q += a.part[threadIdx.x * PPO_GN_SPLIT + sp];
+    s_norm[threadIdx.x] = sqrtf(q);  // per-tensor L2 norm (an fp32 tensor, clip_grad.h: grad.norm())
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     // clip_grad_norm_: total = ||(||g_t||)_t||, coef = clamp(max_norm / (total + 1e-6), max = 1)
     float tot = 0.0f;
-    for (int t = 0; t < a.nt; ++t) tot += a.norm_out[2 + t] * a.norm_out[2 + t];
+    for (int t = 0; t < a.nt; ++t) tot += s_norm[t] * s_norm[t];
     const float total = sqrtf(tot);
     float coef = a.max_norm / (total + 1e-6f);
     coef = coef > 1.0f ? 1.0f : coef;
     s_coef = coef;
-    if (blockIdx.x == 0) { a.norm_out[0] = total; a.norm_out[1] = coef; }
+    if (blockIdx.x == 0) {
+      a.norm_out[0] = total;
+      a.norm_out[1] = coef;
+      if (a.stat_out) a.stat_out[0] = total;
+    }
   }
+  if (blockIdx.x == 0 && threadIdx.x < a.nt) a.norm_out[2 + threadIdx.x] = s_norm[threadIdx.x];
   __syncthreads();
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
@@ -1122,47 +1172,67 @@ __global__ __launch_bounds__(256) void k_perm(int32_t* __restrict__ out, uint32_
   if (i < B) out[i] = (int32_t)perm_index(i, B, pk);
 }
 
-// per minibatch (blockIdx.x): sum of gathered advantages (double) -> local mean
-__global__ __launch_bounds__(1024) void k_adv_sum(AdvArgs a) {
-  __shared__ double red[16];
-  const int mb = blockIdx.x;
-  const int32_t* perm = a.perm + (long)mb * a.M;
-  double s = 0.0;
-  for (int i = threadIdx.x; i < a.M; i += 1024) s += (double)a.adv[perm[i]];
+// Advantage statistics of every minibatch, PPO_ADV_SPLIT workgroups per minibatch: each sums a
+// contiguous slice of the minibatch's permutation entries (double), the partials are then added
+// in slice order by one thread per minibatch — deterministic.
+PPO_DEV double block_sum_d(double s, double* red) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int w = 0; w < 16; ++w) t += red[w];
-    a.stats[2 * mb + 0] = (float)(t / a.M);  // local mean (all-reduced with ncclAvg when G > 1)
-  }
+  double t = 0.0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+  return t;
 }
-// per minibatch: sum (adv - mean)^2 with the (global) mean -> stats[2mb+1] = local sum of squares
-__global__ __launch_bounds__(1024) void k_adv_sq(AdvArgs a) {
-  __shared__ double red[16];
-  const int mb = blockIdx.x;
+// pass 1: slice sums of the gathered advantages
+__global__ __launch_bounds__(256) void k_adv_sum(AdvArgs a) {
+  __shared__ double red[4];
+  const int mb = blockIdx.x, sl = blockIdx.y;
+  const int len = (a.M + PPO_ADV_SPLIT - 1) / PPO_ADV_SPLIT;
+  const int i0 = sl * len, i1 = min(a.M, i0 + len);
+  const int32_t* perm = a.perm + (long)mb * a.M;
+  double s = 0.0;
+  for (int i = i0 + threadIdx.x; i < i1; i += 256) s += (double)a.adv[perm[i]];
+  const double t = block_sum_d(s, red);
+  if (threadIdx.x == 0) a.part[mb * PPO_ADV_SPLIT + sl] = t;
+}
+// -> stats[2mb] = local mean (all-reduced with ncclAvg when G > 1)
+__global__ void k_adv_mean(AdvArgs a) {
+  const int mb = blockIdx.x * blockDim.x + threadIdx.x;
+  if (mb >= a.nmb) return;
+  double t = 0.0;
+  for (int sl = 0; sl < PPO_ADV_SPLIT; ++sl) t += a.part[mb * PPO_ADV_SPLIT + sl];
+  a.stats[2 * mb + 0] = (float)(t / a.M);
+}
+// pass 2: slice sums of (adv - mean)^2 with the (global) mean
+__global__ __launch_bounds__(256) void k_adv_sq(AdvArgs a) {
+  __shared__ double red[4];
+  const int mb = blockIdx.x, sl = blockIdx.y;
+  const int len = (a.M + PPO_ADV_SPLIT - 1) / PPO_ADV_SPLIT;
+  const int i0 = sl * len, i1 = min(a.M, i0 + len);
   const int32_t* perm = a.perm + (long)mb * a.M;
   const float mu = a.stats[2 * mb + 0];
   double s = 0.0;
-  for (int i = threadIdx.x; i < a.M; i += 1024) {
+  for (int i = i0 + threadIdx.x; i < i1; i += 256) {
     const double d = (double)(a.adv[perm[i]] - mu);
     s += d * d;
   }
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int w = 0; w < 16; ++w) t += red[w];
-    a.sq[mb] = (float)t;
-  }
+  const double t = block_sum_d(s, red);
+  if (threadIdx.x == 0) a.part[mb * PPO_ADV_SPLIT + sl] = t;
+}
+// -> sq[mb] = local sum of squares (all-reduced with ncclSum when G > 1); with_std: also the std
+__global__ void k_adv_sqsum(AdvArgs a, int with_std) {
+  const int mb = blockIdx.x * blockDim.x + threadIdx.x;
+  if (mb >= a.nmb) return;
+  double t = 0.0;
+  for (int sl = 0; sl < PPO_ADV_SPLIT; ++sl) t += a.part[mb * PPO_ADV_SPLIT + sl];
+  a.sq[mb] = (float)t;
+  if (with_std) a.stats[2 * mb + 1] = sqrtf((float)((double)a.sq[mb] / (double)(a.world * (long)a.M - 1)));
 }
 // std = sqrt(sum_sq_global / (G * M - 1))  (ac:845-846; ppo's Tensor::std() for G = 1)
 __global__ void k_adv_finalize(AdvArgs a) {
-  const int mb = threadIdx.x;
+  const int mb = blockIdx.x * blockDim.x + threadIdx.x;
   if (mb < a.nmb) a.stats[2 * mb + 1] = sqrtf((float)((double)a.sq[mb] / (double)(a.world * (long)a.M - 1)));
 }
 
@@ -1380,10 +1450,21 @@ int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s) {
   return -1;
 }
 
-void launch_colsum(const ColsumArgs& a, int nseg, long maxlen, hipStream_t s) {
-  hipLaunchKernelGGL(k_colsum, dim3((unsigned)((maxlen + 255) / 256), nseg), dim3(256), 0, s, a);
+void launch_colsum(const ColsumArgs& a_in, int nseg, long maxlen, hipStream_t s) {
+  (void)maxlen;
+  ColsumArgs a = a_in;
+  a.nseg = nseg;
+  int t = 0;
+  for (int i = 0; i < nseg; ++i) {
+    a.tile0[i] = t;
+    t += (a.seg[i].len + 63) / 64;
+  }
+  a.tile0[nseg] = t;
+  hipLaunchKernelGGL(k_colsum, dim3((unsigned)t), dim3(256), 0, s, a);
 }
-void launch_gradnorm(const NormArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_gradnorm, dim3(a.nt), dim3(1024), 0, s, a); }
+void launch_gradnorm(const NormArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_gradnorm, dim3(a.nt, PPO_GN_SPLIT), dim3(256), 0, s, a);
+}
 void launch_adam(const AdamArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_adam, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
 }
@@ -1396,10 +1477,17 @@ void launch_gae(const GaeArgs& a, hipStream_t s) {
 void launch_perm(int32_t* out, uint32_t B, const PermKey& pk, hipStream_t s) {
   hipLaunchKernelGGL(k_perm, dim3((B + 255) / 256), dim3(256), 0, s, out, B, pk);
 }
-void launch_adv_sum(const AdvArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_adv_sum, dim3(a.nmb), dim3(1024), 0, s, a); }
-void launch_adv_sq(const AdvArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_adv_sq, dim3(a.nmb), dim3(1024), 0, s, a); }
+static unsigned nmb_blocks(int nmb) { return (unsigned)((nmb + 255) / 256); }
+void launch_adv_sum(const AdvArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_adv_sum, dim3(a.nmb, PPO_ADV_SPLIT), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_adv_mean, dim3(nmb_blocks(a.nmb)), dim3(256), 0, s, a);
+}
+void launch_adv_sq(const AdvArgs& a, int with_std, hipStream_t s) {
+  hipLaunchKernelGGL(k_adv_sq, dim3(a.nmb, PPO_ADV_SPLIT), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_adv_sqsum, dim3(nmb_blocks(a.nmb)), dim3(256), 0, s, a, with_std);
+}
 void launch_adv_finalize(const AdvArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_adv_finalize, dim3(1), dim3(((a.nmb + 63) / 64) * 64), 0, s, a);
+  hipLaunchKernelGGL(k_adv_finalize, dim3(nmb_blocks(a.nmb)), dim3(256), 0, s, a);
 }
 void launch_synth_reset(const SynthArgs& a, int seed, float* obs, float* done, hipStream_t s) {
   hipLaunchKernelGGL(k_synth_reset, dim3((a.E + 255) / 256), dim3(256), 0, s, a, seed, obs, done);

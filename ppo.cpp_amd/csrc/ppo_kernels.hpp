@@ -51,6 +51,7 @@ struct UpdArgs {
   float* DZ2[2];
   float* slab[2];
   int actn_off, acc_off;  // k_upd: runtime LDS offsets (floats)
+  int trunk0;             // k_upd: trunk of blockIdx.y == 0 (diagnostic single-trunk launches)
 };
 
 // k_upd geometry (ppo_update.hip)
@@ -82,6 +83,8 @@ struct ColsumSeg {
 #define PPO_MAX_SEGS 40
 struct ColsumArgs {
   ColsumSeg seg[PPO_MAX_SEGS];
+  int tile0[PPO_MAX_SEGS + 1];  // first 64-float tile of each segment (set by launch_colsum)
+  int nseg;
 };
 
 struct NormArgs {
@@ -90,8 +93,10 @@ struct NormArgs {
   int off[PPO_LAYOUT_MAX_TENSORS];
   int len[PPO_LAYOUT_MAX_TENSORS];
   float max_norm;
-  float* out;  // [0] total norm, [1] clip coefficient, [2 + t] per-tensor norms
+  float* out;   // [0] total norm, [1] clip coefficient, [2 + t] per-tensor norms (written by k_adam)
+  float* part;  // [nt][PPO_GN_SPLIT] partial sums of squares
 };
+#define PPO_GN_SPLIT 16
 
 struct AdamArgs {
   float* param;
@@ -99,6 +104,8 @@ struct AdamArgs {
   float *m, *v;
   long begin, n;
   float* norm_out;
+  const float* part;  // k_gradnorm partials
+  float* stat_out;    // optional: total norm of this step (minibatch stats slot)
   int nt;
   float max_norm;
   float step_size, sbc2, eps;
@@ -119,8 +126,10 @@ struct AdvArgs {
   const float* adv;
   float* stats;         // [nmb][2]
   float* sq;            // [nmb]
+  double* part;         // [nmb][PPO_ADV_SPLIT] slice partial sums
   int M, nmb, world;
 };
+#define PPO_ADV_SPLIT 32
 
 #define PSYN_MAXO 32  // device synthetic env: max observation width
 struct SynthArgs {
@@ -152,7 +161,7 @@ void launch_transpose(const float* src, float* dst, int H, hipStream_t s);
 void launch_gae(const GaeArgs& a, hipStream_t s);
 void launch_perm(int32_t* out, uint32_t B, const PermKey& pk, hipStream_t s);
 void launch_adv_sum(const AdvArgs& a, hipStream_t s);
-void launch_adv_sq(const AdvArgs& a, hipStream_t s);
+void launch_adv_sq(const AdvArgs& a, int with_std, hipStream_t s);
 void launch_adv_finalize(const AdvArgs& a, hipStream_t s);
 void launch_synth_reset(const SynthArgs& a, int seed, float* obs, float* done, hipStream_t s);
 void launch_synth_step(const SynthArgs& a, int e0, int e1, const float* act, float lo, float hi, float* obs,

@@ -20,6 +20,7 @@
 //    barrier phases overlap the other's MFMA phases.
 // Everything is reduced in a fixed order: results are bitwise reproducible run to run.
 #include "ppo_agent.hpp"
+#include <cstdlib>
 #include "ppo_kernels.hpp"
 
 namespace {
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
   const int wf = wave % WF, wr = wave / WF;
   const int fbase = wf * FT * 16, rbase = wr * RT * 16;
-  const int trunk = blockIdx.y;
+  const int trunk = blockIdx.y + a.trunk0;
   const PackedLayout& K = a.K;
   const TrunkDev& T = K.tr[trunk];
   const float* __restrict__ P = a.P;
@@ -854,10 +855,19 @@ int upd_supported(const PackedLayout& K, int nh_actor, int sg_size, UpdGeoOut* g
 }
 
 int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s) {
+  // diagnostic only: "PPO_UPD_TRUNK=0|1" runs that one trunk on twice the workgroups (the other
+  // trunk's gradient is left stale) to time the two trunks apart
+  const char* ev = getenv("PPO_UPD_TRUNK");
+  UpdArgs b = a;
+  dim3 grid(nblocks, 2);
+  if (ev && (ev[0] == '0' || ev[0] == '1')) {
+    b.trunk0 = ev[0] - '0';
+    grid = dim3(2 * nblocks, 1);
+  }
   return dispatch_upd(a.K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_) {
     hipLaunchKernelGGL((k_upd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value,
                               decltype(NHT_)::value>),
-                       dim3(nblocks, 2), dim3(256), lds_bytes, s, a);
+                       grid, dim3(256), lds_bytes, s, b);
     return 0;
   });
 }

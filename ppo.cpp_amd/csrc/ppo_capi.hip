@@ -233,7 +233,7 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
     }
   }
   for (int k = 0; k < 2; ++k)
-    rc |= dmalloc(&c->slab[k], (size_t)std::max(c->nblk, 2 * c->upd_nblk) * c->sg[k].size);  // 2x: PPO_UPD_TRUNK
+    rc |= dmalloc(&c->slab[k], (size_t)std::max(c->nblk, c->upd_nblk) * c->sg[k].size);
   c->wlds_off = 4 * std::max(c->sg[0].size, c->sg[1].size);
   c->wlds_off = (c->wlds_off + 63) & ~63;
   c->lds_bytes = ((size_t)c->wlds_off + 2 * (size_t)H * 16) * sizeof(float);

@@ -51,7 +51,7 @@ struct UpdArgs {
   float* DZ2[2];
   float* slab[2];
   int actn_off, acc_off;  // k_upd: runtime LDS offsets (floats)
-  int trunk0;             // k_upd: trunk of blockIdx.y == 0 (diagnostic single-trunk launches)
+  int trunk_mask;         // k_upd: trunks to run (bit t = trunk t; 3 = both)
 };
 
 // k_upd geometry (ppo_update.hip)

@@ -23,6 +23,35 @@
 #include <cstdlib>
 #include "ppo_kernels.hpp"
 
+#ifdef PPO_STAMPS
+// diagnostic build only: per-wave shader-clock stamps at phase ends of tiles 2..5 of every workgroup
+#define PPO_NSTAMP 13
+#define PPO_STAMP_TILES 4
+__device__ unsigned long long g_upd_stamps[1024 * 4 * PPO_STAMP_TILES * (PPO_NSTAMP + 1)];
+#define PPO_STAMP(k)                                                                                 \
+  do {                                                                                               \
+    const int tt_ = (it - (int)blockIdx.x) / (int)gridDim.x - 2;                                     \
+    if (tt_ >= 0 && tt_ < PPO_STAMP_TILES) {                                                         \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                    \
+      const int wg_ = trunk * 512 + blockIdx.x;                                            \
+      if (lane == 0 && blockIdx.x < 512)                                                                    \
+        g_upd_stamps[((wg_ * 4 + wave) * PPO_STAMP_TILES + tt_) * (PPO_NSTAMP + 1) + (k) + 1] = t_;  \
+    }                                                                                                \
+  } while (0)
+#define PPO_STAMP_START()                                                                            \
+  do {                                                                                               \
+    const int tt_ = (it - (int)blockIdx.x) / (int)gridDim.x - 2;                                     \
+    if (tt_ >= 0 && tt_ < PPO_STAMP_TILES) {                                                         \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                    \
+      const int wg_ = trunk * 512 + blockIdx.x;                                            \
+      if (lane == 0 && blockIdx.x < 512) g_upd_stamps[((wg_ * 4 + wave) * PPO_STAMP_TILES + tt_) * (PPO_NSTAMP + 1)] = t_; \
+    }                                                                                                \
+  } while (0)
+#else
+#define PPO_STAMP(k) do {} while (0)
+#define PPO_STAMP_START() do {} while (0)
+#endif
+
 namespace {
 
 template <int H_, int NTO_, int NHT_>
@@ -281,7 +310,8 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
   const int wf = wave % WF, wr = wave / WF;
   const int fbase = wf * FT * 16, rbase = wr * RT * 16;
-  const int trunk = blockIdx.y + a.trunk0;
+  const int trunk = blockIdx.y;
+  if (!((a.trunk_mask >> trunk) & 1)) return;
   const PackedLayout& K = a.K;
   const TrunkDev& T = K.tr[trunk];
   const float* __restrict__ P = a.P;
@@ -413,6 +443,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
 
   for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
     const int m0 = it * R;
+    PPO_STAMP_START();
     lds_barrier();  // the previous iteration's LDS readers are done
     if constexpr (PREF) {
       commit(it);
@@ -421,11 +452,13 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       gather_sync(it);
     }
     lds_barrier();
+    PPO_STAMP(0);
 
     // ---------------- layer 1 ----------------
     f4 z[FT][RT];
     init_bias<FT, RT>(z, pb, T.b1 + fbase + 4 * g);
     mm_fr<FT, RT, NTO, OP, LDX>(z, pb, w1lane, xn_in);
+    PPO_STAMP(1);
     float mu1[RT], rs1[RT];
     if constexpr (LN) {
       ln_rows<FT, RT, WF, R, H>(z, mu1, rs1, RED0, RED1, wf, rbase, j, g);
@@ -452,11 +485,13 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     store_tile_rows<FT, RT>(a.H1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
     lds_store_tile<FT, RT, LDA>(ACT, z, rbase, fbase, j, g);
     lds_barrier();
+    PPO_STAMP(2);
 
     // ---------------- layer 2 ----------------
     f4 x2[FT][RT];  // LN: x_hat2; tanh: h2
     init_bias<FT, RT>(x2, pb, T.b2 + fbase + 4 * g);
     mm_fr<FT, RT, NT, H, LDA>(x2, pb, w2lane, act_in);
+    PPO_STAMP(3);
     if constexpr (PREF) pref_data(it + gridDim.x);
     float rs2[RT];
     if constexpr (LN) {
@@ -488,6 +523,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
         return x2[ft][rt];
       }
     };
+    PPO_STAMP(4);
     // ---------------- heads (split-K over this wave's features) ----------------
     f4 hp[NHT][RT];
 #pragma unroll
@@ -523,6 +559,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) SCR[(wf * NHP + 16 * ht + 4 * g + r) * R + rbase + 16 * rt + j] = hp[ht][rt][r];
     lds_barrier();
+    PPO_STAMP(5);
     for (int idx = tid; idx < R * nh; idx += 256) {
       const int row = idx / nh, h = idx - row * nh;
       float s = 0.f;
@@ -531,6 +568,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       PRE[row * LDG + h] = s + P[head_bias(K, trunk, h)];
     }
     lds_barrier();
+    PPO_STAMP(6);
 
     // ---------------- loss and its gradient wrt the head pre-activations ----------------
     float* ITM = SCR;  // R x A x ITS (head partials are consumed)
@@ -572,16 +610,17 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
           float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
           s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
           const float ab = al + be;
-          const float lga = lgammaf(al), lgb = lgammaf(be), lgab = lgammaf(ab);
-          const float psa = digammaf_(al), psb = digammaf_(be), psab = digammaf_(ab);
+          float lga, lgb, lgab, psa, psb, psab, ta, tb, tab;
+          lgamma_digamma_trigamma(al, lga, psa, ta);
+          lgamma_digamma_trigamma(be, lgb, psb, tb);
+          lgamma_digamma_trigamma(ab, lgab, psab, tab);
           it_[0] = xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
           it_[1] = (lga + lgb) - lgab - (2.0f - ab) * psab - ((al - 1.0f) * psa + (be - 1.0f) * psb);
-          const float tab = trigammaf_(ab);
           it_[2] = ((al - 1.0f) != 0.0f ? logf(s) : 0.0f) + psab - psa;            // d lp / d alpha
-          it_[3] = (ab - 2.0f) * tab - (al - 1.0f) * trigammaf_(al);                // d ent / d alpha
+          it_[3] = (ab - 2.0f) * tab - (al - 1.0f) * ta;                            // d ent / d alpha
           it_[4] = softplus_d(pa);
           it_[5] = ((be - 1.0f) != 0.0f ? logf(1.0f - s) : 0.0f) + psab - psb;     // d lp / d beta
-          it_[6] = (ab - 2.0f) * tab - (be - 1.0f) * trigammaf_(be);                // d ent / d beta
+          it_[6] = (ab - 2.0f) * tab - (be - 1.0f) * tb;                            // d ent / d beta
           it_[7] = softplus_d(pbv);
         } else {
           const float mu = PRE[row * LDG + ai];
@@ -653,6 +692,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       }
     }
     lds_barrier();
+    PPO_STAMP(7);
     // head bias (and logstd) gradients: fixed-order sums over the workgroup's rows
     if (tid < nh) {
       float s = 0.f;
@@ -702,6 +742,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       }
     }
 
+    PPO_STAMP(8);
     // ---------------- layer-2 backward: dz2 ----------------
     if constexpr (LN) {
       float s1[RT], s2[RT];
@@ -745,13 +786,16 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     lds_barrier();  // dW3 readers of h2 are done
     lds_store_tile<FT, RT, LDA>(ACT, x2, rbase, fbase, j, g);
     lds_barrier();
+    PPO_STAMP(9);
 
     // ---------------- dh1 = W2^T dz2 ----------------
     zero<FT, RT>(dh);
     mm_fr<FT, RT, NT, H, LDA>(dh, w2t, w2tlane, act_in);
+    PPO_STAMP(10);
     // ---------------- recompute layer 1, layer-1 backward ----------------
     init_bias<FT, RT>(z, pb, T.b1 + fbase + 4 * g);
     mm_fr<FT, RT, NTO, OP, LDX>(z, pb, w1lane, xn_in);
+    PPO_STAMP(11);
     if constexpr (LN) {
       float s1[RT], s2[RT];
 #pragma unroll
@@ -798,6 +842,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     // z = dz1
     col_sums<FT, RT>([&](int ft, int rt, int r) { return z[ft][rt][r]; }, acc + sg.b1, fbase, j, g);
     store_tile_rows<FT, RT>(a.DZ1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
+    PPO_STAMP(12);
   }
   // ---------------- workgroup result (row groups summed in a fixed order) ----------------
   lds_barrier();
@@ -855,15 +900,12 @@ int upd_supported(const PackedLayout& K, int nh_actor, int sg_size, UpdGeoOut* g
 }
 
 int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s) {
-  // diagnostic only: "PPO_UPD_TRUNK=0|1" runs that one trunk on twice the workgroups (the other
-  // trunk's gradient is left stale) to time the two trunks apart
+  // diagnostic only: "PPO_UPD_TRUNK=0|1" runs that one trunk (the other trunk's gradient is left
+  // stale) to time the two trunks apart
   const char* ev = getenv("PPO_UPD_TRUNK");
   UpdArgs b = a;
-  dim3 grid(nblocks, 2);
-  if (ev && (ev[0] == '0' || ev[0] == '1')) {
-    b.trunk0 = ev[0] - '0';
-    grid = dim3(2 * nblocks, 1);
-  }
+  b.trunk_mask = (ev && (ev[0] == '0' || ev[0] == '1')) ? 1 << (ev[0] - '0') : 3;
+  const dim3 grid(nblocks, 2);
   return dispatch_upd(a.K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_) {
     hipLaunchKernelGGL((k_upd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value,
                               decltype(NHT_)::value>),
@@ -871,3 +913,13 @@ int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hi
     return 0;
   });
 }
+
+#ifdef PPO_STAMPS
+extern "C" int ppo_diag_read_stamps(unsigned long long* host, long n) {
+  const long cap = (long)(sizeof(g_upd_stamps) / sizeof(g_upd_stamps[0]));
+  if (n > cap) n = cap;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_upd_stamps), n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -2;
+}
+#endif

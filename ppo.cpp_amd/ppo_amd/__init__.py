@@ -22,7 +22,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libppo_hip.so")
+LIB_PATH = os.environ.get("PPO_HIP_LIB") or os.path.join(PKG_ROOT, "lib", "libppo_hip.so")  # override: diagnostics
 
 PPO_NET_TANH_NORMAL = 0
 PPO_NET_LN_BETA = 1

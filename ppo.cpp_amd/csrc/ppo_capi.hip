@@ -556,6 +556,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   u.Xn = c->Xn;
   u.actn_off = c->upd.actn_off;
   u.acc_off = c->upd.acc_off;
+  u.spar_off = c->upd.spar_off;
   const int nblk = c->use_upd ? c->upd_nblk : c->nblk;  // workgroups that wrote a slab row
   for (int k = 0; k < 2; ++k) {
     u.H1[k] = c->H1[k];

@@ -50,7 +50,7 @@ struct UpdArgs {
   float* DZ1[2];
   float* DZ2[2];
   float* slab[2];
-  int actn_off, acc_off;  // k_upd: runtime LDS offsets (floats)
+  int actn_off, acc_off, spar_off;  // k_upd: runtime LDS offsets (floats)
   int trunk_mask;         // k_upd: trunks to run (bit t = trunk t; 3 = both)
 };
 
@@ -58,7 +58,7 @@ struct UpdArgs {
 #define PPO_UPD_MAXA 24
 struct UpdGeoOut {
   size_t lds_bytes;
-  int actn_off, acc_off, rows;
+  int actn_off, acc_off, spar_off, rows;
 };
 
 struct DwArgs {

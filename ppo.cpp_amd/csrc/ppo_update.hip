@@ -64,7 +64,7 @@ struct Geo {
   static constexpr int R = 16 * RT * WR;         // rows per workgroup iteration
   static constexpr int NTO = NTO_, OP = NTO * 16;
   static constexpr int NHT = NHT_, NHP = 16 * NHT;
-  static constexpr int LDX = ((OP + 63) / 64) * 64 + 4;
+  static constexpr int LDX = OP + 4;  // layer-1 B operands: 2 k-blocks per pass, a 2-way conflict is noise
   static constexpr int LDA = ((H + 63) / 64) * 64 + 4;
   static constexpr int LDG = NHP + 4;
   static constexpr int ITS = 10;  // floats per (row, action) item
@@ -76,6 +76,9 @@ struct Geo {
   static constexpr int oG = oPRE + R * LDG;          // R x LDG head gradients
   static constexpr int oROW = oG + R * LDG;          // R x 8 per-row scalars
   static constexpr int oSCR = oROW + R * 8;          // head partials (WF x NHP x R) / items (R x A x ITS)
+  // staged small parameters: LayerNorm gamma/beta of both layers, head biases, observation
+  // mean / std (placed after the runtime-sized regions)
+  static constexpr int NSPAR = 4 * H + NHP + 2 * OP;
 };
 
 PPO_DEV float lds_f(const float* p) { return *p; }
@@ -302,6 +305,14 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
   float* SCR = lds + GE::oSCR;   // head partials, then per-item scratch
   float* ACTN = lds + a.actn_off;  // R x A stored actions
   float* ACC = lds + a.acc_off;    // WR x sg.size accumulators
+  float* SPAR = lds + a.spar_off;  // staged gamma1 | beta1 | gamma2 | beta2 | head biases
+  float* SG1 = SPAR;
+  float* SBE1 = SPAR + H;
+  float* SG2 = SPAR + 2 * H;
+  float* SBE2 = SPAR + 3 * H;
+  float* SHB = SPAR + 4 * H;
+  float* SOM = SHB + NHP;
+  float* SOS = SOM + OP;
   float* RED0 = RED;
   float* RED1 = RED + WF * R;
   float* RED2 = RED + 2 * WF * R;
@@ -324,6 +335,22 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
   float* acc = ACC + wr * sg.size;
   for (int i = tid; i < GE::WR * sg.size; i += 256) ACC[i] = 0.f;
   for (int i = tid; i < R * LDG; i += 256) GG[i] = 0.f;  // padding heads stay exactly 0
+  // the per-tile LayerNorm / head-bias reads come from LDS instead of an L2 round trip each
+  for (int i = tid; i < GE::NSPAR; i += 256) {
+    const int v = i / H, f = i - v * H;
+    float x = 0.f;
+    if (v < 4) {
+      if constexpr (LN) x = P[(v == 0 ? T.g1 : v == 1 ? T.be1 : v == 2 ? T.g2 : T.be2) + f];
+    } else if (i < 4 * H + NHP) {
+      if (i - 4 * H < nh) x = P[head_bias(K, trunk, i - 4 * H)];
+    } else {
+      const int q = i - 4 * H - NHP, o = q % OP;
+      x = q < OP ? 0.f : 1.f;
+      if constexpr (LN)
+        if (o < O) x = P[(q < OP ? K.omean : K.ostd) + o];
+    }
+    SPAR[i] = x;
+  }
 
   // per-lane A-operand offsets
   const int w1lane = T.W1 + (fbase + j) * OP + 4 * g;
@@ -391,7 +418,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       const int idx = tid + 256 * k, row = idx / OP, f = idx - row * OP, m = mb + row;
       if (idx < R * OP) {
         float v = vg[k];
-        if (LN && pg[k] >= 0) v = (v - P[K.omean + f]) / P[K.ostd + f];
+        if (LN && pg[k] >= 0) v = (v - SOM[f]) / SOS[f];
         XN[row * LDX + f] = v;
         if (trunk == 0 && m < a.M) a.Xn[(size_t)m * OP + f] = v;
       }
@@ -413,7 +440,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       float v = 0.f;
       if (m < a.M && f < O) {
         v = a.obs[(long)a.perm[m] * O + f];
-        if constexpr (LN) v = (v - P[K.omean + f]) / P[K.ostd + f];
+        if constexpr (LN) v = (v - SOM[f]) / SOS[f];
       }
       XN[row * LDX + f] = v;
       if (trunk == 0 && m < a.M) a.Xn[(size_t)m * OP + f] = v;
@@ -464,7 +491,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       ln_rows<FT, RT, WF, R, H>(z, mu1, rs1, RED0, RED1, wf, rbase, j, g);
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
-        const f4 gm = pld4(pb, T.g1 + fbase + 4 * g, 16 * ft), bt = pld4(pb, T.be1 + fbase + 4 * g, 16 * ft);
+        const f4 gm = lds_f4(SG1 + fbase + 4 * g + 16 * ft), bt = lds_f4(SBE1 + fbase + 4 * g + 16 * ft);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -511,7 +538,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     }
     auto h2_of = [&](int ft, int rt) -> f4 {
       if constexpr (LN) {
-        const f4 gm = pld4(pb, T.g2 + fbase + 4 * g, 16 * ft), bt = pld4(pb, T.be2 + fbase + 4 * g, 16 * ft);
+        const f4 gm = lds_f4(SG2 + fbase + 4 * g + 16 * ft), bt = lds_f4(SBE2 + fbase + 4 * g + 16 * ft);
         f4 y;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -565,7 +592,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       float s = 0.f;
 #pragma unroll
       for (int w = 0; w < WF; ++w) s += SCR[(w * NHP + h) * R + row];
-      PRE[row * LDG + h] = s + P[head_bias(K, trunk, h)];
+      PRE[row * LDG + h] = s + SHB[h];
     }
     lds_barrier();
     PPO_STAMP(6);
@@ -750,7 +777,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       for (int rt = 0; rt < RT; ++rt) { s1[rt] = 0.f; s2[rt] = 0.f; }
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
-        const f4 gm = pld4(pb, T.g2 + fbase + 4 * g, 16 * ft), bt = pld4(pb, T.be2 + fbase + 4 * g, 16 * ft);
+        const f4 gm = lds_f4(SG2 + fbase + 4 * g + 16 * ft), bt = lds_f4(SBE2 + fbase + 4 * g + 16 * ft);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -770,7 +797,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r] * x2[ft][rt][r]; }, acc + sg.g2, fbase, j, g);
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
-        const f4 gm = pld4(pb, T.g2 + fbase + 4 * g, 16 * ft);
+        const f4 gm = lds_f4(SG2 + fbase + 4 * g + 16 * ft);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) x2[ft][rt] = rs2[rt] * (dh[ft][rt] * gm - s1[rt] - x2[ft][rt] * s2[rt]);
       }
@@ -802,7 +829,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       for (int rt = 0; rt < RT; ++rt) { s1[rt] = 0.f; s2[rt] = 0.f; }
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
-        const f4 gm = pld4(pb, T.g1 + fbase + 4 * g, 16 * ft), bt = pld4(pb, T.be1 + fbase + 4 * g, 16 * ft);
+        const f4 gm = lds_f4(SG1 + fbase + 4 * g + 16 * ft), bt = lds_f4(SBE1 + fbase + 4 * g + 16 * ft);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -824,7 +851,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r] * z[ft][rt][r]; }, acc + sg.g1, fbase, j, g);
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
-        const f4 gm = pld4(pb, T.g1 + fbase + 4 * g, 16 * ft);
+        const f4 gm = lds_f4(SG1 + fbase + 4 * g + 16 * ft);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) z[ft][rt] = rs1[rt] * (dh[ft][rt] * gm - s1[rt] - z[ft][rt] * s2[rt]);
       }
@@ -868,6 +895,8 @@ static void upd_geo(const PackedLayout& K, int sg_size, UpdGeoOut* g) {
   off = (off + 3) & ~3;
   g->acc_off = off;
   off += GE::WR * sg_size;
+  g->spar_off = off;
+  off += GE::NSPAR;
   g->lds_bytes = (size_t)off * sizeof(float);
   g->rows = GE::R;
 }

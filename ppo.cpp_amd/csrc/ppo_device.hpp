@@ -212,12 +212,27 @@ PPO_DEV f4 mfma16(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x
 
 PPO_DEV float shfl_xor(float v, int m) { return __shfl_xor(v, m, 64); }
 
-// sum over the 4 lane-groups g (lanes j, j+16, j+32, j+48) — completes a per-row feature sum
-PPO_DEV float row_allreduce(float v) {
-  v += shfl_xor(v, 16);
-  v += shfl_xor(v, 32);
-  return v;
+// Cross-lane moves that stay off the LDS pipe: DPP inside 16-lane rows, v_permlane{16,32}_swap
+// across rows. xor16_sum(v) = v + v[lane ^ 16] and xor32_sum(v) = v + v[lane ^ 32], bitwise equal
+// to the shuffle forms (the swaps hand both operands to every lane; float + is commutative).
+template <int CTRL>
+PPO_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
+enum : int { kDppQuadXor1 = 0xB1, kDppQuadMirror = 0x1B, kDppHalfMirror = 0x141, kDppRowRor8 = 0x128 };
+PPO_DEV float xor16_sum(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                  false, false);
+  return __builtin_bit_cast(float, (unsigned)p[0]) + __builtin_bit_cast(float, (unsigned)p[1]);
+}
+PPO_DEV float xor32_sum(float v) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                  false, false);
+  return __builtin_bit_cast(float, (unsigned)p[0]) + __builtin_bit_cast(float, (unsigned)p[1]);
+}
+
+// sum over the 4 lane-groups g (lanes j, j+16, j+32, j+48) — completes a per-row feature sum
+PPO_DEV float row_allreduce(float v) { return xor32_sum(xor16_sum(v)); }
 
 PPO_DEV f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 PPO_DEV void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }

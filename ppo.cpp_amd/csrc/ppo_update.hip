@@ -222,6 +222,17 @@ PPO_DEV void ln_rows(const f4 (&z)[FT][RT], float (&mu)[RT], float (&rs)[RT], fl
   for (int rt = 0; rt < RT; ++rt) rs[rt] = 1.0f / sqrtf(s[rt] * invH + 1e-5f);
 }
 
+template <int CTRL, int LEN, int M>
+PPO_DEV void rs_stage(float (&x)[16], int j) {
+  const bool bit = (j & M) != 0;
+#pragma unroll
+  for (int i = 0; i < LEN / 2; ++i) {
+    const float lo = x[i], hi = x[i + LEN / 2];
+    const float keep = bit ? hi : lo, send = bit ? lo : hi;
+    x[i] = keep + dpp_f<CTRL>(send);
+  }
+}
+
 // column sums over this wave's rows of v(ft, rt, r), added to acc[fbase + feature]:
 // sum over rt in lane, then a 16-lane reduce-scatter (lane j ends with slot j).
 template <int FT, int RT, typename Fn>
@@ -237,16 +248,13 @@ PPO_DEV void col_sums(Fn v, float* acc, int fbase, int j, int g) {
       for (int rt = 1; rt < RT; ++rt) t += v(ft, rt, r);
       x[4 * ft + r] = t;
     }
-#pragma unroll
-  for (int m = 8, len = 16; m >= 1; m >>= 1, len >>= 1) {
-    const bool bit = (j & m) != 0;
-#pragma unroll
-    for (int i = 0; i < len / 2; ++i) {
-      const float lo = x[i], hi = x[i + len / 2];
-      const float keep = bit ? hi : lo, send = bit ? lo : hi;
-      x[i] = keep + shfl_xor(send, m);
-    }
-  }
+  // recursive halving over the 16 lanes j of each lane group with DPP partners: j ^ 8 (row_ror:8),
+  // the mirror in each half (row_half_mirror), the mirror in each quad, j ^ 1. Each stage pairs
+  // lanes of opposite bit m, so lane j still ends with slot j summed over all 16 lanes.
+  rs_stage<kDppRowRor8, 16, 8>(x, j);
+  rs_stage<kDppHalfMirror, 8, 4>(x, j);
+  rs_stage<kDppQuadMirror, 4, 2>(x, j);
+  rs_stage<kDppQuadXor1, 2, 1>(x, j);
   // slot j <-> feature 16 (j >> 2) + 4 g + (j & 3)
   acc[fbase + 16 * (j >> 2) + 4 * g + (j & 3)] += x[0];
 }

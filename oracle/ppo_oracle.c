@@ -702,3 +702,115 @@ void orc_env_step(orc_env_state* s, const float* actions, float lo, float hi, fl
     s->autoreset[e] = tr;
   }
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* CaRL CNN agent forward (include/carla/carla_model.h:222-318; carla_config.h defaults:        */
+/* "roach" encoder :71, no LayerNorm :78, no positional encoding :117)                          */
+/* ------------------------------------------------------------------------------------------ */
+
+/* nn::Conv2d(IC, OC, K).stride(S), no padding, + ReLU; in [IC][IH][IW] -> out [OC][OH][OW] */
+static void conv_relu(const float* in, int IC, int IH, int IW, const float* W, const float* b, int OC, int K, int S,
+                      int OH, int OW, float* out) {
+  for (int oc = 0; oc < OC; ++oc)
+    for (int oy = 0; oy < OH; ++oy)
+      for (int ox = 0; ox < OW; ++ox) {
+        double acc = 0;
+        for (int ic = 0; ic < IC; ++ic)
+          for (int ky = 0; ky < K; ++ky) {
+            const float* w = W + (((long)oc * IC + ic) * K + ky) * K;
+            const float* x = in + ((long)ic * IH + (long)oy * S + ky) * IW + (long)ox * S;
+            for (int kx = 0; kx < K; ++kx) acc += (double)w[kx] * (double)x[kx];
+          }
+        const float y = (float)(acc + (double)b[oc]);
+        out[((long)oc * OH + oy) * OW + ox] = y > 0.0f ? y : 0.0f;
+      }
+}
+static void linear_relu(const float* W, const float* b, const float* x, int in, int out, float* y) {
+  linear(W, b, x, in, out, y);
+  for (int o = 0; o < out; ++o) y[o] = y[o] > 0.0f ? y[o] : 0.0f;
+}
+
+int orc_carla_layout_init(ppo_carla_layout* L, int C, int IH, int IW, int NM, int NV, int A) {
+  return ppo_carla_layout_init(L, C, IH, IW, NM, NV, A);
+}
+
+void orc_carla_forward(const ppo_carla_layout* L, const float* P, float beta_min, int n, const uint8_t* bev,
+                       const float* meas, const float* vmeas, int mode, const float* action_in, uint64_t seed,
+                       int rank, long env_base, long step_id, float* action, float* logprob, float* entropy,
+                       float* value, float* alpha, float* beta, float* features) {
+  const int A = L->A, NM = L->NM, NV = L->NV;
+  long maxa = (long)L->C * L->IH * L->IW;
+  for (int i = 0; i < PPO_CARLA_NCONV; ++i) {
+    const long sz = (long)L->conv_oc[i] * L->conv_oh[i] * L->conv_ow[i];
+    if (sz > maxa) maxa = sz;
+  }
+  float* b0 = (float*)malloc(sizeof(float) * maxa);
+  float* b1 = (float*)malloc(sizeof(float) * maxa);
+  float enc[1024 + 256], s1[256], l1[512], feat[256 + 64], v1[256], v2[256], p1[256], p2[256];
+  const float hi = P[L->hi], lo = P[L->lo];
+  for (int r = 0; r < n; ++r) {
+    /* birdview = bev / 255 (carla_model.h:214-216, :223-224) */
+    const long npx = (long)L->C * L->IH * L->IW;
+    for (long i = 0; i < npx; ++i) b0[i] = (float)bev[(long)r * npx + i] / 255.0f;
+    float* cur = b0;
+    float* nxt = b1;
+    for (int i = 0; i < PPO_CARLA_NCONV; ++i) {
+      conv_relu(cur, L->conv_ic[i], L->conv_ih[i], L->conv_iw[i], P + L->conv_w[i], P + L->conv_b[i], L->conv_oc[i],
+                L->conv_k[i], L->conv_s[i], L->conv_oh[i], L->conv_ow[i], nxt);
+      float* t = cur; cur = nxt; nxt = t;
+    }
+    memcpy(enc, cur, sizeof(float) * 1024);                      /* flatten(x, 1): [C][H][W] order */
+    linear_relu(P + L->st_w[0], P + L->st_b[0], meas + (long)r * NM, NM, 256, s1);
+    linear_relu(P + L->st_w[1], P + L->st_b[1], s1, 256, 256, enc + 1024);
+    linear_relu(P + L->lin_w[0], P + L->lin_b[0], enc, 1024 + 256, 512, l1);
+    linear_relu(P + L->lin_w[1], P + L->lin_b[1], l1, 512, 256, feat);
+    if (features) memcpy(features + (long)r * 256, feat, sizeof(float) * 256);
+    /* value_head on cat(features, value_measurements) (:276-277) */
+    for (int k = 0; k < NV; ++k) feat[256 + k] = vmeas[(long)r * NV + k];
+    linear_relu(P + L->v_w[0], P + L->v_b[0], feat, 256 + NV, 256, v1);
+    linear_relu(P + L->v_w[1], P + L->v_b[1], v1, 256, 256, v2);
+    float vv;
+    linear(P + L->v_w[2], P + L->v_b[2], v2, 256, 1, &vv);
+    if (value) value[r] = vv;
+    /* policy head, Beta(softplus + beta_min) (:279-285) */
+    linear_relu(P + L->pi_w[0], P + L->pi_b[0], feat, 256, 256, p1);
+    linear_relu(P + L->pi_w[1], P + L->pi_b[1], p1, 256, 256, p2);
+    double lp = 0, ent = 0;
+    const long env = env_base + r;
+    for (int a = 0; a < A; ++a) {
+      float pm, ps;
+      linear(P + L->mu_w + (long)a * 256, P + L->mu_b + a, p2, 256, 1, &pm);
+      linear(P + L->sg_w + (long)a * 256, P + L->sg_b + a, p2, 256, 1, &ps);
+      const float al = softplus_f(pm) + beta_min, be = softplus_f(ps) + beta_min;
+      if (alpha) alpha[(long)r * A + a] = al;
+      if (beta) beta[(long)r * A + a] = be;
+      float s;
+      if (mode == PPO_CARLA_GIVEN) {                            /* scale_action (:251-260) */
+        s = (action_in[(long)r * A + a] - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+        s = fminf(fmaxf(s, 0.0f + 1e-7f), 1.0f + 1e-7f);
+      } else if (mode == PPO_CARLA_MEAN) {                      /* rl_utils.h:103-105 */
+        s = al / (al + be);
+      } else if (mode == PPO_CARLA_ROACH) {                     /* rl_utils.h:109-129 */
+        if (al > 1.0f && be > 1.0f) s = (al - 1.0f) / (al + be - 2.0f);
+        else if (al <= 1.0f && be > 1.0f) s = 0.0f;
+        else if (al > 1.0f && be <= 1.0f) s = 1.0f;
+        else s = al / (al + be);
+      } else {                                                  /* Dirichlet sample, Philox contract */
+        const float ga = gamma_mt(al, seed, rank, env, step_id, 0x10000u + (uint32_t)(a * 2 + 0) * 64u);
+        const float gb = gamma_mt(be, seed, rank, env, step_id, 0x10000u + (uint32_t)(a * 2 + 1) * 64u);
+        s = ga / (ga + gb);
+      }
+      const float ab = al + be;
+      float l = xlogy_f(al - 1.0f, s) + xlogy_f(be - 1.0f, 1.0f - s);
+      l += (float)(lgamma((double)ab) - (lgamma((double)al) + lgamma((double)be)));
+      lp += l;
+      ent += lgamma((double)al) + lgamma((double)be) - lgamma((double)ab) - (2.0 - ab) * orc_digamma(ab) -
+             ((al - 1.0) * orc_digamma(al) + (be - 1.0) * orc_digamma(be));
+      if (action) action[(long)r * A + a] = (s - 0.0f) / (1.0f - 0.0f) * (hi - lo) + lo;  /* unscale (:262-268) */
+    }
+    if (logprob) logprob[r] = (float)lp;
+    if (entropy) entropy[r] = (float)ent;
+  }
+  free(b0);
+  free(b1);
+}

@@ -15,6 +15,7 @@
 
 #include <stdint.h>
 #include "../include/ppo_layout.h"
+#include "../include/ppo_carla.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -99,6 +100,15 @@ void orc_env_reset(orc_env_state* s, int seed, float* obs_out);
 void orc_env_step(orc_env_state* s, const float* actions, float act_lo, float act_hi,
                   float* obs_out, float* reward, float* term, float* trunc,
                   float* info_ret, int* info_len);
+
+/* ---- CaRL CNN agent (a23): AgentImpl::forward, include/carla/carla_model.h:222-318 ----
+ * bev uint8 [n, C, IH, IW]; meas [n, NM]; vmeas [n, NV]; mode = PPO_CARLA_* (ppo_carla.h).
+ * Convolutions and Linear layers accumulate in double. Outputs may be NULL; features [n, 256]. */
+int orc_carla_layout_init(ppo_carla_layout* L, int C, int IH, int IW, int NM, int NV, int A);
+void orc_carla_forward(const ppo_carla_layout* L, const float* params, float beta_min, int n, const uint8_t* bev,
+                       const float* meas, const float* vmeas, int mode, const float* action_in, uint64_t seed,
+                       int rank, long env_base, long step_id, float* action, float* logprob, float* entropy,
+                       float* value, float* alpha, float* beta, float* features);
 
 #ifdef __cplusplus
 }

@@ -135,6 +135,81 @@ TORCH_MODULE(ACAgent);
 // ---------------------------------------------------------------------------------------------
 // Deterministic inputs
 // ---------------------------------------------------------------------------------------------
+// CaRL CNN agent (include/carla/carla_model.h:21-318 with the carla_config.h defaults: "roach"
+// encoder, no LayerNorm, no positional encoding). The reference header needs OpenCV and
+// boost::format, absent here, so the module is restated with the same LibTorch modules in the same
+// registration order; the Beta distribution is the reference's own rl_utils.h.
+struct CarlaAgentImpl : nn::Module {
+  nn::Sequential cnn{nullptr}, linear{nullptr}, state_linear{nullptr}, value_head{nullptr}, policy_head{nullptr},
+      dist_mu{nullptr}, dist_sigma{nullptr};
+  Tensor action_space_high, action_space_low;
+  float beta_min;
+  CarlaAgentImpl(int C, int NM, int NV, int A, float hi, float lo, float bmin) : beta_min(bmin) {
+    auto conv = [](int i, int o, int k, int st) { return nn::Conv2d(nn::Conv2dOptions(i, o, k).stride(st)); };
+    cnn = register_module("cnn", nn::Sequential(conv(C, 8, 5, 2), nn::ReLU(), conv(8, 16, 5, 2), nn::ReLU(),
+                                                 conv(16, 32, 5, 2), nn::ReLU(), conv(32, 64, 3, 2), nn::ReLU(),
+                                                 conv(64, 128, 3, 2), nn::ReLU(), conv(128, 256, 3, 1), nn::ReLU()));
+    linear = register_module("linear", nn::Sequential(nn::Linear(1024 + 256, 512), nn::ReLU(), nn::Linear(512, 256),
+                                                      nn::ReLU()));
+    state_linear = register_module("state_linear", nn::Sequential(nn::Linear(NM, 256), nn::ReLU(),
+                                                                  nn::Linear(256, 256), nn::ReLU()));
+    value_head = register_module("value_head", nn::Sequential(nn::Linear(256 + NV, 256), nn::ReLU(),
+                                                              nn::Linear(256, 256), nn::ReLU(), nn::Linear(256, 1)));
+    policy_head = register_module("policy_head", nn::Sequential(nn::Linear(256, 256), nn::ReLU(),
+                                                                nn::Linear(256, 256), nn::ReLU()));
+    dist_mu = register_module("dist_mu", nn::Sequential(nn::Linear(256, A)));
+    dist_sigma = register_module("dist_sigma", nn::Sequential(nn::Linear(256, A)));
+    action_space_high = register_parameter("action_space_high", torch::tensor(hi), false);
+    action_space_low = register_parameter("action_space_low", torch::tensor(lo), false);
+  }
+  Tensor encoder(const Tensor& bev_u8, const Tensor& meas) {  // carla_model.h:222-242
+    Tensor birdview = bev_u8.to(torch::kFloat32) / 255.0f;
+    Tensor x = torch::flatten(cnn->forward(birdview), 1);
+    Tensor latent_state = state_linear->forward(meas);
+    return linear->forward(torch::cat({x, latent_state}, 1));
+  }
+  // carla_model.h:270-318; sample types "mean", "roach", or a given action
+  std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> forward(const Tensor& bev, const Tensor& meas,
+                                                                             const Tensor& vmeas, Tensor actions,
+                                                                             const std::string& mode) {
+    Tensor features = encoder(bev, meas);
+    Tensor values = value_head->forward(torch::cat({features, vmeas}, 1));
+    Tensor latent_pi = policy_head->forward(features);
+    Tensor mu = nn::functional::softplus(dist_mu->forward(latent_pi)) + beta_min;
+    Tensor sigma = nn::functional::softplus(dist_sigma->forward(latent_pi)) + beta_min;
+    const Beta dist(mu, sigma);
+    if (mode == "mean") actions = dist.mean();
+    else if (mode == "roach") actions = dist.roach_deterministic();
+    else {
+      actions = (actions - action_space_low) / (action_space_high - action_space_low) * (1.0f - 0.0f) + 0.0f;
+      actions = torch::clamp(actions, 0.0f + 1e-7f, 1.0f + 1e-7f);
+    }
+    Tensor log_prob = dist.log_prob(actions).sum(1);
+    actions = (actions - 0.0f) / (1.0f - 0.0f) * (action_space_high - action_space_low) + action_space_low;
+    Tensor entropy = dist.entropy().sum(1);
+    return {actions, log_prob, entropy, values, mu, sigma, features};
+  }
+};
+TORCH_MODULE(CarlaAgent);
+
+// Deterministic CaRL inputs / parameters shared with tests/carla_inputs.py (so the 1+ MB image
+// batch and the 1.2 M parameters need not be stored): u = (mix32(mix32(stream * 0x9E3779B1) ^ i)
+// >> 8 + 0.5) * 2^-24, mix32 = the murmur3 finalizer (oracle orc_mix32).
+static uint32_t hmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85EBCA6Bu;
+  h ^= h >> 13; h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+static uint32_t hbits(uint32_t stream, uint32_t i) { return hmix32(hmix32(stream * 0x9E3779B1u) ^ i); }
+static float hu01(uint32_t stream, uint32_t i) { return ((float)(hbits(stream, i) >> 8) + 0.5f) * 5.9604644775390625e-8f; }
+static Tensor hunif(uint32_t stream, std::vector<int64_t> shape, float lo, float hi) {
+  Tensor t = torch::empty(shape, torch::kFloat32);
+  float* p = t.data_ptr<float>();
+  for (int64_t i = 0; i < t.numel(); ++i) p[i] = lo + (hi - lo) * hu01(stream, (uint32_t)i);
+  return t;
+}
+
 static std::mt19937 g_rng(1234);
 static Tensor randn(std::vector<int64_t> shape, float scale = 1.0f) {
   std::normal_distribution<float> d(0.0f, 1.0f);
@@ -488,6 +563,53 @@ int main(int argc, char** argv) {
     dump("gae", "rewards", rewards); dump("gae", "values", values); dump("gae", "dones", dones);
     dump("gae", "next_value", next_value); dump("gae", "next_done", next_done);
     dump("gae", "advantages", advantages); dump("gae", "returns", returns);
+    end_case();
+  }
+
+  // ---- CaRL CNN agent forward (carla_model.h:270-318), SURVEY §8 a23 ----------------------------
+  {
+    torch::NoGradGuard ng;
+    const int N = 3, C = 15, HW = 192, NM = 8, NV = 3, A = 2;
+    CarlaAgent agent(C, NM, NV, A, 1.0f, -1.0f, 1.0f);
+    // parameters: tensor t (named_parameters order) from stream 1000 + t; weights uniform with
+    // He scale sqrt(6 / fan_in), biases uniform in [-0.1, 0.1]; action space [-1, 1]
+    std::vector<Tensor> flat;
+    std::string names = "[";
+    int t = 0;
+    for (auto& kv : agent->named_parameters()) {
+      Tensor p = kv.value();
+      Tensor v;
+      if (kv.key() == "action_space_high") v = torch::tensor(1.0f);
+      else if (kv.key() == "action_space_low") v = torch::tensor(-1.0f);
+      else if (p.dim() >= 2) {
+        const float fan_in = (float)(p.numel() / p.size(0));
+        const float a = std::sqrt(6.0f / fan_in);
+        v = hunif(1000 + t, p.sizes().vec(), -a, a);
+      } else v = hunif(1000 + t, p.sizes().vec(), -0.1f, 0.1f);
+      p.copy_(v.reshape(p.sizes()));
+      flat.push_back(p.detach().reshape({-1}).clone());
+      names += std::string(t ? ", " : "") + "[\"" + kv.key() + "\", " + std::to_string(p.numel()) + "]";
+      ++t;
+    }
+    names += "]";
+    // inputs: bev bytes = top 8 bits of hbits(1, i); meas, vmeas uniform [-1, 1) (streams 2, 3);
+    // given actions uniform [-0.98, 0.98) (stream 4)
+    Tensor bev = torch::empty({N, C, HW, HW}, torch::kUInt8);
+    uint8_t* bp = bev.data_ptr<uint8_t>();
+    for (int64_t i = 0; i < bev.numel(); ++i) bp[i] = (uint8_t)(hbits(1, (uint32_t)i) >> 24);
+    Tensor meas = hunif(2, {N, NM}, -1.0f, 1.0f), vmeas = hunif(3, {N, NV}, -1.0f, 1.0f);
+    Tensor act = hunif(4, {N, A}, -0.98f, 0.98f);
+    begin_case("carla_act", "{\"N\": 3, \"C\": 15, \"H\": 192, \"W\": 192, \"NM\": 8, \"NV\": 3, \"A\": 2, "
+                            "\"beta_min\": 1.0, \"P\": " + std::to_string(torch::cat(flat).numel()) +
+                            ", \"params\": " + names + "}");
+    auto [a, lp, ent, v, mu, sg, feat] = agent->forward(bev, meas, vmeas, act, "given");
+    dump("carla_act", "logprob", lp); dump("carla_act", "entropy", ent); dump("carla_act", "value", v.view(-1));
+    dump("carla_act", "alpha", mu); dump("carla_act", "beta", sg); dump("carla_act", "action_roundtrip", a);
+    dump("carla_act", "features", feat);
+    auto [am, lpm, entm, vm, mum, sgm, fm] = agent->forward(bev, meas, vmeas, Tensor(), "mean");
+    dump("carla_act", "mean_action", am); dump("carla_act", "mean_logprob", lpm);
+    auto [ar, lpr, entr, vr, mur, sgr, fr] = agent->forward(bev, meas, vmeas, Tensor(), "roach");
+    dump("carla_act", "roach_action", ar); dump("carla_act", "roach_logprob", lpr);
     end_case();
   }
 

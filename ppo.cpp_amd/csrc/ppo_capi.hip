@@ -41,6 +41,7 @@ static int fail(const std::string& msg, int code = -1) {
   } while (0)
 
 extern "C" const char* ppo_last_error(void) { return g_err.c_str(); }
+int ppo_fail(const std::string& msg, int code) { return fail(msg, code); }
 extern "C" const char* ppo_version(void) { return "ppo_hip 0.1 (gfx950)"; }
 
 // ------------------------------------------------------------------------------------------

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "ppo_device.hpp"
 #include "ppo_packed.hpp"
 
@@ -145,6 +147,9 @@ struct SynthArgs {
   float* fin_len;
   float* fin_cnt;
 };
+
+// sets the thread-local ppo_last_error() message and returns code (ppo_capi.hip)
+int ppo_fail(const std::string& msg, int code);
 
 int launch_act(const ActArgs& a, hipStream_t s);
 int launch_act3(const ActArgs& a, hipStream_t s);

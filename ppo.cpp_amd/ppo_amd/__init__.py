@@ -64,9 +64,35 @@ class Layout(C.Structure):
                 ("t_off", C.c_long * MAX_T), ("t_len", C.c_long * MAX_T), ("t_grad", C.c_int * MAX_T)]
 
 
+MAX_CT, NCONV = 40, 6
+
+
+class CarlaLayout(C.Structure):  # include/ppo_carla.h
+    _fields_ = [("C", C.c_int), ("IH", C.c_int), ("IW", C.c_int), ("NM", C.c_int), ("NV", C.c_int), ("A", C.c_int),
+                ("P", C.c_long), ("hi", C.c_long), ("lo", C.c_long),
+                ("conv_w", C.c_long * NCONV), ("conv_b", C.c_long * NCONV),
+                ("conv_ic", C.c_int * NCONV), ("conv_oc", C.c_int * NCONV), ("conv_k", C.c_int * NCONV),
+                ("conv_s", C.c_int * NCONV), ("conv_ih", C.c_int * NCONV), ("conv_iw", C.c_int * NCONV),
+                ("conv_oh", C.c_int * NCONV), ("conv_ow", C.c_int * NCONV),
+                ("lin_w", C.c_long * 2), ("lin_b", C.c_long * 2), ("st_w", C.c_long * 2), ("st_b", C.c_long * 2),
+                ("v_w", C.c_long * 3), ("v_b", C.c_long * 3), ("pi_w", C.c_long * 2), ("pi_b", C.c_long * 2),
+                ("mu_w", C.c_long), ("mu_b", C.c_long), ("sg_w", C.c_long), ("sg_b", C.c_long),
+                ("ntensors", C.c_int), ("t_off", C.c_long * MAX_CT), ("t_len", C.c_long * MAX_CT),
+                ("t_grad", C.c_int * MAX_CT)]
+
+
+class CarlaConfig(C.Structure):  # ppo_carla_config; defaults = carla_config.h
+    _fields_ = [("obs_channels", C.c_int), ("bev_h", C.c_int), ("bev_w", C.c_int), ("num_measurements", C.c_int),
+                ("num_value_measurements", C.c_int), ("action_dim", C.c_int), ("beta_min", C.c_float),
+                ("max_batch", C.c_int), ("seed", C.c_uint64), ("rank", C.c_int)]
+
+
+PPO_CARLA_SAMPLE, PPO_CARLA_MEAN, PPO_CARLA_GIVEN, PPO_CARLA_ROACH = range(4)
+
 _LIB = None
 
-# (name, restype, argtypes) of every entry point declared in include/ppo_hip.h / ppo_synth_env.h
+# (name, restype, argtypes) of every entry point declared in include/ppo_hip.h / ppo_synth_env.h /
+# ppo_carla.h
 _VP, _FP, _I, _L, _F, _SZ = C.c_void_p, C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_size_t
 SYMBOLS = [
     ("ppo_last_error", C.c_char_p, []),
@@ -113,6 +139,11 @@ SYMBOLS = [
     ("psyn_step", _I, [_VP, _I, _I, _FP, _F, _F, _FP, _FP, _FP, _VP]),
     ("psyn_episode_stats", _I, [_VP, C.POINTER(_F), C.POINTER(_F), C.POINTER(_F)]),
     ("ppo_rollout_synth", _I, [_VP, _VP, _FP, _FP, _FP, _FP]),
+    ("ppo_carla_create", _I, [C.POINTER(CarlaConfig), _I, C.POINTER(_VP)]),
+    ("ppo_carla_destroy", _I, [_VP]),
+    ("ppo_carla_get_layout", _I, [_VP, C.POINTER(CarlaLayout)]),
+    ("ppo_carla_load_params", _I, [_VP, _FP, _L]),
+    ("ppo_carla_forward", _I, [_VP, _I, _VP, _FP, _FP, _I, _FP, _L, _L, _FP, _FP, _FP, _FP, _FP, _FP, _VP]),
 ]
 
 
@@ -417,6 +448,50 @@ class Agent:
     def comm_allreduce(self, buf: DeviceArray, average=True):
         check(lib().ppo_comm_allreduce(self.h, buf.ptr, int(np.prod(buf.shape)), int(average)))
         self.sync()
+
+
+class CarlaAgent:
+    """The CaRL CNN agent (include/carla/carla_model.h AgentImpl) on the device.
+    forward() mirrors AgentImpl::forward: returns (actions, log_prob, entropy, values, alpha, beta)
+    as DeviceArrays; sample_type is "sample", "mean", "roach" or a given `actions` array."""
+
+    _MODES = {"sample": PPO_CARLA_SAMPLE, "mean": PPO_CARLA_MEAN, "roach": PPO_CARLA_ROACH}
+
+    def __init__(self, max_batch, obs_channels=15, bev=192, num_measurements=8, num_value_measurements=3,
+                 action_dim=2, beta_min=1.0, seed=1, rank=0, device=0):
+        self.cfg = CarlaConfig(obs_channels, bev, bev, num_measurements, num_value_measurements, action_dim, beta_min,
+                               max_batch, seed, rank)
+        self._h = C.c_void_p()
+        check(lib().ppo_carla_create(C.byref(self.cfg), device, C.byref(self._h)))
+        self.layout = CarlaLayout()
+        check(lib().ppo_carla_get_layout(self._h, C.byref(self.layout)))
+
+    def close(self):
+        if self._h:
+            lib().ppo_carla_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def load_params(self, flat):
+        flat = np.ascontiguousarray(flat, np.float32)
+        check(lib().ppo_carla_load_params(self._h, flat.ctypes.data_as(C.c_void_p), flat.size))
+
+    def forward(self, bev: DeviceArray, meas: DeviceArray, vmeas: DeviceArray, actions: DeviceArray | None = None,
+                sample_type="sample", env_base=0, step_id=0):
+        n, A = bev.shape[0], self.layout.A
+        mode = PPO_CARLA_GIVEN if actions is not None else self._MODES[sample_type]
+        out = [DeviceArray((n, A)), DeviceArray((n,)), DeviceArray((n,)), DeviceArray((n,)), DeviceArray((n, A)),
+               DeviceArray((n, A))]
+        check(lib().ppo_carla_forward(self._h, n, bev.ptr, meas.ptr, vmeas.ptr, mode,
+                                      actions.ptr if actions is not None else None, env_base, step_id,
+                                      *[o.ptr for o in out], None))
+        check(lib().ppo_device_sync())
+        return tuple(out)
 
 
 class SynthEnv:

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Forward throughput of the CaRL CNN agent (BASELINE config 5 shapes: bev uint8
+[n, 15, 192, 192], 8 measurements, 3 value measurements, 2 actions) on one GPU: samples/s of
+ppo_carla_forward with inputs resident in HBM, and the algorithmic MFMA rate (87.9 MFLOP per sample,
+SURVEY §8d)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ppo.cpp_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import numpy as np  # noqa: E402
+
+import ppo_amd  # noqa: E402
+import carla_inputs as CI  # noqa: E402
+
+FLOP_PER_SAMPLE = 87_907_008  # SURVEY §8d (conv + MLP forward, 2 K N per layer)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, nargs="+", default=[32, 256])
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    ppo_amd.set_device(0)
+    L = CI.layout()
+    p = CI.params(L)
+    for n in args.batch:
+        ag = ppo_amd.CarlaAgent(max_batch=n)
+        ag.load_params(p)
+        bev, meas, vmeas, _ = CI.inputs(n)
+        d = [ppo_amd.DeviceArray.from_numpy(bev, np.uint8), ppo_amd.DeviceArray.from_numpy(meas),
+             ppo_amd.DeviceArray.from_numpy(vmeas)]
+        for _ in range(3):
+            ag.forward(*d, sample_type="sample")
+        t0 = time.perf_counter()
+        for i in range(args.iters):
+            ag.forward(*d, sample_type="sample", step_id=i)
+        dt = (time.perf_counter() - t0) / args.iters
+        print(json.dumps({"workload": "carla_forward", "batch": n, "ms_per_forward": round(dt * 1e3, 3),
+                          "samples_per_s": round(n / dt, 1),
+                          "tflops": round(n * FLOP_PER_SAMPLE / dt / 1e12, 2)}), flush=True)
+        ag.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -12,11 +12,12 @@ LIB = os.path.join(ROOT, "ppo.cpp_amd", "lib", "libppo_hip.so")
 
 def declared_functions():
     names = []
-    for h in ("ppo_hip.h", "ppo_synth_env.h"):
+    for h in ("ppo_hip.h", "ppo_synth_env.h", "ppo_carla.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         for m in re.finditer(r"^\s*[A-Za-z_][\w\s\*]*?\b((?:ppo|psyn)_\w+)\s*\(", src, flags=re.M):
-            names.append(m.group(1))
+            if "static" not in m.group(0):  # header-only helpers (static inline layout initialisers)
+                names.append(m.group(1))
     return sorted(set(names))
 
 

@@ -41,7 +41,8 @@ struct ConvArgs {
 constexpr int kConvWaves = 4;
 constexpr int kMaxKTab = 2048;  // im2col offset table entries (IC * K * K <= 1280 here)
 
-template <int NOT>
+// a wave: NP tiles of 16 output pixels x NOT tiles of 16 output channels
+template <int NOT, int NP>
 __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
   __shared__ int koff[kMaxKTab];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
@@ -53,18 +54,26 @@ __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
   __syncthreads();
   const int P = a.OH * a.OW;
   const long Q = (long)a.n * P;
-  const long q0 = ((long)blockIdx.x * kConvWaves + wave) * 16;
+  const long q0 = ((long)blockIdx.x * kConvWaves + wave) * 16 * NP;
   if (q0 >= Q) return;
-  // this lane's output pixel (B-operand column j)
-  const long q = q0 + j;
-  const bool qv = q < Q;
-  const long s = qv ? q / P : 0;
-  const int p = qv ? (int)(q - s * P) : 0, oy = p / a.OW, ox = p - oy * a.OW;
-  const long xbase = s * a.in_stride + (long)oy * a.S * a.IW + (long)ox * a.S;
-  const int oc0 = blockIdx.y * 16 * NOT;
-  f4 acc[NOT];
+  // this lane's output pixels (B-operand column j of each pixel tile)
+  long xbase[NP], obase[NP];
+  bool qv[NP];
 #pragma unroll
-  for (int t = 0; t < NOT; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < NP; ++u) {
+    const long q = q0 + 16 * u + j;
+    qv[u] = q < Q;
+    const long s = qv[u] ? q / P : 0;
+    const int p = qv[u] ? (int)(q - s * P) : 0, oy = p / a.OW, ox = p - oy * a.OW;
+    xbase[u] = s * a.in_stride + (long)oy * a.S * a.IW + (long)ox * a.S;
+    obase[u] = s * a.out_stride + p;
+  }
+  const int oc0 = blockIdx.y * 16 * NOT;
+  f4 acc[NOT][NP];
+#pragma unroll
+  for (int t = 0; t < NOT; ++t)
+#pragma unroll
+    for (int u = 0; u < NP; ++u) acc[t][u] = f4{0.f, 0.f, 0.f, 0.f};
   const float* wrow[NOT];
   bool ocv[NOT];
 #pragma unroll
@@ -73,35 +82,41 @@ __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
     ocv[t] = oc < a.OC;
     wrow[t] = a.W + (long)(ocv[t] ? oc : 0) * Kt;
   }
-#pragma unroll 4
+#pragma unroll 8
   for (int k0 = 0; k0 < Kt; k0 += 4) {
     const int k = k0 + g;
     const bool kv = k < Kt;
-    float x = 0.f;
-    if (kv && qv) {
-      if (a.in_u8) x = (float)a.in_u8[xbase + koff[k]] / 255.0f;
-      else x = a.in_f[xbase + koff[k]];
+    const int ko = kv ? koff[k] : 0;
+    float x[NP], w[NOT];
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      x[u] = 0.f;
+      if (kv && qv[u]) x[u] = a.in_u8 ? (float)a.in_u8[xbase[u] + ko] / 255.0f : a.in_f[xbase[u] + ko];
     }
 #pragma unroll
-    for (int t = 0; t < NOT; ++t) {
-      const float w = (kv && ocv[t]) ? wrow[t][k] : 0.f;
-      acc[t] = mfma16(w, x, acc[t]);
-    }
+    for (int t = 0; t < NOT; ++t) w[t] = (kv && ocv[t]) ? wrow[t][k] : 0.f;
+#pragma unroll
+    for (int t = 0; t < NOT; ++t)
+#pragma unroll
+      for (int u = 0; u < NP; ++u) acc[t][u] = mfma16(w[t], x[u], acc[t][u]);
   }
-  // lane (j, g) holds out channel oc0 + 16t + 4g + r of pixel q0 + j
-  if (!qv) return;
-  float* o = a.out + s * a.out_stride + p;
+  // lane (j, g) holds out channel oc0 + 16t + 4g + r of pixel q0 + 16u + j
 #pragma unroll
-  for (int t = 0; t < NOT; ++t)
+  for (int u = 0; u < NP; ++u) {
+    if (!qv[u]) continue;
+    float* o = a.out + obase[u];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int oc = oc0 + 16 * t + 4 * g + r;
-      if (oc < a.OC) {
-        float y = acc[t][r] + a.b[oc];
-        if (a.relu) y = y > 0.0f ? y : 0.0f;
-        o[(long)oc * P] = y;
+    for (int t = 0; t < NOT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int oc = oc0 + 16 * t + 4 * g + r;
+        if (oc < a.OC) {
+          float y = acc[t][u][r] + a.b[oc];
+          if (a.relu) y = y > 0.0f ? y : 0.0f;
+          o[(long)oc * P] = y;
+        }
       }
-    }
+  }
 }
 
 // value_measurements -> columns [256, 256 + NV) of the value-head input (carla_model.h:276)
@@ -178,13 +193,19 @@ __global__ __launch_bounds__(64) void k_carla_head(HeadArgs h) {
 int launch_conv(const ConvArgs& a, hipStream_t s) {
   if (a.IC * a.K * a.K > kMaxKTab) return -1;
   const long Q = (long)a.n * a.OH * a.OW;
-  const unsigned gx = (unsigned)((Q + 16 * kConvWaves - 1) / (16 * kConvWaves));
+  // several pixel tiles per wave where there are pixels to spare (B-operand reuse of every weight
+  // load), one where the layer is narrow (Linear layers, the last convolutions)
+  const int np = Q >= 16L * 4 * 2048 ? 4 : 1;
+  const unsigned gx = (unsigned)((Q + 16 * kConvWaves * np - 1) / (16 * kConvWaves * np));
   if (a.OC >= 64) {
-    hipLaunchKernelGGL(k_conv<4>, dim3(gx, (a.OC + 63) / 64), dim3(256), 0, s, a);
+    if (np == 4) hipLaunchKernelGGL((k_conv<4, 4>), dim3(gx, (a.OC + 63) / 64), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_conv<4, 1>), dim3(gx, (a.OC + 63) / 64), dim3(256), 0, s, a);
   } else if (a.OC >= 32) {
-    hipLaunchKernelGGL(k_conv<2>, dim3(gx, (a.OC + 31) / 32), dim3(256), 0, s, a);
+    if (np == 4) hipLaunchKernelGGL((k_conv<2, 4>), dim3(gx, (a.OC + 31) / 32), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_conv<2, 1>), dim3(gx, (a.OC + 31) / 32), dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL(k_conv<1>, dim3(gx, (a.OC + 15) / 16), dim3(256), 0, s, a);
+    if (np == 4) hipLaunchKernelGGL((k_conv<1, 4>), dim3(gx, (a.OC + 15) / 16), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_conv<1, 1>), dim3(gx, (a.OC + 15) / 16), dim3(256), 0, s, a);
   }
   return 0;
 }

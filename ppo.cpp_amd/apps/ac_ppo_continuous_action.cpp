@@ -161,7 +161,7 @@ int main(int argc, const char** argv) {
   const fs::path exe = fs::canonical(argv[0]);
   const fs::path exp_folder = exe.parent_path() / ".." / "models" / config.exp_name;
   fs::create_directories(exp_folder);
-  ScalarLog logger(exp_folder / ("scalars_" + std::to_string(rank) + ".jsonl"));
+  RunLog logger(exp_folder, "tfevents_logs_" + std::to_string(rank) + ".pb", "scalars_" + std::to_string(rank) + ".jsonl");
 
   const int E = (int)config.num_envs_per_device, T = (int)config.num_steps;
   const bool device_env = config.env_backend == "device";

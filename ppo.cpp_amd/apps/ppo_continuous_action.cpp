@@ -107,7 +107,7 @@ int main(int argc, const char** argv) {
   const fs::path exe = fs::canonical(argv[0]);
   const fs::path exp_folder = exe.parent_path() / ".." / "models" / config.exp_name;
   fs::create_directories(exp_folder);
-  ScalarLog logger(exp_folder / "scalars.jsonl");
+  RunLog logger(exp_folder, "tfevents_logs.pb", "scalars.jsonl");
 
   std::vector<std::shared_ptr<gymcpp::EnvironmentWrapper>> env_array;
   try {

@@ -27,6 +27,7 @@
 #include "../../include/ppo_synth_env.h"
 #include "../gymcpp/gym.h"
 #include "../gymcpp/synthetic_cheetah.h"
+#include "tensorboard_logger.h"
 #include "../gymcpp/wrappers.h"
 
 namespace app {
@@ -217,6 +218,21 @@ class ScalarLog {
   void add_scalar(const std::string& tag, long step, double v) {
     f_ << "{\"tag\": \"" << tag << "\", \"step\": " << step << ", \"value\": " << v << "}\n";
     f_.flush();
+  }
+};
+
+// The reference's TensorBoard event file (tfevents_logs[_rank].pb, ppo:281 / ac:420) plus the same
+// scalars as JSON lines. Steps go to the event file as int, as the reference's static_cast<int>.
+class RunLog {
+  TensorBoardLogger tb_;
+  ScalarLog js_;
+
+ public:
+  RunLog(const std::filesystem::path& dir, const std::string& tfevents_name, const std::string& jsonl_name)
+      : tb_((dir / tfevents_name).string()), js_(dir / jsonl_name) {}
+  void add_scalar(const std::string& tag, long step, double v) {
+    tb_.add_scalar(tag, static_cast<int>(step), v);
+    js_.add_scalar(tag, step, v);
   }
 };
 

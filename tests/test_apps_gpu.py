@@ -38,6 +38,15 @@ def test_ppo_cli_runs():
     assert "SPS:" in out
     p = np.fromfile(os.path.join(MODELS, "t_ppo_cli_3", "model_final.bin"), np.float32)
     assert p.size > 0 and np.isfinite(p).all()
+    # the reference's TensorBoard event file (ppo:281), one record per scalar of the JSON-lines log
+    ev = open(os.path.join(MODELS, "t_ppo_cli_3", "tfevents_logs.pb"), "rb").read()
+    n_lines = len(open(os.path.join(MODELS, "t_ppo_cli_3", "scalars.jsonl")).read().splitlines())
+    pos, records = 0, 0
+    while pos < len(ev):
+        (n,) = np.frombuffer(ev[pos:pos + 8], np.uint64)
+        pos += 12 + int(n) + 4
+        records += 1
+    assert pos == len(ev) and records == n_lines > 0
 
 
 @pytest.mark.gpu

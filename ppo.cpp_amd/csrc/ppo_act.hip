@@ -340,8 +340,8 @@ __global__ __launch_bounds__(512) void k_act3(ActArgs a) {
       float* it = ITM + ((r * A + ai) * 2 + which) * 4;
       it[0] = c;
       it[1] = gs;
-      it[2] = lgammaf(c);
-      it[3] = digammaf_(c);
+      float tg_unused;
+      lgamma_digamma_trigamma(c, it[2], it[3], tg_unused);
     }
     lds_barrier();
     // stage 2: combine per (row, action)
@@ -364,9 +364,11 @@ __global__ __launch_bounds__(512) void k_act3(ActArgs a) {
         sv = ia[1] / (ia[1] + ib[1]);
       }
       const float ab = al + be;
-      const float lga = ia[2], lgb = ib[2], lgab = lgammaf(ab);
+      float lgab, psab, tab_unused;
+      lgamma_digamma_trigamma(ab, lgab, psab, tab_unused);
+      const float lga = ia[2], lgb = ib[2];
       const float lp = xlogyf_(al - 1.0f, sv) + xlogyf_(be - 1.0f, 1.0f - sv) + (lgab - (lga + lgb));
-      const float ent = (lga + lgb) - lgab - (2.0f - ab) * digammaf_(ab) - ((al - 1.0f) * ia[3] + (be - 1.0f) * ib[3]);
+      const float ent = (lga + lgb) - lgab - (2.0f - ab) * psab - ((al - 1.0f) * ia[3] + (be - 1.0f) * ib[3]);
       const float act = (sv - 0.0f) / (1.0f - 0.0f) * (hi - lo) + lo;
       LPE[idx * 2 + 0] = lp;
       LPE[idx * 2 + 1] = ent;

@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import numpy as np  # noqa: E402
 
-import ppo_amd  # noqa: E402  (loads libppo_hip.so before torch, so one HIP runtime serves both)
+import ppo_amd  # noqa: E402  (imports torch before loading libppo_hip.so: one HIP runtime serves both)
 
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector peak (spec)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)

@@ -412,6 +412,38 @@ int main(int argc, char** argv) {
     int n_act = argc > 6 ? std::atoi(argv[6]) : 2000;
     return bench_main(E, T, MB, EP, n_act);
   }
+  if (argc > 1 && std::string(argv[1]) == "--pth-load") {
+    // --pth-load <ppo|ac> O A H <model.pth> <optimizer.pth> <out_dir>: torch::load both archives
+    // into a fresh agent / Adam (ac_ppo_carla.cpp:236-251) and dump what LibTorch read
+    if (argc < 9) { std::fprintf(stderr, "usage: --pth-load <ppo|ac> O A H model optimizer out_dir\n"); return 2; }
+    const std::string kind = argv[2];
+    const int O = std::atoi(argv[3]), A = std::atoi(argv[4]), H = std::atoi(argv[5]);
+    g_out = argv[8];
+    std::filesystem::create_directories(g_out);
+    g_manifest << "{\n";
+    auto run = [&](auto& agent) {
+      torch::optim::Adam opt(agent->parameters(), torch::optim::AdamOptions(1e-3));
+      torch::load(agent, argv[6]);
+      torch::load(opt, argv[7]);
+      long step = 0;
+      for (auto& p : opt.param_groups()[0].params()) {
+        auto it = opt.state().find(p.unsafeGetTensorImpl());
+        if (it != opt.state().end()) { step = static_cast<torch::optim::AdamParamState&>(*it->second).step(); break; }
+      }
+      const auto& o = static_cast<torch::optim::AdamOptions&>(opt.param_groups()[0].options());
+      begin_case("loaded", "{\"step\": " + std::to_string(step) + ", \"lr\": " + std::to_string(o.lr()) +
+                           ", \"eps\": " + std::to_string(o.eps()) + "}");
+      dump("loaded", "params", flat_params(*agent));
+      dump("loaded", "adam_m", flat_state(opt, false));
+      dump("loaded", "adam_v", flat_state(opt, true));
+      end_case();
+    };
+    if (kind == "ppo") { PPOAgent agent(O, A, H); run(agent); }
+    else { ACAgent agent(O, A, H, 1.0f, -1.0f, torch::zeros({O}), torch::ones({O})); run(agent); }
+    g_manifest << "\n}\n";
+    std::ofstream(g_out + "/manifest.json") << g_manifest.str();
+    return 0;
+  }
   g_out = argc > 1 ? argv[1] : "tests/golden";
   std::filesystem::create_directories(g_out);
   g_manifest << "{\n";
@@ -623,6 +655,47 @@ int main(int argc, char** argv) {
     dump("beta_dist", "log_prob", b.log_prob(xs)); dump("beta_dist", "entropy", b.entropy());
     dump("beta_dist", "mean", b.mean());
     end_case();
+  }
+
+  // ---- LibTorch checkpoints: torch::save of agent + Adam (save_state, ppo:173-180), SURVEY §8 f-2 ----
+  // Small agents (O=5, A=2, H=16) after two Adam steps on a surrogate loss; model.pth and
+  // optimizer.pth are the fixtures, params / adam_m / adam_v their flat contents.
+  {
+    const int Op = 5, Ap = 2, Hp = 16, Mp = 8;
+    auto pth_case = [&](const std::string& cname, auto& agent, auto&& loss_fn) {
+      std::string names;
+      set_params(*agent, names);
+      torch::optim::Adam opt(agent->parameters(), torch::optim::AdamOptions(2.5e-4).eps(1e-5));
+      for (int s = 0; s < 2; ++s) {
+        opt.zero_grad();
+        loss_fn().backward();
+        opt.step();
+      }
+      begin_case(cname, "{\"O\": 5, \"A\": 2, \"H\": 16, \"steps\": 2, \"lr\": 0.00025, \"eps\": 1e-05, "
+                        "\"params\": " + names + "}");
+      dump(cname, "params", flat_params(*agent));
+      dump(cname, "adam_m", flat_state(opt, false));
+      dump(cname, "adam_v", flat_state(opt, true));
+      end_case();
+      torch::save(agent, g_out + "/" + cname + "/model.pth");
+      torch::save(opt, g_out + "/" + cname + "/optimizer.pth");
+    };
+    {
+      PPOAgent agent(Op, Ap, Hp);
+      Tensor x = randn({Mp, Op}), act = randn({Mp, Ap}, 0.8f);
+      pth_case("pth_ppo", agent, [&] {
+        auto [a, lp, ent, v, mu] = agent->get_action_and_value(x, act);
+        return -lp.mean() + v.square().mean() - 0.01f * ent.mean();
+      });
+    }
+    {
+      ACAgent agent(Op, Ap, Hp, 1.0f, -1.0f, torch::zeros({Op}), torch::ones({Op}));
+      Tensor x = randn({Mp, Op}), act = randu({Mp, Ap}, -0.98f, 0.98f);
+      pth_case("pth_ac", agent, [&] {
+        auto [a, lp, ent, v, al, be] = agent->get_action_and_value(x, act, "given");
+        return -lp.mean() + v.square().mean() - 0.01f * ent.mean();
+      });
+    }
   }
 
   g_manifest << "\n}\n";

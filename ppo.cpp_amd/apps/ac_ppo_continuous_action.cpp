@@ -254,6 +254,7 @@ int main(int argc, const char** argv) {
     long global_step = 0;
     const auto start_time = std::chrono::high_resolution_clock::now();
     ppo_update_stats st{};
+    double last_lr = config.learning_rate;  // the optimizer's lr at save time
     for (unsigned iteration = 0; iteration < config.num_iterations; ++iteration) {
       float lrnow = config.learning_rate;
       if (config.anneal_lr) {  // ac:634-639
@@ -334,9 +335,10 @@ int main(int argc, const char** argv) {
       check(ppo_update(agent, lrnow, nullptr, &st), "ppo_update");  // stats are rank-averaged inside
       if (rank == 0) {
         char mf[64], of[64];
-        std::snprintf(mf, sizeof mf, "model_latest_%09u.bin", iteration);
-        std::snprintf(of, sizeof of, "optimizer_latest_%09u.bin", iteration);
-        save_state(agent, exp_folder, mf, of);
+        std::snprintf(mf, sizeof mf, "model_latest_%09u.pth", iteration);
+        std::snprintf(of, sizeof of, "optimizer_latest_%09u.pth", iteration);
+        save_state(agent, exp_folder, mf, of, lrnow, config.adam_eps);
+        last_lr = lrnow;
         cleanup_checkpoints(exp_folder, iteration);
         const double secs = seconds_since(start_time);
         float sps = 0.f;
@@ -355,7 +357,7 @@ int main(int argc, const char** argv) {
       }
       std::cout << std::flush;
     }
-    if (rank == 0) save_state(agent, exp_folder, "model_final.bin", "optimizer_final.bin");
+    if (rank == 0) save_state(agent, exp_folder, "model_final.pth", "optimizer_final.pth", last_lr, config.adam_eps);
     // rank 0 evaluation with the Beta mean action on env 0 (ac:965-1001)
     if (rank == 0 && !device_env) {
       std::vector<float> episodic_returns;

@@ -153,6 +153,7 @@ int main(int argc, const char** argv) {
     long global_step = 0;
     const auto start_time = std::chrono::high_resolution_clock::now();
     ppo_update_stats st{};
+    double last_lr = config.learning_rate;  // the optimizer's lr at save time
     for (int iteration = 0; iteration < config.num_iterations; ++iteration) {
       float lrnow = config.learning_rate;
       if (config.anneal_lr) {  // ppo:379-384
@@ -194,9 +195,10 @@ int main(int argc, const char** argv) {
       check(ppo_compute_gae(agent, d_obs, d_done, T, s), "ppo_compute_gae");
       check(ppo_update(agent, lrnow, nullptr, &st), "ppo_update");
       char mf[64], of[64];
-      std::snprintf(mf, sizeof mf, "model_latest_%09d.bin", iteration);
-      std::snprintf(of, sizeof of, "optimizer_latest_%09d.bin", iteration);
-      save_state(agent, exp_folder, mf, of);
+      std::snprintf(mf, sizeof mf, "model_latest_%09d.pth", iteration);
+      std::snprintf(of, sizeof of, "optimizer_latest_%09d.pth", iteration);
+      save_state(agent, exp_folder, mf, of, lrnow, config.adam_eps);
+      last_lr = lrnow;
       cleanup_checkpoints(exp_folder, iteration);
       const double secs = seconds_since(start_time);
       float sps = 0.f;
@@ -213,7 +215,7 @@ int main(int argc, const char** argv) {
       logger.add_scalar("losses/clipfrac", global_step, st.clipfrac);
       logger.add_scalar("charts/SPS", global_step, sps);
     }
-    save_state(agent, exp_folder, "model_final.bin", "optimizer_final.bin");
+    save_state(agent, exp_folder, "model_final.pth", "optimizer_final.pth", last_lr, config.adam_eps);
     // final evaluation on the training envs (normalisation statistics live there, ppo:589-626)
     const float* eobs = envs->reset(config.eval_seed);
     HIPCHECK(hipMemcpyAsync(d_obs, eobs, sizeof(float) * E * O, hipMemcpyHostToDevice, s));

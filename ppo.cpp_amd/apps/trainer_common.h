@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/ppo_hip.h"
+#include "../../include/ppo_pth.h"
 #include "../../include/ppo_synth_env.h"
 #include "../gymcpp/gym.h"
 #include "../gymcpp/synthetic_cheetah.h"
@@ -182,28 +183,32 @@ inline std::vector<float> init_params(const ppo_layout& L, int seed, float act_h
 // checkpoints: flat fp32 parameters + Adam state (reference: torch::save(agent / optimizer) every
 // iteration, ppo:173-180 / :545-563; .pth interop is a SURVEY §8f "next" item)
 // ------------------------------------------------------------------------------------------------
+// save_state (ppo:173-180): torch::save(agent, model_file) and torch::save(optimizer,
+// optimizer_file) as LibTorch module archives (include/ppo_pth.h), loadable by torch::load in the
+// reference's tools (e.g. src/carla/ppo_carla_inference.cpp:104) and by torch.jit.load
 inline void save_state(ppo_t* ctx, const std::filesystem::path& folder, const std::string& model_file,
-                       const std::string& optimizer_file) {
+                       const std::string& optimizer_file, double lr, double adam_eps) {
   ppo_layout L;
   check(ppo_get_layout(ctx, &L), "ppo_get_layout");
   std::vector<float> p(L.P), m(L.P), v(L.P);
   long step = 0;
   check(ppo_save_params(ctx, p.data(), L.P), "ppo_save_params");
   check(ppo_save_adam(ctx, m.data(), v.data(), L.P, &step), "ppo_save_adam");
-  std::ofstream(folder / model_file, std::ios::binary).write((const char*)p.data(), sizeof(float) * L.P);
-  std::ofstream f(folder / optimizer_file, std::ios::binary);
-  f.write((const char*)&step, sizeof(step));
-  f.write((const char*)m.data(), sizeof(float) * L.P);
-  f.write((const char*)v.data(), sizeof(float) * L.P);
+  check(ppo_pth_save_agent(&L, p.data(), (folder / model_file).string().c_str()), "ppo_pth_save_agent");
+  check(ppo_pth_save_adam(&L, m.data(), v.data(), step, lr, adam_eps, (folder / optimizer_file).string().c_str()),
+        "ppo_pth_save_adam");
 }
 
+// keeps only this iteration's model_latest_* / optimizer_latest_* (ppo:548-563)
 inline void cleanup_checkpoints(const std::filesystem::path& folder, long iteration) {
   char keep_m[64], keep_o[64];
-  std::snprintf(keep_m, sizeof keep_m, "model_latest_%09ld.bin", iteration);
-  std::snprintf(keep_o, sizeof keep_o, "optimizer_latest_%09ld.bin", iteration);
+  std::snprintf(keep_m, sizeof keep_m, "model_latest_%09ld.pth", iteration);
+  std::snprintf(keep_o, sizeof keep_o, "optimizer_latest_%09ld.pth", iteration);
   for (const auto& e : std::filesystem::directory_iterator(folder)) {
     const std::string fn = e.path().filename().string();
-    if ((fn.rfind("model_latest_", 0) == 0 && fn != keep_m) || (fn.rfind("optimizer_latest_", 0) == 0 && fn != keep_o))
+    const bool pth = fn.size() > 4 && fn.compare(fn.size() - 4, 4, ".pth") == 0;
+    if (pth && ((fn.rfind("model_latest_", 0) == 0 && fn != keep_m) ||
+                (fn.rfind("optimizer_latest_", 0) == 0 && fn != keep_o)))
       std::filesystem::remove(e.path());
   }
 }

@@ -20,6 +20,16 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
+# One HIP runtime per process. torch bundles its own libamdhip64 and, if libppo_hip.so (linked
+# against /opt/rocm's) is loaded first, `import torch` maps a second runtime next to it and the two
+# tear each other down at exit (free(): invalid pointer). Importing torch first makes libppo_hip.so
+# bind to the runtime already mapped (same soname), so processes that also use torch.distributed
+# (bench.py --gpus N, the gloo tests) run on one runtime.
+try:
+    import torch  # noqa: F401
+except ImportError:  # torch is plumbing only; the library works without it
+    torch = None
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("PPO_HIP_LIB") or os.path.join(PKG_ROOT, "lib", "libppo_hip.so")  # override: diagnostics
@@ -92,7 +102,7 @@ PPO_CARLA_SAMPLE, PPO_CARLA_MEAN, PPO_CARLA_GIVEN, PPO_CARLA_ROACH = range(4)
 _LIB = None
 
 # (name, restype, argtypes) of every entry point declared in include/ppo_hip.h / ppo_synth_env.h /
-# ppo_carla.h
+# ppo_carla.h / ppo_pth.h
 _VP, _FP, _I, _L, _F, _SZ = C.c_void_p, C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_size_t
 SYMBOLS = [
     ("ppo_last_error", C.c_char_p, []),
@@ -144,6 +154,15 @@ SYMBOLS = [
     ("ppo_carla_get_layout", _I, [_VP, C.POINTER(CarlaLayout)]),
     ("ppo_carla_load_params", _I, [_VP, _FP, _L]),
     ("ppo_carla_forward", _I, [_VP, _I, _VP, _FP, _FP, _I, _FP, _L, _L, _FP, _FP, _FP, _FP, _FP, _FP, _VP]),
+    ("ppo_layout_fill", _I, [C.POINTER(Layout), _I, _I, _I, _I]),
+    ("ppo_carla_layout_fill", _I, [C.POINTER(CarlaLayout), _I, _I, _I, _I, _I, _I]),
+    ("ppo_pth_save_agent", _I, [C.POINTER(Layout), _FP, C.c_char_p]),
+    ("ppo_pth_load_agent", _I, [C.POINTER(Layout), C.c_char_p, _FP, _L]),
+    ("ppo_pth_save_adam", _I, [C.POINTER(Layout), _FP, _FP, _L, C.c_double, C.c_double, C.c_char_p]),
+    ("ppo_pth_load_adam", _I, [C.POINTER(Layout), C.c_char_p, _FP, _FP, _L, C.POINTER(_L),
+                               C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    ("ppo_carla_pth_save", _I, [C.POINTER(CarlaLayout), _FP, C.c_char_p]),
+    ("ppo_carla_pth_load", _I, [C.POINTER(CarlaLayout), C.c_char_p, _FP, _L]),
 ]
 
 
@@ -172,6 +191,68 @@ def lib():
 def check(rc):
     if rc != 0:
         raise PPOError(f"libppo_hip error {rc}: {lib().ppo_last_error().decode()}")
+
+
+# ------------------------------------------------------------------------------------------------
+# LibTorch checkpoints (include/ppo_pth.h): model_*.pth / optimizer_*.pth as torch::save writes them
+# ------------------------------------------------------------------------------------------------
+def agent_layout(kind, O, A, H) -> Layout:
+    L = Layout()
+    check(lib().ppo_layout_fill(C.byref(L), kind, O, A, H))
+    return L
+
+
+def carla_layout(C_=15, IH=192, IW=192, NM=8, NV=3, A=2) -> CarlaLayout:
+    L = CarlaLayout()
+    check(lib().ppo_carla_layout_fill(C.byref(L), C_, IH, IW, NM, NV, A))
+    return L
+
+
+def _f32(a, n):
+    a = np.ascontiguousarray(a, dtype=np.float32).reshape(-1)
+    if a.size != n:
+        raise PPOError(f"expected {n} floats, got {a.size}")
+    return a
+
+
+def save_agent_pth(layout: Layout, params, path):
+    """torch::save(agent, path) of the flat parameters (named_parameters() order)."""
+    p = _f32(params, layout.P)
+    check(lib().ppo_pth_save_agent(C.byref(layout), p.ctypes.data, os.fsencode(path)))
+
+
+def load_agent_pth(layout: Layout, path):
+    """torch::load(agent, path) -> flat parameters."""
+    out = np.empty(layout.P, np.float32)
+    check(lib().ppo_pth_load_agent(C.byref(layout), os.fsencode(path), out.ctypes.data, layout.P))
+    return out
+
+
+def save_adam_pth(layout: Layout, m, v, step, lr, eps, path):
+    """torch::save(optimizer, path) of an Adam(agent->parameters(), AdamOptions(lr).eps(eps))."""
+    m, v = _f32(m, layout.P), _f32(v, layout.P)
+    check(lib().ppo_pth_save_adam(C.byref(layout), m.ctypes.data, v.ctypes.data, int(step), float(lr), float(eps),
+                                  os.fsencode(path)))
+
+
+def load_adam_pth(layout: Layout, path):
+    """torch::load(optimizer, path) -> (exp_avg, exp_avg_sq, step, lr, eps)."""
+    m, v = np.empty(layout.P, np.float32), np.empty(layout.P, np.float32)
+    step, lr, eps = C.c_long(0), C.c_double(0), C.c_double(0)
+    check(lib().ppo_pth_load_adam(C.byref(layout), os.fsencode(path), m.ctypes.data, v.ctypes.data, layout.P,
+                                  C.byref(step), C.byref(lr), C.byref(eps)))
+    return m, v, step.value, lr.value, eps.value
+
+
+def save_carla_pth(layout: CarlaLayout, params, path):
+    p = _f32(params, layout.P)
+    check(lib().ppo_carla_pth_save(C.byref(layout), p.ctypes.data, os.fsencode(path)))
+
+
+def load_carla_pth(layout: CarlaLayout, path):
+    out = np.empty(layout.P, np.float32)
+    check(lib().ppo_carla_pth_load(C.byref(layout), os.fsencode(path), out.ctypes.data, layout.P))
+    return out
 
 
 def device_count():

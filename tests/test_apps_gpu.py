@@ -11,6 +11,8 @@ import subprocess
 import numpy as np
 import pytest
 
+import ppo_amd as P
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "ppo.cpp_amd")
 BIN = os.path.join(PKG, "bin")
@@ -36,8 +38,14 @@ def test_ppo_cli_runs():
                 "--num_steps", "64", "--total_timesteps", str(8 * 64 * 3), "--num_eval_runs", "1",
                 "--exp_name_stem", "t_ppo_cli", "--seed", "3"])
     assert "SPS:" in out
-    p = np.fromfile(os.path.join(MODELS, "t_ppo_cli_3", "model_final.bin"), np.float32)
-    assert p.size > 0 and np.isfinite(p).all()
+    # model_final.pth / optimizer_final.pth: LibTorch archives of the reference agent (ppo:587)
+    L = P.agent_layout(P.PPO_NET_TANH_NORMAL, 17, 6, 64)
+    p = P.load_agent_pth(L, os.path.join(MODELS, "t_ppo_cli_3", "model_final.pth"))
+    assert p.size == L.P and np.isfinite(p).all()
+    m, v, step, lr, eps = P.load_adam_pth(L, os.path.join(MODELS, "t_ppo_cli_3", "optimizer_final.pth"))
+    assert step == 3 * 10 * 32 and np.isfinite(m).all() and (v >= 0).all() and eps == pytest.approx(1e-5)
+    latest = [f for f in os.listdir(os.path.join(MODELS, "t_ppo_cli_3")) if f.startswith("model_latest_")]
+    assert len(latest) == 1 and latest[0].endswith(".pth")  # older ones cleaned up (ppo:548-556)
     # the reference's TensorBoard event file (ppo:281), one record per scalar of the JSON-lines log
     ev = open(os.path.join(MODELS, "t_ppo_cli_3", "tfevents_logs.pb"), "rb").read()
     n_lines = len(open(os.path.join(MODELS, "t_ppo_cli_3", "scalars.jsonl")).read().splitlines())
@@ -57,8 +65,9 @@ def test_ac_cli_host_equals_device_env():
           "--num_collect_groups", "5", "--exp_name_stem", "t_ac_host"] + common)
     _run([_exe("ac_ppo_continuous_action"), "--env_id", "SyntheticCheetah-v0", "--env_backend", "device",
           "--exp_name_stem", "t_ac_dev"] + common)
-    a = np.fromfile(os.path.join(MODELS, "t_ac_host_4", "model_final.bin"), np.float32)
-    b = np.fromfile(os.path.join(MODELS, "t_ac_dev_4", "model_final.bin"), np.float32)
+    L = P.agent_layout(P.PPO_NET_LN_BETA, 17, 6, 256)
+    a = P.load_agent_pth(L, os.path.join(MODELS, "t_ac_host_4", "model_final.pth"))
+    b = P.load_agent_pth(L, os.path.join(MODELS, "t_ac_dev_4", "model_final.pth"))
     assert a.size == b.size and a.size > 146189
     np.testing.assert_array_equal(a, b)
 

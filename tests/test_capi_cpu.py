@@ -12,7 +12,7 @@ LIB = os.path.join(ROOT, "ppo.cpp_amd", "lib", "libppo_hip.so")
 
 def declared_functions():
     names = []
-    for h in ("ppo_hip.h", "ppo_synth_env.h", "ppo_carla.h"):
+    for h in ("ppo_hip.h", "ppo_synth_env.h", "ppo_carla.h", "ppo_pth.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         for m in re.finditer(r"^\s*[A-Za-z_][\w\s\*]*?\b((?:ppo|psyn)_\w+)\s*\(", src, flags=re.M):

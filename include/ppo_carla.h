@@ -139,6 +139,39 @@ int ppo_carla_forward(ppo_carla_t* c, int n, const uint8_t* bev, const float* me
                       int sample_type, const float* action_in, long env_base, long step_id, float* action,
                       float* logprob, float* entropy, float* value, float* alpha, float* beta, void* stream);
 
+/* ---- training (ac_ppo_carla.cpp:529-620): one PPO minibatch step --------------------------------
+ * Loss = pg_loss - ent_coef * entropy + vf_coef * v_loss exactly as the MLP agents (clipped
+ * surrogate, clipped value loss, minibatch advantage normalisation with Bessel's correction),
+ * backward through heads, MLPs and all six convolutions, clip_grad_norm_(max_grad_norm), Adam
+ * (betas 0.9 / 0.999, eps = adam_eps, bias-corrected, weight_decay 0), all on the device. */
+typedef struct ppo_carla_train_config {
+  float clip_coef;      /* 0.2 */
+  float ent_coef;       /* 0.0 */
+  float vf_coef;        /* 0.5 */
+  float max_grad_norm;  /* 0.5 */
+  float adam_eps;       /* 1e-5 */
+  int norm_adv;         /* 1 */
+  int clip_vloss;       /* 1 */
+} ppo_carla_train_config;
+
+typedef struct ppo_carla_update_stats {
+  float pg_loss, v_loss, entropy, old_approx_kl, approx_kl, clipfrac;
+  float grad_norm;  /* total norm before clipping */
+} ppo_carla_update_stats;
+
+/* One minibatch of n <= max_batch rows (device pointers): bev uint8 [n, C, IH, IW], meas [n, NM],
+ * vmeas [n, NV], actions [n, A] (env space), old_logp / adv / ret / old_v [n]. stats may be NULL
+ * (no host synchronisation then). */
+int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc, int n, const uint8_t* bev, const float* meas,
+                     const float* vmeas, const float* actions, const float* old_logp, const float* adv,
+                     const float* ret, const float* old_v, float lr, ppo_carla_update_stats* stats, void* stream);
+/* parameters (named_parameters() order) and the raw gradient of the last update, to host */
+int ppo_carla_save_params(ppo_carla_t* c, float* host, long n);
+int ppo_carla_last_grad(ppo_carla_t* c, float* host, long n);
+/* Adam moments in the same flat order, and the step count */
+int ppo_carla_save_adam(ppo_carla_t* c, float* m_host, float* v_host, long n, long* step);
+int ppo_carla_load_adam(ppo_carla_t* c, const float* m_host, const float* v_host, long n, long step);
+
 #ifdef __cplusplus
 }
 #endif

@@ -645,6 +645,85 @@ int main(int argc, char** argv) {
     end_case();
   }
 
+  // ---- CaRL update: loss, backward, clip_grad_norm_, Adam (ac_ppo_carla.cpp:540-619) ----------
+  // Same parameters / input streams as carla_act with N=4 rows; gradients and the stepped
+  // parameters are summarised per tensor (sum, sum of squares, 32 entries at hbits-drawn indices)
+  // so the 1.2 M-float vectors need not be stored.
+  {
+    const int N = 4, C = 15, HW = 192, NM = 8, NV = 3, A = 2;
+    CarlaAgent agent(C, NM, NV, A, 1.0f, -1.0f, 1.0f);
+    {
+      torch::NoGradGuard ng;
+      int t = 0;
+      for (auto& kv : agent->named_parameters()) {
+        Tensor p = kv.value();
+        Tensor v;
+        if (kv.key() == "action_space_high") v = torch::tensor(1.0f);
+        else if (kv.key() == "action_space_low") v = torch::tensor(-1.0f);
+        else if (p.dim() >= 2) {
+          const float a = std::sqrt(6.0f / (float)(p.numel() / p.size(0)));
+          v = hunif(1000 + t, p.sizes().vec(), -a, a);
+        } else v = hunif(1000 + t, p.sizes().vec(), -0.1f, 0.1f);
+        p.copy_(v.reshape(p.sizes()));
+        ++t;
+      }
+    }
+    Tensor bev = torch::empty({N, C, HW, HW}, torch::kUInt8);
+    uint8_t* bp = bev.data_ptr<uint8_t>();
+    for (int64_t i = 0; i < bev.numel(); ++i) bp[i] = (uint8_t)(hbits(1, (uint32_t)i) >> 24);
+    Tensor meas = hunif(2, {N, NM}, -1.0f, 1.0f), vmeas = hunif(3, {N, NV}, -1.0f, 1.0f);
+    Tensor act = hunif(4, {N, A}, -0.98f, 0.98f);
+    Tensor old_logp, old_v;
+    {
+      torch::NoGradGuard ng;
+      auto [a0, lp0, e0, v0, m0, s0, f0] = agent->forward(bev, meas, vmeas, act, "given");
+      old_logp = lp0 + (hunif(5, {N}, 0.0f, 1.0f) - 0.5f) * 0.3f;
+      old_v = v0.view(-1) + (hunif(8, {N}, 0.0f, 1.0f) - 0.5f) * 0.3f;
+    }
+    Tensor adv = hunif(6, {N}, -1.0f, 1.0f), ret = hunif(7, {N}, -1.0f, 1.0f);
+    LossCfg c{0.2f, 0.01f, 0.5f, true, true};
+    auto [a, lp, ent, v, mu, sg, feat] = agent->forward(bev, meas, vmeas, act, "given");
+    auto [loss, st] = ppo_loss(lp, ent, v, old_logp, adv, ret, old_v, c, nullptr, nullptr);
+    loss.backward();
+    const int NS = 32;
+    auto summarise = [&](bool grads) {
+      std::vector<Tensor> rows;
+      std::vector<int64_t> idx;
+      int t = 0;
+      for (auto& kv : agent->named_parameters()) {
+        Tensor x = grads ? (kv.value().grad().defined() ? kv.value().grad() : torch::zeros_like(kv.value()))
+                         : kv.value().detach();
+        x = x.reshape({-1}).to(torch::kFloat64);
+        std::vector<double> r = {x.sum().item<double>(), x.square().sum().item<double>()};
+        for (int i = 0; i < NS; ++i) {
+          const int64_t k = (int64_t)(hbits(2000 + t, (uint32_t)i) % (uint32_t)x.numel());
+          idx.push_back(k);
+          r.push_back(x[k].item<double>());
+        }
+        rows.push_back(torch::tensor(r, torch::kFloat64));
+        ++t;
+      }
+      return std::make_pair(torch::stack(rows).to(torch::kFloat32), torch::tensor(idx, torch::kInt64));
+    };
+    begin_case("carla_update", "{\"N\": 4, \"C\": 15, \"H\": 192, \"W\": 192, \"NM\": 8, \"NV\": 3, \"A\": 2, "
+                               "\"beta_min\": 1.0, \"clip_coef\": 0.2, \"ent_coef\": 0.01, \"vf_coef\": 0.5, "
+                               "\"clip_vloss\": 1, \"norm_adv\": 1, \"max_grad_norm\": 0.5, \"lr\": 0.0003, "
+                               "\"adam_eps\": 1e-05, \"samples_per_tensor\": 32}");
+    dump("carla_update", "old_logp", old_logp); dump("carla_update", "old_v", old_v);
+    dump("carla_update", "adv", adv); dump("carla_update", "ret", ret);
+    dump("carla_update", "logprob", lp); dump("carla_update", "value", v.view(-1));
+    dump("carla_update", "stats", torch::tensor(st));
+    auto [gsum, gidx] = summarise(true);
+    dump("carla_update", "grad_summary", gsum); dump("carla_update", "sample_idx", gidx.view({gsum.size(0), NS}));
+    torch::optim::Adam opt(agent->parameters(), torch::optim::AdamOptions(3e-4).eps(1e-5));
+    const double tn = torch::nn::utils::clip_grad_norm_(agent->parameters(), 0.5);
+    dump("carla_update", "total_norm", torch::tensor({(float)tn}));
+    opt.step();
+    auto [psum, pidx] = summarise(false);
+    dump("carla_update", "param_step1_summary", psum);
+    end_case();
+  }
+
   // ---- Distribution spot values straight from rl_utils.h ------------------------------------
   {
     torch::NoGradGuard ng;

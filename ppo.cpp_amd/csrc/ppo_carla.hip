@@ -15,7 +15,10 @@
 //    action, log_prob and entropy (rl_utils.h:87-132), one thread per row.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <string>
+#include <vector>
 
 #include "../../include/ppo_carla.h"
 #include "../../include/ppo_hip.h"
@@ -139,6 +142,7 @@ struct HeadArgs {
   int rank;
   long env_base, step_id;
   float *action, *logprob, *entropy, *value, *alpha, *beta;
+  float* hpre;  // [n][2A] dist_mu / dist_sigma pre-activations (training), may be null
 };
 
 __global__ __launch_bounds__(64) void k_carla_head(HeadArgs h) {
@@ -160,6 +164,10 @@ __global__ __launch_bounds__(64) void k_carla_head(HeadArgs h) {
     }
     pm += P[h.mu_b + ai];
     ps += P[h.sg_b + ai];
+    if (h.hpre) {
+      h.hpre[(long)r * 2 * h.A + ai] = pm;
+      h.hpre[(long)r * 2 * h.A + h.A + ai] = ps;
+    }
     const float al = softplusf_(pm) + h.beta_min, be = softplusf_(ps) + h.beta_min;
     float sv;
     if (h.mode == PPO_CARLA_GIVEN) {
@@ -224,6 +232,18 @@ struct ppo_carla {
   float* act[PPO_CARLA_NCONV - 1] = {};  // conv1..conv5 outputs
   float *enc = nullptr, *s1 = nullptr, *l1 = nullptr, *feat = nullptr, *v1 = nullptr, *v2 = nullptr, *val = nullptr;
   float *p1 = nullptr, *p2 = nullptr;
+  float* hpre = nullptr;  // [B][2A]
+  // training state (allocated on the first ppo_carla_update)
+  bool train_ready = false;
+  float *G = nullptr, *m = nullptr, *v = nullptr;        // [P]
+  float* dact[PPO_CARLA_NCONV - 1] = {};                 // d(conv1..conv5 outputs), masked
+  float *denc = nullptr, *ds1 = nullptr, *dl1 = nullptr, *dfeat = nullptr, *dv1 = nullptr, *dv2 = nullptr;
+  float *dp1 = nullptr, *dp2 = nullptr, *dhead = nullptr, *dval = nullptr;  // dhead [B][2A], dval [B]
+  float *lp = nullptr, *ent = nullptr, *rowstat = nullptr;                    // rowstat [B][8]
+  float *part = nullptr;                                 // wgrad partials
+  size_t part_floats = 0;
+  float* small = nullptr;  // [0,2) adv mean/std, [8, 8+40) tensor norms, [64, 72) stats
+  long step = 0;
 };
 
 static int carla_alloc(float** p, size_t n) {
@@ -235,10 +255,15 @@ extern "C" int ppo_carla_destroy(ppo_carla_t* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  float* bufs[] = {c->P, c->enc, c->s1, c->l1, c->feat, c->v1, c->v2, c->val, c->p1, c->p2};
+  float* bufs[] = {c->P,    c->enc,  c->s1,  c->l1,  c->feat,  c->v1,  c->v2,      c->val,  c->p1,
+                   c->p2,   c->hpre, c->G,   c->m,   c->v,     c->denc, c->ds1,     c->dl1,  c->dfeat,
+                   c->dv1,  c->dv2,  c->dp1, c->dp2, c->dhead, c->dval, c->lp,      c->ent,  c->rowstat,
+                   c->part, c->small};
   for (float* b : bufs)
     if (b) (void)hipFree(b);
   for (float* b : c->act)
+    if (b) (void)hipFree(b);
+  for (float* b : c->dact)
     if (b) (void)hipFree(b);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -274,6 +299,7 @@ extern "C" int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_car
   rc |= carla_alloc(&c->val, B);
   rc |= carla_alloc(&c->p1, B * 256);
   rc |= carla_alloc(&c->p2, B * 256);
+  rc |= carla_alloc(&c->hpre, B * 2 * L.A);
   if (rc || hipDeviceSynchronize() != hipSuccess) {
     ppo_carla_destroy(c);
     return ppo_fail("ppo_carla_create: device allocation failed", -2);
@@ -350,8 +376,677 @@ extern "C" int ppo_carla_forward(ppo_carla_t* c, int n, const uint8_t* bev, cons
   if (rc) return ppo_fail("ppo_carla_forward: no convolution kernel for this shape", -1);
   HeadArgs h{P,          L.mu_w, L.mu_b,   L.sg_w,    L.sg_b,    L.hi,    L.lo,
              c->p2,      c->val, n,        L.A,       sample_type, c->cfg.beta_min, action_in,
-             c->cfg.seed, c->cfg.rank, env_base, step_id, action, logprob, entropy, value, alpha, beta};
+             c->cfg.seed, c->cfg.rank, env_base, step_id, action, logprob, entropy, value, alpha, beta,
+             c->hpre};
   hipLaunchKernelGGL(k_carla_head, dim3((n + 63) / 64), dim3(64), 0, s, h);
   if (hipGetLastError() != hipSuccess) return ppo_fail("ppo_carla_forward: launch failed", -2);
+  return 0;
+}
+
+// ==========================================================================================
+// Training (ac_ppo_carla.cpp:529-620): the loss, backward through every layer, clip_grad_norm_,
+// Adam. Every convolution and Linear layer uses two kernels, both MFMA 16x16x4 in the
+// batch-on-lanes layout of k_conv:
+//  * k_dgrad — gradient w.r.t. the layer input, times the ReLU mask of that input (the previous
+//    layer's output): a gather-GEMM over (output channel, tap). A strided convolution's input
+//    pixels split into S x S parity classes (blockIdx.z); within a class the contributing taps are
+//    a fixed set (ky = py + S*j), so the reduction has no zero-stuffed taps.
+//  * k_wgrad — dW = dZ^T · im2col(x) with the bias as an extra all-ones column, split over
+//    chunks of output pixels (blockIdx.x); k_wsum adds the chunks in order (deterministic).
+// Linear layers are 1x1 convolutions on a 1x1 plane, as in the forward.
+// ==========================================================================================
+namespace {
+
+struct DgradArgs {
+  const float* dz;  // [n][OC][OH*OW], sample stride dz_stride
+  long dz_stride;
+  const float* W;   // W[oc][w_ic][K][K]
+  int w_ic;
+  const float* x;   // the layer input (post-ReLU) for the mask, [n][IC][IH*IW]
+  long x_stride;
+  float* dx;
+  long dx_stride;
+  int IC, IH, IW, OC, OH, OW, K, S, n, accumulate;
+};
+
+constexpr int kMaxDTab = 3072;
+
+template <int NOT, int NP>
+__global__ __launch_bounds__(256) void k_dgrad(DgradArgs a) {
+  __shared__ int woff[kMaxDTab], zoff[kMaxDTab];
+  __shared__ int dji[kMaxDTab];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int S = a.S, K = a.K, KK = K * K;
+  const int py = blockIdx.z / S, px = blockIdx.z - py * S;
+  const int nj = (K - py + S - 1) / S, ni = (K - px + S - 1) / S;
+  const int OP = a.OH * a.OW, Kt = a.OC * nj * ni;
+  for (int k = tid; k < Kt; k += 256) {
+    const int oc = k / (nj * ni), rem = k - oc * nj * ni, jj = rem / ni, ii = rem - jj * ni;
+    woff[k] = oc * a.w_ic * KK + (py + S * jj) * K + (px + S * ii);
+    zoff[k] = oc * OP - jj * a.OW - ii;
+    dji[k] = (jj << 16) | ii;
+  }
+  __syncthreads();
+  const int H2 = (a.IH - py + S - 1) / S, W2 = (a.IW - px + S - 1) / S, P2 = H2 * W2;
+  const long Q = (long)a.n * P2;
+  const long q0 = ((long)blockIdx.x * 4 + wave) * 16 * NP;
+  if (q0 >= Q) return;
+  long zb[NP], sv[NP];
+  int pix[NP], iy2v[NP], ix2v[NP];
+  bool qv[NP];
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    const long q = q0 + 16 * u + j;
+    qv[u] = q < Q;
+    const long s = qv[u] ? q / P2 : 0;
+    const int p2 = qv[u] ? (int)(q - s * P2) : 0, iy2 = p2 / W2, ix2 = p2 - iy2 * W2;
+    sv[u] = s;
+    iy2v[u] = iy2;
+    ix2v[u] = ix2;
+    zb[u] = s * a.dz_stride + (long)iy2 * a.OW + ix2;
+    pix[u] = (S * iy2 + py) * a.IW + (S * ix2 + px);
+  }
+  const int ic0 = blockIdx.y * 16 * NOT;
+  f4 acc[NOT][NP];
+#pragma unroll
+  for (int t = 0; t < NOT; ++t)
+#pragma unroll
+    for (int u = 0; u < NP; ++u) acc[t][u] = f4{0.f, 0.f, 0.f, 0.f};
+  const float* wrow[NOT];
+  bool icv[NOT];
+#pragma unroll
+  for (int t = 0; t < NOT; ++t) {
+    const int ic = ic0 + 16 * t + j;
+    icv[t] = ic < a.IC;
+    wrow[t] = a.W + (long)(icv[t] ? ic : 0) * KK;
+  }
+#pragma unroll 4
+  for (int k0 = 0; k0 < Kt; k0 += 4) {
+    const int k = k0 + g;
+    const bool kv = k < Kt;
+    const int wo = kv ? woff[k] : 0, zo = kv ? zoff[k] : 0, d = kv ? dji[k] : 0;
+    const int jj = d >> 16, ii = d & 0xFFFF;
+    float xb[NP], wa[NOT];
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      const bool ok = kv && qv[u] && (unsigned)(iy2v[u] - jj) < (unsigned)a.OH && (unsigned)(ix2v[u] - ii) < (unsigned)a.OW;
+      xb[u] = ok ? a.dz[zb[u] + zo] : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < NOT; ++t) wa[t] = (kv && icv[t]) ? wrow[t][wo] : 0.f;
+#pragma unroll
+    for (int t = 0; t < NOT; ++t)
+#pragma unroll
+      for (int u = 0; u < NP; ++u) acc[t][u] = mfma16(wa[t], xb[u], acc[t][u]);
+  }
+  const long plane = (long)a.IH * a.IW;
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    if (!qv[u]) continue;
+#pragma unroll
+    for (int t = 0; t < NOT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ic = ic0 + 16 * t + 4 * g + r;
+        if (ic >= a.IC) continue;
+        const float xm = a.x[sv[u] * a.x_stride + ic * plane + pix[u]];
+        const float gv = xm > 0.0f ? acc[t][u][r] : 0.0f;
+        float* o = a.dx + sv[u] * a.dx_stride + ic * plane + pix[u];
+        *o = a.accumulate ? *o + gv : gv;
+      }
+  }
+}
+
+struct WgradArgs {
+  const float* dz;  // [n][OC][OP], sample stride dz_stride
+  long dz_stride;
+  int OC, OP, OW;
+  const float* x_f;
+  const uint8_t* x_u8;
+  long x_stride;
+  int IC, IH, IW, K, S;
+  int n, Kt;     // Kt = IC*K*K; column Kt is the bias (x = 1)
+  long qchunk;   // output pixels per chunk (multiple of 4)
+  float* part;   // [chunks][OC][Kt + 1]
+};
+
+constexpr int kMaxPTab = 9216;  // output pixels per sample (94 x 94 = 8836 for conv1)
+
+template <int NOT, int NKT>
+__global__ __launch_bounds__(256) void k_wgrad(WgradArgs a) {
+  __shared__ int koff[kMaxKTab];
+  __shared__ int pbase[kMaxPTab];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int KK = a.K * a.K, plane = a.IH * a.IW;
+  for (int k = tid; k < a.Kt; k += 256) {
+    const int ic = k / KK, rem = k - ic * KK, ky = rem / a.K, kx = rem - ky * a.K;
+    koff[k] = ic * plane + ky * a.IW + kx;
+  }
+  for (int p = tid; p < a.OP; p += 256) {
+    const int oy = p / a.OW, ox = p - oy * a.OW;
+    pbase[p] = oy * a.S * a.IW + ox * a.S;
+  }
+  __syncthreads();
+  const long Q = (long)a.n * a.OP;
+  const long qs = (long)blockIdx.x * a.qchunk;
+  const long qe = qs + a.qchunk < Q ? qs + a.qchunk : Q;
+  const int oc0 = blockIdx.y * 16 * NOT;
+  const int kb = (blockIdx.z * 4 + wave) * 16 * NKT;
+  if (kb > a.Kt) return;
+  f4 acc[NOT][NKT];
+#pragma unroll
+  for (int t = 0; t < NOT; ++t)
+#pragma unroll
+    for (int u = 0; u < NKT; ++u) acc[t][u] = f4{0.f, 0.f, 0.f, 0.f};
+  int ko[NKT];
+  int kc[NKT];  // 0: gathered column, 1: bias column, 2: past the end
+#pragma unroll
+  for (int u = 0; u < NKT; ++u) {
+    const int k = kb + 16 * u + j;
+    kc[u] = k < a.Kt ? 0 : (k == a.Kt ? 1 : 2);
+    ko[u] = k < a.Kt ? koff[k] : 0;
+  }
+  long dzo[NOT];
+  bool ocv[NOT];
+#pragma unroll
+  for (int t = 0; t < NOT; ++t) {
+    const int oc = oc0 + 16 * t + j;
+    ocv[t] = oc < a.OC;
+    dzo[t] = (long)(ocv[t] ? oc : 0) * a.OP;
+  }
+  long q = qs + g;
+  long s = q / a.OP;
+  int p = (int)(q - s * a.OP);
+  for (long qb = qs; qb < qe; qb += 4) {
+    const bool qv = q < qe;
+    float av[NOT], bv[NKT];
+    const long sb = s * a.dz_stride, xb = s * a.x_stride + (qv ? pbase[p] : 0);
+#pragma unroll
+    for (int t = 0; t < NOT; ++t) av[t] = (qv && ocv[t]) ? a.dz[sb + dzo[t] + p] : 0.f;
+#pragma unroll
+    for (int u = 0; u < NKT; ++u) {
+      float xv = 0.f;
+      if (qv && kc[u] == 0) xv = a.x_u8 ? (float)a.x_u8[xb + ko[u]] / 255.0f : a.x_f[xb + ko[u]];
+      else if (qv && kc[u] == 1) xv = 1.0f;
+      bv[u] = xv;
+    }
+#pragma unroll
+    for (int t = 0; t < NOT; ++t)
+#pragma unroll
+      for (int u = 0; u < NKT; ++u) acc[t][u] = mfma16(av[t], bv[u], acc[t][u]);
+    q += 4;
+    p += 4;
+    while (p >= a.OP) {
+      p -= a.OP;
+      ++s;
+    }
+  }
+  float* out = a.part + (long)blockIdx.x * a.OC * (a.Kt + 1);
+#pragma unroll
+  for (int t = 0; t < NOT; ++t)
+#pragma unroll
+    for (int u = 0; u < NKT; ++u) {
+      const int k = kb + 16 * u + j;
+      if (k > a.Kt) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int oc = oc0 + 16 * t + 4 * g + r;
+        if (oc < a.OC) out[(long)oc * (a.Kt + 1) + k] = acc[t][u][r];
+      }
+    }
+}
+
+// G[w + oc*Kt + k] / G[b + oc] = sum over chunks, in chunk order
+__global__ void k_wsum(const float* __restrict__ part, int chunks, int OC, int Kt, float* __restrict__ Gw,
+                       float* __restrict__ Gb) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long per = (long)OC * (Kt + 1);
+  if (i >= per) return;
+  float acc = 0.f;
+  for (int c = 0; c < chunks; ++c) acc += part[(long)c * per + i];
+  const int oc = (int)(i / (Kt + 1)), k = (int)(i - (long)oc * (Kt + 1));
+  if (k < Kt) Gw[(long)oc * Kt + k] = acc;
+  else Gb[oc] = acc;
+}
+
+// minibatch advantage mean / std (Bessel), one block, fixed summation order
+__global__ __launch_bounds__(256) void k_carla_advstats(const float* __restrict__ adv, int n, float* __restrict__ out) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += adv[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const float mean = red[0] / (float)n;
+  __syncthreads();
+  float q = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) q += (adv[i] - mean) * (adv[i] - mean);
+  red[threadIdx.x] = q;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = mean;
+    out[1] = sqrtf(red[0] / (float)(n - 1));
+  }
+}
+
+struct HeadBwdArgs {
+  const float* P;
+  long hi, lo;
+  const float* hpre;  // [n][2A]
+  const float* actions;
+  const float *lp, *ent, *val, *old_logp, *adv, *ret, *old_v;
+  const float* advstat;  // mean, std
+  int n, A;
+  float beta_min, clip, ent_coef, vf_coef;
+  int norm_adv, clip_vloss;
+  float* dhead;    // [n][2A]
+  float* dval;     // [n]
+  float* rowstat;  // [n][8]
+};
+
+PPO_DEV float softplus_grad(float x) {
+  if (x > 20.0f) return 1.0f;
+  const float e = expf(x);
+  return e / (e + 1.0f);
+}
+
+// loss -> d(dist_mu, dist_sigma pre-activations), d(value); the terms of the minibatch stats
+__global__ __launch_bounds__(64) void k_carla_head_bwd(HeadBwdArgs h) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= h.n) return;
+  const float invM = 1.0f / (float)h.n, c = h.clip;
+  const float logratio = h.lp[r] - h.old_logp[r];
+  const float ratio = expf(logratio);
+  float an = h.adv[r];
+  if (h.norm_adv) an = (an - h.advstat[0]) / (h.advstat[1] + 1e-8f);
+  const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
+  const float pg1 = -an * ratio, pg2 = -an * rc;
+  // d max(pg1, pg2) / d ratio; ties split the gradient (ATen maximum backward)
+  const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+  const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
+  const float dratio = w1 * (-an) + (1.0f - w1) * (-an) * inr;
+  const float g_logp = invM * dratio * ratio;
+  const float v = h.val[r], R = h.ret[r];
+  float g_v, vterm;
+  if (h.clip_vloss) {
+    const float vu = (v - R) * (v - R);
+    const float dv = v - h.old_v[r];
+    const float vcl = h.old_v[r] + fminf(fmaxf(dv, -c), c);
+    const float vc = (vcl - R) * (vcl - R);
+    vterm = fmaxf(vu, vc);
+    const float u1 = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
+    const float in2 = (dv >= -c && dv <= c) ? 1.0f : 0.0f;
+    g_v = 0.5f * h.vf_coef * invM * (u1 * 2.0f * (v - R) + (1.0f - u1) * 2.0f * (vcl - R) * in2);
+  } else {
+    vterm = (v - R) * (v - R);
+    g_v = 0.5f * h.vf_coef * invM * 2.0f * (v - R);
+  }
+  const float g_ent = -h.ent_coef * invM;
+  const float hi = h.P[h.hi], lo = h.P[h.lo];
+  for (int ai = 0; ai < h.A; ++ai) {
+    const float pm = h.hpre[(long)r * 2 * h.A + ai], ps = h.hpre[(long)r * 2 * h.A + h.A + ai];
+    const float al = softplusf_(pm) + h.beta_min, be = softplusf_(ps) + h.beta_min, ab = al + be;
+    float sv = (h.actions[(long)r * h.A + ai] - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+    sv = fminf(fmaxf(sv, 0.0f + 1e-7f), 1.0f + 1e-7f);
+    const float psab = digammaf_(ab), tab = trigammaf_(ab);
+    const float dla = ((al - 1.0f) != 0.0f ? logf(sv) : 0.0f) + psab - digammaf_(al);
+    const float dlb = ((be - 1.0f) != 0.0f ? logf(1.0f - sv) : 0.0f) + psab - digammaf_(be);
+    const float dea = (ab - 2.0f) * tab - (al - 1.0f) * trigammaf_(al);
+    const float deb = (ab - 2.0f) * tab - (be - 1.0f) * trigammaf_(be);
+    h.dhead[(long)r * 2 * h.A + ai] = (g_logp * dla + g_ent * dea) * softplus_grad(pm);
+    h.dhead[(long)r * 2 * h.A + h.A + ai] = (g_logp * dlb + g_ent * deb) * softplus_grad(ps);
+  }
+  h.dval[r] = g_v;
+  float* st = h.rowstat + (long)r * 8;
+  st[0] = fmaxf(pg1, pg2);
+  st[1] = vterm;
+  st[2] = h.ent[r];
+  st[3] = -logratio;
+  st[4] = (ratio - 1.0f) - logratio;
+  st[5] = fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
+}
+
+// row means of the stats, one block, fixed order: pg, 0.5*v, entropy, old_kl, kl, clipfrac
+__global__ __launch_bounds__(256) void k_carla_stats(const float* __restrict__ rowstat, int n, float* __restrict__ out) {
+  __shared__ float red[6][256];
+  float a[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = threadIdx.x; i < n; i += 256)
+    for (int k = 0; k < 6; ++k) a[k] += rowstat[(long)i * 8 + k];
+  for (int k = 0; k < 6; ++k) red[k][threadIdx.x] = a[k];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+      for (int k = 0; k < 6; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) out[threadIdx.x] = red[threadIdx.x][0] / (float)n * (threadIdx.x == 1 ? 0.5f : 1.0f);
+}
+
+// per-tensor L2 norm of the gradient (clip_grad.h: grad.norm()), one block per tensor
+__global__ __launch_bounds__(256) void k_carla_tnorm(const float* __restrict__ G, const long* __restrict__ off,
+                                                     const long* __restrict__ len, float* __restrict__ norms) {
+  __shared__ float red[256];
+  const int t = blockIdx.x;
+  float q = 0.f;
+  for (long i = threadIdx.x; i < len[t]; i += 256) {
+    const float x = G[off[t] + i];
+    q += x * x;
+  }
+  red[threadIdx.x] = q;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) norms[t] = sqrtf(red[0]);
+}
+
+struct CarlaAdamArgs {
+  float *P, *G, *m, *v;
+  long begin, n;             // trainable range [begin, begin + n)
+  const float* norms;        // [nt] (0 for tensors without gradient)
+  int nt;
+  float max_norm, step_size, sbc2, eps;
+  float* total_out;          // grad_norm stat
+};
+
+__global__ __launch_bounds__(256) void k_carla_adam(CarlaAdamArgs a) {
+  __shared__ float s_coef;
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int t = 0; t < a.nt; ++t) tot += a.norms[t] * a.norms[t];
+    const float total = sqrtf(tot);
+    float coef = a.max_norm / (total + 1e-6f);
+    s_coef = coef > 1.0f ? 1.0f : coef;
+    if (blockIdx.x == 0) a.total_out[0] = total;
+  }
+  __syncthreads();
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const long p = a.begin + i;
+  const float gv = a.G[p] * s_coef;
+  const float m = a.m[p] * 0.9f + gv * 0.1f;
+  const float v = a.v[p] * 0.999f + gv * gv * 0.001f;
+  a.m[p] = m;
+  a.v[p] = v;
+  a.P[p] = a.P[p] - a.step_size * (m / (sqrtf(v) / a.sbc2 + a.eps));
+}
+
+int launch_dgrad(const DgradArgs& a, hipStream_t s) {
+  const int nj = (a.K + a.S - 1) / a.S;
+  if ((long)a.OC * nj * nj > kMaxDTab) return -1;
+  const int H2 = (a.IH + a.S - 1) / a.S, W2 = (a.IW + a.S - 1) / a.S;
+  const long Q = (long)a.n * H2 * W2;
+  const int np = Q >= 16L * 4 * 2048 ? 4 : 1;
+  const unsigned gx = (unsigned)((Q + 64L * np - 1) / (64L * np));
+  const unsigned gz = (unsigned)(a.S * a.S);
+  if (a.IC >= 64) {
+    if (np == 4) hipLaunchKernelGGL((k_dgrad<4, 4>), dim3(gx, (a.IC + 63) / 64, gz), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_dgrad<4, 1>), dim3(gx, (a.IC + 63) / 64, gz), dim3(256), 0, s, a);
+  } else if (a.IC >= 32) {
+    if (np == 4) hipLaunchKernelGGL((k_dgrad<2, 4>), dim3(gx, (a.IC + 31) / 32, gz), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_dgrad<2, 1>), dim3(gx, (a.IC + 31) / 32, gz), dim3(256), 0, s, a);
+  } else {
+    if (np == 4) hipLaunchKernelGGL((k_dgrad<1, 4>), dim3(gx, (a.IC + 15) / 16, gz), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_dgrad<1, 1>), dim3(gx, (a.IC + 15) / 16, gz), dim3(256), 0, s, a);
+  }
+  return 0;
+}
+
+constexpr int kWgradNKT = 2;  // a wave: 32 gathered columns; a workgroup: 128
+
+struct WgradPlan {
+  int not_, ocg, kg, chunks;
+  long qchunk;
+  size_t part_floats;
+};
+
+WgradPlan plan_wgrad(int OC, int Kt, long Q) {
+  WgradPlan p;
+  p.not_ = OC >= 64 ? 4 : (OC >= 32 ? 2 : 1);
+  p.ocg = (OC + 16 * p.not_ - 1) / (16 * p.not_);
+  p.kg = (Kt + 1 + 64 * kWgradNKT - 1) / (64 * kWgradNKT);
+  long chunks = (2048 + (long)p.ocg * p.kg - 1) / ((long)p.ocg * p.kg);
+  chunks = chunks < 1 ? 1 : (chunks > 256 ? 256 : chunks);
+  const long maxc = (Q + 15) / 16;
+  if (chunks > maxc) chunks = maxc < 1 ? 1 : maxc;
+  p.qchunk = ((Q + chunks - 1) / chunks + 3) / 4 * 4;
+  p.chunks = (int)((Q + p.qchunk - 1) / p.qchunk);
+  p.part_floats = (size_t)p.chunks * OC * (Kt + 1);
+  return p;
+}
+
+int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap, hipStream_t s) {
+  if (a.Kt > kMaxKTab || a.OP > kMaxPTab) return -1;
+  const WgradPlan p = plan_wgrad(a.OC, a.Kt, (long)a.n * a.OP);
+  if (p.part_floats > part_cap) return -1;
+  a.qchunk = p.qchunk;
+  a.part = part;
+  const dim3 grid(p.chunks, p.ocg, p.kg);
+  if (p.not_ == 4) hipLaunchKernelGGL((k_wgrad<4, kWgradNKT>), grid, dim3(256), 0, s, a);
+  else if (p.not_ == 2) hipLaunchKernelGGL((k_wgrad<2, kWgradNKT>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((k_wgrad<1, kWgradNKT>), grid, dim3(256), 0, s, a);
+  const long per = (long)a.OC * (a.Kt + 1);
+  hipLaunchKernelGGL(k_wsum, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, part, p.chunks, a.OC, a.Kt, Gw, Gb);
+  return 0;
+}
+
+}  // namespace
+
+// the largest wgrad partial buffer any layer needs at max_batch rows
+static size_t carla_part_floats(const ppo_carla_layout& L, long B) {
+  size_t m = 0;
+  auto need = [&](int OC, int Kt, long Q) {
+    const size_t f = plan_wgrad(OC, Kt, Q).part_floats;
+    if (f > m) m = f;
+  };
+  for (int i = 0; i < PPO_CARLA_NCONV; ++i)
+    need(L.conv_oc[i], L.conv_ic[i] * L.conv_k[i] * L.conv_k[i], B * L.conv_oh[i] * L.conv_ow[i]);
+  need(512, 1280, B);
+  need(256, 512, B);
+  need(256, L.NM, B);
+  need(256, 256, B);
+  need(256, 256 + L.NV, B);
+  need(1, 256, B);
+  need(L.A, 256, B);
+  return m;
+}
+
+static int carla_train_init(ppo_carla_t* c) {
+  if (c->train_ready) return 0;
+  const ppo_carla_layout& L = c->L;
+  const size_t B = (size_t)c->cfg.max_batch;
+  int rc = 0;
+  rc |= carla_alloc(&c->G, L.P);
+  rc |= carla_alloc(&c->m, L.P);
+  rc |= carla_alloc(&c->v, L.P);
+  for (int i = 0; i < PPO_CARLA_NCONV - 1; ++i)
+    rc |= carla_alloc(&c->dact[i], B * L.conv_oc[i] * L.conv_oh[i] * L.conv_ow[i]);
+  rc |= carla_alloc(&c->denc, B * 1280);
+  rc |= carla_alloc(&c->ds1, B * 256);
+  rc |= carla_alloc(&c->dl1, B * 512);
+  rc |= carla_alloc(&c->dfeat, B * 256);
+  rc |= carla_alloc(&c->dv1, B * 256);
+  rc |= carla_alloc(&c->dv2, B * 256);
+  rc |= carla_alloc(&c->dp1, B * 256);
+  rc |= carla_alloc(&c->dp2, B * 256);
+  rc |= carla_alloc(&c->dhead, B * 2 * L.A);
+  rc |= carla_alloc(&c->dval, B);
+  rc |= carla_alloc(&c->lp, B);
+  rc |= carla_alloc(&c->ent, B);
+  rc |= carla_alloc(&c->rowstat, B * 8);
+  c->part_floats = carla_part_floats(L, (long)B);
+  rc |= carla_alloc(&c->part, c->part_floats);
+  rc |= carla_alloc(&c->small, 128 + 4 * PPO_CARLA_MAX_TENSORS);  // + int64 tensor table
+  if (rc) return ppo_fail("ppo_carla_update: device allocation failed", -2);
+  // tensor table (offsets / lengths as int64) after the scalars
+  std::vector<long> tab(2 * PPO_CARLA_MAX_TENSORS, 0);
+  for (int t = 0; t < L.ntensors; ++t) {
+    tab[t] = L.t_off[t];
+    tab[PPO_CARLA_MAX_TENSORS + t] = L.t_grad[t] ? L.t_len[t] : 0;
+  }
+  if (hipMemcpy(c->small + 128, tab.data(), tab.size() * sizeof(long), hipMemcpyHostToDevice) != hipSuccess)
+    return ppo_fail("ppo_carla_update: copy failed", -2);
+  c->train_ready = true;
+  return 0;
+}
+
+extern "C" int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc, int n, const uint8_t* bev,
+                                const float* meas, const float* vmeas, const float* actions, const float* old_logp,
+                                const float* adv, const float* ret, const float* old_v, float lr,
+                                ppo_carla_update_stats* stats, void* stream) {
+  if (!c || !tc || !bev || !meas || !actions || !old_logp || !adv || !ret || !old_v || (!vmeas && c->L.NV > 0))
+    return ppo_fail("ppo_carla_update: null argument", -1);
+  if (n <= 1 && tc->norm_adv) return ppo_fail("ppo_carla_update: advantage normalisation needs n >= 2", -1);
+  if (n <= 0 || n > c->cfg.max_batch) return ppo_fail("ppo_carla_update: n must be in [1, max_batch]", -1);
+  if (hipSetDevice(c->device) != hipSuccess) return ppo_fail("ppo_carla_update: hipSetDevice failed", -2);
+  int rc = carla_train_init(c);
+  if (rc) return rc;
+  const ppo_carla_layout& L = c->L;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  // forward with the given actions (ac_ppo_carla.cpp:543-546); activations stay in the context
+  rc = ppo_carla_forward(c, n, bev, meas, vmeas, PPO_CARLA_GIVEN, actions, 0, 0, nullptr, c->lp, c->ent, nullptr,
+                         nullptr, nullptr, s);
+  if (rc) return rc;
+  float* P = c->P;
+  float* G = c->G;
+  float* sm = c->small;
+  if (tc->norm_adv) hipLaunchKernelGGL(k_carla_advstats, dim3(1), dim3(256), 0, s, adv, n, sm);
+  HeadBwdArgs hb{P,      L.hi,    L.lo,      c->hpre,   actions,     c->lp,        c->ent,        c->val,
+                 old_logp, adv,   ret,       old_v,     sm,          n,            L.A,           c->cfg.beta_min,
+                 tc->clip_coef, tc->ent_coef, tc->vf_coef, tc->norm_adv, tc->clip_vloss, c->dhead, c->dval, c->rowstat};
+  hipLaunchKernelGGL(k_carla_head_bwd, dim3((n + 63) / 64), dim3(64), 0, s, hb);
+  int bad = 0;
+  // y = x W^T + b on rows: dz [n][OUT] (stride dzs), x [n][IN] (stride xs)
+  auto lin_w = [&](const float* dz, long dzs, int OUT, const float* x, long xs, int IN, long w, long b) {
+    WgradArgs a{dz, dzs, OUT, 1, 1, x, nullptr, xs, IN, 1, 1, 1, 1, n, IN, 0, nullptr};
+    bad |= launch_wgrad(a, G + w, G + b, c->part, c->part_floats, s);
+  };
+  auto lin_d = [&](const float* dz, long dzs, int OUT, long w, int w_in, const float* x, long xs, float* dx, long dxs,
+                   int IN, int accumulate) {
+    DgradArgs a{dz, dzs, P + w, w_in, x, xs, dx, dxs, IN, 1, 1, OUT, 1, 1, 1, 1, n, accumulate};
+    bad |= launch_dgrad(a, s);
+  };
+  const long FW = 256 + L.NV;
+  const int A = L.A;
+  // heads (carla_model.h:279-284): dist_mu / dist_sigma on the policy latent
+  lin_w(c->dhead, 2 * A, A, c->p2, 256, 256, L.mu_w, L.mu_b);
+  lin_w(c->dhead + A, 2 * A, A, c->p2, 256, 256, L.sg_w, L.sg_b);
+  lin_d(c->dhead, 2 * A, A, L.mu_w, 256, c->p2, 256, c->dp2, 256, 256, 0);
+  lin_d(c->dhead + A, 2 * A, A, L.sg_w, 256, c->p2, 256, c->dp2, 256, 256, 1);
+  // policy_head (:279)
+  lin_w(c->dp2, 256, 256, c->p1, 256, 256, L.pi_w[1], L.pi_b[1]);
+  lin_d(c->dp2, 256, 256, L.pi_w[1], 256, c->p1, 256, c->dp1, 256, 256, 0);
+  lin_w(c->dp1, 256, 256, c->feat, FW, 256, L.pi_w[0], L.pi_b[0]);
+  lin_d(c->dp1, 256, 256, L.pi_w[0], 256, c->feat, FW, c->dfeat, 256, 256, 0);
+  // value_head (:276-277)
+  lin_w(c->dval, 1, 1, c->v2, 256, 256, L.v_w[2], L.v_b[2]);
+  lin_d(c->dval, 1, 1, L.v_w[2], 256, c->v2, 256, c->dv2, 256, 256, 0);
+  lin_w(c->dv2, 256, 256, c->v1, 256, 256, L.v_w[1], L.v_b[1]);
+  lin_d(c->dv2, 256, 256, L.v_w[1], 256, c->v1, 256, c->dv1, 256, 256, 0);
+  lin_w(c->dv1, 256, 256, c->feat, FW, (int)FW, L.v_w[0], L.v_b[0]);
+  lin_d(c->dv1, 256, 256, L.v_w[0], (int)FW, c->feat, FW, c->dfeat, 256, 256, 1);
+  // linear (:240) and state_linear (:238)
+  lin_w(c->dfeat, 256, 256, c->l1, 512, 512, L.lin_w[1], L.lin_b[1]);
+  lin_d(c->dfeat, 256, 256, L.lin_w[1], 512, c->l1, 512, c->dl1, 512, 512, 0);
+  lin_w(c->dl1, 512, 512, c->enc, 1280, 1280, L.lin_w[0], L.lin_b[0]);
+  lin_d(c->dl1, 512, 512, L.lin_w[0], 1280, c->enc, 1280, c->denc, 1280, 1280, 0);
+  lin_w(c->denc + 1024, 1280, 256, c->s1, 256, 256, L.st_w[1], L.st_b[1]);
+  lin_d(c->denc + 1024, 1280, 256, L.st_w[1], 256, c->s1, 256, c->ds1, 256, 256, 0);
+  lin_w(c->ds1, 256, 256, meas, L.NM, L.NM, L.st_w[0], L.st_b[0]);
+  // cnn (:236), last layer first; conv i reads act[i-1] (the image for i = 0)
+  for (int i = PPO_CARLA_NCONV - 1; i >= 0; --i) {
+    const float* dz = i == PPO_CARLA_NCONV - 1 ? c->denc : c->dact[i];
+    const long dzs = i == PPO_CARLA_NCONV - 1 ? 1280 : (long)L.conv_oc[i] * L.conv_oh[i] * L.conv_ow[i];
+    const float* xf = i > 0 ? c->act[i - 1] : nullptr;
+    const long xs = (long)L.conv_ic[i] * L.conv_ih[i] * L.conv_iw[i];
+    WgradArgs wa{dz,          dzs,         L.conv_oc[i], L.conv_oh[i] * L.conv_ow[i], L.conv_ow[i], xf,
+                 i ? nullptr : bev, xs,    L.conv_ic[i], L.conv_ih[i],                L.conv_iw[i], L.conv_k[i],
+                 L.conv_s[i], n,           L.conv_ic[i] * L.conv_k[i] * L.conv_k[i], 0, nullptr};
+    bad |= launch_wgrad(wa, G + L.conv_w[i], G + L.conv_b[i], c->part, c->part_floats, s);
+    if (i > 0) {
+      DgradArgs da{dz,           dzs,          P + L.conv_w[i], L.conv_ic[i], xf,           xs,
+                   c->dact[i - 1], xs,         L.conv_ic[i],    L.conv_ih[i], L.conv_iw[i], L.conv_oc[i],
+                   L.conv_oh[i], L.conv_ow[i], L.conv_k[i],     L.conv_s[i],  n,            0};
+      bad |= launch_dgrad(da, s);
+    }
+  }
+  if (bad) return ppo_fail("ppo_carla_update: no gradient kernel for this shape", -1);
+  // clip_grad_norm_ + Adam (ac_ppo_carla.cpp:618-619)
+  const long* toff = (const long*)(sm + 128);
+  hipLaunchKernelGGL(k_carla_tnorm, dim3(L.ntensors), dim3(256), 0, s, G, toff, toff + PPO_CARLA_MAX_TENSORS, sm + 8);
+  c->step += 1;
+  const double bc1 = 1.0 - std::pow(0.9, (double)c->step), bc2 = 1.0 - std::pow(0.999, (double)c->step);
+  const long begin = 2;  // action_space_high / _low carry no gradient (registered with requires_grad false)
+  CarlaAdamArgs ad{P, G, c->m, c->v, begin, L.P - begin, sm + 8, L.ntensors, tc->max_grad_norm,
+                   (float)((double)lr / bc1), (float)std::sqrt(bc2), tc->adam_eps, sm + 70};
+  hipLaunchKernelGGL(k_carla_adam, dim3((unsigned)((L.P - begin + 255) / 256)), dim3(256), 0, s, ad);
+  hipLaunchKernelGGL(k_carla_stats, dim3(1), dim3(256), 0, s, c->rowstat, n, sm + 64);
+  if (hipGetLastError() != hipSuccess) return ppo_fail("ppo_carla_update: launch failed", -2);
+  if (stats) {
+    float h[8];
+    if (hipMemcpyAsync(h, sm + 64, sizeof h, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+      return ppo_fail("ppo_carla_update: stats copy failed", -2);
+    stats->pg_loss = h[0];
+    stats->v_loss = h[1];
+    stats->entropy = h[2];
+    stats->old_approx_kl = h[3];
+    stats->approx_kl = h[4];
+    stats->clipfrac = h[5];
+    stats->grad_norm = h[6];
+  }
+  return 0;
+}
+
+static int carla_d2h(ppo_carla_t* c, const float* dev, float* host, long n, const char* what) {
+  if (!c || !host) return ppo_fail(std::string(what) + ": null argument", -1);
+  if (n != c->L.P) return ppo_fail(std::string(what) + ": expected " + std::to_string(c->L.P) + " floats", -1);
+  if (!dev) return ppo_fail(std::string(what) + ": no training state yet (call ppo_carla_update first)", -1);
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess || hipMemcpy(host, dev, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess)
+    return ppo_fail(std::string(what) + ": copy failed", -2);
+  return 0;
+}
+
+extern "C" int ppo_carla_save_params(ppo_carla_t* c, float* host, long n) {
+  return carla_d2h(c, c ? c->P : nullptr, host, n, "ppo_carla_save_params");
+}
+
+extern "C" int ppo_carla_last_grad(ppo_carla_t* c, float* host, long n) {
+  return carla_d2h(c, c ? c->G : nullptr, host, n, "ppo_carla_last_grad");
+}
+
+extern "C" int ppo_carla_save_adam(ppo_carla_t* c, float* m_host, float* v_host, long n, long* step) {
+  if (!c || !step) return ppo_fail("ppo_carla_save_adam: null argument", -1);
+  if (!c->train_ready) {  // a fresh optimizer
+    if (!m_host || !v_host || n != c->L.P) return ppo_fail("ppo_carla_save_adam: bad arguments", -1);
+    std::fill(m_host, m_host + n, 0.0f);
+    std::fill(v_host, v_host + n, 0.0f);
+    *step = 0;
+    return 0;
+  }
+  int rc = carla_d2h(c, c->m, m_host, n, "ppo_carla_save_adam");
+  if (!rc) rc = carla_d2h(c, c->v, v_host, n, "ppo_carla_save_adam");
+  *step = c->step;
+  return rc;
+}
+
+extern "C" int ppo_carla_load_adam(ppo_carla_t* c, const float* m_host, const float* v_host, long n, long step) {
+  if (!c || !m_host || !v_host) return ppo_fail("ppo_carla_load_adam: null argument", -1);
+  if (n != c->L.P || step < 0) return ppo_fail("ppo_carla_load_adam: bad arguments", -1);
+  if (hipSetDevice(c->device) != hipSuccess) return ppo_fail("ppo_carla_load_adam: hipSetDevice failed", -2);
+  int rc = carla_train_init(c);
+  if (rc) return rc;
+  if (hipMemcpy(c->m, m_host, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->v, v_host, sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess)
+    return ppo_fail("ppo_carla_load_adam: copy failed", -2);
+  c->step = step;
   return 0;
 }

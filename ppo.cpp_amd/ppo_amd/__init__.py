@@ -91,6 +91,20 @@ class CarlaLayout(C.Structure):  # include/ppo_carla.h
                 ("t_grad", C.c_int * MAX_CT)]
 
 
+class CarlaTrainConfig(C.Structure):  # ppo_carla_train_config; defaults = carla_config.h:31-40
+    _fields_ = [("clip_coef", C.c_float), ("ent_coef", C.c_float), ("vf_coef", C.c_float),
+                ("max_grad_norm", C.c_float), ("adam_eps", C.c_float), ("norm_adv", C.c_int), ("clip_vloss", C.c_int)]
+
+
+class CarlaUpdateStats(C.Structure):
+    _fields_ = [("pg_loss", C.c_float), ("v_loss", C.c_float), ("entropy", C.c_float),
+                ("old_approx_kl", C.c_float), ("approx_kl", C.c_float), ("clipfrac", C.c_float),
+                ("grad_norm", C.c_float)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class CarlaConfig(C.Structure):  # ppo_carla_config; defaults = carla_config.h
     _fields_ = [("obs_channels", C.c_int), ("bev_h", C.c_int), ("bev_w", C.c_int), ("num_measurements", C.c_int),
                 ("num_value_measurements", C.c_int), ("action_dim", C.c_int), ("beta_min", C.c_float),
@@ -154,6 +168,12 @@ SYMBOLS = [
     ("ppo_carla_get_layout", _I, [_VP, C.POINTER(CarlaLayout)]),
     ("ppo_carla_load_params", _I, [_VP, _FP, _L]),
     ("ppo_carla_forward", _I, [_VP, _I, _VP, _FP, _FP, _I, _FP, _L, _L, _FP, _FP, _FP, _FP, _FP, _FP, _VP]),
+    ("ppo_carla_update", _I, [_VP, C.POINTER(CarlaTrainConfig), _I, _VP, _FP, _FP, _FP, _FP, _FP, _FP, _FP, _F,
+                              C.POINTER(CarlaUpdateStats), _VP]),
+    ("ppo_carla_save_params", _I, [_VP, _FP, _L]),
+    ("ppo_carla_last_grad", _I, [_VP, _FP, _L]),
+    ("ppo_carla_save_adam", _I, [_VP, _FP, _FP, _L, C.POINTER(_L)]),
+    ("ppo_carla_load_adam", _I, [_VP, _FP, _FP, _L, _L]),
     ("ppo_layout_fill", _I, [C.POINTER(Layout), _I, _I, _I, _I]),
     ("ppo_carla_layout_fill", _I, [C.POINTER(CarlaLayout), _I, _I, _I, _I, _I, _I]),
     ("ppo_pth_save_agent", _I, [C.POINTER(Layout), _FP, C.c_char_p]),
@@ -573,6 +593,37 @@ class CarlaAgent:
                                       *[o.ptr for o in out], None))
         check(lib().ppo_device_sync())
         return tuple(out)
+
+    def update(self, bev: DeviceArray, meas: DeviceArray, vmeas: DeviceArray, actions: DeviceArray,
+               old_logp: DeviceArray, adv: DeviceArray, ret: DeviceArray, old_v: DeviceArray, lr=3e-4,
+               clip_coef=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5, adam_eps=1e-5, norm_adv=True,
+               clip_vloss=True, want_stats=True):
+        """One minibatch of ac_ppo_carla.cpp:540-619 (loss, backward, clip_grad_norm_, Adam)."""
+        tc = CarlaTrainConfig(clip_coef, ent_coef, vf_coef, max_grad_norm, adam_eps, int(norm_adv), int(clip_vloss))
+        st = CarlaUpdateStats()
+        check(lib().ppo_carla_update(self._h, C.byref(tc), bev.shape[0], bev.ptr, meas.ptr, vmeas.ptr, actions.ptr,
+                                     old_logp.ptr, adv.ptr, ret.ptr, old_v.ptr, lr,
+                                     C.byref(st) if want_stats else None, None))
+        return st.as_dict() if want_stats else None
+
+    def params(self):
+        out = np.empty(self.layout.P, np.float32)
+        check(lib().ppo_carla_save_params(self._h, out.ctypes.data, out.size))
+        return out
+
+    def last_grad(self):
+        out = np.empty(self.layout.P, np.float32)
+        check(lib().ppo_carla_last_grad(self._h, out.ctypes.data, out.size))
+        return out
+
+    def adam_state(self):
+        m, v, step = np.empty(self.layout.P, np.float32), np.empty(self.layout.P, np.float32), C.c_long(0)
+        check(lib().ppo_carla_save_adam(self._h, m.ctypes.data, v.ctypes.data, m.size, C.byref(step)))
+        return m, v, step.value
+
+    def load_adam(self, m, v, step):
+        m, v = np.ascontiguousarray(m, np.float32), np.ascontiguousarray(v, np.float32)
+        check(lib().ppo_carla_load_adam(self._h, m.ctypes.data, v.ctypes.data, m.size, int(step)))
 
 
 class SynthEnv:

@@ -7,7 +7,8 @@
 //    1x1 plane — tiles over samples) x 16·NOT output channels. The im2col offsets of the K = IC·k·k
 //    reduction are a per-workgroup LDS table, so a B operand is one gathered load per lane and
 //    k-step; A operands (weights [OC][IC·k·k]) stream from L2. The uint8 image is converted
-//    (x / 255, carla_model.h:214-216) inside the first convolution's gather.
+//    (x / 255, carla_model.h:214-216, as x * (1/255): within 1 ulp) inside the first convolution's
+//    gather.
 //  * Concatenations are strides: conv6 and state_linear.2 write the two halves of the [n, 1280]
 //    linear input, linear.2 writes the first 256 columns of the [n, 256 + NV] value-head input.
 //  * k_carla_head: dist_mu / dist_sigma dot products, softplus + beta_min, the Beta sample (the
@@ -43,16 +44,19 @@ struct ConvArgs {
 
 constexpr int kConvWaves = 4;
 constexpr int kMaxKTab = 2048;  // im2col offset table entries (IC * K * K <= 1280 here)
+constexpr int kUK = 4;          // k-steps per loop iteration: their loads are all in flight together
 
 // a wave: NP tiles of 16 output pixels x NOT tiles of 16 output channels
-template <int NOT, int NP>
-__global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
-  __shared__ int koff[kMaxKTab];
+// Loads are unconditional from clamped addresses and masked with selects afterwards: a load under a
+// per-lane branch is followed by its own s_waitcnt, which serialises the gather latency.
+template <int NOT, int NP, bool U8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) void k_conv(ConvArgs a) {
+  __shared__ int koff[kMaxKTab + 4 * kUK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
   const int KK = a.K * a.K, Kt = a.IC * KK, plane = a.IH * a.IW;
-  for (int k = tid; k < Kt; k += 256) {
+  for (int k = tid; k < Kt + 4 * kUK; k += 256) {  // padding: the last iteration reads without a branch
     const int ic = k / KK, rem = k - ic * KK, ky = rem / a.K, kx = rem - ky * a.K;
-    koff[k] = ic * plane + ky * a.IW + kx;
+    koff[k] = k < Kt ? ic * plane + ky * a.IW + kx : 0;
   }
   __syncthreads();
   const int P = a.OH * a.OW;
@@ -85,23 +89,35 @@ __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
     ocv[t] = oc < a.OC;
     wrow[t] = a.W + (long)(ocv[t] ? oc : 0) * Kt;
   }
-#pragma unroll 8
-  for (int k0 = 0; k0 < Kt; k0 += 4) {
-    const int k = k0 + g;
-    const bool kv = k < Kt;
-    const int ko = kv ? koff[k] : 0;
-    float x[NP], w[NOT];
+  for (int k0 = 0; k0 < Kt; k0 += 4 * kUK) {
+    float x[kUK][NP], w[kUK][NOT];
 #pragma unroll
-    for (int u = 0; u < NP; ++u) {
-      x[u] = 0.f;
-      if (kv && qv[u]) x[u] = a.in_u8 ? (float)a.in_u8[xbase[u] + ko] / 255.0f : a.in_f[xbase[u] + ko];
+    for (int st = 0; st < kUK; ++st) {
+      const int k = k0 + 4 * st + g;
+      const bool kv = k < Kt;
+      const int ko = koff[k];
+#pragma unroll
+      for (int u = 0; u < NP; ++u) {
+        const bool ok = kv && qv[u];
+        const long off = ok ? xbase[u] + ko : 0;
+        if constexpr (U8) {
+          // unconditional load, masked as an integer; x / 255 as x * (1 / 255) (within 1 ulp of the
+          // reference's division: a division sequence serialises the gather behind VCC)
+          const int raw = a.in_u8[off];
+          x[st][u] = (float)(ok ? raw : 0) * (1.0f / 255.0f);
+        } else {
+          x[st][u] = a.in_f[off] * (ok ? 1.0f : 0.0f);  // a multiplicative mask keeps the load unconditional
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NOT; ++t) w[st][t] = wrow[t][kv ? k : 0] * ((kv && ocv[t]) ? 1.0f : 0.0f);
     }
 #pragma unroll
-    for (int t = 0; t < NOT; ++t) w[t] = (kv && ocv[t]) ? wrow[t][k] : 0.f;
+    for (int st = 0; st < kUK; ++st)
 #pragma unroll
-    for (int t = 0; t < NOT; ++t)
+      for (int t = 0; t < NOT; ++t)
 #pragma unroll
-      for (int u = 0; u < NP; ++u) acc[t][u] = mfma16(w[t], x[u], acc[t][u]);
+        for (int u = 0; u < NP; ++u) acc[t][u] = mfma16(w[st][t], x[st][u], acc[t][u]);
   }
   // lane (j, g) holds out channel oc0 + 16t + 4g + r of pixel q0 + 16u + j
 #pragma unroll
@@ -205,16 +221,24 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
   // load), one where the layer is narrow (Linear layers, the last convolutions)
   const int np = Q >= 16L * 4 * 2048 ? 4 : 1;
   const unsigned gx = (unsigned)((Q + 16 * kConvWaves * np - 1) / (16 * kConvWaves * np));
+  const bool u8 = a.in_u8 != nullptr;
+#define PPO_CONV_LAUNCH(NOT_, NP_)                                                                          \
+  do {                                                                                                     \
+    const dim3 grid(gx, (a.OC + 16 * NOT_ - 1) / (16 * NOT_));                                             \
+    if (u8) hipLaunchKernelGGL((k_conv<NOT_, NP_, true>), grid, dim3(256), 0, s, a);                        \
+    else hipLaunchKernelGGL((k_conv<NOT_, NP_, false>), grid, dim3(256), 0, s, a);                          \
+  } while (0)
   if (a.OC >= 64) {
-    if (np == 4) hipLaunchKernelGGL((k_conv<4, 4>), dim3(gx, (a.OC + 63) / 64), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_conv<4, 1>), dim3(gx, (a.OC + 63) / 64), dim3(256), 0, s, a);
+    if (np == 4) PPO_CONV_LAUNCH(4, 4);
+    else PPO_CONV_LAUNCH(4, 1);
   } else if (a.OC >= 32) {
-    if (np == 4) hipLaunchKernelGGL((k_conv<2, 4>), dim3(gx, (a.OC + 31) / 32), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_conv<2, 1>), dim3(gx, (a.OC + 31) / 32), dim3(256), 0, s, a);
+    if (np == 4) PPO_CONV_LAUNCH(2, 4);
+    else PPO_CONV_LAUNCH(2, 1);
   } else {
-    if (np == 4) hipLaunchKernelGGL((k_conv<1, 4>), dim3(gx, (a.OC + 15) / 16), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_conv<1, 1>), dim3(gx, (a.OC + 15) / 16), dim3(256), 0, s, a);
+    if (np == 4) PPO_CONV_LAUNCH(1, 4);
+    else PPO_CONV_LAUNCH(1, 1);
   }
+#undef PPO_CONV_LAUNCH
   return 0;
 }
 
@@ -242,7 +266,7 @@ struct ppo_carla {
   float *lp = nullptr, *ent = nullptr, *rowstat = nullptr;                    // rowstat [B][8]
   float *part = nullptr;                                 // wgrad partials
   size_t part_floats = 0;
-  float* small = nullptr;  // [0,2) adv mean/std, [8, 8+40) tensor norms, [64, 72) stats
+  float* small = nullptr;  // scalars, tensor table and norm slices (carla_train_init)
   long step = 0;
 };
 
@@ -412,19 +436,20 @@ struct DgradArgs {
 constexpr int kMaxDTab = 3072;
 
 template <int NOT, int NP>
-__global__ __launch_bounds__(256) void k_dgrad(DgradArgs a) {
-  __shared__ int woff[kMaxDTab], zoff[kMaxDTab];
-  __shared__ int dji[kMaxDTab];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) void k_dgrad(DgradArgs a) {
+  __shared__ int woff[kMaxDTab + 4 * kUK], zoff[kMaxDTab + 4 * kUK];
+  __shared__ int dji[kMaxDTab + 4 * kUK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
   const int S = a.S, K = a.K, KK = K * K;
   const int py = blockIdx.z / S, px = blockIdx.z - py * S;
   const int nj = (K - py + S - 1) / S, ni = (K - px + S - 1) / S;
   const int OP = a.OH * a.OW, Kt = a.OC * nj * ni;
-  for (int k = tid; k < Kt; k += 256) {
+  for (int k = tid; k < Kt + 4 * kUK; k += 256) {  // padding entries (valid offsets) for the last iteration
     const int oc = k / (nj * ni), rem = k - oc * nj * ni, jj = rem / ni, ii = rem - jj * ni;
-    woff[k] = oc * a.w_ic * KK + (py + S * jj) * K + (px + S * ii);
-    zoff[k] = oc * OP - jj * a.OW - ii;
-    dji[k] = (jj << 16) | ii;
+    const bool in = k < Kt;
+    woff[k] = in ? oc * a.w_ic * KK + (py + S * jj) * K + (px + S * ii) : 0;
+    zoff[k] = in ? oc * OP - jj * a.OW - ii : 0;
+    dji[k] = in ? (jj << 16) | ii : 0;
   }
   __syncthreads();
   const int H2 = (a.IH - py + S - 1) / S, W2 = (a.IW - px + S - 1) / S, P2 = H2 * W2;
@@ -460,24 +485,29 @@ __global__ __launch_bounds__(256) void k_dgrad(DgradArgs a) {
     icv[t] = ic < a.IC;
     wrow[t] = a.W + (long)(icv[t] ? ic : 0) * KK;
   }
-#pragma unroll 4
-  for (int k0 = 0; k0 < Kt; k0 += 4) {
-    const int k = k0 + g;
-    const bool kv = k < Kt;
-    const int wo = kv ? woff[k] : 0, zo = kv ? zoff[k] : 0, d = kv ? dji[k] : 0;
-    const int jj = d >> 16, ii = d & 0xFFFF;
-    float xb[NP], wa[NOT];
+  for (int k0 = 0; k0 < Kt; k0 += 4 * kUK) {
+    float xb[kUK][NP], wa[kUK][NOT];
 #pragma unroll
-    for (int u = 0; u < NP; ++u) {
-      const bool ok = kv && qv[u] && (unsigned)(iy2v[u] - jj) < (unsigned)a.OH && (unsigned)(ix2v[u] - ii) < (unsigned)a.OW;
-      xb[u] = ok ? a.dz[zb[u] + zo] : 0.f;
+    for (int st = 0; st < kUK; ++st) {
+      const int k = k0 + 4 * st + g;
+      const bool kv = k < Kt;
+      const int wo = woff[k], zo = zoff[k], d = dji[k];
+      const int jj = d >> 16, ii = d & 0xFFFF;
+#pragma unroll
+      for (int u = 0; u < NP; ++u) {
+        const bool ok =
+            kv && qv[u] && (unsigned)(iy2v[u] - jj) < (unsigned)a.OH && (unsigned)(ix2v[u] - ii) < (unsigned)a.OW;
+        xb[st][u] = a.dz[ok ? zb[u] + zo : 0] * (ok ? 1.0f : 0.0f);
+      }
+#pragma unroll
+      for (int t = 0; t < NOT; ++t) wa[st][t] = wrow[t][wo] * ((kv && icv[t]) ? 1.0f : 0.0f);
     }
 #pragma unroll
-    for (int t = 0; t < NOT; ++t) wa[t] = (kv && icv[t]) ? wrow[t][wo] : 0.f;
+    for (int st = 0; st < kUK; ++st)
 #pragma unroll
-    for (int t = 0; t < NOT; ++t)
+      for (int t = 0; t < NOT; ++t)
 #pragma unroll
-      for (int u = 0; u < NP; ++u) acc[t][u] = mfma16(wa[t], xb[u], acc[t][u]);
+        for (int u = 0; u < NP; ++u) acc[t][u] = mfma16(wa[st][t], xb[st][u], acc[t][u]);
   }
   const long plane = (long)a.IH * a.IW;
 #pragma unroll
@@ -512,8 +542,8 @@ struct WgradArgs {
 
 constexpr int kMaxPTab = 9216;  // output pixels per sample (94 x 94 = 8836 for conv1)
 
-template <int NOT, int NKT>
-__global__ __launch_bounds__(256) void k_wgrad(WgradArgs a) {
+template <int NOT, int NKT, bool U8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) void k_wgrad(WgradArgs a) {
   __shared__ int koff[kMaxKTab];
   __shared__ int pbase[kMaxPTab];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
@@ -557,29 +587,53 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs a) {
   long q = qs + g;
   long s = q / a.OP;
   int p = (int)(q - s * a.OP);
-  for (long qb = qs; qb < qe; qb += 4) {
-    const bool qv = q < qe;
-    float av[NOT], bv[NKT];
-    const long sb = s * a.dz_stride, xb = s * a.x_stride + (qv ? pbase[p] : 0);
+  const bool wrap1 = a.OP >= 4;
+  // U q-steps per iteration: all their loads are issued before their MFMAs (the narrow layers have
+  // the longest pixel runs and the fewest MFMAs per load, so they get the deepest batch)
+  constexpr int U = NOT == 1 ? 8 : 2;
+  for (long qb = qs; qb < qe; qb += 4 * U) {
+    float av[U][NOT], bv[U][NKT];
 #pragma unroll
-    for (int t = 0; t < NOT; ++t) av[t] = (qv && ocv[t]) ? a.dz[sb + dzo[t] + p] : 0.f;
+    for (int st = 0; st < U; ++st) {
+      const bool qv = q < qe;
+      const long sb = s * a.dz_stride, xb = s * a.x_stride + (qv ? pbase[p] : 0);
 #pragma unroll
-    for (int u = 0; u < NKT; ++u) {
-      float xv = 0.f;
-      if (qv && kc[u] == 0) xv = a.x_u8 ? (float)a.x_u8[xb + ko[u]] / 255.0f : a.x_f[xb + ko[u]];
-      else if (qv && kc[u] == 1) xv = 1.0f;
-      bv[u] = xv;
+      for (int t = 0; t < NOT; ++t) {
+        const bool ok = qv && ocv[t];
+        av[st][t] = a.dz[ok ? sb + dzo[t] + p : 0] * (ok ? 1.0f : 0.0f);
+      }
+#pragma unroll
+      for (int u = 0; u < NKT; ++u) {
+        const bool ok = qv && kc[u] == 0;
+        const long off = ok ? xb + ko[u] : 0;
+        float v;
+        if constexpr (U8) {
+          const int raw = a.x_u8[off];
+          v = (float)(ok ? raw : 0) * (1.0f / 255.0f);
+        } else {
+          v = a.x_f[off] * (ok ? 1.0f : 0.0f);
+        }
+        bv[st][u] = (qv && kc[u] == 1) ? 1.0f : v;
+      }
+      q += 4;
+      p += 4;
+      if (wrap1) {  // OP >= 4: at most one sample boundary per step (branch-free)
+        const bool w = p >= a.OP;
+        p -= w ? a.OP : 0;
+        s += w ? 1 : 0;
+      } else {
+        while (p >= a.OP) {
+          p -= a.OP;
+          ++s;
+        }
+      }
     }
 #pragma unroll
-    for (int t = 0; t < NOT; ++t)
+    for (int st = 0; st < U; ++st)
 #pragma unroll
-      for (int u = 0; u < NKT; ++u) acc[t][u] = mfma16(av[t], bv[u], acc[t][u]);
-    q += 4;
-    p += 4;
-    while (p >= a.OP) {
-      p -= a.OP;
-      ++s;
-    }
+      for (int t = 0; t < NOT; ++t)
+#pragma unroll
+        for (int u = 0; u < NKT; ++u) acc[t][u] = mfma16(av[st][t], bv[st][u], acc[t][u]);
   }
   float* out = a.part + (long)blockIdx.x * a.OC * (a.Kt + 1);
 #pragma unroll
@@ -596,7 +650,20 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs a) {
     }
 }
 
-// G[w + oc*Kt + k] / G[b + oc] = sum over chunks, in chunk order
+// G[w + oc*Kt + k] / G[b + oc] = sum over chunks. Level 1 (k_wsum1) adds groups of kSumGroup
+// consecutive chunks in parallel (blockIdx.y = group), level 2 (k_wsum) adds the group sums in order:
+// a fixed order, so the result is deterministic.
+constexpr int kSumGroup = 32;
+
+__global__ void k_wsum1(const float* __restrict__ part, int chunks, long per, float* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= per) return;
+  const int c0 = blockIdx.y * kSumGroup, c1 = c0 + kSumGroup < chunks ? c0 + kSumGroup : chunks;
+  float acc = 0.f;
+  for (int c = c0; c < c1; ++c) acc += part[(long)c * per + i];
+  out[(long)blockIdx.y * per + i] = acc;
+}
+
 __global__ void k_wsum(const float* __restrict__ part, int chunks, int OC, int Kt, float* __restrict__ Gw,
                        float* __restrict__ Gb) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -729,13 +796,16 @@ __global__ __launch_bounds__(256) void k_carla_stats(const float* __restrict__ r
   if (threadIdx.x < 6) out[threadIdx.x] = red[threadIdx.x][0] / (float)n * (threadIdx.x == 1 ? 0.5f : 1.0f);
 }
 
-// per-tensor L2 norm of the gradient (clip_grad.h: grad.norm()), one block per tensor
+constexpr int kNormSplit = 32;
+
+// per-tensor sums of squares of the gradient, kNormSplit slices per tensor (blockIdx.y)
 __global__ __launch_bounds__(256) void k_carla_tnorm(const float* __restrict__ G, const long* __restrict__ off,
-                                                     const long* __restrict__ len, float* __restrict__ norms) {
+                                                     const long* __restrict__ len, float* __restrict__ part) {
   __shared__ float red[256];
-  const int t = blockIdx.x;
+  const int t = blockIdx.x, sp = blockIdx.y;
+  const long n = len[t], per = (n + kNormSplit - 1) / kNormSplit, b = sp * per, e = b + per < n ? b + per : n;
   float q = 0.f;
-  for (long i = threadIdx.x; i < len[t]; i += 256) {
+  for (long i = b + threadIdx.x; i < e; i += 256) {
     const float x = G[off[t] + i];
     q += x * x;
   }
@@ -745,33 +815,38 @@ __global__ __launch_bounds__(256) void k_carla_tnorm(const float* __restrict__ G
     if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) norms[t] = sqrtf(red[0]);
+  if (threadIdx.x == 0) part[t * kNormSplit + sp] = red[0];
+}
+
+// clip_grad_norm_ (clip_grad.h): norm_t = ||g_t|| (slices added in order), total = ||(norm_t)||,
+// coef = clamp(max_norm / (total + 1e-6), max = 1); out = {total, coef}
+__global__ void k_carla_tsum(const float* __restrict__ part, int nt, float max_norm, float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  float tot = 0.f;
+  for (int t = 0; t < nt; ++t) {
+    float q = 0.f;
+    for (int sp = 0; sp < kNormSplit; ++sp) q += part[t * kNormSplit + sp];
+    const float nrm = sqrtf(q);
+    tot += nrm * nrm;
+  }
+  const float total = sqrtf(tot);
+  const float coef = max_norm / (total + 1e-6f);
+  out[0] = total;
+  out[1] = coef > 1.0f ? 1.0f : coef;
 }
 
 struct CarlaAdamArgs {
   float *P, *G, *m, *v;
-  long begin, n;             // trainable range [begin, begin + n)
-  const float* norms;        // [nt] (0 for tensors without gradient)
-  int nt;
-  float max_norm, step_size, sbc2, eps;
-  float* total_out;          // grad_norm stat
+  long begin, n;        // trainable range [begin, begin + n)
+  const float* clip;    // {total, coef} from k_carla_tsum
+  float step_size, sbc2, eps;
 };
 
 __global__ __launch_bounds__(256) void k_carla_adam(CarlaAdamArgs a) {
-  __shared__ float s_coef;
-  if (threadIdx.x == 0) {
-    float tot = 0.f;
-    for (int t = 0; t < a.nt; ++t) tot += a.norms[t] * a.norms[t];
-    const float total = sqrtf(tot);
-    float coef = a.max_norm / (total + 1e-6f);
-    s_coef = coef > 1.0f ? 1.0f : coef;
-    if (blockIdx.x == 0) a.total_out[0] = total;
-  }
-  __syncthreads();
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= a.n) return;
   const long p = a.begin + i;
-  const float gv = a.G[p] * s_coef;
+  const float gv = a.G[p] * a.clip[1];
   const float m = a.m[p] * 0.9f + gv * 0.1f;
   const float v = a.v[p] * 0.999f + gv * gv * 0.001f;
   a.m[p] = m;
@@ -813,13 +888,16 @@ WgradPlan plan_wgrad(int OC, int Kt, long Q) {
   p.not_ = OC >= 64 ? 4 : (OC >= 32 ? 2 : 1);
   p.ocg = (OC + 16 * p.not_ - 1) / (16 * p.not_);
   p.kg = (Kt + 1 + 64 * kWgradNKT - 1) / (64 * kWgradNKT);
-  long chunks = (2048 + (long)p.ocg * p.kg - 1) / ((long)p.ocg * p.kg);
-  chunks = chunks < 1 ? 1 : (chunks > 256 ? 256 : chunks);
+  long chunks = (8192 + (long)p.ocg * p.kg - 1) / ((long)p.ocg * p.kg);
+  chunks = chunks < 1 ? 1 : (chunks > 4096 ? 4096 : chunks);
+  const long cap = (32L << 20) / ((long)OC * (Kt + 1));  // partials <= 32 M floats
+  if (chunks > cap) chunks = cap < 1 ? 1 : cap;
   const long maxc = (Q + 15) / 16;
   if (chunks > maxc) chunks = maxc < 1 ? 1 : maxc;
   p.qchunk = ((Q + chunks - 1) / chunks + 3) / 4 * 4;
   p.chunks = (int)((Q + p.qchunk - 1) / p.qchunk);
-  p.part_floats = (size_t)p.chunks * OC * (Kt + 1);
+  const int groups = (p.chunks + kSumGroup - 1) / kSumGroup;
+  p.part_floats = (size_t)(p.chunks + (p.chunks > kSumGroup ? groups : 0)) * OC * (Kt + 1);
   return p;
 }
 
@@ -830,11 +908,26 @@ int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap
   a.qchunk = p.qchunk;
   a.part = part;
   const dim3 grid(p.chunks, p.ocg, p.kg);
-  if (p.not_ == 4) hipLaunchKernelGGL((k_wgrad<4, kWgradNKT>), grid, dim3(256), 0, s, a);
-  else if (p.not_ == 2) hipLaunchKernelGGL((k_wgrad<2, kWgradNKT>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((k_wgrad<1, kWgradNKT>), grid, dim3(256), 0, s, a);
+  if (a.x_u8) {
+    if (p.not_ == 4) hipLaunchKernelGGL((k_wgrad<4, kWgradNKT, true>), grid, dim3(256), 0, s, a);
+    else if (p.not_ == 2) hipLaunchKernelGGL((k_wgrad<2, kWgradNKT, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_wgrad<1, kWgradNKT, true>), grid, dim3(256), 0, s, a);
+  } else {
+    if (p.not_ == 4) hipLaunchKernelGGL((k_wgrad<4, kWgradNKT, false>), grid, dim3(256), 0, s, a);
+    else if (p.not_ == 2) hipLaunchKernelGGL((k_wgrad<2, kWgradNKT, false>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_wgrad<1, kWgradNKT, false>), grid, dim3(256), 0, s, a);
+  }
   const long per = (long)a.OC * (a.Kt + 1);
-  hipLaunchKernelGGL(k_wsum, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, s, part, p.chunks, a.OC, a.Kt, Gw, Gb);
+  const unsigned gb = (unsigned)((per + 255) / 256);
+  if (p.chunks > kSumGroup) {
+    // level 1 writes its group sums after the chunk partials (sized by plan_wgrad)
+    const int groups = (p.chunks + kSumGroup - 1) / kSumGroup;
+    float* lvl = part + (size_t)p.chunks * per;
+    hipLaunchKernelGGL(k_wsum1, dim3(gb, groups), dim3(256), 0, s, part, p.chunks, per, lvl);
+    hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, lvl, groups, a.OC, a.Kt, Gw, Gb);
+  } else {
+    hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, part, p.chunks, a.OC, a.Kt, Gw, Gb);
+  }
   return 0;
 }
 
@@ -884,7 +977,8 @@ static int carla_train_init(ppo_carla_t* c) {
   rc |= carla_alloc(&c->rowstat, B * 8);
   c->part_floats = carla_part_floats(L, (long)B);
   rc |= carla_alloc(&c->part, c->part_floats);
-  rc |= carla_alloc(&c->small, 128 + 4 * PPO_CARLA_MAX_TENSORS);  // + int64 tensor table
+  // [0,2) adv mean/std, [64,71) stats + {total, coef}, [128,288) int64 tensor table, [320,...) norm slices
+  rc |= carla_alloc(&c->small, 320 + PPO_CARLA_MAX_TENSORS * kNormSplit);
   if (rc) return ppo_fail("ppo_carla_update: device allocation failed", -2);
   // tensor table (offsets / lengths as int64) after the scalars
   std::vector<long> tab(2 * PPO_CARLA_MAX_TENSORS, 0);
@@ -981,12 +1075,14 @@ extern "C" int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc
   if (bad) return ppo_fail("ppo_carla_update: no gradient kernel for this shape", -1);
   // clip_grad_norm_ + Adam (ac_ppo_carla.cpp:618-619)
   const long* toff = (const long*)(sm + 128);
-  hipLaunchKernelGGL(k_carla_tnorm, dim3(L.ntensors), dim3(256), 0, s, G, toff, toff + PPO_CARLA_MAX_TENSORS, sm + 8);
+  hipLaunchKernelGGL(k_carla_tnorm, dim3(L.ntensors, kNormSplit), dim3(256), 0, s, G, toff,
+                     toff + PPO_CARLA_MAX_TENSORS, sm + 320);
+  hipLaunchKernelGGL(k_carla_tsum, dim3(1), dim3(64), 0, s, sm + 320, L.ntensors, tc->max_grad_norm, sm + 70);
   c->step += 1;
   const double bc1 = 1.0 - std::pow(0.9, (double)c->step), bc2 = 1.0 - std::pow(0.999, (double)c->step);
   const long begin = 2;  // action_space_high / _low carry no gradient (registered with requires_grad false)
-  CarlaAdamArgs ad{P, G, c->m, c->v, begin, L.P - begin, sm + 8, L.ntensors, tc->max_grad_norm,
-                   (float)((double)lr / bc1), (float)std::sqrt(bc2), tc->adam_eps, sm + 70};
+  CarlaAdamArgs ad{P, G, c->m, c->v, begin, L.P - begin, sm + 70, (float)((double)lr / bc1), (float)std::sqrt(bc2),
+                   tc->adam_eps};
   hipLaunchKernelGGL(k_carla_adam, dim3((unsigned)((L.P - begin + 255) / 256)), dim3(256), 0, s, ad);
   hipLaunchKernelGGL(k_carla_stats, dim3(1), dim3(256), 0, s, c->rowstat, n, sm + 64);
   if (hipGetLastError() != hipSuccess) return ppo_fail("ppo_carla_update: launch failed", -2);

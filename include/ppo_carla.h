@@ -172,6 +172,20 @@ int ppo_carla_last_grad(ppo_carla_t* c, float* host, long n);
 int ppo_carla_save_adam(ppo_carla_t* c, float* m_host, float* v_host, long n, long* step);
 int ppo_carla_load_adam(ppo_carla_t* c, const float* m_host, const float* v_host, long n, long step);
 
+/* ---- data parallelism (ac_ppo_carla.cpp:243, 561-616; torchfort::Comm, distributed.cpp:81-224) ----
+ * One RCCL communicator per agent; id from ppo_comm_unique_id (ppo_hip.h), PPO_COMM_ID_BYTES bytes.
+ * With a communicator attached (any world >= 1), every ppo_carla_update
+ *   - takes the minibatch advantage mean as the rank average of the local means and the std
+ *     from the all-reduced sum of squares with Bessel's correction over world * n - 1
+ *     (ac_ppo_carla.cpp:561-580),
+ *   - all-reduces (average) the gradient of every trainable tensor before clip_grad_norm_ (:608-616),
+ *   - averages the returned loss statistics over ranks (:645-651; grad_norm is already global).
+ * world = 1 runs the same collective sequence over a one-rank communicator (results equal the
+ * communicator-free update bit for bit). */
+int ppo_carla_comm_init(ppo_carla_t* c, const char* id, int rank, int world);
+/* ac_ppo_carla.cpp:241-244: every parameter from `root` to all ranks */
+int ppo_carla_comm_broadcast_params(ppo_carla_t* c, int root);
+
 #ifdef __cplusplus
 }
 #endif

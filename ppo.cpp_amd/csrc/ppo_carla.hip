@@ -15,9 +15,11 @@
 //    Philox / Marsaglia-Tsang contract of the MLP agents), mean, roach_deterministic or the given
 //    action, log_prob and entropy (rl_utils.h:87-132), one thread per row.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -268,6 +270,9 @@ struct ppo_carla {
   size_t part_floats = 0;
   float* small = nullptr;  // scalars, tensor table and norm slices (carla_train_init)
   long step = 0;
+  // data parallelism (ppo_carla_comm_init): one RCCL communicator, any world >= 1
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1;
 };
 
 static int carla_alloc(float** p, size_t n) {
@@ -279,6 +284,7 @@ extern "C" int ppo_carla_destroy(ppo_carla_t* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
   float* bufs[] = {c->P,    c->enc,  c->s1,  c->l1,  c->feat,  c->v1,  c->v2,      c->val,  c->p1,
                    c->p2,   c->hpre, c->G,   c->m,   c->v,     c->denc, c->ds1,     c->dl1,  c->dfeat,
                    c->dv1,  c->dv2,  c->dp1, c->dp2, c->dhead, c->dval, c->lp,      c->ent,  c->rowstat,
@@ -676,6 +682,34 @@ __global__ void k_wsum(const float* __restrict__ part, int chunks, int OC, int K
   else Gb[oc] = acc;
 }
 
+// the same statistics in the distributed order of ac_ppo_carla.cpp:561-580, one block each:
+// phase 0: out[0] = local mean; phase 1: out[2] = sum (adv - out[0])^2 about the (all-reduced) mean
+__global__ __launch_bounds__(256) void k_carla_adv_part(const float* __restrict__ adv, int n, float* __restrict__ out,
+                                                        int phase) {
+  __shared__ float red[256];
+  float s = 0.f;
+  if (phase == 0) {
+    for (int i = threadIdx.x; i < n; i += 256) s += adv[i];
+  } else {
+    const float mean = out[0];
+    for (int i = threadIdx.x; i < n; i += 256) s += (adv[i] - mean) * (adv[i] - mean);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (phase == 0) out[0] = red[0] / (float)n;
+    else out[2] = red[0];
+  }
+}
+// out[1] = sqrt(sum of squares over all ranks / (world * n - 1))
+__global__ void k_carla_adv_fin(float* __restrict__ out, float denom) {
+  if (threadIdx.x == 0) out[1] = sqrtf(out[2] / denom);
+}
+
 // minibatch advantage mean / std (Bessel), one block, fixed summation order
 __global__ __launch_bounds__(256) void k_carla_advstats(const float* __restrict__ adv, int n, float* __restrict__ out) {
   __shared__ float red[256];
@@ -1012,7 +1046,19 @@ extern "C" int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc
   float* P = c->P;
   float* G = c->G;
   float* sm = c->small;
-  if (tc->norm_adv) hipLaunchKernelGGL(k_carla_advstats, dim3(1), dim3(256), 0, s, adv, n, sm);
+  if (tc->norm_adv) {
+    if (c->comm) {  // ac_ppo_carla.cpp:564-578: averaged mean, summed squares, Bessel over world * n
+      hipLaunchKernelGGL(k_carla_adv_part, dim3(1), dim3(256), 0, s, adv, n, sm, 0);
+      if (ncclAllReduce(sm, sm, 1, ncclFloat, ncclAvg, c->comm, s) != ncclSuccess)
+        return ppo_fail("ppo_carla_update: advantage mean all-reduce failed", -3);
+      hipLaunchKernelGGL(k_carla_adv_part, dim3(1), dim3(256), 0, s, adv, n, sm, 1);
+      if (ncclAllReduce(sm + 2, sm + 2, 1, ncclFloat, ncclSum, c->comm, s) != ncclSuccess)
+        return ppo_fail("ppo_carla_update: advantage variance all-reduce failed", -3);
+      hipLaunchKernelGGL(k_carla_adv_fin, dim3(1), dim3(64), 0, s, sm, (float)(c->world * n - 1));
+    } else {
+      hipLaunchKernelGGL(k_carla_advstats, dim3(1), dim3(256), 0, s, adv, n, sm);
+    }
+  }
   HeadBwdArgs hb{P,      L.hi,    L.lo,      c->hpre,   actions,     c->lp,        c->ent,        c->val,
                  old_logp, adv,   ret,       old_v,     sm,          n,            L.A,           c->cfg.beta_min,
                  tc->clip_coef, tc->ent_coef, tc->vf_coef, tc->norm_adv, tc->clip_vloss, c->dhead, c->dval, c->rowstat};
@@ -1073,6 +1119,10 @@ extern "C" int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc
     }
   }
   if (bad) return ppo_fail("ppo_carla_update: no gradient kernel for this shape", -1);
+  const long begin = 2;  // action_space_high / _low carry no gradient (registered with requires_grad false)
+  // gradient average over ranks before clipping (ac_ppo_carla.cpp:608-616)
+  if (c->comm && ncclAllReduce(G + begin, G + begin, (size_t)(L.P - begin), ncclFloat, ncclAvg, c->comm, s) != ncclSuccess)
+    return ppo_fail("ppo_carla_update: gradient all-reduce failed", -3);
   // clip_grad_norm_ + Adam (ac_ppo_carla.cpp:618-619)
   const long* toff = (const long*)(sm + 128);
   hipLaunchKernelGGL(k_carla_tnorm, dim3(L.ntensors, kNormSplit), dim3(256), 0, s, G, toff,
@@ -1080,13 +1130,15 @@ extern "C" int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc
   hipLaunchKernelGGL(k_carla_tsum, dim3(1), dim3(64), 0, s, sm + 320, L.ntensors, tc->max_grad_norm, sm + 70);
   c->step += 1;
   const double bc1 = 1.0 - std::pow(0.9, (double)c->step), bc2 = 1.0 - std::pow(0.999, (double)c->step);
-  const long begin = 2;  // action_space_high / _low carry no gradient (registered with requires_grad false)
   CarlaAdamArgs ad{P, G, c->m, c->v, begin, L.P - begin, sm + 70, (float)((double)lr / bc1), (float)std::sqrt(bc2),
                    tc->adam_eps};
   hipLaunchKernelGGL(k_carla_adam, dim3((unsigned)((L.P - begin + 255) / 256)), dim3(256), 0, s, ad);
   hipLaunchKernelGGL(k_carla_stats, dim3(1), dim3(256), 0, s, c->rowstat, n, sm + 64);
   if (hipGetLastError() != hipSuccess) return ppo_fail("ppo_carla_update: launch failed", -2);
   if (stats) {
+    // loss statistics averaged over ranks (ac_ppo_carla.cpp:645-651); the total norm is global already
+    if (c->comm && ncclAllReduce(sm + 64, sm + 64, 6, ncclFloat, ncclAvg, c->comm, s) != ncclSuccess)
+      return ppo_fail("ppo_carla_update: statistics all-reduce failed", -3);
     float h[8];
     if (hipMemcpyAsync(h, sm + 64, sizeof h, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
       return ppo_fail("ppo_carla_update: stats copy failed", -2);
@@ -1145,4 +1197,37 @@ extern "C" int ppo_carla_load_adam(ppo_carla_t* c, const float* m_host, const fl
     return ppo_fail("ppo_carla_load_adam: copy failed", -2);
   c->step = step;
   return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// data parallelism: RCCL communicator (replaces torchfort::Comm, distributed.cpp:81-224)
+// ------------------------------------------------------------------------------------------
+extern "C" int ppo_carla_comm_init(ppo_carla_t* c, const char* id, int rank, int world) {
+  if (!c || !id) return ppo_fail("ppo_carla_comm_init: null argument", -1);
+  if (world < 1 || rank < 0 || rank >= world) return ppo_fail("ppo_carla_comm_init: bad rank / world", -1);
+  if (hipSetDevice(c->device) != hipSuccess) return ppo_fail("ppo_carla_comm_init: hipSetDevice failed", -2);
+  if (c->comm) {
+    (void)ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  ncclUniqueId uid;
+  static_assert(sizeof(ncclUniqueId) <= PPO_COMM_ID_BYTES, "ncclUniqueId size");
+  memcpy(&uid, id, sizeof(uid));
+  const ncclResult_t r = ncclCommInitRank(&c->comm, world, uid, rank);
+  if (r != ncclSuccess) {
+    c->comm = nullptr;
+    return ppo_fail(std::string("ppo_carla_comm_init: ncclCommInitRank: ") + ncclGetErrorString(r), -3);
+  }
+  c->rank = rank;
+  c->world = world;
+  return 0;
+}
+
+extern "C" int ppo_carla_comm_broadcast_params(ppo_carla_t* c, int root) {
+  if (!c) return ppo_fail("ppo_carla_comm_broadcast_params: null argument", -1);
+  if (!c->comm) return 0;
+  if (hipSetDevice(c->device) != hipSuccess) return ppo_fail("ppo_carla_comm_broadcast_params: hipSetDevice failed", -2);
+  if (ncclBroadcast(c->P, c->P, (size_t)c->L.P, ncclFloat, root, c->comm, c->stream) != ncclSuccess)
+    return ppo_fail("ppo_carla_comm_broadcast_params: ncclBroadcast failed", -3);
+  return hipStreamSynchronize(c->stream) == hipSuccess ? 0 : ppo_fail("ppo_carla_comm_broadcast_params: sync failed", -2);
 }

@@ -174,6 +174,8 @@ SYMBOLS = [
     ("ppo_carla_last_grad", _I, [_VP, _FP, _L]),
     ("ppo_carla_save_adam", _I, [_VP, _FP, _FP, _L, C.POINTER(_L)]),
     ("ppo_carla_load_adam", _I, [_VP, _FP, _FP, _L, _L]),
+    ("ppo_carla_comm_init", _I, [_VP, C.c_char_p, _I, _I]),
+    ("ppo_carla_comm_broadcast_params", _I, [_VP, _I]),
     ("ppo_layout_fill", _I, [C.POINTER(Layout), _I, _I, _I, _I]),
     ("ppo_carla_layout_fill", _I, [C.POINTER(CarlaLayout), _I, _I, _I, _I, _I, _I]),
     ("ppo_pth_save_agent", _I, [C.POINTER(Layout), _FP, C.c_char_p]),
@@ -624,6 +626,14 @@ class CarlaAgent:
     def load_adam(self, m, v, step):
         m, v = np.ascontiguousarray(m, np.float32), np.ascontiguousarray(v, np.float32)
         check(lib().ppo_carla_load_adam(self._h, m.ctypes.data, v.ctypes.data, m.size, int(step)))
+
+    def comm_init(self, uid: bytes, rank=0, world=1):
+        """Attach an RCCL communicator (ac_ppo_carla.cpp:561-616 data parallelism); uid from
+        Agent.comm_unique_id()."""
+        check(lib().ppo_carla_comm_init(self._h, uid, rank, world))
+
+    def comm_broadcast_params(self, root=0):
+        check(lib().ppo_carla_comm_broadcast_params(self._h, root))
 
 
 class SynthEnv:

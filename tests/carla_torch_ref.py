@@ -40,7 +40,11 @@ def _beta_lp_ent(al, be, x):
 
 
 def update(L, p, bev, meas, vmeas, act, old_logp, adv, ret, old_v, clip=0.2, ent_coef=0.01, vf_coef=0.5,
-           max_grad_norm=0.5, lr=3e-4, eps=1e-5, beta_min=1.0, norm_adv=True, clip_vloss=True):
+           max_grad_norm=0.5, lr=3e-4, eps=1e-5, beta_min=1.0, norm_adv=True, clip_vloss=True, adv_stats=None,
+           allreduce_grads=None):
+    """adv_stats: (mean, std) to normalise with instead of this minibatch's own (the all-reduced
+    statistics of ac_ppo_carla.cpp:561-580); allreduce_grads(list of grad tensors): called after
+    backward and before clip_grad_norm_ (:608-616)."""
     names, t = _tensors(L, p)
     x = torch.tensor(bev).float() / 255.0
     for i in range(6):
@@ -65,7 +69,10 @@ def update(L, p, bev, meas, vmeas, act, old_logp, adv, ret, old_v, clip=0.2, ent
     ratio = logratio.exp()
     mb_adv = torch.tensor(adv)
     if norm_adv:
-        mb_adv = (mb_adv - mb_adv.mean()) / (mb_adv.std() + 1e-8)
+        if adv_stats is None:
+            mb_adv = (mb_adv - mb_adv.mean()) / (mb_adv.std() + 1e-8)
+        else:
+            mb_adv = (mb_adv - adv_stats[0]) / (adv_stats[1] + 1e-8)
     pg = torch.max(-mb_adv * ratio, -mb_adv * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
     R, ov = torch.tensor(ret), torch.tensor(old_v)
     if clip_vloss:
@@ -75,6 +82,8 @@ def update(L, p, bev, meas, vmeas, act, old_logp, adv, ret, old_v, clip=0.2, ent
         vl = 0.5 * ((value - R) ** 2).mean()
     loss = pg - ent_coef * ent.mean() + vf_coef * vl
     loss.backward()
+    if allreduce_grads is not None:
+        allreduce_grads([t[n].grad for n in names if t[n].grad is not None])
     with torch.no_grad():
         stats = [pg.item(), vl.item(), ent.mean().item(), (-logratio).mean().item(),
                  ((ratio - 1) - logratio).mean().item(), ((ratio - 1).abs() > clip).float().mean().item()]

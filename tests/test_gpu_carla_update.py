@@ -116,3 +116,34 @@ def test_update_argument_errors(agent):
     x = DeviceArray.from_numpy(np.zeros((1, 2), np.float32))
     with pytest.raises(ppo_amd.PPOError, match="n >= 2"):
         agent.update(DeviceArray.from_numpy(np.zeros((1, 15, 192, 192), np.uint8), np.uint8), x, x, x, x, x, x, x)
+
+
+def test_update_with_one_rank_communicator_is_bit_identical():
+    """ppo_carla_comm_init with world = 1 runs the distributed sequence (split advantage statistics,
+    RCCL all-reduces of the advantage mean, sum of squares, gradient and loss stats); on one rank it
+    must reproduce the communicator-free update bit for bit. The 2-rank exchange itself is covered
+    by tests/test_carla_dist_gloo.py."""
+    L = CI.layout()
+    p = CI.params(L)
+    n = 8
+    rng = np.random.default_rng(3)
+    bev = rng.integers(0, 256, size=(n, 15, 192, 192), dtype=np.uint8)
+    f = lambda *shape: rng.uniform(-1, 1, shape).astype(np.float32)  # noqa: E731
+    batch = (bev, f(n, 8), f(n, 3), f(n, 2) * 0.9, f(n) * 0.2, rng.standard_normal(n).astype(np.float32),
+             rng.standard_normal(n).astype(np.float32), f(n) * 0.1)
+    out = []
+    for with_comm in (False, True):
+        ag = ppo_amd.CarlaAgent(max_batch=n, seed=7)
+        try:
+            ag.load_params(p)
+            if with_comm:
+                ag.comm_init(ppo_amd.Agent.comm_unique_id(), 0, 1)
+                ag.comm_broadcast_params(0)
+            res = [_run_update(ag, *batch) for _ in range(2)]
+            out.append(res)
+        finally:
+            ag.close()
+    for (st0, g0, p0), (st1, g1, p1) in zip(*out):
+        np.testing.assert_array_equal(g0, g1)
+        np.testing.assert_array_equal(p0, p1)
+        assert st0 == st1

@@ -54,6 +54,7 @@ struct UpdArgs {
   float* slab[2];
   int actn_off, acc_off, spar_off;  // k_upd: runtime LDS offsets (floats)
   int trunk_mask;         // k_upd: trunks to run (bit t = trunk t; 3 = both)
+  int sched;              // k_upd: bit 0 actor workgroups dispatched first, bit 1 actor wave priority
 };
 
 // k_upd geometry (ppo_update.hip)

@@ -329,8 +329,12 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
   const int wf = wave % WF, wr = wave / WF;
   const int fbase = wf * FT * 16, rbase = wr * RT * 16;
-  const int trunk = blockIdx.y;
+  // The actor's tile is the longer one (Beta loss, larger head); the hardware issues the oldest
+  // wave first, so the actor workgroups are dispatched first (grid row 0) and, with sched bit 1,
+  // also raise their wave priority; the critic's MFMA stream fills the actor's latency gaps.
+  const int trunk = (a.sched & 1) ? 1 - (int)blockIdx.y : (int)blockIdx.y;
   if (!((a.trunk_mask >> trunk) & 1)) return;
+  if ((a.sched & 2) && trunk == 1) __builtin_amdgcn_s_setprio(1);
   const PackedLayout& K = a.K;
   const TrunkDev& T = K.tr[trunk];
   const float* __restrict__ P = a.P;
@@ -942,6 +946,9 @@ int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hi
   const char* ev = getenv("PPO_UPD_TRUNK");
   UpdArgs b = a;
   b.trunk_mask = (ev && (ev[0] == '0' || ev[0] == '1')) ? 1 << (ev[0] - '0') : 3;
+  // schedule bits (UpdArgs::sched); PPO_UPD_SCHED=<0..3> for A/B
+  const char* es = getenv("PPO_UPD_SCHED");
+  b.sched = (es && es[0] >= '0' && es[0] <= '3') ? es[0] - '0' : 1;
   const dim3 grid(nblocks, 2);
   return dispatch_upd(a.K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_) {
     hipLaunchKernelGGL((k_upd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value,

@@ -570,6 +570,29 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) hp[ht][rt] = f4{0.f, 0.f, 0.f, 0.f};
     lds_barrier();  // every wave is done reading h1 from ACT
+    if (trunk == 0) {
+      // critic: one real head of NHP — a per-row dot product on the VALU (in-lane over the wave's
+      // features, then the 4 lane groups) instead of 15/16-padding MFMAs
+      float pv[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) pv[rt] = 0.f;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+        const f4 w = pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const f4 h2 = h2_of(ft, rt);
+          lds_st4(ACT + (rbase + 16 * rt + j) * LDA + fbase + 16 * ft + 4 * g, h2);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pv[rt] = fmaf(w[r], h2[r], pv[rt]);
+        }
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        pv[rt] = row_allreduce(pv[rt]);
+        if (g == 0) SCR[(wf * NHP) * R + rbase + 16 * rt + j] = pv[rt];
+      }
+    } else {
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft) {
       f4 wv[NHT];
@@ -597,6 +620,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) SCR[(wf * NHP + 16 * ht + 4 * g + r) * R + rbase + 16 * rt + j] = hp[ht][rt][r];
+    }  // actor heads
     lds_barrier();
     PPO_STAMP(5);
     for (int idx = tid; idx < R * nh; idx += 256) {
@@ -748,6 +772,21 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     // ---------------- head backward: dh2 = W3^T G^T, dW3 += G^T h2 ----------------
     f4 dh[FT][RT];
     zero<FT, RT>(dh);
+    if (trunk == 0) {
+      // critic: dh2 = w3 g (outer product), dW3 = column sums of g h2 over the rows (VALU)
+      float gr[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) gr[rt] = lds_f(GG + (rbase + 16 * rt + j) * LDG);
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+        const f4 w = pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dh[ft][rt][r] = w[r] * gr[rt];
+      }
+      col_sums<FT, RT>([&](int ft, int rt, int r) { return gr[rt] * h2_of(ft, rt)[r]; }, acc + sg.hW, fbase, j, g);
+    } else {
 #pragma unroll
     for (int ht = 0; ht < NHT; ++ht) {
 #pragma unroll
@@ -780,6 +819,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
         }
       }
     }
+    }  // actor head backward
 
     PPO_STAMP(8);
     // ---------------- layer-2 backward: dz2 ----------------

@@ -91,7 +91,10 @@ PPO_DEV float bld1(PBuf b, int lane_floats, int uni_floats) {
 // out[ft][rt] (+)= sum_k W[fbase + 16 ft + i][k] * IN[rbase + 16 rt + j][k], k in [0, 16 NKB)
 //   wlane = (fbase + i) * LDW + 4 g (per lane), in = IN + (rbase + j) * LDI + 4 g (LDS, per lane)
 // A (weights) double-buffered one 16-wide k-block ahead; B (activations) one ds_read_b128 per row tile.
-template <int FT, int RT, int NKB, int LDW, int LDI>
+// KL (1 or 4): k-steps of the last 16-wide k-block that hold a real column — step c covers columns
+// 16 kb + 4 g + c, so with KL = 1 (K = 16 (NKB - 1) + 1, layer 1 at O = 17) the last block's y / z / w
+// steps are all padding and are skipped (5 of 8 steps).
+template <int FT, int RT, int NKB, int LDW, int LDI, int KL = 4>
 PPO_DEV void mm_fr(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* in) {
   f4 w[2][FT];
 #pragma unroll
@@ -107,14 +110,17 @@ PPO_DEV void mm_fr(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* in) {
     f4 b[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) b[rt] = lds_f4(in + 16 * rt * LDI + 16 * kb);
+    const bool full = kb + 1 < NKB || KL >= 4;
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
         out[ft][rt] = mfma16(w[kb & 1][ft].x, b[rt].x, out[ft][rt]);
-        out[ft][rt] = mfma16(w[kb & 1][ft].y, b[rt].y, out[ft][rt]);
-        out[ft][rt] = mfma16(w[kb & 1][ft].z, b[rt].z, out[ft][rt]);
-        out[ft][rt] = mfma16(w[kb & 1][ft].w, b[rt].w, out[ft][rt]);
+        if (full) {
+          out[ft][rt] = mfma16(w[kb & 1][ft].y, b[rt].y, out[ft][rt]);
+          out[ft][rt] = mfma16(w[kb & 1][ft].z, b[rt].z, out[ft][rt]);
+          out[ft][rt] = mfma16(w[kb & 1][ft].w, b[rt].w, out[ft][rt]);
+        }
       }
   }
 }
@@ -297,7 +303,7 @@ PPO_DEV int head_bias(const PackedLayout& K, int trunk, int h) {
 
 }  // namespace
 
-template <int H, int KIND, int NTO, int NHT>
+template <int H, int KIND, int NTO, int NHT, int KL1>
 __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
   using GE = Geo<H, NTO, NHT>;
   constexpr int FT = GE::FT, RT = GE::RT, WF = GE::WF, R = GE::R, NT = GE::NT, OP = GE::OP;
@@ -496,7 +502,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     // ---------------- layer 1 ----------------
     f4 z[FT][RT];
     init_bias<FT, RT>(z, pb, T.b1 + fbase + 4 * g);
-    mm_fr<FT, RT, NTO, OP, LDX>(z, pb, w1lane, xn_in);
+    mm_fr<FT, RT, NTO, OP, LDX, KL1>(z, pb, w1lane, xn_in);
     PPO_STAMP(1);
     float mu1[RT], rs1[RT];
     if constexpr (LN) {
@@ -873,7 +879,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     PPO_STAMP(10);
     // ---------------- recompute layer 1, layer-1 backward ----------------
     init_bias<FT, RT>(z, pb, T.b1 + fbase + 4 * g);
-    mm_fr<FT, RT, NTO, OP, LDX>(z, pb, w1lane, xn_in);
+    mm_fr<FT, RT, NTO, OP, LDX, KL1>(z, pb, w1lane, xn_in);
     PPO_STAMP(11);
     if constexpr (LN) {
       float s1[RT], s2[RT];
@@ -956,23 +962,28 @@ static void upd_geo(const PackedLayout& K, int sg_size, UpdGeoOut* g) {
 template <typename F>
 static int dispatch_upd(const PackedLayout& K, int nh, F&& f) {
   const int nto = K.OP / 16, nht = (nh + 15) / 16;
-#define PPO_UPD_CASE(H_, KIND_, NTO_, NHT_)                                                                   \
-  if (K.H == H_ && K.kind == KIND_ && nto == NTO_ && nht == NHT_)                                             \
+  const int kl = (K.O == 16 * (nto - 1) + 1) ? 1 : 4;  // layer 1: one real column in the last k-block
+#define PPO_UPD_CASE(H_, KIND_, NTO_, NHT_, KL_)                                                             \
+  if (K.H == H_ && K.kind == KIND_ && nto == NTO_ && nht == NHT_ && kl == KL_)                               \
     return f(std::integral_constant<int, H_>{}, std::integral_constant<int, KIND_>{},                        \
-             std::integral_constant<int, NTO_>{}, std::integral_constant<int, NHT_>{});
-  PPO_UPD_CASE(256, PPO_NET_LN_BETA, 1, 1) PPO_UPD_CASE(256, PPO_NET_LN_BETA, 2, 1)
-  PPO_UPD_CASE(256, PPO_NET_LN_BETA, 7, 1) PPO_UPD_CASE(256, PPO_NET_LN_BETA, 24, 3)
-  PPO_UPD_CASE(256, PPO_NET_LN_BETA, 2, 3) PPO_UPD_CASE(256, PPO_NET_TANH_NORMAL, 2, 1)
+             std::integral_constant<int, NTO_>{}, std::integral_constant<int, NHT_>{},                       \
+             std::integral_constant<int, KL_>{});
+  PPO_UPD_CASE(256, PPO_NET_LN_BETA, 1, 1, 4) PPO_UPD_CASE(256, PPO_NET_LN_BETA, 2, 1, 4)
+  PPO_UPD_CASE(256, PPO_NET_LN_BETA, 2, 1, 1) PPO_UPD_CASE(256, PPO_NET_LN_BETA, 7, 1, 4)
+  PPO_UPD_CASE(256, PPO_NET_LN_BETA, 24, 3, 4) PPO_UPD_CASE(256, PPO_NET_LN_BETA, 2, 3, 4)
+  PPO_UPD_CASE(256, PPO_NET_LN_BETA, 2, 3, 1) PPO_UPD_CASE(256, PPO_NET_TANH_NORMAL, 2, 1, 4)
+  PPO_UPD_CASE(256, PPO_NET_TANH_NORMAL, 2, 1, 1)
 #undef PPO_UPD_CASE
   return -1;
 }
 
 int upd_supported(const PackedLayout& K, int nh_actor, int sg_size, UpdGeoOut* g) {
   // both trunks run in one launch: the geometry must cover the actor's head count (critic: 1)
-  return dispatch_upd(K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_) {
+  return dispatch_upd(K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_, auto KL_) {
     (void)KIND_;
     upd_geo<decltype(H_)::value, decltype(NTO_)::value, decltype(NHT_)::value>(K, sg_size, g);
-    const auto k = k_upd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value, decltype(NHT_)::value>;
+    const auto k = k_upd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value, decltype(NHT_)::value,
+                         decltype(KL_)::value>;
     return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) ==
                    hipSuccess
                ? 0
@@ -990,9 +1001,9 @@ int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hi
   const char* es = getenv("PPO_UPD_SCHED");
   b.sched = (es && es[0] >= '0' && es[0] <= '3') ? es[0] - '0' : 1;
   const dim3 grid(nblocks, 2);
-  return dispatch_upd(a.K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_) {
+  return dispatch_upd(a.K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_, auto KL_) {
     hipLaunchKernelGGL((k_upd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value,
-                              decltype(NHT_)::value>),
+                              decltype(NHT_)::value, decltype(KL_)::value>),
                        grid, dim3(256), lds_bytes, s, b);
     return 0;
   });

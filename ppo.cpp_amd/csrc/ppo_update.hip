@@ -486,6 +486,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     pref_data(blockIdx.x);
   }
 
+  float lst[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // per-lane loss statistics over this workgroup's tiles
   for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
     const int m0 = it * R;
     PPO_STAMP_START();
@@ -747,19 +748,9 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
         }
       }
     }
-    // loss statistics: rows live in wave 0 (R <= 64)
-    if (wave == 0) {
-      float s0 = st_a, s1 = st_b, s2 = st_c, s3 = st_d, s4 = st_e, s5 = st_f;
-#pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) {
-        s0 += shfl_xor(s0, m); s1 += shfl_xor(s1, m); s2 += shfl_xor(s2, m);
-        s3 += shfl_xor(s3, m); s4 += shfl_xor(s4, m); s5 += shfl_xor(s5, m);
-      }
-      if (lane == 0) {
-        float* st = ACC + sg.stats;  // row group 0's accumulator
-        st[ST_PG] += s0; st[ST_V] += s1; st[ST_ENT] += s2; st[ST_OKL] += s3; st[ST_KL] += s4; st[ST_CF] += s5;
-      }
-    }
+    // loss statistics: rows live in wave 0 (R <= 64); summed per lane over the tiles, reduced
+    // across lanes once after the tile loop (reported values only, no gradient depends on them)
+    lst[0] += st_a; lst[1] += st_b; lst[2] += st_c; lst[3] += st_d; lst[4] += st_e; lst[5] += st_f;
     lds_barrier();
     PPO_STAMP(7);
     // head bias (and logstd) gradients: fixed-order sums over the workgroup's rows
@@ -930,6 +921,17 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     PPO_STAMP(12);
   }
   // ---------------- workgroup result (row groups summed in a fixed order) ----------------
+  if (wave == 0) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) lst[k] += shfl_xor(lst[k], m);
+    if (lane == 0) {
+      float* st = ACC + sg.stats;  // row group 0's accumulator
+      st[ST_PG] += lst[0]; st[ST_V] += lst[1]; st[ST_ENT] += lst[2];
+      st[ST_OKL] += lst[3]; st[ST_KL] += lst[4]; st[ST_CF] += lst[5];
+    }
+  }
   lds_barrier();
   float* out = a.slab[trunk] + (size_t)blockIdx.x * sg.size;
   for (int i = tid; i < sg.size; i += 256) {

@@ -1139,8 +1139,12 @@ __global__ void k_transpose(const float* __restrict__ src, float* __restrict__ d
 }
 
 // =============================================================================================
-// k_gae — one thread per env, t = T-1 .. 0; op-for-op fp32 (no contraction), ppo:447-467
+// k_gae — one thread per env, t = T-1 .. 0; op-for-op fp32 (no contraction), ppo:447-467.
+// The recurrence stays serial per env (bit-exact with the reference's order); its inputs are not:
+// rewards / values / dones of kGaeChunk steps are loaded together (coalesced over envs, loads
+// unconditional with a clamped step), so T steps cost T / kGaeChunk memory round trips.
 // =============================================================================================
+constexpr int kGaeChunk = 32;
 __global__ __launch_bounds__(256) void k_gae(GaeArgs a) {
 #pragma clang fp contract(off)
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1150,17 +1154,30 @@ __global__ __launch_bounds__(256) void k_gae(GaeArgs a) {
   float last = 0.0f;
   float nnt = (1.0f - a.next_done[e]);
   float nv = a.next_value[e];
-  for (int t = a.T - 1; t >= 0; --t) {
-    const long idx = (long)t * E + e;
-    const float r = a.rewards[idx], v = a.values[idx];
-    const float gnv = (a.gamma * nv);
-    const float delta = ((r + (gnv * nnt)) - v);
-    const float adv = (delta + ((gl * nnt) * last));
-    a.adv[idx] = adv;
-    a.ret[idx] = (adv + v);
-    last = adv;
-    nnt = (1.0f - a.dones[idx]);
-    nv = v;
+  for (int t1 = a.T - 1; t1 >= 0; t1 -= kGaeChunk) {
+    float rr[kGaeChunk], vv[kGaeChunk], dd[kGaeChunk];
+#pragma unroll
+    for (int k = 0; k < kGaeChunk; ++k) {
+      const int t = t1 - k >= 0 ? t1 - k : 0;
+      const long idx = (long)t * E + e;
+      rr[k] = a.rewards[idx];
+      vv[k] = a.values[idx];
+      dd[k] = a.dones[idx];
+    }
+#pragma unroll
+    for (int k = 0; k < kGaeChunk; ++k) {
+      if (t1 - k < 0) break;
+      const long idx = (long)(t1 - k) * E + e;
+      const float r = rr[k], v = vv[k];
+      const float gnv = (a.gamma * nv);
+      const float delta = ((r + (gnv * nnt)) - v);
+      const float adv = (delta + ((gl * nnt) * last));
+      a.adv[idx] = adv;
+      a.ret[idx] = (adv + v);
+      last = adv;
+      nnt = (1.0f - dd[k]);
+      nv = v;
+    }
   }
 }
 

@@ -846,7 +846,7 @@ struct psyn_env {
 
 extern "C" int psyn_create(int E, int O, int A, psyn_t** out) {
   if (!out || E <= 0 || O <= 0 || A <= 0) return fail("psyn_create: bad arguments");
-  if (O > PSYN_MAXO) return fail("psyn_create: obs_dim > 32 is not supported by the device env");
+  if (O > PSYN_MAXO) return fail("psyn_create: obs_dim > 384 is not supported by the device env");
   psyn_t* env = new psyn_t();
   memset(&env->a, 0, sizeof(env->a));
   (void)hipGetDevice(&env->device);

@@ -1349,6 +1349,91 @@ __global__ __launch_bounds__(256) void k_synth_step(SynthArgs a, int e0, int e1,
   a.autoreset[e] = tr ? 1 : 0;
 }
 
+// Wide observations (32 < O <= 64 * kSynthWideChunks, e.g. Ant 105, Humanoid 376): one wave per
+// env, lane l holds dims l, l + 64, ...; every old q is in registers before any write, so the
+// in-place update keeps the same semantics (and the same fp32 ops) as k_synth_step.
+constexpr int kSynthWideChunks = 6;
+__global__ __launch_bounds__(256) void k_synth_step_wide(SynthArgs a, int e0, int e1, const float* __restrict__ act,
+                                                         float lo, float hi, float* __restrict__ obs,
+                                                         float* __restrict__ reward, float* __restrict__ done) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const int e = e0 + blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= e1) return;  // uniform per wave
+  const int O = a.O, A = a.A;
+  float* __restrict__ q = a.q + (long)e * O;
+  const float* __restrict__ ar = act + (long)(e - e0) * A;
+  float qv[kSynthWideChunks];
+#pragma unroll
+  for (int c = 0; c < kSynthWideChunks; ++c) {
+    const int i = 64 * c + lane;
+    qv[c] = q[i < O ? i : O - 1];
+  }
+  const bool reset = a.autoreset[e] != 0;
+  if (reset) {
+    const uint32_t rs = a.rseed[e], rc = a.rcount[e];
+#pragma unroll
+    for (int c = 0; c < kSynthWideChunks; ++c) {
+      const int i = 64 * c + lane;
+      if (i < O) {
+        uint32_t r[4];
+        philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, r);
+        const float v = (0.1f * ((2.0f * u01(r[0])) - 1.0f));
+        q[i] = v;
+        obs[(long)e * O + i] = v;
+      }
+    }
+    if (lane == 0) {
+      a.rcount[e] = rc + 1;
+      a.t[e] = 0;
+      a.ep_ret[e] = 0.0f;
+      a.ep_len[e] = 0;
+      reward[e] = 0.0f;
+      done[e] = 0.0f;
+      a.autoreset[e] = 0;
+    }
+    return;
+  }
+  const float q0 = __shfl(qv[0], 0, 64);
+  float q0_new = 0.0f, q0_old = 0.0f;
+#pragma unroll
+  for (int c = 0; c < kSynthWideChunks; ++c) {
+    // old q_(i+1 mod O): the next lane, lane 0 of the next chunk, or q_0 for i = O - 1
+    const float up = __shfl(qv[c], (lane + 1) & 63, 64);
+    const float nxt = c + 1 < kSynthWideChunks ? __shfl(qv[c + 1 < kSynthWideChunks ? c + 1 : c], 0, 64) : 0.0f;
+    const int i = 64 * c + lane;
+    const float qn = (i + 1 == O) ? q0 : (lane < 63 ? up : nxt);
+    if (i < O) {
+      const float ai = fminf(fmaxf(ar[i % A], lo), hi);
+      const float nq = __fmaf_rn(0.9f, qv[c], __fmaf_rn(0.1f, ai, (0.05f * qn)));
+      q[i] = nq;
+      obs[(long)e * O + i] = nq;
+      if (i == 0) { q0_new = nq; q0_old = qv[c]; }
+    }
+  }
+  if (lane != 0) return;
+  const float vel = ((q0_new - q0_old) / 0.05f);
+  float ctrl = 0.0f;
+  for (int k = 0; k < A; ++k) {
+    const float ak = fminf(fmaxf(ar[k], lo), hi);
+    ctrl = (ctrl + ((0.1f * ak) * ak));
+  }
+  const float r = (vel - ctrl);
+  const int t = a.t[e] + 1;
+  a.t[e] = t;
+  const bool tr = t >= 1000;
+  reward[e] = r;
+  done[e] = tr ? 1.0f : 0.0f;
+  a.ep_ret[e] = (a.ep_ret[e] + r);
+  a.ep_len[e] += 1;
+  if (tr) {
+    a.fin_ret[e] += a.ep_ret[e];
+    a.fin_len[e] += (float)a.ep_len[e];
+    a.fin_cnt[e] += 1.0f;
+  }
+  a.autoreset[e] = tr ? 1 : 0;
+}
+
 // =============================================================================================
 // explicit instantiations / launch wrappers
 // =============================================================================================
@@ -1511,6 +1596,11 @@ void launch_synth_reset(const SynthArgs& a, int seed, float* obs, float* done, h
 }
 void launch_synth_step(const SynthArgs& a, int e0, int e1, const float* act, float lo, float hi, float* obs,
                        float* reward, float* done, hipStream_t s) {
+  if (a.O > 32) {
+    hipLaunchKernelGGL(k_synth_step_wide, dim3((e1 - e0 + 3) / 4), dim3(256), 0, s, a, e0, e1, act, lo, hi, obs,
+                       reward, done);
+    return;
+  }
   hipLaunchKernelGGL(k_synth_step, dim3((e1 - e0 + 7) / 8), dim3(256), 0, s, a, e0, e1, act, lo, hi, obs, reward,
                      done);
 }

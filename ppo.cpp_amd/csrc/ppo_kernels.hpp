@@ -134,7 +134,7 @@ struct AdvArgs {
 };
 #define PPO_ADV_SPLIT 32
 
-#define PSYN_MAXO 32  // device synthetic env: max observation width
+#define PSYN_MAXO 384  // device synthetic env: max observation width (k_synth_step_wide above 32)
 struct SynthArgs {
   int E, O, A;
   float* q;

@@ -276,8 +276,10 @@ def test_permutation_matches_oracle_and_is_a_permutation():
 # ------------------------------------------------------------------------------------------------
 # synthetic device env vs oracle env (bit-exact) and a full small iteration vs the oracle
 # ------------------------------------------------------------------------------------------------
-def test_synth_env_bit_exact_vs_oracle():
-    E, O_, A = 300, 17, 6
+@pytest.mark.parametrize("O_,A", [(17, 6), (105, 8), (376, 17)])
+def test_synth_env_bit_exact_vs_oracle(O_, A):
+    """k_synth_step (O <= 32) and k_synth_step_wide (Ant / Humanoid widths) vs the oracle env."""
+    E = 300
     env = ppo_amd.SynthEnv(E, O_, A)
     oenv = O.SynthEnv(E, O_, A)
     obs = DeviceArray((E, O_)); done = DeviceArray(E); rew = DeviceArray(E)

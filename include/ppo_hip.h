@@ -114,9 +114,21 @@ float* ppo_buffer(ppo_t* ctx, int which);
 /* ---- data-parallel communicator (RCCL over xGMI) ---- */
 #define PPO_COMM_ID_BYTES 128
 int ppo_comm_unique_id(char id_out[PPO_COMM_ID_BYTES]);
-/* attaches a communicator for (rank, world) to the context; subsequent ppo_update calls average
- * gradients and advantage statistics over ranks. */
+/* attaches an RCCL communicator for (rank, world) to the context (world = 1 included: a one-rank
+ * group runs the distributed sequence). While one is attached, ppo_update computes the advantage
+ * statistics over the group (mean averaged, sum of squares summed, Bessel over world * M;
+ * ac:830-849), averages the flat gradient before clip_grad_norm_ (ac:877-885) and averages the
+ * logged stats (ac:895-901). A context created with world_size > 1 refuses ppo_update until a
+ * communicator is attached. */
 int ppo_comm_init(ppo_t* ctx, const char id[PPO_COMM_ID_BYTES], int rank, int world);
+/* Host-transport communicator: the same sequence with every all-reduce handed to fn in host memory
+ * (in place over n floats; average != 0: mean over ranks, else sum; return 0 on success) — the
+ * reference Comm's MPI path for CPU tensors (distributed.cpp:134-148). Lets MPI / gloo callers
+ * drive the data-parallel update without RCCL. */
+typedef int (*ppo_host_allreduce_fn)(float* host_buf, long n, int average, void* user);
+int ppo_comm_init_host(ppo_t* ctx, int rank, int world, ppo_host_allreduce_fn fn, void* user);
+int ppo_comm_destroy(ppo_t* ctx);
+/* comm->broadcast of every parameter from root (ac:551-553) */
 int ppo_comm_broadcast_params(ppo_t* ctx, int root);
 int ppo_comm_allreduce(ppo_t* ctx, float* buf_dev, long n, int average);
 

@@ -814,3 +814,108 @@ void orc_carla_forward(const ppo_carla_layout* L, const float* P, float beta_min
   free(b0);
   free(b1);
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* PPO env wrapper chain over a scripted env (ppo:41-49; stateful_observation.h:56-84,          */
+/* stateful_reward.h:55-91, common.h:11-66, gym.h:141-159)                                      */
+/* ------------------------------------------------------------------------------------------ */
+static float stream_u01(uint32_t stream, uint32_t i) { return orc_u01(orc_mix32(orc_mix32(stream * 0x9E3779B1u) ^ i)); }
+
+typedef struct wrap_state {
+  int O, c, ep_len;
+  float ep_ret;
+  float *om, *ov, ocount;                /* NormalizeObservation: float32 state, count_ = 1e-4 */
+  float rmean, rvar, racc, rcount;       /* NormalizeReward: count_ = 1e-8 */
+} wrap_state;
+
+static void wrap_obs(wrap_state* w, const float* x, float* y) {
+  /* update (stateful_observation.h:64-84), then (x - mean) / sqrt(var + eps), then clamp (ppo:44) */
+  const float batch_count = 1.0f;
+  const float tot_count = w->ocount + batch_count;
+  for (int i = 0; i < w->O; ++i) {
+    const float delta = x[i] - w->om[i];
+    const float new_mean = w->om[i] + delta * batch_count / tot_count;
+    const float m_a = w->ov[i] * w->ocount;
+    const float m_b = 0.0f * batch_count;
+    const float M2 = m_a + m_b + (delta * delta) * w->ocount * batch_count / tot_count;
+    w->om[i] = new_mean;
+    w->ov[i] = M2 / tot_count;
+  }
+  w->ocount = tot_count;
+  for (int i = 0; i < w->O; ++i) {
+    float v = (x[i] - w->om[i]) / sqrtf(w->ov[i] + 1e-4f);
+    y[i] = v < -10.0f ? -10.0f : (v > 10.0f ? 10.0f : v);
+  }
+}
+
+static void script_obs(const wrap_state* w, float* x) {
+  for (int i = 0; i < w->O; ++i) {
+    const float lo = (float)i - 2.0f, hi = (float)i + 3.0f;
+    x[i] = lo + (hi - lo) * stream_u01(30, (uint32_t)(w->c * w->O + i));
+  }
+}
+
+void orc_wrappers_run(int O, int T, int reset_at, float gamma, float* obs, float* reward, float* term, float* trunc,
+                      float* info_ret, float* info_len, float* obs_mean, float* obs_var) {
+  wrap_state w;
+  memset(&w, 0, sizeof(w));
+  w.O = O;
+  w.om = (float*)calloc((size_t)O, sizeof(float));
+  w.ov = (float*)malloc(sizeof(float) * O);
+  for (int i = 0; i < O; ++i) w.ov[i] = 1.0f;
+  w.ocount = 1e-4f;
+  w.rvar = 1.0f;
+  w.rcount = 1e-8f;
+  float* x = (float*)malloc(sizeof(float) * O);
+  /* reset: RecordEpisodeStatistics clears its counters; NormalizeReward keeps its accumulator */
+#define WRAP_RESET(dst)                    \
+  do {                                     \
+    script_obs(&w, x);                     \
+    w.c++;                                 \
+    w.ep_ret = 0.0f;                       \
+    w.ep_len = 0;                          \
+    wrap_obs(&w, x, (dst));                \
+  } while (0)
+  WRAP_RESET(obs);
+  int autoreset = 0;
+  for (int t = 0; t < T; ++t) {
+    float* o = obs + (size_t)(t + 1) * O;
+    if (t == reset_at || autoreset) {
+      WRAP_RESET(o);
+      reward[t] = 0.0f; term[t] = 0.0f; trunc[t] = 0.0f; info_ret[t] = 0.0f; info_len[t] = 0.0f;
+      autoreset = 0;
+      continue;
+    }
+    script_obs(&w, x);
+    const float r = -1.0f + 5.0f * stream_u01(31, (uint32_t)w.c);
+    const int te = (w.c % 29) == 28, tr = (w.c % 61) == 60;
+    w.c++;
+    w.ep_ret += r;
+    w.ep_len += 1;
+    info_ret[t] = (te || tr) ? w.ep_ret : 0.0f;
+    info_len[t] = (te || tr) ? (float)w.ep_len : 0.0f;
+    wrap_obs(&w, x, o);
+    w.racc = w.racc * gamma * (1.0f - (float)te) + r;
+    {
+      const float batch_count = 1.0f;
+      const float delta = w.racc - w.rmean;
+      const float tot_count = w.rcount + batch_count;
+      const float new_mean = w.rmean + delta * batch_count / tot_count;
+      const float m_a = w.rvar * w.rcount;
+      const float m_b = 0.0f * batch_count;
+      const float M2 = m_a + m_b + (delta * delta) * w.rcount * batch_count / tot_count;
+      w.rcount = tot_count;
+      w.rmean = new_mean;
+      w.rvar = M2 / tot_count;
+    }
+    const float rn = r / sqrtf(w.rvar + 1e-8f);
+    reward[t] = rn < -10.0f ? -10.0f : (rn > 10.0f ? 10.0f : rn);
+    term[t] = (float)te;
+    trunc[t] = (float)tr;
+    autoreset = te || tr;
+  }
+#undef WRAP_RESET
+  memcpy(obs_mean, w.om, sizeof(float) * O);
+  memcpy(obs_var, w.ov, sizeof(float) * O);
+  free(w.om); free(w.ov); free(x);
+}

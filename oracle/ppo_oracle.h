@@ -101,6 +101,18 @@ void orc_env_step(orc_env_state* s, const float* actions, float act_lo, float ac
                   float* obs_out, float* reward, float* term, float* trunc,
                   float* info_ret, int* info_len);
 
+/* ---- PPO env wrapper chain (a20): ppo:41-49 make_env over a scripted single env ----
+ * RecordEpisodeStatistics (common.h:11-66) -> NormalizeObservation kFloat32 (stateful_observation.h:
+ * 56-84: Welford with batch_count 1, update BEFORE normalising, also on reset) -> clamp +-10 ->
+ * NormalizeReward (stateful_reward.h:55-91: discounted-return variance) -> clamp +-10, driven with
+ * SeqVectorEnv's next-step autoreset (gym.h:141-159) and a plain reset(3) at step reset_at.
+ * Scripted env, call c (reset or step): obs[i] = (i - 2) + 5 u(30, c*O + i); step reward
+ * -1 + 5 u(31, c); termination c % 29 == 28; truncation c % 61 == 60 (u = orc_u01 of the
+ * murmur3 hash stream of tests/carla_inputs.py). Writes obs [T+1][O] (row 0 = the first reset)
+ * and reward / term / trunc / info_ret / info_len [T]; mean/var of the final obs statistics. */
+void orc_wrappers_run(int O, int T, int reset_at, float gamma, float* obs, float* reward, float* term, float* trunc,
+                      float* info_ret, float* info_len, float* obs_mean, float* obs_var);
+
 /* ---- CaRL CNN agent (a23): AgentImpl::forward, include/carla/carla_model.h:222-318 ----
  * bev uint8 [n, C, IH, IW]; meas [n, NM]; vmeas [n, NV]; mode = PPO_CARLA_* (ppo_carla.h).
  * Convolutions and Linear layers accumulate in double. Outputs may be NULL; features [n, 256]. */

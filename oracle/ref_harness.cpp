@@ -17,7 +17,9 @@
 #include <rl_utils.h>
 #include <torch/torch.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <cstdio>
 #include <cstdlib>
 #include <filesystem>
@@ -404,6 +406,369 @@ static int bench_main(int E, int T, int MB, int EP, int n_act) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Round-2 cases: the agents at the widths the reference builds (AC 2x256 LayerNorm trunks,
+// ac:159-186, at HalfCheetah O=17/A=6 and Ant O=105/A=8; the PPO 2x64 tanh agent at Humanoid
+// O=376/A=17, ppo:122-139), GAE at cfg2's T=2048 and at ragged T, and the PPO env wrapper chain.
+// Parameters are drawn from hash streams (tests/golden_inputs.py restates the draw), so only the
+// inputs and outputs are stored.
+// ---------------------------------------------------------------------------------------------
+// tensor t of named_parameters() from stream base + t: 2-D weights U(+-sqrt(3 / fan_in)), LayerNorm
+// gamma U(0.8, 1.2), biases / LayerNorm beta U(+-0.1), mean_ U(+-0.1), std_ U(0.8, 1.5),
+// actor_logstd U(-0.7, -0.3), action_space_high / low = hi / lo
+static Tensor hash_params(nn::Module& m, uint32_t base, float hi, float lo, std::string& names_json) {
+  torch::NoGradGuard ng;
+  std::vector<Tensor> flat;
+  names_json = "[";
+  uint32_t t = 0;
+  for (auto& kv : m.named_parameters()) {
+    Tensor p = kv.value();
+    const std::string& n = kv.key();
+    const uint32_t s = base + t;
+    const std::vector<int64_t> shape = p.sizes().vec();
+    Tensor v;
+    if (n == "action_space_high") v = torch::tensor(hi);
+    else if (n == "action_space_low") v = torch::tensor(lo);
+    else if (n == "mean_") v = hunif(s, shape, -0.1f, 0.1f);
+    else if (n == "std_") v = hunif(s, shape, 0.8f, 1.5f);
+    else if (n == "actor_logstd") v = hunif(s, shape, -0.7f, -0.3f);
+    else if (n.find("weight") != std::string::npos && p.dim() == 1) v = hunif(s, shape, 0.8f, 1.2f);
+    else if (n.find("weight") != std::string::npos) {
+      const float a = std::sqrt(3.0f / (float)p.size(1));
+      v = hunif(s, shape, -a, a);
+    } else v = hunif(s, shape, -0.1f, 0.1f);
+    p.copy_(v.reshape(p.sizes()));
+    flat.push_back(p.detach().reshape({-1}).clone());
+    names_json += std::string(t ? ", " : "") + "[\"" + n + "\", " + std::to_string(p.numel()) + ", " +
+                  (p.requires_grad() ? "1" : "0") + "]";
+    ++t;
+  }
+  names_json += "]";
+  return torch::cat(flat);
+}
+
+// GAE exactly as ppo:447-467 / ac:759-779 (LibTorch ops, float32)
+static std::pair<Tensor, Tensor> gae_ref(const Tensor& rewards, const Tensor& values, const Tensor& dones,
+                                         const Tensor& next_value, const Tensor& next_done, float gamma,
+                                         float gae_lambda) {
+  torch::NoGradGuard ng;
+  const int64_t T = rewards.size(0), E = rewards.size(1);
+  Tensor advantages = torch::zeros({T, E});
+  Tensor lastgaelam = torch::zeros({E});
+  Tensor nextnonterminal, nextvalues;
+  for (int64_t t = T - 1; t >= 0; --t) {
+    if (t == T - 1) { nextnonterminal = 1.0f - next_done; nextvalues = next_value; }
+    else { nextnonterminal = 1.0 - dones.index({t + 1}); nextvalues = values.index({t + 1}); }
+    Tensor delta = rewards.index({t}) + gamma * nextvalues * nextnonterminal - values.index({t});
+    advantages.index({t}) = delta + gamma * gae_lambda * nextnonterminal * lastgaelam;
+    lastgaelam = advantages.index({t});
+  }
+  return {advantages, advantages + values};
+}
+
+// FNV-1a 64 over the float32 bit patterns of column e, rows t = 0 .. T-1 (bit-exact check of a
+// [T, E] array without storing it; tests/golden_inputs.py computes the same)
+static Tensor column_fnv(const Tensor& a) {
+  Tensor c = a.contiguous();
+  const int64_t T = c.size(0), E = c.size(1);
+  const float* p = c.data_ptr<float>();
+  Tensor out = torch::empty({E}, torch::kInt64);
+  int64_t* o = out.data_ptr<int64_t>();
+  for (int64_t e = 0; e < E; ++e) {
+    uint64_t h = 14695981039346656037ull;
+    for (int64_t t = 0; t < T; ++t) {
+      uint32_t b;
+      std::memcpy(&b, p + t * E + e, 4);
+      h ^= b;
+      h *= 1099511628211ull;
+    }
+    o[e] = (int64_t)h;
+  }
+  return out;
+}
+
+static std::string f2s(float v) {
+  std::ostringstream s;
+  s.precision(9);
+  s << v;
+  return s.str();
+}
+
+static void ppo_width_case(const std::string& pre, int O, int A, int H, int M, uint32_t base) {
+  PPOAgent agent(O, A, H);
+  std::string names;
+  Tensor p0 = hash_params(*agent, base, 1.0f, -1.0f, names);
+  Tensor x = randn({M, O});
+  Tensor act = randn({M, A}, 0.5f);
+  const std::string dims = "\"kind\": 0, \"O\": " + std::to_string(O) + ", \"A\": " + std::to_string(A) +
+                           ", \"H\": " + std::to_string(H) + ", \"hash_base\": " + std::to_string(base);
+  const std::string ca = pre + "_act";
+  begin_case(ca, "{" + dims + ", \"n\": " + std::to_string(M) + ", \"params\": " + names + "}");
+  {
+    torch::NoGradGuard ng;
+    auto [a, lp, ent, v, mu] = agent->get_action_and_value(x, act);
+    dump(ca, "x", x); dump(ca, "action", act);
+    dump(ca, "logprob", lp); dump(ca, "entropy", ent); dump(ca, "value", v.view(-1)); dump(ca, "mean", mu);
+  }
+  end_case();
+  const LossCfg c{0.2f, 0.01f, 0.5f, true, true};
+  Tensor old_logp, old_v, adv = randn({M}), ret = randn({M});
+  {
+    torch::NoGradGuard ng;
+    auto [a, lp, ent, v, mu] = agent->get_action_and_value(x, act);
+    old_logp = lp + randn({M}, 0.15f);
+    old_v = v.view(-1) + randn({M}, 0.15f);
+  }
+  torch::optim::Adam opt(agent->parameters(), torch::optim::AdamOptions(3e-4).eps(1e-5));
+  const std::string cu = pre + "_update";
+  begin_case(cu, "{" + dims + ", \"M\": " + std::to_string(M) +
+                     ", \"clip_coef\": 0.2, \"ent_coef\": 0.01, \"vf_coef\": 0.5, \"clip_vloss\": 1, \"norm_adv\": 1, "
+                     "\"max_grad_norm\": 0.5, \"lr\": 0.0003, \"adam_eps\": 1e-05}");
+  dump(cu, "x", x); dump(cu, "action", act); dump(cu, "old_logp", old_logp); dump(cu, "adv", adv);
+  dump(cu, "ret", ret); dump(cu, "old_v", old_v);
+  for (int s = 1; s <= 3; ++s) {  // ppo:497-540, Tensor::std() advantage normalisation
+    auto [a, lp, ent, v, mu] = agent->get_action_and_value(x, act);
+    auto [loss, st] = ppo_loss(lp, ent, v, old_logp, adv, ret, old_v, c, nullptr, nullptr);
+    opt.zero_grad();
+    loss.backward();
+    if (s == 1) { dump(cu, "grad_raw", flat_grads(*agent)); dump(cu, "stats", torch::tensor(st)); }
+    const double tn = torch::nn::utils::clip_grad_norm_(agent->parameters(), 0.5);
+    if (s == 1) dump(cu, "total_norm", torch::tensor({(float)tn}));
+    opt.step();
+    if (s == 1) dump(cu, "params_step1", flat_params(*agent));
+  }
+  dump(cu, "params_step3", flat_params(*agent));
+  end_case();
+}
+
+static void ac_width_case(const std::string& pre, int O, int A, int H, int M, uint32_t base, float hi, float lo) {
+  ACAgent agent(O, A, H, hi, lo, torch::zeros({O}), torch::ones({O}));
+  std::string names;
+  Tensor p0 = hash_params(*agent, base, hi, lo, names);
+  Tensor x = randn({M, O});
+  Tensor act = lo + (hi - lo) * randu({M, A}, 0.01f, 0.99f);
+  const std::string dims = "\"kind\": 1, \"O\": " + std::to_string(O) + ", \"A\": " + std::to_string(A) +
+                           ", \"H\": " + std::to_string(H) + ", \"hi\": " + f2s(hi) + ", \"lo\": " + f2s(lo) +
+                           ", \"hash_base\": " + std::to_string(base);
+  const std::string ca = pre + "_act";
+  begin_case(ca, "{" + dims + ", \"n\": " + std::to_string(M) + ", \"params\": " + names + "}");
+  {
+    torch::NoGradGuard ng;
+    auto [a, lp, ent, v, al, be] = agent->get_action_and_value(x, act, "given");
+    dump(ca, "x", x); dump(ca, "action", act);
+    dump(ca, "logprob", lp); dump(ca, "entropy", ent); dump(ca, "value", v.view(-1));
+    dump(ca, "alpha", al); dump(ca, "beta", be); dump(ca, "action_roundtrip", a);
+    auto [am, lpm, entm, vm, alm, bem] = agent->get_action_and_value(x, Tensor(), "mean");
+    dump(ca, "mean_action", am); dump(ca, "mean_logprob", lpm);
+  }
+  end_case();
+  const LossCfg c{0.1f, 0.01f, 0.5f, true, true};
+  Tensor old_logp, old_v, adv = randn({M}), ret = randn({M});
+  {
+    torch::NoGradGuard ng;
+    auto [a, lp, ent, v, al, be] = agent->get_action_and_value(x, act, "given");
+    old_logp = lp + randn({M}, 0.1f);
+    old_v = v.view(-1) + randn({M}, 0.1f);
+  }
+  torch::optim::Adam opt(agent->parameters(), torch::optim::AdamOptions(2.5e-4).eps(1e-5));
+  const std::string cu = pre + "_update";
+  begin_case(cu, "{" + dims + ", \"M\": " + std::to_string(M) +
+                     ", \"clip_coef\": 0.1, \"ent_coef\": 0.01, \"vf_coef\": 0.5, \"clip_vloss\": 1, \"norm_adv\": 1, "
+                     "\"max_grad_norm\": 0.5, \"lr\": 0.00025, \"adam_eps\": 1e-05}");
+  dump(cu, "x", x); dump(cu, "action", act); dump(cu, "old_logp", old_logp); dump(cu, "adv", adv);
+  dump(cu, "ret", ret); dump(cu, "old_v", old_v);
+  // the AC trainer's advantage statistics (ac:830-849) over G row shards
+  auto dist_stats = [&](int G) {
+    const int64_t Md = M / G;
+    Tensor amean = torch::zeros({});
+    for (int r = 0; r < G; ++r) amean = amean + adv.slice(0, r * Md, (r + 1) * Md).mean();
+    amean = amean / (float)G;  // ncclAvg
+    Tensor ssum = torch::zeros({});
+    for (int r = 0; r < G; ++r) ssum = ssum + torch::sum(torch::square(adv.slice(0, r * Md, (r + 1) * Md) - amean));
+    Tensor astd = torch::sqrt(ssum / static_cast<float>(G * Md - 1));
+    return std::make_pair(amean, astd);
+  };
+  {  // G = 2: per-rank losses with the distributed statistics, gradients averaged (ac:877-885)
+    auto [amean, astd] = dist_stats(2);
+    const int64_t Md = M / 2;
+    Tensor gsum;
+    for (int r = 0; r < 2; ++r) {
+      auto sl = [&](const Tensor& t) { return t.slice(0, r * Md, (r + 1) * Md); };
+      auto [a, lp, ent, v, al, be] = agent->get_action_and_value(sl(x), sl(act), "given");
+      auto [loss, st] = ppo_loss(lp, ent, v, sl(old_logp), sl(adv), sl(ret), sl(old_v), c, &amean, &astd);
+      opt.zero_grad();
+      loss.backward();
+      Tensor g = flat_grads(*agent);
+      gsum = gsum.defined() ? gsum + g : g;
+    }
+    dump(cu, "grad_dist2_avg", gsum / 2.0f);
+    dump(cu, "dist2_adv_stats", torch::stack({amean, astd}));
+  }
+  auto [amean1, astd1] = dist_stats(1);
+  for (int s = 1; s <= 3; ++s) {  // world_size = 1 form of ac:830-888
+    auto [a, lp, ent, v, al, be] = agent->get_action_and_value(x, act, "given");
+    auto [loss, st] = ppo_loss(lp, ent, v, old_logp, adv, ret, old_v, c, &amean1, &astd1);
+    opt.zero_grad();
+    loss.backward();
+    if (s == 1) { dump(cu, "grad_raw", flat_grads(*agent)); dump(cu, "stats", torch::tensor(st)); }
+    const double tn = torch::nn::utils::clip_grad_norm_(agent->parameters(), 0.5);
+    if (s == 1) dump(cu, "total_norm", torch::tensor({(float)tn}));
+    opt.step();
+    if (s == 1) dump(cu, "params_step1", flat_params(*agent));
+  }
+  dump(cu, "params_step3", flat_params(*agent));
+  end_case();
+}
+
+// The PPO env wrapper chain of ppo:41-49 (RecordEpisodeStatistics -> NormalizeObservation(kFloat32)
+// -> TransformObservation(clamp +-10) -> NormalizeReward(gamma) -> TransformReward(clamp +-10)),
+// replayed with the LibTorch calls of stateful_observation.h:56-84 / stateful_reward.h:55-91 over a
+// scripted env (the reference headers include gym.h, which needs boost, absent here).
+// Scripted env: call c (reset or step) returns obs[i] = U(stream 30, c*O + i) on [i - 2, i + 3),
+// step reward U(stream 31, c) on [-1, 4), termination when c % 29 == 28, truncation when c % 61 == 60.
+struct WrapChain {
+  int O;
+  int c = 0;
+  float ep_ret = 0.0f;
+  int ep_len = 0;
+  Tensor om, ov;         // NormalizeObservation mean_ / var_ (kFloat32)
+  float ocount = 1e-4f;  // count_ = epsilon
+  const float oeps = 1e-4f;
+  float rmean = 0.0f, rvar = 1.0f, racc = 0.0f, rcount = 1e-8f;
+  const float reps = 1e-8f, gamma = 0.99f;
+  explicit WrapChain(int O_) : O(O_) { om = torch::zeros({O}, torch::kFloat32); ov = torch::ones({O}, torch::kFloat32); }
+  Tensor raw_obs() {
+    Tensor o = torch::empty({O}, torch::kFloat32);
+    float* p = o.data_ptr<float>();
+    for (int i = 0; i < O; ++i) {
+      const float lo = (float)i - 2.0f, hi = (float)i + 3.0f;
+      p[i] = lo + (hi - lo) * hu01(30, (uint32_t)(c * O + i));
+    }
+    return o;
+  }
+  Tensor obs_wrappers(const Tensor& x) {  // NormalizeObservation::observation + clamp
+    torch::NoGradGuard ng;
+    {
+      const Tensor batch_mean = x;
+      const Tensor batch_var = torch::zeros_like(x);
+      constexpr float batch_count = 1.0f;
+      const Tensor delta = x - om;
+      const float tot_count = ocount + batch_count;
+      const Tensor new_mean = om + delta * batch_count / tot_count;
+      const Tensor m_a = ov * ocount;
+      const Tensor m_b = batch_var * batch_count;
+      const Tensor M2 = m_a + m_b + (delta * delta) * ocount * batch_count / tot_count;
+      const Tensor new_var = M2 / tot_count;
+      ocount = tot_count;
+      om = new_mean;
+      ov = new_var;
+      (void)batch_mean;
+    }
+    Tensor y = (x - om) / torch::sqrt(ov + oeps);
+    return torch::clamp(y, -10.0f, 10.0f);
+  }
+  Tensor reset() {
+    Tensor o = raw_obs();
+    ++c;
+    ep_ret = 0.0f;
+    ep_len = 0;
+    return obs_wrappers(o);
+  }
+  // -> obs, reward, term, trunc, info_ret, info_len
+  std::tuple<Tensor, float, bool, bool, float, int> step() {
+    Tensor o = raw_obs();
+    const float r = -1.0f + 5.0f * hu01(31, (uint32_t)c);
+    const bool te = (c % 29) == 28, tr = (c % 61) == 60;
+    ++c;
+    ep_ret += r;
+    ep_len += 1;
+    float ir = 0.0f;
+    int il = 0;
+    if (te || tr) { ir = ep_ret; il = ep_len; }
+    Tensor oo = obs_wrappers(o);
+    racc = racc * gamma * (1.0f - static_cast<float>(te)) + r;
+    {
+      constexpr float batch_var = 0.0f;
+      constexpr float batch_count = 1.0f;
+      const float delta = racc - rmean;
+      const float tot_count = rcount + batch_count;
+      const float new_mean = rmean + delta * batch_count / tot_count;
+      const float m_a = rvar * rcount;
+      constexpr float m_b = batch_var * batch_count;
+      const float M2 = m_a + m_b + (delta * delta) * rcount * batch_count / tot_count;
+      rcount = tot_count;
+      rmean = new_mean;
+      rvar = M2 / tot_count;
+    }
+    const float rn = std::clamp(r / std::sqrt(rvar + reps), -10.0f, 10.0f);
+    return {oo, rn, te, tr, ir, il};
+  }
+};
+
+static void width_cases() {
+  ac_width_case("ac256", 17, 6, 256, 256, 3000, 1.0f, -1.0f);
+  ac_width_case("ant256", 105, 8, 256, 256, 3100, 1.0f, -1.0f);
+  ppo_width_case("hum376", 376, 17, 64, 256, 3200);
+
+  {  // GAE at cfg2's T = 2048 (E = 1024): inputs from hash streams 11-15, outputs as column hashes
+    const int T = 2048, E = 1024;
+    Tensor rewards = hunif(11, {T, E}, -1.0f, 1.0f), values = hunif(12, {T, E}, -1.0f, 1.0f);
+    Tensor dones = (hunif(13, {T, E}, 0.0f, 1.0f) < 0.002f).to(torch::kFloat32);
+    dones.index_put_({0}, 1.0f);
+    dones.index_put_({T - 1, torch::indexing::Slice(0, E / 2)}, 1.0f);
+    Tensor next_value = hunif(14, {E}, -1.0f, 1.0f);
+    Tensor next_done = (hunif(15, {E}, 0.0f, 1.0f) < 0.5f).to(torch::kFloat32);
+    auto [adv, ret] = gae_ref(rewards, values, dones, next_value, next_done, 0.99f, 0.95f);
+    begin_case("gae_long", "{\"T\": 2048, \"E\": 1024, \"gamma\": 0.99, \"gae_lambda\": 0.95, \"streams\": "
+                           "[11, 12, 13, 14, 15], \"done_p\": 0.002}");
+    dump("gae_long", "adv_fnv", column_fnv(adv)); dump("gae_long", "ret_fnv", column_fnv(ret));
+    dump("gae_long", "adv_cols8", adv.slice(1, 0, 8)); dump("gae_long", "ret_cols8", ret.slice(1, 0, 8));
+    end_case();
+  }
+  for (int T : {1, 7, 33}) {  // ragged T (k_gae loads 32-step chunks), E = 37
+    const int E = 37;
+    Tensor rewards = randn({T, E}), values = randn({T, E});
+    Tensor dones = (randu({T, E}, 0.0f, 1.0f) < 0.1f).to(torch::kFloat32);
+    Tensor next_value = randn({E});
+    Tensor next_done = (randu({E}, 0.0f, 1.0f) < 0.5f).to(torch::kFloat32);
+    auto [adv, ret] = gae_ref(rewards, values, dones, next_value, next_done, 0.99f, 0.95f);
+    const std::string cn = "gae_t" + std::to_string(T);
+    begin_case(cn, "{\"T\": " + std::to_string(T) + ", \"E\": 37, \"gamma\": 0.99, \"gae_lambda\": 0.95}");
+    dump(cn, "rewards", rewards); dump(cn, "values", values); dump(cn, "dones", dones);
+    dump(cn, "next_value", next_value); dump(cn, "next_done", next_done);
+    dump(cn, "advantages", adv); dump(cn, "returns", ret);
+    end_case();
+  }
+  {  // wrapper chain over the scripted env, one env with next-step autoreset (gym.h:141-159) and a
+     // plain reset(3) at t = 120
+    const int O = 5, T = 200;
+    WrapChain w(O);
+    std::vector<float> obs, rew, te, tr, ir, il;
+    auto put = [&](const Tensor& o) { for (int i = 0; i < O; ++i) obs.push_back(o.data_ptr<float>()[i]); };
+    put(w.reset());
+    bool autoreset = false;
+    for (int t = 0; t < T; ++t) {
+      if (t == 120) { put(w.reset()); rew.push_back(0.0f); te.push_back(0); tr.push_back(0); ir.push_back(0); il.push_back(0); autoreset = false; continue; }
+      if (autoreset) {
+        put(w.reset());
+        rew.push_back(0.0f); te.push_back(0); tr.push_back(0); ir.push_back(0); il.push_back(0);
+        autoreset = false;
+        continue;
+      }
+      auto [o, r, a, b, iret, ilen] = w.step();
+      put(o); rew.push_back(r); te.push_back(a); tr.push_back(b); ir.push_back(iret); il.push_back((float)ilen);
+      autoreset = a || b;
+    }
+    begin_case("wrappers", "{\"O\": 5, \"T\": 200, \"gamma\": 0.99, \"reset_at\": 120, \"obs_stream\": 30, "
+                           "\"reward_stream\": 31, \"term_mod\": 29, \"trunc_mod\": 61}");
+    dump("wrappers", "obs", torch::tensor(obs).view({T + 1, O})); dump("wrappers", "reward", torch::tensor(rew));
+    dump("wrappers", "term", torch::tensor(te)); dump("wrappers", "trunc", torch::tensor(tr));
+    dump("wrappers", "info_ret", torch::tensor(ir)); dump("wrappers", "info_len", torch::tensor(il));
+    dump("wrappers", "obs_mean_final", w.om); dump("wrappers", "obs_var_final", w.ov);
+    end_case();
+  }
+}
+
 int main(int argc, char** argv) {
   torch::set_num_threads(1);
   if (argc > 1 && std::string(argv[1]) == "--bench") {
@@ -776,6 +1141,9 @@ int main(int argc, char** argv) {
       });
     }
   }
+
+  // ---- round 2: the reference's real widths, long / ragged GAE, the PPO env wrappers ----------
+  width_cases();
 
   g_manifest << "\n}\n";
   std::ofstream(g_out + "/manifest.json") << g_manifest.str();

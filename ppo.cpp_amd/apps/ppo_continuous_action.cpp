@@ -47,18 +47,6 @@ struct GlobalConfig {  // ppo_continuous_action.cpp:51-118
   }
 };
 
-static std::shared_ptr<gymcpp::EnvironmentWrapper> make_env(const std::shared_ptr<gymcpp::Environment>& env_0,
-                                                            float gamma) {  // ppo:41-49
-  auto env_1 = std::make_shared<gymcpp::RecordEpisodeStatistics>(env_0);
-  auto env_2 = std::make_shared<gymcpp::NormalizeObservation>(env_1, env_1->get_observation_space());
-  auto env_3 = std::make_shared<gymcpp::TransformObservation>(env_2, [](float* x, int n) {
-    for (int i = 0; i < n; ++i) x[i] = std::clamp(x[i], -10.0f, 10.0f);
-  });
-  auto env_4 = std::make_shared<gymcpp::NormalizeReward>(env_3, gamma);
-  auto env_5 = std::make_shared<gymcpp::TransformReward>(env_4, [](float x) { return std::clamp(x, -10.0f, 10.0f); });
-  return env_5;
-}
-
 int main(int argc, const char** argv) {
   std::ios_base::sync_with_stdio(false);
   GlobalConfig config;
@@ -111,7 +99,7 @@ int main(int argc, const char** argv) {
 
   std::vector<std::shared_ptr<gymcpp::EnvironmentWrapper>> env_array;
   try {
-    for (int i = 0; i < config.num_envs; ++i) env_array.push_back(make_env(make_base_env(config.env_id), config.gamma));
+    for (int i = 0; i < config.num_envs; ++i) env_array.push_back(gymcpp::make_env(make_base_env(config.env_id), config.gamma));
   } catch (const std::invalid_argument& e) {
     std::cerr << e.what() << std::endl;
     return 1;

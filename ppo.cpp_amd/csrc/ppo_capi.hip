@@ -90,7 +90,12 @@ struct ppo_ctx {
   long adam_step = 0;
   long iteration = 0;
   ncclComm_t comm = nullptr;
-  int world = 1, rank = 0;
+  ppo_host_allreduce_fn host_ar = nullptr;  // host transport (ppo_comm_init_host)
+  void* host_user = nullptr;
+  std::vector<float> host_stage;
+  int world = 1, rank = 0;  // data-parallel group of the attached communicator (1 / cfg.rank without one)
+  int upd_trunk_mask = 3, upd_sched = 1;   // k_upd launch options (PPO_UPD_TRUNK: PPO_DIAG builds only)
+  int dw_fused = 1;
   // profiling
   unsigned prof_mask = 0;
   std::mutex prof_mu;
@@ -146,6 +151,7 @@ static void prof_drain(ppo_t* c) {
 }
 
 static hipStream_t S(ppo_t* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+static void comm_detach(ppo_t* c);
 
 // ------------------------------------------------------------------------------------------
 // create / destroy
@@ -194,7 +200,17 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   c->nmb = cfg->num_minibatches;
   c->M = (int)(B / cfg->num_minibatches);
   c->rank = cfg->rank;
-  c->world = cfg->world_size > 0 ? cfg->world_size : 1;
+  c->world = 1;  // statistics and collectives span the communicator attached later (ppo_comm_init*)
+  {  // kernel selection, read once (A/B switches of complete kernels; never read on a launch path)
+    const char* es = getenv("PPO_UPD_SCHED");
+    if (es && es[0] >= '0' && es[0] <= '3') c->upd_sched = es[0] - '0';
+    const char* ed = getenv("PPO_DW_FUSED");
+    c->dw_fused = !(ed && ed[0] == '0');
+#ifdef PPO_DIAG
+    const char* et = getenv("PPO_UPD_TRUNK");
+    if (et && (et[0] == '0' || et[0] == '1')) c->upd_trunk_mask = 1 << (et[0] - '0');
+#endif
+  }
   const int H = cfg->hidden, A = cfg->act_dim, O = cfg->obs_dim, OP = c->K.OP;
   c->sg[0] = make_sg(H, 1, A);
   c->sg[1] = make_sg(H, cfg->net_kind == PPO_NET_LN_BETA ? 2 * A : A, A);
@@ -279,7 +295,7 @@ extern "C" int ppo_destroy(ppo_t* c) {
     if (c->dwslab[k]) (void)hipFree(c->dwslab[k]);
   if (c->perms) (void)hipFree(c->perms);
   if (c->advpart) (void)hipFree(c->advpart);
-  if (c->comm) (void)ncclCommDestroy(c->comm);
+  comm_detach(c);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -486,10 +502,26 @@ static int gae_launch(ppo_t* c, const float* next_value, const float* next_done,
 // ------------------------------------------------------------------------------------------
 // update
 // ------------------------------------------------------------------------------------------
+static bool distributed(const ppo_t* c) { return c->comm != nullptr || c->host_ar != nullptr; }
+
+// In-place all-reduce over the attached communicator (no communicator: identity). RCCL runs on the
+// context stream; the host transport synchronises the stream, hands the values to the caller's
+// function in host memory and copies the result back.
 static int allreduce(ppo_t* c, float* buf, long n, int average, hipStream_t s) {
-  if (!c->comm || c->world <= 1) return 0;
-  ProfScope ps(c, PK_ALLREDUCE, s);
-  NCCL_TRY(ncclAllReduce(buf, buf, (size_t)n, ncclFloat, average ? ncclAvg : ncclSum, c->comm, s));
+  if (c->comm) {
+    ProfScope ps(c, PK_ALLREDUCE, s);
+    NCCL_TRY(ncclAllReduce(buf, buf, (size_t)n, ncclFloat, average ? ncclAvg : ncclSum, c->comm, s));
+    return 0;
+  }
+  if (c->host_ar) {
+    if ((long)c->host_stage.size() < n) c->host_stage.resize((size_t)n);
+    float* h = c->host_stage.data();
+    HIP_TRY(hipMemcpyAsync(h, buf, sizeof(float) * n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (c->host_ar(h, n, average, c->host_user) != 0) return fail("ppo host all-reduce callback failed", -3);
+    HIP_TRY(hipMemcpyAsync(buf, h, sizeof(float) * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));  // the staging buffer is reused by the next call
+  }
   return 0;
 }
 
@@ -500,6 +532,10 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   const ppo_hip_config& cfg = c->cfg;
   const int EP = cfg.update_epochs, MB = c->nmb, M = c->M, H = c->K.H, OP = c->K.OP, A = c->K.A;
   const long B = c->B;
+  const bool multi = distributed(c);
+  if (cfg.world_size > 1 && !multi)
+    return fail("ppo_update: world_size " + std::to_string(cfg.world_size) +
+                " but no communicator attached (ppo_comm_init / ppo_comm_init_host)");
   // ---- permutations (torch::randperm per epoch, ppo:490 / ac:804) ----
   const int32_t* perms = perms_dev;
   if (!perms) {
@@ -518,12 +554,11 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   aa.part = c->advpart;
   aa.M = M;
   aa.nmb = EP * MB;
-  aa.world = c->world;
+  aa.world = multi ? c->world : 1;
   if (cfg.norm_adv) {
     ProfScope ps(c, PK_ADV, s);
     launch_adv_sum(aa, s);
-    if (allreduce(c, c->advstats, 2L * EP * MB, 1, s)) return -3;
-    const bool multi = c->comm && c->world > 1;
+    if (multi && allreduce(c, c->advstats, 2L * EP * MB, 1, s)) return -3;
     launch_adv_sq(aa, multi ? 0 : 1, s);
     if (multi) {
       if (allreduce(c, c->advsq, (long)EP * MB, 0, s)) return -3;
@@ -558,6 +593,8 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   u.actn_off = c->upd.actn_off;
   u.acc_off = c->upd.acc_off;
   u.spar_off = c->upd.spar_off;
+  u.trunk_mask = c->upd_trunk_mask;
+  u.sched = c->upd_sched;
   const int nblk = c->use_upd ? c->upd_nblk : c->nblk;  // workgroups that wrote a slab row
   for (int k = 0; k < 2; ++k) {
     u.H1[k] = c->H1[k];
@@ -569,6 +606,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   memset(&dw, 0, sizeof(dw));
   dw.M = M;
   dw.rows_per_chunk = c->rows_per_chunk;
+  dw.fused = c->dw_fused;
   dw.xn = c->Xn;
   dw.slab_stride = (long)H * H + (long)H * OP;
   for (int k = 0; k < 2; ++k) {
@@ -675,7 +713,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
         ProfScope ps(c, PK_COLSUM, s);
         launch_colsum(cs, ns, maxlen, s);
       }
-      if (allreduce(c, c->G + tb, trainable_n, 1, s)) return -3;
+      if (multi && allreduce(c, c->G + tb, trainable_n, 1, s)) return -3;  // ac:877-885, before the clip
       {
         ProfScope ps(c, PK_GRADNORM, s);
         launch_gradnorm(na, s);
@@ -696,7 +734,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   c->iteration += 1;
   if (out) {
     std::vector<float> h((size_t)8 * EP * MB);
-    if (c->world > 1 && allreduce(c, c->mbstats, 8L * EP * MB, 1, s)) return -3;
+    if (multi && allreduce(c, c->mbstats, 8L * EP * MB, 1, s)) return -3;  // logging averages, ac:895-901
     HIP_TRY(hipMemcpyAsync(h.data(), c->mbstats, sizeof(float) * h.size(), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     const float* last = h.data() + 8 * (EP * MB - 1);
@@ -742,25 +780,60 @@ extern "C" int ppo_comm_unique_id(char id_out[PPO_COMM_ID_BYTES]) {
   return 0;
 }
 
+static void comm_detach(ppo_t* c) {
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  c->comm = nullptr;
+  c->host_ar = nullptr;
+  c->host_user = nullptr;
+  c->world = 1;
+}
+
+// A real RCCL communicator for every world size, world = 1 included: a one-rank group runs the
+// same distributed update sequence (advantage statistics, gradient and stats all-reduces) as a
+// multi-GPU job, which is how the single-GPU tests exercise it.
 extern "C" int ppo_comm_init(ppo_t* c, const char id[PPO_COMM_ID_BYTES], int rank, int world) {
   if (!c || !id) return fail("ppo_comm_init: null argument");
+  if (world < 1 || rank < 0 || rank >= world) return fail("ppo_comm_init: bad rank / world size");
   HIP_TRY(hipSetDevice(c->device));
   ncclUniqueId uid;
   memcpy(&uid, id, sizeof(uid));
-  if (c->comm) {
-    (void)ncclCommDestroy(c->comm);
-    c->comm = nullptr;
-  }
-  if (world > 1) NCCL_TRY(ncclCommInitRank(&c->comm, world, uid, rank));
+  comm_detach(c);
+  NCCL_TRY(ncclCommInitRank(&c->comm, world, uid, rank));
   c->rank = rank;
   c->world = world;
   return 0;
 }
 
+extern "C" int ppo_comm_init_host(ppo_t* c, int rank, int world, ppo_host_allreduce_fn fn, void* user) {
+  if (!c || !fn) return fail("ppo_comm_init_host: null argument");
+  if (world < 1 || rank < 0 || rank >= world) return fail("ppo_comm_init_host: bad rank / world size");
+  comm_detach(c);
+  c->host_ar = fn;
+  c->host_user = user;
+  c->rank = rank;
+  c->world = world;
+  return 0;
+}
+
+extern "C" int ppo_comm_destroy(ppo_t* c) {
+  if (!c) return fail("null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  comm_detach(c);
+  return 0;
+}
+
 extern "C" int ppo_comm_broadcast_params(ppo_t* c, int root) {
   if (!c) return fail("null ctx");
-  if (!c->comm || c->world <= 1) return 0;
-  NCCL_TRY(ncclBroadcast(c->P, c->P, (size_t)c->K.size, ncclFloat, root, c->comm, c->stream));
+  if (!distributed(c)) return 0;
+  if (root < 0 || root >= c->world) return fail("ppo_comm_broadcast_params: bad root");
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->comm) {
+    NCCL_TRY(ncclBroadcast(c->P, c->P, (size_t)c->K.size, ncclFloat, root, c->comm, c->stream));
+  } else {  // host transport: sum with zeros from every rank but the root (x + 0 == x exactly)
+    if (c->rank != root) HIP_TRY(hipMemsetAsync(c->P, 0, sizeof(float) * c->K.size, c->stream));
+    if (allreduce(c, c->P, (long)c->K.size, 0, c->stream)) return -3;
+  }
   if (refresh_w2t(c)) return -2;
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;

@@ -1529,14 +1529,8 @@ static int launch_dwf_t(const DwArgs& a, int nchunks, hipStream_t s) {
   return 0;
 }
 
-// "PPO_DW_FUSED=0" forces the two-phase k_dw where k_dwf applies (tests compare the two)
-static bool dw_fused_enabled() {
-  const char* ev = getenv("PPO_DW_FUSED");
-  return !(ev && ev[0] == '0');
-}
-
 int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s) {
-  if (H == 256 && dw_fused_enabled()) {
+  if (H == 256 && a.fused) {  // a.fused = 0: the two-phase k_dw (PPO_DW_FUSED=0 at ppo_create)
     if (OP == 16) return launch_dwf_t<256, 16>(a, nchunks, s);
     if (OP == 32) return launch_dwf_t<256, 32>(a, nchunks, s);
   }

@@ -53,7 +53,7 @@ struct UpdArgs {
   float* DZ2[2];
   float* slab[2];
   int actn_off, acc_off, spar_off;  // k_upd: runtime LDS offsets (floats)
-  int trunk_mask;         // k_upd: trunks to run (bit t = trunk t; 3 = both)
+  int trunk_mask;         // k_upd: trunks to run (bit t = trunk t; 3 = both; other values: PPO_DIAG builds only)
   int sched;              // k_upd: bit 0 actor workgroups dispatched first, bit 1 actor wave priority
 };
 
@@ -73,6 +73,7 @@ struct DwArgs {
   long slab_stride;
   int M;
   int rows_per_chunk;
+  int fused;          // 1: k_dwf (dW2 and dW1 in one pass) where it applies; 0: two-phase k_dw
 };
 
 struct ColsumSeg {

@@ -994,14 +994,12 @@ int upd_supported(const PackedLayout& K, int nh_actor, int sg_size, UpdGeoOut* g
 }
 
 int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s) {
-  // diagnostic only: "PPO_UPD_TRUNK=0|1" runs that one trunk (the other trunk's gradient is left
-  // stale) to time the two trunks apart
-  const char* ev = getenv("PPO_UPD_TRUNK");
+  // trunk_mask / sched come from the context (ppo_create); a trunk mask other than 3 exists only in
+  // the diagnostic build (PPO_DIAG), where it times the two trunks apart
   UpdArgs b = a;
-  b.trunk_mask = (ev && (ev[0] == '0' || ev[0] == '1')) ? 1 << (ev[0] - '0') : 3;
-  // schedule bits (UpdArgs::sched); PPO_UPD_SCHED=<0..3> for A/B
-  const char* es = getenv("PPO_UPD_SCHED");
-  b.sched = (es && es[0] >= '0' && es[0] <= '3') ? es[0] - '0' : 1;
+#ifndef PPO_DIAG
+  b.trunk_mask = 3;
+#endif
   const dim3 grid(nblocks, 2);
   return dispatch_upd(a.K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_, auto KL_) {
     hipLaunchKernelGGL((k_upd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value,

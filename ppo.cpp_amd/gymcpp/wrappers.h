@@ -7,6 +7,7 @@
 //   TransformReward          libs/gymcpp/wrappers/vectorize_reward.h
 #pragma once
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <functional>
@@ -172,5 +173,18 @@ class TransformReward final : public EnvironmentWrapper {
   float get_action_space_min() const override { return env_->get_action_space_min(); }
   float get_action_space_max() const override { return env_->get_action_space_max(); }
 };
+
+// The PPO trainer's wrapper chain (ppo_continuous_action.cpp:41-49): episode statistics on the raw
+// env, running observation normalisation clamped to +-10, discounted-return reward scaling clamped
+// to +-10.
+inline std::shared_ptr<EnvironmentWrapper> make_env(const std::shared_ptr<Environment>& env_0, float gamma) {
+  auto env_1 = std::make_shared<RecordEpisodeStatistics>(env_0);
+  auto env_2 = std::make_shared<NormalizeObservation>(env_1, env_1->get_observation_space());
+  auto env_3 = std::make_shared<TransformObservation>(env_2, [](float* x, int n) {
+    for (int i = 0; i < n; ++i) x[i] = std::clamp(x[i], -10.0f, 10.0f);
+  });
+  auto env_4 = std::make_shared<NormalizeReward>(env_3, gamma);
+  return std::make_shared<TransformReward>(env_4, [](float x) { return std::clamp(x, -10.0f, 10.0f); });
+}
 
 }  // namespace gymcpp

@@ -46,6 +46,10 @@ class PPOError(RuntimeError):
     pass
 
 
+# int (*ppo_host_allreduce_fn)(float* host_buf, long n, int average, void* user)  (include/ppo_hip.h)
+HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_float), C.c_long, C.c_int, C.c_void_p)
+
+
 class HipConfig(C.Structure):
     _fields_ = [("net_kind", C.c_int), ("obs_dim", C.c_int), ("act_dim", C.c_int), ("hidden", C.c_int),
                 ("num_envs", C.c_int), ("num_steps", C.c_int), ("num_minibatches", C.c_int),
@@ -143,6 +147,8 @@ SYMBOLS = [
     ("ppo_buffer", _VP, [_VP, _I]),
     ("ppo_comm_unique_id", _I, [C.c_char_p]),
     ("ppo_comm_init", _I, [_VP, C.c_char_p, _I, _I]),
+    ("ppo_comm_init_host", _I, [_VP, _I, _I, C.c_void_p, _VP]),
+    ("ppo_comm_destroy", _I, [_VP]),
     ("ppo_comm_broadcast_params", _I, [_VP, _I]),
     ("ppo_comm_allreduce", _I, [_VP, _FP, _L, _I]),
     ("ppo_set_device", _I, [_I]),
@@ -544,6 +550,22 @@ class Agent:
 
     def comm_init(self, uid: bytes, rank, world):
         check(lib().ppo_comm_init(self.h, uid, rank, world))
+
+    def comm_init_host(self, rank, world, allreduce):
+        """Attach the host-transport communicator: allreduce(np.ndarray float32, average: bool)
+        reduces the array in place over all ranks (e.g. torch.distributed gloo, or MPI)."""
+        def _cb(buf, n, average, _user):
+            try:
+                allreduce(np.ctypeslib.as_array(buf, shape=(n,)), bool(average))
+                return 0
+            except Exception:  # noqa: BLE001 — reported to the library as a failed collective
+                return 1
+        self._host_cb = HOST_ALLREDUCE_FN(_cb)  # keep the trampoline alive while attached
+        check(lib().ppo_comm_init_host(self.h, rank, world, C.cast(self._host_cb, C.c_void_p), None))
+
+    def comm_destroy(self):
+        check(lib().ppo_comm_destroy(self.h))
+        self._host_cb = None
 
     def comm_broadcast_params(self, root=0):
         check(lib().ppo_comm_broadcast_params(self.h, root))

@@ -1,0 +1,134 @@
+"""GPU parity at the widths the reference builds, straight against the LibTorch-replay golden vectors
+(oracle/ref_harness.cpp width_cases()), through the C-ABI:
+
+  ac256   AC agent, 2x256 LayerNorm trunks + Beta heads (ac:150-249), HalfCheetah O=17 / A=6
+          -> k_act3 (act), k_upd<256, LN_BETA> + k_dwf (update)
+  ant256  the same agent at Ant-v5 O=105 / A=8 (cfg4)
+  hum376  PPO agent, 2x64 tanh + Normal (ppo:120-157), Humanoid-v4 O=376 / A=17 (cfg2)
+          -> k_act2<64, TANH> (act), k_fwdbwd<376> + k_dw (update)
+  gae_long / gae_t{1,7,33}  k_gae at cfg2's T=2048 (E=1024) and at ragged T (32-step load chunks)
+
+Tolerances (fp32; MFMA f32 chains vs LibTorch's CPU GEMMs, the same bars as test_gpu_parity.py):
+  log-probs / entropies / values     rtol 2e-5 .. 1e-4
+  raw gradient                        relative L2 < 2e-4 overall, < 2e-3 per tensor
+  parameters after 1 / 3 Adam steps   atol 2e-6 / 6e-6
+  GAE                                 bit-exact
+"""
+import numpy as np
+import pytest
+
+from golden_inputs import column_fnv, gae_long_inputs, hash_params
+from golden_io import load_case
+
+pytestmark = pytest.mark.gpu
+
+ppo_amd = pytest.importorskip("ppo_amd")
+from ppo_amd import DeviceArray  # noqa: E402
+
+WIDTH_CASES = [("ac256", 1), ("ant256", 1), ("hum376", 0)]
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def agent_for(meta, E, T=1, MB=1, EP=1, **kw):
+    hc = ppo_amd.HipConfig(meta["kind"], meta["O"], meta["A"], meta["H"], E, T, MB, EP, 0.99, 0.95,
+                           kw.get("clip", 0.2), kw.get("ent", 0.01), kw.get("vf", 0.5), kw.get("mgn", 0.5),
+                           kw.get("eps", 1e-5), 1, 1, 1, 0, 1)
+    return ppo_amd.Agent(hc)
+
+
+def golden_params(pre):
+    meta, _ = load_case(pre + "_act")
+    L = ppo_amd.agent_layout(meta["kind"], meta["O"], meta["A"], meta["H"])
+    return meta, hash_params(L, meta["hash_base"], meta.get("hi", 1.0), meta.get("lo", -1.0))
+
+
+@pytest.mark.parametrize("pre,kind", WIDTH_CASES)
+def test_act_vs_golden_at_reference_width(pre, kind):
+    meta, p = golden_params(pre)
+    _, d = load_case(pre + "_act")
+    n = d["x"].shape[0]
+    ag = agent_for(meta, n)
+    ag.load_params(p)
+    np.testing.assert_array_equal(ag.params(), p)
+    x, a = DeviceArray.from_numpy(d["x"]), DeviceArray.from_numpy(d["action"])
+    act, lp, ent, v = ag.get_action_and_value(x, ppo_amd.PPO_GIVEN, a)
+    np.testing.assert_allclose(lp.numpy(), d["logprob"], rtol=2e-5, atol=1e-4)
+    np.testing.assert_allclose(ent.numpy(), d["entropy"], rtol=2e-5, atol=1e-4)
+    np.testing.assert_allclose(v.numpy(), d["value"], rtol=2e-5, atol=2e-5)
+    am, lpm, _, _ = ag.get_action_and_value(x, ppo_amd.PPO_MEAN)
+    if kind == 1:
+        np.testing.assert_allclose(act.numpy(), d["action_roundtrip"], rtol=0, atol=2e-7)
+        np.testing.assert_allclose(am.numpy(), d["mean_action"], rtol=1e-5, atol=2e-6)
+        np.testing.assert_allclose(lpm.numpy(), d["mean_logprob"], rtol=2e-5, atol=1e-4)
+    else:
+        np.testing.assert_allclose(am.numpy(), d["mean"], rtol=1e-5, atol=2e-6)
+    # the rollout act kernel (the one the trainer launches every step) on the same rows
+    ag.close()
+
+
+@pytest.mark.parametrize("pre,kind", WIDTH_CASES)
+def test_update_vs_golden_at_reference_width(pre, kind):
+    meta, p = golden_params(pre)
+    mu, d = load_case(pre + "_update")
+    M = mu["M"]
+    ag = agent_for(meta, M, clip=mu["clip_coef"], ent=mu["ent_coef"], vf=mu["vf_coef"], mgn=mu["max_grad_norm"],
+                   eps=mu["adam_eps"])
+    ag.load_params(p)
+    O_, A = meta["O"], meta["A"]
+    ag.buffer(ppo_amd.BUF_OBS, (1, M, O_)).upload(d["x"].reshape(1, M, O_))
+    ag.buffer(ppo_amd.BUF_ACTIONS, (1, M, A)).upload(d["action"].reshape(1, M, A))
+    for buf, key in ((ppo_amd.BUF_LOGPROBS, "old_logp"), (ppo_amd.BUF_ADVANTAGES, "adv"),
+                     (ppo_amd.BUF_RETURNS, "ret"), (ppo_amd.BUF_VALUES, "old_v")):
+        ag.buffer(buf, (1, M)).upload(d[key].reshape(1, M))
+    perm = DeviceArray.from_numpy(np.arange(M, dtype=np.int32))
+    st = ag.update(mu["lr"], perms=perm)
+    g = ag.last_grad()
+    assert rel(g, d["grad_raw"]) < 2e-4, rel(g, d["grad_raw"])
+    L = ag.layout
+    for t in range(L.ntensors):
+        o, n = L.t_off[t], L.t_len[t]
+        if L.t_grad[t]:
+            assert rel(g[o:o + n], d["grad_raw"][o:o + n]) < 2e-3, (t, rel(g[o:o + n], d["grad_raw"][o:o + n]))
+    np.testing.assert_allclose([st["pg_loss"], st["v_loss"], st["entropy"], st["old_approx_kl"], st["approx_kl"],
+                                st["clipfrac"]], d["stats"][:6], rtol=2e-4, atol=2e-5)
+    np.testing.assert_allclose(st["grad_norm"], d["total_norm"][0], rtol=2e-4)
+    np.testing.assert_allclose(ag.params(), d["params_step1"], rtol=0, atol=2e-6)
+    ag.update(mu["lr"], perms=perm)
+    ag.update(mu["lr"], perms=perm)
+    np.testing.assert_allclose(ag.params(), d["params_step3"], rtol=0, atol=6e-6)
+    ag.close()
+
+
+@pytest.mark.parametrize("T", [1, 7, 33])
+def test_gae_ragged_bit_exact_vs_golden(T):
+    _, d = load_case(f"gae_t{T}")
+    E = d["rewards"].shape[1]
+    ag = agent_for({"kind": 0, "O": 17, "A": 6, "H": 64}, E, T=T)
+    for buf, key in ((ppo_amd.BUF_REWARDS, "rewards"), (ppo_amd.BUF_VALUES, "values"), (ppo_amd.BUF_DONES, "dones")):
+        ag.buffer(buf, (T, E)).upload(d[key])
+    ag.gae_from_values(DeviceArray.from_numpy(d["next_value"]), DeviceArray.from_numpy(d["next_done"]))
+    np.testing.assert_array_equal(ag.buffer(ppo_amd.BUF_ADVANTAGES, (T, E)).numpy(), d["advantages"])
+    np.testing.assert_array_equal(ag.buffer(ppo_amd.BUF_RETURNS, (T, E)).numpy(), d["returns"])
+    ag.close()
+
+
+def test_gae_long_bit_exact_vs_golden():
+    """cfg2's T=2048 at E=1024: 64 load chunks per env; compared through per-column FNV hashes."""
+    meta, d = load_case("gae_long")
+    T, E = meta["T"], meta["E"]
+    r, v, dn, nv, nd = gae_long_inputs(T, E)
+    ag = agent_for({"kind": 0, "O": 17, "A": 6, "H": 64}, E, T=T)
+    ag.buffer(ppo_amd.BUF_REWARDS, (T, E)).upload(r)
+    ag.buffer(ppo_amd.BUF_VALUES, (T, E)).upload(v)
+    ag.buffer(ppo_amd.BUF_DONES, (T, E)).upload(dn)
+    ag.gae_from_values(DeviceArray.from_numpy(nv), DeviceArray.from_numpy(nd))
+    adv = ag.buffer(ppo_amd.BUF_ADVANTAGES, (T, E)).numpy()
+    ret = ag.buffer(ppo_amd.BUF_RETURNS, (T, E)).numpy()
+    np.testing.assert_array_equal(adv[:, :8], d["adv_cols8"])
+    np.testing.assert_array_equal(column_fnv(adv), d["adv_fnv"])
+    np.testing.assert_array_equal(column_fnv(ret), d["ret_fnv"])
+    ag.close()

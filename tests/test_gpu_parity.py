@@ -434,3 +434,50 @@ def test_fused_dw_matches_two_phase_dw(kind, O_, A, H, monkeypatch):
         ag.close()
     assert np.isfinite(grads[0]).all()
     np.testing.assert_array_equal(grads[1], grads[0])
+
+
+def test_cfg1_shape_iteration_vs_oracle():
+    """BASELINE cfg1's shape (ppo_continuous_action defaults, ppo:57-66: num_envs=1, num_steps=2048,
+    32 minibatches of 64 rows, 10 epochs): one full iteration -- 2048 batch-1 rollout acts on the
+    device env, GAE over T=2048 for one env, 320 optimizer steps -- against the oracle doing the
+    same with the same Philox counters and Feistel permutations. 320 chained Adam steps let fp32
+    rounding differences grow, hence atol 1e-4 on the parameters (lr 3e-4 per step)."""
+    E, T, MB, EP = 1, 2048, 32, 10
+    O_, A, H = 17, 6, 64
+    rng = np.random.default_rng(23)
+    L = O.layout_init(0, O_, A, H)
+    p = random_params(L, rng)
+    p[L.logstd:L.logstd + A] = -0.5
+    cfg = ppo_amd.PPOConfig(num_envs=E, num_steps=T, num_minibatches=MB, update_epochs=EP, env_id="HalfCheetah-v5",
+                            total_timesteps=E * T * 2, ent_coef=0.0)
+    tr = ppo_amd.Trainer(cfg, params=p)
+    tr.iterate()
+    gpu_p = tr.agent.params()
+    gpu_obs = tr.agent.buffer(ppo_amd.BUF_OBS, (T, E, O_)).numpy()
+    gpu_adv = tr.agent.buffer(ppo_amd.BUF_ADVANTAGES, (T, E)).numpy()
+    oenv = O.SynthEnv(E, O_, A)
+    nobs = oenv.reset(cfg.seed)
+    ndone = np.zeros(E, np.float32)
+    bo = np.zeros((T, E, O_), np.float32); ba = np.zeros((T, E, A), np.float32)
+    bl = np.zeros((T, E), np.float32); br = np.zeros((T, E), np.float32)
+    bd = np.zeros((T, E), np.float32); bv = np.zeros((T, E), np.float32)
+    for t in range(T):
+        bo[t] = nobs; bd[t] = ndone
+        a, lp, _, v = O.get_action_and_value(L, p, nobs, 0, seed=cfg.seed, rank=0, env_base=0, step_id=t)
+        ba[t] = a; bl[t] = lp; bv[t] = v
+        nobs, r, te, trn, _, _ = oenv.step(a)
+        br[t] = r
+        ndone = np.maximum(te, trn)
+    assert bd.sum() >= 2  # the 1000-step truncation and its autoreset happen inside the rollout
+    _, _, _, nv = O.get_action_and_value(L, p, nobs, 2)
+    adv, ret = O.gae(br, bv, bd, nv, ndone, 0.99, 0.95)
+    np.testing.assert_allclose(gpu_obs, bo, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(gpu_adv, adv, rtol=1e-3, atol=1e-3)
+    lcfg = O.LossCfg(0.2, 0.0, 0.5, 1, 1)
+    lr = float(np.float32(cfg.learning_rate))
+    op, _, _, _, _ = O.update(L, p, np.zeros(L.P), np.zeros(L.P), 0, bo.reshape(-1, O_), ba.reshape(-1, A),
+                              bl.reshape(-1), adv.reshape(-1), ret.reshape(-1), bv.reshape(-1), EP, MB, lr, 0.5, 1e-5,
+                              lcfg, seed=cfg.seed, rank=0, epoch_counter0=0)
+    np.testing.assert_allclose(gpu_p, op, rtol=0, atol=1e-4)
+    assert np.abs(gpu_p - p).max() > 1e-3  # 320 steps actually moved the parameters
+    tr.close()

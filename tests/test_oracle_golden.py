@@ -125,3 +125,116 @@ def test_gae_bit_exact():
                      meta["gae_lambda"])
     np.testing.assert_array_equal(adv, d["advantages"])
     np.testing.assert_array_equal(ret, d["returns"])
+
+
+# ------------------------------------------------------------------------------------------------
+# round-2 cases at the reference's real widths (AC 2x256 LayerNorm trunks at HalfCheetah and Ant
+# dims, ac:159-186; PPO 2x64 tanh at Humanoid O=376 / A=17, ppo:122-139), ragged and long GAE
+# ------------------------------------------------------------------------------------------------
+from golden_inputs import column_fnv, gae_long_inputs, hash_params  # noqa: E402
+
+WIDTH_CASES = [("ac256", 1), ("ant256", 1), ("hum376", 0)]
+
+
+def width_params(pre):
+    meta, _ = load_case(pre + "_act")
+    L = O.layout_init(meta["kind"], meta["O"], meta["A"], meta["H"])
+    return meta, L, hash_params(L, meta["hash_base"], meta.get("hi", 1.0), meta.get("lo", -1.0))
+
+
+def ac_adv_stats(adv, G=1):
+    """ac:830-849: mean averaged over G row shards, sum of squares summed, Bessel over G*M_dev."""
+    adv = np.asarray(adv, np.float32)
+    Md = adv.size // G
+    mean = np.float32(np.mean([adv[r * Md:(r + 1) * Md].astype(np.float64).mean() for r in range(G)]))
+    ss = sum(float(np.sum((adv[r * Md:(r + 1) * Md].astype(np.float64) - mean) ** 2)) for r in range(G))
+    return mean, np.float32(np.sqrt(ss / (G * Md - 1)))
+
+
+@pytest.mark.parametrize("pre,kind", WIDTH_CASES)
+def test_width_layout_matches_named_parameters(pre, kind):
+    meta, L, p = width_params(pre)
+    names = meta["params"]
+    assert L.ntensors == len(names) and L.P == sum(n for _, n, _ in names)
+    for i, (name, n, grad) in enumerate(names):
+        assert L.t_len[i] == n and L.t_grad[i] == grad, name
+
+
+@pytest.mark.parametrize("pre,kind", WIDTH_CASES)
+def test_width_act_vs_golden(pre, kind):
+    meta, L, p = width_params(pre)
+    _, d = load_case(pre + "_act")
+    _, lp, ent, v = O.get_action_and_value(L, p, d["x"], 1, d["action"])
+    np.testing.assert_allclose(lp, d["logprob"], rtol=1e-5, atol=5e-5)
+    np.testing.assert_allclose(ent, d["entropy"], rtol=1e-5, atol=5e-5)
+    np.testing.assert_allclose(v, d["value"], rtol=1e-5, atol=1e-5)
+    am, lpm, _, _ = O.get_action_and_value(L, p, d["x"], 2)
+    if kind == 1:
+        np.testing.assert_allclose(am, d["mean_action"], rtol=1e-5, atol=2e-6)
+        np.testing.assert_allclose(lpm, d["mean_logprob"], rtol=1e-5, atol=5e-5)
+    else:
+        np.testing.assert_allclose(am, d["mean"], rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("pre,kind", WIDTH_CASES)
+def test_width_update_vs_golden(pre, kind):
+    """grad, stats, clip norm, 1 and 3 Adam steps; AC uses the trainer's distributed-form advantage
+    statistics with world_size = 1 (ac:830-849), PPO Tensor::std() (ppo:511)."""
+    meta, L, p = width_params(pre)
+    mu, du = load_case(pre + "_update")
+    cfg = O.LossCfg(mu["clip_coef"], mu["ent_coef"], mu["vf_coef"], mu["clip_vloss"], mu["norm_adv"])
+    am, asd = ac_adv_stats(du["adv"]) if kind == 1 else O.adv_stats(du["adv"])
+    args = (du["x"], du["action"], du["old_logp"], du["adv"], du["ret"], du["old_v"])
+    grad, stats = O.minibatch_grad(L, p, *args, cfg, adv_mean=am, adv_std=asd)
+    np.testing.assert_allclose(stats[:6], du["stats"][:6], rtol=5e-5, atol=5e-6)
+    assert rel(grad, du["grad_raw"]) < 2e-5
+    for t in range(L.ntensors):
+        o, n = L.t_off[t], L.t_len[t]
+        if L.t_grad[t]:
+            assert rel(grad[o:o + n], du["grad_raw"][o:o + n]) < 2e-4, t
+    m = np.zeros(L.P, np.float32); v = np.zeros(L.P, np.float32)
+    for s in range(1, 4):
+        if s > 1:
+            grad, _ = O.minibatch_grad(L, p, *args, cfg, adv_mean=am, adv_std=asd)
+        g, tn = O.clip_grad_norm(L, grad, mu["max_grad_norm"])
+        if s == 1:
+            assert abs(tn - du["total_norm"][0]) / du["total_norm"][0] < 2e-5
+        p, m, v = O.adam_step(L, p, g, m, v, s, mu["lr"], mu["adam_eps"])
+        if s == 1:
+            np.testing.assert_allclose(p, du["params_step1"], rtol=0, atol=5e-7)
+    np.testing.assert_allclose(p, du["params_step3"], rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("pre", ["ac256", "ant256"])
+def test_width_distributed_two_shards(pre):
+    meta, L, p = width_params(pre)
+    mu, d = load_case(pre + "_update")
+    cfg = O.LossCfg(mu["clip_coef"], mu["ent_coef"], mu["vf_coef"], mu["clip_vloss"], mu["norm_adv"])
+    mean, std = ac_adv_stats(d["adv"], G=2)
+    np.testing.assert_allclose([mean, std], d["dist2_adv_stats"], rtol=1e-6)
+    Md = d["adv"].size // 2
+    gs = []
+    for r in range(2):
+        sl = slice(r * Md, (r + 1) * Md)
+        g, _ = O.minibatch_grad(L, p, d["x"][sl], d["action"][sl], d["old_logp"][sl], d["adv"][sl], d["ret"][sl],
+                                d["old_v"][sl], cfg, adv_mean=mean, adv_std=std)
+        gs.append(g)
+    assert rel((gs[0] + gs[1]) / 2, d["grad_dist2_avg"]) < 2e-5
+
+
+@pytest.mark.parametrize("T", [1, 7, 33])
+def test_gae_ragged_bit_exact(T):
+    meta, d = load_case(f"gae_t{T}")
+    adv, ret = O.gae(d["rewards"], d["values"], d["dones"], d["next_value"], d["next_done"], 0.99, 0.95)
+    np.testing.assert_array_equal(adv, d["advantages"])
+    np.testing.assert_array_equal(ret, d["returns"])
+
+
+def test_gae_long_bit_exact():
+    """cfg2's T=2048 (E=1024): inputs regenerated from the hash streams, outputs via column hashes."""
+    meta, d = load_case("gae_long")
+    r, v, dn, nv, nd = gae_long_inputs(meta["T"], meta["E"])
+    adv, ret = O.gae(r, v, dn, nv, nd, 0.99, 0.95)
+    np.testing.assert_array_equal(adv[:, :8], d["adv_cols8"])
+    np.testing.assert_array_equal(column_fnv(adv), d["adv_fnv"])
+    np.testing.assert_array_equal(column_fnv(ret), d["ret_fnv"])

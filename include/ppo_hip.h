@@ -66,6 +66,17 @@ enum { PPO_BUF_OBS = 0, PPO_BUF_ACTIONS, PPO_BUF_LOGPROBS, PPO_BUF_REWARDS, PPO_
 
 const char* ppo_last_error(void);
 const char* ppo_version(void);
+/* 0 if exactly one HIP runtime (libamdhip64) is mapped in the process; otherwise an error naming
+ * them (a second one appears when a PyTorch-ROCm wheel is imported AFTER libppo_hip.so is loaded)
+ * and an exit guard that ends the process with status 70 instead of a corrupted-heap abort at exit.
+ * ppo_create / ppo_set_device / ppo_dev_malloc run this check first. */
+int ppo_runtime_check(void);
+
+/* The AC agent's fixed observation normalisation for env_id (AgentImpl mean_ / std_; reference
+ * ac_ppo_continuous_action.cpp Humanoid-v4 :496-497, Ant-v5 :521-522, Hopper-v5 :533-534).
+ * HalfCheetah-v5 uses zeros / ones (:510-511): returns 0 with *n = 0. Unknown env id: error.
+ * The arrays are static (owned by the library). */
+int ppo_obs_norm(const char* env_id, const float** mean, const float** std, int* n);
 
 int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
 int ppo_destroy(ppo_t* ctx);

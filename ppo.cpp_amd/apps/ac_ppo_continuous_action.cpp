@@ -74,6 +74,7 @@ static int env_int(const char* a, const char* b, int def) {
 
 int main(int argc, const char** argv) {
   std::ios_base::sync_with_stdio(false);
+  const auto process_start = std::filesystem::file_time_type::clock::now();
   const int rank = env_int("RANK", "OMPI_COMM_WORLD_RANK", 0);
   const int world_size = env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", 1);
   const int local_rank = env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", rank);
@@ -201,25 +202,61 @@ int main(int argc, const char** argv) {
     check(ppo_create(&hc, device, &agent), "ppo_create");
     ppo_layout L;
     check(ppo_get_layout(agent, &L), "ppo_get_layout");
-    auto p0 = init_params(L, config.seed, act_hi, act_lo, {}, {});
+    std::vector<float> obs_mean, obs_std;  // per-env-id constants (ac:480-534)
+    {
+      const float *m = nullptr, *sd = nullptr;
+      int n = 0;
+      if (ppo_obs_norm(config.env_id.c_str(), &m, &sd, &n) == 0 && n == O) {
+        obs_mean.assign(m, m + n);
+        obs_std.assign(sd, sd + n);
+      }
+    }
+    auto p0 = init_params(L, config.seed, act_hi, act_lo, obs_mean, obs_std);
     check(ppo_load_params(agent, p0.data(), L.P), "ppo_load_params");
     if (world_size > 1) {  // ncclUniqueId exchange through a file (no MPI in this build)
+      // The file carries a per-launch key (PPO_RUN_ID / TORCHELASTIC_RUN_ID / the MPI job id, when
+      // the launcher sets one) and must be newer than this process: a file left behind by an
+      // earlier launch on the same port is never taken for this one's. Rank 0 removes it once the
+      // communicator is up (ncclCommInitRank returns only after every rank has joined).
       const std::string path = config.rdzv_file.empty()
                                    ? "/tmp/ppo_rdzv_" + std::to_string(config.tcp_store_port) + ".id"
                                    : config.rdzv_file;
+      std::string key;
+      for (const char* v : {"PPO_RUN_ID", "TORCHELASTIC_RUN_ID", "OMPI_MCA_ess_base_jobid", "SLURM_JOB_ID"})
+        if (const char* e = getenv(v)) { key = e; break; }
       char id[PPO_COMM_ID_BYTES];
       if (rank == 0) {
         check(ppo_comm_unique_id(id), "ppo_comm_unique_id");
-        std::ofstream(path + ".tmp", std::ios::binary).write(id, PPO_COMM_ID_BYTES);
+        {
+          std::ofstream f(path + ".tmp", std::ios::binary | std::ios::trunc);
+          const uint32_t kl = (uint32_t)key.size();
+          f.write(reinterpret_cast<const char*>(&kl), sizeof(kl));
+          f.write(key.data(), kl);
+          f.write(id, PPO_COMM_ID_BYTES);
+        }
         fs::rename(path + ".tmp", path);
       } else {
-        for (int tries = 0; !fs::exists(path); ++tries) {
-          if (tries > 6000) throw std::runtime_error("timed out waiting for " + path);
+        const auto not_before = process_start - std::chrono::seconds(30);
+        for (int tries = 0;; ++tries) {
+          if (tries > 6000) throw std::runtime_error("timed out waiting for " + path + " (rank 0's communicator id)");
+          std::error_code ec;
+          if (fs::exists(path, ec) && fs::last_write_time(path, ec) >= not_before && !ec) {
+            std::ifstream f(path, std::ios::binary);
+            uint32_t kl = 0;
+            std::string k;
+            if (f.read(reinterpret_cast<char*>(&kl), sizeof(kl)) && kl < 4096) {
+              k.resize(kl);
+              if (f.read(k.data(), kl) && k == key && f.read(id, PPO_COMM_ID_BYTES)) break;
+            }
+          }
           std::this_thread::sleep_for(std::chrono::milliseconds(10));
         }
-        std::ifstream(path, std::ios::binary).read(id, PPO_COMM_ID_BYTES);
       }
       check(ppo_comm_init(agent, id, rank, world_size), "ppo_comm_init");
+      if (rank == 0) {
+        std::error_code ec;
+        fs::remove(path, ec);
+      }
       check(ppo_comm_broadcast_params(agent, 0), "ppo_comm_broadcast_params");  // ac:551-553
     }
     if (rank == 0) std::cout << "Number of parameters in model: " << (L.P - L.train_begin) << std::endl;

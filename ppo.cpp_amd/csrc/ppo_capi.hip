@@ -8,6 +8,10 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+#include <link.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -41,6 +45,72 @@ static int fail(const std::string& msg, int code = -1) {
   } while (0)
 
 extern "C" const char* ppo_last_error(void) { return g_err.c_str(); }
+
+// ------------------------------------------------------------------------------------------
+// one HIP runtime per process
+// ------------------------------------------------------------------------------------------
+// libppo_hip.so links /opt/rocm's libamdhip64.so.7. A PyTorch-ROCm wheel bundles its own copy and
+// its libraries ask for it as "libamdhip64.so"; if libppo_hip.so is loaded first, `import torch`
+// then maps a second HIP runtime, and the two tear each other down at exit (free(): invalid
+// pointer, exit 134). Every runtime-initialising entry point checks for that and fails with a
+// clear message; the first failed check also installs an exit guard that ends the process with
+// status 70 before either runtime's teardown runs.
+static int hip_runtime_paths(std::vector<std::string>* out) {
+  out->clear();
+  dl_iterate_phdr(
+      [](struct dl_phdr_info* info, size_t, void* data) -> int {
+        auto* v = static_cast<std::vector<std::string>*>(data);
+        const char* name = info->dlpi_name;
+        if (!name || !strstr(name, "libamdhip64.so")) return 0;
+        char buf[4096];
+        std::string path = realpath(name, buf) ? std::string(buf) : std::string(name);
+        if (std::find(v->begin(), v->end(), path) == v->end()) v->push_back(path);
+        return 0;
+      },
+      out);
+  return (int)out->size();
+}
+
+static std::string g_runtime_msg;
+static void runtime_exit_guard() {
+  fprintf(stderr, "libppo_hip: %s -- exiting (70) before the HIP runtimes' teardown\n", g_runtime_msg.c_str());
+  fflush(stderr);
+  _exit(70);
+}
+
+extern "C" int ppo_runtime_check(void) {
+  std::vector<std::string> paths;
+  if (hip_runtime_paths(&paths) <= 1) return 0;
+  std::string msg = "two HIP runtimes are mapped in this process (";
+  for (size_t i = 0; i < paths.size(); ++i) msg += (i ? ", " : "") + paths[i];
+  msg += "): load libppo_hip.so after `import torch` (ppo_amd does), or do not import torch";
+  static std::once_flag guard;
+  std::call_once(guard, [&] {
+    g_runtime_msg = msg;
+    atexit(runtime_exit_guard);
+  });
+  return fail(msg, -4);
+}
+
+// ------------------------------------------------------------------------------------------
+// per-env-id observation normalisation of the AC agent (ac:480-534)
+// ------------------------------------------------------------------------------------------
+#include "ppo_obs_norm.inc"
+
+extern "C" int ppo_obs_norm(const char* env_id, const float** mean, const float** stdv, int* n) {
+  if (!env_id || !mean || !stdv || !n) return fail("ppo_obs_norm: null argument");
+  *mean = *stdv = nullptr;
+  *n = 0;
+  if (!strcmp(env_id, "HalfCheetah-v5")) return 0;  // zeros / ones (ac:510-511): identity
+  for (const ObsNormEntry& e : k_obs_norm)
+    if (!strcmp(env_id, e.env_id)) {
+      *mean = e.mean;
+      *stdv = e.std;
+      *n = e.n;
+      return 0;
+    }
+  return fail(std::string("ppo_obs_norm: env_id ") + env_id + " is not implemented.", -1);
+}
 int ppo_fail(const std::string& msg, int code) { return fail(msg, code); }
 extern "C" const char* ppo_version(void) { return "ppo_hip 0.1 (gfx950)"; }
 
@@ -167,6 +237,7 @@ static int dmalloc(T** p, size_t n) {
 
 extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   if (!cfg || !out) return fail("ppo_create: null argument");
+  if (int rc = ppo_runtime_check()) return rc;
   ppo_layout L;
   if (ppo_layout_init(&L, cfg->net_kind, cfg->obs_dim, cfg->act_dim, cfg->hidden) != 0)
     return fail("ppo_create: bad net kind / dims");
@@ -847,11 +918,16 @@ extern "C" int ppo_comm_allreduce(ppo_t* c, float* buf, long n, int average) {
 // ------------------------------------------------------------------------------------------
 // device helpers
 // ------------------------------------------------------------------------------------------
-extern "C" int ppo_set_device(int d) { HIP_TRY(hipSetDevice(d)); return 0; }
+extern "C" int ppo_set_device(int d) {
+  if (int rc = ppo_runtime_check()) return rc;
+  HIP_TRY(hipSetDevice(d));
+  return 0;
+}
 extern "C" int ppo_device_count(int* n) { HIP_TRY(hipGetDeviceCount(n)); return 0; }
 // The helpers are host-synchronous and device-wide ordered: contexts run on non-blocking streams,
 // which are NOT ordered against the legacy null stream that plain hipMemcpy/hipMemset use.
 extern "C" int ppo_dev_malloc(void** p, size_t bytes) {
+  if (int rc = ppo_runtime_check()) return rc;
   HIP_TRY(hipMalloc(p, bytes ? bytes : 1));
   HIP_TRY(hipMemset(*p, 0, bytes ? bytes : 1));
   HIP_TRY(hipDeviceSynchronize());

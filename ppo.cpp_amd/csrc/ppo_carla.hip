@@ -302,6 +302,7 @@ extern "C" int ppo_carla_destroy(ppo_carla_t* c) {
 
 extern "C" int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_carla_t** out) {
   if (!cfg || !out) return ppo_fail("ppo_carla_create: null argument", -1);
+  if (int rc = ppo_runtime_check()) return rc;
   ppo_carla_layout L;
   if (ppo_carla_layout_init(&L, cfg->obs_channels, cfg->bev_h, cfg->bev_w, cfg->num_measurements,
                             cfg->num_value_measurements, cfg->action_dim) != 0)

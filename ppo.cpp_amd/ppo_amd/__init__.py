@@ -124,7 +124,10 @@ _LIB = None
 _VP, _FP, _I, _L, _F, _SZ = C.c_void_p, C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_size_t
 SYMBOLS = [
     ("ppo_last_error", C.c_char_p, []),
+    ("ppo_runtime_check", _I, []),
     ("ppo_version", C.c_char_p, []),
+    ("ppo_obs_norm", _I, [C.c_char_p, C.POINTER(C.POINTER(C.c_float)), C.POINTER(C.POINTER(C.c_float)),
+                          C.POINTER(_I)]),
     ("ppo_create", _I, [C.POINTER(HipConfig), _I, C.POINTER(_VP)]),
     ("ppo_destroy", _I, [_VP]),
     ("ppo_get_layout", _I, [_VP, C.POINTER(Layout)]),
@@ -281,6 +284,16 @@ def load_carla_pth(layout: CarlaLayout, path):
     out = np.empty(layout.P, np.float32)
     check(lib().ppo_carla_pth_load(C.byref(layout), os.fsencode(path), out.ctypes.data, layout.P))
     return out
+
+
+def obs_norm(env_id):
+    """(mean, std) the AC agent normalises observations with for env_id (ac:480-534); None for
+    HalfCheetah-v5 (zeros / ones)."""
+    m, s, n = C.POINTER(C.c_float)(), C.POINTER(C.c_float)(), C.c_int(0)
+    check(lib().ppo_obs_norm(env_id.encode(), C.byref(m), C.byref(s), C.byref(n)))
+    if n.value == 0:
+        return None
+    return (np.ctypeslib.as_array(m, shape=(n.value,)).copy(), np.ctypeslib.as_array(s, shape=(n.value,)).copy())
 
 
 def device_count():
@@ -780,6 +793,10 @@ def init_params(layout: Layout, seed=1, env_id=None, obs_mean=None, obs_std=None
             lo, hi = ENV_DIMS[env_id][2], ENV_DIMS[env_id][3]
         P[L.hi] = hi
         P[L.lo] = lo
+        if obs_mean is None and env_id in ENV_DIMS and ENV_DIMS[env_id][0] == O:
+            table = obs_norm(env_id)
+            if table is not None:
+                obs_mean, obs_std = table
         put(L.omean, np.zeros(O, np.float32) if obs_mean is None else np.asarray(obs_mean, np.float32))
         put(L.ostd, np.ones(O, np.float32) if obs_std is None else np.asarray(obs_std, np.float32))
         for tr in (L.critic, L.actor):

@@ -106,7 +106,7 @@ def test_one_rank_host_transport_equals_no_communicator_bitwise(data):
     nmb = 2 * 2
     assert calls[0] == (2 * nmb, True) and calls[1] == (nmb, False)
     grads = [(n, avg) for n, avg in calls if n > 100_000]  # the flat (packed) gradient, 146 K floats
-    assert len(grads) == nmb and all(avg for _, avg in grads)
+    assert len(grads) == 2 * nmb and all(avg for _, avg in grads)  # two updates
     ag.close()
 
 

@@ -45,20 +45,66 @@ def algorithmic_work(O, A, H, E, T, MB, nh):
     }
 
 
+def host_cores():
+    """CPU threads this job may use: the launcher's thread budget (OMP_NUM_THREADS, set to the box's
+    CPU share), else the cgroup quota, else the affinity mask."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+        if n > 0:
+            return n
+    except ValueError:
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            return max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        pass
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(E, T, MB, EP):
-    """The reference's CPU arithmetic on this host (1 intra-op thread, as ac:288 sets), bounded sample."""
+    """The reference's CPU arithmetic on this host, bounded sample: rollout inference on `cores`
+    host threads (the reference's per-env collection threads, ac:575-618 / :641-698), update with
+    one intra-op thread (ac:288-289)."""
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    cores = host_cores()
     if os.path.exists(harness):
         try:
-            out = subprocess.run([harness, "--bench", str(E), str(T), str(MB), str(EP), "2000"], capture_output=True,
-                                 text=True, timeout=300, check=True).stdout.strip().splitlines()[-1]
+            out = subprocess.run([harness, "--bench", str(E), str(T), str(MB), str(EP), "300", str(cores)],
+                                 capture_output=True, text=True, timeout=300, check=True).stdout.strip().splitlines()[-1]
             r = json.loads(out)
-            return {"value": round(r["sps"], 2), "unit": "env_steps/s", "cores": 1, "kind": "reference",
-                    "sample": (f"LibTorch CPU replay of the reference AC-PPO arithmetic (rl_utils.h Beta, 1 thread): "
-                               f"{r['n_act']} batch-1 get_action_and_value calls ({r['t_act_batch1_s']*1e3:.3f} ms each) "
-                               f"+ 1 optimizer step on M={r['M']} rows ({r['t_opt_step_s']:.2f} s) + GAE "
-                               f"({r['t_gae_s']*1e3:.1f} ms), extrapolated to one iteration ({E*T} acts, {EP*MB} "
-                               f"optimizer steps); env physics excluded")}
+            res = {"value": round(r["sps"], 2), "unit": "env_steps/s", "cores": cores, "kind": "reference",
+                   "cpu_model": cpu_model(), "value_1thread": round(r["sps_1thread"], 2),
+                   "sample": (f"LibTorch CPU replay of the reference AC-PPO arithmetic (rl_utils.h Beta): "
+                              f"{cores} host threads x {r['n_act']} batch-1 get_action_and_value calls "
+                              f"({r['t_act_batch1_s']*1e3:.3f} ms per call aggregate, "
+                              f"{r['t_act_batch1_1thread_s']*1e3:.3f} ms on 1 thread) + 1 optimizer step on "
+                              f"M={r['M']} rows, 1 intra-op thread as ac:288 sets ({r['t_opt_step_s']:.2f} s) + GAE "
+                              f"({r['t_gae_s']*1e3:.1f} ms), extrapolated to one iteration ({E*T} acts, {EP*MB} "
+                              f"optimizer steps); env physics excluded")}
+            try:  # BASELINE cfg1 (ppo_continuous_action defaults, CPU-only by design) beside the published SPS
+                o1 = subprocess.run([harness, "--bench-ppo", "1", "2048", "32", "10", "2048"], capture_output=True,
+                                    text=True, timeout=120, check=True).stdout.strip().splitlines()[-1]
+                r1 = json.loads(o1)
+                res["cfg1"] = {"value": round(r1["sps"], 1), "unit": "env_steps/s", "published": 1900,
+                               "sample": "ppo_continuous_action HalfCheetah-v5 num_envs=1: 2048 batch-1 acts + 64 "
+                                         "optimizer steps of 64 rows + GAE over T=2048 on 1 thread, extrapolated to "
+                                         "one iteration (2048 acts, 320 steps); physics, checkpoint and logging "
+                                         "excluded (the published ~1900 SPS includes MuJoCo)"}
+            except Exception as e:  # noqa: BLE001
+                print(f"[bench] cfg1 reference timing failed: {e}", file=sys.stderr)
+            return res
         except Exception as e:  # noqa: BLE001
             print(f"[bench] reference harness failed: {e}", file=sys.stderr)
     # C restatement (oracle) — port baseline
@@ -84,6 +130,25 @@ def cpu_baseline(E, T, MB, EP):
             "sample": f"C oracle: {Ms}-row minibatch gradient + 512 sampled acts, extrapolated to one iteration"}
 
 
+def cli_sps(E, T, iterations):
+    """SPS as the reference defines and prints it (ac:928-935: global_step / seconds since before
+    iteration 0, so the rollout, GAE, update, per-iteration checkpoint and logging are all inside):
+    the drop-in ac_ppo_continuous_action executable on the device env, last printed value."""
+    exe = os.path.join(ROOT, "ppo.cpp_amd", "bin", "ac_ppo_continuous_action")
+    if not os.path.exists(exe):
+        return None
+    cmd = [exe, "--env_id", "HalfCheetah-v5", "--env_backend", "device", "--num_envs", str(E), "--num_steps", str(T),
+           "--total_timesteps", str(E * T * iterations), "--exp_name_stem", "bench_cli", "--num_eval_runs", "1"]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True)
+        sps = [float(l.split(":")[1]) for l in r.stdout.splitlines() if l.startswith("SPS:")]
+        return {"value": sps[-1], "unit": "env_steps/s", "iterations": iterations,
+                "cmd": " ".join(os.path.relpath(c, ROOT) if c == exe else c for c in cmd)} if sps else None
+    except Exception as e:  # noqa: BLE001
+        print(f"[bench] CLI run failed: {e}", file=sys.stderr)
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,6 +159,8 @@ def main():
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-all", action="store_true", help="HIP-event time every kernel class")
+    ap.add_argument("--no-cli", action="store_true", help="skip the ac_ppo_continuous_action CLI SPS run")
+    ap.add_argument("--cli-iterations", type=int, default=30)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -185,6 +252,8 @@ def main():
         }
         if args.profile_all:
             out["kernels_ms_per_step"] = {k: round(v[0] / args.steps, 3) for k, v in prof.items()}
+        if world == 1 and not args.no_cli:
+            out["cli_value"] = cli_sps(E_total, T, args.cli_iterations)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(E, T, cfg.num_minibatches, cfg.update_epochs)
         print(json.dumps(out), flush=True)

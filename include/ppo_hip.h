@@ -118,6 +118,14 @@ int ppo_update(ppo_t* ctx, float lr, const int32_t* perms_dev, ppo_update_stats*
 int ppo_sync(ppo_t* ctx);
 /* test hook: raw (pre-clip, post all-reduce) gradient of the last minibatch, flat reference order */
 int ppo_debug_last_grad(ppo_t* ctx, float* host, long n);
+/* Asynchronous checkpoint source (the reference saves agent + optimizer every iteration inside its
+ * SPS span, ppo:545-563 / ac:904-927): ppo_snapshot_state enqueues a device-side copy of the
+ * parameters and the Adam state on the context stream (ordered after the last update, before the
+ * next) and returns at once; ppo_read_snapshot, callable from another host thread, waits for that
+ * copy only and unpacks it in the flat reference order. One snapshot buffer: call
+ * ppo_read_snapshot before the next ppo_snapshot_state. */
+int ppo_snapshot_state(ppo_t* ctx);
+int ppo_read_snapshot(ppo_t* ctx, float* params_host, float* m_host, float* v_host, long n, long* step);
 long ppo_iteration(const ppo_t* ctx);
 int ppo_set_iteration(ppo_t* ctx, long iteration);
 float* ppo_buffer(ppo_t* ctx, int which);

@@ -28,6 +28,10 @@ int psyn_step(psyn_t* env, int env_begin, int env_end, const float* action_dev, 
               float* obs_dev, float* reward_dev, float* done_dev, void* stream);
 /* sums of finished-episode returns / lengths / counts since the last call (host floats) */
 int psyn_episode_stats(psyn_t* env, float* sum_return, float* sum_length, float* count);
+/* the same without a device-wide sync: _begin enqueues the read-out (and the reset of the sums)
+ * on `stream`; _end waits for that read-out only and returns the sums (same values as above) */
+int psyn_episode_stats_begin(psyn_t* env, void* stream);
+int psyn_episode_stats_end(psyn_t* env, float* sum_return, float* sum_length, float* count);
 
 /* Device-resident rollout driver: num_steps x {ppo_rollout_act, psyn_step, ppo_rollout_reward} on
  * the context stream (ppo_continuous_action.cpp:387-434 with this env behind the boundary).

@@ -27,6 +27,7 @@
 #include <random>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 using torch::Tensor;
@@ -322,88 +323,6 @@ static std::tuple<Tensor, std::vector<float>> ppo_loss(const Tensor& newlogprob,
   std::vector<float> st = {pg_loss.item<float>(),      v_loss.item<float>(),   entropy_loss.item<float>(),
                            old_approx_kl.item<float>(), approx_kl.item<float>(), clipfrac, loss.item<float>()};
   return {loss, st};
-}
-
-// ---------------------------------------------------------------------------------------------
-// --bench: times the reference's CPU arithmetic for one AC-PPO iteration on a bounded sample
-// (1 intra-op thread, as ac_ppo_continuous_action.cpp:288-289 sets):
-//   * n_act batch-1 Agent::get_action_and_value calls with a per-env generator ("sample", ac:655)
-//   * one full optimizer step on a minibatch of M rows (ac:815-888: forward, loss, backward,
-//     clip_grad_norm_, Adam)
-//   * the GAE loop over [T, E] (ac:759-779)
-// and prints a JSON line; bench.py extrapolates it to one iteration (E*T acts, EP*MB steps).
-// ---------------------------------------------------------------------------------------------
-static int bench_main(int E, int T, int MB, int EP, int n_act) {
-  using clk = std::chrono::steady_clock;
-  const int O = 17, A = 6, H = 256;
-  const long B = (long)E * T, M = B / MB;
-  ACAgent agent(O, A, H, 1.0f, -1.0f, torch::zeros({O}), torch::ones({O}));
-  std::string names;
-  set_params(*agent, names);
-  torch::optim::Adam opt(agent->parameters(), torch::optim::AdamOptions(2.5e-4).eps(1e-5));
-  // batch-1 rollout inference
-  auto gen = at::make_generator<at::CPUGeneratorImpl>(1);
-  Tensor x1 = randn({1, O});
-  double t_act;
-  {
-    torch::NoGradGuard ng;
-    Tensor xn, feat, al, be;
-    auto t0 = clk::now();
-    for (int i = 0; i < n_act; ++i) {
-      Tensor xx = (x1 - agent->mean_) / agent->std_;
-      feat = agent->actor_encoder->forward(xx);
-      al = nn::functional::softplus(agent->dist_alpha->forward(feat)) + 1.0f;
-      be = nn::functional::softplus(agent->dist_beta->forward(feat)) + 1.0f;
-      const Beta probs(al, be);
-      Tensor a = probs.sample(gen);
-      Tensor lp = probs.log_prob(a).sum(1);
-      a = agent->unscale_action(a);
-      Tensor ent = probs.entropy().sum(1);
-      Tensor v = agent->critic->forward(xx);
-      (void)lp; (void)ent; (void)v;
-    }
-    t_act = std::chrono::duration<double>(clk::now() - t0).count() / n_act;
-  }
-  // one optimizer step on M rows
-  Tensor bx = randn({M, O}), ba = randu({M, A}, -0.99f, 0.99f), blp = randn({M}, 0.1f) - 5.0f;
-  Tensor badv = randn({M}), bret = randn({M}), bval = randn({M});
-  LossCfg c{0.1f, 0.01f, 0.5f, true, true};
-  double t_opt;
-  {
-    auto t0 = clk::now();
-    auto [a, lp, ent, v, al, be] = agent->get_action_and_value(bx, ba, "given");
-    Tensor amean = badv.mean();
-    Tensor astd = torch::sqrt(torch::sum(torch::square(badv - amean)) / static_cast<float>(M - 1));
-    auto [loss, st] = ppo_loss(lp, ent, v, blp, badv, bret, bval, c, &amean, &astd);
-    opt.zero_grad();
-    loss.backward();
-    torch::nn::utils::clip_grad_norm_(agent->parameters(), 0.5);
-    opt.step();
-    t_opt = std::chrono::duration<double>(clk::now() - t0).count();
-  }
-  // GAE over [T, E]
-  double t_gae;
-  {
-    torch::NoGradGuard ng;
-    Tensor rewards = randn({T, E}), values = randn({T, E}), dones = torch::zeros({T, E});
-    Tensor next_value = randn({E}), next_done = torch::zeros({E}), advantages = torch::zeros({T, E});
-    auto t0 = clk::now();
-    Tensor lastgaelam = torch::zeros({E}), nnt, nv;
-    for (int t = T - 1; t >= 0; --t) {
-      if (t == T - 1) { nnt = 1.0f - next_done; nv = next_value; }
-      else { nnt = 1.0 - dones.index({t + 1}); nv = values.index({t + 1}); }
-      Tensor delta = rewards.index({t}) + 0.99f * nv * nnt - values.index({t});
-      advantages.index({t}) = delta + 0.99f * 0.95f * nnt * lastgaelam;
-      lastgaelam = advantages.index({t});
-    }
-    Tensor returns = advantages + values;
-    t_gae = std::chrono::duration<double>(clk::now() - t0).count();
-  }
-  const double t_iter = t_act * (double)B + t_opt * (double)(EP * MB) + t_gae;
-  std::printf("{\"t_act_batch1_s\": %.9g, \"t_opt_step_s\": %.9g, \"t_gae_s\": %.9g, \"n_act\": %d, \"M\": %ld, "
-              "\"t_iter_s\": %.9g, \"sps\": %.9g, \"threads\": 1}\n",
-              t_act, t_opt, t_gae, n_act, M, t_iter, (double)B / t_iter);
-  return 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -769,13 +688,155 @@ static void width_cases() {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// --bench: times the reference's CPU arithmetic for one AC-PPO iteration on a bounded sample.
+// The reference runs with one intra-op thread (ac_ppo_continuous_action.cpp:288-289) and collects
+// with E/G host threads, each calling the shared agent with batch 1 on its own generator
+// (ac:575-618, :641-698). So:
+//   * rollout inference: `threads` host threads, each making n_act batch-1
+//     Agent::get_action_and_value calls ("sample", ac:655) on the same module under NoGradGuard;
+//     the per-call cost is wall time / (threads * n_act) (and the 1-thread cost on its own)
+//   * one full optimizer step on a minibatch of M rows (ac:815-888: forward, loss, backward,
+//     clip_grad_norm_, Adam) -- single-threaded, as the reference's update is
+//   * the GAE loop over [T, E] (ac:759-779)
+// and prints a JSON line; bench.py extrapolates it to one iteration (E*T acts, EP*MB steps).
+// --bench-ppo: the same for ppo_continuous_action (ppo:387-542; cfg1: E=1, T=2048, 32 x 10
+// minibatches of 64 rows, HalfCheetah O=17 / A=6, one thread by design ppo:187).
+// ---------------------------------------------------------------------------------------------
+static double time_ac_acts(ACAgent& agent, int O, int n_act, int threads) {
+  using clk = std::chrono::steady_clock;
+  std::vector<std::thread> pool;
+  std::vector<Tensor> xs;
+  for (int t = 0; t < threads; ++t) xs.push_back(randn({1, O}));
+  auto t0 = clk::now();
+  for (int t = 0; t < threads; ++t)
+    pool.emplace_back([&, t] {
+      torch::NoGradGuard ng;
+      auto gen = at::make_generator<at::CPUGeneratorImpl>(t);
+      for (int i = 0; i < n_act; ++i) {
+        Tensor xx = (xs[t] - agent->mean_) / agent->std_;
+        Tensor feat = agent->actor_encoder->forward(xx);
+        Tensor al = nn::functional::softplus(agent->dist_alpha->forward(feat)) + 1.0f;
+        Tensor be = nn::functional::softplus(agent->dist_beta->forward(feat)) + 1.0f;
+        const Beta probs(al, be);
+        Tensor a = probs.sample(gen);
+        Tensor lp = probs.log_prob(a).sum(1);
+        a = agent->unscale_action(a);
+        Tensor ent = probs.entropy().sum(1);
+        Tensor v = agent->critic->forward(xx);
+        (void)lp; (void)ent; (void)v;
+      }
+    });
+  for (auto& th : pool) th.join();
+  return std::chrono::duration<double>(clk::now() - t0).count() / ((double)n_act * threads);
+}
+
+static double time_gae(int T, int E) {
+  using clk = std::chrono::steady_clock;
+  Tensor rewards = randn({T, E}), values = randn({T, E}), dones = torch::zeros({T, E});
+  Tensor next_value = randn({E}), next_done = torch::zeros({E});
+  auto t0 = clk::now();
+  auto r = gae_ref(rewards, values, dones, next_value, next_done, 0.99f, 0.95f);
+  (void)r;
+  return std::chrono::duration<double>(clk::now() - t0).count();
+}
+
+static int bench_main(int E, int T, int MB, int EP, int n_act, int threads) {
+  using clk = std::chrono::steady_clock;
+  const int O = 17, A = 6, H = 256;
+  const long B = (long)E * T, M = B / MB;
+  ACAgent agent(O, A, H, 1.0f, -1.0f, torch::zeros({O}), torch::ones({O}));
+  std::string names;
+  set_params(*agent, names);
+  torch::optim::Adam opt(agent->parameters(), torch::optim::AdamOptions(2.5e-4).eps(1e-5));
+  const double t_act1 = time_ac_acts(agent, O, n_act / 4 > 0 ? n_act / 4 : 1, 1);
+  const double t_act = threads > 1 ? time_ac_acts(agent, O, n_act, threads) : t_act1;
+  // one optimizer step on M rows
+  Tensor bx = randn({M, O}), ba = randu({M, A}, -0.99f, 0.99f), blp = randn({M}, 0.1f) - 5.0f;
+  Tensor badv = randn({M}), bret = randn({M}), bval = randn({M});
+  LossCfg c{0.1f, 0.01f, 0.5f, true, true};
+  double t_opt;
+  {
+    auto t0 = clk::now();
+    auto [a, lp, ent, v, al, be] = agent->get_action_and_value(bx, ba, "given");
+    Tensor amean = badv.mean();
+    Tensor astd = torch::sqrt(torch::sum(torch::square(badv - amean)) / static_cast<float>(M - 1));
+    auto [loss, st] = ppo_loss(lp, ent, v, blp, badv, bret, bval, c, &amean, &astd);
+    opt.zero_grad();
+    loss.backward();
+    torch::nn::utils::clip_grad_norm_(agent->parameters(), 0.5);
+    opt.step();
+    t_opt = std::chrono::duration<double>(clk::now() - t0).count();
+  }
+  const double t_gae = time_gae(T, E);
+  const double t_iter = t_act * (double)B + t_opt * (double)(EP * MB) + t_gae;
+  const double t_iter1 = t_act1 * (double)B + t_opt * (double)(EP * MB) + t_gae;
+  std::printf("{\"t_act_batch1_s\": %.9g, \"t_act_batch1_1thread_s\": %.9g, \"t_opt_step_s\": %.9g, \"t_gae_s\": %.9g, "
+              "\"n_act\": %d, \"M\": %ld, \"t_iter_s\": %.9g, \"sps\": %.9g, \"threads\": %d, \"sps_1thread\": %.9g}\n",
+              t_act, t_act1, t_opt, t_gae, n_act, M, t_iter, (double)B / t_iter, threads, (double)B / t_iter1);
+  return 0;
+}
+
+static int bench_ppo_main(int E, int T, int MB, int EP, int n_act) {
+  using clk = std::chrono::steady_clock;
+  const int O = 17, A = 6, H = 64;
+  const long B = (long)E * T, M = B / MB;
+  PPOAgent agent(O, A, H);
+  std::string names;
+  set_params(*agent, names);
+  torch::optim::Adam opt(agent->parameters(), torch::optim::AdamOptions(3e-4).eps(1e-5));
+  Tensor x1 = randn({E, O});
+  double t_act;
+  {
+    torch::NoGradGuard ng;
+    auto t0 = clk::now();
+    for (int i = 0; i < n_act; ++i) {  // ppo:395 with the sampling of ppo:150-151 (Normal, at::normal)
+      const Tensor mu = agent->actor_mean->forward(x1);
+      const Tensor sd = torch::exp(agent->actor_logstd.expand_as(mu));
+      const Normal probs(mu, sd);
+      Tensor a = probs.sample(std::nullopt);
+      Tensor lp = probs.log_prob(a).sum(1), ent = probs.entropy().sum(1), v = agent->critic->forward(x1);
+      (void)lp; (void)ent; (void)v;
+    }
+    t_act = std::chrono::duration<double>(clk::now() - t0).count() / n_act;
+  }
+  Tensor bx = randn({M, O}), ba = randn({M, A}, 0.5f), blp = randn({M}, 0.1f) - 5.0f;
+  Tensor badv = randn({M}), bret = randn({M}), bval = randn({M});
+  const LossCfg c{0.2f, 0.0f, 0.5f, true, true};
+  const int n_opt = 64;
+  auto t0 = clk::now();
+  for (int i = 0; i < n_opt; ++i) {  // ppo:494-540
+    auto [a, lp, ent, v, mu] = agent->get_action_and_value(bx, ba);
+    auto [loss, st] = ppo_loss(lp, ent, v, blp, badv, bret, bval, c, nullptr, nullptr);
+    opt.zero_grad();
+    loss.backward();
+    torch::nn::utils::clip_grad_norm_(agent->parameters(), 0.5);
+    opt.step();
+  }
+  const double t_opt = std::chrono::duration<double>(clk::now() - t0).count() / n_opt;
+  const double t_gae = time_gae(T, E);
+  const double t_iter = t_act * (double)T + t_opt * (double)(EP * MB) + t_gae;
+  std::printf("{\"t_act_s\": %.9g, \"t_opt_step_s\": %.9g, \"t_gae_s\": %.9g, \"n_act\": %d, \"M\": %ld, "
+              "\"t_iter_s\": %.9g, \"sps\": %.9g, \"threads\": 1}\n",
+              t_act, t_opt, t_gae, n_act, M, t_iter, (double)B / t_iter);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   torch::set_num_threads(1);
   if (argc > 1 && std::string(argv[1]) == "--bench") {
+    // --bench E T MB EP n_act threads
     int E = argc > 2 ? std::atoi(argv[2]) : 4096, T = argc > 3 ? std::atoi(argv[3]) : 128;
     int MB = argc > 4 ? std::atoi(argv[4]) : 4, EP = argc > 5 ? std::atoi(argv[5]) : 4;
-    int n_act = argc > 6 ? std::atoi(argv[6]) : 2000;
-    return bench_main(E, T, MB, EP, n_act);
+    int n_act = argc > 6 ? std::atoi(argv[6]) : 2000, threads = argc > 7 ? std::atoi(argv[7]) : 1;
+    return bench_main(E, T, MB, EP, n_act, threads < 1 ? 1 : threads);
+  }
+  if (argc > 1 && std::string(argv[1]) == "--bench-ppo") {
+    // --bench-ppo E T MB EP n_act   (cfg1 defaults: 1 2048 32 10)
+    int E = argc > 2 ? std::atoi(argv[2]) : 1, T = argc > 3 ? std::atoi(argv[3]) : 2048;
+    int MB = argc > 4 ? std::atoi(argv[4]) : 32, EP = argc > 5 ? std::atoi(argv[5]) : 10;
+    int n_act = argc > 6 ? std::atoi(argv[6]) : 2048;
+    return bench_ppo_main(E, T, MB, EP, n_act);
   }
   if (argc > 1 && std::string(argv[1]) == "--pth-load") {
     // --pth-load <ppo|ac> O A H <model.pth> <optimizer.pth> <out_dir>: torch::load both archives

@@ -289,6 +289,9 @@ int main(int argc, const char** argv) {
     HIPCHECK(hipDeviceSynchronize());
 
     long global_step = 0;
+    float* d_stats = nullptr;  // episode sums all-reduced over ranks (ac:700-727)
+    HIPCHECK(hipMalloc(&d_stats, sizeof(float) * 3));
+    AsyncCheckpointer ckpt(agent);
     const auto start_time = std::chrono::high_resolution_clock::now();
     ppo_update_stats st{};
     double last_lr = config.learning_rate;  // the optimizer's lr at save time
@@ -301,9 +304,9 @@ int main(int argc, const char** argv) {
       double sum_r = 0, sum_l = 0, n_ep = 0;
       if (device_env) {
         check(ppo_rollout_synth(agent, denv, d_obs, d_done, d_act, d_rew), "ppo_rollout_synth");
-        float r, l, n;
-        check(psyn_episode_stats(denv, &r, &l, &n), "psyn_episode_stats");
-        sum_r = r; sum_l = l; n_ep = n;
+        // episode sums read out behind the rollout, without a device-wide sync; collected after
+        // the update has been enqueued (the values are those of this rollout)
+        check(psyn_episode_stats_begin(denv, s), "psyn_episode_stats_begin");
       } else {
         // asynchronous collection: one host thread + HIP stream per env group
         std::vector<std::thread> th;
@@ -348,17 +351,21 @@ int main(int argc, const char** argv) {
         if (failed) throw std::runtime_error("collection failed");
         for (int gi = 0; gi < G; ++gi) { sum_r += gr[gi]; sum_l += gl[gi]; n_ep += gn[gi]; }
       }
+      check(ppo_compute_gae(agent, d_obs, d_done, T, s), "ppo_compute_gae");
+      check(ppo_update(agent, lrnow, nullptr, &st), "ppo_update");  // stats are rank-averaged inside
+      if (device_env) {
+        float r, l, n;
+        check(psyn_episode_stats_end(denv, &r, &l, &n), "psyn_episode_stats_end");
+        sum_r = r; sum_l = l; n_ep = n;
+      }
       global_step += (long)config.num_envs * config.num_steps;  // ac:730
       // episode statistics summed over ranks (ac:700-727), through the RCCL communicator
       float h_stats[3] = {(float)sum_r, (float)sum_l, (float)n_ep};
       if (world_size > 1) {
-        float* d_stats;
-        HIPCHECK(hipMalloc(&d_stats, sizeof(h_stats)));
-        HIPCHECK(hipMemcpy(d_stats, h_stats, sizeof(h_stats), hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpyAsync(d_stats, h_stats, sizeof(h_stats), hipMemcpyHostToDevice, s));
         check(ppo_comm_allreduce(agent, d_stats, 3, 0), "ppo_comm_allreduce");
+        HIPCHECK(hipMemcpyAsync(h_stats, d_stats, sizeof(h_stats), hipMemcpyDeviceToHost, s));
         HIPCHECK(hipStreamSynchronize(s));
-        HIPCHECK(hipMemcpy(h_stats, d_stats, sizeof(h_stats), hipMemcpyDeviceToHost));
-        (void)hipFree(d_stats);
       }
       if (rank == 0 && h_stats[2] > 0) {
         const float avg_return = h_stats[0] / h_stats[2], avg_length = h_stats[1] / h_stats[2];
@@ -368,15 +375,12 @@ int main(int argc, const char** argv) {
                   << avg_return << " \n";
         logger.add_scalar("charts/episodic_return_per_sec", std::lround(seconds_since(start_time)), avg_return);
       }
-      check(ppo_compute_gae(agent, d_obs, d_done, T, s), "ppo_compute_gae");
-      check(ppo_update(agent, lrnow, nullptr, &st), "ppo_update");  // stats are rank-averaged inside
       if (rank == 0) {
         char mf[64], of[64];
         std::snprintf(mf, sizeof mf, "model_latest_%09u.pth", iteration);
         std::snprintf(of, sizeof of, "optimizer_latest_%09u.pth", iteration);
-        save_state(agent, exp_folder, mf, of, lrnow, config.adam_eps);
+        ckpt.request(exp_folder, mf, of, lrnow, config.adam_eps, iteration);  // written while the GPU runs on
         last_lr = lrnow;
-        cleanup_checkpoints(exp_folder, iteration);
         const double secs = seconds_since(start_time);
         float sps = 0.f;
         if (secs > 0) {
@@ -394,6 +398,7 @@ int main(int argc, const char** argv) {
       }
       std::cout << std::flush;
     }
+    ckpt.finish();
     if (rank == 0) save_state(agent, exp_folder, "model_final.pth", "optimizer_final.pth", last_lr, config.adam_eps);
     // rank 0 evaluation with the Beta mean action on env 0 (ac:965-1001)
     if (rank == 0 && !device_env) {
@@ -426,6 +431,7 @@ int main(int argc, const char** argv) {
     for (auto gs : gstreams)
       if (gs) (void)hipStreamDestroy(gs);
     if (denv) psyn_destroy(denv);
+    (void)hipFree(d_stats);
     (void)hipFree(d_obs); (void)hipFree(d_done); (void)hipFree(d_act); (void)hipFree(d_rew);
     if (h_obs) { (void)hipHostFree(h_obs); (void)hipHostFree(h_act); (void)hipHostFree(h_rew); (void)hipHostFree(h_done); }
     ppo_destroy(agent);

@@ -139,6 +139,7 @@ int main(int argc, const char** argv) {
     HIPCHECK(hipMemsetAsync(d_done, 0, sizeof(float) * E, s));
 
     long global_step = 0;
+    AsyncCheckpointer ckpt(agent);
     const auto start_time = std::chrono::high_resolution_clock::now();
     ppo_update_stats st{};
     double last_lr = config.learning_rate;  // the optimizer's lr at save time
@@ -185,9 +186,8 @@ int main(int argc, const char** argv) {
       char mf[64], of[64];
       std::snprintf(mf, sizeof mf, "model_latest_%09d.pth", iteration);
       std::snprintf(of, sizeof of, "optimizer_latest_%09d.pth", iteration);
-      save_state(agent, exp_folder, mf, of, lrnow, config.adam_eps);
+      ckpt.request(exp_folder, mf, of, lrnow, config.adam_eps, iteration);  // written while the GPU runs on
       last_lr = lrnow;
-      cleanup_checkpoints(exp_folder, iteration);
       const double secs = seconds_since(start_time);
       float sps = 0.f;
       if (secs > 0) {
@@ -203,6 +203,7 @@ int main(int argc, const char** argv) {
       logger.add_scalar("losses/clipfrac", global_step, st.clipfrac);
       logger.add_scalar("charts/SPS", global_step, sps);
     }
+    ckpt.finish();
     save_state(agent, exp_folder, "model_final.pth", "optimizer_final.pth", last_lr, config.adam_eps);
     // final evaluation on the training envs (normalisation statistics live there, ppo:589-626)
     const float* eobs = envs->reset(config.eval_seed);

@@ -9,6 +9,9 @@
 
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <filesystem>
@@ -200,6 +203,103 @@ inline void save_state(ppo_t* ctx, const std::filesystem::path& folder, const st
 }
 
 // keeps only this iteration's model_latest_* / optimizer_latest_* (ppo:548-563)
+inline void cleanup_checkpoints(const std::filesystem::path& folder, long iteration);
+
+// The per-iteration checkpoint of the reference (ppo:545-563, ac:904-927: model_latest_%09d.pth +
+// optimizer_latest_%09d.pth, older ones deleted) off the critical path: request()
+// enqueues a device-side snapshot of parameters + Adam state behind the update just launched and
+// returns; a writer thread waits for that snapshot, copies it out and writes / prunes the archives
+// while the GPU runs the next iteration. One request in flight: a new one first waits until the
+// writer has copied the previous snapshot out. Errors surface on the next request() / finish().
+class AsyncCheckpointer {
+  struct Job {
+    std::filesystem::path folder;
+    std::string model_file, optimizer_file;
+    double lr, eps;
+    long cleanup_iteration;  // < 0: no pruning
+  };
+  ppo_t* ctx_;
+  ppo_layout L_{};
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool have_job_ = false, snapshot_free_ = true, idle_ = true, stop_ = false;
+  Job job_;
+  std::string error_;
+
+  void run() {
+    std::vector<float> p(L_.P), m(L_.P), v(L_.P);
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return have_job_ || stop_; });
+        if (!have_job_ && stop_) return;
+        j = job_;
+        have_job_ = false;
+        idle_ = false;
+      }
+      std::string err;
+      long step = 0;
+      if (ppo_read_snapshot(ctx_, p.data(), m.data(), v.data(), L_.P, &step) != 0) err = ppo_last_error();
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        snapshot_free_ = true;
+      }
+      cv_.notify_all();
+      if (err.empty() && ppo_pth_save_agent(&L_, p.data(), (j.folder / j.model_file).string().c_str()) != 0)
+        err = ppo_last_error();
+      if (err.empty() && ppo_pth_save_adam(&L_, m.data(), v.data(), step, j.lr, j.eps,
+                                           (j.folder / j.optimizer_file).string().c_str()) != 0)
+        err = ppo_last_error();
+      if (err.empty() && j.cleanup_iteration >= 0) {
+        try {
+          cleanup_checkpoints(j.folder, j.cleanup_iteration);
+        } catch (const std::exception& e) {
+          err = e.what();
+        }
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!err.empty() && error_.empty()) error_ = "checkpoint: " + err;
+        idle_ = true;
+      }
+      cv_.notify_all();
+    }
+  }
+
+ public:
+  explicit AsyncCheckpointer(ppo_t* ctx) : ctx_(ctx) {
+    check(ppo_get_layout(ctx, &L_), "ppo_get_layout");
+    th_ = std::thread([this] { run(); });
+  }
+  ~AsyncCheckpointer() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+  void request(const std::filesystem::path& folder, const std::string& model_file, const std::string& optimizer_file,
+               double lr, double eps, long cleanup_iteration) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return snapshot_free_ && !have_job_; });
+    if (!error_.empty()) throw std::runtime_error(error_);
+    check(ppo_snapshot_state(ctx_), "ppo_snapshot_state");
+    job_ = Job{folder, model_file, optimizer_file, lr, eps, cleanup_iteration};
+    have_job_ = true;
+    snapshot_free_ = false;
+    lk.unlock();
+    cv_.notify_all();
+  }
+  // waits until every requested checkpoint is on disk
+  void finish() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return !have_job_ && idle_; });
+    if (!error_.empty()) throw std::runtime_error(error_);
+  }
+};
 inline void cleanup_checkpoints(const std::filesystem::path& folder, long iteration) {
   char keep_m[64], keep_o[64];
   std::snprintf(keep_m, sizeof keep_m, "model_latest_%09ld.pth", iteration);

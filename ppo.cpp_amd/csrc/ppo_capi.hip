@@ -157,6 +157,10 @@ struct ppo_ctx {
   float* normout = nullptr;
   float* gnpart = nullptr;
   float* mbstats = nullptr;  // [EP*MB][8]
+  float* snap = nullptr;     // ppo_snapshot_state: P | Am | Av (packed)
+  hipEvent_t snap_ev = nullptr;
+  hipStream_t snap_stream = nullptr;
+  long snap_step = 0;
   long adam_step = 0;
   long iteration = 0;
   ncclComm_t comm = nullptr;
@@ -367,6 +371,9 @@ extern "C" int ppo_destroy(ppo_t* c) {
   if (c->perms) (void)hipFree(c->perms);
   if (c->advpart) (void)hipFree(c->advpart);
   comm_detach(c);
+  if (c->snap) (void)hipFree(c->snap);
+  if (c->snap_ev) (void)hipEventDestroy(c->snap_ev);
+  if (c->snap_stream) (void)hipStreamDestroy(c->snap_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -833,6 +840,40 @@ extern "C" int ppo_debug_last_grad(ppo_t* c, float* host, long n) {
   return 0;
 }
 
+extern "C" int ppo_snapshot_state(ppo_t* c) {
+  if (!c) return fail("null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t n = c->K.size;
+  if (!c->snap) {
+    HIP_TRY(hipMalloc(&c->snap, 3 * n * sizeof(float)));
+    HIP_TRY(hipEventCreateWithFlags(&c->snap_ev, hipEventDisableTiming));
+    HIP_TRY(hipStreamCreateWithFlags(&c->snap_stream, hipStreamNonBlocking));
+  }
+  HIP_TRY(hipMemcpyAsync(c->snap, c->P, n * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->snap + n, c->Am, n * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->snap + 2 * n, c->Av, n * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(hipEventRecord(c->snap_ev, c->stream));
+  c->snap_step = c->adam_step;
+  return 0;
+}
+
+extern "C" int ppo_read_snapshot(ppo_t* c, float* p, float* m, float* v, long n, long* step) {
+  if (!c) return fail("null ctx");
+  if (!c->snap) return fail("ppo_read_snapshot: no snapshot taken");
+  if (n != c->L.P) return fail("ppo_read_snapshot: size mismatch");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t K = c->K.size;
+  std::vector<float> h(3 * K);
+  HIP_TRY(hipStreamWaitEvent(c->snap_stream, c->snap_ev, 0));
+  HIP_TRY(hipMemcpyAsync(h.data(), c->snap, 3 * K * sizeof(float), hipMemcpyDeviceToHost, c->snap_stream));
+  HIP_TRY(hipStreamSynchronize(c->snap_stream));
+  if (p) unpack_params(c->K, c->L, h.data(), p);
+  if (m) unpack_params(c->K, c->L, h.data() + K, m);
+  if (v) unpack_params(c->K, c->L, h.data() + 2 * K, v);
+  if (step) *step = c->snap_step;
+  return 0;
+}
+
 extern "C" int ppo_sync(ppo_t* c) {
   if (!c) return fail("null ctx");
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -991,6 +1032,8 @@ extern "C" int ppo_profile_reset(ppo_t* c) {
 struct psyn_env {
   SynthArgs a;
   int device;
+  float* host_stats = nullptr;  // pinned [3][E]: psyn_episode_stats_begin / _end
+  hipEvent_t stats_ev = nullptr;
 };
 
 extern "C" int psyn_create(int E, int O, int A, psyn_t** out) {
@@ -1027,6 +1070,8 @@ extern "C" int psyn_destroy(psyn_t* env) {
   void* ptrs[] = {a.q, a.t, a.autoreset, a.rseed, a.rcount, a.ep_ret, a.ep_len, a.fin_ret, a.fin_len, a.fin_cnt};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (env->host_stats) (void)hipHostFree(env->host_stats);
+  if (env->stats_ev) (void)hipEventDestroy(env->stats_ev);
   delete env;
   return 0;
 }
@@ -1067,6 +1112,36 @@ extern "C" int ppo_rollout_synth(ppo_t* c, psyn_t* env, float* next_obs, float* 
     }
   }
   HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+extern "C" int psyn_episode_stats_begin(psyn_t* env, void* stream) {
+  if (!env) return fail("null env");
+  const int E = env->a.E;
+  hipStream_t s = (hipStream_t)stream;
+  if (!env->host_stats) {
+    HIP_TRY(hipHostMalloc(&env->host_stats, sizeof(float) * 3 * E));
+    HIP_TRY(hipEventCreateWithFlags(&env->stats_ev, hipEventDisableTiming));
+  }
+  float* src[3] = {env->a.fin_ret, env->a.fin_len, env->a.fin_cnt};
+  for (int k = 0; k < 3; ++k) {
+    HIP_TRY(hipMemcpyAsync(env->host_stats + (size_t)k * E, src[k], sizeof(float) * E, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemsetAsync(src[k], 0, sizeof(float) * E, s));
+  }
+  HIP_TRY(hipEventRecord(env->stats_ev, s));
+  return 0;
+}
+
+extern "C" int psyn_episode_stats_end(psyn_t* env, float* sr, float* sl, float* sc) {
+  if (!env || !env->stats_ev) return fail("psyn_episode_stats_end: no read-out pending");
+  HIP_TRY(hipEventSynchronize(env->stats_ev));
+  const int E = env->a.E;
+  double R = 0, Lsum = 0, N = 0;
+  const float* h = env->host_stats;
+  for (int i = 0; i < E; ++i) { R += h[i]; Lsum += h[E + i]; N += h[2 * E + i]; }
+  if (sr) *sr = (float)R;
+  if (sl) *sl = (float)Lsum;
+  if (sc) *sc = (float)N;
   return 0;
 }
 

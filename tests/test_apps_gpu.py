@@ -81,3 +81,90 @@ def test_cli_flag_errors():
     assert r.returncode != 0 and "norm_adv" in r.stderr
     r = subprocess.run([exe, "--help"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "--num_envs" in r.stdout
+
+
+def tb_scalars(path):
+    """(tag, step, simple_value) of every Summary.Value in a TFRecord event file (minimal protobuf
+    reader: Event.step = field 2 varint, Event.summary = field 5, Summary.value = field 1,
+    Value.tag = field 1, Value.simple_value = field 2 float)."""
+    import struct
+
+    def fields(buf):
+        i = 0
+        while i < len(buf):
+            key, i = _varint(buf, i)
+            f, wt = key >> 3, key & 7
+            if wt == 0:
+                v, i = _varint(buf, i)
+            elif wt == 1:
+                v, i = buf[i:i + 8], i + 8
+            elif wt == 5:
+                v, i = buf[i:i + 4], i + 4
+            else:
+                n, i = _varint(buf, i)
+                v, i = buf[i:i + n], i + n
+            yield f, v
+
+    ev = open(path, "rb").read()
+    out, pos = [], 0
+    while pos < len(ev):
+        (n,) = struct.unpack_from("<Q", ev, pos)
+        rec = ev[pos + 12:pos + 12 + n]
+        pos += 12 + n + 4
+        step = 0
+        for f, v in fields(rec):
+            if f == 2:
+                step = v
+            elif f == 5:
+                for sf, sv in fields(v):
+                    if sf == 1:
+                        tag, val = None, None
+                        for vf, vv in fields(sv):
+                            if vf == 1:
+                                tag = vv.decode()
+                            elif vf == 2:
+                                val = struct.unpack("<f", vv)[0]
+                        out.append((tag, step, val))
+    return out
+
+
+def _varint(b, i):
+    r, s = 0, 0
+    while True:
+        c = b[i]
+        i += 1
+        r |= (c & 0x7F) << s
+        s += 7
+        if not c & 0x80:
+            return r, i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exe,lr0,E,T", [("ppo_continuous_action", 3e-4, 8, 64), ("ac_ppo_continuous_action", 2.5e-4, 16, 16)])
+def test_lr_anneal_schedule_and_async_checkpoints(exe, lr0, E, T):
+    """LR anneal (ppo:379-384, ac:634-639): lrnow = (1 - it / num_iterations) * lr0 in float32,
+    read back from the charts/learning_rate scalars of the TensorBoard file; and the checkpoints
+    written off the critical path: the last model_latest_*.pth (async snapshot after the last
+    update) holds exactly the parameters of model_final.pth."""
+    n_it = 5
+    stem = f"t_lr_{exe[:3]}"
+    extra = ["--env_backend", "device"] if exe.startswith("ac") else []
+    _run([_exe(exe), "--env_id", "SyntheticCheetah-v0", "--num_envs", str(E), "--num_steps", str(T),
+          "--total_timesteps", str(E * T * n_it), "--num_eval_runs", "1", "--exp_name_stem", stem, "--seed", "2"] + extra)
+    d = os.path.join(MODELS, f"{stem}_2")
+    tb = "tfevents_logs.pb" if exe.startswith("ppo") else "tfevents_logs_0.pb"
+    lrs = [(s, v) for tag, s, v in tb_scalars(os.path.join(d, tb)) if tag == "charts/learning_rate"]
+    assert len(lrs) == n_it
+    want = [np.float32(np.float32(1.0) - np.float32(i) / np.float32(n_it)) * np.float32(lr0) for i in range(n_it)]
+    np.testing.assert_array_equal(np.float32([v for _, v in lrs]), np.float32(want))
+    assert [s for s, _ in lrs] == [E * T * (i + 1) for i in range(n_it)]
+    kind = P.PPO_NET_TANH_NORMAL if exe.startswith("ppo") else P.PPO_NET_LN_BETA
+    L = P.agent_layout(kind, 17, 6, 64 if kind == P.PPO_NET_TANH_NORMAL else 256)
+    latest = sorted(f for f in os.listdir(d) if f.startswith("model_latest_"))
+    assert latest == [f"model_latest_{n_it - 1:09d}.pth"]
+    np.testing.assert_array_equal(P.load_agent_pth(L, os.path.join(d, latest[0])),
+                                  P.load_agent_pth(L, os.path.join(d, "model_final.pth")))
+    m, v, step, lr, eps = P.load_adam_pth(L, os.path.join(d, f"optimizer_latest_{n_it - 1:09d}.pth"))
+    mf, vf, stepf, _, _ = P.load_adam_pth(L, os.path.join(d, "optimizer_final.pth"))
+    assert step == stepf and np.array_equal(m, mf) and np.array_equal(v, vf)
+    assert lr == pytest.approx(float(want[-1]), rel=1e-6)

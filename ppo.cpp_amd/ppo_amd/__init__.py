@@ -145,6 +145,8 @@ SYMBOLS = [
     ("ppo_update", _I, [_VP, _F, _VP, C.POINTER(UpdateStats)]),
     ("ppo_sync", _I, [_VP]),
     ("ppo_debug_last_grad", _I, [_VP, _FP, _L]),
+    ("ppo_snapshot_state", _I, [_VP]),
+    ("ppo_read_snapshot", _I, [_VP, _FP, _FP, _FP, _L, C.POINTER(_L)]),
     ("ppo_iteration", _L, [_VP]),
     ("ppo_set_iteration", _I, [_VP, _L]),
     ("ppo_buffer", _VP, [_VP, _I]),
@@ -171,6 +173,8 @@ SYMBOLS = [
     ("psyn_reset", _I, [_VP, _I, _FP, _FP, _VP]),
     ("psyn_step", _I, [_VP, _I, _I, _FP, _F, _F, _FP, _FP, _FP, _VP]),
     ("psyn_episode_stats", _I, [_VP, C.POINTER(_F), C.POINTER(_F), C.POINTER(_F)]),
+    ("psyn_episode_stats_begin", _I, [_VP, _VP]),
+    ("psyn_episode_stats_end", _I, [_VP, C.POINTER(_F), C.POINTER(_F), C.POINTER(_F)]),
     ("ppo_rollout_synth", _I, [_VP, _VP, _FP, _FP, _FP, _FP]),
     ("ppo_carla_create", _I, [C.POINTER(CarlaConfig), _I, C.POINTER(_VP)]),
     ("ppo_carla_destroy", _I, [_VP]),

@@ -300,6 +300,22 @@ static float gamma_mt(float alpha, uint64_t seed, int rank, long env, long step,
   return d;
 }
 
+void orc_normal_noise(uint64_t seed, int rank, long env, long step, int A, float* z) {
+  for (int a = 0; a < A; ++a) {
+    uint32_t rr[4];
+    philox_draw(seed, rank, env, step, (uint32_t)(a >> 1), rr);
+    float z0, z1;
+    box_muller(rr[0], rr[1], &z0, &z1);
+    z[a] = (a & 1) ? z1 : z0;
+  }
+}
+
+float orc_beta_sample01(float alpha, float beta, uint64_t seed, int rank, long env, long step, int a) {
+  const float ga = gamma_mt(alpha, seed, rank, env, step, 0x10000u + (uint32_t)(a * 2 + 0) * 64u);
+  const float gb = gamma_mt(beta, seed, rank, env, step, 0x10000u + (uint32_t)(a * 2 + 1) * 64u);
+  return ga / (ga + gb);
+}
+
 void orc_get_action_and_value(const ppo_layout* L, const float* P, int n, const float* x, int mode,
                               const float* action_in, uint64_t seed, int rank, long env_base, long step_id,
                               float* action_out, float* logprob, float* entropy, float* value) {

@@ -95,6 +95,12 @@ typedef struct orc_env_state {
 } orc_env_state;
 
 void orc_env_reset(orc_env_state* s, int seed, float* obs_out);
+/* The sampling draws of the Philox contract, for replays that compute the distribution elsewhere
+ * (oracle/ref_harness.cpp end-to-end case): the A standard-normal draws of Normal.sample for
+ * (env, step), and the Beta(alpha, beta) sample in [0, 1] of action index a (Marsaglia-Tsang
+ * gammas), exactly as orc_get_action_and_value draws them. */
+void orc_normal_noise(uint64_t seed, int rank, long env, long step, int A, float* z);
+float orc_beta_sample01(float alpha, float beta, uint64_t seed, int rank, long env, long step, int a);
 /* SeqVectorEnv::step semantics (gym.h:131-163) with clip_actions and RecordEpisodeStatistics.
  * info_ret/info_len get the finished episode stats (info_len = 0 if none). */
 void orc_env_step(orc_env_state* s, const float* actions, float act_lo, float act_hi,

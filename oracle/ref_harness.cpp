@@ -17,6 +17,8 @@
 #include <rl_utils.h>
 #include <torch/torch.h>
 
+#include "ppo_oracle.h"  // the synthetic env and the Philox sampling draws (end-to-end case only)
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -624,6 +626,161 @@ struct WrapChain {
   }
 };
 
+
+// ---------------------------------------------------------------------------------------------
+// End-to-end replay (SURVEY §8c "end-to-end run fixture"; north_star: episodic returns on identical
+// seeds): NIT iterations of the trainer loop -- lr anneal (ppo:379-384 / ac:634-639), rollout
+// (ppo:387-434), GAE, EP x MB minibatch updates with clip_grad_norm_ + Adam (ppo:489-540 /
+// ac:803-888) -- with the reference's LibTorch arithmetic, on the synthetic device env's dynamics
+// (oracle env, bit-identical to the device env) and the build's RNG contract injected: the
+// Normal noise / Beta samples of the Philox counters and the Feistel minibatch permutations
+// (LibTorch's own generators cannot be reproduced on the GPU). Records per-iteration loss
+// statistics, finished-episode returns and the final parameters.
+// ---------------------------------------------------------------------------------------------
+template <typename AgentT>
+static void e2e_case(const std::string& cname, AgentT& agent, int kind, int E, int T, int MB, int EP, int NIT,
+                     float lr0, const LossCfg& c, uint32_t base) {
+  const int O = 17, A = 6;
+  std::string names;
+  hash_params(*agent, base, 1.0f, -1.0f, names);
+  const uint64_t seed = 1;
+  torch::optim::Adam opt(agent->parameters(), torch::optim::AdamOptions(lr0).eps(1e-5));
+  // env
+  std::vector<float> q((size_t)E * O);
+  std::vector<int> et(E), ar(E), elen(E);
+  std::vector<uint32_t> rs(E), rc(E);
+  std::vector<float> eret(E);
+  orc_env_state env{E, O, A, q.data(), et.data(), ar.data(), rs.data(), rc.data(), eret.data(), elen.data()};
+  Tensor next_obs = torch::empty({E, O});
+  orc_env_reset(&env, (int)seed, next_obs.data_ptr<float>());
+  Tensor next_done = torch::zeros({E});
+  const long B = (long)E * T, M = B / MB;
+  std::vector<float> stats;   // per iteration: pg, v, ent, old_kl, kl (last minibatch), clipfrac (mean), ret_sum, n_ep
+  for (int it = 0; it < NIT; ++it) {
+    const float frac = 1.0f - static_cast<float>(it) / static_cast<float>(NIT);
+    const float lrnow = frac * lr0;
+    static_cast<torch::optim::AdamOptions&>(opt.param_groups()[0].options()).set_lr(lrnow);
+    Tensor obs = torch::zeros({T, E, O}), actions = torch::zeros({T, E, A}), logprobs = torch::zeros({T, E});
+    Tensor rewards = torch::zeros({T, E}), dones = torch::zeros({T, E}), values = torch::zeros({T, E});
+    double ret_sum = 0.0, n_ep = 0.0;
+    for (int t = 0; t < T; ++t) {
+      torch::NoGradGuard ng;
+      obs.index_put_({t}, next_obs);
+      dones.index_put_({t}, next_done);
+      const long step = (long)it * T + t;
+      Tensor act, lp, v;
+      if constexpr (std::is_same_v<AgentT, PPOAgent>) {
+        const Tensor mu = agent->actor_mean->forward(next_obs);
+        const Tensor sd = torch::exp(agent->actor_logstd.expand_as(mu));
+        Tensor z = torch::empty({E, A});
+        for (int e = 0; e < E; ++e) orc_normal_noise(seed, 0, e, step, A, z.data_ptr<float>() + (long)e * A);
+        act = mu + z * sd;  // Normal::sample = mean + std * eps (rl_utils.h:34-37)
+        const Normal probs(mu, sd);
+        lp = probs.log_prob(act).sum(1);
+        v = agent->critic->forward(next_obs).view(-1);
+      } else {
+        Tensor xn = (next_obs - agent->mean_) / agent->std_;
+        Tensor feat = agent->actor_encoder->forward(xn);
+        Tensor al = nn::functional::softplus(agent->dist_alpha->forward(feat)) + 1.0f;
+        Tensor be = nn::functional::softplus(agent->dist_beta->forward(feat)) + 1.0f;
+        Tensor s01 = torch::empty({E, A});
+        for (int e = 0; e < E; ++e)
+          for (int a = 0; a < A; ++a)
+            s01.data_ptr<float>()[e * A + a] = orc_beta_sample01(al[e][a].item<float>(), be[e][a].item<float>(), seed, 0,
+                                                                e, step, a);
+        const Beta probs(al, be);
+        lp = probs.log_prob(s01).sum(1);
+        act = agent->unscale_action(s01);
+        v = agent->critic->forward(xn).view(-1);
+      }
+      actions.index_put_({t}, act);
+      logprobs.index_put_({t}, lp);
+      values.index_put_({t}, v);
+      Tensor ob = torch::empty({E, O}), r = torch::empty({E}), te = torch::empty({E}), tr = torch::empty({E});
+      Tensor ir = torch::empty({E});
+      std::vector<int> il(E);
+      Tensor ac = act.contiguous();
+      orc_env_step(&env, ac.data_ptr<float>(), -1.0f, 1.0f, ob.data_ptr<float>(), r.data_ptr<float>(),
+                   te.data_ptr<float>(), tr.data_ptr<float>(), ir.data_ptr<float>(), il.data());
+      for (int e = 0; e < E; ++e)
+        if (il[e] > 0) { ret_sum += ir.data_ptr<float>()[e]; n_ep += 1.0; }
+      rewards.index_put_({t}, r);
+      next_obs = ob;
+      next_done = torch::maximum(te, tr);
+    }
+    Tensor next_value;
+    {
+      torch::NoGradGuard ng;
+      if constexpr (std::is_same_v<AgentT, PPOAgent>) next_value = agent->get_value(next_obs).flatten();
+      else next_value = agent->critic->forward((next_obs - agent->mean_) / agent->std_).flatten();
+    }
+    auto [adv, ret] = gae_ref(rewards, values, dones, next_value, next_done, 0.99f, 0.95f);
+    Tensor b_obs = obs.reshape({B, O}), b_act = actions.reshape({B, A}), b_lp = logprobs.reshape({B});
+    Tensor b_adv = adv.reshape({B}), b_ret = ret.reshape({B}), b_val = values.reshape({B});
+    std::vector<float> st_last;
+    double cf_sum = 0.0;
+    for (int ep = 0; ep < EP; ++ep) {
+      std::vector<int64_t> perm(B);
+      orc_perm(B, seed, 0, (long)it * EP + ep, perm.data());
+      Tensor b_inds = torch::from_blob(perm.data(), {B}, torch::kInt64).clone();
+      for (long start = 0; start < B; start += M) {
+        Tensor mb = b_inds.index({torch::indexing::Slice(start, start + M)});
+        Tensor lp, ent, v;
+        if constexpr (std::is_same_v<AgentT, PPOAgent>) {
+          auto [a_, lp_, ent_, v_, mu_] = agent->get_action_and_value(b_obs.index({mb}), b_act.index({mb}));
+          lp = lp_; ent = ent_; v = v_;
+        } else {
+          auto [a_, lp_, ent_, v_, al_, be_] = agent->get_action_and_value(b_obs.index({mb}), b_act.index({mb}), "given");
+          lp = lp_; ent = ent_; v = v_;
+        }
+        Tensor madv = b_adv.index({mb});
+        std::tuple<Tensor, std::vector<float>> res;
+        if (kind == 1) {  // ac:830-849 with world_size = 1
+          Tensor amean, astd;
+          {
+            torch::NoGradGuard ng;
+            amean = madv.mean();
+            astd = torch::sqrt(torch::sum(torch::square(madv - amean)) / static_cast<float>(M - 1));
+          }
+          res = ppo_loss(lp, ent, v, b_lp.index({mb}), madv, b_ret.index({mb}), b_val.index({mb}), c, &amean, &astd);
+        } else {
+          res = ppo_loss(lp, ent, v, b_lp.index({mb}), madv, b_ret.index({mb}), b_val.index({mb}), c, nullptr, nullptr);
+        }
+        auto& [loss, st] = res;
+        opt.zero_grad();
+        loss.backward();
+        torch::nn::utils::clip_grad_norm_(agent->parameters(), 0.5);
+        opt.step();
+        st_last = st;
+        cf_sum += st[5];
+      }
+    }
+    stats.insert(stats.end(), {st_last[0], st_last[1], st_last[2], st_last[3], st_last[4],
+                               (float)(cf_sum / (EP * (B / M))), (float)ret_sum, (float)n_ep});
+  }
+  begin_case(cname, "{\"kind\": " + std::to_string(kind) + ", \"E\": " + std::to_string(E) + ", \"T\": " +
+                        std::to_string(T) + ", \"MB\": " + std::to_string(MB) + ", \"EP\": " + std::to_string(EP) +
+                        ", \"iterations\": " + std::to_string(NIT) + ", \"lr\": " + f2s(lr0) + ", \"clip_coef\": " +
+                        f2s(c.clip_coef) + ", \"ent_coef\": " + f2s(c.ent_coef) + ", \"hash_base\": " +
+                        std::to_string(base) + ", \"seed\": 1, \"stats\": [\"pg_loss\", \"v_loss\", \"entropy\", "
+                        "\"old_approx_kl\", \"approx_kl\", \"clipfrac_mean\", \"episodic_return_sum\", \"episodes\"]}");
+  dump(cname, "stats", torch::tensor(stats).view({NIT, 8}));
+  dump(cname, "params_final", flat_params(*agent));
+  end_case();
+}
+
+static void e2e_cases() {
+  const int E = 8, T = 128, MB = 4, EP = 4, NIT = 8;  // 1024 steps per env: every env finishes an episode
+  {
+    PPOAgent agent(17, 6, 64);
+    e2e_case("e2e_ppo", agent, 0, E, T, MB, EP, NIT, 3e-4f, LossCfg{0.2f, 0.0f, 0.5f, true, true}, 3300);
+  }
+  {
+    ACAgent agent(17, 6, 256, 1.0f, -1.0f, torch::zeros({17}), torch::ones({17}));
+    e2e_case("e2e_ac", agent, 1, E, T, MB, EP, NIT, 2.5e-4f, LossCfg{0.1f, 0.01f, 0.5f, true, true}, 3400);
+  }
+}
+
 static void width_cases() {
   ac_width_case("ac256", 17, 6, 256, 256, 3000, 1.0f, -1.0f);
   ac_width_case("ant256", 105, 8, 256, 256, 3100, 1.0f, -1.0f);
@@ -1205,6 +1362,7 @@ int main(int argc, char** argv) {
 
   // ---- round 2: the reference's real widths, long / ragged GAE, the PPO env wrappers ----------
   width_cases();
+  e2e_cases();
 
   g_manifest << "\n}\n";
   std::ofstream(g_out + "/manifest.json") << g_manifest.str();

@@ -1,0 +1,60 @@
+"""End-to-end learning parity (north_star: "matching the reference's episodic returns within a
+stated FP tolerance on identical seeds"; SURVEY §8c end-to-end fixture): 8 iterations of the full
+trainer loop (lr anneal, 128-step rollout on the device env, GAE, 4 epochs x 4 minibatches with
+clip_grad_norm_ + Adam) on the GPU through the C-ABI, against the LibTorch replay of the reference
+arithmetic in oracle/ref_harness.cpp (golden cases e2e_ppo / e2e_ac) fed the same env dynamics,
+the same Philox action noise / Beta samples and the same Feistel minibatch permutations.
+
+E=8 envs x T=128 steps x 8 iterations = 1024 steps per env, so every env finishes its
+1000-step episode in the last iteration and the episodic returns are compared too.
+
+Tolerances (stated; fp32 on both sides, MFMA vs LibTorch CPU accumulation orders): the rollouts
+feed back into themselves over 1024 steps and 128 optimizer steps, so differences of a few ulps
+per op compound:
+  per-iteration v_loss / pg_loss / entropy     rtol 2e-3 (atol 1e-4)
+  approx_kl / old_approx_kl                    atol 2e-4
+  clipfrac (mean over 16 minibatches)          atol 1e-2  (a ratio sitting on 1 +- clip can flip)
+  episodic return sum (8 episodes)             rtol 1e-3
+  final parameters                              atol 2e-4 (128 Adam steps of lr <= 3e-4)
+"""
+import numpy as np
+import pytest
+
+from golden_inputs import hash_params
+from golden_io import load_case
+
+pytestmark = pytest.mark.gpu
+
+ppo_amd = pytest.importorskip("ppo_amd")
+
+
+@pytest.mark.parametrize("case", ["e2e_ppo", "e2e_ac"])
+def test_end_to_end_iterations_vs_libtorch_replay(case):
+    meta, d = load_case(case)
+    kind, E, T, MB, EP, NIT = meta["kind"], meta["E"], meta["T"], meta["MB"], meta["EP"], meta["iterations"]
+    common = dict(num_envs=E, num_steps=T, num_minibatches=MB, update_epochs=EP, total_timesteps=E * T * NIT,
+                  env_id="HalfCheetah-v5", seed=1, learning_rate=meta["lr"], clip_coef=meta["clip_coef"],
+                  ent_coef=meta["ent_coef"])
+    cfg = ppo_amd.PPOConfig(**common) if kind == 0 else ppo_amd.ACPPOConfig(**common)
+    L = ppo_amd.agent_layout(kind, 17, 6, cfg.hidden)
+    p0 = hash_params(L, meta["hash_base"])
+    tr = ppo_amd.Trainer(cfg, params=p0)
+    rows = []
+    for _ in range(NIT):
+        st = tr.iterate(want_stats=True)
+        r, _, n = tr.env.episode_stats()
+        rows.append([st["pg_loss"], st["v_loss"], st["entropy"], st["old_approx_kl"], st["approx_kl"], st["clipfrac"],
+                     r, n])
+    got = np.array(rows, np.float64)
+    want = d["stats"].astype(np.float64)
+    print("\n" + case + " max |diff| per stat:", np.abs(got - want).max(axis=0))
+    np.testing.assert_allclose(got[:, :3], want[:, :3], rtol=2e-3, atol=1e-4)
+    np.testing.assert_allclose(got[:, 3:5], want[:, 3:5], rtol=0, atol=2e-4)
+    np.testing.assert_allclose(got[:, 5], want[:, 5], rtol=0, atol=1e-2)
+    np.testing.assert_array_equal(got[:, 7], want[:, 7])  # episodes finished per iteration
+    assert want[-1, 7] == E
+    np.testing.assert_allclose(got[:, 6], want[:, 6], rtol=1e-3, atol=1e-3)
+    p = tr.agent.params()
+    print(case + " final params max |diff|:", np.abs(p - d["params_final"]).max())
+    np.testing.assert_allclose(p, d["params_final"], rtol=0, atol=2e-4)
+    tr.close()

@@ -715,6 +715,15 @@ static void e2e_case(const std::string& cname, AgentT& agent, int kind, int E, i
       else next_value = agent->critic->forward((next_obs - agent->mean_) / agent->std_).flatten();
     }
     auto [adv, ret] = gae_ref(rewards, values, dones, next_value, next_done, 0.99f, 0.95f);
+    if (const char* dbg = std::getenv("E2E_DEBUG_DIR")) {  // diagnostics: the rollout of every iteration
+      const std::string pre = std::string(dbg) + "/" + cname + "_it" + std::to_string(it);
+      for (auto& [nm, tt] : std::vector<std::pair<std::string, Tensor>>{{"actions", actions}, {"logprobs", logprobs},
+                                                                         {"values", values}, {"obs", obs}}) {
+        Tensor c2 = tt.contiguous();
+        std::ofstream(pre + "_" + nm + ".f32", std::ios::binary)
+            .write(reinterpret_cast<const char*>(c2.data_ptr<float>()), c2.numel() * 4);
+      }
+    }
     Tensor b_obs = obs.reshape({B, O}), b_act = actions.reshape({B, A}), b_lp = logprobs.reshape({B});
     Tensor b_adv = adv.reshape({B}), b_ret = ret.reshape({B}), b_val = values.reshape({B});
     std::vector<float> st_last;

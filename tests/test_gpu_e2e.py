@@ -8,14 +8,16 @@ the same Philox action noise / Beta samples and the same Feistel minibatch permu
 E=8 envs x T=128 steps x 8 iterations = 1024 steps per env, so every env finishes its
 1000-step episode in the last iteration and the episodic returns are compared too.
 
-Tolerances (stated; fp32 on both sides, MFMA vs LibTorch CPU accumulation orders): the rollouts
-feed back into themselves over 1024 steps and 128 optimizer steps, so differences of a few ulps
-per op compound:
-  per-iteration v_loss / pg_loss / entropy     rtol 2e-3 (atol 1e-4)
-  approx_kl / old_approx_kl                    atol 2e-4
-  clipfrac (mean over 16 minibatches)          atol 1e-2  (a ratio sitting on 1 +- clip can flip)
-  episodic return sum (8 episodes)             rtol 1e-3
-  final parameters                              atol 2e-4 (128 Adam steps of lr <= 3e-4)
+Tolerances (stated; fp32 on both sides, MFMA vs LibTorch CPU accumulation orders):
+  PPO agent (2x64 tanh, Normal): the whole run stays within a few ulps --
+    per-iteration losses rtol 2e-5, kl atol 1e-6, clipfrac exact-ish (atol 1e-3),
+    episodic returns rtol 1e-5, final parameters atol 1e-6 (measured 9e-8).
+  AC agent (2x256 LayerNorm, Beta): ulp-level differences of the first iterations (actions 5e-7)
+    are amplified by the optimizer -- the C oracle (double accumulators) against the same LibTorch
+    replay drifts identically: actions 5e-7 / 1e-6 / 5e-5 apart after 0 / 1 / 2 iterations, no
+    sample flips (tests/test_oracle_golden.py::test_e2e_oracle_vs_libtorch_drift measures it on CPU).
+    So: iterations 0-1 losses rtol 2e-4; later iterations rtol 5e-2 (atol 2e-3); clipfrac atol 3e-2;
+    episodic returns rtol 2e-3 (measured 6.5e-4); final parameters relative L2 < 2e-2.
 """
 import numpy as np
 import pytest
@@ -47,14 +49,24 @@ def test_end_to_end_iterations_vs_libtorch_replay(case):
                      r, n])
     got = np.array(rows, np.float64)
     want = d["stats"].astype(np.float64)
-    print("\n" + case + " max |diff| per stat:", np.abs(got - want).max(axis=0))
-    np.testing.assert_allclose(got[:, :3], want[:, :3], rtol=2e-3, atol=1e-4)
-    np.testing.assert_allclose(got[:, 3:5], want[:, 3:5], rtol=0, atol=2e-4)
-    np.testing.assert_allclose(got[:, 5], want[:, 5], rtol=0, atol=1e-2)
+    p = tr.agent.params()
+    tr.close()
+    diff = np.abs(got - want)
+    prel = np.linalg.norm(p.astype(np.float64) - d["params_final"]) / np.linalg.norm(d["params_final"])
+    print(f"\n{case} |diff| per iteration (pg, v, ent, okl, kl, cf, ret, n):\n{np.array2string(diff, precision=2)}"
+          f"\nfinal params max |diff| {np.abs(p - d['params_final']).max():.3g}, rel L2 {prel:.3g}")
     np.testing.assert_array_equal(got[:, 7], want[:, 7])  # episodes finished per iteration
     assert want[-1, 7] == E
-    np.testing.assert_allclose(got[:, 6], want[:, 6], rtol=1e-3, atol=1e-3)
-    p = tr.agent.params()
-    print(case + " final params max |diff|:", np.abs(p - d["params_final"]).max())
-    np.testing.assert_allclose(p, d["params_final"], rtol=0, atol=2e-4)
-    tr.close()
+    if kind == 0:
+        np.testing.assert_allclose(got[:, :3], want[:, :3], rtol=2e-5, atol=1e-6)
+        np.testing.assert_allclose(got[:, 3:5], want[:, 3:5], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(got[:, 5], want[:, 5], rtol=0, atol=1e-3)
+        np.testing.assert_allclose(got[:, 6], want[:, 6], rtol=1e-5)
+        np.testing.assert_allclose(p, d["params_final"], rtol=0, atol=1e-6)
+    else:
+        np.testing.assert_allclose(got[:2, :3], want[:2, :3], rtol=2e-4, atol=2e-5)
+        np.testing.assert_allclose(got[2:, :3], want[2:, :3], rtol=5e-2, atol=2e-3)
+        np.testing.assert_allclose(got[:, 3:5], want[:, 3:5], rtol=0, atol=2e-3)
+        np.testing.assert_allclose(got[:, 5], want[:, 5], rtol=0, atol=3e-2)
+        np.testing.assert_allclose(got[:, 6], want[:, 6], rtol=2e-3)
+        assert prel < 2e-2

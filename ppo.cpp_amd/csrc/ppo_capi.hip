@@ -148,6 +148,7 @@ struct ppo_ctx {
   float* slab[2] = {};
   int tiles_per_block = 1, nblk = 1;
   bool use_upd = false;  // feature-split k_upd (ppo_update.hip) instead of k_fwdbwd
+  bool use_upd2 = false;  // two-trunk k_upd2 (ppo_update_narrow.hip, H = 64 tanh agent)
   UpdGeoOut upd = {};
   int upd_nblk = 0;
   size_t lds_bytes = 0;
@@ -318,7 +319,11 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   {
     const char* ev = getenv("PPO_UPD_KERNEL");  // "0": force the wave-per-16-rows k_fwdbwd
     const int sgmax = std::max(c->sg[0].size, c->sg[1].size);
-    if (!(ev && ev[0] == '0') && upd_supported(c->K, c->sg[1].nh, sgmax, &c->upd) == 0) {
+    if (!(ev && ev[0] == '0') && upd2_supported(c->K, &c->upd) == 0) {
+      c->use_upd = c->use_upd2 = true;
+      const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
+      c->upd_nblk = std::min(ut, 512);  // both trunks per workgroup, 2 workgroups per CU x 256 CUs
+    } else if (!(ev && ev[0] == '0') && upd_supported(c->K, c->sg[1].nh, sgmax, &c->upd) == 0) {
       c->use_upd = true;
       const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
       c->upd_nblk = std::min(ut, 256);  // 2 workgroups per CU x 256 CUs over the two trunks
@@ -331,6 +336,7 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   c->lds_bytes = ((size_t)c->wlds_off + 2 * (size_t)H * 16) * sizeof(float);
   // dW split-K: ~128 row chunks per trunk (256 workgroups for the two trunks), 16-row multiples
   c->rows_per_chunk = std::max(64, (((c->M + 127) / 128) + 15) & ~15);
+  if (c->use_upd2) c->rows_per_chunk = std::max(32, (((c->M + 255) / 256) + 31) & ~31);  // k_dw2: both trunks
   c->nchunks = (c->M + c->rows_per_chunk - 1) / c->rows_per_chunk;
   for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->dwslab[k], (size_t)c->nchunks * (H * H + H * OP));
   rc |= dmalloc(&c->normout, 2 + PPO_LAYOUT_MAX_TENSORS + 2);
@@ -686,6 +692,8 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   dw.rows_per_chunk = c->rows_per_chunk;
   dw.fused = c->dw_fused;
   dw.xn = c->Xn;
+  dw.obs = c->buf[PPO_BUF_OBS];
+  dw.O = c->K.O;
   dw.slab_stride = (long)H * H + (long)H * OP;
   for (int k = 0; k < 2; ++k) {
     dw.dz2[k] = c->DZ2[k];
@@ -773,15 +781,18 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
       const int gi = e * MB + mb;
       u.perm = perms + (size_t)e * B + (size_t)mb * M;
       u.adv_stats = c->advstats + 2 * gi;
+      if (c->use_upd2) dw.perm = u.perm;  // k_dw gathers dW1's input rows itself
       {
         ProfScope ps(c, PK_FWDBWD, s);
-        const int rc_ = c->use_upd ? launch_upd(u, c->sg[1].nh, c->upd_nblk, c->upd.lds_bytes, s)
-                                   : launch_fwdbwd(u, nblk, c->lds_bytes, s);
+        const int rc_ = c->use_upd2  ? launch_upd2(u, c->upd_nblk, c->upd.lds_bytes, s)
+                        : c->use_upd ? launch_upd(u, c->sg[1].nh, c->upd_nblk, c->upd.lds_bytes, s)
+                                     : launch_fwdbwd(u, nblk, c->lds_bytes, s);
         if (rc_ != 0) return fail("no update kernel for this configuration");
       }
       {
         ProfScope ps(c, PK_DW2, s);
-        if (launch_dw(dw, H, OP, c->nchunks, s) != 0) return fail("no dW kernel for this configuration");
+        const int rc_ = c->use_upd2 ? launch_dw2(dw, OP, c->nchunks, s) : launch_dw(dw, H, OP, c->nchunks, s);
+        if (rc_ != 0) return fail("no dW kernel for this configuration");
       }
       float* st = c->mbstats + 8 * gi;
       cs.seg[stats_seg0 + 0] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_PG, st + ST_PG, c->sg[1].size, nblk, 1, 1.f / M};

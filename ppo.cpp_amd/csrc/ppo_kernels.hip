@@ -765,7 +765,8 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 
 template <int NO, int NI, int LDI, int WO, int WI, int NTH>
 PPO_DEV void dw_phase(const float* __restrict__ DZ, const float* __restrict__ IN, long m0, long m1,
-                      float* __restrict__ out, float* lds, int tid) {
+                      float* __restrict__ out, float* lds, int tid, const int32_t* __restrict__ perm = nullptr,
+                      int O = 0) {
   constexpr int TO = NO / 32, TI = (NI + 31) / 32;
   constexpr int TOW = TO / WO, TIW = (TI + WI - 1) / WI;
   constexpr int KS = 16;                       // rows per stage
@@ -796,7 +797,20 @@ PPO_DEV void dw_phase(const float* __restrict__ DZ, const float* __restrict__ IN
       } else if (c < NF4) {
         const int f2 = 4 * (c - NF4Z);
         const long row = mb + f2 / LDI;
-        if (row < m1) v = ld4(IN + row * LDI + f2 % LDI);
+        if (row < m1) {
+          if (perm) {  // IN = obs rows [.][O] through the permutation, zero padded to LDI
+            const int col = f2 % LDI;
+            const float* src = IN + (long)perm[row] * O + col;
+            if ((O & 3) == 0) {
+              if (col < O) v = ld4(src);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] = col + q < O ? src[q] : 0.f;
+            }
+          } else {
+            v = ld4(IN + row * LDI + f2 % LDI);
+          }
+        }
       }
       st[u] = v;
     }
@@ -869,7 +883,10 @@ __global__ __launch_bounds__(512) void k_dw(DwArgs a) {
   if (m0 < m1) {
     dw_phase<H, H, H, WO2, WI2, 512>(a.dz2[trunk], a.h1[trunk], m0, m1, out, lds, threadIdx.x);
     lds_barrier();
-    dw_phase<H, OP, OP, WO1, WI1, 512>(a.dz1[trunk], a.xn, m0, m1, out + H * H, lds, threadIdx.x);
+    if (a.perm)
+      dw_phase<H, OP, OP, WO1, WI1, 512>(a.dz1[trunk], a.obs, m0, m1, out + H * H, lds, threadIdx.x, a.perm, a.O);
+    else
+      dw_phase<H, OP, OP, WO1, WI1, 512>(a.dz1[trunk], a.xn, m0, m1, out + H * H, lds, threadIdx.x);
   }
 }
 

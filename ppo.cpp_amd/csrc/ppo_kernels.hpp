@@ -69,6 +69,9 @@ struct DwArgs {
   const float* h1[2];
   const float* dz1[2];
   const float* xn;
+  const int32_t* perm;  // non-null: dW1's input rows are gathered as obs[perm[m]] (O wide, zero padded to OP)
+  const float* obs;     //   instead of read from xn (k_upd2: no input normalisation, no Xn round trip)
+  int O;
   float* slab[2];     // [nchunks][H*H + H*OP] per trunk
   long slab_stride;
   int M;
@@ -159,6 +162,9 @@ int launch_fwdbwd(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s
 int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes);
 int upd_supported(const PackedLayout& K, int nh_actor, int sg_size, UpdGeoOut* g);
 int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s);
+int upd2_supported(const PackedLayout& K, UpdGeoOut* g);  // ppo_update_narrow.hip (H = 64 tanh agent)
+int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s);
+int launch_dw2(const DwArgs& a, int OP, int nchunks, hipStream_t s);  // both 64-wide trunks, rows gathered once
 int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s);
 size_t dw_lds_bytes(int H, int OP);
 void launch_colsum(const ColsumArgs& a, int nseg, long maxlen, hipStream_t s);

@@ -1,0 +1,828 @@
+// ppo_update_narrow.hip — k_upd2: the fused minibatch forward / PPO loss / backward of the PPO
+// agent (two 64-wide tanh trunks + Normal head, ppo:120-157; loss and backward ppo:495-538) with
+// BOTH trunks in one workgroup, for any observation width (cfg1 HalfCheetah O = 17, cfg2
+// Humanoid O = 376).
+//
+// Why a separate kernel: at H = 64 the work is dominated by layer 1 (K = O = 376 against N = 64),
+// and the wave-per-16-rows k_fwdbwd re-streams each trunk's 96 KB W1 per 64 rows through a
+// barrier per 16-column k-tile and then recomputes layer 1 for the backward. Here:
+//  * a workgroup (4 waves) owns 32 rows per tile; waves 0-1 are the critic, 2-3 the actor, and
+//    each wave owns 32 output features x 32 rows (2 x 2 accumulator tiles of 16x16x4 f32 MFMA),
+//    so every W1 A-operand load feeds 8 MFMAs;
+//  * the gathered observation rows are staged ONCE in LDS for both trunks, in 128-column chunks
+//    (double-buffered; the next chunk's gather is in flight under the current chunk's MFMAs, and
+//    the last chunk prefetches the next tile's first one);
+//  * tanh' needs only h1, which stays in registers: no layer-1 recompute;
+//  * bias / head-weight / logstd gradients and the loss statistics accumulate in registers over
+//    all of a workgroup's tiles and are reduced across lanes once, in a fixed order, at the end.
+// The dW1 / dW2 GEMMs stay in k_dw, which gathers the observation rows through the permutation
+// itself (no Xn round trip: the PPO agent has no input normalisation).
+#include "ppo_agent.hpp"
+#include "ppo_kernels.hpp"
+
+namespace {
+
+constexpr int H2 = 64, FT2 = 2, RT2 = 2, R2 = 32, LDA2 = H2 + 4;
+
+template <int NTO, int NHT, int VEC>
+struct Geo2 {
+  static constexpr int OP = NTO * 16;
+  static constexpr int CKB = NTO < 8 ? NTO : 8;      // k-blocks (16 columns) per staged X chunk
+  static constexpr int NCH = (NTO + CKB - 1) / CKB;  // chunks per tile
+  static constexpr int CW = CKB * 16;                // columns per chunk
+  static constexpr int LDX = CW + 4;                 // row stride = 4 mod 64 banks
+  static constexpr int NB = NCH > 1 ? 2 : 1;         // X chunk buffers
+  static constexpr int NHP = NHT * 16, LDG = NHP + 4;
+  static constexpr int PERROW = VEC == 4 ? CW / 4 : CW;  // gather items per row and chunk
+  static constexpr int NGI = (R2 * PERROW + 255) / 256;  // gather items per thread
+  static constexpr int NU = (R2 * NHP + 255) / 256;      // (row, action) items per thread (upper bound)
+  // LDS carve (floats); the (row, action) item and action regions follow at runtime offsets
+  static constexpr int oXS = 0;
+  static constexpr int oACT = oXS + NB * R2 * LDX;     // [2 trunks][R][LDA]: h1, then h2, then dz2
+  static constexpr int oSCR = oACT + 2 * R2 * LDA2;    // actor head partials [2][NHP][R] | critic [2][R]
+  static constexpr int oGG = oSCR + 2 * NHP * R2 + 2 * R2;  // [R][LDG] d loss / d mu
+  static constexpr int oROWS = oGG + R2 * LDG;          // [R][8] per-row scalars
+  static constexpr int oSP = oROWS + R2 * 8;            // head biases | sd | var | log sd (NHP each) | critic bias
+  static constexpr int oITM = oSP + 4 * NHP + 4;        // [R*A][4] items, then [R*A] actions
+};
+
+PPO_DEV float lf(const float* p) { return *p; }
+PPO_DEV f4 lf4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+PPO_DEV void sf4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+PPO_DEV float bl1(PBuf b, int lane_floats, int uni_floats) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b.r, lane_floats * 4, uni_floats * 4, 0));
+}
+
+// Column sums over the 16 rows j of a lane group: x[4 ft + r] (feature 16 ft + 4 g + r of this lane's
+// row) is reduce-scattered with DPP partners j ^ 8 (row_ror:8), the mirror in each half, the mirror in
+// each quad, then summed with j ^ 1: lane j returns slot s = j >> 1 summed over all 16 rows
+// (feature 16 (s >> 2) + 4 g + (s & 3)); lanes j and j ^ 1 hold the same value. Fixed order.
+template <int CTRL, int LEN, int MB>
+PPO_DEV void rs8_stage(float (&x)[8], int j) {
+  const bool bit = (j & MB) != 0;
+#pragma unroll
+  for (int i = 0; i < LEN / 2; ++i) {
+    const float lo = x[i], hi = x[i + LEN / 2];
+    const float keep = bit ? hi : lo, send = bit ? lo : hi;
+    x[i] = keep + dpp_f<CTRL>(send);
+  }
+}
+PPO_DEV float colsum8(float (&x)[8], int j) {
+  rs8_stage<kDppRowRor8, 8, 8>(x, j);
+  rs8_stage<kDppHalfMirror, 4, 4>(x, j);
+  rs8_stage<kDppQuadMirror, 2, 2>(x, j);
+  return x[0] + dpp_f<kDppQuadXor1>(x[0]);
+}
+
+// out[ft][rt] (+)= sum_k W[fbase + 16 ft + i][k] * IN[16 rt + j][k] for a 64-wide input in LDS
+PPO_DEV void mm64(f4 (&out)[FT2][RT2], PBuf wb, int wlane, int ldw, const float* in) {
+  f4 w[2][FT2];
+#pragma unroll
+  for (int ft = 0; ft < FT2; ++ft) w[0][ft] = pld4(wb, wlane, 16 * ft * ldw);
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    if (kb + 1 < 4) {
+#pragma unroll
+      for (int ft = 0; ft < FT2; ++ft) w[(kb + 1) & 1][ft] = pld4(wb, wlane, 16 * ft * ldw + 16 * (kb + 1));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f4 b[RT2];
+#pragma unroll
+    for (int rt = 0; rt < RT2; ++rt) b[rt] = lf4(in + 16 * rt * LDA2 + 16 * kb);
+#pragma unroll
+    for (int ft = 0; ft < FT2; ++ft)
+#pragma unroll
+      for (int rt = 0; rt < RT2; ++rt) {
+        out[ft][rt] = mfma16(w[kb & 1][ft].x, b[rt].x, out[ft][rt]);
+        out[ft][rt] = mfma16(w[kb & 1][ft].y, b[rt].y, out[ft][rt]);
+        out[ft][rt] = mfma16(w[kb & 1][ft].z, b[rt].z, out[ft][rt]);
+        out[ft][rt] = mfma16(w[kb & 1][ft].w, b[rt].w, out[ft][rt]);
+      }
+  }
+}
+
+}  // namespace
+
+template <int NTO, int NHT, int VEC>
+__global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
+  using GE = Geo2<NTO, NHT, VEC>;
+  constexpr int OP = GE::OP, CKB = GE::CKB, NCH = GE::NCH, CW = GE::CW, LDX = GE::LDX, NHP = GE::NHP;
+  constexpr int LDG = GE::LDG, PERROW = GE::PERROW, NGI = GE::NGI, NU = GE::NU;
+  constexpr int R = R2, FT = FT2, RT = RT2, LDA = LDA2, H = H2;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* XS = lds + GE::oXS;
+  float* SCR = lds + GE::oSCR;
+  float* GG = lds + GE::oGG;
+  float* ROWS = lds + GE::oROWS;
+  float* SHB = lds + GE::oSP;  // actor head biases
+  float* SSD = SHB + NHP;      // exp(logstd)
+  float* SVAR = SSD + NHP;     // sd^2
+  float* SLSD = SVAR + NHP;    // log(sd)
+  float* SCB = SLSD + NHP;     // critic head bias
+  float* ITM = lds + GE::oITM;
+  float* ACTN = lds + a.actn_off;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int trunk = wave >> 1, wf = wave & 1, fbase = 32 * wf;
+  const PackedLayout& K = a.K;
+  const TrunkDev& T = K.tr[trunk];
+  const float* __restrict__ P = a.P;
+  const PBuf pb = make_pbuf(P, K.size);
+  const PBuf w2t = make_pbuf(a.W2T[trunk], H * H);
+  const int O = K.O, A = K.A, M = a.M;
+  const float c = a.clip_coef;
+  const float adv_mean = a.adv_stats[0], adv_std = a.adv_stats[1];
+  float* ACT = lds + GE::oACT + trunk * R * LDA;
+
+  for (int i = tid; i < R * LDG; i += 256) GG[i] = 0.f;  // padding heads stay exactly 0
+  if (tid < NHP) {
+    const bool real = tid < A;
+    const float sd = real ? expf(P[K.logstd + tid]) : 1.f;
+    SHB[tid] = real ? P[K.ab3 + tid] : 0.f;
+    SSD[tid] = sd;
+    SVAR[tid] = sd * sd;
+    SLSD[tid] = logf(sd);
+  }
+  if (tid == 0) SCB[0] = P[K.cb3];
+
+  // per-lane A-operand offsets
+  const int w1lane = T.W1 + (fbase + j) * OP + 4 * g;
+  const int w2lane = T.W2 + (fbase + j) * H + 4 * g;
+  const int w2tlane = (fbase + j) * H + 4 * g;
+  const float* act_in = ACT + j * LDA + 4 * g;
+  // head operands (loaded per tile from L1/L2): actor forward A = W3[16 ht + j][fbase + 16 ft + 4 g + c],
+  // backward A = W3^T: W3[16 ht + 4 g + c][fbase + 16 ft + j]; critic w3[fbase + 16 ft + 4 g + c]
+  auto head_fwd = [&](int ht, int ft) -> f4 {
+    const int hf = 16 * ht + j;
+    return hf < A ? pld4(pb, K.aW3 + hf * H + fbase + 4 * g, 16 * ft) : f4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto head_bwd = [&](int ht, int ft) -> f4 {
+    f4 w;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int hb = 16 * ht + 4 * g + r;
+      w[r] = hb < A ? bl1(pb, K.aW3 + hb * H + fbase + j, 16 * ft) : 0.f;
+    }
+    return w;
+  };
+  const int ntiles = (M + R - 1) / R;
+
+  // ---- gather of the observation rows, chunk by chunk, through the permutation ----
+  int pcur[NGI], pnext[NGI];
+  f4 xv[NGI];  // VEC == 1: component x only
+  auto perms_of = [&](int itn, int (&pm)[NGI]) {
+#pragma unroll
+    for (int u = 0; u < NGI; ++u) {
+      const int idx = tid + 256 * u, row = idx / PERROW, m = itn * R + row;
+      pm[u] = (itn < ntiles && idx < R * PERROW && m < M) ? a.perm[m] : -1;
+    }
+  };
+  auto issue = [&](const int (&pm)[NGI], int ch) {
+#pragma unroll
+    for (int u = 0; u < NGI; ++u) {
+      const int idx = tid + 256 * u, row = idx / PERROW, q = idx - row * PERROW;
+      (void)row;
+      if constexpr (VEC == 4) {
+        const int col = ch * CW + 4 * q;
+        xv[u] = (pm[u] >= 0 && col < O) ? ld4(a.obs + (long)pm[u] * O + col) : f4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        const int col = ch * CW + q;
+        xv[u].x = (pm[u] >= 0 && col < O) ? a.obs[(long)pm[u] * O + col] : 0.f;
+      }
+    }
+  };
+  auto commit = [&](int ch) {
+    float* xs = XS + (ch & 1) * R * LDX;
+#pragma unroll
+    for (int u = 0; u < NGI; ++u) {
+      const int idx = tid + 256 * u, row = idx / PERROW, q = idx - row * PERROW;
+      if (idx < R * PERROW) {
+        if constexpr (VEC == 4) sf4(xs + row * LDX + 4 * q, xv[u]);
+        else xs[row * LDX + q] = xv[u].x;
+      }
+    }
+  };
+
+  // register accumulators over all of this workgroup's tiles
+  // column sums: one slot per lane (colsum8), feature fbase + 16 (s >> 2) + 4 g + (s & 3), s = j >> 1
+  float acc_b1 = 0.f, acc_b2 = 0.f, acc_hw = 0.f;
+  f4 d3acc[NHT][FT];  // actor dW3 tiles (rows already contracted)
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht) d3acc[ht][ft] = f4{0.f, 0.f, 0.f, 0.f};
+  float gacc[NU], lacc[NU];  // per (row, action) item: head-bias and logstd gradient sums
+#pragma unroll
+  for (int u = 0; u < NU; ++u) { gacc[u] = 0.f; lacc[u] = 0.f; }
+  float cbacc = 0.f;                        // critic head bias (tid < R)
+  float lst[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // pg, v, ent, old kl, kl, clipfrac (tid < R)
+
+  perms_of(blockIdx.x, pcur);
+  issue(pcur, 0);
+
+  for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
+    const int m0 = it * R;
+    perms_of(it + gridDim.x, pnext);
+    // per-row data of this tile (consumed after layer 1)
+    float rd[4] = {0.f, 0.f, 0.f, 0.f};
+    if (tid < R && m0 + tid < M) {
+      const long b = a.perm[m0 + tid];
+      rd[0] = a.ret[b]; rd[1] = a.val[b]; rd[2] = a.logp[b]; rd[3] = a.adv[b];
+    }
+    float av[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int idx = tid + 256 * u, row = idx / A, m = m0 + row;
+      av[u] = (idx < R * A && m < M) ? a.actions[(long)a.perm[m] * A + (idx - row * A)] : 0.f;
+    }
+
+    // ---------------- layer 1 (both trunks share the staged rows) ----------------
+    f4 z[FT][RT];
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      const f4 bv = pld4(pb, T.b1 + fbase + 4 * g, 16 * ft);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) z[ft][rt] = bv;
+    }
+    {
+      f4 w[2][FT];
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) w[0][ft] = pld4(pb, w1lane, 16 * ft * OP);
+#pragma unroll
+      for (int kb = 0; kb < NTO; ++kb) {
+        if (kb % CKB == 0) {
+          const int ch = kb / CKB;
+          commit(ch);
+          lds_barrier();
+          if (ch + 1 < NCH) issue(pcur, ch + 1);
+          else issue(pnext, 0);
+        }
+        if (kb + 1 < NTO) {
+#pragma unroll
+          for (int ft = 0; ft < FT; ++ft) w[(kb + 1) & 1][ft] = pld4(pb, w1lane, 16 * ft * OP + 16 * (kb + 1));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const float* xs = XS + ((kb / CKB) & 1) * R * LDX + j * LDX + 16 * (kb % CKB) + 4 * g;
+        f4 b[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) b[rt] = lf4(xs + 16 * rt * LDX);
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) {
+            z[ft][rt] = mfma16(w[kb & 1][ft].x, b[rt].x, z[ft][rt]);
+            z[ft][rt] = mfma16(w[kb & 1][ft].y, b[rt].y, z[ft][rt]);
+            z[ft][rt] = mfma16(w[kb & 1][ft].z, b[rt].z, z[ft][rt]);
+            z[ft][rt] = mfma16(w[kb & 1][ft].w, b[rt].w, z[ft][rt]);
+          }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NGI; ++u) pcur[u] = pnext[u];
+    // h1 = tanh(z1): kept in registers for the backward, stored for dW2 and as layer 2's input
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z[ft][rt][r] = tanhf(z[ft][rt][r]);
+        const int row = 16 * rt + j, m = m0 + row;
+        sf4(ACT + row * LDA + fbase + 16 * ft + 4 * g, z[ft][rt]);
+        if (m < M) st4(a.H1[trunk] + (size_t)m * H + fbase + 16 * ft + 4 * g, z[ft][rt]);
+      }
+    if (tid < R) {
+      ROWS[tid * 8 + 0] = rd[0]; ROWS[tid * 8 + 1] = rd[1]; ROWS[tid * 8 + 2] = rd[2]; ROWS[tid * 8 + 3] = rd[3];
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int idx = tid + 256 * u;
+      if (idx < R * A) ACTN[idx] = av[u];
+    }
+    lds_barrier();
+
+    // ---------------- layer 2 ----------------
+    f4 h2[FT][RT];
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      const f4 bv = pld4(pb, T.b2 + fbase + 4 * g, 16 * ft);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) h2[ft][rt] = bv;
+    }
+    mm64(h2, pb, w2lane, H, act_in);
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h2[ft][rt][r] = tanhf(h2[ft][rt][r]);
+    lds_barrier();  // every wave is done reading h1
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) sf4(ACT + (16 * rt + j) * LDA + fbase + 16 * ft + 4 * g, h2[ft][rt]);
+
+    // ---------------- heads: partial sums over this wave's 32 features ----------------
+    if (trunk == 0) {
+      f4 cw3[FT];
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) cw3[ft] = pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        float pv = 0.f;
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pv = fmaf(cw3[ft][r], h2[ft][rt][r], pv);
+        pv = row_allreduce(pv);
+        if (g == 0) SCR[2 * NHP * R + wf * R + 16 * rt + j] = pv;
+      }
+    } else {
+      f4 hp[NHT][RT];
+#pragma unroll
+      for (int ht = 0; ht < NHT; ++ht) {
+        f4 hw[FT];
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft) hw[ft] = head_fwd(ht, ft);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          hp[ht][rt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ft = 0; ft < FT; ++ft) {
+            hp[ht][rt] = mfma16(hw[ft].x, h2[ft][rt].x, hp[ht][rt]);
+            hp[ht][rt] = mfma16(hw[ft].y, h2[ft][rt].y, hp[ht][rt]);
+            hp[ht][rt] = mfma16(hw[ft].z, h2[ft][rt].z, hp[ht][rt]);
+            hp[ht][rt] = mfma16(hw[ft].w, h2[ft][rt].w, hp[ht][rt]);
+          }
+        }
+      }
+#pragma unroll
+      for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) SCR[(wf * NHP + 16 * ht + 4 * g + r) * R + 16 * rt + j] = hp[ht][rt][r];
+    }
+    lds_barrier();
+
+    // ---------------- loss, pass 1: per (row, action) Normal log-prob / entropy terms ----------------
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int idx = tid + 256 * u;
+      if (idx < R * A) {
+        const int row = idx / A, ai = idx - row * A;
+        const bool valid = m0 + row < M;
+        const float mu = (SCR[ai * R + row] + SCR[(NHP + ai) * R + row]) + SHB[ai];
+        const float var = SVAR[ai], lsd = SLSD[ai];
+        const float act = valid ? ACTN[idx] : mu;
+        const float d = act - mu;
+        float* it_ = ITM + 4 * idx;
+        it_[0] = -(d * d) / (2.0f * var) - lsd - kLz;
+        it_[1] = kEntC + lsd;
+        it_[2] = d / var;
+        it_[3] = d * d / var - 1.0f;
+      }
+    }
+    // critic rows: value loss and d loss / d value (ppo:515-527)
+    if (tid < R) {
+      const bool valid = m0 + tid < M;
+      const float v = (SCR[2 * NHP * R + tid] + SCR[2 * NHP * R + R + tid]) + SCB[0];
+      const float rt_ = ROWS[tid * 8 + 0], ov = ROWS[tid * 8 + 1];
+      float gv, sv;
+      if (a.clip_vloss) {
+        const float vu = (v - rt_) * (v - rt_);
+        const float dv = v - ov;
+        const float vcl = ov + fminf(fmaxf(dv, -c), c);
+        const float vc = (vcl - rt_) * (vcl - rt_);
+        sv = fmaxf(vu, vc);
+        const float w1 = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
+        const float inr = (dv >= -c && dv <= c) ? 1.0f : 0.0f;
+        gv = 0.5f * a.vf_coef * a.inv_m * (w1 * 2.0f * (v - rt_) + (1.0f - w1) * 2.0f * (vcl - rt_) * inr);
+      } else {
+        sv = (v - rt_) * (v - rt_);
+        gv = 0.5f * a.vf_coef * a.inv_m * 2.0f * (v - rt_);
+      }
+      if (!valid) { gv = 0.f; sv = 0.f; }
+      ROWS[tid * 8 + 6] = gv;
+      cbacc += gv;
+      lst[1] += sv;
+    }
+    lds_barrier();
+    // ---------------- loss, per row: clipped surrogate (ppo:497-513) ----------------
+    if (tid < R) {
+      const bool valid = m0 + tid < M;
+      float lp = 0.f, ent = 0.f;
+      for (int ai = 0; ai < A; ++ai) {
+        lp += ITM[4 * (tid * A + ai) + 0];
+        ent += ITM[4 * (tid * A + ai) + 1];
+      }
+      const float oldlp = valid ? ROWS[tid * 8 + 2] : lp;
+      const float logratio = lp - oldlp;
+      const float ratio = expf(logratio);
+      float an = valid ? ROWS[tid * 8 + 3] : 0.f;
+      if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
+      const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
+      const float pg1 = -an * ratio, pg2 = -an * rc;
+      const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+      const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
+      float g_logp = a.inv_m * (w1 * (-an) + (1.0f - w1) * (-an) * inr) * ratio;
+      float g_ent = -a.ent_coef * a.inv_m;
+      if (valid) {
+        lst[0] += fmaxf(pg1, pg2);
+        lst[2] += ent;
+        lst[3] += -logratio;
+        lst[4] += (ratio - 1.0f) - logratio;
+        lst[5] += fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
+      } else {
+        g_logp = 0.f;
+        g_ent = 0.f;
+      }
+      ROWS[tid * 8 + 4] = g_logp;
+      ROWS[tid * 8 + 5] = g_ent;
+    }
+    lds_barrier();
+    // ---------------- loss, pass 2: d loss / d mu and d loss / d logstd ----------------
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int idx = tid + 256 * u;
+      if (idx < R * A) {
+        const int row = idx / A, ai = idx - row * A;
+        const float g_logp = ROWS[row * 8 + 4], g_ent = ROWS[row * 8 + 5];
+        const float* it_ = ITM + 4 * idx;
+        const float gmu = g_logp * it_[2];
+        GG[row * LDG + ai] = gmu;
+        gacc[u] += gmu;
+        lacc[u] += g_logp * it_[3] + g_ent;
+      }
+    }
+    lds_barrier();
+
+    // ---------------- head backward: dh2, dW3 ----------------
+    f4 dh[FT][RT];
+    if (trunk == 0) {
+      float gr[RT], x[8];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) gr[rt] = lf(ROWS + (16 * rt + j) * 8 + 6);
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+        const f4 cw = pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float s = 0.f;
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) {
+            dh[ft][rt][r] = cw[r] * gr[rt];
+            s = fmaf(gr[rt], h2[ft][rt][r], s);
+          }
+          x[4 * ft + r] = s;
+        }
+      }
+      acc_hw += colsum8(x, j);
+    } else {
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) dh[ft][rt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ht = 0; ht < NHT; ++ht) {
+          const f4 hw = head_bwd(ht, ft);
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) {
+            const f4 gv = lf4(GG + (16 * rt + j) * LDG + 16 * ht + 4 * g);
+            dh[ft][rt] = mfma16(hw.x, gv.x, dh[ft][rt]);
+            dh[ft][rt] = mfma16(hw.y, gv.y, dh[ft][rt]);
+            dh[ft][rt] = mfma16(hw.z, gv.z, dh[ft][rt]);
+            dh[ft][rt] = mfma16(hw.w, gv.w, dh[ft][rt]);
+          }
+          // dW3 tile (heads 16 ht.., features fbase + 16 ft ..), contracted over the tile's rows
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * rt + 4 * g + r;
+              d3acc[ht][ft] = mfma16(lf(GG + row * LDG + 16 * ht + j), lf(ACT + row * LDA + fbase + 16 * ft + j),
+                                     d3acc[ht][ft]);
+            }
+        }
+      }
+    }
+    // dz2 = dh2 * (1 - h2^2)
+    {
+      float x[8];
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const f4 dz = dh[ft][rt] * (1.0f - h2[ft][rt] * h2[ft][rt]);
+          dh[ft][rt] = dz;
+          const int m = m0 + 16 * rt + j;
+          if (m < M) st4(a.DZ2[trunk] + (size_t)m * H + fbase + 16 * ft + 4 * g, dz);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[4 * ft + r] = dh[ft][0][r] + dh[ft][1][r];
+      }
+      acc_b2 += colsum8(x, j);
+    }
+    lds_barrier();  // the actor's dW3 readers of h2 are done
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) sf4(ACT + (16 * rt + j) * LDA + fbase + 16 * ft + 4 * g, dh[ft][rt]);
+    lds_barrier();
+
+    // ---------------- dh1 = W2^T dz2, dz1 = dh1 * (1 - h1^2) ----------------
+    f4 d1[FT][RT];
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) d1[ft][rt] = f4{0.f, 0.f, 0.f, 0.f};
+    mm64(d1, w2t, w2tlane, H, act_in);
+    {
+      float x[8];
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          d1[ft][rt] = d1[ft][rt] * (1.0f - z[ft][rt] * z[ft][rt]);
+          const int m = m0 + 16 * rt + j;
+          if (m < M) st4(a.DZ1[trunk] + (size_t)m * H + fbase + 16 * ft + 4 * g, d1[ft][rt]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[4 * ft + r] = d1[ft][0][r] + d1[ft][1][r];
+      }
+      acc_b1 += colsum8(x, j);
+    }
+  }
+
+  // ---------------- workgroup result: one slab row per trunk (fixed-order reductions) ----------------
+  const SmallGradLayout sg = a.sg[trunk];
+  float* out = a.slab[trunk] + (size_t)blockIdx.x * sg.size;
+  if ((j & 1) == 0) {
+    const int s = j >> 1, f = fbase + 16 * (s >> 2) + 4 * g + (s & 3);
+    out[sg.b1 + f] = acc_b1;
+    out[sg.b2 + f] = acc_b2;
+    if (trunk == 0) out[sg.hW + f] = acc_hw;
+  }
+  if (trunk == 1) {
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = 16 * ht + 4 * g + r;
+          if (h < A) out[sg.hW + h * H + fbase + 16 * ft + j] = d3acc[ht][ft][r];
+        }
+  }
+  // per-item head-bias / logstd sums -> LDS, then summed over rows per action in row order
+  lds_barrier();
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int idx = tid + 256 * u;
+    if (idx < R * A) {
+      ITM[2 * idx] = gacc[u];
+      ITM[2 * idx + 1] = lacc[u];
+    }
+  }
+  if (wave == 0) {
+#pragma unroll
+    for (int mm = 32; mm >= 1; mm >>= 1) {
+      cbacc += __shfl_xor(cbacc, mm, 64);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) lst[k] += __shfl_xor(lst[k], mm, 64);
+    }
+  }
+  lds_barrier();
+  if (tid < A) {
+    float s = 0.f, q = 0.f;
+    for (int row = 0; row < R; ++row) {
+      s += ITM[2 * (row * A + tid)];
+      q += ITM[2 * (row * A + tid) + 1];
+    }
+    float* o1 = a.slab[1] + (size_t)blockIdx.x * a.sg[1].size;
+    o1[a.sg[1].hb + tid] = s;
+    o1[a.sg[1].ls + tid] = q;
+  }
+  if (tid == 0) {
+    float* o0 = a.slab[0] + (size_t)blockIdx.x * a.sg[0].size;
+    float* o1 = a.slab[1] + (size_t)blockIdx.x * a.sg[1].size;
+    o0[a.sg[0].hb] = cbacc;
+    o0[a.sg[0].stats + ST_V] = lst[1];
+    o1[a.sg[1].stats + ST_PG] = lst[0];
+    o1[a.sg[1].stats + ST_ENT] = lst[2];
+    o1[a.sg[1].stats + ST_OKL] = lst[3];
+    o1[a.sg[1].stats + ST_KL] = lst[4];
+    o1[a.sg[1].stats + ST_CF] = lst[5];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+template <typename F>
+static int dispatch_upd2(const PackedLayout& K, F&& f) {
+  if (K.H != 64 || K.kind != PPO_NET_TANH_NORMAL || K.A > 32) return -1;
+  const int nto = K.OP / 16, nht = (K.A + 15) / 16, vec = (K.O % 4 == 0) ? 4 : 1;
+#define PPO_UPD2_CASE(NTO_, NHT_, VEC_)                                                              \
+  if (nto == NTO_ && nht == NHT_ && vec == VEC_)                                                     \
+    return f(std::integral_constant<int, NTO_>{}, std::integral_constant<int, NHT_>{},               \
+             std::integral_constant<int, VEC_>{});
+  PPO_UPD2_CASE(1, 1, 1) PPO_UPD2_CASE(2, 1, 1) PPO_UPD2_CASE(7, 1, 1) PPO_UPD2_CASE(24, 2, 4)
+  PPO_UPD2_CASE(2, 2, 1) PPO_UPD2_CASE(24, 2, 1) PPO_UPD2_CASE(1, 1, 4) PPO_UPD2_CASE(2, 1, 4)
+#undef PPO_UPD2_CASE
+  return -1;
+}
+
+int upd2_supported(const PackedLayout& K, UpdGeoOut* g) {
+  return dispatch_upd2(K, [&](auto NTO_, auto NHT_, auto VEC_) {
+    using GE = Geo2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value>;
+    int off = GE::oITM + 4 * R2 * K.A;
+    g->actn_off = off;
+    off += R2 * K.A;
+    g->acc_off = 0;
+    g->spar_off = 0;
+    g->lds_bytes = (size_t)off * sizeof(float);
+    g->rows = R2;
+    const auto k = k_upd2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value>;
+    return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) ==
+                   hipSuccess
+               ? 0
+               : -2;
+  });
+}
+
+int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s) {
+  return dispatch_upd2(a.K, [&](auto NTO_, auto NHT_, auto VEC_) {
+    hipLaunchKernelGGL((k_upd2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value>), dim3(nblocks),
+                       dim3(256), lds_bytes, s, a);
+    return 0;
+  });
+}
+
+// =============================================================================================
+// k_dw2 — the weight gradients of BOTH 64-wide trunks for one chunk of minibatch rows:
+//   dW1[t][o][i] = sum_m DZ1[t][m][o] * X[perm[m]][i]   (2 x 64 x OP; X gathered ONCE for both)
+//   dW2[t][o][i] = sum_m DZ2[t][m][o] * H1[t][m][i]     (2 x 64 x 64)
+// 8 waves, MFMA 32x32x2 f32. dW1 is one 128 x OP GEMM (o = 64 t + feature): wave (wo, wi) owns
+// o-tile wo and i-tiles [TIW wi, TIW wi + TIW); dW2 is 8 tiles of 32 x 32, one per wave. 32-row
+// stages go through one LDS buffer; the next stage's rows (and the permutation two stages ahead)
+// are in flight in registers under the current stage's MFMAs. Partials per chunk go to the slab
+// (k_colsum adds the chunks in a fixed order).
+// =============================================================================================
+typedef float f16v2 __attribute__((ext_vector_type(16)));
+
+template <int OP, int VEC>
+__global__ __launch_bounds__(512) void k_dw2(DwArgs a) {
+  constexpr int H = 64, KS = 32, NTH = 512;
+  constexpr int LDXS = OP + 4, LDZ = 2 * H + 4;
+  constexpr int TI = (OP + 31) / 32, TIW = (TI + 1) / 2;
+  constexpr int XPR = VEC == 4 ? OP / 4 : OP;             // X items per row
+  constexpr int NXI = (KS * XPR + NTH - 1) / NTH;         // X items per thread
+  constexpr int NZ = KS * 2 * H / 4;                      // f4 per 128-wide row block (DZ1 | DZ2 | H1)
+  constexpr int NZI = (NZ + NTH - 1) / NTH;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* XS = lds;
+  float* Z1 = XS + KS * LDXS;
+  float* Z2 = Z1 + KS * LDZ;
+  float* HH = Z2 + KS * LDZ;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hs = lane >> 5;
+  const long m0 = (long)blockIdx.x * a.rows_per_chunk;
+  const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
+  if (m0 >= m1) return;
+  const int nst = (int)((m1 - m0 + KS - 1) / KS);
+  const int O = a.O;
+  const int wo = wave & 3, wi = wave >> 2;                // dW1 tiles
+  const int t2 = wave >> 2, ot2 = (wave >> 1) & 1, it2 = wave & 1;  // dW2 tile
+
+  f16v2 acc1[TIW], acc2;
+#pragma unroll
+  for (int v = 0; v < TIW; ++v)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc1[v][r] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
+
+  int pr[NXI];     // permutation of the rows of the stage being loaded
+  int pn[NXI];     // ... of the stage after it
+  f4 xv[NXI];
+  f4 zv[3][NZI];   // DZ1 | DZ2 | H1 (both trunks)
+  auto perm_of = [&](int st, int (&p)[NXI]) {
+#pragma unroll
+    for (int u = 0; u < NXI; ++u) {
+      const int idx = tid + NTH * u, row = idx / XPR;
+      const long m = m0 + (long)st * KS + row;
+      p[u] = (st < nst && idx < KS * XPR && m < m1) ? a.perm[m] : -1;
+    }
+  };
+  auto load = [&](int st) {
+#pragma unroll
+    for (int u = 0; u < NXI; ++u) {
+      const int idx = tid + NTH * u, row = idx / XPR, q = idx - row * XPR;
+      (void)row;
+      if constexpr (VEC == 4) {
+        xv[u] = (pr[u] >= 0 && 4 * q < O) ? ld4(a.obs + (long)pr[u] * O + 4 * q) : f4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        xv[u].x = (pr[u] >= 0 && q < O) ? a.obs[(long)pr[u] * O + q] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NZI; ++u) {
+      const int c = tid + NTH * u, row = c / 32, q = c - row * 32, t = q >> 4, f = 4 * (q & 15);
+      const long m = m0 + (long)st * KS + row;
+      const bool ok = c < NZ && st < nst && m < m1;
+      zv[0][u] = ok ? ld4(a.dz1[t] + m * H + f) : f4{0.f, 0.f, 0.f, 0.f};
+      zv[1][u] = ok ? ld4(a.dz2[t] + m * H + f) : f4{0.f, 0.f, 0.f, 0.f};
+      zv[2][u] = ok ? ld4(a.h1[t] + m * H + f) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < NXI; ++u) {
+      const int idx = tid + NTH * u, row = idx / XPR, q = idx - row * XPR;
+      if (idx < KS * XPR) {
+        if constexpr (VEC == 4) *reinterpret_cast<f4*>(XS + row * LDXS + 4 * q) = xv[u];
+        else XS[row * LDXS + q] = xv[u].x;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NZI; ++u) {
+      const int c = tid + NTH * u, row = c / 32, q = c - row * 32;
+      if (c < NZ) {
+        const int o = row * LDZ + 4 * q;
+        *reinterpret_cast<f4*>(Z1 + o) = zv[0][u];
+        *reinterpret_cast<f4*>(Z2 + o) = zv[1][u];
+        *reinterpret_cast<f4*>(HH + o) = zv[2][u];
+      }
+    }
+  };
+
+  perm_of(0, pr);
+  perm_of(1, pn);
+  load(0);
+  store();
+  lds_barrier();
+#pragma unroll
+  for (int u = 0; u < NXI; ++u) pr[u] = pn[u];
+  perm_of(2, pn);
+  load(1);
+  for (int st = 0; st < nst; ++st) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll 4
+    for (int k = 0; k < KS; k += 2) {
+      const int row = k + hs;
+      const float av = Z1[row * LDZ + 32 * wo + l32];
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) {
+        const int col = 32 * (TIW * wi + v) + l32;
+        const float bv = col < OP ? XS[row * LDXS + col] : 0.f;
+        acc1[v] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc1[v], 0, 0, 0);
+      }
+      const float a2 = Z2[row * LDZ + 64 * t2 + 32 * ot2 + l32];
+      const float b2 = HH[row * LDZ + 64 * t2 + 32 * it2 + l32];
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a2, b2, acc2, 0, 0, 0);
+    }
+    lds_barrier();  // every wave is done with this stage
+    if (st + 1 < nst) {
+      store();
+#pragma unroll
+      for (int u = 0; u < NXI; ++u) pr[u] = pn[u];
+      perm_of(st + 3, pn);
+      lds_barrier();
+      if (st + 2 < nst) load(st + 2);
+    }
+  }
+  // ---- partials of this chunk ----
+#pragma unroll
+  for (int v = 0; v < TIW; ++v)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = 32 * wo + (r & 3) + 8 * (r >> 2) + 4 * hs, t = o >> 6;
+      const int i = 32 * (TIW * wi + v) + l32;
+      if (i < OP) a.slab[t][(size_t)blockIdx.x * a.slab_stride + H * H + (size_t)(o & 63) * OP + i] = acc1[v][r];
+    }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int o = 32 * ot2 + (r & 3) + 8 * (r >> 2) + 4 * hs, i = 32 * it2 + l32;
+    a.slab[t2][(size_t)blockIdx.x * a.slab_stride + o * H + i] = acc2[r];
+  }
+}
+
+size_t dw2_lds_bytes(int OP) { return (size_t)(32 * (OP + 4) + 3 * 32 * (2 * 64 + 4)) * sizeof(float); }
+
+template <int OP, int VEC>
+static int launch_dw2_t(const DwArgs& a, int nchunks, hipStream_t s) {
+  const size_t lds = dw2_lds_bytes(OP);
+  static const bool ok = hipFuncSetAttribute((const void*)k_dw2<OP, VEC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds) == hipSuccess;
+  if (!ok) return -2;
+  hipLaunchKernelGGL((k_dw2<OP, VEC>), dim3(nchunks), dim3(512), lds, s, a);
+  return 0;
+}
+
+int launch_dw2(const DwArgs& a, int OP, int nchunks, hipStream_t s) {
+  const bool v4 = (a.O % 4) == 0;
+  if (OP == 16) return v4 ? launch_dw2_t<16, 4>(a, nchunks, s) : launch_dw2_t<16, 1>(a, nchunks, s);
+  if (OP == 32) return v4 ? launch_dw2_t<32, 4>(a, nchunks, s) : launch_dw2_t<32, 1>(a, nchunks, s);
+  if (OP == 112) return v4 ? launch_dw2_t<112, 4>(a, nchunks, s) : launch_dw2_t<112, 1>(a, nchunks, s);
+  if (OP == 384) return v4 ? launch_dw2_t<384, 4>(a, nchunks, s) : launch_dw2_t<384, 1>(a, nchunks, s);
+  return -1;
+}

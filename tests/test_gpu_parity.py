@@ -366,17 +366,18 @@ def test_metric_config_iteration_properties_and_determinism():
     assert s0["grad_norm"] > 0
 
 
-@pytest.mark.parametrize("kind,O_,A,H", [(1, 17, 6, 256), (0, 17, 6, 256)])
+@pytest.mark.parametrize("kind,O_,A,H", [(1, 17, 6, 256), (0, 17, 6, 256), (0, 17, 6, 64), (0, 376, 17, 64),
+                                         (0, 11, 3, 64)])
 def test_update_kernels_agree(kind, O_, A, H, monkeypatch):
-    """The feature-split k_upd and the wave-per-16-rows k_fwdbwd compute the same minibatch
-    gradient (different summation orders only) at a size where every workgroup loops several
-    times (M = 12 800 rows, ragged last tile)."""
+    """The feature-split k_upd (H = 256) / the two-trunk k_upd2 (H = 64) and the wave-per-16-rows
+    k_fwdbwd compute the same minibatch gradient (different summation orders only) at a size where
+    every workgroup loops several times (M = 12 792 rows, ragged last tile)."""
     rng = np.random.default_rng(5)
     L = O.layout_init(kind, O_, A, H)
     p = random_params(L, rng)
     if kind == 0:
         p[L.logstd:L.logstd + A] = -0.5
-    E, T = 1600, 8
+    E, T = 1599, 8
     B = T * E
     x = rng.standard_normal((B, O_)).astype(np.float32)
     act = (rng.uniform(-0.95, 0.95, (B, A)) if kind else rng.standard_normal((B, A))).astype(np.float32)

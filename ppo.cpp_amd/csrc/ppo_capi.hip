@@ -169,6 +169,7 @@ struct ppo_ctx {
   void* host_user = nullptr;
   std::vector<float> host_stage;
   int world = 1, rank = 0;  // data-parallel group of the attached communicator (1 / cfg.rank without one)
+  int act_kernel = 0;  // 0: the fastest act kernel for the shape; 2 / 4: force k_act2 / k_act4 (PPO_ACT_KERNEL, A/B)
   int upd_trunk_mask = 3, upd_sched = 1;   // k_upd launch options (PPO_UPD_TRUNK: PPO_DIAG builds only)
   int dw_fused = 1;
   // profiling
@@ -280,6 +281,8 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   {  // kernel selection, read once (A/B switches of complete kernels; never read on a launch path)
     const char* es = getenv("PPO_UPD_SCHED");
     if (es && es[0] >= '0' && es[0] <= '3') c->upd_sched = es[0] - '0';
+    const char* ea = getenv("PPO_ACT_KERNEL");
+    if (ea && (ea[0] == '2' || ea[0] == '4')) c->act_kernel = ea[0] - '0';
     const char* ed = getenv("PPO_DW_FUSED");
     c->dw_fused = !(ed && ed[0] == '0');
 #ifdef PPO_DIAG
@@ -475,6 +478,7 @@ static ActArgs base_act(ppo_t* c) {
   a.rank = c->rank;
   a.store_step = -1;
   a.E = c->cfg.num_envs;
+  a.kernel = c->act_kernel;
   return a;
 }
 

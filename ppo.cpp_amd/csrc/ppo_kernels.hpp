@@ -32,6 +32,7 @@ struct ActArgs {
   int E;
   const float* next_done;
   float *s_obs, *s_actions, *s_logp, *s_dones, *s_values;
+  int kernel;  // 0: fastest for the shape; 2 / 4: force k_act2 / k_act4 (A/B comparisons)
 };
 
 struct UpdArgs {
@@ -158,6 +159,7 @@ int ppo_fail(const std::string& msg, int code);
 
 int launch_act(const ActArgs& a, hipStream_t s);
 int launch_act3(const ActArgs& a, hipStream_t s);
+int launch_act4(const ActArgs& a, hipStream_t s);  // ppo_act_narrow.hip (H = 64 tanh agent)
 int launch_fwdbwd(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s);
 int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes);
 int upd_supported(const PackedLayout& K, int nh_actor, int sg_size, UpdGeoOut* g);

@@ -170,11 +170,14 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
   // ---- gather of the observation rows, chunk by chunk, through the permutation ----
   int pcur[NGI], pnext[NGI];
   f4 xv[NGI];  // VEC == 1: component x only
+  // Every load below is unconditional (clamped address, value masked afterwards): a load under a
+  // per-lane branch gets its own s_waitcnt vmcnt(0) and serialises the gather.
   auto perms_of = [&](int itn, int (&pm)[NGI]) {
 #pragma unroll
     for (int u = 0; u < NGI; ++u) {
       const int idx = tid + 256 * u, row = idx / PERROW, m = itn * R + row;
-      pm[u] = (itn < ntiles && idx < R * PERROW && m < M) ? a.perm[m] : -1;
+      const int p = a.perm[min(m, M - 1)];
+      pm[u] = (itn < ntiles && idx < R * PERROW && m < M) ? p : -1;
     }
   };
   auto issue = [&](const int (&pm)[NGI], int ch) {
@@ -182,12 +185,15 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
     for (int u = 0; u < NGI; ++u) {
       const int idx = tid + 256 * u, row = idx / PERROW, q = idx - row * PERROW;
       (void)row;
+      const long b = (long)(pm[u] >= 0 ? pm[u] : 0) * O;
       if constexpr (VEC == 4) {
         const int col = ch * CW + 4 * q;
-        xv[u] = (pm[u] >= 0 && col < O) ? ld4(a.obs + (long)pm[u] * O + col) : f4{0.f, 0.f, 0.f, 0.f};
+        const f4 v = ld4(a.obs + b + min(col, O - 4));
+        xv[u] = (pm[u] >= 0 && col < O) ? v : f4{0.f, 0.f, 0.f, 0.f};
       } else {
         const int col = ch * CW + q;
-        xv[u].x = (pm[u] >= 0 && col < O) ? a.obs[(long)pm[u] * O + col] : 0.f;
+        const float v = a.obs[b + min(col, O - 1)];
+        xv[u].x = (pm[u] >= 0 && col < O) ? v : 0.f;
       }
     }
   };
@@ -225,15 +231,24 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
     perms_of(it + gridDim.x, pnext);
     // per-row data of this tile (consumed after layer 1)
     float rd[4] = {0.f, 0.f, 0.f, 0.f};
-    if (tid < R && m0 + tid < M) {
-      const long b = a.perm[m0 + tid];
+    if (wave == 0) {  // lanes >= R load a duplicate row (unconditional loads, see above)
+      const long b = a.perm[min(m0 + (tid & (R - 1)), M - 1)];
       rd[0] = a.ret[b]; rd[1] = a.val[b]; rd[2] = a.logp[b]; rd[3] = a.adv[b];
     }
     float av[NU];
+    {
+      int pa[NU];
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int idx = tid + 256 * u, row = idx / A, m = m0 + row;
-      av[u] = (idx < R * A && m < M) ? a.actions[(long)a.perm[m] * A + (idx - row * A)] : 0.f;
+      for (int u = 0; u < NU; ++u) {
+        const int idx = min(tid + 256 * u, R * A - 1), row = idx / A;
+        pa[u] = a.perm[min(m0 + row, M - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int idx = tid + 256 * u, ic = min(idx, R * A - 1), row = ic / A;
+        const float v = a.actions[(long)pa[u] * A + (ic - row * A)];
+        av[u] = (idx < R * A && m0 + row < M) ? v : 0.f;
+      }
     }
 
     // ---------------- layer 1 (both trunks share the staged rows) ----------------
@@ -663,7 +678,7 @@ int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s) 
 //   dW1[t][o][i] = sum_m DZ1[t][m][o] * X[perm[m]][i]   (2 x 64 x OP; X gathered ONCE for both)
 //   dW2[t][o][i] = sum_m DZ2[t][m][o] * H1[t][m][i]     (2 x 64 x 64)
 // 8 waves, MFMA 32x32x2 f32. dW1 is one 128 x OP GEMM (o = 64 t + feature): wave (wo, wi) owns
-// o-tile wo and i-tiles [TIW wi, TIW wi + TIW); dW2 is 8 tiles of 32 x 32, one per wave. 32-row
+// o-tile wo and i-tiles [TIW wi, TIW wi + TIW); dW2 is 8 tiles of 32 x 32, one per wave. 16-row
 // stages go through one LDS buffer; the next stage's rows (and the permutation two stages ahead)
 // are in flight in registers under the current stage's MFMAs. Partials per chunk go to the slab
 // (k_colsum adds the chunks in a fixed order).
@@ -672,7 +687,7 @@ typedef float f16v2 __attribute__((ext_vector_type(16)));
 
 template <int OP, int VEC>
 __global__ __launch_bounds__(512) void k_dw2(DwArgs a) {
-  constexpr int H = 64, KS = 32, NTH = 512;
+  constexpr int H = 64, KS = 16, NTH = 512;
   constexpr int LDXS = OP + 4, LDZ = 2 * H + 4;
   constexpr int TI = (OP + 31) / 32, TIW = (TI + 1) / 2;
   constexpr int XPR = VEC == 4 ? OP / 4 : OP;             // X items per row
@@ -705,33 +720,48 @@ __global__ __launch_bounds__(512) void k_dw2(DwArgs a) {
   int pn[NXI];     // ... of the stage after it
   f4 xv[NXI];
   f4 zv[3][NZI];   // DZ1 | DZ2 | H1 (both trunks)
+  // unconditional loads (clamped addresses, masked values): a per-lane branch around a load costs
+  // it its own s_waitcnt vmcnt(0)
   auto perm_of = [&](int st, int (&p)[NXI]) {
 #pragma unroll
     for (int u = 0; u < NXI; ++u) {
       const int idx = tid + NTH * u, row = idx / XPR;
       const long m = m0 + (long)st * KS + row;
-      p[u] = (st < nst && idx < KS * XPR && m < m1) ? a.perm[m] : -1;
+      const int v = a.perm[min(m, m1 - 1)];
+      p[u] = (st < nst && idx < KS * XPR && m < m1) ? v : -1;
     }
   };
+  const float* dz1[2] = {a.dz1[0], a.dz1[1]};
+  const float* dz2[2] = {a.dz2[0], a.dz2[1]};
+  const float* h1[2] = {a.h1[0], a.h1[1]};
   auto load = [&](int st) {
 #pragma unroll
     for (int u = 0; u < NXI; ++u) {
       const int idx = tid + NTH * u, row = idx / XPR, q = idx - row * XPR;
       (void)row;
+      const long b = (long)(pr[u] >= 0 ? pr[u] : 0) * O;
       if constexpr (VEC == 4) {
-        xv[u] = (pr[u] >= 0 && 4 * q < O) ? ld4(a.obs + (long)pr[u] * O + 4 * q) : f4{0.f, 0.f, 0.f, 0.f};
+        const f4 v = ld4(a.obs + b + min(4 * q, O - 4));
+        xv[u] = (pr[u] >= 0 && 4 * q < O) ? v : f4{0.f, 0.f, 0.f, 0.f};
       } else {
-        xv[u].x = (pr[u] >= 0 && q < O) ? a.obs[(long)pr[u] * O + q] : 0.f;
+        const float v = a.obs[b + min(q, O - 1)];
+        xv[u].x = (pr[u] >= 0 && q < O) ? v : 0.f;
       }
     }
 #pragma unroll
     for (int u = 0; u < NZI; ++u) {
-      const int c = tid + NTH * u, row = c / 32, q = c - row * 32, t = q >> 4, f = 4 * (q & 15);
+      const int c = tid + NTH * u, row = c / 32, q = c - row * 32, f = 4 * (q & 15);
+      const bool t = (q >> 4) != 0;
       const long m = m0 + (long)st * KS + row;
       const bool ok = c < NZ && st < nst && m < m1;
-      zv[0][u] = ok ? ld4(a.dz1[t] + m * H + f) : f4{0.f, 0.f, 0.f, 0.f};
-      zv[1][u] = ok ? ld4(a.dz2[t] + m * H + f) : f4{0.f, 0.f, 0.f, 0.f};
-      zv[2][u] = ok ? ld4(a.h1[t] + m * H + f) : f4{0.f, 0.f, 0.f, 0.f};
+      const long o = min(m, m1 - 1) * H + f;
+      const f4 v0 = ld4((t ? dz1[1] : dz1[0]) + o);
+      const f4 v1 = ld4((t ? dz2[1] : dz2[0]) + o);
+      const f4 v2 = ld4((t ? h1[1] : h1[0]) + o);
+      const f4 zz = f4{0.f, 0.f, 0.f, 0.f};
+      zv[0][u] = ok ? v0 : zz;
+      zv[1][u] = ok ? v1 : zz;
+      zv[2][u] = ok ? v2 : zz;
     }
   };
   auto store = [&]() {
@@ -766,19 +796,33 @@ __global__ __launch_bounds__(512) void k_dw2(DwArgs a) {
   load(1);
   for (int st = 0; st < nst; ++st) {
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll 4
-    for (int k = 0; k < KS; k += 2) {
+    // operands of k-step k + 2 are read while k-step k's MFMAs run
+    float opn[TIW + 3];
+    auto rd_ops = [&](int k, float (&o)[TIW + 3]) {
       const int row = k + hs;
-      const float av = Z1[row * LDZ + 32 * wo + l32];
+      o[0] = Z1[row * LDZ + 32 * wo + l32];
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) {
+        const int col = min(32 * (TIW * wi + v) + l32, OP + 3);  // cols >= OP read the zero pad / row end
+        o[1 + v] = XS[row * LDXS + col];
+      }
+      o[TIW + 1] = Z2[row * LDZ + 64 * t2 + 32 * ot2 + l32];
+      o[TIW + 2] = HH[row * LDZ + 64 * t2 + 32 * it2 + l32];
+    };
+    rd_ops(0, opn);
+#pragma unroll
+    for (int k = 0; k < KS; k += 2) {
+      float op[TIW + 3];
+#pragma unroll
+      for (int q = 0; q < TIW + 3; ++q) op[q] = opn[q];
+      if (k + 2 < KS) rd_ops(k + 2, opn);
 #pragma unroll
       for (int v = 0; v < TIW; ++v) {
         const int col = 32 * (TIW * wi + v) + l32;
-        const float bv = col < OP ? XS[row * LDXS + col] : 0.f;
-        acc1[v] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc1[v], 0, 0, 0);
+        acc1[v] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[0], col < OP ? op[1 + v] : 0.f, acc1[v], 0, 0, 0);
       }
-      const float a2 = Z2[row * LDZ + 64 * t2 + 32 * ot2 + l32];
-      const float b2 = HH[row * LDZ + 64 * t2 + 32 * it2 + l32];
-      acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a2, b2, acc2, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(op[TIW + 1], op[TIW + 2], acc2, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();  // every wave is done with this stage
     if (st + 1 < nst) {
@@ -806,7 +850,7 @@ __global__ __launch_bounds__(512) void k_dw2(DwArgs a) {
   }
 }
 
-size_t dw2_lds_bytes(int OP) { return (size_t)(32 * (OP + 4) + 3 * 32 * (2 * 64 + 4)) * sizeof(float); }
+size_t dw2_lds_bytes(int OP) { return (size_t)(16 * (OP + 4) + 3 * 16 * (2 * 64 + 4)) * sizeof(float); }
 
 template <int OP, int VEC>
 static int launch_dw2_t(const DwArgs& a, int nchunks, hipStream_t s) {

@@ -318,6 +318,10 @@ def test_full_iteration_vs_oracle(kind):
     gpu_p = tr.agent.params()
     gpu_obs = tr.agent.buffer(ppo_amd.BUF_OBS, (T, E, O_)).numpy()
     gpu_adv = tr.agent.buffer(ppo_amd.BUF_ADVANTAGES, (T, E)).numpy()
+    gb = {k: tr.agent.buffer(b, (T, E)).numpy() for k, b in (("logp", ppo_amd.BUF_LOGPROBS),
+                                                              ("ret", ppo_amd.BUF_RETURNS),
+                                                              ("val", ppo_amd.BUF_VALUES))}
+    gpu_act = tr.agent.buffer(ppo_amd.BUF_ACTIONS, (T, E, A)).numpy()
     # oracle replay
     oenv = O.SynthEnv(E, O_, A)
     nobs = oenv.reset(cfg.seed)
@@ -338,9 +342,13 @@ def test_full_iteration_vs_oracle(kind):
     np.testing.assert_allclose(gpu_adv, adv, rtol=1e-3, atol=1e-3)
     lcfg = O.LossCfg(clip, 0.01, 0.5, 1, 1)
     lr = float(np.float32(1.0) * np.float32(cfg.learning_rate))
-    op, _, _, _, _ = O.update(L, p, np.zeros(L.P), np.zeros(L.P), 0, bo.reshape(-1, O_), ba.reshape(-1, A),
-                              bl.reshape(-1), adv.reshape(-1), ret.reshape(-1), bv.reshape(-1), EP, MB, lr, 0.5, 1e-5,
-                              lcfg, seed=cfg.seed, rank=0, epoch_counter0=0)
+    np.testing.assert_allclose(gpu_act, ba, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(gb["logp"], bl, rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(gb["ret"], ret, rtol=1e-3, atol=1e-3)
+    op, _, _, _, _ = O.update(L, p, np.zeros(L.P), np.zeros(L.P), 0, gpu_obs.reshape(-1, O_), gpu_act.reshape(-1, A),
+                              gb["logp"].reshape(-1), gpu_adv.reshape(-1), gb["ret"].reshape(-1),
+                              gb["val"].reshape(-1), EP, MB, lr, 0.5, 1e-5, lcfg, seed=cfg.seed, rank=0,
+                              epoch_counter0=0)
     np.testing.assert_allclose(gpu_p, op, rtol=0, atol=2e-5)
 
 
@@ -405,6 +413,34 @@ def test_update_kernels_agree(kind, O_, A, H, monkeypatch):
     np.testing.assert_allclose(stats[1], stats[0], rtol=2e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("O_,A,n", [(376, 17, 1000), (17, 6, 777), (11, 3, 5)])
+def test_act_kernels_agree(O_, A, n, monkeypatch):
+    """The K-split two-trunk k_act4 and the feature-split k_act2 (64-wide tanh agent) give the same
+    forward (summation order only) and, through the shared Philox contract, the same samples."""
+    rng = np.random.default_rng(9)
+    L = O.layout_init(0, O_, A, 64)
+    p = random_params(L, rng)
+    p[L.logstd:L.logstd + A] = -0.5
+    x = rng.standard_normal((n, O_)).astype(np.float32)
+    given = rng.standard_normal((n, A)).astype(np.float32)
+    outs = []
+    for env in ("2", "4"):
+        monkeypatch.setenv("PPO_ACT_KERNEL", env)
+        ag = make_agent(0, O_, A, 64, n)
+        ag.load_params(p)
+        xd = DeviceArray.from_numpy(x)
+        res = []
+        for mode, ain in ((ppo_amd.PPO_SAMPLE, None), (ppo_amd.PPO_MEAN, None),
+                          (ppo_amd.PPO_GIVEN, DeviceArray.from_numpy(given))):
+            act, lp, ent, v = ag.get_action_and_value(xd, mode, ain, env_base=3, step_id=11)
+            res.append([t.numpy() for t in (act, lp, ent, v)])
+        outs.append(res)
+        ag.close()
+    for r2, r4 in zip(*outs):
+        for t2, t4 in zip(r2, r4):
+            np.testing.assert_allclose(t4, t2, rtol=1e-5, atol=2e-5)
+
+
 @pytest.mark.parametrize("kind,O_,A,H", [(1, 17, 6, 256), (0, 17, 6, 256), (1, 9, 3, 256)])
 def test_fused_dw_matches_two_phase_dw(kind, O_, A, H, monkeypatch):
     """k_dwf (dW2 and dW1 in one pass over the rows) and the two-phase k_dw run the same MFMA
@@ -441,8 +477,11 @@ def test_cfg1_shape_iteration_vs_oracle():
     """BASELINE cfg1's shape (ppo_continuous_action defaults, ppo:57-66: num_envs=1, num_steps=2048,
     32 minibatches of 64 rows, 10 epochs): one full iteration -- 2048 batch-1 rollout acts on the
     device env, GAE over T=2048 for one env, 320 optimizer steps -- against the oracle doing the
-    same with the same Philox counters and Feistel permutations. 320 chained Adam steps let fp32
-    rounding differences grow, hence atol 1e-4 on the parameters (lr 3e-4 per step)."""
+    same with the same Philox counters and Feistel permutations. The rollout is checked against
+    the oracle's rollout; the update against the oracle's update of the GPU's own rollout buffers
+    (identical inputs: 2048 env steps would otherwise feed ulp-level action differences into 320
+    chained Adam steps). The Adam chain still lets fp32 rounding differences grow, hence atol 1e-4
+    on the parameters (lr 3e-4 per step)."""
     E, T, MB, EP = 1, 2048, 32, 10
     O_, A, H = 17, 6, 64
     rng = np.random.default_rng(23)
@@ -456,6 +495,10 @@ def test_cfg1_shape_iteration_vs_oracle():
     gpu_p = tr.agent.params()
     gpu_obs = tr.agent.buffer(ppo_amd.BUF_OBS, (T, E, O_)).numpy()
     gpu_adv = tr.agent.buffer(ppo_amd.BUF_ADVANTAGES, (T, E)).numpy()
+    gb = {k: tr.agent.buffer(b, (T, E)).numpy() for k, b in (("logp", ppo_amd.BUF_LOGPROBS),
+                                                              ("ret", ppo_amd.BUF_RETURNS),
+                                                              ("val", ppo_amd.BUF_VALUES))}
+    gpu_act = tr.agent.buffer(ppo_amd.BUF_ACTIONS, (T, E, A)).numpy()
     oenv = O.SynthEnv(E, O_, A)
     nobs = oenv.reset(cfg.seed)
     ndone = np.zeros(E, np.float32)
@@ -476,9 +519,13 @@ def test_cfg1_shape_iteration_vs_oracle():
     np.testing.assert_allclose(gpu_adv, adv, rtol=1e-3, atol=1e-3)
     lcfg = O.LossCfg(0.2, 0.0, 0.5, 1, 1)
     lr = float(np.float32(cfg.learning_rate))
-    op, _, _, _, _ = O.update(L, p, np.zeros(L.P), np.zeros(L.P), 0, bo.reshape(-1, O_), ba.reshape(-1, A),
-                              bl.reshape(-1), adv.reshape(-1), ret.reshape(-1), bv.reshape(-1), EP, MB, lr, 0.5, 1e-5,
-                              lcfg, seed=cfg.seed, rank=0, epoch_counter0=0)
+    np.testing.assert_allclose(gpu_act, ba, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(gb["logp"], bl, rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(gb["ret"], ret, rtol=1e-3, atol=1e-3)
+    op, _, _, _, _ = O.update(L, p, np.zeros(L.P), np.zeros(L.P), 0, gpu_obs.reshape(-1, O_), gpu_act.reshape(-1, A),
+                              gb["logp"].reshape(-1), gpu_adv.reshape(-1), gb["ret"].reshape(-1),
+                              gb["val"].reshape(-1), EP, MB, lr, 0.5, 1e-5, lcfg, seed=cfg.seed, rank=0,
+                              epoch_counter0=0)
     np.testing.assert_allclose(gpu_p, op, rtol=0, atol=1e-4)
     assert np.abs(gpu_p - p).max() > 1e-3  # 320 steps actually moved the parameters
     tr.close()

@@ -145,6 +145,10 @@ PPO_DEV void act_activate(f4 (&acc)[2][RT], const float* sp_g, const float* sp_b
   }
 }
 
+PPO_DEV float bld1f(PBuf b, int off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b.r, off * 4, 0, 0));
+}
+
 PPO_DEV int act_head_row(const PackedLayout& K, int trunk, int h) {
   if (trunk == 0) return h == 0 ? K.cW3 : -1;
   if (K.kind == PPO_NET_LN_BETA) {
@@ -192,12 +196,16 @@ __global__ __launch_bounds__(512) void k_act3(ActArgs a) {
   const int nh = trunk == 0 ? 1 : (KIND == PPO_NET_LN_BETA ? 2 * A : A);
 
   // ---- kernel start: issue every independent load (inputs, W1 ring, staged params) ----
+  // Branch-free: clamped addresses with the value masked afterwards, or buffer loads whose
+  // offset is past the descriptor's end (they return 0). A load under a per-lane branch gets its
+  // own s_waitcnt vmcnt(0), which serialises the prologue into several memory round trips.
   constexpr int NX = (R * OP + kActThreads - 1) / kActThreads;
   float xv[NX];
 #pragma unroll
   for (int k = 0; k < NX; ++k) {
     const int idx = tid + kActThreads * k, r = idx / OP, f = idx - r * OP, row = row0 + r;
-    xv[k] = (idx < R * OP && row < a.n && f < O) ? a.x[(size_t)row * a.ldx + f] : 0.0f;
+    const float v = a.x[(size_t)min(row, a.n - 1) * a.ldx + min(f, O - 1)];
+    xv[k] = (idx < R * OP && row < a.n && f < O) ? v : 0.0f;
   }
   constexpr int NSP4 = GE::NSP / 4;
   constexpr int NSPT = (NSP4 + kActThreads - 1) / kActThreads;
@@ -207,7 +215,8 @@ __global__ __launch_bounds__(512) void k_act3(ActArgs a) {
     const int q = tid + kActThreads * k;  // f4 index into SP
     f4 v = f4{0.f, 0.f, 0.f, 0.f};
     if (q < NSP4) {
-      const int fl = 4 * q, vec = fl / H, off = fl - vec * H;
+      // q / 64 is the wave index plus 8 k: wave-uniform, so the source selection is scalar
+      const int fl = 4 * q, vec = __builtin_amdgcn_readfirstlane(fl / H), off = fl - vec * H;
       int src = -1;
       if (vec < 6) {
         const int base = vec == 0 ? T.b1 : vec == 1 ? T.g1 : vec == 2 ? T.be1 : vec == 3 ? T.b2 : vec == 4 ? T.g2 : T.be2;
@@ -216,19 +225,42 @@ __global__ __launch_bounds__(512) void k_act3(ActArgs a) {
         const int hr = act_head_row(K, trunk, vec - 6);
         src = hr >= 0 ? hr + off : -1;
       }
-      if (src >= 0) v = pld4(pb, src, 0);
+      v = pld4(pb, src >= 0 ? src : K.size, 0);  // past the end: 0
     }
     spv[k] = v;
   }
-  float hbias = 0.f;
-  if (tid < NHP) {
-    const int bo = act_head_bias(K, trunk, tid);
-    hbias = bo >= 0 ? P[bo] : 0.f;
+  const int hbo = tid < NHP ? act_head_bias(K, trunk, tid) : -1;
+  const float hbias = bld1f(pb, hbo >= 0 ? hbo : K.size);
+  float ndone = 0.f;  // the critic stores next_done with the value (rollout)
+  if (trunk == 0 && a.store_step >= 0 && a.next_done) ndone = a.next_done[min(row0 + (tid & (R - 1)), a.n - 1)];
+  // the sampling draws of this thread's first distribution item do not depend on the network:
+  // computed here, under the weight fetch (Beta: Marsaglia-Tsang attempt 0; Normal: the z pair)
+  const SampleKey key = sample_key(a.seed, a.rank);
+  GammaDraw gd0 = GammaDraw{0.f, 0.f};
+  float nz0 = 0.f;
+  if (trunk == 1 && a.mode == PPO_SAMPLE) {
+    if constexpr (KIND == PPO_NET_LN_BETA) {
+      if (tid < R * A * 2) {
+        const int which = tid & 1, ra = tid >> 1, r = ra / A, ai = ra - r * A;
+        gd0 = gamma_draw(key, a.env_base + row0 + r, a.step_id, 0x10000u + (uint32_t)(ai * 2 + which) * 64u);
+      }
+    } else {
+      if (tid < R * A) {
+        const int r = tid / A, ai = tid - r * A;
+        uint32_t rr[4];
+        philox_draw(key, a.env_base + row0 + r, a.step_id, (uint32_t)(ai >> 1), rr);
+        float z0, z1;
+        box_muller(rr[0], rr[1], z0, z1);
+        nz0 = (ai & 1) ? z1 : z0;
+      }
+    }
   }
-  // ---- inputs -> LDS (normalized for the LN agent) ----
+  // ---- inputs -> LDS (normalized for the LN agent); the raw rows into the rollout storage ----
 #pragma unroll
   for (int k = 0; k < NX; ++k) {
     const int idx = tid + kActThreads * k, r = idx / OP, f = idx - r * OP;
+    if (trunk == 0 && a.store_step >= 0 && idx < R * OP && row0 + r < a.n && f < O)
+      a.s_obs[((long)a.store_step * a.E + a.env_base + row0 + r) * O + f] = xv[k];
     if (idx < R * OP) {
       float v = xv[k];
       if constexpr (KIND == PPO_NET_LN_BETA)
@@ -270,8 +302,16 @@ __global__ __launch_bounds__(512) void k_act3(ActArgs a) {
     for (int rt = 0; rt < RT; ++rt) acc[u][rt] = bv;
   }
   const float* hin = HB + j * LDH + 4 * g;
+#ifdef PPO_STAMPS
+  // diagnostic build only: a.kernel bit 8 skips layer 2 (h2 := h1), bit 9 the layer-2 LayerNorm
+  const int diag = a.kernel >> 8;
+  if (!(diag & 1))
+#endif
   act_layer<16, 8, H, RT>(acc, pb, T.W2 + (32 * wave + j) * H + 4 * g,
                           [&](int t, int rt) { return *reinterpret_cast<const f4*>(hin + 16 * rt * LDH + 16 * t); });
+#ifdef PPO_STAMPS
+  if (!(diag & 2))
+#endif
   act_activate<KIND, RT>(acc, SP + GE::sG2, SP + GE::sBE2, RED, wave, j, g);
   // ---- heads: split-K partials over this wave's 32 features ----
 #pragma unroll
@@ -314,21 +354,23 @@ __global__ __launch_bounds__(512) void k_act3(ActArgs a) {
         if (a.store_step >= 0) {
           const long srow = (long)a.store_step * a.E + a.env_base + row;
           a.s_values[srow] = v;
-          a.s_dones[srow] = a.next_done ? a.next_done[row] : 0.0f;
+          a.s_dones[srow] = ndone;
         }
-      }
-    }
-    if (a.store_step >= 0) {
-      for (int idx = tid; idx < R * O; idx += kActThreads) {
-        const int r = idx / O, f = idx - r * O, row = row0 + r;
-        if (row < a.n) a.s_obs[((long)a.store_step * a.E + a.env_base + row) * O + f] = a.x[(size_t)row * a.ldx + f];
       }
     }
     return;
   }
 
   // ---- actor distribution ----
-  const SampleKey key = sample_key(a.seed, a.rank);
+#ifdef PPO_STAMPS
+  if (diag & 4) {  // diagnostic: skip the distribution, write the head pre-activations
+    if (tid < R * A) {
+      const int r = tid / A, ai = tid - r * A;
+      if (row0 + r < a.n && a.action_out) a.action_out[(size_t)(row0 + r) * A + ai] = PRE[r * LDP + ai];
+    }
+    return;
+  }
+#endif
   if constexpr (KIND == PPO_NET_LN_BETA) {
     // stage 1: one (row, action, alpha|beta) item per thread
     for (int idx = tid; idx < R * A * 2; idx += kActThreads) {
@@ -336,7 +378,10 @@ __global__ __launch_bounds__(512) void k_act3(ActArgs a) {
       const long env = a.env_base + row0 + r;
       const float c = softplusf_(PRE[r * LDP + ai + which * A]) + 1.0f;
       float gs = 0.f;
-      if (a.mode == PPO_SAMPLE) gs = gamma_mt(c, key, env, a.step_id, 0x10000u + (uint32_t)(ai * 2 + which) * 64u);
+      if (a.mode == PPO_SAMPLE) {
+        const uint32_t db = 0x10000u + (uint32_t)(ai * 2 + which) * 64u;
+        gs = idx == tid ? gamma_mt_d0(c, gd0, key, env, a.step_id, db) : gamma_mt(c, key, env, a.step_id, db);
+      }
       float* it = ITM + ((r * A + ai) * 2 + which) * 4;
       it[0] = c;
       it[1] = gs;
@@ -391,11 +436,15 @@ __global__ __launch_bounds__(512) void k_act3(ActArgs a) {
       } else if (a.mode == PPO_MEAN) {
         act = mu;
       } else {
-        uint32_t rr[4];
-        philox_draw(key, env, a.step_id, (uint32_t)(ai >> 1), rr);
-        float z0, z1;
-        box_muller(rr[0], rr[1], z0, z1);
-        act = mu + ((ai & 1) ? z1 : z0) * sd;
+        float z = nz0;
+        if (idx != tid) {
+          uint32_t rr[4];
+          philox_draw(key, env, a.step_id, (uint32_t)(ai >> 1), rr);
+          float z0, z1;
+          box_muller(rr[0], rr[1], z0, z1);
+          z = (ai & 1) ? z1 : z0;
+        }
+        act = mu + z * sd;
       }
       const float d = act - mu;
       LPE[idx * 2 + 0] = -(d * d) / (2.0f * var) - lsd - kLz;

@@ -5,43 +5,43 @@
 // A rollout launch is one pass over E rows with cold weights, so its time is the critical path of
 // dependent memory round trips, not MFMA work. k_act2 (one trunk per workgroup, waves split the
 // output features) streams the 376-wide W1 k-block by k-block: 24 dependent L2/MALL fetches.
-// Here both trunks share a 512-thread workgroup of 16 rows, layer 1 is split over K (wave
-// (trunk, ks) owns k-blocks [ks NKW, ks NKW + NKW) for all 64 outputs), and EVERY operand the wave
-// needs — its input columns, its W1 slice, its W2 rows, head rows, biases and the per-item
-// parameters — is requested at kernel start, so the launch costs about one round trip plus
-// ~100 MFMAs per wave. Partial sums meet in LDS in a fixed order. Sampling uses the Philox
-// contract of k_act2 (same counters), so samples match it for any batching.
+// Here a 256-thread workgroup owns 16 rows of ONE trunk (the launch time is set by the weight bytes
+// each CU must pull in, so the trunks go to different CUs), layer 1 is split over K (wave ks owns
+// k-blocks [ks NKW, ks NKW + NKW) for all 64 outputs), and EVERY operand the wave needs — its input
+// columns, its W1 slice, its W2 rows, head rows, biases and the per-item parameters and Normal
+// draws — is requested at kernel start, so the launch costs about one round trip plus ~100 MFMAs
+// per wave. Partial sums meet in LDS in a fixed order. Sampling uses the Philox contract of k_act2
+// (same counters), so samples match it for any batching.
 #include "ppo_agent.hpp"
 #include "ppo_kernels.hpp"
 
 namespace {
-constexpr int kA4Threads = 512, kA4Rows = 16, kA4H = 64, kA4LDP = kA4Rows + 1, kA4LDH = kA4H + 4;
+constexpr int kA4Threads = 256, kA4Rows = 16, kA4H = 64, kA4LDP = kA4Rows + 1, kA4LDH = kA4H + 4;
 }
 
 template <int NTO, int NHT>
-__global__ __launch_bounds__(512) void k_act4(ActArgs a) {
+__global__ __launch_bounds__(256) void k_act4(ActArgs a) {
   constexpr int H = kA4H, R = kA4Rows, OP = NTO * 16, NKW = (NTO + 3) / 4, NHP = NHT * 16;
   constexpr int LDP = kA4LDP, LDH = kA4LDH;
-  __shared__ float P1[2][4][H][LDP];       // layer-1 partials per (trunk, k-slice)
-  __shared__ __attribute__((aligned(16))) float H1[2][R][LDH];
+  __shared__ float P1[4][H][LDP];          // layer-1 partials per k-slice
+  __shared__ __attribute__((aligned(16))) float H1[R][LDH];
   __shared__ float HP[4][NHP][LDP];        // actor head partials per k-slice (feature quarter)
   __shared__ float VP[4][R];               // critic head partials
   __shared__ float ITM[R * NHP][2];        // per (row, action): log-prob / entropy terms
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
-  const int trunk = wave >> 2, ks = wave & 3;
+  const int trunk = blockIdx.y, ks = wave;
   const PackedLayout& K = a.K;
   const TrunkDev& T = K.tr[trunk];
   const float* __restrict__ P = a.P;
   const PBuf pb = make_pbuf(P, K.size);
   const int row0 = blockIdx.x * R, O = K.O, A = K.A;
   const int row = row0 + j, rowc = min(row, a.n - 1);
-  const bool active = trunk == 0 || a.need_actor;  // wave-uniform
   const int kb0 = ks * NKW;
 
   // ---------------- kernel start: every independent load ----------------
   f4 xv[NKW], wa[NKW][4], w2v[4];
   f4 b1 = f4{0.f, 0.f, 0.f, 0.f}, b2 = b1, hv = b1, hw[NHT];
-  if (active) {
+  {
 #pragma unroll
     for (int q = 0; q < NKW; ++q) {
       const int kb = kb0 + q;
@@ -67,22 +67,48 @@ __global__ __launch_bounds__(512) void k_act4(ActArgs a) {
       hw[ht] = (trunk == 1 && h < A) ? w : f4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  // per-item parameters (item = tid: row tid / A, action tid % A)
-  const bool item = a.need_actor && tid < R * A;
-  const int ir = min(tid, R * A - 1) / A, ia = min(tid, R * A - 1) - ir * A, irow = row0 + ir;
-  float i_b3 = 0.f, i_lstd = 0.f, i_act = 0.f, c_b3 = 0.f, c_done = 0.f;
-  if (item) {
-    i_b3 = P[K.ab3 + ia];
-    i_lstd = P[K.logstd + ia];
-    if (a.mode == PPO_GIVEN) i_act = a.action_in[(size_t)min(irow, a.n - 1) * A + ia];
+  // the rollout keeps the observation the action was taken on: the critic's waves hold every
+  // (row, column) of the tile once between them, stored as soon as it arrives
+  if (trunk == 0 && a.store_step >= 0 && row < a.n) {
+    float* so = a.s_obs + ((long)a.store_step * a.E + a.env_base + row) * O;
+#pragma unroll
+    for (int q = 0; q < NKW; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int col = 16 * (kb0 + q) + 4 * g + c;
+        if (kb0 + q < NTO && col < O) so[col] = xv[q][c];
+      }
   }
-  if (tid < R) {
+  // per-item parameters (item tid + 256 u: row / A, action % A) and the Normal draws, which do not
+  // depend on the network: all fetched / computed here, under the weight fetch
+  constexpr int NI = (R * NHP + kA4Threads - 1) / kA4Threads;
+  float i_b3[NI], i_lstd[NI], i_act[NI], nz[NI];
+  float c_b3 = 0.f, c_done = 0.f;
+  const SampleKey key = sample_key(a.seed, a.rank);
+#pragma unroll
+  for (int u = 0; u < NI; ++u) {
+    const int idx = min(tid + kA4Threads * u, R * A - 1), ir = idx / A, ia = idx - ir * A, irow = row0 + ir;
+    i_b3[u] = 0.f; i_lstd[u] = 0.f; i_act[u] = 0.f; nz[u] = 0.f;
+    if (trunk == 1) {
+      i_b3[u] = P[K.ab3 + ia];
+      i_lstd[u] = P[K.logstd + ia];
+      if (a.mode == PPO_GIVEN) i_act[u] = a.action_in[(size_t)min(irow, a.n - 1) * A + ia];
+      if (a.mode == PPO_SAMPLE) {
+        uint32_t rr[4];
+        philox_draw(key, a.env_base + irow, a.step_id, (uint32_t)(ia >> 1), rr);
+        float z0, z1;
+        box_muller(rr[0], rr[1], z0, z1);
+        nz[u] = (ia & 1) ? z1 : z0;
+      }
+    }
+  }
+  if (trunk == 0 && tid < R) {
     c_b3 = P[K.cb3];
     if (a.next_done) c_done = a.next_done[min(row0 + tid, a.n - 1)];
   }
 
   // ---------------- layer 1: partial products over this wave's k-blocks ----------------
-  if (active) {
+  {
     f4 acc[4];
 #pragma unroll
     for (int ft = 0; ft < 4; ++ft) acc[ft] = f4{0.f, 0.f, 0.f, 0.f};
@@ -101,27 +127,27 @@ __global__ __launch_bounds__(512) void k_act4(ActArgs a) {
 #pragma unroll
     for (int ft = 0; ft < 4; ++ft)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) P1[trunk][ks][16 * ft + 4 * g + r][j] = acc[ft][r];
+      for (int r = 0; r < 4; ++r) P1[ks][16 * ft + 4 * g + r][j] = acc[ft][r];
   }
   __syncthreads();
   // ---------------- h1 tile ks = tanh(b1 + sum of the 4 k-slices) ----------------
-  if (active) {
+  {
     f4 h;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = 16 * ks + 4 * g + r;
-      const float z = (((P1[trunk][0][f][j] + P1[trunk][1][f][j]) + P1[trunk][2][f][j]) + P1[trunk][3][f][j]) + b1[r];
+      const float z = (((P1[0][f][j] + P1[1][f][j]) + P1[2][f][j]) + P1[3][f][j]) + b1[r];
       h[r] = tanhf(z);
     }
-    *reinterpret_cast<f4*>(&H1[trunk][j][16 * ks + 4 * g]) = h;
+    *reinterpret_cast<f4*>(&H1[j][16 * ks + 4 * g]) = h;
   }
   __syncthreads();
   // ---------------- layer 2 (output tile ks), heads ----------------
-  if (active) {
+  {
     f4 z2 = b2;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-      const f4 hb = *reinterpret_cast<const f4*>(&H1[trunk][j][16 * kb + 4 * g]);
+      const f4 hb = *reinterpret_cast<const f4*>(&H1[j][16 * kb + 4 * g]);
       z2 = mfma16(w2v[kb].x, hb.x, z2);
       z2 = mfma16(w2v[kb].y, hb.y, z2);
       z2 = mfma16(w2v[kb].z, hb.z, z2);
@@ -150,7 +176,7 @@ __global__ __launch_bounds__(512) void k_act4(ActArgs a) {
   __syncthreads();
 
   // ---------------- outputs ----------------
-  if (tid < R) {
+  if (trunk == 0 && tid < R) {
     const int rw = row0 + tid;
     if (rw < a.n) {
       const float v = (((VP[0][tid] + VP[1][tid]) + VP[2][tid]) + VP[3][tid]) + c_b3;
@@ -162,40 +188,30 @@ __global__ __launch_bounds__(512) void k_act4(ActArgs a) {
       }
     }
   }
-  if (item) {
-    const long env = a.env_base + irow;
-    const bool valid = irow < a.n;
-    const float mu = (((HP[0][ia][ir] + HP[1][ia][ir]) + HP[2][ia][ir]) + HP[3][ia][ir]) + i_b3;
-    const float sd = expf(i_lstd);
-    const float var = sd * sd, lsd = logf(sd);
-    float act;
-    if (a.mode == PPO_GIVEN) {
-      act = valid ? i_act : 0.0f;
-    } else if (a.mode == PPO_MEAN) {
-      act = mu;
-    } else {
-      const SampleKey key = sample_key(a.seed, a.rank);
-      uint32_t rr[4];
-      philox_draw(key, env, a.step_id, (uint32_t)(ia >> 1), rr);
-      float z0, z1;
-      box_muller(rr[0], rr[1], z0, z1);
-      act = mu + ((ia & 1) ? z1 : z0) * sd;
-    }
-    const float d = act - mu;
-    ITM[tid][0] = -(d * d) / (2.0f * var) - lsd - kLz;
-    ITM[tid][1] = kEntC + lsd;
-    if (valid) {
-      if (a.action_out) a.action_out[(size_t)irow * A + ia] = act;
-      if (a.store_step >= 0) a.s_actions[((long)a.store_step * a.E + env) * A + ia] = act;
+#pragma unroll
+  for (int u = 0; u < NI; ++u) {
+    const int idx = tid + kA4Threads * u;
+    if (trunk == 1 && idx < R * A) {
+      const int ir = idx / A, ia = idx - ir * A, irow = row0 + ir;
+      const long env = a.env_base + irow;
+      const bool valid = irow < a.n;
+      const float mu = (((HP[0][ia][ir] + HP[1][ia][ir]) + HP[2][ia][ir]) + HP[3][ia][ir]) + i_b3[u];
+      const float sd = expf(i_lstd[u]);
+      const float var = sd * sd, lsd = logf(sd);
+      float act;
+      if (a.mode == PPO_GIVEN) act = valid ? i_act[u] : 0.0f;
+      else if (a.mode == PPO_MEAN) act = mu;
+      else act = mu + nz[u] * sd;
+      const float d = act - mu;
+      ITM[idx][0] = -(d * d) / (2.0f * var) - lsd - kLz;
+      ITM[idx][1] = kEntC + lsd;
+      if (valid) {
+        if (a.action_out) a.action_out[(size_t)irow * A + ia] = act;
+        if (a.store_step >= 0) a.s_actions[((long)a.store_step * a.E + env) * A + ia] = act;
+      }
     }
   }
-  if (a.store_step >= 0) {  // the rollout keeps the observation the action was taken on
-    for (int idx = tid; idx < R * O; idx += kA4Threads) {
-      const int r = idx / O, f = idx - r * O, rw = row0 + r;
-      if (rw < a.n) a.s_obs[((long)a.store_step * a.E + a.env_base + rw) * O + f] = a.x[(size_t)rw * a.ldx + f];
-    }
-  }
-  if (!a.need_actor) return;
+  if (trunk == 0) return;
   __syncthreads();
   if (tid < R) {
     const int rw = row0 + tid;
@@ -217,9 +233,9 @@ __global__ __launch_bounds__(512) void k_act4(ActArgs a) {
 // k_act2's feature split is faster, 6.3 vs 8.0 us). Returns -1 when not covered (caller: k_act2).
 int launch_act4(const ActArgs& a, hipStream_t s) {
   if (a.K.H != 64 || a.K.kind != PPO_NET_TANH_NORMAL || a.K.A > 32 || a.n <= 0) return -1;
-  if (a.K.OP < 112 && a.kernel != 4) return -1;  // kernel 4: forced (tests)
+  if (a.K.OP < 112 && (a.kernel & 0xFF) != 4) return -1;  // kernel 4: forced (tests)
   const int nto = a.K.OP / 16, nht = (a.K.A + 15) / 16;
-  const dim3 grid((a.n + kA4Rows - 1) / kA4Rows);
+  const dim3 grid((a.n + kA4Rows - 1) / kA4Rows, a.need_actor ? 2 : 1);
 #define PPO_ACT4_CASE(NTO_, NHT_)                                                    \
   if (nto == NTO_ && nht == NHT_) {                                                  \
     hipLaunchKernelGGL((k_act4<NTO_, NHT_>), grid, dim3(kA4Threads), 0, s, a);       \

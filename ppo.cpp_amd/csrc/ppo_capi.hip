@@ -283,6 +283,10 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
     if (es && es[0] >= '0' && es[0] <= '3') c->upd_sched = es[0] - '0';
     const char* ea = getenv("PPO_ACT_KERNEL");
     if (ea && (ea[0] == '2' || ea[0] == '4')) c->act_kernel = ea[0] - '0';
+#ifdef PPO_STAMPS
+    const char* eg = getenv("PPO_ACT_DIAG");  // diagnostic build: phases of k_act3 to skip (bits, << 8)
+    if (eg) c->act_kernel |= atoi(eg) << 8;
+#endif
     const char* ed = getenv("PPO_DW_FUSED");
     c->dw_fused = !(ed && ed[0] == '0');
 #ifdef PPO_DIAG

@@ -81,6 +81,39 @@ PPO_DEV float gamma_mt(float alpha, SampleKey k, long env, long step, uint32_t d
   return d;
 }
 
+// The first Marsaglia-Tsang attempt's normal / uniform do not depend on alpha: act kernels draw
+// them at kernel start (under the weight fetch) and finish with gamma_mt_d0, which is gamma_mt
+// with attempt 0's draw supplied (same arithmetic, same result).
+struct GammaDraw {
+  float z, u;
+};
+PPO_DEV GammaDraw gamma_draw(SampleKey k, long env, long step, uint32_t draw) {
+  uint32_t r[4];
+  philox_draw(k, env, step, draw, r);
+  float z, z1;
+  box_muller(r[0], r[1], z, z1);
+  return GammaDraw{z, u01(r[2])};
+}
+PPO_DEV float gamma_mt_d0(float alpha, GammaDraw d0, SampleKey k, long env, long step, uint32_t draw_base) {
+  const float d = alpha - 0.33333334f;
+  const float cc = 1.0f / sqrtf(9.0f * d);
+  for (uint32_t t = 0; t < 64; ++t) {
+    float z = d0.z, u = d0.u;
+    if (t > 0) {
+      const GammaDraw g = gamma_draw(k, env, step, draw_base + t);
+      z = g.z;
+      u = g.u;
+    }
+    const float y = 1.0f + cc * z;
+    if (y <= 0.0f) continue;
+    const float v = y * y * y;
+    const float xx = z * z;
+    if (u < 1.0f - 0.0331f * xx * xx) return d * v;
+    if (logf(u) < 0.5f * xx + d * (1.0f - v + logf(v))) return d * v;
+  }
+  return d;
+}
+
 // Feistel permutation of [0,B) keyed by (seed, rank, epoch counter); replaces torch::randperm
 // (ppo:490, ac:804). Mirrors orc_perm_index.
 struct PermKey {

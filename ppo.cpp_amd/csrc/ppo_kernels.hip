@@ -1470,7 +1470,7 @@ static int dispatch_net(const PackedLayout& K, F&& f) {
 
 int launch_act(const ActArgs& a, hipStream_t s) {
   if (launch_act3(a, s) == 0) return 0;  // 256-wide agents (ppo_act.hip)
-  if (a.kernel != 2 && launch_act4(a, s) == 0) return 0;  // 64-wide tanh agent (ppo_act_narrow.hip)
+  if ((a.kernel & 0xFF) != 2 && launch_act4(a, s) == 0) return 0;  // 64-wide tanh agent (ppo_act_narrow.hip)
   return dispatch_net(a.K, [&](auto H_, auto KIND_, auto NTO_) {
     constexpr int H = decltype(H_)::value, KIND = decltype(KIND_)::value, NTO = decltype(NTO_)::value;
     if (a.K.A > 20) return -1;

@@ -37,6 +37,8 @@ def main():
     ppo_amd.set_device(0)
     lib().ppo_stream.restype = C.c_void_p
     cases = [(0, 376, 17, 64), (0, 17, 6, 64), (1, 17, 6, 256), (1, 105, 8, 256)]
+    if os.environ.get("ACT_MICRO_CASES"):  # e.g. "1,17,6,256;0,376,17,64"
+        cases = [tuple(int(v) for v in c.split(",")) for c in os.environ["ACT_MICRO_CASES"].split(";")]
     for kind, O_, A, H in cases:
         for E in (64, 512, 1024, 4096):
             hc = ppo_amd.HipConfig(kind, O_, A, H, E, 4, 1, 1, 0.99, 0.95, 0.2, 0.01, 0.5, 0.5, 1e-5, 1, 1, 1, 0, 1)
@@ -50,7 +52,7 @@ def main():
             t_api = time_launches(lambda: lib().ppo_get_action_and_value(ag.h, E, x.ptr, 0, None, 0, 0, act.ptr, lp.ptr,
                                                                         ent.ptr, val.ptr, None), s)
             t_val = time_launches(lambda: lib().ppo_get_value(ag.h, E, x.ptr, val.ptr, None), s)
-            print(json.dumps({"kind": kind, "O": O_, "A": A, "H": H, "E": E, "rollout_act_us": round(t_roll, 2),
+            print(json.dumps({"diag": os.environ.get("PPO_ACT_DIAG", ""), "kind": kind, "O": O_, "A": A, "H": H, "E": E, "rollout_act_us": round(t_roll, 2),
                               "api_act_us": round(t_api, 2), "get_value_us": round(t_val, 2)}), flush=True)
             ag.close()
 

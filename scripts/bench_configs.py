@@ -46,13 +46,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--only", default="", help="cfg2 or cfg4_shard")
     args = ap.parse_args()
     ppo_amd.set_device(0)
     n = args.iters + args.warmup + 2
-    run("cfg2", ppo_amd.PPOConfig(env_id="Humanoid-v4", num_envs=1024, num_steps=2048,
-                                  total_timesteps=1024 * 2048 * n), args.iters, args.warmup)
-    run("cfg4_shard", ppo_amd.ACPPOConfig(env_id="Ant-v5", num_envs=1024, num_steps=128,
-                                          total_timesteps=1024 * 128 * n), args.iters, args.warmup)
+    if args.only != "cfg4_shard":
+        run("cfg2", ppo_amd.PPOConfig(env_id="Humanoid-v4", num_envs=1024, num_steps=2048,
+                                      total_timesteps=1024 * 2048 * n), args.iters, args.warmup)
+    if args.only != "cfg2":
+        run("cfg4_shard", ppo_amd.ACPPOConfig(env_id="Ant-v5", num_envs=1024, num_steps=128,
+                                              total_timesteps=1024 * 128 * n), args.iters, args.warmup)
 
 
 if __name__ == "__main__":

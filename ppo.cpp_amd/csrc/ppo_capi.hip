@@ -326,7 +326,9 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   {
     const char* ev = getenv("PPO_UPD_KERNEL");  // "0": force the wave-per-16-rows k_fwdbwd
     const int sgmax = std::max(c->sg[0].size, c->sg[1].size);
-    if (!(ev && ev[0] == '0') && upd2_supported(c->K, &c->upd) == 0) {
+    // k_upd2 addresses the rollout storage with 32-bit buffer offsets
+    const bool fits32 = (double)B * (double)std::max(O, A) * 4.0 < 4294967040.0;
+    if (!(ev && ev[0] == '0') && fits32 && upd2_supported(c->K, &c->upd) == 0) {
       c->use_upd = c->use_upd2 = true;
       const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
       c->upd_nblk = std::min(ut, 512);  // both trunks per workgroup, 2 workgroups per CU x 256 CUs
@@ -675,6 +677,8 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   u.adv = c->buf[PPO_BUF_ADVANTAGES];
   u.ret = c->buf[PPO_BUF_RETURNS];
   u.val = c->buf[PPO_BUF_VALUES];
+  u.rows_n = B;
+  u.obs_n = B * c->K.O;
   u.clip_coef = cfg.clip_coef;
   u.ent_coef = cfg.ent_coef;
   u.vf_coef = cfg.vf_coef;

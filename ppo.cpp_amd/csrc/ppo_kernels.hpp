@@ -45,6 +45,7 @@ struct UpdArgs {
   int wlds_off;  // float offset of the weight staging buffers in dynamic LDS
   const int32_t* perm;
   const float *obs, *actions, *logp, *adv, *ret, *val;
+  long rows_n, obs_n;      // rollout storage rows (T E) and obs floats (T E O): k_upd2's buffer descriptors
   const float* adv_stats;  // [2] mean, std of this minibatch
   float clip_coef, ent_coef, vf_coef, inv_m;
   int clip_vloss, norm_adv;

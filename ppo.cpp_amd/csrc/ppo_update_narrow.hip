@@ -10,8 +10,13 @@
 //    each wave owns 32 output features x 32 rows (2 x 2 accumulator tiles of 16x16x4 f32 MFMA),
 //    so every W1 A-operand load feeds 8 MFMAs;
 //  * the gathered observation rows are staged ONCE in LDS for both trunks, in 128-column chunks
-//    (double-buffered; the next chunk's gather is in flight under the current chunk's MFMAs, and
-//    the last chunk prefetches the next tile's first one);
+//    moved by LDS DMA (buffer_load ... lds: no staging registers; out-of-range columns and rows
+//    read as 0), double-buffered (the next chunk's gather is in flight under the current chunk's
+//    MFMAs, the last chunk prefetches the next tile's first one), 16-byte units XOR-swizzled by
+//    row so the B-operand ds_read_b128 stay conflict-free without row padding;
+//  * the next tile's per-row data (return, value, old log-prob, advantage, actions) is DMA'd into
+//    LDS once this tile's loss no longer needs it, through permutation entries loaded a tile ahead:
+//    no dependent perm -> data round trip at a tile's start;
 //  * tanh' needs only h1, which stays in registers: no layer-1 recompute;
 //  * bias / head-weight / logstd gradients and the loss statistics accumulate in registers over
 //    all of a workgroup's tiles and are reduced across lanes once, in a fixed order, at the end.
@@ -24,26 +29,30 @@ namespace {
 
 constexpr int H2 = 64, FT2 = 2, RT2 = 2, R2 = 32, LDA2 = H2 + 4;
 
-template <int NTO, int NHT, int VEC>
+template <int NTO, int NHT, int VEC, int NUA>
 struct Geo2 {
   static constexpr int OP = NTO * 16;
   static constexpr int CKB = NTO < 8 ? NTO : 8;      // k-blocks (16 columns) per staged X chunk
   static constexpr int NCH = (NTO + CKB - 1) / CKB;  // chunks per tile
   static constexpr int CW = CKB * 16;                // columns per chunk
-  static constexpr int LDX = CW + 4;                 // row stride = 4 mod 64 banks
-  static constexpr int NB = NCH > 1 ? 2 : 1;         // X chunk buffers
+  static constexpr int LDX = CW;                     // unpadded rows (DMA writes 64 lanes x VEC floats)
+  static constexpr int UPR = CW / 4;                 // 16-byte units per row
+  static constexpr int SWZ = (UPR % 16 == 0) ? 16 : (UPR % 8 == 0) ? 8 : 4;  // unit XOR swizzle span
+  static constexpr int NB = 2;  // X chunk buffers, alternating by running chunk count (a DMA lands at once)
   static constexpr int NHP = NHT * 16, LDG = NHP + 4;
-  static constexpr int PERROW = VEC == 4 ? CW / 4 : CW;  // gather items per row and chunk
-  static constexpr int NGI = (R2 * PERROW + 255) / 256;  // gather items per thread
-  static constexpr int NU = (R2 * NHP + 255) / 256;      // (row, action) items per thread (upper bound)
+  static constexpr int PERROW = VEC == 4 ? UPR : CW;     // DMA lanes per row and chunk
+  static constexpr int NGI = R2 * PERROW / 256;          // DMA instructions per wave per chunk
+  static_assert(R2 * PERROW % 256 == 0, "chunk must be a whole number of DMA instructions per wave");
+  static constexpr int NU = NUA;                         // (row, action) items per thread: ceil(R A / 256)
   // LDS carve (floats); the (row, action) item and action regions follow at runtime offsets
   static constexpr int oXS = 0;
   static constexpr int oACT = oXS + NB * R2 * LDX;     // [2 trunks][R][LDA]: h1, then h2, then dz2
   static constexpr int oSCR = oACT + 2 * R2 * LDA2;    // actor head partials [2][NHP][R] | critic [2][R]
   static constexpr int oGG = oSCR + 2 * NHP * R2 + 2 * R2;  // [R][LDG] d loss / d mu
-  static constexpr int oROWS = oGG + R2 * LDG;          // [R][8] per-row scalars
-  static constexpr int oSP = oROWS + R2 * 8;            // head biases | sd | var | log sd (NHP each) | critic bias
-  static constexpr int oITM = oSP + 4 * NHP + 4;        // [R*A][4] items, then [R*A] actions
+  static constexpr int oROWS = oGG + R2 * LDG;          // [R][8] per-row scalars computed by the loss
+  static constexpr int oRD = oROWS + R2 * 8;            // [4][64] DMA'd return | value | old log-prob | advantage
+  static constexpr int oSP = oRD + 4 * 64;              // head biases | sd | var | log sd (NHP each) | critic bias
+  static constexpr int oITM = oSP + 4 * NHP + 4;        // [R*A][4] items, then [64 ceil(R*A / 64)] actions
 };
 
 PPO_DEV float lf(const float* p) { return *p; }
@@ -51,6 +60,20 @@ PPO_DEV f4 lf4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 PPO_DEV void sf4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
 PPO_DEV float bl1(PBuf b, int lane_floats, int uni_floats) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b.r, lane_floats * 4, uni_floats * 4, 0));
+}
+
+// buffer resource over `bytes` bytes (offsets at or past the end read as 0)
+PPO_DEV PBuf make_pbuf_b(const void* base, uint32_t bytes) {
+  return PBuf{__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000)};
+}
+constexpr uint32_t kOOB = 0xFFFFFFF0u;  // a byte offset past every buffer: the DMA writes zeros
+// LDS DMA: every lane of the wave loads `size` bytes at its byte offset into lds_wave + lane * size
+// (lds_wave must be wave-uniform); completion is counted by vmcnt
+template <int SIZE>
+PPO_DEV void dma(PBuf b, float* lds_wave, uint32_t voff) {
+  auto* l = (__attribute__((address_space(3))) void*)lds_wave;
+  if constexpr (SIZE == 16) __builtin_amdgcn_raw_ptr_buffer_load_lds(b.r, l, 16, voff, 0, 0, 0);
+  else __builtin_amdgcn_raw_ptr_buffer_load_lds(b.r, l, 4, voff, 0, 0, 0);
 }
 
 // Column sums over the 16 rows j of a lane group: x[4 ft + r] (feature 16 ft + 4 g + r of this lane's
@@ -103,17 +126,19 @@ PPO_DEV void mm64(f4 (&out)[FT2][RT2], PBuf wb, int wlane, int ldw, const float*
 
 }  // namespace
 
-template <int NTO, int NHT, int VEC>
+template <int NTO, int NHT, int VEC, int NUA>
 __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
-  using GE = Geo2<NTO, NHT, VEC>;
+  using GE = Geo2<NTO, NHT, VEC, NUA>;
   constexpr int OP = GE::OP, CKB = GE::CKB, NCH = GE::NCH, CW = GE::CW, LDX = GE::LDX, NHP = GE::NHP;
-  constexpr int LDG = GE::LDG, PERROW = GE::PERROW, NGI = GE::NGI, NU = GE::NU;
+  constexpr int LDG = GE::LDG, PERROW = GE::PERROW, NGI = GE::NGI, NU = GE::NU, UPR = GE::UPR, SWZ = GE::SWZ;
+  constexpr int W1D = 2;  // W1 A-operand prefetch depth (k-blocks)
   constexpr int R = R2, FT = FT2, RT = RT2, LDA = LDA2, H = H2;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* XS = lds + GE::oXS;
   float* SCR = lds + GE::oSCR;
   float* GG = lds + GE::oGG;
   float* ROWS = lds + GE::oROWS;
+  float* RD = lds + GE::oRD;   // [0] return [64] value [128] old log-prob [192] advantage (DMA)
   float* SHB = lds + GE::oSP;  // actor head biases
   float* SSD = SHB + NHP;      // exp(logstd)
   float* SVAR = SSD + NHP;     // sd^2
@@ -167,44 +192,65 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
   };
   const int ntiles = (M + R - 1) / R;
 
-  // ---- gather of the observation rows, chunk by chunk, through the permutation ----
+  // ---- gather of the observation rows, chunk by chunk, through the permutation, by LDS DMA ----
+  // DMA lane (u, lane) of wave w covers chunk element e = (w NGI + u) 64 + lane: VEC 4: 16-byte unit
+  // e, VEC 1: float e (unit e / 4, component e % 4). Physical unit p of row r holds logical unit
+  // p ^ (r & (SWZ - 1)).
+  const PBuf ob = make_pbuf_b(a.obs, (uint32_t)min(a.obs_n * 4, (long)0xFFFFFFFF));
   int pcur[NGI], pnext[NGI];
-  f4 xv[NGI];  // VEC == 1: component x only
-  // Every load below is unconditional (clamped address, value masked afterwards): a load under a
-  // per-lane branch gets its own s_waitcnt vmcnt(0) and serialises the gather.
   auto perms_of = [&](int itn, int (&pm)[NGI]) {
 #pragma unroll
     for (int u = 0; u < NGI; ++u) {
-      const int idx = tid + 256 * u, row = idx / PERROW, m = itn * R + row;
-      const int p = a.perm[min(m, M - 1)];
-      pm[u] = (itn < ntiles && idx < R * PERROW && m < M) ? p : -1;
+      const int e = (wave * NGI + u) * 64 + lane, row = e / PERROW, m = itn * R + row;
+      const int p = a.perm[min(m, M - 1)];  // unconditional (clamped), masked below
+      pm[u] = (itn < ntiles && m < M) ? p : -1;
     }
   };
-  auto issue = [&](const int (&pm)[NGI], int ch) {
+  // column chunk ch of the rows in pm into X buffer buf
+  auto issue = [&](const int (&pm)[NGI], int ch, int buf) {
+    float* xs = XS + buf * R * LDX;
 #pragma unroll
     for (int u = 0; u < NGI; ++u) {
-      const int idx = tid + 256 * u, row = idx / PERROW, q = idx - row * PERROW;
-      (void)row;
-      const long b = (long)(pm[u] >= 0 ? pm[u] : 0) * O;
-      if constexpr (VEC == 4) {
-        const int col = ch * CW + 4 * q;
-        const f4 v = ld4(a.obs + b + min(col, O - 4));
-        xv[u] = (pm[u] >= 0 && col < O) ? v : f4{0.f, 0.f, 0.f, 0.f};
-      } else {
-        const int col = ch * CW + q;
-        const float v = a.obs[b + min(col, O - 1)];
-        xv[u].x = (pm[u] >= 0 && col < O) ? v : 0.f;
-      }
+      const int e = (wave * NGI + u) * 64 + lane;
+      const int unit = VEC == 4 ? e : e >> 2, comp = VEC == 4 ? 0 : e & 3;
+      const int row = unit / UPR, pu = unit - row * UPR, lu = pu ^ (row & (SWZ - 1));
+      const int col = ch * CW + 4 * lu + comp;
+      const uint32_t voff = (pm[u] >= 0 && col < O) ? (uint32_t)(pm[u] * O + col) * 4u : kOOB;
+      dma<4 * VEC>(ob, xs + (wave * NGI + u) * 64 * VEC, voff);
     }
   };
-  auto commit = [&](int ch) {
-    float* xs = XS + (ch & 1) * R * LDX;
+  // ---- per-row data of a tile into LDS by DMA (RD, ACTN), through permutation entries held a tile ahead ----
+  const int NV = (R * A + 63) / 64;  // action DMA instructions (wave w issues v = w, w + 4, ...)
+  constexpr int NVW = (R * NHP + 255) / 256;
+  const PBuf bret = make_pbuf_b(a.ret, (uint32_t)(a.rows_n * 4)), bval = make_pbuf_b(a.val, (uint32_t)(a.rows_n * 4));
+  const PBuf blogp = make_pbuf_b(a.logp, (uint32_t)(a.rows_n * 4)), badv = make_pbuf_b(a.adv, (uint32_t)(a.rows_n * 4));
+  const PBuf bact = make_pbuf_b(a.actions, (uint32_t)min(a.rows_n * A * 4, (long)0xFFFFFFFF));
+  int prow = -1, pact[NVW];
+  auto row_perms = [&](int itn) {
+    const int m = itn * R + lane;
+    const int p = a.perm[min(m, M - 1)];
+    prow = (wave == 0 && lane < R && itn < ntiles && m < M) ? p : -1;
 #pragma unroll
-    for (int u = 0; u < NGI; ++u) {
-      const int idx = tid + 256 * u, row = idx / PERROW, q = idx - row * PERROW;
-      if (idx < R * PERROW) {
-        if constexpr (VEC == 4) sf4(xs + row * LDX + 4 * q, xv[u]);
-        else xs[row * LDX + q] = xv[u].x;
+    for (int k = 0; k < NVW; ++k) {
+      const int idx = (wave + 4 * k) * 64 + lane, row = min(idx, R * A - 1) / A, mm = itn * R + row;
+      const int q = a.perm[min(mm, M - 1)];
+      pact[k] = (idx < R * A && itn < ntiles && mm < M) ? q : -1;
+    }
+  };
+  auto row_dma = [&]() {
+    if (wave == 0) {
+      const uint32_t voff = prow >= 0 ? (uint32_t)prow * 4u : kOOB;
+      dma<4>(bret, RD, voff);
+      dma<4>(bval, RD + 64, voff);
+      dma<4>(blogp, RD + 128, voff);
+      dma<4>(badv, RD + 192, voff);
+    }
+#pragma unroll
+    for (int k = 0; k < NVW; ++k) {
+      const int v = wave + 4 * k;
+      if (v < NV) {  // wave-uniform
+        const int idx = v * 64 + lane, ai = idx - (min(idx, R * A - 1) / A) * A;
+        dma<4>(bact, ACTN + v * 64, pact[k] >= 0 ? (uint32_t)(pact[k] * A + ai) * 4u : kOOB);
       }
     }
   };
@@ -224,33 +270,18 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
   float lst[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // pg, v, ent, old kl, kl, clipfrac (tid < R)
 
   perms_of(blockIdx.x, pcur);
-  issue(pcur, 0);
+  issue(pcur, 0, 0);
+  row_perms(blockIdx.x);
+  row_dma();
 
-  for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
+  int tp = 0;  // buffer of this tile's chunk 0: the running chunk count's parity
+  for (int it = blockIdx.x; it < ntiles; it += gridDim.x, tp ^= NCH & 1) {
     const int m0 = it * R;
+    // chunk 0 and the row data of this tile were DMA'd during the previous tile
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
     perms_of(it + gridDim.x, pnext);
-    // per-row data of this tile (consumed after layer 1)
-    float rd[4] = {0.f, 0.f, 0.f, 0.f};
-    if (wave == 0) {  // lanes >= R load a duplicate row (unconditional loads, see above)
-      const long b = a.perm[min(m0 + (tid & (R - 1)), M - 1)];
-      rd[0] = a.ret[b]; rd[1] = a.val[b]; rd[2] = a.logp[b]; rd[3] = a.adv[b];
-    }
-    float av[NU];
-    {
-      int pa[NU];
-#pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        const int idx = min(tid + 256 * u, R * A - 1), row = idx / A;
-        pa[u] = a.perm[min(m0 + row, M - 1)];
-      }
-#pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        const int idx = tid + 256 * u, ic = min(idx, R * A - 1), row = ic / A;
-        const float v = a.actions[(long)pa[u] * A + (ic - row * A)];
-        av[u] = (idx < R * A && m0 + row < M) ? v : 0.f;
-      }
-    }
-
+    row_perms(it + gridDim.x);
     // ---------------- layer 1 (both trunks share the staged rows) ----------------
     f4 z[FT][RT];
 #pragma unroll
@@ -260,35 +291,44 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
       for (int rt = 0; rt < RT; ++rt) z[ft][rt] = bv;
     }
     {
-      f4 w[2][FT];
+      if (NCH > 1) issue(pcur, 1, tp ^ 1);
+      else issue(pnext, 0, tp ^ 1);
+      f4 w[W1D + 1][FT];
 #pragma unroll
-      for (int ft = 0; ft < FT; ++ft) w[0][ft] = pld4(pb, w1lane, 16 * ft * OP);
+      for (int q = 0; q < W1D && q < NTO; ++q)
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft) w[q][ft] = pld4(pb, w1lane, 16 * ft * OP + 16 * q);
 #pragma unroll
       for (int kb = 0; kb < NTO; ++kb) {
-        if (kb % CKB == 0) {
-          const int ch = kb / CKB;
-          commit(ch);
+        if (kb > 0 && kb % CKB == 0) {
+          // chunk kb / CKB landed: only the W1 loads of k-blocks kb, kb + 1 may still be in flight
+          static_assert(W1D * FT2 == 4, "vmcnt below");
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
           lds_barrier();
-          if (ch + 1 < NCH) issue(pcur, ch + 1);
-          else issue(pnext, 0);
+          const int ch = kb / CKB;
+          if (ch + 1 < NCH) issue(pcur, ch + 1, tp ^ ((ch + 1) & 1));
+          else issue(pnext, 0, tp ^ (NCH & 1));
         }
-        if (kb + 1 < NTO) {
+        if (kb + W1D < NTO) {
 #pragma unroll
-          for (int ft = 0; ft < FT; ++ft) w[(kb + 1) & 1][ft] = pld4(pb, w1lane, 16 * ft * OP + 16 * (kb + 1));
+          for (int ft = 0; ft < FT; ++ft)
+            w[(kb + W1D) % (W1D + 1)][ft] = pld4(pb, w1lane, 16 * ft * OP + 16 * (kb + W1D));
         }
         __builtin_amdgcn_sched_barrier(0);
-        const float* xs = XS + ((kb / CKB) & 1) * R * LDX + j * LDX + 16 * (kb % CKB) + 4 * g;
+        const int lu = 4 * (kb % CKB) + g;
+        const float* xs = XS + (tp ^ ((kb / CKB) & 1)) * R * LDX + j * LDX + 4 * (lu ^ (j & (SWZ - 1)));
         f4 b[RT];
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) b[rt] = lf4(xs + 16 * rt * LDX);
+        for (int rt = 0; rt < RT; ++rt) b[rt] = lf4(xs + 16 * rt * LDX);  // (16 rt + j) & (SWZ - 1) = j & (SWZ - 1)
+        const int wq = kb % (W1D + 1);
 #pragma unroll
         for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt) {
-            z[ft][rt] = mfma16(w[kb & 1][ft].x, b[rt].x, z[ft][rt]);
-            z[ft][rt] = mfma16(w[kb & 1][ft].y, b[rt].y, z[ft][rt]);
-            z[ft][rt] = mfma16(w[kb & 1][ft].z, b[rt].z, z[ft][rt]);
-            z[ft][rt] = mfma16(w[kb & 1][ft].w, b[rt].w, z[ft][rt]);
+            z[ft][rt] = mfma16(w[wq][ft].x, b[rt].x, z[ft][rt]);
+            z[ft][rt] = mfma16(w[wq][ft].y, b[rt].y, z[ft][rt]);
+            z[ft][rt] = mfma16(w[wq][ft].z, b[rt].z, z[ft][rt]);
+            z[ft][rt] = mfma16(w[wq][ft].w, b[rt].w, z[ft][rt]);
           }
       }
     }
@@ -305,14 +345,6 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
         sf4(ACT + row * LDA + fbase + 16 * ft + 4 * g, z[ft][rt]);
         if (m < M) st4(a.H1[trunk] + (size_t)m * H + fbase + 16 * ft + 4 * g, z[ft][rt]);
       }
-    if (tid < R) {
-      ROWS[tid * 8 + 0] = rd[0]; ROWS[tid * 8 + 1] = rd[1]; ROWS[tid * 8 + 2] = rd[2]; ROWS[tid * 8 + 3] = rd[3];
-    }
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int idx = tid + 256 * u;
-      if (idx < R * A) ACTN[idx] = av[u];
-    }
     lds_barrier();
 
     // ---------------- layer 2 ----------------
@@ -401,7 +433,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
     if (tid < R) {
       const bool valid = m0 + tid < M;
       const float v = (SCR[2 * NHP * R + tid] + SCR[2 * NHP * R + R + tid]) + SCB[0];
-      const float rt_ = ROWS[tid * 8 + 0], ov = ROWS[tid * 8 + 1];
+      const float rt_ = RD[tid], ov = RD[64 + tid];
       float gv, sv;
       if (a.clip_vloss) {
         const float vu = (v - rt_) * (v - rt_);
@@ -430,10 +462,10 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
         lp += ITM[4 * (tid * A + ai) + 0];
         ent += ITM[4 * (tid * A + ai) + 1];
       }
-      const float oldlp = valid ? ROWS[tid * 8 + 2] : lp;
+      const float oldlp = valid ? RD[128 + tid] : lp;
       const float logratio = lp - oldlp;
       const float ratio = expf(logratio);
-      float an = valid ? ROWS[tid * 8 + 3] : 0.f;
+      float an = valid ? RD[192 + tid] : 0.f;
       if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
       const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
       const float pg1 = -an * ratio, pg2 = -an * rc;
@@ -455,6 +487,8 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
       ROWS[tid * 8 + 5] = g_ent;
     }
     lds_barrier();
+    // every read of this tile's RD / ACTN is done: DMA the next tile's
+    row_dma();
     // ---------------- loss, pass 2: d loss / d mu and d loss / d logstd ----------------
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
@@ -636,28 +670,31 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
 template <typename F>
 static int dispatch_upd2(const PackedLayout& K, F&& f) {
   if (K.H != 64 || K.kind != PPO_NET_TANH_NORMAL || K.A > 32) return -1;
-  const int nto = K.OP / 16, nht = (K.A + 15) / 16, vec = (K.O % 4 == 0) ? 4 : 1;
-#define PPO_UPD2_CASE(NTO_, NHT_, VEC_)                                                              \
-  if (nto == NTO_ && nht == NHT_ && vec == VEC_)                                                     \
+  const int nto = K.OP / 16, nht = (K.A + 15) / 16, nu = (R2 * K.A + 255) / 256;
+  const int vec = (K.O % 4 == 0 && nto >= 2) ? 4 : 1;  // 16-byte DMA needs >= 8 units per row (256 per chunk)
+#define PPO_UPD2_CASE(NTO_, NHT_, VEC_, NU_)                                                         \
+  if (nto == NTO_ && nht == NHT_ && vec == VEC_ && nu == NU_)                                        \
     return f(std::integral_constant<int, NTO_>{}, std::integral_constant<int, NHT_>{},               \
-             std::integral_constant<int, VEC_>{});
-  PPO_UPD2_CASE(1, 1, 1) PPO_UPD2_CASE(2, 1, 1) PPO_UPD2_CASE(7, 1, 1) PPO_UPD2_CASE(24, 2, 4)
-  PPO_UPD2_CASE(2, 2, 1) PPO_UPD2_CASE(24, 2, 1) PPO_UPD2_CASE(1, 1, 4) PPO_UPD2_CASE(2, 1, 4)
+             std::integral_constant<int, VEC_>{}, std::integral_constant<int, NU_>{});
+  // NU = 1: A <= 8; 2: A <= 16; 3: A <= 24; 4: A <= 32
+  PPO_UPD2_CASE(1, 1, 1, 1) PPO_UPD2_CASE(2, 1, 1, 1) PPO_UPD2_CASE(2, 1, 1, 2) PPO_UPD2_CASE(7, 1, 1, 1)
+  PPO_UPD2_CASE(24, 2, 4, 3) PPO_UPD2_CASE(2, 2, 1, 3) PPO_UPD2_CASE(24, 2, 1, 3)
+  PPO_UPD2_CASE(2, 1, 4, 1) PPO_UPD2_CASE(24, 1, 4, 2) PPO_UPD2_CASE(24, 2, 4, 4)
 #undef PPO_UPD2_CASE
   return -1;
 }
 
 int upd2_supported(const PackedLayout& K, UpdGeoOut* g) {
-  return dispatch_upd2(K, [&](auto NTO_, auto NHT_, auto VEC_) {
-    using GE = Geo2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value>;
+  return dispatch_upd2(K, [&](auto NTO_, auto NHT_, auto VEC_, auto NU_) {
+    using GE = Geo2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value, decltype(NU_)::value>;
     int off = GE::oITM + 4 * R2 * K.A;
     g->actn_off = off;
-    off += R2 * K.A;
+    off += 64 * ((R2 * K.A + 63) / 64);
     g->acc_off = 0;
     g->spar_off = 0;
     g->lds_bytes = (size_t)off * sizeof(float);
     g->rows = R2;
-    const auto k = k_upd2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value>;
+    const auto k = k_upd2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value, decltype(NU_)::value>;
     return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) ==
                    hipSuccess
                ? 0
@@ -666,9 +703,10 @@ int upd2_supported(const PackedLayout& K, UpdGeoOut* g) {
 }
 
 int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s) {
-  return dispatch_upd2(a.K, [&](auto NTO_, auto NHT_, auto VEC_) {
-    hipLaunchKernelGGL((k_upd2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value>), dim3(nblocks),
-                       dim3(256), lds_bytes, s, a);
+  return dispatch_upd2(a.K, [&](auto NTO_, auto NHT_, auto VEC_, auto NU_) {
+    hipLaunchKernelGGL((k_upd2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value,
+                               decltype(NU_)::value>),
+                       dim3(nblocks), dim3(256), lds_bytes, s, a);
     return 0;
   });
 }

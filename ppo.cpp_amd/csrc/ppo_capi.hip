@@ -281,6 +281,9 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   {  // kernel selection, read once (A/B switches of complete kernels; never read on a launch path)
     const char* es = getenv("PPO_UPD_SCHED");
     if (es && es[0] >= '0' && es[0] <= '3') c->upd_sched = es[0] - '0';
+#ifdef PPO_STAMPS
+    if (es) c->upd_sched = atoi(es);  // diagnostic build: bits 4..7 skip stores (ppo_update.hip)
+#endif
     const char* ea = getenv("PPO_ACT_KERNEL");
     if (ea && (ea[0] == '2' || ea[0] == '4')) c->act_kernel = ea[0] - '0';
 #ifdef PPO_STAMPS

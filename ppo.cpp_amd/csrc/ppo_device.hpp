@@ -252,7 +252,13 @@ template <int CTRL>
 PPO_DEV float dpp_f(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
-enum : int { kDppQuadXor1 = 0xB1, kDppQuadMirror = 0x1B, kDppHalfMirror = 0x141, kDppRowRor8 = 0x128 };
+enum : int { kDppQuadXor1 = 0xB1, kDppQuadXor2 = 0x4E, kDppQuadMirror = 0x1B, kDppHalfMirror = 0x141, kDppRowRor8 = 0x128 };
+// sum over each aligned group of 8 lanes, the same bits in all 8 (pairwise sums are commutative)
+PPO_DEV float group8_sum(float v) {
+  v += dpp_f<kDppQuadXor1>(v);
+  v += dpp_f<kDppQuadXor2>(v);
+  return v + dpp_f<kDppHalfMirror>(v);
+}
 PPO_DEV float xor16_sum(float v) {
   const auto p = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
                                                   false, false);

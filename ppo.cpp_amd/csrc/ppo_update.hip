@@ -24,32 +24,41 @@
 #include "ppo_kernels.hpp"
 
 #ifdef PPO_STAMPS
-// diagnostic build only: per-wave shader-clock stamps at phase ends of tiles 2..5 of every workgroup
+// diagnostic build only: per-wave shader-clock stamps at phase ends of the first 16 tiles of every workgroup
 #define PPO_NSTAMP 13
-#define PPO_STAMP_TILES 4
-__device__ unsigned long long g_upd_stamps[1024 * 4 * PPO_STAMP_TILES * (PPO_NSTAMP + 1)];
+#define PPO_STAMP_TILES 16
+#define PPO_STAMP_REC (PPO_NSTAMP + 2)  // start, 13 phase ends, hardware wave id (HW_ID | XCC_ID << 32)
+__device__ unsigned long long g_upd_stamps[1024 * 4 * PPO_STAMP_TILES * PPO_STAMP_REC];
 #define PPO_STAMP(k)                                                                                 \
   do {                                                                                               \
-    const int tt_ = (it - (int)blockIdx.x) / (int)gridDim.x - 2;                                     \
+    const int tt_ = (it - (int)blockIdx.x) / (int)gridDim.x;                                     \
     if (tt_ >= 0 && tt_ < PPO_STAMP_TILES) {                                                         \
       const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                    \
       const int wg_ = trunk * 512 + blockIdx.x;                                            \
       if (lane == 0 && blockIdx.x < 512)                                                                    \
-        g_upd_stamps[((wg_ * 4 + wave) * PPO_STAMP_TILES + tt_) * (PPO_NSTAMP + 1) + (k) + 1] = t_;  \
+        g_upd_stamps[((wg_ * 4 + wave) * PPO_STAMP_TILES + tt_) * PPO_STAMP_REC + (k) + 1] = t_;      \
     }                                                                                                \
   } while (0)
 #define PPO_STAMP_START()                                                                            \
   do {                                                                                               \
-    const int tt_ = (it - (int)blockIdx.x) / (int)gridDim.x - 2;                                     \
+    const int tt_ = (it - (int)blockIdx.x) / (int)gridDim.x;                                     \
     if (tt_ >= 0 && tt_ < PPO_STAMP_TILES) {                                                         \
       const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                    \
       const int wg_ = trunk * 512 + blockIdx.x;                                            \
-      if (lane == 0 && blockIdx.x < 512) g_upd_stamps[((wg_ * 4 + wave) * PPO_STAMP_TILES + tt_) * (PPO_NSTAMP + 1)] = t_; \
+      const unsigned long long id_ = (unsigned long long)__builtin_amdgcn_s_getreg(0xF804) |          \
+                                     ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32);  \
+      if (lane == 0 && blockIdx.x < 512) {                                                           \
+        g_upd_stamps[((wg_ * 4 + wave) * PPO_STAMP_TILES + tt_) * PPO_STAMP_REC] = t_;               \
+        g_upd_stamps[((wg_ * 4 + wave) * PPO_STAMP_TILES + tt_) * PPO_STAMP_REC + PPO_NSTAMP + 1] = id_; \
+      }                                                                                              \
     }                                                                                                \
   } while (0)
+// a.sched bits 4..7 skip the H1 / DZ2 / DZ1 / Xn stores (timing experiments only)
+#define PPO_DIAG_SKIP(bit) ((a.sched >> (bit)) & 1)
 #else
 #define PPO_STAMP(k) do {} while (0)
 #define PPO_STAMP_START() do {} while (0)
+#define PPO_DIAG_SKIP(bit) false
 #endif
 
 namespace {
@@ -341,6 +350,11 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
   const int trunk = (a.sched & 1) ? 1 - (int)blockIdx.y : (int)blockIdx.y;
   if (!((a.trunk_mask >> trunk) & 1)) return;
   if ((a.sched & 2) && trunk == 1) __builtin_amdgcn_s_setprio(1);
+#ifdef PPO_STAMPS
+  // timing experiment: start the actor workgroups (a.sched >> 8) x ~8 K cycles late
+  if (trunk == 1)
+    for (int i = 0; i < (a.sched >> 8); ++i) __builtin_amdgcn_s_sleep(127);
+#endif
   const PackedLayout& K = a.K;
   const TrunkDev& T = K.tr[trunk];
   const float* __restrict__ P = a.P;
@@ -438,7 +452,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
         float v = vg[k];
         if (LN && pg[k] >= 0) v = (v - SOM[f]) / SOS[f];
         XN[row * LDX + f] = v;
-        if (trunk == 0 && m < a.M) a.Xn[(size_t)m * OP + f] = v;
+        if (trunk == 0 && m < a.M && !PPO_DIAG_SKIP(7)) a.Xn[(size_t)m * OP + f] = v;
       }
     }
     if (tid < R) {
@@ -461,7 +475,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
         if constexpr (LN) v = (v - SOM[f]) / SOS[f];
       }
       XN[row * LDX + f] = v;
-      if (trunk == 0 && m < a.M) a.Xn[(size_t)m * OP + f] = v;
+      if (trunk == 0 && m < a.M && !PPO_DIAG_SKIP(7)) a.Xn[(size_t)m * OP + f] = v;
     }
     if (tid < R) {
       const int m = mb + tid;
@@ -497,6 +511,22 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     } else {
       gather_sync(it);
     }
+    // one head tile (NHT == 1): its weights, in the layout the head backward reads them (critic: w3
+    // features 4 g + r, which the forward dot product uses too; actor: heads 4 g + r of feature j),
+    // are requested here, a whole forward pass before their first use, instead of in the head
+    // phases (where they were the only loads a wave waited on outside the matrix phases)
+    f4 hwb[FT];
+    if constexpr (NHT == 1) {
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+        if (trunk == 0) {
+          hwb[ft] = pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) hwb[ft][r] = hrow_b[0][r] >= 0 ? bld1(pb, hrow_b[0][r] + fbase + j, 16 * ft) : 0.0f;
+        }
+      }
+    }
     lds_barrier();
     PPO_STAMP(0);
 
@@ -528,7 +558,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) z[ft][rt][r] = tanhf(z[ft][rt][r]);
     }
-    store_tile_rows<FT, RT>(a.H1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
+    if (!PPO_DIAG_SKIP(4)) store_tile_rows<FT, RT>(a.H1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
     lds_store_tile<FT, RT, LDA>(ACT, z, rbase, fbase, j, g);
     lds_barrier();
     PPO_STAMP(2);
@@ -585,7 +615,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       for (int rt = 0; rt < RT; ++rt) pv[rt] = 0.f;
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
-        const f4 w = pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
+        const f4 w = NHT == 1 ? hwb[ft] : pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
           const f4 h2 = h2_of(ft, rt);
@@ -665,6 +695,56 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
         if (!valid) { gv = 0.f; sv = 0.f; }
         GG[tid * LDG] = gv;
         st_b = sv;
+      }
+    } else if (LN && R == 32 && A <= 8) {
+      // Beta actor, one row per 8-lane group (32 rows x 8 lanes = the workgroup), one (row, action)
+      // item per lane: the row's log-prob / entropy sums are DPP sums inside the group, every lane
+      // of the group evaluates the row's surrogate, and the head gradients are written straight to
+      // GG — no item scratch in LDS and one barrier instead of three
+      const int row = tid >> 3, ai = tid & 7;
+      const bool item = ai < A;
+      const bool valid = m0 + row < a.M;
+      const int ac = item ? ai : 0;  // lanes past A evaluate item 0 and drop it (uniform control flow)
+      const float hi = P[K.hi], lo = P[K.lo];
+      const float pa = PRE[row * LDG + ac], pbv = PRE[row * LDG + A + ac];
+      const float al = softplusf_(pa) + 1.0f, be = softplusf_(pbv) + 1.0f;
+      const float av = valid ? ACTN[row * A + ac] : 0.5f * (hi + lo);
+      float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+      s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
+      const float ab = al + be;
+      float lga, lgb, lgab, psa, psb, psab, ta, tb, tab;
+      lgamma_digamma_trigamma(al, lga, psa, ta);
+      lgamma_digamma_trigamma(be, lgb, psb, tb);
+      lgamma_digamma_trigamma(ab, lgab, psab, tab);
+      const float lpi = xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
+      const float eni = (lga + lgb) - lgab - (2.0f - ab) * psab - ((al - 1.0f) * psa + (be - 1.0f) * psb);
+      const float lp = group8_sum(item ? lpi : 0.0f), ent = group8_sum(item ? eni : 0.0f);
+      const float oldlp = valid ? ROWS[row * 8 + 1] : lp;
+      const float logratio = lp - oldlp;
+      const float ratio = expf(logratio);
+      float an = valid ? ROWS[row * 8 + 2] : 0.f;
+      if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
+      const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
+      const float pg1 = -an * ratio, pg2 = -an * rc;
+      const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+      const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
+      float g_logp = a.inv_m * (w1 * (-an) + (1.0f - w1) * (-an) * inr) * ratio;
+      float g_ent = -a.ent_coef * a.inv_m;
+      if (!valid) { g_logp = 0.f; g_ent = 0.f; }
+      if (ai == 0 && valid) {  // the row's statistics, once per row
+        st_a = fmaxf(pg1, pg2);
+        st_c = ent;
+        st_d = -logratio;
+        st_e = (ratio - 1.0f) - logratio;
+        st_f = fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
+      }
+      if (item) {
+        const float dla = ((al - 1.0f) != 0.0f ? logf(s) : 0.0f) + psab - psa;         // d lp / d alpha
+        const float dea = (ab - 2.0f) * tab - (al - 1.0f) * ta;                         // d ent / d alpha
+        const float dlb = ((be - 1.0f) != 0.0f ? logf(1.0f - s) : 0.0f) + psab - psb;  // d lp / d beta
+        const float deb = (ab - 2.0f) * tab - (be - 1.0f) * tb;                         // d ent / d beta
+        GG[row * LDG + ai] = (g_logp * dla + g_ent * dea) * softplus_d(pa);
+        GG[row * LDG + A + ai] = (g_logp * dlb + g_ent * deb) * softplus_d(pbv);
       }
     } else {
       // pass 1: per (row, action) log-prob / entropy terms and derivative pieces
@@ -748,8 +828,8 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
         }
       }
     }
-    // loss statistics: rows live in wave 0 (R <= 64); summed per lane over the tiles, reduced
-    // across lanes once after the tile loop (reported values only, no gradient depends on them)
+    // loss statistics: summed per lane over the tiles, reduced across lanes and waves once after
+    // the tile loop (reported values only, no gradient depends on them)
     lst[0] += st_a; lst[1] += st_b; lst[2] += st_c; lst[3] += st_d; lst[4] += st_e; lst[5] += st_f;
     lds_barrier();
     PPO_STAMP(7);
@@ -776,7 +856,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       for (int rt = 0; rt < RT; ++rt) gr[rt] = lds_f(GG + (rbase + 16 * rt + j) * LDG);
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
-        const f4 w = pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
+        const f4 w = NHT == 1 ? hwb[ft] : pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -789,9 +869,13 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
         f4 wT;
+        if constexpr (NHT == 1) {
+          wT = hwb[ft];
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          wT[r] = hrow_b[ht][r] >= 0 ? bld1(pb, hrow_b[ht][r] + fbase + j, 16 * ft) : 0.0f;
+          for (int r = 0; r < 4; ++r)
+            wT[r] = hrow_b[ht][r] >= 0 ? bld1(pb, hrow_b[ht][r] + fbase + j, 16 * ft) : 0.0f;
+        }
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
           const f4 gv = lds_f4(GG + (rbase + 16 * rt + j) * LDG + 16 * ht + 4 * g);
@@ -858,7 +942,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     }
     // x2 = dz2
     col_sums<FT, RT>([&](int ft, int rt, int r) { return x2[ft][rt][r]; }, acc + sg.b2, fbase, j, g);
-    store_tile_rows<FT, RT>(a.DZ2[trunk], H, x2, m0, a.M, rbase, fbase, j, g);
+    if (!PPO_DIAG_SKIP(5)) store_tile_rows<FT, RT>(a.DZ2[trunk], H, x2, m0, a.M, rbase, fbase, j, g);
     lds_barrier();  // dW3 readers of h2 are done
     lds_store_tile<FT, RT, LDA>(ACT, x2, rbase, fbase, j, g);
     lds_barrier();
@@ -917,20 +1001,27 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     }
     // z = dz1
     col_sums<FT, RT>([&](int ft, int rt, int r) { return z[ft][rt][r]; }, acc + sg.b1, fbase, j, g);
-    store_tile_rows<FT, RT>(a.DZ1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
+    if (!PPO_DIAG_SKIP(6)) store_tile_rows<FT, RT>(a.DZ1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
     PPO_STAMP(12);
   }
   // ---------------- workgroup result (row groups summed in a fixed order) ----------------
-  if (wave == 0) {
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1)
+  for (int m = 32; m >= 1; m >>= 1)
 #pragma unroll
-      for (int k = 0; k < 6; ++k) lst[k] += shfl_xor(lst[k], m);
-    if (lane == 0) {
-      float* st = ACC + sg.stats;  // row group 0's accumulator
-      st[ST_PG] += lst[0]; st[ST_V] += lst[1]; st[ST_ENT] += lst[2];
-      st[ST_OKL] += lst[3]; st[ST_KL] += lst[4]; st[ST_CF] += lst[5];
-    }
+    for (int k = 0; k < 6; ++k) lst[k] += shfl_xor(lst[k], m);
+  lds_barrier();  // RED is free
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) RED[wave * 8 + k] = lst[k];
+  }
+  lds_barrier();
+  if (tid == 0) {
+    float t[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) t[k] = (RED[k] + RED[8 + k]) + (RED[16 + k] + RED[24 + k]);
+    float* st = ACC + sg.stats;  // row group 0's accumulator
+    st[ST_PG] += t[0]; st[ST_V] += t[1]; st[ST_ENT] += t[2];
+    st[ST_OKL] += t[3]; st[ST_KL] += t[4]; st[ST_CF] += t[5];
   }
   lds_barrier();
   float* out = a.slab[trunk] + (size_t)blockIdx.x * sg.size;

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Per-phase cycle breakdown of k_upd from the diagnostic stamps build (make -C ppo.cpp_amd stamps).
 Runs one metric-config iteration (AC HalfCheetah, E=4096) and prints, per trunk, the median
-shader-clock cycles of each phase over waves and tiles 2..5 of every workgroup."""
+shader-clock cycles of each phase over waves and tiles 2..13 of every workgroup. With an output
+path argument it also saves the raw stamps ([wg, wave, tile, start + 13 phase ends + hardware id],
+uint64) for scripts/corun_analysis.py."""
 import ctypes as C
 import os
 import sys
@@ -15,7 +17,8 @@ import ppo_amd  # noqa: E402
 
 NAMES = ["top+gather", "L1 mm", "LN1+st+bar", "L2 mm issue", "LN2", "heads+bar", "PRE+bar", "loss+bar",
          "hbias+head bwd", "LN2bwd+cs+st", "dh1 mm issue", "L1 re mm", "LN1bwd+cs+st"]
-NS, NT = len(NAMES) + 1, 4
+NP = len(NAMES)
+NS, NT = NP + 2, 16
 cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=4096, num_steps=128, total_timesteps=4096 * 128 * 4)
 tr = ppo_amd.Trainer(cfg, num_envs_per_device=4096)
 tr.iterate()
@@ -25,11 +28,17 @@ n = 1024 * 4 * NT * NS
 buf = (C.c_ulonglong * n)()
 lib.ppo_diag_read_stamps.restype = C.c_int
 got = lib.ppo_diag_read_stamps(buf, C.c_long(n))
-st = np.frombuffer(buf, dtype=np.uint64).astype(np.int64).reshape(1024, 4, NT, NS)
-d = np.diff(st, axis=-1)  # [wg, wave, tile, phase]
+raw = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 4, NT, NS).copy()
+if len(sys.argv) > 1:
+    np.save(sys.argv[1], raw)
+st = raw[..., :NP + 1].astype(np.int64)
+d = np.diff(st, axis=-1)[:, :, 2:NT - 2]  # [wg, wave, tile, phase]
 for trunk, sl in (("critic", slice(0, 256)), ("actor", slice(512, 768))):
-    x = d[sl].reshape(-1, NS - 1)
+    x = d[sl].reshape(-1, NP)
     x = x[(x > 0).all(axis=1) & (x < 10**7).all(axis=1)]
+    if not len(x):
+        print(f"{trunk}: no tiles")
+        continue
     med = np.median(x, axis=0)
     tot = med.sum()
     print(f"{trunk}: {len(x)} wave-tiles, median tile {tot:.0f} cycles")

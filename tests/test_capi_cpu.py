@@ -79,3 +79,50 @@ int main(void) {
     L = O.layout_init(1, 17, 6, 256)
     assert L.P - L.train_begin == 146189
     assert O.layout_init(0, 17, 6, 64).P == 11085
+
+
+
+BAD_CONFIGS = [
+    ("num_envs", 0, "sizes must be positive"),            # empty rollout
+    ("num_steps", -1, "sizes must be positive"),
+    ("num_minibatches", 0, "sizes must be positive"),
+    ("update_epochs", 0, "sizes must be positive"),
+    ("num_minibatches", 7, "must divide by num_minibatches"),  # ragged minibatches (ac:407 asserts it too)
+    ("num_envs", 1 << 24, "batch too large"),            # T*E rows beyond a 31-bit index
+    ("hidden", 128, "hidden must be 64 or 256"),
+    ("act_dim", 0, "bad net kind / dims"),
+    ("net_kind", 5, "bad net kind / dims"),
+]
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libppo_hip.so not built")
+def test_create_rejects_bad_configs():
+    """ppo_create validates its configuration before touching the GPU: every bad shape is refused
+    with a message through ppo_last_error and no context is returned (the reference asserts the
+    same preconditions, ac:399-407). Run in a fresh interpreter: ppo_amd loads torch first, as
+    every consumer of the library must (an earlier test here maps the library without torch)."""
+    import json
+    import subprocess
+    import sys
+    script = r'''
+import ctypes, json, sys
+sys.path.insert(0, sys.argv[1])
+import ppo_amd
+lib = ppo_amd.lib()
+out = []
+for field, value, _ in json.loads(sys.argv[2]):
+    cfg = ppo_amd.HipConfig(net_kind=1, obs_dim=17, act_dim=6, hidden=256, num_envs=4096, num_steps=128,
+                            num_minibatches=4, update_epochs=4)
+    setattr(cfg, field, value)
+    ctx = ctypes.c_void_p()
+    rc = lib.ppo_create(ctypes.byref(cfg), 0, ctypes.byref(ctx))
+    out.append([rc, bool(ctx.value), lib.ppo_last_error().decode()])
+print(json.dumps(out))
+'''
+    res = subprocess.run([sys.executable, "-c", script, os.path.join(ROOT, "ppo.cpp_amd"), json.dumps(BAD_CONFIGS)],
+                         capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-2000:]
+    got = json.loads(res.stdout.strip().splitlines()[-1])
+    for (field, value, message), (rc, has_ctx, err) in zip(BAD_CONFIGS, got):
+        assert rc != 0 and not has_ctx, (field, value)
+        assert message in err, (field, value, err)

@@ -140,6 +140,108 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
   }
 }
 
+// ---- the first convolution (uint8 image, OC <= 16): input patch staged in LDS ----------------
+// k_conv's gather issues one vector-memory byte load per lane, pixel tile and k-step (with the weight
+// loads, 1.25 vector-memory instructions per MFMA), and conv1 — 15 x 25 taps per output pixel, most
+// of the network's FLOPs — was bound by that instruction rate. Here a workgroup owns a 16 x 16 tile
+// of output pixels of one sample (wave w: output rows 4w .. 4w + 3, lane j: column j): the
+// (15 S + K)^2 x IC input patch is staged in LDS as bytes with aligned dword loads (~0.2 per MFMA),
+// the weights and the im2col offsets are staged too, and every B operand is a ds_read_u8. The MFMA
+// chain, the k order and the operands of every lane are those of k_conv: the outputs are bitwise
+// equal (tested).
+constexpr int kImgTile = 16;
+template <int K, int S>
+struct ImgGeo {
+  static constexpr int TI = (kImgTile - 1) * S + K;  // input patch edge
+  static constexpr int TIP = (TI + 3) & ~3;          // patch row pitch in bytes (whole dwords)
+};
+static size_t img_lds_bytes(int IC, int K, int S, int OC) {
+  const int TI = (kImgTile - 1) * S + K, TIP = (TI + 3) & ~3, Kt = IC * K * K;
+  const size_t patch = ((size_t)IC * TI * TIP + 15) & ~(size_t)15;
+  return patch + (size_t)OC * Kt * 4 + ((size_t)Kt + 64) * 4;
+}
+
+template <int K, int S>
+__global__ __launch_bounds__(256) void k_conv_img(ConvArgs a) {
+  using G = ImgGeo<K, S>;
+  constexpr int TI = G::TI, TIP = G::TIP, DW = TIP / 4, UK = 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int KK = K * K, Kt = a.IC * KK, OC = a.OC;
+  const size_t patch = ((size_t)a.IC * TI * TIP + 15) & ~(size_t)15;
+  unsigned char* tile = smem;
+  float* wl = reinterpret_cast<float*>(smem + patch);        // [OC][Kt]
+  int* koff = reinterpret_cast<int*>(wl + (size_t)OC * Kt);  // [Kt + 64]: patch offset of tap k
+  const int tiles_x = (a.OW + kImgTile - 1) / kImgTile;
+  const int ty = (int)blockIdx.x / tiles_x, tx = (int)blockIdx.x - ty * tiles_x, smp = blockIdx.y;
+  const int x0 = tx * kImgTile * S, y0 = ty * kImgTile * S;
+  // patch rows: bytes [x0, x0 + TIP) of input rows y0 .. y0 + TI - 1 of every channel. Rows or
+  // columns past the image read the next row / channel (or zeros past the buffer): they only reach
+  // output pixels outside the image, which are not stored.
+  {
+    const unsigned char* base = a.in_u8 + (size_t)smp * a.in_stride;
+    const size_t left = (size_t)(a.n - smp) * a.in_stride;
+    const PBuf ib{__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
+                                                    (int)(left < 0xFFFFFFF0u ? left : 0xFFFFFFF0u), 0x00020000)};
+    const int plane = a.IH * a.IW, total = a.IC * TI * DW;
+    for (int e = tid; e < total; e += 256) {
+      const int ic = e / (TI * DW), rem = e - ic * (TI * DW), r = rem / DW, d = rem - r * DW;
+      const int off = ic * plane + (y0 + r) * a.IW + x0 + 4 * d;
+      const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(ib.r, off, 0, 0);
+      *reinterpret_cast<unsigned*>(tile + (ic * TI + r) * TIP + 4 * d) = v;
+    }
+  }
+  for (int e = tid; e < OC * Kt; e += 256) wl[e] = a.W[e];
+  for (int k = tid; k < Kt + 64; k += 256) {
+    const int ic = k / KK, rem = k - ic * KK, ky = rem / K, kx = rem - ky * K;
+    koff[k] = k < Kt ? (ic * TI + ky) * TIP + kx : 0;
+  }
+  __syncthreads();
+  int pix[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) pix[u] = S * (4 * wave + u) * TIP + S * j;
+  const float* wrow = wl + (size_t)(j < OC ? j : 0) * Kt;
+  const float wm = j < OC ? 1.0f : 0.0f;
+  f4 acc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc[u] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < Kt; k0 += 4 * UK) {
+    float x[UK][4], w[UK];
+#pragma unroll
+    for (int st = 0; st < UK; ++st) {
+      const int k = k0 + 4 * st + g;
+      const bool kv = k < Kt;
+      const int ko = koff[k];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int raw = tile[ko + pix[u]];
+        x[st][u] = (float)(kv ? raw : 0) * (1.0f / 255.0f);
+      }
+      w[st] = wrow[kv ? k : 0] * (kv ? wm : 0.0f);
+    }
+#pragma unroll
+    for (int st = 0; st < UK; ++st)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = mfma16(w[st], x[st][u], acc[u]);
+  }
+  const int P = a.OH * a.OW;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int oy = ty * kImgTile + 4 * wave + u, ox = tx * kImgTile + j;
+    if (oy >= a.OH || ox >= a.OW) continue;
+    float* o = a.out + (size_t)smp * a.out_stride + (size_t)oy * a.OW + ox;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int oc = 4 * g + r;
+      if (oc < OC) {
+        float y = acc[u][r] + a.b[oc];
+        if (a.relu) y = y > 0.0f ? y : 0.0f;
+        o[(size_t)oc * P] = y;
+      }
+    }
+  }
+}
+
 // value_measurements -> columns [256, 256 + NV) of the value-head input (carla_model.h:276)
 __global__ void k_carla_pack(const float* __restrict__ vmeas, float* __restrict__ feat, int n, int NV) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -216,8 +318,14 @@ __global__ __launch_bounds__(64) void k_carla_head(HeadArgs h) {
   if (h.value) h.value[r] = h.val[r];
 }
 
-int launch_conv(const ConvArgs& a, hipStream_t s) {
+int launch_conv(const ConvArgs& a, hipStream_t s, bool img = true) {
   if (a.IC * a.K * a.K > kMaxKTab) return -1;
+  if (img && a.in_u8 && a.K == 5 && a.S == 2 && a.OC <= 16 && a.IW % 4 == 0 && a.in_stride % 4 == 0 &&
+      a.OH <= 16 * 64 && img_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {
+    const int tiles = ((a.OW + kImgTile - 1) / kImgTile) * ((a.OH + kImgTile - 1) / kImgTile);
+    hipLaunchKernelGGL((k_conv_img<5, 2>), dim3(tiles, a.n), dim3(256), img_lds_bytes(a.IC, a.K, a.S, a.OC), s, a);
+    return 0;
+  }
   const long Q = (long)a.n * a.OH * a.OW;
   // several pixel tiles per wave where there are pixels to spare (B-operand reuse of every weight
   // load), one where the layer is narrow (Linear layers, the last convolutions)
@@ -270,6 +378,7 @@ struct ppo_carla {
   size_t part_floats = 0;
   float* small = nullptr;  // scalars, tensor table and norm slices (carla_train_init)
   long step = 0;
+  bool conv_img = true;  // conv1 through k_conv_img (PPO_CARLA_CONV1=0 at create: k_conv, for A/B)
   // data parallelism (ppo_carla_comm_init): one RCCL communicator, any world >= 1
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
@@ -316,6 +425,10 @@ extern "C" int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_car
   c->cfg = *cfg;
   c->L = L;
   c->device = device;
+  {
+    const char* e = getenv("PPO_CARLA_CONV1");
+    c->conv_img = !(e && e[0] == '0');
+  }
   int rc = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess ? 0 : -2;
   const size_t B = (size_t)cfg->max_batch;
   rc |= carla_alloc(&c->P, L.P);
@@ -371,7 +484,7 @@ extern "C" int ppo_carla_forward(ppo_carla_t* c, int n, const uint8_t* bev, cons
   auto conv = [&](const float* in_f, const uint8_t* in_u8, long in_stride, int IC, int IH, int IW, long w, long b,
                   float* out, long out_stride, int OC, int OH, int OW, int K, int S, int relu) {
     ConvArgs a{in_f, in_u8, in_stride, IC, IH, IW, P + w, P + b, out, out_stride, OC, OH, OW, K, S, relu, n};
-    return launch_conv(a, s);
+    return launch_conv(a, s, c->conv_img);
   };
   auto linear = [&](const float* in, long in_stride, int IN, long w, long b, float* out, long out_stride, int OUT,
                     int relu) { return conv(in, nullptr, in_stride, IN, 1, 1, w, b, out, out_stride, OUT, 1, 1, 1, 1, relu); };
@@ -657,6 +770,101 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
     }
 }
 
+// ---- conv1's weight gradient (uint8 image, OC <= 16): input patch and dZ tile staged in LDS ----
+// dW[oc][k] (+ the bias column k = Kt) = sum over output pixels of dZ[oc][px] * im2col(x)[px][k].
+// k_wgrad gathers every B operand from global memory (a byte per lane and k-step): for conv1, with
+// 18 M output pixels per 2 048-row minibatch, that instruction rate was the bound. Here workgroup c
+// walks output tiles [c * tpc, (c + 1) * tpc) (16 x 16 pixels of one sample each); per tile the
+// (15 S + K)^2 x IC uint8 patch and the OC x 256 dZ tile (zero outside the image) are staged in LDS,
+// and wave w accumulates column tiles 6w .. 6w + 5 of the [OC] x [Kt + 1] product over the tile's
+// 256 pixels (A = dZ, B = ds_read_u8 gathers), across all its tiles. Partials: part[c][OC][Kt + 1],
+// reduced by k_wsum1 / k_wsum in chunk order as k_wgrad's.
+constexpr int kWimgCT = 6;  // column tiles per wave: 4 waves x 6 x 16 = 384 >= Kt + 1 = 376
+static size_t wimg_lds_bytes(int IC, int K, int S, int OC) {
+  const int TI = (kImgTile - 1) * S + K, TIP = (TI + 3) & ~3;
+  const size_t patch = ((size_t)IC * TI * TIP + 15) & ~(size_t)15;
+  return patch + (size_t)OC * 260 * 4;
+}
+
+template <int K, int S>
+__global__ __launch_bounds__(256) void k_wgrad_img(WgradArgs a, int tiles_x, int tps, int tiles, int tpc) {
+  using G = ImgGeo<K, S>;
+  constexpr int TI = G::TI, TIP = G::TIP, DW = TIP / 4, DZP = 260;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int KK = K * K, Kt = a.Kt, OC = a.OC, plane = a.IH * a.IW;
+  const size_t patch = ((size_t)a.IC * TI * TIP + 15) & ~(size_t)15;
+  unsigned char* tile = smem;
+  float* dzl = reinterpret_cast<float*>(smem + patch);  // [OC][DZP]: pixel 16 ly + lx
+  // this lane's B columns: patch offset of tap col (gathered), or the bias / padding column
+  int ko[kWimgCT];
+  float cb[kWimgCT];  // 1 for the bias column, 0 for padding columns, -1 for gathered columns
+#pragma unroll
+  for (int u = 0; u < kWimgCT; ++u) {
+    const int col = (wave * kWimgCT + u) * 16 + j;
+    const int ic = col / KK, rem = col - ic * KK, ky = rem / K, kx = rem - ky * K;
+    ko[u] = col < Kt ? (ic * TI + ky) * TIP + kx : 0;
+    cb[u] = col < Kt ? -1.0f : (col == Kt ? 1.0f : 0.0f);
+  }
+  const float* arow = dzl + (j < OC ? j : 0) * DZP;
+  const float am = j < OC ? 1.0f : 0.0f;
+  f4 acc[kWimgCT];
+#pragma unroll
+  for (int u = 0; u < kWimgCT; ++u) acc[u] = f4{0.f, 0.f, 0.f, 0.f};
+  const size_t total_bytes = (size_t)a.n * a.x_stride;
+  const int t0 = blockIdx.x * tpc, t1 = min(tiles, t0 + tpc);
+  for (int t = t0; t < t1; ++t) {
+    const int smp = t / tps, tt = t - smp * tps;
+    const int ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    const int OH = a.OP / a.OW;
+    const int x0 = tx * kImgTile * S, y0 = ty * kImgTile * S;
+    __syncthreads();  // the previous tile's readers are done
+    {
+      const size_t sb = (size_t)smp * a.x_stride, left = total_bytes - sb;
+      const PBuf ib{__builtin_amdgcn_make_buffer_rsrc((void*)(a.x_u8 + sb), (short)0,
+                                                      (int)(left < 0xFFFFFFF0u ? left : 0xFFFFFFF0u), 0x00020000)};
+      const int tot = a.IC * TI * DW;
+      for (int e = tid; e < tot; e += 256) {
+        const int ic = e / (TI * DW), rem = e - ic * (TI * DW), r = rem / DW, d = rem - r * DW;
+        const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(ib.r, ic * plane + (y0 + r) * a.IW + x0 + 4 * d, 0, 0);
+        *reinterpret_cast<unsigned*>(tile + (ic * TI + r) * TIP + 4 * d) = v;
+      }
+      const float* dz = a.dz + (size_t)smp * a.dz_stride;
+      for (int e = tid; e < OC * 256; e += 256) {
+        const int oc = e >> 8, px = e & 255, oy = ty * kImgTile + (px >> 4), ox = tx * kImgTile + (px & 15);
+        const bool in = oy < OH && ox < a.OW;
+        const float v = dz[in ? (size_t)oc * a.OP + oy * a.OW + ox : 0];
+        dzl[oc * DZP + px] = in ? v : 0.0f;
+      }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int st = 0; st < 64; ++st) {
+      const int px = 4 * st + g, ly = px >> 4, lx = px & 15;
+      const int po = S * ly * TIP + S * lx;
+      const float av = arow[px] * am;
+#pragma unroll
+      for (int u = 0; u < kWimgCT; ++u) {
+        const int raw = tile[ko[u] + po];
+        const float xv = (float)raw * (1.0f / 255.0f);
+        const float bv = cb[u] < 0.0f ? xv : cb[u];
+        acc[u] = mfma16(av, bv, acc[u]);
+      }
+    }
+  }
+  float* out = a.part + (size_t)blockIdx.x * OC * (Kt + 1);
+#pragma unroll
+  for (int u = 0; u < kWimgCT; ++u) {
+    const int col = (wave * kWimgCT + u) * 16 + j;
+    if (col > Kt) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int oc = 4 * g + r;
+      if (oc < OC) out[(size_t)oc * (Kt + 1) + col] = acc[u][r];
+    }
+  }
+}
+
 // G[w + oc*Kt + k] / G[b + oc] = sum over chunks. Level 1 (k_wsum1) adds groups of kSumGroup
 // consecutive chunks in parallel (blockIdx.y = group), level 2 (k_wsum) adds the group sums in order:
 // a fixed order, so the result is deterministic.
@@ -936,8 +1144,33 @@ WgradPlan plan_wgrad(int OC, int Kt, long Q) {
   return p;
 }
 
-int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap, hipStream_t s) {
+int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap, hipStream_t s, bool img = true) {
   if (a.Kt > kMaxKTab || a.OP > kMaxPTab) return -1;
+  const long per = (long)a.OC * (a.Kt + 1);
+  const int OH = a.OP / a.OW;
+  if (img && a.x_u8 && a.K == 5 && a.S == 2 && a.OC <= 16 && a.Kt + 1 <= 4 * kWimgCT * 16 && a.IW % 4 == 0 &&
+      a.x_stride % 4 == 0 && wimg_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {
+    const int tiles_x = (a.OW + kImgTile - 1) / kImgTile, tiles_y = (OH + kImgTile - 1) / kImgTile;
+    const int tiles = a.n * tiles_x * tiles_y;
+    int chunks = std::min(tiles, 1024);
+    const int tpc = (tiles + chunks - 1) / chunks;
+    chunks = (tiles + tpc - 1) / tpc;
+    const int groups = (chunks + kSumGroup - 1) / kSumGroup;
+    if ((size_t)(chunks + (chunks > kSumGroup ? groups : 0)) * per <= part_cap) {
+      a.part = part;
+      hipLaunchKernelGGL((k_wgrad_img<5, 2>), dim3(chunks), dim3(256), wimg_lds_bytes(a.IC, a.K, a.S, a.OC), s, a,
+                         tiles_x, tiles_x * tiles_y, tiles, tpc);
+      const unsigned gb = (unsigned)((per + 255) / 256);
+      if (chunks > kSumGroup) {
+        float* lvl = part + (size_t)chunks * per;
+        hipLaunchKernelGGL(k_wsum1, dim3(gb, groups), dim3(256), 0, s, part, chunks, per, lvl);
+        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, lvl, groups, a.OC, a.Kt, Gw, Gb);
+      } else {
+        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, part, chunks, a.OC, a.Kt, Gw, Gb);
+      }
+      return 0;
+    }
+  }
   const WgradPlan p = plan_wgrad(a.OC, a.Kt, (long)a.n * a.OP);
   if (p.part_floats > part_cap) return -1;
   a.qchunk = p.qchunk;
@@ -952,7 +1185,6 @@ int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap
     else if (p.not_ == 2) hipLaunchKernelGGL((k_wgrad<2, kWgradNKT, false>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_wgrad<1, kWgradNKT, false>), grid, dim3(256), 0, s, a);
   }
-  const long per = (long)a.OC * (a.Kt + 1);
   const unsigned gb = (unsigned)((per + 255) / 256);
   if (p.chunks > kSumGroup) {
     // level 1 writes its group sums after the chunk partials (sized by plan_wgrad)
@@ -1111,7 +1343,7 @@ extern "C" int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc
     WgradArgs wa{dz,          dzs,         L.conv_oc[i], L.conv_oh[i] * L.conv_ow[i], L.conv_ow[i], xf,
                  i ? nullptr : bev, xs,    L.conv_ic[i], L.conv_ih[i],                L.conv_iw[i], L.conv_k[i],
                  L.conv_s[i], n,           L.conv_ic[i] * L.conv_k[i] * L.conv_k[i], 0, nullptr};
-    bad |= launch_wgrad(wa, G + L.conv_w[i], G + L.conv_b[i], c->part, c->part_floats, s);
+    bad |= launch_wgrad(wa, G + L.conv_w[i], G + L.conv_b[i], c->part, c->part_floats, s, c->conv_img);
     if (i > 0) {
       DgradArgs da{dz,           dzs,          P + L.conv_w[i], L.conv_ic[i], xf,           xs,
                    c->dact[i - 1], xs,         L.conv_ic[i],    L.conv_ih[i], L.conv_iw[i], L.conv_oc[i],

@@ -81,3 +81,48 @@ def test_errors(carla):
         run(ag, big, np.repeat(meas, 17, 0), np.repeat(vmeas, 17, 0), mode="mean")
     with pytest.raises(ppo_amd.PPOError):
         ppo_amd.CarlaAgent(max_batch=4, bev=128)  # roach encoder needs 256 x 2 x 2 at the end
+
+
+def test_staged_conv1_kernels_match_generic(monkeypatch):
+    """conv1 runs through k_conv_img / k_wgrad_img (uint8 patch staged in LDS, ds_read_u8 gathers);
+    with PPO_CARLA_CONV1=0 at create the generic k_conv / k_wgrad gather from global memory.
+    Forward: same MFMA chain and operands, every output bitwise equal (n = 7: partial 16 x 16 tiles,
+    94 = 5 x 16 + 14). Update: every gradient tensor but conv1's is bitwise equal; conv1's weight and
+    bias gradients sum the 7 x 8 836 pixels in another order (relative L2 < 1e-5); the stepped
+    parameters then differ through the clip coefficient (atol 1e-7)."""
+    import carla_torch_ref  # noqa: F401  (skip like the update tests when torch is absent)
+    n = 7
+    L = CI.layout()
+    p = CI.params(L)
+    bev, meas, vmeas, act = CI.inputs(n)
+    rng = np.random.default_rng(3)
+    old_logp = rng.normal(-2.0, 0.3, n).astype(np.float32)
+    adv = rng.normal(0.0, 1.0, n).astype(np.float32)
+    ret = rng.normal(0.0, 1.0, n).astype(np.float32)
+    old_v = rng.normal(0.0, 1.0, n).astype(np.float32)
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("PPO_CARLA_CONV1", flag)
+        ag = ppo_amd.CarlaAgent(max_batch=16, seed=7)
+        ag.load_params(p)
+        res = [run(ag, bev, meas, vmeas, mode=m, env_base=3, step_id=5) for m in ("sample", "mean", "roach")]
+        res.append(run(ag, bev, meas, vmeas, act))
+        d = [DeviceArray.from_numpy(bev, np.uint8)] + [DeviceArray.from_numpy(np.ascontiguousarray(x, np.float32))
+                                                       for x in (meas, vmeas, act, old_logp, adv, ret, old_v)]
+        ag.update(*d, lr=3e-4, clip_coef=0.2, ent_coef=0.01, vf_coef=0.5, max_grad_norm=0.5, adam_eps=1e-5)
+        res.append([ag.last_grad(), ag.params()])
+        outs.append(res)
+        ag.close()
+    for r0, r1 in zip(outs[0][:4], outs[1][:4]):
+        for x0, x1 in zip(r0, r1):
+            np.testing.assert_array_equal(x0, x1)
+    (g0, p0), (g1, p1) = outs[0][4], outs[1][4]
+    conv1 = {L.conv_w[0], L.conv_b[0]}
+    for t in range(L.ntensors):
+        o, m = L.t_off[t], L.t_len[t]
+        if o in conv1:
+            r = np.linalg.norm((g1[o:o + m] - g0[o:o + m]).astype(np.float64)) / np.linalg.norm(g0[o:o + m])
+            assert r < 1e-5, (t, r)
+        else:
+            np.testing.assert_array_equal(g1[o:o + m], g0[o:o + m])
+    np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-7)

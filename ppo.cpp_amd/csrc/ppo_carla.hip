@@ -378,7 +378,7 @@ struct ppo_carla {
   size_t part_floats = 0;
   float* small = nullptr;  // scalars, tensor table and norm slices (carla_train_init)
   long step = 0;
-  bool conv_img = true;  // conv1 through k_conv_img (PPO_CARLA_CONV1=0 at create: k_conv, for A/B)
+  bool conv_img = true;  // LDS-staged conv1 / conv2 kernels (PPO_CARLA_CONV1=0 at create: generic, for A/B)
   // data parallelism (ppo_carla_comm_init): one RCCL communicator, any world >= 1
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
@@ -647,6 +647,100 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
   }
 }
 
+// ---- stride-2 input gradient with the dZ region staged in LDS (conv2: IC 8, OC 16, K 5) --------
+// k_dgrad gathers every B operand (a dZ value) from global memory per lane and k-step. Here a
+// workgroup owns a 32 x 32 block of input pixels of one sample: the OC x 18 x 18 dZ region those
+// pixels read (zero outside the output plane) and the weights are staged in LDS. Wave w takes rows
+// 4w .. 4w + 3 of each of the four parity classes (16 x 16 pixels each), so the 9-, 6-, 6- and
+// 4-tap classes are spread evenly. Per class the k order (oc, jj, ii), the k-steps and each lane's
+// operands are those of k_dgrad: the results are bitwise equal (tested).
+constexpr int kDs2Tile = 32;                          // input pixels per block edge
+constexpr int kDs2R = kDs2Tile / 2 + 2;               // dZ region edge for K = 5, S = 2
+static size_t ds2_lds_bytes(int IC, int OC) {
+  return ((size_t)OC * kDs2R * kDs2R + (size_t)OC * IC * 25 + 4 * 2 * (16 * 9 + 16)) * 4;
+}
+
+__global__ __launch_bounds__(256) void k_dgrad_s2(DgradArgs a, int tiles_x, int tps) {
+  constexpr int K = 5, S = 2, KK = 25, R = kDs2R;
+  extern __shared__ __attribute__((aligned(16))) float dsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int OC = a.OC, IC = a.IC, OP = a.OH * a.OW;
+  float* dzl = dsm;                                // [OC][R][R]
+  float* wl = dzl + OC * R * R;                    // W[oc][ic][K][K] of this layer (w_ic == IC)
+  int* woff = reinterpret_cast<int*>(wl + OC * IC * KK);  // [4][16 * 9 + 16]
+  int* zoff = woff + 4 * (16 * 9 + 16);
+  const int smp = blockIdx.x / tps, tt = blockIdx.x - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
+  const int oy0 = ty * (kDs2Tile / 2) - 2, ox0 = tx * (kDs2Tile / 2) - 2;  // dZ region origin
+  {
+    const float* dz = a.dz + (size_t)smp * a.dz_stride;
+    for (int e = tid; e < OC * R * R; e += 256) {
+      const int oc = e / (R * R), rem = e - oc * R * R, r = rem / R, q = rem - r * R;
+      const int oy = oy0 + r, ox = ox0 + q;
+      const bool in = (unsigned)oy < (unsigned)a.OH && (unsigned)ox < (unsigned)a.OW;
+      const float v = dz[in ? (size_t)oc * OP + oy * a.OW + ox : 0];
+      dzl[e] = in ? v : 0.0f;
+    }
+    for (int e = tid; e < OC * IC * KK; e += 256) wl[e] = a.W[e];
+    for (int e = tid; e < 4 * (16 * 9 + 16); e += 256) {
+      const int c = e / (16 * 9 + 16), k = e - c * (16 * 9 + 16), py = c >> 1, px = c & 1;
+      const int nj = (K - py + S - 1) / S, ni = (K - px + S - 1) / S, Kt = OC * nj * ni;
+      const int oc = k / (nj * ni), rem = k - oc * nj * ni, jj = rem / ni, ii = rem - jj * ni;
+      const bool in = k < Kt;
+      woff[e] = in ? oc * IC * KK + (py + S * jj) * K + (px + S * ii) : 0;
+      zoff[e] = in ? oc * R * R - jj * R - ii : 0;
+    }
+  }
+  __syncthreads();
+  const int icr = j < IC ? j : 0;
+  const float wm = j < IC ? 1.0f : 0.0f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int py = c >> 1, px = c & 1;
+    const int nj = (K - py + S - 1) / S, ni = (K - px + S - 1) / S, Kt = OC * nj * ni;
+    const int* wo_c = woff + c * (16 * 9 + 16);
+    const int* zo_c = zoff + c * (16 * 9 + 16);
+    // class-local pixel (ly, lx) = (4 wave + u, j): dZ row ly + 2 - jj, column lx + 2 - ii
+    int zb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) zb[u] = (4 * wave + u + 2) * R + j + 2;
+    f4 acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < Kt; k0 += 4 * kUK) {
+      float xb[kUK][4], wa[kUK];
+#pragma unroll
+      for (int st = 0; st < kUK; ++st) {
+        const int k = k0 + 4 * st + g;
+        const bool kv = k < Kt;
+        const int wo = wo_c[k], zo = zo_c[k];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) xb[st][u] = dzl[zb[u] + zo] * (kv ? 1.0f : 0.0f);
+        wa[st] = wl[icr * KK + wo] * (kv ? wm : 0.0f);
+      }
+#pragma unroll
+      for (int st = 0; st < kUK; ++st)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] = mfma16(wa[st], xb[st][u], acc[u]);
+    }
+    const long plane = (long)a.IH * a.IW;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int iy = ty * kDs2Tile + S * (4 * wave + u) + py, ix = tx * kDs2Tile + S * j + px;
+      if (iy >= a.IH || ix >= a.IW) continue;
+      const long pix = (long)iy * a.IW + ix;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ic = 4 * g + r;
+        if (ic >= IC) continue;
+        const float xm = a.x[smp * a.x_stride + ic * plane + pix];
+        const float gv = xm > 0.0f ? acc[u][r] : 0.0f;
+        float* o = a.dx + smp * a.dx_stride + ic * plane + pix;
+        *o = a.accumulate ? *o + gv : gv;
+      }
+    }
+  }
+}
+
 struct WgradArgs {
   const float* dz;  // [n][OC][OP], sample stride dz_stride
   long dz_stride;
@@ -847,7 +941,8 @@ __global__ __launch_bounds__(256) void k_wgrad_img(WgradArgs a, int tiles_x, int
       for (int u = 0; u < kWimgCT; ++u) {
         const int raw = tile[ko[u] + po];
         const float xv = (float)raw * (1.0f / 255.0f);
-        const float bv = cb[u] < 0.0f ? xv : cb[u];
+        // columns >= Kt (bias, padding) exist only in the last tile of the last wave
+        const float bv = u == kWimgCT - 1 ? (cb[u] < 0.0f ? xv : cb[u]) : xv;
         acc[u] = mfma16(av, bv, acc[u]);
       }
     }
@@ -1097,7 +1192,13 @@ __global__ __launch_bounds__(256) void k_carla_adam(CarlaAdamArgs a) {
   a.P[p] = a.P[p] - a.step_size * (m / (sqrtf(v) / a.sbc2 + a.eps));
 }
 
-int launch_dgrad(const DgradArgs& a, hipStream_t s) {
+int launch_dgrad(const DgradArgs& a, hipStream_t s, bool staged = true) {
+  if (staged && a.K == 5 && a.S == 2 && a.IC <= 16 && a.OC <= 16 && a.w_ic == a.IC &&
+      ds2_lds_bytes(a.IC, a.OC) <= 64 * 1024) {
+    const int tiles_x = (a.IW + kDs2Tile - 1) / kDs2Tile, tps = tiles_x * ((a.IH + kDs2Tile - 1) / kDs2Tile);
+    hipLaunchKernelGGL(k_dgrad_s2, dim3(a.n * tps), dim3(256), ds2_lds_bytes(a.IC, a.OC), s, a, tiles_x, tps);
+    return 0;
+  }
   const int nj = (a.K + a.S - 1) / a.S;
   if ((long)a.OC * nj * nj > kMaxDTab) return -1;
   const int H2 = (a.IH + a.S - 1) / a.S, W2 = (a.IW + a.S - 1) / a.S;
@@ -1148,7 +1249,8 @@ int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap
   if (a.Kt > kMaxKTab || a.OP > kMaxPTab) return -1;
   const long per = (long)a.OC * (a.Kt + 1);
   const int OH = a.OP / a.OW;
-  if (img && a.x_u8 && a.K == 5 && a.S == 2 && a.OC <= 16 && a.Kt + 1 <= 4 * kWimgCT * 16 && a.IW % 4 == 0 &&
+  if (img && a.x_u8 && a.K == 5 && a.S == 2 && a.OC <= 16 && a.Kt + 1 <= 4 * kWimgCT * 16 &&
+      a.Kt >= (4 * kWimgCT - 1) * 16 && a.IW % 4 == 0 &&
       a.x_stride % 4 == 0 && wimg_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {
     const int tiles_x = (a.OW + kImgTile - 1) / kImgTile, tiles_y = (OH + kImgTile - 1) / kImgTile;
     const int tiles = a.n * tiles_x * tiles_y;
@@ -1348,7 +1450,7 @@ extern "C" int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc
       DgradArgs da{dz,           dzs,          P + L.conv_w[i], L.conv_ic[i], xf,           xs,
                    c->dact[i - 1], xs,         L.conv_ic[i],    L.conv_ih[i], L.conv_iw[i], L.conv_oc[i],
                    L.conv_oh[i], L.conv_ow[i], L.conv_k[i],     L.conv_s[i],  n,            0};
-      bad |= launch_dgrad(da, s);
+      bad |= launch_dgrad(da, s, c->conv_img);
     }
   }
   if (bad) return ppo_fail("ppo_carla_update: no gradient kernel for this shape", -1);

@@ -42,6 +42,8 @@ struct ConvArgs {
   int OC, OH, OW;
   int K, S, relu;
   int n;
+  float* part;  // split-K partial sums [Z][n * OH * OW][OC] (launch_conv sets kc and part)
+  int kc;       // k-range per blockIdx.z (0: no split)
 };
 
 constexpr int kConvWaves = 4;
@@ -91,12 +93,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
     ocv[t] = oc < a.OC;
     wrow[t] = a.W + (long)(ocv[t] ? oc : 0) * Kt;
   }
-  for (int k0 = 0; k0 < Kt; k0 += 4 * kUK) {
+  const int kbeg = a.kc ? (int)blockIdx.z * a.kc : 0, kend = a.kc ? min(Kt, kbeg + a.kc) : Kt;
+  for (int k0 = kbeg; k0 < kend; k0 += 4 * kUK) {
     float x[kUK][NP], w[kUK][NOT];
 #pragma unroll
     for (int st = 0; st < kUK; ++st) {
       const int k = k0 + 4 * st + g;
-      const bool kv = k < Kt;
+      const bool kv = k < kend;
       const int ko = koff[k];
 #pragma unroll
       for (int u = 0; u < NP; ++u) {
@@ -122,6 +125,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
         for (int u = 0; u < NP; ++u) acc[t][u] = mfma16(w[st][t], x[st][u], acc[t][u]);
   }
   // lane (j, g) holds out channel oc0 + 16t + 4g + r of pixel q0 + 16u + j
+  if (a.kc) {  // split K: raw partial sums, added in z order by k_conv_fin
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      if (!qv[u]) continue;
+      float* o = a.part + ((size_t)blockIdx.z * Q + q0 + 16 * u + j) * a.OC;
+#pragma unroll
+      for (int t = 0; t < NOT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int oc = oc0 + 16 * t + 4 * g + r;
+          if (oc < a.OC) o[oc] = acc[t][u][r];
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < NP; ++u) {
     if (!qv[u]) continue;
@@ -139,6 +157,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
       }
   }
 }
+
+// split-K finish: out = relu(sum over z of the partials, in z order, + bias)
+__global__ __launch_bounds__(256) void k_conv_fin(ConvArgs a, int Z) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const int P = a.OH * a.OW;
+  const long Q = (long)a.n * P;
+  if (i >= Q * a.OC) return;
+  const long q = i / a.OC;
+  const int oc = (int)(i - q * a.OC);
+  float v = 0.f;
+  for (int z = 0; z < Z; ++z) v += a.part[(size_t)z * Q * a.OC + i];
+  float y = v + a.b[oc];
+  if (a.relu) y = y > 0.0f ? y : 0.0f;
+  const long smp = q / P;
+  a.out[smp * a.out_stride + (long)oc * P + (q - smp * P)] = y;
+}
+
+// split-K policy, by layer shape only (so every output element sums its k range in the same
+// chunks for any batch): few output pixels per sample and a deep reduction — the Linear layers,
+// conv5 and conv6 — get 128-wide k chunks. With few rows (the rollout's batches) those layers
+// otherwise run a handful of workgroups whose waves each walk the whole reduction as one
+// latency-bound load chain.
+constexpr int kSplitKC = 128;
+static int conv_split_z(int Kt, int P) { return (P <= 16 && Kt >= 256) ? (Kt + kSplitKC - 1) / kSplitKC : 1; }
 
 // ---- the first convolution (uint8 image, OC <= 16): input patch staged in LDS ----------------
 // k_conv's gather issues one vector-memory byte load per lane, pixel tile and k-step (with the weight
@@ -332,11 +374,14 @@ int launch_conv(const ConvArgs& a, hipStream_t s, bool img = true) {
   const int np = Q >= 16L * 4 * 2048 ? 4 : 1;
   const unsigned gx = (unsigned)((Q + 16 * kConvWaves * np - 1) / (16 * kConvWaves * np));
   const bool u8 = a.in_u8 != nullptr;
+  const int Z = (a.part && !u8) ? conv_split_z(a.IC * a.K * a.K, a.OH * a.OW) : 1;
+  ConvArgs b = a;
+  b.kc = Z > 1 ? kSplitKC : 0;
 #define PPO_CONV_LAUNCH(NOT_, NP_)                                                                          \
   do {                                                                                                     \
-    const dim3 grid(gx, (a.OC + 16 * NOT_ - 1) / (16 * NOT_));                                             \
-    if (u8) hipLaunchKernelGGL((k_conv<NOT_, NP_, true>), grid, dim3(256), 0, s, a);                        \
-    else hipLaunchKernelGGL((k_conv<NOT_, NP_, false>), grid, dim3(256), 0, s, a);                          \
+    const dim3 grid(gx, (a.OC + 16 * NOT_ - 1) / (16 * NOT_), Z);                                          \
+    if (u8) hipLaunchKernelGGL((k_conv<NOT_, NP_, true>), grid, dim3(256), 0, s, b);                        \
+    else hipLaunchKernelGGL((k_conv<NOT_, NP_, false>), grid, dim3(256), 0, s, b);                          \
   } while (0)
   if (a.OC >= 64) {
     if (np == 4) PPO_CONV_LAUNCH(4, 4);
@@ -349,6 +394,7 @@ int launch_conv(const ConvArgs& a, hipStream_t s, bool img = true) {
     else PPO_CONV_LAUNCH(1, 1);
   }
 #undef PPO_CONV_LAUNCH
+  if (Z > 1) hipLaunchKernelGGL(k_conv_fin, dim3((unsigned)((Q * a.OC + 255) / 256)), dim3(256), 0, s, b, Z);
   return 0;
 }
 
@@ -367,6 +413,7 @@ struct ppo_carla {
   float *enc = nullptr, *s1 = nullptr, *l1 = nullptr, *feat = nullptr, *v1 = nullptr, *v2 = nullptr, *val = nullptr;
   float *p1 = nullptr, *p2 = nullptr;
   float* hpre = nullptr;  // [B][2A]
+  float* ksplit = nullptr;  // split-K partials of the forward's narrow layers (conv_split_z)
   // training state (allocated on the first ppo_carla_update)
   bool train_ready = false;
   float *G = nullptr, *m = nullptr, *v = nullptr;        // [P]
@@ -397,7 +444,7 @@ extern "C" int ppo_carla_destroy(ppo_carla_t* c) {
   float* bufs[] = {c->P,    c->enc,  c->s1,  c->l1,  c->feat,  c->v1,  c->v2,      c->val,  c->p1,
                    c->p2,   c->hpre, c->G,   c->m,   c->v,     c->denc, c->ds1,     c->dl1,  c->dfeat,
                    c->dv1,  c->dv2,  c->dp1, c->dp2, c->dhead, c->dval, c->lp,      c->ent,  c->rowstat,
-                   c->part, c->small};
+                   c->part, c->small,  c->ksplit};
   for (float* b : bufs)
     if (b) (void)hipFree(b);
   for (float* b : c->act)
@@ -444,6 +491,18 @@ extern "C" int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_car
   rc |= carla_alloc(&c->p1, B * 256);
   rc |= carla_alloc(&c->p2, B * 256);
   rc |= carla_alloc(&c->hpre, B * 2 * L.A);
+  {  // the largest split-K partial buffer of the forward's layers
+    size_t m = 0;
+    auto need = [&](int Kt, int P, int OC) {
+      const int Z = conv_split_z(Kt, P);
+      if (Z > 1) m = std::max(m, (size_t)Z * B * P * OC);
+    };
+    for (int i = 1; i < PPO_CARLA_NCONV; ++i)
+      need(L.conv_ic[i] * L.conv_k[i] * L.conv_k[i], L.conv_oh[i] * L.conv_ow[i], L.conv_oc[i]);
+    need(L.NM, 1, 256); need(256, 1, 256); need(1280, 1, 512); need(512, 1, 256);
+    need(256 + L.NV, 1, 256); need(256, 1, 256); need(256, 1, 1);
+    if (m) rc |= carla_alloc(&c->ksplit, m);
+  }
   if (rc || hipDeviceSynchronize() != hipSuccess) {
     ppo_carla_destroy(c);
     return ppo_fail("ppo_carla_create: device allocation failed", -2);
@@ -483,7 +542,8 @@ extern "C" int ppo_carla_forward(ppo_carla_t* c, int n, const uint8_t* bev, cons
   const float* P = c->P;
   auto conv = [&](const float* in_f, const uint8_t* in_u8, long in_stride, int IC, int IH, int IW, long w, long b,
                   float* out, long out_stride, int OC, int OH, int OW, int K, int S, int relu) {
-    ConvArgs a{in_f, in_u8, in_stride, IC, IH, IW, P + w, P + b, out, out_stride, OC, OH, OW, K, S, relu, n};
+    ConvArgs a{in_f, in_u8, in_stride, IC, IH, IW, P + w, P + b, out, out_stride, OC, OH, OW, K, S, relu, n,
+               c->ksplit, 0};
     return launch_conv(a, s, c->conv_img);
   };
   auto linear = [&](const float* in, long in_stride, int IN, long w, long b, float* out, long out_stride, int OUT,

@@ -371,7 +371,7 @@ int launch_conv(const ConvArgs& a, hipStream_t s, bool img = true) {
   const long Q = (long)a.n * a.OH * a.OW;
   // several pixel tiles per wave where there are pixels to spare (B-operand reuse of every weight
   // load), one where the layer is narrow (Linear layers, the last convolutions)
-  const int np = Q >= 16L * 4 * 2048 ? 4 : 1;
+  const int np = Q >= 16L * 4 * 1024 ? 4 : 1;
   const unsigned gx = (unsigned)((Q + 16 * kConvWaves * np - 1) / (16 * kConvWaves * np));
   const bool u8 = a.in_u8 != nullptr;
   const int Z = (a.part && !u8) ? conv_split_z(a.IC * a.K * a.K, a.OH * a.OW) : 1;
@@ -1263,7 +1263,7 @@ int launch_dgrad(const DgradArgs& a, hipStream_t s, bool staged = true) {
   if ((long)a.OC * nj * nj > kMaxDTab) return -1;
   const int H2 = (a.IH + a.S - 1) / a.S, W2 = (a.IW + a.S - 1) / a.S;
   const long Q = (long)a.n * H2 * W2;
-  const int np = Q >= 16L * 4 * 2048 ? 4 : 1;
+  const int np = Q >= 16L * 4 * 1024 ? 4 : 1;
   const unsigned gx = (unsigned)((Q + 64L * np - 1) / (64L * np));
   const unsigned gz = (unsigned)(a.S * a.S);
   if (a.IC >= 64) {

@@ -200,7 +200,7 @@ struct ImgGeo {
 static size_t img_lds_bytes(int IC, int K, int S, int OC) {
   const int TI = (kImgTile - 1) * S + K, TIP = (TI + 3) & ~3, Kt = IC * K * K;
   const size_t patch = ((size_t)IC * TI * TIP + 15) & ~(size_t)15;
-  return patch + (size_t)OC * Kt * 4 + ((size_t)Kt + 64) * 4;
+  return patch + (size_t)OC * (Kt + 64) * 4 + ((size_t)Kt + 64) * 4;
 }
 
 template <int K, int S>
@@ -212,8 +212,9 @@ __global__ __launch_bounds__(256) void k_conv_img(ConvArgs a) {
   const int KK = K * K, Kt = a.IC * KK, OC = a.OC;
   const size_t patch = ((size_t)a.IC * TI * TIP + 15) & ~(size_t)15;
   unsigned char* tile = smem;
-  float* wl = reinterpret_cast<float*>(smem + patch);        // [OC][Kt]
-  int* koff = reinterpret_cast<int*>(wl + (size_t)OC * Kt);  // [Kt + 64]: patch offset of tap k
+  const int Ktp = Kt + 64;                                    // weight row pitch: zeros past Kt
+  float* wl = reinterpret_cast<float*>(smem + patch);         // [OC][Ktp]
+  int* koff = reinterpret_cast<int*>(wl + (size_t)OC * Ktp);  // [Ktp]: patch offset of tap k (0 past Kt)
   const int tiles_x = (a.OW + kImgTile - 1) / kImgTile;
   const int ty = (int)blockIdx.x / tiles_x, tx = (int)blockIdx.x - ty * tiles_x, smp = blockIdx.y;
   const int x0 = tx * kImgTile * S, y0 = ty * kImgTile * S;
@@ -233,7 +234,10 @@ __global__ __launch_bounds__(256) void k_conv_img(ConvArgs a) {
       *reinterpret_cast<unsigned*>(tile + (ic * TI + r) * TIP + 4 * d) = v;
     }
   }
-  for (int e = tid; e < OC * Kt; e += 256) wl[e] = a.W[e];
+  for (int e = tid; e < OC * Ktp; e += 256) {
+    const int oc = e / Ktp, k = e - oc * Ktp;
+    wl[e] = k < Kt ? a.W[oc * Kt + k] : 0.0f;
+  }
   for (int k = tid; k < Kt + 64; k += 256) {
     const int ic = k / KK, rem = k - ic * KK, ky = rem / K, kx = rem - ky * K;
     koff[k] = k < Kt ? (ic * TI + ky) * TIP + kx : 0;
@@ -242,24 +246,22 @@ __global__ __launch_bounds__(256) void k_conv_img(ConvArgs a) {
   int pix[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) pix[u] = S * (4 * wave + u) * TIP + S * j;
-  const float* wrow = wl + (size_t)(j < OC ? j : 0) * Kt;
+  const float* wrow = wl + (size_t)(j < OC ? j : 0) * Ktp;
   const float wm = j < OC ? 1.0f : 0.0f;
   f4 acc[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) acc[u] = f4{0.f, 0.f, 0.f, 0.f};
+  // taps past Kt read offset 0 of the patch (a finite value) against a zero weight: the product is
+  // +0, as k_conv's masked operands give, so no per-step masks are needed
   for (int k0 = 0; k0 < Kt; k0 += 4 * UK) {
     float x[UK][4], w[UK];
 #pragma unroll
     for (int st = 0; st < UK; ++st) {
       const int k = k0 + 4 * st + g;
-      const bool kv = k < Kt;
       const int ko = koff[k];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int raw = tile[ko + pix[u]];
-        x[st][u] = (float)(kv ? raw : 0) * (1.0f / 255.0f);
-      }
-      w[st] = wrow[kv ? k : 0] * (kv ? wm : 0.0f);
+      for (int u = 0; u < 4; ++u) x[st][u] = (float)tile[ko + pix[u]] * (1.0f / 255.0f);
+      w[st] = wrow[k] * wm;
     }
 #pragma unroll
     for (int st = 0; st < UK; ++st)

@@ -364,7 +364,8 @@ __global__ __launch_bounds__(64) void k_carla_head(HeadArgs h) {
 
 int launch_conv(const ConvArgs& a, hipStream_t s, bool img = true) {
   if (a.IC * a.K * a.K > kMaxKTab) return -1;
-  if (img && a.in_u8 && a.K == 5 && a.S == 2 && a.OC <= 16 && a.IW % 4 == 0 && a.in_stride % 4 == 0 &&
+  if (img && a.in_u8 && ((uintptr_t)a.in_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 16 && a.IW % 4 == 0 &&
+      a.in_stride % 4 == 0 &&
       a.OH <= 16 * 64 && img_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {
     const int tiles = ((a.OW + kImgTile - 1) / kImgTile) * ((a.OH + kImgTile - 1) / kImgTile);
     hipLaunchKernelGGL((k_conv_img<5, 2>), dim3(tiles, a.n), dim3(256), img_lds_bytes(a.IC, a.K, a.S, a.OC), s, a);
@@ -1311,7 +1312,8 @@ int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap
   if (a.Kt > kMaxKTab || a.OP > kMaxPTab) return -1;
   const long per = (long)a.OC * (a.Kt + 1);
   const int OH = a.OP / a.OW;
-  if (img && a.x_u8 && a.K == 5 && a.S == 2 && a.OC <= 16 && a.Kt + 1 <= 4 * kWimgCT * 16 &&
+  if (img && a.x_u8 && ((uintptr_t)a.x_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 16 &&
+      a.Kt + 1 <= 4 * kWimgCT * 16 &&
       a.Kt >= (4 * kWimgCT - 1) * 16 && a.IW % 4 == 0 &&
       a.x_stride % 4 == 0 && wimg_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {
     const int tiles_x = (a.OW + kImgTile - 1) / kImgTile, tiles_y = (OH + kImgTile - 1) / kImgTile;

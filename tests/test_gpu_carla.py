@@ -128,3 +128,19 @@ def test_staged_conv1_kernels_match_generic(monkeypatch):
         else:
             np.testing.assert_array_equal(g1[o:o + m], g0[o:o + m])
     np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-7)
+
+
+def test_unaligned_image_pointer(carla):
+    """The staged first-layer kernels load the uint8 image as dwords: an image pointer that is not
+    4-byte aligned takes the generic gather path and gives the same outputs, bitwise."""
+    ag = carla[0]
+    n = 3
+    bev, meas, vmeas, _ = CI.inputs(n)
+    ref = run(ag, bev, meas, vmeas, mode="mean")
+    raw = np.zeros(bev.size + 4, np.uint8)
+    raw[1:1 + bev.size] = bev.ravel()
+    buf = DeviceArray.from_numpy(raw, np.uint8)
+    shifted = DeviceArray.wrap(buf.ptr + 1, bev.shape, np.uint8)
+    out = ag.forward(shifted, DeviceArray.from_numpy(meas), DeviceArray.from_numpy(vmeas), sample_type="mean")
+    for r, o in zip(ref, out):
+        np.testing.assert_array_equal(o.numpy(), r)

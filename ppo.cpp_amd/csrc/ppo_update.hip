@@ -465,33 +465,67 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       if (trunk == 1 && idx < R * A) ACTN[idx] = vac[k];
     }
   };
+  // wide inputs: the tile's loads go out in chunks of GC items from clamped indices (the chunk's
+  // permutation entries, then its observation values), masked afterwards — a load under a per-lane
+  // branch would wait for itself, one dependent round trip pair per item
   auto gather_sync = [&](int itc) {
     const int mb = itc * R;
-    for (int idx = tid; idx < R * OP; idx += 256) {
-      const int row = idx / OP, f = idx - row * OP, m = mb + row;
-      float v = 0.f;
-      if (m < a.M && f < O) {
-        v = a.obs[(long)a.perm[m] * O + f];
-        if constexpr (LN) v = (v - SOM[f]) / SOS[f];
+    constexpr int NGS = (R * OP + 255) / 256, GC = 4;
+#pragma unroll 1
+    for (int k0 = 0; k0 < NGS; k0 += GC) {
+      int rp[GC];
+      float v[GC];
+#pragma unroll
+      for (int c = 0; c < GC; ++c) {
+        const int idx = tid + 256 * (k0 + c), row = min(idx / OP, R - 1);
+        rp[c] = a.perm[min(mb + row, a.M - 1)];
       }
-      XN[row * LDX + f] = v;
-      if (trunk == 0 && m < a.M && !PPO_DIAG_SKIP(7)) a.Xn[(size_t)m * OP + f] = v;
+#pragma unroll
+      for (int c = 0; c < GC; ++c) {
+        const int idx = tid + 256 * (k0 + c), f = idx - (idx / OP) * OP;
+        v[c] = a.obs[(long)rp[c] * O + min(f, O - 1)];
+      }
+#pragma unroll
+      for (int c = 0; c < GC; ++c) {
+        const int idx = tid + 256 * (k0 + c), row = idx / OP, f = idx - row * OP, m = mb + row;
+        if (k0 + c < NGS && idx < R * OP) {
+          const bool ok = m < a.M && f < O;
+          float x = ok ? v[c] : 0.f;
+          if constexpr (LN)
+            if (ok) x = (x - SOM[f]) / SOS[f];
+          XN[row * LDX + f] = x;
+          if (trunk == 0 && m < a.M && !PPO_DIAG_SKIP(7)) a.Xn[(size_t)m * OP + f] = x;
+        }
+      }
     }
-    if (tid < R) {
-      const int m = mb + tid;
-      float r1 = 0.f, r2 = 0.f;
-      if (m < a.M) {
-        const long b = a.perm[m];
-        if (trunk == 0) { r1 = a.ret[b]; r2 = a.val[b]; }
-        else { r1 = a.logp[b]; r2 = a.adv[b]; }
+    {
+      const int rrow = a.perm[min(mb + min(tid, R - 1), a.M - 1)];
+      const float r1 = trunk == 0 ? a.ret[rrow] : a.logp[rrow];
+      const float r2 = trunk == 0 ? a.val[rrow] : a.adv[rrow];
+      if (tid < R) {
+        const bool ok = mb + tid < a.M;
+        ROWS[tid * 8 + 1] = ok ? r1 : 0.f;
+        ROWS[tid * 8 + 2] = ok ? r2 : 0.f;
       }
-      ROWS[tid * 8 + 1] = r1;
-      ROWS[tid * 8 + 2] = r2;
     }
     if (trunk == 1) {
-      for (int idx = tid; idx < R * A; idx += 256) {
-        const int row = idx / A, ai = idx - row * A, m = mb + row;
-        ACTN[idx] = m < a.M ? a.actions[(long)a.perm[m] * A + ai] : 0.f;
+      constexpr int NAS = (R * PPO_UPD_MAXA + 255) / 256;
+      int ap[NAS];
+#pragma unroll
+      for (int k = 0; k < NAS; ++k) {
+        const int idx = tid + 256 * k, row = min(idx / (A > 0 ? A : 1), R - 1);
+        ap[k] = a.perm[min(mb + row, a.M - 1)];
+      }
+      float av[NAS];
+#pragma unroll
+      for (int k = 0; k < NAS; ++k) {
+        const int idx = tid + 256 * k, ai = idx - (idx / (A > 0 ? A : 1)) * A;
+        av[k] = a.actions[(long)ap[k] * A + ai];
+      }
+#pragma unroll
+      for (int k = 0; k < NAS; ++k) {
+        const int idx = tid + 256 * k, m = mb + idx / (A > 0 ? A : 1);
+        if (idx < R * A) ACTN[idx] = m < a.M ? av[k] : 0.f;
       }
     }
   };

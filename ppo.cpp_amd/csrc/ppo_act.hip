@@ -51,15 +51,16 @@ struct ActGeo {
 
 // one Linear layer for this wave's 2 output tiles x RT row tiles:
 // acc[u][rt] (+)= W[32 w + 16 u + i][:] . IN[16 rt + j][:], A-operands streamed through a PD-deep
-// register ring; bfrag(t, rt) = this lane's B f4 for k-block t of row tile rt
-template <int NKB, int PD, int LDW, int RT, typename BF>
+// register ring from the swizzled copy (sw_index: tile u, k-block t at wlane + 256 (NKB u + t));
+// bfrag(t, rt) = this lane's B f4 for k-block t of row tile rt
+template <int NKB, int PD, int RT, typename BF>
 PPO_DEV void act_layer(f4 (&acc)[2][RT], PBuf wb, int wlane, BF bfrag) {
   constexpr int D = PD < NKB ? PD : NKB;
   f4 w[D][2];
 #pragma unroll
   for (int p = 0; p < D; ++p)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) w[p][u] = pld4(wb, wlane, 16 * u * LDW + 16 * p);
+    for (int u = 0; u < 2; ++u) w[p][u] = pld4(wb, wlane, 256 * (NKB * u + p));
   // keep the scheduler from sinking the ring loads towards their uses (it otherwise re-issues
   // them two k-blocks ahead and waits vmcnt(0) every block)
   __builtin_amdgcn_sched_barrier(0);
@@ -78,7 +79,7 @@ PPO_DEV void act_layer(f4 (&acc)[2][RT], PBuf wb, int wlane, BF bfrag) {
     }
     if (t + D < NKB) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) w[t % D][u] = pld4(wb, wlane, 16 * u * LDW + 16 * (t + D));
+      for (int u = 0; u < 2; ++u) w[t % D][u] = pld4(wb, wlane, 256 * (NKB * u + t + D));
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -278,7 +279,8 @@ __global__ __launch_bounds__(512) void k_act3(ActArgs a) {
     for (int rt = 0; rt < RT; ++rt) acc[u][rt] = bv;
   }
   const float* xin = XS + j * LDX + 4 * g;
-  act_layer<NTO, 8, OP, RT>(acc, pb, T.W1 + (32 * wave + j) * OP + 4 * g,
+  const PBuf wsw = make_pbuf(a.WSW[trunk], (int)sw_size(H, OP));
+  act_layer<NTO, 8, RT>(acc, wsw, ((2 * wave) * NTO * 64 + lane) * 4,
                             [&](int t, int rt) { return *reinterpret_cast<const f4*>(xin + 16 * rt * LDX + 16 * t); });
   // staged params land in LDS (visible after the next barrier)
 #pragma unroll
@@ -307,7 +309,7 @@ __global__ __launch_bounds__(512) void k_act3(ActArgs a) {
   const int diag = a.kernel >> 8;
   if (!(diag & 1))
 #endif
-  act_layer<16, 8, H, RT>(acc, pb, T.W2 + (32 * wave + j) * H + 4 * g,
+  act_layer<16, 8, RT>(acc, wsw, H * OP + ((2 * wave) * 16 * 64 + lane) * 4,
                           [&](int t, int rt) { return *reinterpret_cast<const f4*>(hin + 16 * rt * LDH + 16 * t); });
 #ifdef PPO_STAMPS
   if (!(diag & 2))

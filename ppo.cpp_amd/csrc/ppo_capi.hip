@@ -139,6 +139,7 @@ struct ppo_ctx {
   long B = 0;
   int M = 0, nmb = 0;
   float *P = nullptr, *G = nullptr, *Am = nullptr, *Av = nullptr, *W2T[2] = {nullptr, nullptr};
+  float* WSW[2] = {nullptr, nullptr};  // swizzled W1 | W2 | W2^T per trunk (sw_index)
   float* buf[PPO_BUF_COUNT] = {};
   float* next_value = nullptr;
   int32_t* perms = nullptr;
@@ -305,6 +306,7 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   const size_t PS = c->K.size;
   rc |= dmalloc(&c->P, PS); rc |= dmalloc(&c->G, PS); rc |= dmalloc(&c->Am, PS); rc |= dmalloc(&c->Av, PS);
   for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->W2T[k], (size_t)H * H);
+  for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->WSW[k], (size_t)sw_size(H, c->K.OP));
   const size_t E = cfg->num_envs, T = cfg->num_steps;
   rc |= dmalloc(&c->buf[PPO_BUF_OBS], T * E * O);
   rc |= dmalloc(&c->buf[PPO_BUF_ACTIONS], T * E * A);
@@ -373,7 +375,7 @@ extern "C" int ppo_destroy(ppo_t* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   prof_drain(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
-  float* ptrs[] = {c->P, c->G, c->Am, c->Av, c->W2T[0], c->W2T[1], c->next_value, c->advstats, c->advsq, c->Xn,
+  float* ptrs[] = {c->P, c->G, c->Am, c->Av, c->W2T[0], c->W2T[1], c->WSW[0], c->WSW[1], c->next_value, c->advstats, c->advsq, c->Xn,
                    c->normout, c->gnpart, c->mbstats};
   for (float* p : ptrs)
     if (p) (void)hipFree(p);
@@ -419,6 +421,8 @@ extern "C" float* ppo_buffer(ppo_t* c, int which) {
 // ------------------------------------------------------------------------------------------
 static int refresh_w2t(ppo_t* c) {
   for (int k = 0; k < 2; ++k) launch_transpose(c->P + c->K.tr[k].W2, c->W2T[k], c->K.H, c->stream);
+  for (int k = 0; k < 2; ++k)
+    launch_swizzle(c->P + c->K.tr[k].W1, c->P + c->K.tr[k].W2, c->WSW[k], c->K.H, c->K.OP, c->stream);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -488,6 +492,8 @@ static ActArgs base_act(ppo_t* c) {
   a.store_step = -1;
   a.E = c->cfg.num_envs;
   a.kernel = c->act_kernel;
+  a.WSW[0] = c->WSW[0];
+  a.WSW[1] = c->WSW[1];
   return a;
 }
 
@@ -668,6 +674,8 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   u.P = c->P;
   u.W2T[0] = c->W2T[0];
   u.W2T[1] = c->W2T[1];
+  u.WSW[0] = c->WSW[0];
+  u.WSW[1] = c->WSW[1];
   u.K = c->K;
   u.sg[0] = c->sg[0];
   u.sg[1] = c->sg[1];
@@ -785,9 +793,12 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   ad.max_norm = cfg.max_grad_norm;
   ad.eps = cfg.adam_eps;
   ad.H = H;
+  ad.OP = c->K.OP;
   for (int k = 0; k < 2; ++k) {
     ad.w2_off[k] = c->K.tr[k].W2;
     ad.w2t[k] = c->W2T[k];
+    ad.w1_off[k] = c->K.tr[k].W1;
+    ad.wsw[k] = c->WSW[k];
   }
   const long trainable_n = c->K.size - tb;
 

@@ -16,6 +16,7 @@
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 #define PPO_DEV __device__ __forceinline__
+#define PPO_DEV_HOST __host__ __device__
 
 // ------------------------------------------------------------------------------------------
 // RNG contract (mirrored by oracle/ppo_oracle.c)

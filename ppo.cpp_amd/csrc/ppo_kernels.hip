@@ -1144,7 +1144,29 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
     if (o >= 0 && o < (long)a.H * a.H) {
       const int r = (int)(o / a.H), cI = (int)(o % a.H);
       a.w2t[k][(size_t)cI * a.H + r] = np;
+      if (a.wsw[k]) {
+        float* w = a.wsw[k] + (long)a.H * a.OP;
+        w[sw_index(r, cI, a.H)] = np;
+        w[(long)a.H * a.H + sw_index(cI, r, a.H)] = np;
+      }
     }
+    const long o1 = p - a.w1_off[k];
+    if (a.wsw[k] && o1 >= 0 && o1 < (long)a.H * a.OP) a.wsw[k][sw_index((int)(o1 / a.OP), (int)(o1 % a.OP), a.OP)] = np;
+  }
+}
+
+// swizzled copies of one trunk (sw_index): [W1 (H x OP) | W2 (H x H) | W2^T (H x H)]
+__global__ void k_swizzle(const float* __restrict__ w1, const float* __restrict__ w2, float* __restrict__ dst, int H,
+                          int OP) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n1 = (long)H * OP, n2 = (long)H * H;
+  if (i < n1) {
+    dst[sw_index((int)(i / OP), (int)(i % OP), OP)] = w1[i];
+  } else if (i < n1 + n2) {
+    const long o = i - n1;
+    const int r = (int)(o / H), c = (int)(o % H);
+    dst[n1 + sw_index(r, c, H)] = w2[o];
+    dst[n1 + n2 + sw_index(c, r, H)] = w2[o];
   }
 }
 
@@ -1584,6 +1606,10 @@ void launch_adam(const AdamArgs& a, hipStream_t s) {
 }
 void launch_transpose(const float* src, float* dst, int H, hipStream_t s) {
   hipLaunchKernelGGL(k_transpose, dim3((H * H + 255) / 256), dim3(256), 0, s, src, dst, H);
+}
+void launch_swizzle(const float* w1, const float* w2, float* dst, int H, int OP, hipStream_t s) {
+  const long n = (long)H * OP + (long)H * H;
+  hipLaunchKernelGGL(k_swizzle, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w1, w2, dst, H, OP);
 }
 void launch_gae(const GaeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_gae, dim3((a.E + 255) / 256), dim3(256), 0, s, a);

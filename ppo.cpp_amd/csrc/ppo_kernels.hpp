@@ -33,11 +33,24 @@ struct ActArgs {
   const float* next_done;
   float *s_obs, *s_actions, *s_logp, *s_dones, *s_values;
   int kernel;  // 0: fastest for the shape; 2 / 4: force k_act2 / k_act4 (A/B comparisons)
+  const float* WSW[2];  // swizzled W1 | W2 | W2^T per trunk (k_act3)
 };
+
+// A-operand ("swizzled") copies of a trunk's weight matrices: the 16 x 16 block (feature block fb,
+// k-block kb) of a row-major [NR][NC] matrix is stored as 64 lane-major float4s, lane (j, g) =
+// j + 16 g holding row 16 fb + j, columns 16 kb + 4 g .. + 3, i.e. exactly the float4 that lane
+// reads as its MFMA A operand, so one wave-load reads 1 KB contiguous (the row-major layout reads
+// 16 rows x 64 B: ~2.6x less L2 throughput, scripts/probe/l2bw_probe.hip). Per trunk:
+// [W1 (H x OP) | W2 (H x H) | W2^T (H x H)], refreshed by k_adam with the parameters.
+PPO_DEV_HOST inline long sw_index(int r, int c, int ncols) {
+  return ((long)((r >> 4) * (ncols >> 4) + (c >> 4)) * 64 + ((c & 15) >> 2) * 16 + (r & 15)) * 4 + (c & 3);
+}
+PPO_DEV_HOST inline long sw_size(int H, int OP) { return (long)H * OP + 2L * H * H; }
 
 struct UpdArgs {
   const float* P;
   const float* W2T[2];
+  const float* WSW[2];  // swizzled W1 | W2 | W2^T per trunk (sw_index)
   PackedLayout K;
   SmallGradLayout sg[2];
   int M;
@@ -121,6 +134,9 @@ struct AdamArgs {
   long w2_off[2];
   float* w2t[2];
   int H;
+  long w1_off[2];
+  float* wsw[2];  // swizzled copies (sw_index), refreshed with the parameters
+  int OP;
 };
 
 struct GaeArgs {
@@ -174,6 +190,7 @@ void launch_colsum(const ColsumArgs& a, int nseg, long maxlen, hipStream_t s);
 void launch_gradnorm(const NormArgs& a, hipStream_t s);
 void launch_adam(const AdamArgs& a, hipStream_t s);
 void launch_transpose(const float* src, float* dst, int H, hipStream_t s);
+void launch_swizzle(const float* w1, const float* w2, float* dst, int H, int OP, hipStream_t s);
 void launch_gae(const GaeArgs& a, hipStream_t s);
 void launch_perm(int32_t* out, uint32_t B, const PermKey& pk, hipStream_t s);
 void launch_adv_sum(const AdvArgs& a, hipStream_t s);

@@ -98,21 +98,24 @@ PPO_DEV float bld1(PBuf b, int lane_floats, int uni_floats) {
 }
 
 // out[ft][rt] (+)= sum_k W[fbase + 16 ft + i][k] * IN[rbase + 16 rt + j][k], k in [0, 16 NKB)
-//   wlane = (fbase + i) * LDW + 4 g (per lane), in = IN + (rbase + j) * LDI + 4 g (LDS, per lane)
+//   in = IN + (rbase + j) * LDI + 4 g (LDS, per lane)
 // A (weights) double-buffered one 16-wide k-block ahead; B (activations) one ds_read_b128 per row tile.
 // KL (1 or 4): k-steps of the last 16-wide k-block that hold a real column — step c covers columns
 // 16 kb + 4 g + c, so with KL = 1 (K = 16 (NKB - 1) + 1, layer 1 at O = 17) the last block's y / z / w
 // steps are all padding and are skipped (5 of 8 steps).
-template <int FT, int RT, int NKB, int LDW, int LDI, int KL = 4>
+// A operands come from the swizzled copy (sw_index): feature tile ft, k-block kb of this wave at
+// wlane + FS ft + KS kb with FS = 256 NKB, KS = 256 (one contiguous 1 KB per wave-load)
+template <int FT, int RT, int NKB, int LDI, int KL = 4>
 PPO_DEV void mm_fr(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* in) {
+  constexpr int FS = 256 * NKB, KS = 256;
   f4 w[2][FT];
 #pragma unroll
-  for (int ft = 0; ft < FT; ++ft) w[0][ft] = pld4(wb, wlane, 16 * ft * LDW);
+  for (int ft = 0; ft < FT; ++ft) w[0][ft] = pld4(wb, wlane, FS * ft);
 #pragma unroll
   for (int kb = 0; kb < NKB; ++kb) {
     if (kb + 1 < NKB) {
 #pragma unroll
-      for (int ft = 0; ft < FT; ++ft) w[(kb + 1) & 1][ft] = pld4(wb, wlane, 16 * ft * LDW + 16 * (kb + 1));
+      for (int ft = 0; ft < FT; ++ft) w[(kb + 1) & 1][ft] = pld4(wb, wlane, FS * ft + KS * (kb + 1));
     }
     // pin the prefetch here: the scheduler otherwise sinks it next to its use (vmcnt(0) per block)
     __builtin_amdgcn_sched_barrier(0);
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
   const TrunkDev& T = K.tr[trunk];
   const float* __restrict__ P = a.P;
   const PBuf pb = make_pbuf(P, K.size);
-  const PBuf w2t = make_pbuf(a.W2T[trunk], H * H);
+  const PBuf wsw = make_pbuf(a.WSW[trunk], (int)sw_size(H, OP));
   const SmallGradLayout sg = a.sg[trunk];
   const int O = K.O, A = K.A, nh = sg.nh;
   const float c = a.clip_coef;
@@ -384,10 +387,10 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     SPAR[i] = x;
   }
 
-  // per-lane A-operand offsets
-  const int w1lane = T.W1 + (fbase + j) * OP + 4 * g;
-  const int w2lane = T.W2 + (fbase + j) * H + 4 * g;
-  const int w2tlane = (fbase + j) * H + 4 * g;
+  // per-lane A-operand offsets into the swizzled W1 | W2 | W2^T (sw_index): this wave's feature blocks
+  const int w1lane = ((fbase >> 4) * NTO * 64 + lane) * 4;
+  const int w2lane = H * OP + ((fbase >> 4) * NT * 64 + lane) * 4;
+  const int w2tlane = H * OP + H * H + ((fbase >> 4) * NT * 64 + lane) * 4;
   const float* xn_in = XN + (rbase + j) * LDX + 4 * g;
   const float* act_in = ACT + (rbase + j) * LDA + 4 * g;
   // head rows for the forward (A = W3[16 ht + i][..]) and the backward (A = W3^T: heads 16 ht + 4 g + r)
@@ -567,7 +570,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     // ---------------- layer 1 ----------------
     f4 z[FT][RT];
     init_bias<FT, RT>(z, pb, T.b1 + fbase + 4 * g);
-    mm_fr<FT, RT, NTO, OP, LDX, KL1>(z, pb, w1lane, xn_in);
+    mm_fr<FT, RT, NTO, LDX, KL1>(z, wsw, w1lane, xn_in);
     PPO_STAMP(1);
     float mu1[RT], rs1[RT];
     if constexpr (LN) {
@@ -600,7 +603,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     // ---------------- layer 2 ----------------
     f4 x2[FT][RT];  // LN: x_hat2; tanh: h2
     init_bias<FT, RT>(x2, pb, T.b2 + fbase + 4 * g);
-    mm_fr<FT, RT, NT, H, LDA>(x2, pb, w2lane, act_in);
+    mm_fr<FT, RT, NT, LDA>(x2, wsw, w2lane, act_in);
     PPO_STAMP(3);
     if constexpr (PREF) pref_data(it + gridDim.x);
     float rs2[RT];
@@ -984,11 +987,11 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
 
     // ---------------- dh1 = W2^T dz2 ----------------
     zero<FT, RT>(dh);
-    mm_fr<FT, RT, NT, H, LDA>(dh, w2t, w2tlane, act_in);
+    mm_fr<FT, RT, NT, LDA>(dh, wsw, w2tlane, act_in);
     PPO_STAMP(10);
     // ---------------- recompute layer 1, layer-1 backward ----------------
     init_bias<FT, RT>(z, pb, T.b1 + fbase + 4 * g);
-    mm_fr<FT, RT, NTO, OP, LDX, KL1>(z, pb, w1lane, xn_in);
+    mm_fr<FT, RT, NTO, LDX, KL1>(z, wsw, w1lane, xn_in);
     PPO_STAMP(11);
     if constexpr (LN) {
       float s1[RT], s2[RT];

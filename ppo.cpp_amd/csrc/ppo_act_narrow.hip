@@ -34,6 +34,7 @@ __global__ __launch_bounds__(256) void k_act4(ActArgs a) {
   const TrunkDev& T = K.tr[trunk];
   const float* __restrict__ P = a.P;
   const PBuf pb = make_pbuf(P, K.size);
+  const PBuf wsw = make_pbuf(a.WSW[trunk], (int)sw_size(H, OP));  // swizzled W1 | W2 (sw_index)
   const int row0 = blockIdx.x * R, O = K.O, A = K.A;
   const int row = row0 + j, rowc = min(row, a.n - 1);
   const int kb0 = ks * NKW;
@@ -53,10 +54,10 @@ __global__ __launch_bounds__(256) void k_act4(ActArgs a) {
       }
 #pragma unroll
       for (int ft = 0; ft < 4; ++ft)
-        wa[q][ft] = pld4(pb, T.W1 + (16 * ft + j) * OP + 4 * g, 16 * min(kb, NTO - 1));
+        wa[q][ft] = pld4(wsw, 4 * lane, 256 * (ft * NTO + min(kb, NTO - 1)));
     }
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) w2v[kb] = pld4(pb, T.W2 + (16 * ks + j) * H + 4 * g, 16 * kb);
+    for (int kb = 0; kb < 4; ++kb) w2v[kb] = pld4(wsw, H * OP + 4 * lane, 256 * (4 * ks + kb));
     b1 = pld4(pb, T.b1 + 16 * ks + 4 * g, 0);
     b2 = pld4(pb, T.b2 + 16 * ks + 4 * g, 0);
     if (trunk == 0) hv = pld4(pb, K.cW3 + 16 * ks + 4 * g, 0);

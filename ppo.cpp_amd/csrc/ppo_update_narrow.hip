@@ -97,16 +97,17 @@ PPO_DEV float colsum8(float (&x)[8], int j) {
   return x[0] + dpp_f<kDppQuadXor1>(x[0]);
 }
 
-// out[ft][rt] (+)= sum_k W[fbase + 16 ft + i][k] * IN[16 rt + j][k] for a 64-wide input in LDS
-PPO_DEV void mm64(f4 (&out)[FT2][RT2], PBuf wb, int wlane, int ldw, const float* in) {
+// out[ft][rt] (+)= sum_k W[fbase + 16 ft + i][k] * IN[16 rt + j][k] for a 64-wide input in LDS;
+// A operands from the swizzled copy (sw_index: feature tile ft, k-block kb at wlane + 1024 ft + 256 kb)
+PPO_DEV void mm64(f4 (&out)[FT2][RT2], PBuf wb, int wlane, const float* in) {
   f4 w[2][FT2];
 #pragma unroll
-  for (int ft = 0; ft < FT2; ++ft) w[0][ft] = pld4(wb, wlane, 16 * ft * ldw);
+  for (int ft = 0; ft < FT2; ++ft) w[0][ft] = pld4(wb, wlane, 1024 * ft);
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb) {
     if (kb + 1 < 4) {
 #pragma unroll
-      for (int ft = 0; ft < FT2; ++ft) w[(kb + 1) & 1][ft] = pld4(wb, wlane, 16 * ft * ldw + 16 * (kb + 1));
+      for (int ft = 0; ft < FT2; ++ft) w[(kb + 1) & 1][ft] = pld4(wb, wlane, 1024 * ft + 256 * (kb + 1));
     }
     __builtin_amdgcn_sched_barrier(0);
     f4 b[RT2];
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
   const TrunkDev& T = K.tr[trunk];
   const float* __restrict__ P = a.P;
   const PBuf pb = make_pbuf(P, K.size);
-  const PBuf w2t = make_pbuf(a.W2T[trunk], H * H);
+  const PBuf wsw = make_pbuf(a.WSW[trunk], (int)sw_size(H, OP));
   const int O = K.O, A = K.A, M = a.M;
   const float c = a.clip_coef;
   const float adv_mean = a.adv_stats[0], adv_std = a.adv_stats[1];
@@ -170,10 +171,10 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
   }
   if (tid == 0) SCB[0] = P[K.cb3];
 
-  // per-lane A-operand offsets
-  const int w1lane = T.W1 + (fbase + j) * OP + 4 * g;
-  const int w2lane = T.W2 + (fbase + j) * H + 4 * g;
-  const int w2tlane = (fbase + j) * H + 4 * g;
+  // per-lane A-operand offsets into the swizzled W1 | W2 | W2^T (sw_index)
+  const int w1lane = ((fbase >> 4) * NTO * 64 + lane) * 4;
+  const int w2lane = H * OP + ((fbase >> 4) * 4 * 64 + lane) * 4;
+  const int w2tlane = H * OP + H * H + ((fbase >> 4) * 4 * 64 + lane) * 4;
   const float* act_in = ACT + j * LDA + 4 * g;
   // head operands (loaded per tile from L1/L2): actor forward A = W3[16 ht + j][fbase + 16 ft + 4 g + c],
   // backward A = W3^T: W3[16 ht + 4 g + c][fbase + 16 ft + j]; critic w3[fbase + 16 ft + 4 g + c]
@@ -297,7 +298,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
 #pragma unroll
       for (int q = 0; q < W1D && q < NTO; ++q)
 #pragma unroll
-        for (int ft = 0; ft < FT; ++ft) w[q][ft] = pld4(pb, w1lane, 16 * ft * OP + 16 * q);
+        for (int ft = 0; ft < FT; ++ft) w[q][ft] = pld4(wsw, w1lane, 256 * NTO * ft + 256 * q);
 #pragma unroll
       for (int kb = 0; kb < NTO; ++kb) {
         if (kb > 0 && kb % CKB == 0) {
@@ -312,7 +313,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
         if (kb + W1D < NTO) {
 #pragma unroll
           for (int ft = 0; ft < FT; ++ft)
-            w[(kb + W1D) % (W1D + 1)][ft] = pld4(pb, w1lane, 16 * ft * OP + 16 * (kb + W1D));
+            w[(kb + W1D) % (W1D + 1)][ft] = pld4(wsw, w1lane, 256 * NTO * ft + 256 * (kb + W1D));
         }
         __builtin_amdgcn_sched_barrier(0);
         const int lu = 4 * (kb % CKB) + g;
@@ -355,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) h2[ft][rt] = bv;
     }
-    mm64(h2, pb, w2lane, H, act_in);
+    mm64(h2, wsw, w2lane, act_in);
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
@@ -584,7 +585,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
     for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) d1[ft][rt] = f4{0.f, 0.f, 0.f, 0.f};
-    mm64(d1, w2t, w2tlane, H, act_in);
+    mm64(d1, wsw, w2tlane, act_in);
     {
       float x[8];
 #pragma unroll

@@ -251,6 +251,34 @@ PPO_DEV void rs_stage(float (&x)[16], int j) {
   }
 }
 
+// Stages j ^ 8 and half-mirror (bit 2 of j) of the reduce-scatter with bank-masked DPP adds: lanes
+// whose bit is 0 (banks 0-1, resp. 0 and 2) keep slot i and add the partner's slot i; lanes whose
+// bit is 1 keep slot i + LEN / 2 and add the partner's, written into slot i. The second add of a
+// pair reads only upper slots, which the first does not write. s_nop 1: the DPP sources may have
+// been written by the instruction just before the block.
+PPO_DEV void rs_stage_banked(float (&x)[16]) {
+#define PPO_RS_A(i, C, B) "v_add_f32_dpp %" #i ", %" #i ", %" #i " " C " row_mask:0xf bank_mask:" B "\n\t"
+#define PPO_RS_B(i, k, C, B) "v_add_f32_dpp %" #i ", %" #k ", %" #k " " C " row_mask:0xf bank_mask:" B "\n\t"
+  asm("s_nop 1\n\t"
+      PPO_RS_A(0, "row_ror:8", "0x3") PPO_RS_A(1, "row_ror:8", "0x3") PPO_RS_A(2, "row_ror:8", "0x3")
+      PPO_RS_A(3, "row_ror:8", "0x3") PPO_RS_A(4, "row_ror:8", "0x3") PPO_RS_A(5, "row_ror:8", "0x3")
+      PPO_RS_A(6, "row_ror:8", "0x3") PPO_RS_A(7, "row_ror:8", "0x3")
+      PPO_RS_B(0, 8, "row_ror:8", "0xc") PPO_RS_B(1, 9, "row_ror:8", "0xc") PPO_RS_B(2, 10, "row_ror:8", "0xc")
+      PPO_RS_B(3, 11, "row_ror:8", "0xc") PPO_RS_B(4, 12, "row_ror:8", "0xc") PPO_RS_B(5, 13, "row_ror:8", "0xc")
+      PPO_RS_B(6, 14, "row_ror:8", "0xc") PPO_RS_B(7, 15, "row_ror:8", "0xc")
+      : "+&v"(x[0]), "+&v"(x[1]), "+&v"(x[2]), "+&v"(x[3]), "+&v"(x[4]), "+&v"(x[5]), "+&v"(x[6]), "+&v"(x[7])
+      : "v"(x[8]), "v"(x[9]), "v"(x[10]), "v"(x[11]), "v"(x[12]), "v"(x[13]), "v"(x[14]), "v"(x[15]));
+  asm("s_nop 1\n\t"
+      PPO_RS_A(0, "row_half_mirror", "0x5") PPO_RS_A(1, "row_half_mirror", "0x5")
+      PPO_RS_A(2, "row_half_mirror", "0x5") PPO_RS_A(3, "row_half_mirror", "0x5")
+      PPO_RS_B(0, 4, "row_half_mirror", "0xa") PPO_RS_B(1, 5, "row_half_mirror", "0xa")
+      PPO_RS_B(2, 6, "row_half_mirror", "0xa") PPO_RS_B(3, 7, "row_half_mirror", "0xa")
+      : "+&v"(x[0]), "+&v"(x[1]), "+&v"(x[2]), "+&v"(x[3])
+      : "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]));
+#undef PPO_RS_A
+#undef PPO_RS_B
+}
+
 // column sums over this wave's rows of v(ft, rt, r), added to acc[fbase + feature]:
 // sum over rt in lane, then a 16-lane reduce-scatter (lane j ends with slot j).
 template <int FT, int RT, typename Fn>
@@ -269,8 +297,9 @@ PPO_DEV void col_sums(Fn v, float* acc, int fbase, int j, int g) {
   // recursive halving over the 16 lanes j of each lane group with DPP partners: j ^ 8 (row_ror:8),
   // the mirror in each half (row_half_mirror), the mirror in each quad, j ^ 1. Each stage pairs
   // lanes of opposite bit m, so lane j still ends with slot j summed over all 16 lanes.
-  rs_stage<kDppRowRor8, 16, 8>(x, j);
-  rs_stage<kDppHalfMirror, 8, 4>(x, j);
+  // The first two stages split the lanes by DPP bank (bank = j >> 2): one bank-masked add per slot
+  // and half, own + partner exactly as the select form, without the two selects per slot.
+  rs_stage_banked(x);
   rs_stage<kDppQuadMirror, 4, 2>(x, j);
   rs_stage<kDppQuadXor1, 2, 1>(x, j);
   // slot j <-> feature 16 (j >> 2) + 4 g + (j & 3)

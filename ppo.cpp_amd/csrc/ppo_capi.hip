@@ -419,7 +419,7 @@ extern "C" float* ppo_buffer(ppo_t* c, int which) {
 // ------------------------------------------------------------------------------------------
 // parameters / optimizer state
 // ------------------------------------------------------------------------------------------
-static int refresh_w2t(ppo_t* c) {
+static int refresh_weight_copies(ppo_t* c) {
   for (int k = 0; k < 2; ++k) launch_transpose(c->P + c->K.tr[k].W2, c->W2T[k], c->K.H, c->stream);
   for (int k = 0; k < 2; ++k)
     launch_swizzle(c->P + c->K.tr[k].W1, c->P + c->K.tr[k].W2, c->WSW[k], c->K.H, c->K.OP, c->stream);
@@ -437,7 +437,7 @@ extern "C" int ppo_load_params(ppo_t* c, const float* host, long n) {
   HIP_TRY(hipMemsetAsync(c->Am, 0, sizeof(float) * c->K.size, c->stream));
   HIP_TRY(hipMemsetAsync(c->Av, 0, sizeof(float) * c->K.size, c->stream));
   c->adam_step = 0;
-  if (refresh_w2t(c)) return -2;
+  if (refresh_weight_copies(c)) return -2;
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;
 }
@@ -983,7 +983,7 @@ extern "C" int ppo_comm_broadcast_params(ppo_t* c, int root) {
     if (c->rank != root) HIP_TRY(hipMemsetAsync(c->P, 0, sizeof(float) * c->K.size, c->stream));
     if (allreduce(c, c->P, (long)c->K.size, 0, c->stream)) return -3;
   }
-  if (refresh_w2t(c)) return -2;
+  if (refresh_weight_copies(c)) return -2;
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;
 }

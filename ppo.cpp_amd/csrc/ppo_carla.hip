@@ -53,20 +53,26 @@ constexpr int kUK = 4;          // k-steps per loop iteration: their loads are a
 // a wave: NP tiles of 16 output pixels x NOT tiles of 16 output channels
 // Loads are unconditional from clamped addresses and masked with selects afterwards: a load under a
 // per-lane branch is followed by its own s_waitcnt, which serialises the gather latency.
+// The 4 waves of a workgroup share the output channels, so the weight tile of each 16-wide k group
+// (16 NOT channels x 16 k) is loaded once per workgroup — coalesced, one float4 per thread and
+// channel quarter — and staged in LDS in A-operand order: lane (j, g) of tile t reads its four
+// k-steps as one ds_read_b128 (the per-wave scalar weight gathers read 16 rows x 16 B per
+// instruction, 4 times over). Double-buffered, one barrier per k group; same operands and MFMA
+// chain as before, so results are unchanged bit for bit.
 template <int NOT, int NP, bool U8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) void k_conv(ConvArgs a) {
   __shared__ int koff[kMaxKTab + 4 * kUK];
+  __shared__ __attribute__((aligned(16))) float wst[2][NOT * 256];  // [buf][t][g][j][st]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
   const int KK = a.K * a.K, Kt = a.IC * KK, plane = a.IH * a.IW;
   for (int k = tid; k < Kt + 4 * kUK; k += 256) {  // padding: the last iteration reads without a branch
     const int ic = k / KK, rem = k - ic * KK, ky = rem / a.K, kx = rem - ky * a.K;
     koff[k] = k < Kt ? ic * plane + ky * a.IW + kx : 0;
   }
-  __syncthreads();
   const int P = a.OH * a.OW;
   const long Q = (long)a.n * P;
+  // waves past the last pixel stay (masked) for the workgroup's staging and barriers
   const long q0 = ((long)blockIdx.x * kConvWaves + wave) * 16 * NP;
-  if (q0 >= Q) return;
   // this lane's output pixels (B-operand column j of each pixel tile)
   long xbase[NP], obase[NP];
   bool qv[NP];
@@ -85,17 +91,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
   for (int t = 0; t < NOT; ++t)
 #pragma unroll
     for (int u = 0; u < NP; ++u) acc[t][u] = f4{0.f, 0.f, 0.f, 0.f};
-  const float* wrow[NOT];
-  bool ocv[NOT];
-#pragma unroll
-  for (int t = 0; t < NOT; ++t) {
-    const int oc = oc0 + 16 * t + j;
-    ocv[t] = oc < a.OC;
-    wrow[t] = a.W + (long)(ocv[t] ? oc : 0) * Kt;
-  }
   const int kbeg = a.kc ? (int)blockIdx.z * a.kc : 0, kend = a.kc ? min(Kt, kbeg + a.kc) : Kt;
-  for (int k0 = kbeg; k0 < kend; k0 += 4 * kUK) {
-    float x[kUK][NP], w[kUK][NOT];
+  // staging: thread (o = tid >> 2 + 64 h, c = tid & 3) owns channel oc0 + o, k-steps st = c: k0 + 4 c .. + 3
+  const bool vec = (Kt & 3) == 0;  // rows start on 16-byte boundaries (uniform)
+  constexpr int NH = (16 * NOT + 63) / 64;
+  const int so = tid >> 2, sc = tid & 3;
+  f4 wreg[NH];
+  auto wload = [&](int k0) {
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const int o = so + 64 * h, oc = oc0 + o, k = k0 + 4 * sc;
+      const bool ocok = o < 16 * NOT && oc < a.OC;
+      const float* row = a.W + (long)(ocok ? oc : 0) * Kt;
+      f4 v;
+      if (vec) {
+        v = *reinterpret_cast<const f4*>(row + min(k, Kt - 4));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = row[min(k + i, Kt - 1)];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] *= (ocok && k + i < kend) ? 1.0f : 0.0f;
+      wreg[h] = v;
+    }
+  };
+  auto wstore = [&](int buf) {
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const int o = so + 64 * h;
+      if (o < 16 * NOT) {
+        const int t = o >> 4, jj = o & 15;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wst[buf][((t * 4 + i) * 16 + jj) * 4 + sc] = wreg[h][i];
+      }
+    }
+  };
+  wload(kbeg);
+  wstore(0);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = kbeg; k0 < kend; k0 += 4 * kUK, buf ^= 1) {
+    const bool more = k0 + 4 * kUK < kend;
+    if (more) wload(k0 + 4 * kUK);
+    float x[kUK][NP];
 #pragma unroll
     for (int st = 0; st < kUK; ++st) {
       const int k = k0 + 4 * st + g;
@@ -114,15 +152,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
           x[st][u] = a.in_f[off] * (ok ? 1.0f : 0.0f);  // a multiplicative mask keeps the load unconditional
         }
       }
-#pragma unroll
-      for (int t = 0; t < NOT; ++t) w[st][t] = wrow[t][kv ? k : 0] * ((kv && ocv[t]) ? 1.0f : 0.0f);
     }
+    f4 w[NOT];  // w[t][st] = W[oc0 + 16 t + j][k0 + 4 st + g]
+#pragma unroll
+    for (int t = 0; t < NOT; ++t) w[t] = *reinterpret_cast<const f4*>(&wst[buf][(t * 64 + lane) * 4]);
 #pragma unroll
     for (int st = 0; st < kUK; ++st)
 #pragma unroll
       for (int t = 0; t < NOT; ++t)
 #pragma unroll
-        for (int u = 0; u < NP; ++u) acc[t][u] = mfma16(w[st][t], x[st][u], acc[t][u]);
+        for (int u = 0; u < NP; ++u) acc[t][u] = mfma16(w[t][st], x[st][u], acc[t][u]);
+    if (more) wstore(buf ^ 1);
+    __syncthreads();
   }
   // lane (j, g) holds out channel oc0 + 16t + 4g + r of pixel q0 + 16u + j
   if (a.kc) {  // split K: raw partial sums, added in z order by k_conv_fin

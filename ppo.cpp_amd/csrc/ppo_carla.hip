@@ -663,6 +663,7 @@ template <int NOT, int NP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) void k_dgrad(DgradArgs a) {
   __shared__ int woff[kMaxDTab + 4 * kUK], zoff[kMaxDTab + 4 * kUK];
   __shared__ int dji[kMaxDTab + 4 * kUK];
+  __shared__ __attribute__((aligned(16))) float wst[2][NOT * 256];  // staged weights, as in k_conv
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
   const int S = a.S, K = a.K, KK = K * K;
   const int py = blockIdx.z / S, px = blockIdx.z - py * S;
@@ -678,8 +679,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
   __syncthreads();
   const int H2 = (a.IH - py + S - 1) / S, W2 = (a.IW - px + S - 1) / S, P2 = H2 * W2;
   const long Q = (long)a.n * P2;
-  const long q0 = ((long)blockIdx.x * 4 + wave) * 16 * NP;
-  if (q0 >= Q) return;
+  const long q0 = ((long)blockIdx.x * 4 + wave) * 16 * NP;  // waves past Q stay (masked) for the staging
   long zb[NP], sv[NP];
   int pix[NP], iy2v[NP], ix2v[NP];
   bool qv[NP];
@@ -701,21 +701,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
   for (int t = 0; t < NOT; ++t)
 #pragma unroll
     for (int u = 0; u < NP; ++u) acc[t][u] = f4{0.f, 0.f, 0.f, 0.f};
-  const float* wrow[NOT];
-  bool icv[NOT];
+  // weight tile of each k group (16 NOT input channels x 16 (oc, tap) entries) gathered once per
+  // workgroup into LDS in A-operand order (k_conv's scheme): thread (o, c) loads k0 + 4 c .. + 3
+  constexpr int NH = (16 * NOT + 63) / 64;
+  const int so = tid >> 2, sc = tid & 3;
+  float wreg[NH][4];
+  auto wload = [&](int k0) {
 #pragma unroll
-  for (int t = 0; t < NOT; ++t) {
-    const int ic = ic0 + 16 * t + j;
-    icv[t] = ic < a.IC;
-    wrow[t] = a.W + (long)(icv[t] ? ic : 0) * KK;
-  }
-  for (int k0 = 0; k0 < Kt; k0 += 4 * kUK) {
-    float xb[kUK][NP], wa[kUK][NOT];
+    for (int h = 0; h < NH; ++h) {
+      const int o = so + 64 * h, ic = ic0 + o;
+      const bool icok = o < 16 * NOT && ic < a.IC;
+      const float* wr = a.W + (long)(icok ? ic : 0) * KK;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + 4 * sc + i;
+        wreg[h][i] = wr[woff[k]] * ((icok && k < Kt) ? 1.0f : 0.0f);
+      }
+    }
+  };
+  auto wstore = [&](int buf) {
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const int o = so + 64 * h;
+      if (o < 16 * NOT) {
+        const int t = o >> 4, jo = o & 15;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wst[buf][((t * 4 + i) * 16 + jo) * 4 + sc] = wreg[h][i];
+      }
+    }
+  };
+  wload(0);
+  wstore(0);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < Kt; k0 += 4 * kUK, buf ^= 1) {
+    const bool more = k0 + 4 * kUK < Kt;
+    if (more) wload(k0 + 4 * kUK);
+    float xb[kUK][NP];
 #pragma unroll
     for (int st = 0; st < kUK; ++st) {
       const int k = k0 + 4 * st + g;
       const bool kv = k < Kt;
-      const int wo = woff[k], zo = zoff[k], d = dji[k];
+      const int zo = zoff[k], d = dji[k];
       const int jj = d >> 16, ii = d & 0xFFFF;
 #pragma unroll
       for (int u = 0; u < NP; ++u) {
@@ -723,15 +750,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
             kv && qv[u] && (unsigned)(iy2v[u] - jj) < (unsigned)a.OH && (unsigned)(ix2v[u] - ii) < (unsigned)a.OW;
         xb[st][u] = a.dz[ok ? zb[u] + zo : 0] * (ok ? 1.0f : 0.0f);
       }
-#pragma unroll
-      for (int t = 0; t < NOT; ++t) wa[st][t] = wrow[t][wo] * ((kv && icv[t]) ? 1.0f : 0.0f);
     }
+    f4 wa[NOT];  // wa[t][st] = W[oc(k)][ic0 + 16 t + j][tap(k)], k = k0 + 4 st + g
+#pragma unroll
+    for (int t = 0; t < NOT; ++t) wa[t] = *reinterpret_cast<const f4*>(&wst[buf][(t * 64 + lane) * 4]);
 #pragma unroll
     for (int st = 0; st < kUK; ++st)
 #pragma unroll
       for (int t = 0; t < NOT; ++t)
 #pragma unroll
-        for (int u = 0; u < NP; ++u) acc[t][u] = mfma16(wa[st][t], xb[st][u], acc[t][u]);
+        for (int u = 0; u < NP; ++u) acc[t][u] = mfma16(wa[t][st], xb[st][u], acc[t][u]);
+    if (more) wstore(buf ^ 1);
+    __syncthreads();
   }
   const long plane = (long)a.IH * a.IW;
 #pragma unroll
@@ -862,8 +892,14 @@ constexpr int kMaxPTab = 9216;  // output pixels per sample (94 x 94 = 8836 for 
 
 template <int NOT, int NKT, bool U8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) void k_wgrad(WgradArgs a) {
+  // U q-steps per iteration: all their loads are issued before their MFMAs (the narrow layers have
+  // the longest pixel runs and the fewest MFMAs per load, so they get the deepest batch)
+  constexpr int U = NOT == 1 ? 8 : 2;
+  constexpr int NA = 16 * NOT * 4 * U;           // dZ tile of one iteration (channels x pixels)
+  constexpr int NAT = (NA + 255) / 256;          // dZ elements staged per thread
   __shared__ int koff[kMaxKTab];
   __shared__ int pbase[kMaxPTab];
+  __shared__ __attribute__((aligned(16))) float ast[2][NA];  // [buf][t][g][j][st]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
   const int KK = a.K * a.K, plane = a.IH * a.IW;
   for (int k = tid; k < a.Kt; k += 256) {
@@ -874,13 +910,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
     const int oy = p / a.OW, ox = p - oy * a.OW;
     pbase[p] = oy * a.S * a.IW + ox * a.S;
   }
-  __syncthreads();
   const long Q = (long)a.n * a.OP;
   const long qs = (long)blockIdx.x * a.qchunk;
   const long qe = qs + a.qchunk < Q ? qs + a.qchunk : Q;
   const int oc0 = blockIdx.y * 16 * NOT;
+  // waves whose columns start past Kt stay (their columns are masked) for the workgroup's staging
   const int kb = (blockIdx.z * 4 + wave) * 16 * NKT;
-  if (kb > a.Kt) return;
   f4 acc[NOT][NKT];
 #pragma unroll
   for (int t = 0; t < NOT; ++t)
@@ -888,38 +923,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
     for (int u = 0; u < NKT; ++u) acc[t][u] = f4{0.f, 0.f, 0.f, 0.f};
   int ko[NKT];
   int kc[NKT];  // 0: gathered column, 1: bias column, 2: past the end
+  __syncthreads();
 #pragma unroll
   for (int u = 0; u < NKT; ++u) {
     const int k = kb + 16 * u + j;
     kc[u] = k < a.Kt ? 0 : (k == a.Kt ? 1 : 2);
     ko[u] = k < a.Kt ? koff[k] : 0;
   }
-  long dzo[NOT];
-  bool ocv[NOT];
+  // The dZ operand (the A side) is the same for the workgroup's 4 waves: each iteration's
+  // 16 NOT x 4 U tile is loaded once per workgroup (element e = tid + 256 h: channel e / (4 U),
+  // pixel qb + e % (4 U), consecutive threads on consecutive pixels) and staged in LDS in A-operand
+  // order (lane (j, g) reads its U steps of tile t as one vector). Same operands and MFMA chain as
+  // the per-wave gathers: bitwise unchanged.
+  long as_[NAT];
+  int ap_[NAT];
+  auto apos = [&](int h, long q) {  // (sample, pixel) of pixel q for staging slot h
+    const long sm = q / a.OP;
+    as_[h] = sm;
+    ap_[h] = (int)(q - sm * a.OP);
+  };
 #pragma unroll
-  for (int t = 0; t < NOT; ++t) {
-    const int oc = oc0 + 16 * t + j;
-    ocv[t] = oc < a.OC;
-    dzo[t] = (long)(ocv[t] ? oc : 0) * a.OP;
-  }
+  for (int h = 0; h < NAT; ++h) apos(h, qs + (tid + 256 * h) % (4 * U));
+  float areg[NAT];
+  auto aload = [&](long qb) {
+#pragma unroll
+    for (int h = 0; h < NAT; ++h) {
+      const int e = tid + 256 * h, o = e / (4 * U), pi = e - o * (4 * U), oc = oc0 + o;
+      const bool ok = e < NA && oc < a.OC && qb + pi < qe;
+      areg[h] = a.dz[ok ? as_[h] * a.dz_stride + (long)oc * a.OP + ap_[h] : 0] * (ok ? 1.0f : 0.0f);
+      // advance to the next iteration's pixel (qb + 4 U + pi)
+      long sm = as_[h];
+      int pp = ap_[h] + 4 * U;
+      while (pp >= a.OP) {
+        pp -= a.OP;
+        ++sm;
+      }
+      as_[h] = sm;
+      ap_[h] = pp;
+    }
+  };
+  auto astore = [&](int buf) {
+#pragma unroll
+    for (int h = 0; h < NAT; ++h) {
+      const int e = tid + 256 * h;
+      if (e < NA) {
+        const int o = e / (4 * U), pi = e - o * (4 * U), t = o >> 4, jo = o & 15, st = pi >> 2, gg = pi & 3;
+        ast[buf][((t * 4 + gg) * 16 + jo) * U + st] = areg[h];
+      }
+    }
+  };
   long q = qs + g;
   long s = q / a.OP;
   int p = (int)(q - s * a.OP);
   const bool wrap1 = a.OP >= 4;
-  // U q-steps per iteration: all their loads are issued before their MFMAs (the narrow layers have
-  // the longest pixel runs and the fewest MFMAs per load, so they get the deepest batch)
-  constexpr int U = NOT == 1 ? 8 : 2;
-  for (long qb = qs; qb < qe; qb += 4 * U) {
-    float av[U][NOT], bv[U][NKT];
+  aload(qs);
+  astore(0);
+  __syncthreads();
+  int buf = 0;
+  for (long qb = qs; qb < qe; qb += 4 * U, buf ^= 1) {
+    const bool more = qb + 4 * U < qe;
+    if (more) aload(qb + 4 * U);
+    float bv[U][NKT];
 #pragma unroll
     for (int st = 0; st < U; ++st) {
       const bool qv = q < qe;
-      const long sb = s * a.dz_stride, xb = s * a.x_stride + (qv ? pbase[p] : 0);
-#pragma unroll
-      for (int t = 0; t < NOT; ++t) {
-        const bool ok = qv && ocv[t];
-        av[st][t] = a.dz[ok ? sb + dzo[t] + p : 0] * (ok ? 1.0f : 0.0f);
-      }
+      const long xb = s * a.x_stride + (qv ? pbase[p] : 0);
 #pragma unroll
       for (int u = 0; u < NKT; ++u) {
         const bool ok = qv && kc[u] == 0;
@@ -946,12 +1014,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
         }
       }
     }
+    float av[NOT][U];  // av[t][st] = dZ[oc0 + 16 t + j][pixel qb + 4 st + g]
+#pragma unroll
+    for (int t = 0; t < NOT; ++t)
+#pragma unroll
+      for (int st = 0; st < U; ++st) av[t][st] = ast[buf][((t * 4 + g) * 16 + j) * U + st];
 #pragma unroll
     for (int st = 0; st < U; ++st)
 #pragma unroll
       for (int t = 0; t < NOT; ++t)
 #pragma unroll
-        for (int u = 0; u < NKT; ++u) acc[t][u] = mfma16(av[st][t], bv[st][u], acc[t][u]);
+        for (int u = 0; u < NKT; ++u) acc[t][u] = mfma16(av[t][st], bv[st][u], acc[t][u]);
+    if (more) astore(buf ^ 1);
+    __syncthreads();
   }
   float* out = a.part + (long)blockIdx.x * a.OC * (a.Kt + 1);
 #pragma unroll

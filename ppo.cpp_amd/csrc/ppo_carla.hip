@@ -327,6 +327,111 @@ __global__ __launch_bounds__(256) void k_conv_img(ConvArgs a) {
   }
 }
 
+// ---- conv1 with OC <= 8: two output columns per MFMA column --------------------------------
+// With OC = 8, half of every 16-row A tile of k_conv_img is padding. Here A row oc + 8 dx holds the
+// weights of channel oc shifted by dx output columns (S input columns) over an extended tap row
+// kx' in [0, K + S): row oc + 8 dx, tap (ic, ky, kx') = W[oc][ic][ky][kx' - S dx] (0 outside the
+// kernel), and lane column j of the B tile is output column 2 j, so one MFMA yields 16 output
+// columns x 2 for all 8 channels. 15 x 5 x 7 = 525 taps per 32 outputs instead of 375 per 16:
+// 31 % fewer MFMAs and LDS reads per output. The f32 MFMA accumulates like a sequential fma chain
+// over k, the added taps carry exact zero weights (fma(+0, x >= 0, acc) = acc) and the real taps
+// keep k_conv's order, so the outputs stay bitwise equal to k_conv's (tested).
+constexpr int kImg2W = 32;  // output columns per workgroup tile
+template <int K, int S>
+struct Img2Geo {
+  static constexpr int TI = (kImgTile - 1) * S + K;  // patch rows
+  static constexpr int TW = (kImg2W - 1) * S + K;    // patch columns
+  static constexpr int TIP = (TW + 3) & ~3;          // patch row pitch in bytes
+  static constexpr int KX = K + S;                   // extended taps per kernel row
+};
+static size_t img2_lds_bytes(int IC, int K, int S, int OC) {
+  const int TI = (kImgTile - 1) * S + K, TW = (kImg2W - 1) * S + K, TIP = (TW + 3) & ~3;
+  const int Kt = IC * K * K, Kx = IC * K * (K + S);
+  const size_t patch = ((size_t)IC * TI * TIP + 15) & ~(size_t)15;
+  return patch + (size_t)OC * Kt * 4 + 2 * ((size_t)Kx + 64) * 4;
+}
+
+template <int K, int S>
+__global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a) {
+  using G = Img2Geo<K, S>;
+  constexpr int TI = G::TI, TIP = G::TIP, DW = TIP / 4, UK = 4, KX = G::KX;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int KK = K * K, Kt = a.IC * KK, Kx = a.IC * K * KX, OC = a.OC;
+  const size_t patch = ((size_t)a.IC * TI * TIP + 15) & ~(size_t)15;
+  unsigned char* tile = smem;
+  float* wl = reinterpret_cast<float*>(smem + patch);         // [OC][Kt]
+  int* poff = reinterpret_cast<int*>(wl + (size_t)OC * Kt);   // [Kx + 64]: patch offset of tap k'
+  int* wtap = poff + Kx + 64;                                 // [Kx + 64]: (ic K + ky) K << 8 | kx'
+  const int tiles_x = (a.OW + kImg2W - 1) / kImg2W;
+  const int ty = (int)blockIdx.x / tiles_x, tx = (int)blockIdx.x - ty * tiles_x, smp = blockIdx.y;
+  const int x0 = tx * kImg2W * S, y0 = ty * kImgTile * S;
+  {  // the uint8 patch, as k_conv_img (bytes past the image only reach outputs that are not stored)
+    const unsigned char* base = a.in_u8 + (size_t)smp * a.in_stride;
+    const size_t left = (size_t)(a.n - smp) * a.in_stride;
+    const PBuf ib{__builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
+                                                    (int)(left < 0xFFFFFFF0u ? left : 0xFFFFFFF0u), 0x00020000)};
+    const int plane = a.IH * a.IW, total = a.IC * TI * DW;
+    for (int e = tid; e < total; e += 256) {
+      const int ic = e / (TI * DW), rem = e - ic * (TI * DW), r = rem / DW, d = rem - r * DW;
+      const int off = ic * plane + (y0 + r) * a.IW + x0 + 4 * d;
+      const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(ib.r, off, 0, 0);
+      *reinterpret_cast<unsigned*>(tile + (ic * TI + r) * TIP + 4 * d) = v;
+    }
+  }
+  for (int e = tid; e < OC * Kt; e += 256) wl[e] = a.W[e];
+  for (int k = tid; k < Kx + 64; k += 256) {
+    const int ic = k / (K * KX), rem = k - ic * (K * KX), ky = rem / KX, kxp = rem - ky * KX;
+    const bool in = k < Kx;
+    poff[k] = in ? (ic * TI + ky) * TIP + kxp : 0;
+    wtap[k] = in ? (((ic * K + ky) * K) << 8) | kxp : 255;  // kx' = 255: no tap (zero weight)
+  }
+  __syncthreads();
+  int pix[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) pix[u] = S * (4 * wave + u) * TIP + 2 * S * j;
+  const int aoc = j & 7, adx = j >> 3;  // A row j: channel aoc, shifted by adx output columns
+  const bool aok = aoc < OC;
+  const float* wrow = wl + (size_t)(aok ? aoc : 0) * Kt;
+  f4 acc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc[u] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < Kx; k0 += 4 * UK) {
+    float x[UK][4], w[UK];
+#pragma unroll
+    for (int st = 0; st < UK; ++st) {
+      const int k = k0 + 4 * st + g;
+      const int po = poff[k], wt = wtap[k];
+      const int kx = (wt & 255) - S * adx;
+      const bool ok = aok && kx >= 0 && kx < K;
+      const float wv = wrow[(wt >> 8) + min(max(kx, 0), K - 1)];
+      w[st] = ok ? wv : 0.0f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[st][u] = (float)tile[po + pix[u]] * (1.0f / 255.0f);
+    }
+#pragma unroll
+    for (int st = 0; st < UK; ++st)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = mfma16(w[st], x[st][u], acc[u]);
+  }
+  // lane (j, g), register r: channel (4 g + r) & 7 of output column 2 j + ((4 g + r) >> 3)
+  const int P = a.OH * a.OW;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int oy = ty * kImgTile + 4 * wave + u;
+    if (oy >= a.OH) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ocp = 4 * g + r, oc = ocp & 7, ox = tx * kImg2W + 2 * j + (ocp >> 3);
+      if (oc < OC && ox < a.OW) {
+        float y = acc[u][r] + a.b[oc];
+        if (a.relu) y = y > 0.0f ? y : 0.0f;
+        a.out[(size_t)smp * a.out_stride + (size_t)oc * P + (size_t)oy * a.OW + ox] = y;
+      }
+    }
+  }
+}
+
 // value_measurements -> columns [256, 256 + NV) of the value-head input (carla_model.h:276)
 __global__ void k_carla_pack(const float* __restrict__ vmeas, float* __restrict__ feat, int n, int NV) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -405,6 +510,12 @@ __global__ __launch_bounds__(64) void k_carla_head(HeadArgs h) {
 
 int launch_conv(const ConvArgs& a, hipStream_t s, bool img = true) {
   if (a.IC * a.K * a.K > kMaxKTab) return -1;
+  if (img && a.in_u8 && ((uintptr_t)a.in_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 8 && a.IW % 4 == 0 &&
+      a.in_stride % 4 == 0 && a.OH <= 16 * 64 && img2_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {
+    const int tiles = ((a.OW + kImg2W - 1) / kImg2W) * ((a.OH + kImgTile - 1) / kImgTile);
+    hipLaunchKernelGGL((k_conv_img2<5, 2>), dim3(tiles, a.n), dim3(256), img2_lds_bytes(a.IC, a.K, a.S, a.OC), s, a);
+    return 0;
+  }
   if (img && a.in_u8 && ((uintptr_t)a.in_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 16 && a.IW % 4 == 0 &&
       a.in_stride % 4 == 0 &&
       a.OH <= 16 * 64 && img_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {

@@ -1535,10 +1535,144 @@ WgradPlan plan_wgrad(int OC, int Kt, long Q) {
   return p;
 }
 
+// ---- conv1's weight gradient with OC <= 8: two output columns per A row pair ------------------
+// As k_conv_img2: A row oc + 8 dx is dZ[oc] at the odd (dx = 1) or even (dx = 0) output column of
+// each column pair, the k dimension is the tile's 128 column pairs, and the B columns are the
+// extended taps (ic, ky, kx'), kx' in [0, K + S), plus the bias column: D[oc + 8 dx][(ic, ky, kx')]
+// sums dZ x input over the even (dx = 0) or odd (dx = 1) output columns, and
+// dW[oc][ic, ky, kx] = D[oc][(ic, ky, kx)] + D[oc + 8][(ic, ky, kx + S)] (bias: both halves).
+// 25 % fewer MFMAs than k_wgrad_img; the pixel sum is split into its even and odd halves, so the
+// result differs from k_wgrad's in rounding only. The combine runs once per workgroup through LDS.
+constexpr int kWimg2CT = 9;  // column tiles per wave: 4 x 9 x 16 = 576 >= IC K (K + S) + 1 = 526
+static size_t wimg2_lds_bytes(int IC, int K, int S, int OC) {
+  const int TI = (kImgTile - 1) * S + K, TIP = (TI + 3) & ~3;
+  const size_t patch = ((size_t)IC * TI * TIP + 15) & ~(size_t)15;
+  const size_t stage = patch + (size_t)OC * 260 * 4, comb = (size_t)16 * 4 * kWimg2CT * 16 * 4;
+  return stage > comb ? stage : comb;
+}
+
+template <int K, int S>
+__global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, int tps, int tiles, int tpc) {
+  using G = ImgGeo<K, S>;
+  constexpr int TI = G::TI, TIP = G::TIP, DW = TIP / 4, DZP = 260, KX = K + S, NC = 4 * kWimg2CT * 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int Kt = a.Kt, OC = a.OC, plane = a.IH * a.IW, Kx = a.IC * K * KX;
+  const size_t patch = ((size_t)a.IC * TI * TIP + 15) & ~(size_t)15;
+  unsigned char* tile = smem;
+  float* dzl = reinterpret_cast<float*>(smem + patch);  // [OC][DZP]: pixel 16 ly + lx
+  // B columns: extended tap col (gathered), the bias column (col == Kx) or padding
+  int ko[kWimg2CT];
+  float cb[kWimg2CT];  // 1 for the bias column, 0 for padding columns, -1 for gathered columns
+#pragma unroll
+  for (int u = 0; u < kWimg2CT; ++u) {
+    const int col = (wave * kWimg2CT + u) * 16 + j;
+    const int ic = col / (K * KX), rem = col - ic * (K * KX), ky = rem / KX, kxp = rem - ky * KX;
+    ko[u] = col < Kx ? (ic * TI + ky) * TIP + kxp : 0;
+    cb[u] = col < Kx ? -1.0f : (col == Kx ? 1.0f : 0.0f);
+  }
+  // A row j: channel j & 7 at the odd (j >= 8) or even column of each pair
+  const int aoc = j & 7, adx = j >> 3;
+  const float* arow = dzl + (aoc < OC ? aoc : 0) * DZP + adx;
+  const float am = aoc < OC ? 1.0f : 0.0f;
+  f4 acc[kWimg2CT];
+#pragma unroll
+  for (int u = 0; u < kWimg2CT; ++u) acc[u] = f4{0.f, 0.f, 0.f, 0.f};
+  const size_t total_bytes = (size_t)a.n * a.x_stride;
+  const int t0 = blockIdx.x * tpc, t1 = min(tiles, t0 + tpc);
+  for (int t = t0; t < t1; ++t) {
+    const int smp = t / tps, tt = t - smp * tps;
+    const int ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    const int OH = a.OP / a.OW;
+    const int x0 = tx * kImgTile * S, y0 = ty * kImgTile * S;
+    __syncthreads();  // the previous tile's readers are done
+    {
+      const size_t sb = (size_t)smp * a.x_stride, left = total_bytes - sb;
+      const PBuf ib{__builtin_amdgcn_make_buffer_rsrc((void*)(a.x_u8 + sb), (short)0,
+                                                      (int)(left < 0xFFFFFFF0u ? left : 0xFFFFFFF0u), 0x00020000)};
+      const int tot = a.IC * TI * DW;
+      for (int e = tid; e < tot; e += 256) {
+        const int ic = e / (TI * DW), rem = e - ic * (TI * DW), r = rem / DW, d = rem - r * DW;
+        const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(ib.r, ic * plane + (y0 + r) * a.IW + x0 + 4 * d, 0, 0);
+        *reinterpret_cast<unsigned*>(tile + (ic * TI + r) * TIP + 4 * d) = v;
+      }
+      const float* dz = a.dz + (size_t)smp * a.dz_stride;
+      for (int e = tid; e < OC * 256; e += 256) {
+        const int oc = e >> 8, px = e & 255, oy = ty * kImgTile + (px >> 4), ox = tx * kImgTile + (px & 15);
+        const bool in = oy < OH && ox < a.OW;
+        const float v = dz[in ? (size_t)oc * a.OP + oy * a.OW + ox : 0];
+        dzl[oc * DZP + px] = in ? v : 0.0f;
+      }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int st = 0; st < 32; ++st) {
+      const int m = 4 * st + g, ly = m >> 3, lx2 = m & 7;  // column pair (2 lx2, 2 lx2 + 1) of row ly
+      const int po = S * ly * TIP + 2 * S * lx2;
+      const float av = arow[16 * ly + 2 * lx2] * am;
+#pragma unroll
+      for (int u = 0; u < kWimg2CT; ++u) {
+        const int raw = tile[ko[u] + po];
+        const float xv = (float)raw * (1.0f / 255.0f);
+        // the bias and padding columns lie in the last 4 tiles of the last wave (launch condition)
+        const float bv = u >= kWimg2CT - 4 ? (cb[u] < 0.0f ? xv : cb[u]) : xv;
+        acc[u] = mfma16(av, bv, acc[u]);
+      }
+    }
+  }
+  // combine through LDS: D[16][NC] (row 4 g + r, column (wave 9 + u) 16 + j), then
+  // dW[oc][(ic, ky, kx)] = D[oc][(ic, ky, kx)] + D[oc + 8][(ic, ky, kx + S)]
+  __syncthreads();
+  float* dl = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int u = 0; u < kWimg2CT; ++u)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dl[(4 * g + r) * NC + (wave * kWimg2CT + u) * 16 + j] = acc[u][r];
+  __syncthreads();
+  float* out = a.part + (size_t)blockIdx.x * OC * (Kt + 1);
+  for (int e = tid; e < OC * (Kt + 1); e += 256) {
+    const int oc = e / (Kt + 1), k = e - oc * (Kt + 1);
+    float v;
+    if (k == Kt) {
+      v = dl[oc * NC + Kx] + dl[(oc + 8) * NC + Kx];
+    } else {
+      const int ic = k / (K * K), rem = k - ic * (K * K), ky = rem / K, kx = rem - ky * K;
+      const int c = (ic * K + ky) * KX + kx;
+      v = dl[oc * NC + c] + dl[(oc + 8) * NC + c + S];
+    }
+    out[e] = v;
+  }
+}
+
 int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap, hipStream_t s, bool img = true) {
   if (a.Kt > kMaxKTab || a.OP > kMaxPTab) return -1;
   const long per = (long)a.OC * (a.Kt + 1);
   const int OH = a.OP / a.OW;
+  if (img && a.x_u8 && ((uintptr_t)a.x_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 8 &&
+      a.IC * a.K * (a.K + a.S) + 1 <= 4 * kWimg2CT * 16 && a.IC * a.K * (a.K + a.S) >= (4 * kWimg2CT - 4) * 16 &&
+      a.IW % 4 == 0 && a.x_stride % 4 == 0 &&
+      wimg2_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {
+    const int tiles_x = (a.OW + kImgTile - 1) / kImgTile, tiles_y = (OH + kImgTile - 1) / kImgTile;
+    const int tiles = a.n * tiles_x * tiles_y;
+    int chunks = std::min(tiles, 1024);
+    const int tpc = (tiles + chunks - 1) / chunks;
+    chunks = (tiles + tpc - 1) / tpc;
+    const int groups = (chunks + kSumGroup - 1) / kSumGroup;
+    if ((size_t)(chunks + (chunks > kSumGroup ? groups : 0)) * per <= part_cap) {
+      a.part = part;
+      hipLaunchKernelGGL((k_wgrad_img2<5, 2>), dim3(chunks), dim3(256), wimg2_lds_bytes(a.IC, a.K, a.S, a.OC), s, a,
+                         tiles_x, tiles_x * tiles_y, tiles, tpc);
+      const unsigned gb = (unsigned)((per + 255) / 256);
+      if (chunks > kSumGroup) {
+        float* lvl = part + (size_t)chunks * per;
+        hipLaunchKernelGGL(k_wsum1, dim3(gb, groups), dim3(256), 0, s, part, chunks, per, lvl);
+        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, lvl, groups, a.OC, a.Kt, Gw, Gb);
+      } else {
+        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, part, chunks, a.OC, a.Kt, Gw, Gb);
+      }
+      return 0;
+    }
+  }
   if (img && a.x_u8 && ((uintptr_t)a.x_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 16 &&
       a.Kt + 1 <= 4 * kWimgCT * 16 &&
       a.Kt >= (4 * kWimgCT - 1) * 16 && a.IW % 4 == 0 &&

@@ -84,11 +84,12 @@ def test_errors(carla):
 
 
 def test_staged_conv1_kernels_match_generic(monkeypatch):
-    """conv1 runs through k_conv_img / k_wgrad_img (uint8 patch staged in LDS, ds_read_u8 gathers)
-    and conv2's input gradient through k_dgrad_s2 (dZ region staged in LDS); with
-    PPO_CARLA_CONV1=0 at create the generic k_conv / k_wgrad / k_dgrad gather from global memory.
-    Forward: same MFMA chain and operands, every output bitwise equal (n = 7: partial 16 x 16 tiles,
-    94 = 5 x 16 + 14). Update: k_dgrad_s2 keeps k_dgrad's chain (bitwise), so every gradient tensor
+    """conv1 runs through k_conv_img2 / k_wgrad_img2 (uint8 patch staged in LDS, ds_read_u8 gathers,
+    two output columns per MFMA column for OC = 8) and conv2's input gradient through k_dgrad_s2 (dZ
+    region staged in LDS); with PPO_CARLA_CONV1=0 at create the generic k_conv / k_wgrad / k_dgrad
+    gather from global memory. Forward: the real taps in k_conv's order, the extra taps with exact
+    zero weights (the f32 MFMA accumulates as a sequential fma chain), so every output is bitwise
+    equal (n = 7: partial tiles, 94 = 2 x 32 + 30 = 5 x 16 + 14). Update: k_dgrad_s2 keeps k_dgrad's chain (bitwise), so every gradient tensor
     but conv1's is bitwise equal; conv1's weight and bias gradients sum the 7 x 8 836 pixels in
     another order (relative L2 < 1e-5); the stepped parameters then differ through the clip
     coefficient (atol 1e-7)."""

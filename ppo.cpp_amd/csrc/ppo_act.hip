@@ -481,12 +481,13 @@ static int launch_act3_rt(const ActArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((k_act3<KIND, NTO, NHT, RT>), grid, dim3(kActThreads), lds, s, a);
   return 0;
 }
-// rows per workgroup: every workgroup re-reads the 256 KB layer-2 weights from the memory side
-// (cold L2 per launch), so wide batches use 32 rows (128 workgroups per trunk at E = 4096)
+// rows per workgroup: 16 at every E since the layer-2 weights stream in MFMA order (swizzled
+// copies); before, wide batches used 32 rows to halve the per-row weight bytes. Measured at E = 4 096
+// (rollout act): 19.4 us with 16 rows, 20.3 with 32, 32.7 with 64 (profiles/r02/act/act_rt_ab.txt)
 template <int KIND, int NTO, int NHT>
 static int launch_act3_t(const ActArgs& a, hipStream_t s) {
   static const int force = [] { const char* e = getenv("PPO_ACT_RT"); return e ? atoi(e) : 0; }();
-  const int rt = force ? force : (a.n >= 2048 ? 2 : 1);
+  const int rt = force ? force : 1;
   if (rt == 4) return launch_act3_rt<KIND, NTO, NHT, 4>(a, s);
   if (rt == 2) return launch_act3_rt<KIND, NTO, NHT, 2>(a, s);
   return launch_act3_rt<KIND, NTO, NHT, 1>(a, s);

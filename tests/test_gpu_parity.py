@@ -529,3 +529,33 @@ def test_cfg1_shape_iteration_vs_oracle():
     np.testing.assert_allclose(gpu_p, op, rtol=0, atol=1e-4)
     assert np.abs(gpu_p - p).max() > 1e-3  # 320 steps actually moved the parameters
     tr.close()
+
+
+@pytest.mark.parametrize("net_kind,hidden,env_id,O_", [(1, 256, "HalfCheetah-v5", 17), (1, 256, "Ant-v5", 105),
+                                                       (0, 64, "Humanoid-v4", 376)])
+def test_weight_copies_track_adam(net_kind, hidden, env_id, O_):
+    """k_act3 / k_act4 / k_upd / k_upd2 read W1, W2 and W2^T from transposed and MFMA-order
+    (swizzled) copies that k_adam rewrites next to every parameter update. After a full iteration
+    (16 or 64 Adam steps), act and value outputs computed from the incrementally maintained copies
+    must equal, bitwise, those after the copies are rebuilt from the parameters (ppo_load_params
+    -> k_transpose / k_swizzle)."""
+    E, T = 256, 16
+    C = ppo_amd.ACPPOConfig if net_kind == 1 else ppo_amd.PPOConfig
+    cfg = C(num_envs=E, num_steps=T, num_minibatches=4, update_epochs=4, env_id=env_id, net_kind=net_kind,
+            hidden=hidden, total_timesteps=E * T * 4)
+    tr = ppo_amd.Trainer(cfg)
+    p0 = tr.agent.params()
+    tr.iterate()
+    p1 = tr.agent.params()
+    assert not np.array_equal(p0, p1)
+    x = DeviceArray.from_numpy(np.random.default_rng(9).standard_normal((E, O_)).astype(np.float32))
+    outs = []
+    for rebuild in (False, True):
+        if rebuild:
+            tr.agent.load_params(p1)
+        m, lp, ent, v = tr.agent.get_action_and_value(x, sample_type=ppo_amd.PPO_MEAN)
+        outs.append([m.numpy(), lp.numpy(), ent.numpy(), v.numpy(), tr.agent.get_value(x).numpy()])
+    for a, b in zip(*outs):
+        assert np.isfinite(a).all()
+        np.testing.assert_array_equal(a, b)
+    tr.close()

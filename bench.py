@@ -161,6 +161,9 @@ def main():
     ap.add_argument("--profile-all", action="store_true", help="HIP-event time every kernel class")
     ap.add_argument("--no-cli", action="store_true", help="skip the ac_ppo_continuous_action CLI SPS run")
     ap.add_argument("--cli-iterations", type=int, default=30)
+    ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
+                    help="N > 1 data path: RCCL (one GPU per rank), or the host transport over gloo with every "
+                         "rank on GPU 0 (rehearses this script's multi-rank path on a one-GPU box)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -170,7 +173,7 @@ def main():
     if world > 1:
         import torch.distributed as dist  # gloo (CPU) only for rendezvous, barriers and timing max
         dist.init_process_group("gloo")
-    ppo_amd.set_device(local_rank)
+    ppo_amd.set_device(0 if args.comm == "host" else local_rank)
 
     E_total = args.num_envs if args.scaling == "strong" else args.num_envs * world
     E = E_total // world
@@ -179,9 +182,19 @@ def main():
                               total_timesteps=E_total * T * (args.steps + args.warmup + 1))
     tr = ppo_amd.Trainer(cfg, num_envs_per_device=E, rank=rank, world_size=world)
     if world > 1:
-        uid = [ppo_amd.Agent.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        tr.agent.comm_init(uid[0], rank, world)
+        if args.comm == "host":
+            import torch
+
+            def allreduce(buf, average):
+                t = torch.from_numpy(buf)  # the library's host staging buffer, reduced in place
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                if average:
+                    t /= world
+            tr.agent.comm_init_host(rank, world, allreduce)
+        else:
+            uid = [ppo_amd.Agent.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            tr.agent.comm_init(uid[0], rank, world)
         tr.agent.comm_broadcast_params(0)
 
     for _ in range(args.warmup):
@@ -247,7 +260,9 @@ def main():
             "config": {"workload": f"ac_ppo_continuous_action HalfCheetah-v5 num_envs={E_total} num_steps={T} "
                                    f"num_minibatches={cfg.num_minibatches} update_epochs={cfg.update_epochs}",
                        "num_envs": E_total, "num_envs_per_device": E, "num_steps": T,
-                       "minibatch_per_device": E * T // cfg.num_minibatches, "parallelism": f"dp{world}"},
+                       "minibatch_per_device": E * T // cfg.num_minibatches, "parallelism": f"dp{world}",
+                       **({"comm": "host transport (gloo), all ranks on GPU 0: rehearsal, not a scaling number"}
+                          if world > 1 and args.comm == "host" else {})},
             "roofline": roof,
         }
         if args.profile_all:

@@ -1,0 +1,43 @@
+"""bench.py contract (the driver's JSON line) on one GPU, and its multi-rank path rehearsed with the
+host transport (every rank on GPU 0, torch.distributed.run over 127.0.0.1)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config", "roofline")
+
+
+def last_json(out):
+    return json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+
+
+def test_bench_single_rank_line():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--no-cli", "--no-cpu-baseline", "--num-envs", "512"], capture_output=True, text=True,
+                       timeout=300, cwd=ROOT, check=True)
+    d = last_json(r.stdout)
+    for k in KEYS:
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["value"] > 0
+    roof = d["roofline"]
+    assert roof["bound"] == "mfma" and 0 < roof["frac"] < 1 and roof["peak"] == 157.3
+    assert abs(d["value"] - 512 * 128 / (d["ms_per_step"] / 1e3)) / d["value"] < 0.01
+
+
+def test_bench_two_ranks_host_transport():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--comm", "host", "--num-envs", "1024"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env, check=True)
+    d = last_json(r.stdout)
+    for k in KEYS:
+        assert k in d, k
+    assert d["n_gpus"] == 2 and d["config"]["num_envs_per_device"] == 512 and d["config"]["parallelism"] == "dp2"
+    assert d["value"] > 0 and "comm" in d["config"]

@@ -1019,6 +1019,22 @@ __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
     if (i < S.len) {
       const float* src = S.src + i;
       int r = q;
+      // eight loads in flight (one round trip for the usual 128 chunks); each accumulator still
+      // takes its rows in the order of the four-wide loop below, so the sums are unchanged
+      for (; r + 112 < S.count; r += 128) {
+        const f4 x0 = ld4(src + (size_t)r * S.stride), x1 = ld4(src + (size_t)(r + 16) * S.stride);
+        const f4 x2 = ld4(src + (size_t)(r + 32) * S.stride), x3 = ld4(src + (size_t)(r + 48) * S.stride);
+        const f4 x4 = ld4(src + (size_t)(r + 64) * S.stride), x5 = ld4(src + (size_t)(r + 80) * S.stride);
+        const f4 x6 = ld4(src + (size_t)(r + 96) * S.stride), x7 = ld4(src + (size_t)(r + 112) * S.stride);
+        acc0 += x0;
+        acc1 += x1;
+        acc2 += x2;
+        acc3 += x3;
+        acc0 += x4;
+        acc1 += x5;
+        acc2 += x6;
+        acc3 += x7;
+      }
       for (; r + 48 < S.count; r += 64) {
         acc0 += ld4(src + (size_t)r * S.stride);
         acc1 += ld4(src + (size_t)(r + 16) * S.stride);

@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import numpy as np  # noqa: E402
 
-import ppo_amd  # noqa: E402  (imports torch before loading libppo_hip.so: one HIP runtime serves both)
+ppo_amd = None  # imported in main(), after the launcher decision (ppo_amd loads libppo_hip.so)
 
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix = vector peak (spec)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
@@ -149,7 +149,32 @@ def cli_sps(E, T, iterations):
         return None
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(argv, n, port):
+    """The one-process-per-GPU launch of this script for `--gpus n` (the reference's
+    `mpirun -n G`, README.md:56-59): torch.distributed.run on this node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def relaunch(n):
+    """`bench.py --gpus n` without an external launcher: start the n ranks as a child process (never
+    an exec, and before anything in this process touches the GPU). Rank 0 prints the JSON line to
+    the inherited stdout; this process exits with the launcher's status."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    r = subprocess.run(launcher_cmd(sys.argv[1:], n, free_port()), env=env)
+    return r.returncode
+
+
 def main():
+    global ppo_amd
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -166,7 +191,14 @@ def main():
                          "rank on GPU 0 (rehearses this script's multi-rank path on a one-GPU box)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU "
+                         f"(or drop the external launcher and let --gpus start the ranks)")
+    import ppo_amd as _ppo_amd  # imports torch before loading libppo_hip.so: one HIP runtime serves both
+    ppo_amd = _ppo_amd
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -196,6 +228,9 @@ def main():
             dist.broadcast_object_list(uid, src=0)
             tr.agent.comm_init(uid[0], rank, world)
         tr.agent.comm_broadcast_params(0)
+    comm_kind, _, comm_world = tr.agent.comm_info()
+    if world > 1 and comm_world != world:
+        raise SystemExit(f"bench.py: the {comm_kind} communicator reports {comm_world} ranks, expected {world}")
 
     for _ in range(args.warmup):
         tr.iterate()
@@ -261,6 +296,7 @@ def main():
                                    f"num_minibatches={cfg.num_minibatches} update_epochs={cfg.update_epochs}",
                        "num_envs": E_total, "num_envs_per_device": E, "num_steps": T,
                        "minibatch_per_device": E * T // cfg.num_minibatches, "parallelism": f"dp{world}",
+                       "comm_ranks": comm_world, "comm_kind": comm_kind,
                        **({"comm": "host transport (gloo), all ranks on GPU 0: rehearsal, not a scaling number"}
                           if world > 1 and args.comm == "host" else {})},
             "roofline": roof,

@@ -150,6 +150,11 @@ int ppo_comm_destroy(ppo_t* ctx);
 /* comm->broadcast of every parameter from root (ac:551-553) */
 int ppo_comm_broadcast_params(ppo_t* ctx, int root);
 int ppo_comm_allreduce(ppo_t* ctx, float* buf_dev, long n, int average);
+/* The attached communicator as its transport sees it: kind 0 = none, 1 = RCCL (rank and world
+ * from ncclCommUserRank / ncclCommCount), 2 = host transport. comm->rank / comm->size
+ * (distributed.cpp:66-79). */
+enum { PPO_COMM_NONE = 0, PPO_COMM_RCCL = 1, PPO_COMM_HOST = 2 };
+int ppo_comm_info(const ppo_t* ctx, int* kind, int* rank, int* world);
 
 /* ---- device memory helpers (so C / ctypes callers need no HIP headers) ---- */
 int ppo_set_device(int device);

@@ -23,6 +23,10 @@ int psyn_create(int num_envs, int obs_dim, int act_dim, psyn_t** out);
 int psyn_destroy(psyn_t* env);
 /* reset(seed + i) for every env; writes obs [E,O] and done [E] (= 0) */
 int psyn_reset(psyn_t* env, int seed, float* obs_dev, float* done_dev, void* stream);
+/* The env's action space (default [-1, 1]); ppo_rollout_synth clips actions to it (clip_actions,
+ * gym.h:141-144), e.g. Humanoid-v4's [-0.4, 0.4] (libs/gymcpp/mujoco/humanoid_v4.h:29-30). */
+int psyn_set_action_space(psyn_t* env, float lo, float hi);
+int psyn_action_space(const psyn_t* env, float* lo, float* hi);
 /* one SeqVectorEnv step on envs [env_begin, env_end); actions are clipped to [lo, hi] */
 int psyn_step(psyn_t* env, int env_begin, int env_end, const float* action_dev, float lo, float hi,
               float* obs_dev, float* reward_dev, float* done_dev, void* stream);

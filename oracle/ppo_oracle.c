@@ -401,18 +401,22 @@ void orc_adv_stats(int M, const float* adv, float* mean, float* stdv) {
   *stdv = (float)sqrt(q / (double)(M - 1));
 }
 
-void orc_minibatch_grad(const ppo_layout* L, const float* P, int M, const float* x, const float* actions,
-                        const float* old_logp, const float* adv, const float* ret, const float* old_v,
-                        float adv_mean, float adv_std, const orc_loss_cfg* cfg, float* grad, float* stats) {
+/* Rows [r0, r1) of an M-row minibatch (ppo:497-538, ac:815-875): adds the loss gradient of those
+ * rows (already scaled by 1/M) into G (double, flat layout) and the six per-row loss sums
+ * (pg, v, entropy, old_kl, kl, clipfrac) into sums[6]. orc_minibatch_grad is the whole range; tests
+ * run disjoint ranges on several threads and add the partials in a fixed order (large minibatches). */
+void orc_minibatch_grad_part(const ppo_layout* L, const float* P, int M, int r0, int r1, const float* x,
+                             const float* actions, const float* old_logp, const float* adv, const float* ret,
+                             const float* old_v, float adv_mean, float adv_std, const orc_loss_cfg* cfg,
+                             double* G, double* sums) {
   const int O = L->O, A = L->A, H = L->H;
-  double* G = (double*)calloc((size_t)L->P, sizeof(double));
   trunk_cache* cc = (trunk_cache*)malloc(sizeof(trunk_cache));
   trunk_cache* ca = (trunk_cache*)malloc(sizeof(trunk_cache));
   double s_pg = 0, s_v = 0, s_ent = 0, s_okl = 0, s_kl = 0, s_cf = 0;
   const double invM = 1.0 / M;
   const float c = cfg->clip_coef;
   float xn[MAXO];
-  for (int r = 0; r < M; ++r) {
+  for (int r = r0; r < r1; ++r) {
     agent_input(L, P, x + (long)r * O, xn);
     trunk_forward(L, &L->critic, P, xn, cc);
     trunk_forward(L, &L->actor, P, xn, ca);
@@ -528,19 +532,40 @@ void orc_minibatch_grad(const ppo_layout* L, const float* P, int M, const float*
     }
     trunk_backward(L, &L->actor, P, ca, dh2, G);
   }
-  for (long i = 0; i < L->P; ++i) grad[i] = (float)G[i];
-  if (stats) {
-    stats[0] = (float)(s_pg * invM);
-    stats[1] = (float)(0.5 * s_v * invM);
-    stats[2] = (float)(s_ent * invM);
-    stats[3] = (float)(s_okl * invM);
-    stats[4] = (float)(s_kl * invM);
-    stats[5] = (float)(s_cf * invM);
-    stats[6] = (float)(stats[0] - cfg->ent_coef * stats[2] + stats[1] * cfg->vf_coef);
-  }
-  free(G);
+  sums[0] += s_pg;
+  sums[1] += s_v;
+  sums[2] += s_ent;
+  sums[3] += s_okl;
+  sums[4] += s_kl;
+  sums[5] += s_cf;
   free(cc);
   free(ca);
+}
+
+/* Finishes a minibatch from the accumulated partials: grad = (float)G, stats from the sums. */
+void orc_minibatch_finish(const ppo_layout* L, int M, const double* G, const double* sums, const orc_loss_cfg* cfg,
+                          float* grad, float* stats) {
+  const double invM = 1.0 / M;
+  for (long i = 0; i < L->P; ++i) grad[i] = (float)G[i];
+  if (stats) {
+    stats[0] = (float)(sums[0] * invM);
+    stats[1] = (float)(0.5 * sums[1] * invM);
+    stats[2] = (float)(sums[2] * invM);
+    stats[3] = (float)(sums[3] * invM);
+    stats[4] = (float)(sums[4] * invM);
+    stats[5] = (float)(sums[5] * invM);
+    stats[6] = (float)(stats[0] - cfg->ent_coef * stats[2] + stats[1] * cfg->vf_coef);
+  }
+}
+
+void orc_minibatch_grad(const ppo_layout* L, const float* P, int M, const float* x, const float* actions,
+                        const float* old_logp, const float* adv, const float* ret, const float* old_v,
+                        float adv_mean, float adv_std, const orc_loss_cfg* cfg, float* grad, float* stats) {
+  double* G = (double*)calloc((size_t)L->P, sizeof(double));
+  double sums[6] = {0, 0, 0, 0, 0, 0};
+  orc_minibatch_grad_part(L, P, M, 0, M, x, actions, old_logp, adv, ret, old_v, adv_mean, adv_std, cfg, G, sums);
+  orc_minibatch_finish(L, M, G, sums, cfg, grad, stats);
+  free(G);
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -844,23 +869,81 @@ typedef struct wrap_state {
   float rmean, rvar, racc, rcount;       /* NormalizeReward: count_ = 1e-8 */
 } wrap_state;
 
-static void wrap_obs(wrap_state* w, const float* x, float* y) {
-  /* update (stateful_observation.h:64-84), then (x - mean) / sqrt(var + eps), then clamp (ppo:44) */
+/* NormalizeObservation::observation of one env (stateful_observation.h:64-84: update, then
+ * (x - mean) / sqrt(var + eps)) and the clamp of ppo:44; mean / var / count are that env's state. */
+static void wrap_obs_one(float* om, float* ov, float* ocount, int O, const float* x, float* y) {
   const float batch_count = 1.0f;
-  const float tot_count = w->ocount + batch_count;
-  for (int i = 0; i < w->O; ++i) {
-    const float delta = x[i] - w->om[i];
-    const float new_mean = w->om[i] + delta * batch_count / tot_count;
-    const float m_a = w->ov[i] * w->ocount;
+  const float tot_count = *ocount + batch_count;
+  for (int i = 0; i < O; ++i) {
+    const float delta = x[i] - om[i];
+    const float new_mean = om[i] + delta * batch_count / tot_count;
+    const float m_a = ov[i] * *ocount;
     const float m_b = 0.0f * batch_count;
-    const float M2 = m_a + m_b + (delta * delta) * w->ocount * batch_count / tot_count;
-    w->om[i] = new_mean;
-    w->ov[i] = M2 / tot_count;
+    const float M2 = m_a + m_b + (delta * delta) * *ocount * batch_count / tot_count;
+    om[i] = new_mean;
+    ov[i] = M2 / tot_count;
   }
-  w->ocount = tot_count;
-  for (int i = 0; i < w->O; ++i) {
-    float v = (x[i] - w->om[i]) / sqrtf(w->ov[i] + 1e-4f);
+  *ocount = tot_count;
+  for (int i = 0; i < O; ++i) {
+    float v = (x[i] - om[i]) / sqrtf(ov[i] + 1e-4f);
     y[i] = v < -10.0f ? -10.0f : (v > 10.0f ? 10.0f : v);
+  }
+}
+
+/* NormalizeReward::step of one env (stateful_reward.h:55-91) and the clamp of ppo:46 */
+static float wrap_rew_one(float* rmean, float* rvar, float* racc, float* rcount, float gamma, float r, float te) {
+  *racc = *racc * gamma * (1.0f - te) + r;
+  const float batch_count = 1.0f;
+  const float delta = *racc - *rmean;
+  const float tot_count = *rcount + batch_count;
+  const float new_mean = *rmean + delta * batch_count / tot_count;
+  const float m_a = *rvar * *rcount;
+  const float m_b = 0.0f * batch_count;
+  const float M2 = m_a + m_b + (delta * delta) * *rcount * batch_count / tot_count;
+  *rcount = tot_count;
+  *rmean = new_mean;
+  *rvar = M2 / tot_count;
+  const float rn = r / sqrtf(*rvar + 1e-8f);
+  return rn < -10.0f ? -10.0f : (rn > 10.0f ? 10.0f : rn);
+}
+
+static void wrap_obs(wrap_state* w, const float* x, float* y) { wrap_obs_one(w->om, w->ov, &w->ocount, w->O, x, y); }
+
+/* The chain behind a vector env (one state per env, ppo:300-354): st is [E*O] obs mean, [E*O] obs
+ * var, then [E] each of obs count, reward mean, reward var, return accumulator, reward count.
+ * orc_vwrap_reset: the observations of reset_all (stats updated, normalised in place);
+ * orc_vwrap_step: one vector-env step in place -- every obs goes through the obs chain; where
+ * is_reset[e] != 0 (the step was the env's next-step autoreset, gym.h:141-149) the reward (0) does
+ * not pass NormalizeReward, otherwise it does with the termination flag te[e]. */
+static void vwrap_ptrs(float* st, int E, int O, float** om, float** ov, float** oc, float** rm, float** rv, float** ra,
+                       float** rc) {
+  *om = st; *ov = st + (long)E * O; *oc = st + 2L * E * O;
+  *rm = *oc + E; *rv = *rm + E; *ra = *rv + E; *rc = *ra + E;
+}
+void orc_vwrap_init(float* st, int E, int O) {
+  float *om, *ov, *oc, *rm, *rv, *ra, *rc;
+  vwrap_ptrs(st, E, O, &om, &ov, &oc, &rm, &rv, &ra, &rc);
+  for (long k = 0; k < (long)E * O; ++k) { om[k] = 0.0f; ov[k] = 1.0f; }
+  for (int e = 0; e < E; ++e) { oc[e] = 1e-4f; rm[e] = 0.0f; rv[e] = 1.0f; ra[e] = 0.0f; rc[e] = 1e-8f; }
+}
+void orc_vwrap_reset(float* st, int E, int O, float* obs) {
+  float *om, *ov, *oc, *rm, *rv, *ra, *rc;
+  vwrap_ptrs(st, E, O, &om, &ov, &oc, &rm, &rv, &ra, &rc);
+  float y[MAXO];
+  for (int e = 0; e < E; ++e) {
+    wrap_obs_one(om + (long)e * O, ov + (long)e * O, oc + e, O, obs + (long)e * O, y);
+    memcpy(obs + (long)e * O, y, sizeof(float) * O);
+  }
+}
+void orc_vwrap_step(float* st, int E, int O, float gamma, float* obs, float* reward, const float* te,
+                    const float* is_reset) {
+  float *om, *ov, *oc, *rm, *rv, *ra, *rc;
+  vwrap_ptrs(st, E, O, &om, &ov, &oc, &rm, &rv, &ra, &rc);
+  float y[MAXO];
+  for (int e = 0; e < E; ++e) {
+    wrap_obs_one(om + (long)e * O, ov + (long)e * O, oc + e, O, obs + (long)e * O, y);
+    memcpy(obs + (long)e * O, y, sizeof(float) * O);
+    if (is_reset[e] == 0.0f) reward[e] = wrap_rew_one(rm + e, rv + e, ra + e, rc + e, gamma, reward[e], te ? te[e] : 0.0f);
   }
 }
 
@@ -868,6 +951,34 @@ static void script_obs(const wrap_state* w, float* x) {
   for (int i = 0; i < w->O; ++i) {
     const float lo = (float)i - 2.0f, hi = (float)i + 3.0f;
     x[i] = lo + (hi - lo) * stream_u01(30, (uint32_t)(w->c * w->O + i));
+  }
+}
+
+/* The raw (unwrapped) stream of orc_wrappers_run's scripted env: obs of the initial reset and of
+ * every step [(T+1)*O], reward / termination / truncation per step, and is_reset[t] = 1 where step t
+ * was a reset (the plain reset at reset_at or the next-step autoreset). Feeds device wrapper tests. */
+void orc_wrappers_script(int O, int T, int reset_at, float* raw_obs, float* reward, float* term, float* trunc,
+                         float* is_reset) {
+  wrap_state w;
+  memset(&w, 0, sizeof(w));
+  w.O = O;
+  script_obs(&w, raw_obs);
+  w.c++;
+  int autoreset = 0;
+  for (int t = 0; t < T; ++t) {
+    float* o = raw_obs + (size_t)(t + 1) * O;
+    script_obs(&w, o);
+    if (t == reset_at || autoreset) {
+      w.c++;
+      reward[t] = 0.0f; term[t] = 0.0f; trunc[t] = 0.0f; is_reset[t] = 1.0f;
+      autoreset = 0;
+      continue;
+    }
+    const int te = (w.c % 29) == 28, tr = (w.c % 61) == 60;
+    reward[t] = -1.0f + 5.0f * stream_u01(31, (uint32_t)w.c);
+    w.c++;
+    term[t] = (float)te; trunc[t] = (float)tr; is_reset[t] = 0.0f;
+    autoreset = te || tr;
   }
 }
 
@@ -911,21 +1022,7 @@ void orc_wrappers_run(int O, int T, int reset_at, float gamma, float* obs, float
     info_ret[t] = (te || tr) ? w.ep_ret : 0.0f;
     info_len[t] = (te || tr) ? (float)w.ep_len : 0.0f;
     wrap_obs(&w, x, o);
-    w.racc = w.racc * gamma * (1.0f - (float)te) + r;
-    {
-      const float batch_count = 1.0f;
-      const float delta = w.racc - w.rmean;
-      const float tot_count = w.rcount + batch_count;
-      const float new_mean = w.rmean + delta * batch_count / tot_count;
-      const float m_a = w.rvar * w.rcount;
-      const float m_b = 0.0f * batch_count;
-      const float M2 = m_a + m_b + (delta * delta) * w.rcount * batch_count / tot_count;
-      w.rcount = tot_count;
-      w.rmean = new_mean;
-      w.rvar = M2 / tot_count;
-    }
-    const float rn = r / sqrtf(w.rvar + 1e-8f);
-    reward[t] = rn < -10.0f ? -10.0f : (rn > 10.0f ? 10.0f : rn);
+    reward[t] = wrap_rew_one(&w.rmean, &w.rvar, &w.racc, &w.rcount, gamma, r, (float)te);
     term[t] = (float)te;
     trunc[t] = (float)tr;
     autoreset = te || tr;

@@ -57,6 +57,15 @@ void orc_minibatch_grad(const ppo_layout* L, const float* params, int M, const f
                         const float* actions, const float* old_logp, const float* adv,
                         const float* ret, const float* old_v, float adv_mean, float adv_std,
                         const orc_loss_cfg* cfg, float* grad, float* stats);
+/* The same over rows [r0, r1) of the M-row minibatch: adds into double G[L->P] and sums[6]
+ * (pg, v, ent, old_kl, kl, clipfrac row sums); orc_minibatch_finish turns the accumulated partials
+ * into grad / stats. Disjoint ranges may run on different threads. */
+void orc_minibatch_grad_part(const ppo_layout* L, const float* params, int M, int r0, int r1, const float* x,
+                             const float* actions, const float* old_logp, const float* adv, const float* ret,
+                             const float* old_v, float adv_mean, float adv_std, const orc_loss_cfg* cfg,
+                             double* G, double* sums);
+void orc_minibatch_finish(const ppo_layout* L, int M, const double* G, const double* sums,
+                          const orc_loss_cfg* cfg, float* grad, float* stats);
 
 /* per-minibatch advantage statistics: mean, unbiased std (ppo:511; distributed form ac:833-846) */
 void orc_adv_stats(int M, const float* adv, float* mean, float* stdv);
@@ -116,6 +125,14 @@ void orc_env_step(orc_env_state* s, const float* actions, float act_lo, float ac
  * -1 + 5 u(31, c); termination c % 29 == 28; truncation c % 61 == 60 (u = orc_u01 of the
  * murmur3 hash stream of tests/carla_inputs.py). Writes obs [T+1][O] (row 0 = the first reset)
  * and reward / term / trunc / info_ret / info_len [T]; mean/var of the final obs statistics. */
+/* The PPO wrapper chain behind a vector env, one state per env (layout in ppo_oracle.c):
+ * st has 2*E*O + 5*E floats. */
+void orc_vwrap_init(float* st, int E, int O);
+void orc_vwrap_reset(float* st, int E, int O, float* obs);
+void orc_vwrap_step(float* st, int E, int O, float gamma, float* obs, float* reward, const float* te,
+                    const float* is_reset);
+void orc_wrappers_script(int O, int T, int reset_at, float* raw_obs, float* reward, float* term, float* trunc,
+                         float* is_reset);
 void orc_wrappers_run(int O, int T, int reset_at, float gamma, float* obs, float* reward, float* term, float* trunc,
                       float* info_ret, float* info_len, float* obs_mean, float* obs_var);
 

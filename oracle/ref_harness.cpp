@@ -20,6 +20,7 @@
 #include "ppo_oracle.h"  // the synthetic env and the Philox sampling draws (end-to-end case only)
 
 #include <algorithm>
+#include <memory>
 #include <chrono>
 #include <cstring>
 #include <cstdio>
@@ -627,6 +628,52 @@ struct WrapChain {
 };
 
 
+// The PPO trainer's per-env wrapper chain (ppo:41-49) over E envs at once for the end-to-end
+// replay: NormalizeObservation's LibTorch ops of stateful_observation.h:64-84 applied row-wise to the
+// [E, O] observations (one mean_ / var_ / count_ per env: count_ is an [E, 1] column, every other op
+// elementwise, so each element sees exactly the per-env operations), the clamp, and
+// NormalizeReward's float arithmetic (stateful_reward.h:55-91, std::sqrt) per env.
+struct VecWrap {
+  int E, O;
+  Tensor om, ov, oc;  // [E, O], [E, O], [E, 1]
+  std::vector<float> rmean, rvar, racc, rcount;
+  const float gamma = 0.99f;
+  VecWrap(int E_, int O_) : E(E_), O(O_), rmean(E_, 0.0f), rvar(E_, 1.0f), racc(E_, 0.0f), rcount(E_, 1e-8f) {
+    om = torch::zeros({E, O}, torch::kFloat32);
+    ov = torch::ones({E, O}, torch::kFloat32);
+    oc = torch::full({E, 1}, 1e-4f, torch::kFloat32);
+  }
+  Tensor obs(const Tensor& x) {
+    torch::NoGradGuard ng;
+    constexpr float batch_count = 1.0f;
+    const Tensor batch_var = torch::zeros_like(x);
+    const Tensor delta = x - om;
+    const Tensor tot_count = oc + batch_count;
+    const Tensor new_mean = om + delta * batch_count / tot_count;
+    const Tensor m_a = ov * oc;
+    const Tensor m_b = batch_var * batch_count;
+    const Tensor M2 = m_a + m_b + (delta * delta) * oc * batch_count / tot_count;
+    ov = M2 / tot_count;
+    om = new_mean;
+    oc = tot_count;
+    return torch::clamp((x - om) / torch::sqrt(ov + 1e-4f), -10.0f, 10.0f);
+  }
+  float reward(int e, float r, float te) {
+    racc[e] = racc[e] * gamma * (1.0f - te) + r;
+    constexpr float batch_count = 1.0f;
+    const float delta = racc[e] - rmean[e];
+    const float tot_count = rcount[e] + batch_count;
+    const float new_mean = rmean[e] + delta * batch_count / tot_count;
+    const float m_a = rvar[e] * rcount[e];
+    constexpr float m_b = 0.0f * batch_count;
+    const float M2 = m_a + m_b + (delta * delta) * rcount[e] * batch_count / tot_count;
+    rcount[e] = tot_count;
+    rmean[e] = new_mean;
+    rvar[e] = M2 / tot_count;
+    return std::clamp(r / std::sqrt(rvar[e] + 1e-8f), -10.0f, 10.0f);
+  }
+};
+
 // ---------------------------------------------------------------------------------------------
 // End-to-end replay (SURVEY §8c "end-to-end run fixture"; north_star: episodic returns on identical
 // seeds): NIT iterations of the trainer loop -- lr anneal (ppo:379-384 / ac:634-639), rollout
@@ -639,7 +686,7 @@ struct WrapChain {
 // ---------------------------------------------------------------------------------------------
 template <typename AgentT>
 static void e2e_case(const std::string& cname, AgentT& agent, int kind, int E, int T, int MB, int EP, int NIT,
-                     float lr0, const LossCfg& c, uint32_t base) {
+                     float lr0, const LossCfg& c, uint32_t base, bool wrappers = false) {
   const int O = 17, A = 6;
   std::string names;
   hash_params(*agent, base, 1.0f, -1.0f, names);
@@ -653,6 +700,11 @@ static void e2e_case(const std::string& cname, AgentT& agent, int kind, int E, i
   orc_env_state env{E, O, A, q.data(), et.data(), ar.data(), rs.data(), rc.data(), eret.data(), elen.data()};
   Tensor next_obs = torch::empty({E, O});
   orc_env_reset(&env, (int)seed, next_obs.data_ptr<float>());
+  std::unique_ptr<VecWrap> wrap;
+  if (wrappers) {
+    wrap = std::make_unique<VecWrap>(E, O);
+    next_obs = wrap->obs(next_obs).contiguous();
+  }
   Tensor next_done = torch::zeros({E});
   const long B = (long)E * T, M = B / MB;
   std::vector<float> stats;   // per iteration: pg, v, ent, old_kl, kl (last minibatch), clipfrac (mean), ret_sum, n_ep
@@ -704,6 +756,12 @@ static void e2e_case(const std::string& cname, AgentT& agent, int kind, int E, i
                    te.data_ptr<float>(), tr.data_ptr<float>(), ir.data_ptr<float>(), il.data());
       for (int e = 0; e < E; ++e)
         if (il[e] > 0) { ret_sum += ir.data_ptr<float>()[e]; n_ep += 1.0; }
+      if (wrap) {  // gym.h:141-149: an env whose previous step ended is reset now (reward 0, not normalised)
+        ob = wrap->obs(ob).contiguous();
+        for (int e = 0; e < E; ++e)
+          if (next_done.data_ptr<float>()[e] == 0.0f)
+            r.data_ptr<float>()[e] = wrap->reward(e, r.data_ptr<float>()[e], te.data_ptr<float>()[e]);
+      }
       rewards.index_put_({t}, r);
       next_obs = ob;
       next_done = torch::maximum(te, tr);
@@ -767,7 +825,8 @@ static void e2e_case(const std::string& cname, AgentT& agent, int kind, int E, i
     stats.insert(stats.end(), {st_last[0], st_last[1], st_last[2], st_last[3], st_last[4],
                                (float)(cf_sum / (EP * (B / M))), (float)ret_sum, (float)n_ep});
   }
-  begin_case(cname, "{\"kind\": " + std::to_string(kind) + ", \"E\": " + std::to_string(E) + ", \"T\": " +
+  begin_case(cname, "{\"kind\": " + std::to_string(kind) + ", \"wrappers\": " + (wrappers ? "true" : "false") +
+                        ", \"E\": " + std::to_string(E) + ", \"T\": " +
                         std::to_string(T) + ", \"MB\": " + std::to_string(MB) + ", \"EP\": " + std::to_string(EP) +
                         ", \"iterations\": " + std::to_string(NIT) + ", \"lr\": " + f2s(lr0) + ", \"clip_coef\": " +
                         f2s(c.clip_coef) + ", \"ent_coef\": " + f2s(c.ent_coef) + ", \"hash_base\": " +
@@ -783,6 +842,10 @@ static void e2e_cases() {
   {
     PPOAgent agent(17, 6, 64);
     e2e_case("e2e_ppo", agent, 0, E, T, MB, EP, NIT, 3e-4f, LossCfg{0.2f, 0.0f, 0.5f, true, true}, 3300);
+  }
+  {  // the PPO trainer as the reference runs it: every env behind the ppo:41-49 wrapper chain
+    PPOAgent agent(17, 6, 64);
+    e2e_case("e2e_ppo_wrapped", agent, 0, E, T, MB, EP, NIT, 3e-4f, LossCfg{0.2f, 0.0f, 0.5f, true, true}, 3500, true);
   }
   {
     ACAgent agent(17, 6, 256, 1.0f, -1.0f, torch::zeros({17}), torch::ones({17}));

@@ -184,9 +184,14 @@ int main(int argc, const char** argv) {
     A = envs[0]->get_action_space();
     act_lo = envs[0]->get_action_space_min();
     act_hi = envs[0]->get_action_space_max();
-  } else if (config.env_id != "SyntheticCheetah-v0" && config.env_id != "HalfCheetah-v5") {
-    std::cerr << "env_backend device provides the HalfCheetah-shaped synthetic env only\n";
-    return 1;
+  } else {
+    EnvShape sh;
+    if (!device_env_shape(config.env_id, &sh)) {
+      std::cerr << "env_backend device: unknown env_id " << config.env_id
+                << " (HalfCheetah-v5, Humanoid-v4, Ant-v5, Hopper-v5, SyntheticCheetah-v0)\n";
+      return 1;
+    }
+    O = sh.O; A = sh.A; act_lo = sh.lo; act_hi = sh.hi;
   }
 
   ppo_hip_config hc{};
@@ -273,7 +278,8 @@ int main(int argc, const char** argv) {
     std::vector<hipStream_t> gstreams(G);
     if (device_env) {
       check(psyn_create(E, O, A, &denv), "psyn_create");
-      check(psyn_reset(denv, config.seed, d_obs, d_done, s), "psyn_reset");
+      check(psyn_set_action_space(denv, act_lo, act_hi), "psyn_set_action_space");
+      check(psyn_reset(denv, config.seed, d_obs, d_done, s), "psyn_reset");  // env i: seed + i on every rank (ac:606)
     } else {
       HIPCHECK(hipHostMalloc(&h_obs, sizeof(float) * E * O));
       HIPCHECK(hipHostMalloc(&h_act, sizeof(float) * E * A));

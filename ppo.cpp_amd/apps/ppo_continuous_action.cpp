@@ -2,7 +2,9 @@
 // (src/ppo_continuous_action.cpp): same flags, defaults, stdout lines and per-iteration flow
 // (lr anneal -> rollout -> GAE -> epochs x minibatches -> checkpoint -> SPS/log), with the agent,
 // GAE and the whole update running as gfx950 kernels behind include/ppo_hip.h. The envs stay on
-// the host behind the gymcpp interface (ParVectorEnv + the reference's wrapper chain, ppo:41-49).
+// the host behind the gymcpp interface (ParVectorEnv + the reference's wrapper chain, ppo:41-49),
+// or, with --env_backend device, are the synthetic device env at the env id's shapes with the same
+// wrapper chain on the device (include/ppo_env_wrappers.h): nothing crosses PCIe per step.
 #include "trainer_common.h"
 
 #include <algorithm>
@@ -37,6 +39,7 @@ struct GlobalConfig {  // ppo_continuous_action.cpp:51-118
   std::string env_id = "Humanoid-v4";
   std::string render = "rgb_array";
   int device = 0;
+  std::string env_backend = "host";
   std::string exp_name;
   int batch_size = 0, minibatch_size = 0, num_iterations = 0;
   void derive() {  // ppo:268-272
@@ -78,6 +81,8 @@ int main(int argc, const char** argv) {
   flags.add("render", "Set to human for Visualizing the training with OpenGL, rgb_array for no visualization",
             &config.render);
   flags.add("device", "HIP device index", &config.device);
+  flags.add("env_backend", "host (gymcpp envs on the CPU) or device (synthetic env + wrapper chain in HBM)",
+            &config.env_backend);
   try {
     flags.parse(argc, argv);
   } catch (const HelpRequested&) {
@@ -97,14 +102,30 @@ int main(int argc, const char** argv) {
   fs::create_directories(exp_folder);
   RunLog logger(exp_folder, "tfevents_logs.pb", "scalars.jsonl");
 
-  std::vector<std::shared_ptr<gymcpp::EnvironmentWrapper>> env_array;
-  try {
-    for (int i = 0; i < config.num_envs; ++i) env_array.push_back(gymcpp::make_env(make_base_env(config.env_id), config.gamma));
-  } catch (const std::invalid_argument& e) {
-    std::cerr << e.what() << std::endl;
+  const bool device_env = config.env_backend == "device";
+  if (!device_env && config.env_backend != "host") {
+    std::cerr << "env_backend must be host or device\n";
     return 1;
   }
-  const int O = env_array[0]->get_observation_space(), A = env_array[0]->get_action_space();
+  std::vector<std::shared_ptr<gymcpp::EnvironmentWrapper>> env_array;
+  EnvShape sh{0, 0, -1.0f, 1.0f};
+  if (device_env) {
+    if (!device_env_shape(config.env_id, &sh)) {
+      std::cerr << "env_backend device: unknown env_id " << config.env_id
+                << " (HalfCheetah-v5, Humanoid-v4, Ant-v5, Hopper-v5, SyntheticCheetah-v0)\n";
+      return 1;
+    }
+  } else {
+    try {
+      for (int i = 0; i < config.num_envs; ++i) env_array.push_back(gymcpp::make_env(make_base_env(config.env_id), config.gamma));
+    } catch (const std::invalid_argument& e) {
+      std::cerr << e.what() << std::endl;
+      return 1;
+    }
+    sh = {env_array[0]->get_observation_space(), env_array[0]->get_action_space(),
+          env_array[0]->get_action_space_min(), env_array[0]->get_action_space_max()};
+  }
+  const int O = sh.O, A = sh.A;
   const int E = config.num_envs, T = config.num_steps;
 
   ppo_hip_config hc{};
@@ -115,15 +136,18 @@ int main(int argc, const char** argv) {
   hc.adam_eps = config.adam_eps; hc.norm_adv = config.norm_adv; hc.clip_vloss = config.clip_vloss;
   hc.seed = (uint64_t)config.seed; hc.rank = 0; hc.world_size = 1;
   ppo_t* agent = nullptr;
+  psyn_t* denv = nullptr;
+  pwrap_t* dwrap = nullptr;
   try {
     check(ppo_create(&hc, config.device, &agent), "ppo_create");
     ppo_layout L;
     check(ppo_get_layout(agent, &L), "ppo_get_layout");
-    auto p0 = init_params(L, config.seed, env_array[0]->get_action_space_max(), env_array[0]->get_action_space_min(), {}, {});
+    auto p0 = init_params(L, config.seed, sh.hi, sh.lo, {}, {});
     check(ppo_load_params(agent, p0.data(), L.P), "ppo_load_params");
     std::cout << "Number of parameters in model: " << (L.P - L.train_begin) << std::endl;
 
-    auto envs = std::make_shared<gymcpp::ParVectorEnv>(env_array, config.clip_actions);
+    std::shared_ptr<gymcpp::ParVectorEnv> envs;
+    if (!device_env) envs = std::make_shared<gymcpp::ParVectorEnv>(env_array, config.clip_actions);
     float *d_obs, *d_done, *d_act, *d_rew;
     HIPCHECK(hipMalloc(&d_obs, sizeof(float) * E * O));
     HIPCHECK(hipMalloc(&d_done, sizeof(float) * E));
@@ -134,9 +158,18 @@ int main(int argc, const char** argv) {
     HIPCHECK(hipHostMalloc(&h_done, sizeof(float) * E));
     hipStream_t s = (hipStream_t)ppo_stream(agent);
 
-    const float* obs0 = envs->reset(config.seed);
-    HIPCHECK(hipMemcpyAsync(d_obs, obs0, sizeof(float) * E * O, hipMemcpyHostToDevice, s));
-    HIPCHECK(hipMemsetAsync(d_done, 0, sizeof(float) * E, s));
+    if (device_env) {  // ParVectorEnv(make_env(...)) on the device: synthetic env + the ppo:41-49 chain
+      check(psyn_create(E, O, A, &denv), "psyn_create");
+      if (config.clip_actions) check(psyn_set_action_space(denv, sh.lo, sh.hi), "psyn_set_action_space");
+      else check(psyn_set_action_space(denv, -3.0e38f, 3.0e38f), "psyn_set_action_space");
+      check(pwrap_create(E, O, config.gamma, &dwrap), "pwrap_create");
+      check(psyn_attach_wrappers(denv, dwrap), "psyn_attach_wrappers");
+      check(psyn_reset(denv, config.seed, d_obs, d_done, s), "psyn_reset");
+    } else {
+      const float* obs0 = envs->reset(config.seed);
+      HIPCHECK(hipMemcpyAsync(d_obs, obs0, sizeof(float) * E * O, hipMemcpyHostToDevice, s));
+      HIPCHECK(hipMemsetAsync(d_done, 0, sizeof(float) * E, s));
+    }
 
     long global_step = 0;
     AsyncCheckpointer ckpt(agent);
@@ -150,7 +183,12 @@ int main(int argc, const char** argv) {
         lrnow = frac * config.learning_rate;
       }
       double env_time = 0;
-      for (int step = 0; step < T; ++step) {
+      if (device_env) {  // T x {act, env step + wrappers, reward store} on the device (ppo:387-434)
+        global_step += (long)E * T;
+        check(ppo_rollout_synth(agent, denv, d_obs, d_done, d_act, d_rew), "ppo_rollout_synth");
+        check(psyn_episode_stats_begin(denv, s), "psyn_episode_stats_begin");
+      }
+      for (int step = 0; step < T && !device_env; ++step) {
         global_step += E;
         check(ppo_rollout_act(agent, step, 0, E, d_obs, d_done, d_act, s), "ppo_rollout_act");
         HIPCHECK(hipMemcpyAsync(h_act, d_act, sizeof(float) * E * A, hipMemcpyDeviceToHost, s));
@@ -183,6 +221,17 @@ int main(int argc, const char** argv) {
       std::cout << std::fixed << std::setprecision(6) << "Total env step time " << env_time << " seconds \n";
       check(ppo_compute_gae(agent, d_obs, d_done, T, s), "ppo_compute_gae");
       check(ppo_update(agent, lrnow, nullptr, &st), "ppo_update");
+      if (device_env) {  // finished episodes of this rollout (raw returns: RecordEpisodeStatistics is innermost)
+        float sr = 0.f, sl = 0.f, n = 0.f;
+        check(psyn_episode_stats_end(denv, &sr, &sl, &n), "psyn_episode_stats_end");
+        if (n > 0) {
+          std::cout << "global_step=" << global_step << ", episodic_return=" << std::fixed << std::setprecision(2)
+                    << sr / n << " (mean of " << (long)n << " episodes)\n";
+          logger.add_scalar("charts/episodic_return", global_step, sr / n);
+          logger.add_scalar("charts/episodic_length", global_step, sl / n);
+          logger.add_scalar("charts/episodic_return_per_sec", std::lround(seconds_since(start_time)), sr / n);
+        }
+      }
       char mf[64], of[64];
       std::snprintf(mf, sizeof mf, "model_latest_%09d.pth", iteration);
       std::snprintf(of, sizeof of, "optimizer_latest_%09d.pth", iteration);
@@ -206,7 +255,31 @@ int main(int argc, const char** argv) {
     ckpt.finish();
     save_state(agent, exp_folder, "model_final.pth", "optimizer_final.pth", last_lr, config.adam_eps);
     // final evaluation on the training envs (normalisation statistics live there, ppo:589-626)
-    const float* eobs = envs->reset(config.eval_seed);
+    if (device_env) {
+      check(psyn_reset(denv, config.eval_seed, d_obs, d_done, s), "psyn_reset");
+      float sr0, sl0, n0;
+      check(psyn_episode_stats(denv, &sr0, &sl0, &n0), "psyn_episode_stats");  // clears the sums
+      double sum_r = 0, n_ep = 0;
+      long eval_step = 0;
+      while (n_ep < config.num_eval_runs && eval_step < 100000000L) {
+        check(ppo_get_action_and_value(agent, E, d_obs, PPO_SAMPLE, nullptr, 0, (1L << 40) + eval_step++, d_act,
+                                       nullptr, nullptr, nullptr, s), "ppo_get_action_and_value");
+        check(psyn_step(denv, 0, E, d_act, config.clip_actions ? sh.lo : -3.0e38f, config.clip_actions ? sh.hi : 3.0e38f,
+                        d_obs, d_rew, d_done, s), "psyn_step");
+        if (eval_step % 50 == 0) {
+          float sr, sl, n;
+          check(psyn_episode_stats(denv, &sr, &sl, &n), "psyn_episode_stats");
+          sum_r += sr;
+          n_ep += n;
+        }
+      }
+      const double avg = n_ep > 0 ? sum_r / n_ep : 0.0;
+      logger.add_scalar("eval/avg_return", (long)n_ep, avg);
+      std::cout << "Average evaluation return=" << std::fixed << std::setprecision(2) << avg << " over " << (long)n_ep
+                << " episodes" << std::endl;
+    }
+    const float* eobs = device_env ? nullptr : envs->reset(config.eval_seed);
+    if (!device_env) {
     HIPCHECK(hipMemcpyAsync(d_obs, eobs, sizeof(float) * E * O, hipMemcpyHostToDevice, s));
     std::vector<float> episodic_returns;
     long eval_step = 0;
@@ -232,11 +305,16 @@ int main(int argc, const char** argv) {
     logger.add_scalar("eval/avg_return", (long)episodic_returns.size(), avg);
     std::cout << "Average evaluation return=" << std::fixed << std::setprecision(2) << avg << " over "
               << episodic_returns.size() << " episodes" << std::endl;
+    }
+    if (denv) psyn_destroy(denv);
+    if (dwrap) pwrap_destroy(dwrap);
     (void)hipFree(d_obs); (void)hipFree(d_done); (void)hipFree(d_act); (void)hipFree(d_rew);
     (void)hipHostFree(h_act); (void)hipHostFree(h_done);
     ppo_destroy(agent);
   } catch (const std::exception& e) {
     std::cerr << e.what() << std::endl;
+    if (denv) psyn_destroy(denv);
+    if (dwrap) pwrap_destroy(dwrap);
     if (agent) ppo_destroy(agent);
     return 2;
   }

@@ -29,6 +29,7 @@
 #include "../../include/ppo_hip.h"
 #include "../../include/ppo_pth.h"
 #include "../../include/ppo_synth_env.h"
+#include "../../include/ppo_env_wrappers.h"
 #include "../gymcpp/gym.h"
 #include "../gymcpp/synthetic_cheetah.h"
 #include "tensorboard_logger.h"
@@ -348,6 +349,23 @@ struct EnvSpec {
   int obs_dim = 0, act_dim = 0;
   float act_min = -1, act_max = 1;
 };
+
+// Shape of the device env (--env_backend device) for an env id: the synthetic dynamics of
+// include/ppo_synth_env.h at the observation / action widths and action bounds of the reference's
+// MuJoCo env (libs/gymcpp/mujoco/half_cheetah_v5.h:31-34, humanoid_v4.h:27-30, ant_v5.h:38-41,
+// hopper_v5.h:35-38). Returns false for an unknown id.
+struct EnvShape {
+  int O, A;
+  float lo, hi;
+};
+inline bool device_env_shape(const std::string& env_id, EnvShape* s) {
+  if (env_id == "HalfCheetah-v5" || env_id == "SyntheticCheetah-v0") *s = {17, 6, -1.0f, 1.0f};
+  else if (env_id == "Humanoid-v4") *s = {376, 17, -0.4f, 0.4f};
+  else if (env_id == "Ant-v5") *s = {105, 8, -1.0f, 1.0f};
+  else if (env_id == "Hopper-v5") *s = {11, 3, -1.0f, 1.0f};
+  else return false;
+  return true;
+}
 
 // creates one base env; MuJoCo envs need libmujoco 3.2.0 (absent from this build)
 inline std::shared_ptr<gymcpp::Environment> make_base_env(const std::string& env_id) {

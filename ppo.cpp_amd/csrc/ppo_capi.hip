@@ -23,6 +23,7 @@
 
 #include "../../include/ppo_hip.h"
 #include "../../include/ppo_synth_env.h"
+#include "../../include/ppo_env_wrappers.h"
 #include "ppo_kernels.hpp"
 
 // ------------------------------------------------------------------------------------------
@@ -993,6 +994,24 @@ extern "C" int ppo_comm_allreduce(ppo_t* c, float* buf, long n, int average) {
   return allreduce(c, buf, n, average, c->stream);
 }
 
+extern "C" int ppo_comm_info(const ppo_t* c, int* kind, int* rank, int* world) {
+  if (!c || !kind || !rank || !world) return fail("ppo_comm_info: null argument");
+  if (c->comm) {
+    *kind = PPO_COMM_RCCL;
+    NCCL_TRY(ncclCommCount(c->comm, world));
+    NCCL_TRY(ncclCommUserRank(c->comm, rank));
+  } else if (c->host_ar) {
+    *kind = PPO_COMM_HOST;
+    *rank = c->rank;
+    *world = c->world;
+  } else {
+    *kind = PPO_COMM_NONE;
+    *rank = c->rank;
+    *world = c->world;
+  }
+  return 0;
+}
+
 // ------------------------------------------------------------------------------------------
 // device helpers
 // ------------------------------------------------------------------------------------------
@@ -1068,6 +1087,7 @@ extern "C" int ppo_profile_reset(ppo_t* c) {
 // ------------------------------------------------------------------------------------------
 struct psyn_env {
   SynthArgs a;
+  float act_lo = -1.0f, act_hi = 1.0f;  // the env's action space (clip_actions, gym.h:141-144)
   int device;
   float* host_stats = nullptr;  // pinned [3][E]: psyn_episode_stats_begin / _end
   hipEvent_t stats_ev = nullptr;
@@ -1137,7 +1157,7 @@ extern "C" int ppo_rollout_synth(ppo_t* c, psyn_t* env, float* next_obs, float* 
   if (!c || !env || !next_obs || !next_done || !act_scratch || !rew_scratch) return fail("ppo_rollout_synth: null argument");
   const int E = c->cfg.num_envs;
   if (env->a.E != E || env->a.O != c->K.O || env->a.A != c->K.A) return fail("ppo_rollout_synth: env shape mismatch");
-  const float lo = -1.0f, hi = 1.0f;
+  const float lo = env->act_lo, hi = env->act_hi;
   for (int t = 0; t < c->cfg.num_steps; ++t) {
     int rc = ppo_rollout_act(c, t, 0, E, next_obs, next_done, act_scratch, nullptr);
     if (rc) return rc;
@@ -1199,5 +1219,104 @@ extern "C" int psyn_episode_stats(psyn_t* env, float* sr, float* sl, float* sc) 
   if (sr) *sr = (float)R;
   if (sl) *sl = (float)Lsum;
   if (sc) *sc = (float)N;
+  return 0;
+}
+
+extern "C" int psyn_set_action_space(psyn_t* env, float lo, float hi) {
+  if (!env || !(lo < hi)) return fail("psyn_set_action_space: bad arguments");
+  env->act_lo = lo;
+  env->act_hi = hi;
+  return 0;
+}
+
+extern "C" int psyn_action_space(const psyn_t* env, float* lo, float* hi) {
+  if (!env || !lo || !hi) return fail("psyn_action_space: null argument");
+  *lo = env->act_lo;
+  *hi = env->act_hi;
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// PPO env wrapper chain on the device (include/ppo_env_wrappers.h)
+// ------------------------------------------------------------------------------------------
+struct pwrap {
+  WrapArgs w;
+  int E, O;
+  float* state = nullptr;  // 2*E*O + 5*E floats (orc_vwrap_* layout)
+};
+
+extern "C" int pwrap_create(int E, int O, float gamma, pwrap_t** out) {
+  if (!out || E <= 0 || O <= 0) return fail("pwrap_create: bad arguments");
+  pwrap_t* p = new pwrap_t();
+  p->E = E;
+  p->O = O;
+  const size_t n = 2 * (size_t)E * O + 5 * (size_t)E;
+  if (dmalloc(&p->state, n)) {
+    delete p;
+    return -2;
+  }
+  std::vector<float> h(n, 0.0f);  // mean 0, var 1, obs count 1e-4; reward mean 0, var 1, acc 0, count 1e-8
+  for (size_t k = (size_t)E * O; k < 2 * (size_t)E * O; ++k) h[k] = 1.0f;
+  float* tail = h.data() + 2 * (size_t)E * O;
+  for (int e = 0; e < E; ++e) {
+    tail[e] = 1e-4f;
+    tail[2 * E + e] = 1.0f;
+    tail[4 * E + e] = 1e-8f;
+  }
+  HIP_TRY(hipMemcpy(p->state, h.data(), n * sizeof(float), hipMemcpyHostToDevice));
+  WrapArgs& w = p->w;
+  w.om = p->state;
+  w.ov = p->state + (size_t)E * O;
+  w.ocount = p->state + 2 * (size_t)E * O;
+  w.rmean = w.ocount + E;
+  w.rvar = w.rmean + E;
+  w.racc = w.rvar + E;
+  w.rcount = w.racc + E;
+  w.gamma = gamma;
+  w.on = 1;
+  *out = p;
+  return 0;
+}
+
+extern "C" int pwrap_destroy(pwrap_t* p) {
+  if (!p) return 0;
+  if (p->state) (void)hipFree(p->state);
+  delete p;
+  return 0;
+}
+
+extern "C" int pwrap_reset(pwrap_t* p, int e0, int e1, float* obs, void* stream) {
+  if (!p || !obs) return fail("pwrap_reset: null argument");
+  if (e0 < 0 || e1 > p->E || e0 >= e1) return fail("pwrap_reset: env range out of bounds");
+  launch_wrap_step(p->w, p->O, e0, e1, obs, nullptr, nullptr, nullptr, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+extern "C" int pwrap_step(pwrap_t* p, int e0, int e1, float* obs, float* reward, const float* term,
+                          const float* is_reset, void* stream) {
+  if (!p || !obs || !reward) return fail("pwrap_step: null argument");
+  if (e0 < 0 || e1 > p->E || e0 >= e1) return fail("pwrap_step: env range out of bounds");
+  launch_wrap_step(p->w, p->O, e0, e1, obs, reward, term, is_reset, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+extern "C" int pwrap_read_state(pwrap_t* p, float* host, long n) {
+  if (!p || !host) return fail("pwrap_read_state: null argument");
+  if (n != 2L * p->E * p->O + 5L * p->E) return fail("pwrap_read_state: size mismatch");
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(host, p->state, n * sizeof(float), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int psyn_attach_wrappers(psyn_t* env, pwrap_t* p) {
+  if (!env) return fail("psyn_attach_wrappers: null env");
+  if (!p) {
+    env->a.w = WrapArgs{};
+    return 0;
+  }
+  if (p->E != env->a.E || p->O != env->a.O) return fail("psyn_attach_wrappers: shape mismatch");
+  env->a.w = p->w;
   return 0;
 }

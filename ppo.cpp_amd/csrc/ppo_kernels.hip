@@ -1312,17 +1312,82 @@ __global__ void k_adv_finalize(AdvArgs a) {
 // synthetic device env (SeqVectorEnv + RecordEpisodeStatistics semantics; bit-identical to the
 // host SyntheticCheetah and the oracle)
 // =============================================================================================
+// ---------------------------------------------------------------------------------------------
+// PPO env wrapper chain (ppo:41-49) on the device, one state per env. Same fp32 operations, in the
+// same order, as gymcpp/wrappers.h and the oracle (orc_vwrap_*): no contraction, IEEE division and
+// square root, so the chain is bit-exact against both.
+// ---------------------------------------------------------------------------------------------
+// NormalizeObservation::observation for dimension i of env e (stateful_observation.h:64-84: the
+// Welford update with batch_count 1 BEFORE normalising) + TransformObservation clamp +-10 (ppo:44).
+// oc is the env's count_ as read before this step; the caller stores oc + 1 once per env.
+PPO_DEV float wrap_obs_dim(const WrapArgs& w, long e, int O, int i, float oc, float x) {
+#pragma clang fp contract(off)
+  float* om = w.om + e * O + i;
+  float* ov = w.ov + e * O + i;
+  const float batch_count = 1.0f;
+  const float tot_count = oc + batch_count;
+  const float delta = x - *om;
+  const float new_mean = *om + delta * batch_count / tot_count;
+  const float m_a = *ov * oc;
+  const float m_b = 0.0f * batch_count;
+  const float M2 = m_a + m_b + (delta * delta) * oc * batch_count / tot_count;
+  const float new_var = M2 / tot_count;
+  *om = new_mean;
+  *ov = new_var;
+  const float v = (x - new_mean) / sqrtf(new_var + 1e-4f);
+  return v < -10.0f ? -10.0f : (v > 10.0f ? 10.0f : v);
+}
+
+// NormalizeReward::step (stateful_reward.h:55-91; te = termination) + TransformReward clamp +-10
+PPO_DEV float wrap_reward(const WrapArgs& w, long e, float r, float te) {
+#pragma clang fp contract(off)
+  const float racc = w.racc[e] * w.gamma * (1.0f - te) + r;
+  const float rmean = w.rmean[e], rvar = w.rvar[e], rcount = w.rcount[e];
+  const float batch_count = 1.0f;
+  const float delta = racc - rmean;
+  const float tot_count = rcount + batch_count;
+  const float new_mean = rmean + delta * batch_count / tot_count;
+  const float m_a = rvar * rcount;
+  const float m_b = 0.0f * batch_count;
+  const float M2 = m_a + m_b + (delta * delta) * rcount * batch_count / tot_count;
+  const float new_var = M2 / tot_count;
+  w.racc[e] = racc;
+  w.rcount[e] = tot_count;
+  w.rmean[e] = new_mean;
+  w.rvar[e] = new_var;
+  const float rn = r / sqrtf(new_var + 1e-8f);
+  return rn < -10.0f ? -10.0f : (rn > 10.0f ? 10.0f : rn);
+}
+
+// The chain as its own pass over envs [e0, e1) of a vector env's output (pwrap_step / pwrap_reset):
+// one wave per env, lanes over the observation. is_reset[e] != 0 marks the next-step autoreset
+// (gym.h:141-149: the reward, 0, bypasses NormalizeReward); reward == nullptr: observations only.
+__global__ __launch_bounds__(256) void k_wrap_step(WrapArgs w, int O, int e0, int e1, float* __restrict__ obs,
+                                                   float* __restrict__ reward, const float* __restrict__ term,
+                                                   const float* __restrict__ is_reset) {
+  const int lane = threadIdx.x & 63;
+  const int e = e0 + blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= e1) return;  // uniform per wave
+  const float oc = w.ocount[e];
+  for (int i = lane; i < O; i += 64) obs[(long)e * O + i] = wrap_obs_dim(w, e, O, i, oc, obs[(long)e * O + i]);
+  if (lane != 0) return;
+  w.ocount[e] = oc + 1.0f;
+  if (reward && !(is_reset && is_reset[e] != 0.0f)) reward[e] = wrap_reward(w, e, reward[e], term ? term[e] : 0.0f);
+}
+
 PPO_DEV void synth_reset_one(SynthArgs& a, int e, int seed, float* obs) {
 #pragma clang fp contract(off)
   if (seed > 0) { a.rseed[e] = (uint32_t)seed; a.rcount[e] = 0; }
   const uint32_t rs = a.rseed[e], rc = a.rcount[e];
+  const float oc = a.w.on ? a.w.ocount[e] : 0.0f;
   for (int i = 0; i < a.O; ++i) {
     uint32_t r[4];
     philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, r);
     const float q = (0.1f * ((2.0f * u01(r[0])) - 1.0f));
     a.q[(long)e * a.O + i] = q;
-    obs[(long)e * a.O + i] = q;
+    obs[(long)e * a.O + i] = a.w.on ? wrap_obs_dim(a.w, e, a.O, i, oc, q) : q;
   }
+  if (a.w.on) a.w.ocount[e] = oc + 1.0f;
   a.rcount[e] = rc + 1;
   a.t[e] = 0;
   a.ep_ret[e] = 0.0f;
@@ -1358,14 +1423,16 @@ __global__ __launch_bounds__(256) void k_synth_step(SynthArgs a, int e0, int e1,
   const int lane = threadIdx.x & 63;
   const float qn = __shfl(qi, (i + 1 < O) ? lane + 1 : lane - i, 64);
   if (!live || i >= O) return;
+  const float oc = a.w.on ? a.w.ocount[e] : 0.0f;  // read by every lane before lane 0 stores oc + 1
   if (reset) {
     const uint32_t rs = a.rseed[e], rc = a.rcount[e];
     uint32_t r[4];
     philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, r);
     const float v = (0.1f * ((2.0f * u01(r[0])) - 1.0f));
     q[i] = v;
-    obs[(long)e * O + i] = v;
+    obs[(long)e * O + i] = a.w.on ? wrap_obs_dim(a.w, e, O, i, oc, v) : v;
     if (i == 0) {
+      if (a.w.on) a.w.ocount[e] = oc + 1.0f;
       a.rcount[e] = rc + 1;
       a.t[e] = 0;
       a.ep_ret[e] = 0.0f;
@@ -1380,8 +1447,9 @@ __global__ __launch_bounds__(256) void k_synth_step(SynthArgs a, int e0, int e1,
   const float ai = fminf(fmaxf(ar[i % A], lo), hi);
   const float nq = __fmaf_rn(0.9f, qi, __fmaf_rn(0.1f, ai, (0.05f * qn)));
   q[i] = nq;
-  obs[(long)e * O + i] = nq;
+  obs[(long)e * O + i] = a.w.on ? wrap_obs_dim(a.w, e, O, i, oc, nq) : nq;
   if (i != 0) return;
+  if (a.w.on) a.w.ocount[e] = oc + 1.0f;
   const float vel = ((nq - qi) / 0.05f);
   float ctrl = 0.0f;
   for (int k = 0; k < A; ++k) {
@@ -1392,7 +1460,7 @@ __global__ __launch_bounds__(256) void k_synth_step(SynthArgs a, int e0, int e1,
   const int t = a.t[e] + 1;
   a.t[e] = t;
   const bool tr = t >= 1000;
-  reward[e] = r;
+  reward[e] = a.w.on ? wrap_reward(a.w, e, r, 0.0f) : r;  // the synthetic env never terminates
   done[e] = tr ? 1.0f : 0.0f;
   a.ep_ret[e] = (a.ep_ret[e] + r);
   a.ep_len[e] += 1;
@@ -1425,6 +1493,7 @@ __global__ __launch_bounds__(256) void k_synth_step_wide(SynthArgs a, int e0, in
     qv[c] = q[i < O ? i : O - 1];
   }
   const bool reset = a.autoreset[e] != 0;
+  const float oc = a.w.on ? a.w.ocount[e] : 0.0f;  // read by every lane before lane 0 stores oc + 1
   if (reset) {
     const uint32_t rs = a.rseed[e], rc = a.rcount[e];
 #pragma unroll
@@ -1435,10 +1504,11 @@ __global__ __launch_bounds__(256) void k_synth_step_wide(SynthArgs a, int e0, in
         philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, r);
         const float v = (0.1f * ((2.0f * u01(r[0])) - 1.0f));
         q[i] = v;
-        obs[(long)e * O + i] = v;
+        obs[(long)e * O + i] = a.w.on ? wrap_obs_dim(a.w, e, O, i, oc, v) : v;
       }
     }
     if (lane == 0) {
+      if (a.w.on) a.w.ocount[e] = oc + 1.0f;
       a.rcount[e] = rc + 1;
       a.t[e] = 0;
       a.ep_ret[e] = 0.0f;
@@ -1462,11 +1532,12 @@ __global__ __launch_bounds__(256) void k_synth_step_wide(SynthArgs a, int e0, in
       const float ai = fminf(fmaxf(ar[i % A], lo), hi);
       const float nq = __fmaf_rn(0.9f, qv[c], __fmaf_rn(0.1f, ai, (0.05f * qn)));
       q[i] = nq;
-      obs[(long)e * O + i] = nq;
+      obs[(long)e * O + i] = a.w.on ? wrap_obs_dim(a.w, e, O, i, oc, nq) : nq;
       if (i == 0) { q0_new = nq; q0_old = qv[c]; }
     }
   }
   if (lane != 0) return;
+  if (a.w.on) a.w.ocount[e] = oc + 1.0f;
   const float vel = ((q0_new - q0_old) / 0.05f);
   float ctrl = 0.0f;
   for (int k = 0; k < A; ++k) {
@@ -1477,7 +1548,7 @@ __global__ __launch_bounds__(256) void k_synth_step_wide(SynthArgs a, int e0, in
   const int t = a.t[e] + 1;
   a.t[e] = t;
   const bool tr = t >= 1000;
-  reward[e] = r;
+  reward[e] = a.w.on ? wrap_reward(a.w, e, r, 0.0f) : r;  // the synthetic env never terminates
   done[e] = tr ? 1.0f : 0.0f;
   a.ep_ret[e] = (a.ep_ret[e] + r);
   a.ep_len[e] += 1;
@@ -1644,6 +1715,10 @@ void launch_adv_sq(const AdvArgs& a, int with_std, hipStream_t s) {
 }
 void launch_adv_finalize(const AdvArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_adv_finalize, dim3(nmb_blocks(a.nmb)), dim3(256), 0, s, a);
+}
+void launch_wrap_step(const WrapArgs& w, int O, int e0, int e1, float* obs, float* reward, const float* term,
+                      const float* is_reset, hipStream_t s) {
+  hipLaunchKernelGGL(k_wrap_step, dim3((e1 - e0 + 3) / 4), dim3(256), 0, s, w, O, e0, e1, obs, reward, term, is_reset);
 }
 void launch_synth_reset(const SynthArgs& a, int seed, float* obs, float* done, hipStream_t s) {
   hipLaunchKernelGGL(k_synth_reset, dim3((a.E + 255) / 256), dim3(256), 0, s, a, seed, obs, done);

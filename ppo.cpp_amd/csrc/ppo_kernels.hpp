@@ -156,8 +156,23 @@ struct AdvArgs {
 };
 #define PPO_ADV_SPLIT 32
 
+// The PPO trainer's env wrapper chain behind a device vector env (ppo:41-49; include/ppo_env_wrappers.h),
+// one state per env in one allocation of 2*E*O + 5*E floats (the oracle's orc_vwrap_* layout).
+struct WrapArgs {
+  float* om;      // [E][O] NormalizeObservation mean_ (stateful_observation.h:56-84)
+  float* ov;      // [E][O] var_
+  float* ocount;  // [E]    count_
+  float* rmean;   // [E]    NormalizeReward mean_ / var_ / accumulated_reward_ / count_ (stateful_reward.h:55-91)
+  float* rvar;
+  float* racc;
+  float* rcount;
+  float gamma;
+  int on;         // 0: no chain (the AC trainer's envs, ac:50-53)
+};
+
 #define PSYN_MAXO 384  // device synthetic env: max observation width (k_synth_step_wide above 32)
 struct SynthArgs {
+  WrapArgs w;  // applied inside the env's own kernels when w.on
   int E, O, A;
   float* q;
   int* t;
@@ -199,3 +214,5 @@ void launch_adv_finalize(const AdvArgs& a, hipStream_t s);
 void launch_synth_reset(const SynthArgs& a, int seed, float* obs, float* done, hipStream_t s);
 void launch_synth_step(const SynthArgs& a, int e0, int e1, const float* act, float lo, float hi, float* obs,
                        float* reward, float* done, hipStream_t s);
+void launch_wrap_step(const WrapArgs& w, int O, int e0, int e1, float* obs, float* reward, const float* term,
+                      const float* is_reset, hipStream_t s);

@@ -156,6 +156,7 @@ SYMBOLS = [
     ("ppo_comm_destroy", _I, [_VP]),
     ("ppo_comm_broadcast_params", _I, [_VP, _I]),
     ("ppo_comm_allreduce", _I, [_VP, _FP, _L, _I]),
+    ("ppo_comm_info", _I, [_VP, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
     ("ppo_set_device", _I, [_I]),
     ("ppo_device_count", _I, [C.POINTER(_I)]),
     ("ppo_dev_malloc", _I, [C.POINTER(_VP), _SZ]),
@@ -176,6 +177,14 @@ SYMBOLS = [
     ("psyn_episode_stats_begin", _I, [_VP, _VP]),
     ("psyn_episode_stats_end", _I, [_VP, C.POINTER(_F), C.POINTER(_F), C.POINTER(_F)]),
     ("ppo_rollout_synth", _I, [_VP, _VP, _FP, _FP, _FP, _FP]),
+    ("psyn_set_action_space", _I, [_VP, _F, _F]),
+    ("psyn_action_space", _I, [_VP, C.POINTER(_F), C.POINTER(_F)]),
+    ("psyn_attach_wrappers", _I, [_VP, _VP]),
+    ("pwrap_create", _I, [_I, _I, _F, C.POINTER(_VP)]),
+    ("pwrap_destroy", _I, [_VP]),
+    ("pwrap_reset", _I, [_VP, _I, _I, _FP, _VP]),
+    ("pwrap_step", _I, [_VP, _I, _I, _FP, _FP, _FP, _FP, _VP]),
+    ("pwrap_read_state", _I, [_VP, _FP, _L]),
     ("ppo_carla_create", _I, [C.POINTER(CarlaConfig), _I, C.POINTER(_VP)]),
     ("ppo_carla_destroy", _I, [_VP]),
     ("ppo_carla_get_layout", _I, [_VP, C.POINTER(CarlaLayout)]),
@@ -591,6 +600,13 @@ class Agent:
         check(lib().ppo_comm_allreduce(self.h, buf.ptr, int(np.prod(buf.shape)), int(average)))
         self.sync()
 
+    def comm_info(self):
+        """(kind, rank, world) of the attached communicator: kind "none" / "rccl" / "host"; for RCCL
+        rank and world are what the communicator itself reports (ncclCommUserRank / ncclCommCount)."""
+        k, r, w = C.c_int(), C.c_int(), C.c_int()
+        check(lib().ppo_comm_info(self.h, C.byref(k), C.byref(r), C.byref(w)))
+        return ({0: "none", 1: "rccl", 2: "host"}[k.value], r.value, w.value)
+
 
 class CarlaAgent:
     """The CaRL CNN agent (include/carla/carla_model.h AgentImpl) on the device.
@@ -697,9 +713,58 @@ class SynthEnv:
         check(lib().psyn_episode_stats(self.h, C.byref(r), C.byref(l_), C.byref(n)))
         return r.value, l_.value, n.value
 
+    def set_action_space(self, lo, hi):
+        check(lib().psyn_set_action_space(self.h, lo, hi))
+
+    def attach_wrappers(self, wrappers: "EnvWrappers | None"):
+        """Run the wrapper chain inside the env's own kernels (psyn_attach_wrappers); None detaches."""
+        check(lib().psyn_attach_wrappers(self.h, wrappers.h if wrappers is not None else None))
+        self._wrappers = wrappers  # keep the state alive while attached
+
     def close(self):
         if getattr(self, "h", None):
             lib().psyn_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class EnvWrappers:
+    """The PPO trainer's env wrapper chain on the device (include/ppo_env_wrappers.h; ppo:41-49):
+    NormalizeObservation -> clamp -> NormalizeReward -> clamp, one state per env in HBM."""
+
+    def __init__(self, num_envs, obs_dim, gamma=0.99):
+        h = C.c_void_p()
+        check(lib().pwrap_create(num_envs, obs_dim, gamma, C.byref(h)))
+        self.h = h.value
+        self.E, self.O, self.gamma = num_envs, obs_dim, gamma
+
+    def reset(self, obs: DeviceArray, e0=0, e1=None, stream=None):
+        check(lib().pwrap_reset(self.h, e0, self.E if e1 is None else e1, obs.ptr, stream))
+
+    def step(self, obs: DeviceArray, reward: DeviceArray, term: DeviceArray | None = None,
+             is_reset: DeviceArray | None = None, e0=0, e1=None, stream=None):
+        check(lib().pwrap_step(self.h, e0, self.E if e1 is None else e1, obs.ptr, reward.ptr,
+                               term.ptr if term is not None else None, is_reset.ptr if is_reset is not None else None,
+                               stream))
+
+    def state(self):
+        """dict of the per-env state: obs_mean / obs_var [E,O], obs_count, rew_mean, rew_var, rew_acc,
+        rew_count [E]"""
+        E, O = self.E, self.O
+        h = np.empty(2 * E * O + 5 * E, np.float32)
+        check(lib().pwrap_read_state(self.h, h.ctypes.data, h.size))
+        t = h[2 * E * O:].reshape(5, E)
+        return {"obs_mean": h[:E * O].reshape(E, O), "obs_var": h[E * O:2 * E * O].reshape(E, O), "obs_count": t[0],
+                "rew_mean": t[1], "rew_var": t[2], "rew_acc": t[3], "rew_count": t[4]}
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().pwrap_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -713,7 +778,11 @@ class Trainer:
     """The reference main() loop (ppo:375-586 / ac:624-950) on the device-resident synthetic env:
     lr anneal -> rollout (T x act + env step) -> GAE -> update. One call = one iteration."""
 
-    def __init__(self, cfg: PPOConfig, num_envs_per_device=None, rank=0, world_size=1, device=0, params=None):
+    def __init__(self, cfg: PPOConfig, num_envs_per_device=None, rank=0, world_size=1, device=0, params=None,
+                 wrappers=None):
+        """wrappers: the PPO env wrapper chain (ppo:41-49) on the device env; default = what the
+        reference trainer uses: on for the PPO agent (ppo_continuous_action), off for the AC agent
+        (ac_ppo_continuous_action wraps its envs in RecordEpisodeStatistics only, ac:50-53)."""
         self.cfg = cfg
         self.hcfg = hip_config(cfg, num_envs_per_device, rank, world_size)
         self.agent = Agent(self.hcfg, device)
@@ -722,6 +791,13 @@ class Trainer:
         self.agent.load_params(params)
         E, O, A = self.hcfg.num_envs, self.hcfg.obs_dim, self.hcfg.act_dim
         self.env = SynthEnv(E, O, A)
+        if cfg.env_id in ENV_DIMS:
+            self.env.set_action_space(ENV_DIMS[cfg.env_id][2], ENV_DIMS[cfg.env_id][3])
+        if wrappers is None:
+            wrappers = self.hcfg.net_kind == PPO_NET_TANH_NORMAL
+        self.wrappers = EnvWrappers(E, O, cfg.gamma) if wrappers else None
+        if self.wrappers is not None:
+            self.env.attach_wrappers(self.wrappers)
         self.next_obs = DeviceArray((E, O))
         self.next_done = DeviceArray(E)
         self.act_scratch = DeviceArray((E, A))
@@ -755,6 +831,8 @@ class Trainer:
     def close(self):
         self.agent.close()
         self.env.close()
+        if self.wrappers is not None:
+            self.wrappers.close()
 
 
 def init_params(layout: Layout, seed=1, env_id=None, obs_mean=None, obs_std=None):

@@ -132,6 +132,36 @@ def minibatch_grad(L, params, x, action, old_logp, adv, ret, old_v, cfg, adv_mea
     return grad, stats
 
 
+def minibatch_grad_parallel(L, params, x, action, old_logp, adv, ret, old_v, cfg, adv_mean=None, adv_std=None,
+                            threads=None, chunk=4096):
+    """minibatch_grad over large M: fixed row chunks on a thread pool (ctypes drops the GIL), partials
+    added in chunk order in double, then finished exactly as the serial form. Equal to
+    minibatch_grad up to the double-precision order of the row sums."""
+    from concurrent.futures import ThreadPoolExecutor
+    M = x.shape[0]
+    if adv_mean is None:
+        adv_mean, adv_std = adv_stats(adv)
+    args = [f32(a) for a in (params, x, action, old_logp, adv, ret, old_v)]
+    bounds = [(r, min(M, r + chunk)) for r in range(0, M, chunk)]
+    threads = threads or max(1, min(len(bounds), int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1))
+
+    def run(b):
+        G = np.zeros(L.P, np.float64); s = np.zeros(6, np.float64)
+        lib().orc_minibatch_grad_part(C.byref(L), fp(args[0]), C.c_int(M), C.c_int(b[0]), C.c_int(b[1]),
+                                      *[fp(a) for a in args[1:]], C.c_float(adv_mean), C.c_float(adv_std),
+                                      C.byref(cfg), fp(G), fp(s))
+        return G, s
+
+    with ThreadPoolExecutor(threads) as ex:
+        parts = list(ex.map(run, bounds))
+    G = np.zeros(L.P, np.float64); s = np.zeros(6, np.float64)
+    for g, ss in parts:
+        G += g; s += ss
+    grad = np.zeros(L.P, np.float32); stats = np.zeros(7, np.float32)
+    lib().orc_minibatch_finish(C.byref(L), C.c_int(M), fp(G), fp(s), C.byref(cfg), fp(grad), fp(stats))
+    return grad, stats
+
+
 def clip_grad_norm(L, grad, max_norm):
     g = f32(grad).copy()
     tn = lib().orc_clip_grad_norm(C.byref(L), fp(g), C.c_float(max_norm))
@@ -172,10 +202,47 @@ def update(L, params, m, v, step, b_obs, b_act, b_logp, b_adv, b_ret, b_val, epo
     return p, m, v, st.value, stats
 
 
-class SynthEnv:
-    """Oracle synthetic vector env (SeqVectorEnv + RecordEpisodeStatistics semantics)."""
+class VecWrappers:
+    """Oracle PPO wrapper chain behind a vector env (ppo:41-49; orc_vwrap_*), one state per env."""
 
-    def __init__(self, E, O, A):
+    def __init__(self, E, O, gamma=0.99):
+        self.E, self.O, self.gamma = E, O, gamma
+        self.st = np.zeros(2 * E * O + 5 * E, np.float32)
+        lib().orc_vwrap_init(fp(self.st), C.c_int(E), C.c_int(O))
+
+    def reset(self, obs):
+        obs = f32(obs).copy()
+        lib().orc_vwrap_reset(fp(self.st), C.c_int(self.E), C.c_int(self.O), fp(obs))
+        return obs
+
+    def step(self, obs, reward, term, is_reset):
+        obs = f32(obs).copy(); reward = f32(reward).copy()
+        lib().orc_vwrap_step(fp(self.st), C.c_int(self.E), C.c_int(self.O), C.c_float(self.gamma), fp(obs), fp(reward),
+                             fp(f32(term)), fp(f32(is_reset)))
+        return obs, reward
+
+    def state(self):
+        E, O = self.E, self.O
+        t = self.st[2 * E * O:].reshape(5, E)
+        return {"obs_mean": self.st[:E * O].reshape(E, O), "obs_var": self.st[E * O:2 * E * O].reshape(E, O),
+                "obs_count": t[0], "rew_mean": t[1], "rew_var": t[2], "rew_acc": t[3], "rew_count": t[4]}
+
+
+def wrappers_script(O, T, reset_at):
+    """The raw stream of the `wrappers` golden case's scripted env: obs [T+1, O], reward, term, trunc,
+    is_reset [T]."""
+    raw = np.zeros((T + 1, O), np.float32)
+    r, te, tr, rs = (np.zeros(T, np.float32) for _ in range(4))
+    lib().orc_wrappers_script(C.c_int(O), C.c_int(T), C.c_int(reset_at), fp(raw), fp(r), fp(te), fp(tr), fp(rs))
+    return raw, r, te, tr, rs
+
+
+class SynthEnv:
+    """Oracle synthetic vector env (SeqVectorEnv + RecordEpisodeStatistics semantics); with
+    wrappers=True the PPO trainer's wrapper chain (ppo:41-49) sits on top, like make_env."""
+
+    def __init__(self, E, O, A, wrappers=False, gamma=0.99):
+        self.wrap = VecWrappers(E, O, gamma) if wrappers else None
         self.E, self.O, self.A = E, O, A
         self.q = np.zeros((E, O), np.float32); self.t = np.zeros(E, np.int32)
         self.ar = np.zeros(E, np.int32); self.rseed = np.zeros(E, np.uint32); self.rcount = np.zeros(E, np.uint32)
@@ -186,13 +253,16 @@ class SynthEnv:
     def reset(self, seed):
         obs = np.zeros((self.E, self.O), np.float32)
         lib().orc_env_reset(C.byref(self.s), C.c_int(seed), fp(obs))
-        return obs
+        return self.wrap.reset(obs) if self.wrap else obs
 
     def step(self, actions, lo=-1.0, hi=1.0):
         E = self.E
         obs = np.zeros((E, self.O), np.float32)
         r = np.zeros(E, np.float32); te = np.zeros(E, np.float32); tr = np.zeros(E, np.float32)
         ir = np.zeros(E, np.float32); il = np.zeros(E, np.int32)
+        is_reset = (self.ar != 0).astype(np.float32)  # next-step autoreset pending before this step
         lib().orc_env_step(C.byref(self.s), fp(f32(actions)), C.c_float(lo), C.c_float(hi), fp(obs), fp(r), fp(te),
                            fp(tr), fp(ir), fp(il))
+        if self.wrap:
+            obs, r = self.wrap.step(obs, r, te, is_reset)
         return obs, r, te, tr, ir, il

@@ -72,6 +72,49 @@ def test_ac_cli_host_equals_device_env():
     np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.gpu
+def test_ppo_cli_host_equals_device_env():
+    """ppo_continuous_action with host envs (ParVectorEnv of gymcpp::make_env: the wrapper chain of
+    ppo:41-49 on the CPU) and with --env_backend device (the same chain fused into the device env's
+    kernels) ends with bit-identical weights over 3 iterations with autoresets: the device chain
+    reproduces the host chain bit for bit inside the full training loop."""
+    common = ["--env_id", "SyntheticCheetah-v0", "--num_envs", "4", "--num_steps", "400", "--num_minibatches", "4",
+              "--update_epochs", "2", "--total_timesteps", str(4 * 400 * 3), "--seed", "5", "--num_eval_runs", "1"]
+    _run([_exe("ppo_continuous_action"), "--env_backend", "host", "--exp_name_stem", "t_ppo_host"] + common)
+    _run([_exe("ppo_continuous_action"), "--env_backend", "device", "--exp_name_stem", "t_ppo_dev"] + common)
+    L = P.agent_layout(P.PPO_NET_TANH_NORMAL, 17, 6, 64)
+    a = P.load_agent_pth(L, os.path.join(MODELS, "t_ppo_host_5", "model_final.pth"))
+    b = P.load_agent_pth(L, os.path.join(MODELS, "t_ppo_dev_5", "model_final.pth"))
+    np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_ppo_cli_cfg2_humanoid_device_env():
+    """BASELINE cfg2 through the drop-in executable: Humanoid-v4 shapes (O=376, A=17, actions in
+    [-0.4, 0.4]), num_envs=1024, the reference defaults otherwise (num_steps 2048, 32 minibatches,
+    10 epochs), the wrapper chain on the device; two iterations and the final evaluation."""
+    E, T = 1024, 2048
+    out = _run([_exe("ppo_continuous_action"), "--env_id", "Humanoid-v4", "--env_backend", "device", "--num_envs",
+                str(E), "--total_timesteps", str(E * T * 2), "--exp_name_stem", "t_ppo_cfg2", "--seed", "1"])
+    assert out.count("SPS:") == 2 and "Average evaluation return=" in out
+    L = P.agent_layout(P.PPO_NET_TANH_NORMAL, 376, 17, 64)
+    p = P.load_agent_pth(L, os.path.join(MODELS, "t_ppo_cfg2_1", "model_final.pth"))
+    assert p.size == L.P and np.isfinite(p).all()
+
+
+@pytest.mark.gpu
+def test_ac_cli_ant_device_env():
+    """cfg4's agent shape (Ant-v5: O=105, A=8, the Ant observation normalisation table) on the device env
+    through ac_ppo_continuous_action."""
+    out = _run([_exe("ac_ppo_continuous_action"), "--env_id", "Ant-v5", "--env_backend", "device", "--num_envs", "256",
+                "--num_steps", "32", "--total_timesteps", str(256 * 32 * 2), "--exp_name_stem", "t_ac_ant",
+                "--num_eval_runs", "1"])
+    assert out.count("SPS:") == 2
+    L = P.agent_layout(P.PPO_NET_LN_BETA, 105, 8, 256)
+    p = P.load_agent_pth(L, os.path.join(MODELS, "t_ac_ant_1", "model_final.pth"))
+    assert np.isfinite(p).all()
+
+
 def test_cli_flag_errors():
     """Flag parsing follows args.hxx: unknown flags / bad bool values fail with a message (no GPU)."""
     exe = _exe("ac_ppo_continuous_action")

@@ -41,3 +41,17 @@ def test_bench_two_ranks_host_transport():
         assert k in d, k
     assert d["n_gpus"] == 2 and d["config"]["num_envs_per_device"] == 512 and d["config"]["parallelism"] == "dp2"
     assert d["value"] > 0 and "comm" in d["config"]
+
+
+def test_bench_gpus_flag_starts_the_ranks_itself():
+    """`bench.py --gpus 2` with no external launcher runs two ranks (the driver's SCALE runs may call
+    it that way); the communicator itself reports the rank count."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup",
+                        "1", "--comm", "host", "--num-envs", "4096", "--no-cli"], capture_output=True, text=True,
+                       timeout=300, cwd=ROOT, env=env, check=True)
+    d = last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["num_envs_per_device"] == 2048 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["comm_ranks"] == 2 and d["config"]["comm_kind"] == "host"
+    assert "cpu_baseline" not in d
+

@@ -40,7 +40,7 @@ def test_end_to_end_iterations_vs_libtorch_replay(case):
     cfg = ppo_amd.PPOConfig(**common) if kind == 0 else ppo_amd.ACPPOConfig(**common)
     L = ppo_amd.agent_layout(kind, 17, 6, cfg.hidden)
     p0 = hash_params(L, meta["hash_base"])
-    tr = ppo_amd.Trainer(cfg, params=p0)
+    tr = ppo_amd.Trainer(cfg, params=p0, wrappers=False)  # these replays feed the raw env (see e2e_ppo_wrapped)
     rows = []
     for _ in range(NIT):
         st = tr.iterate(want_stats=True)

@@ -2,10 +2,10 @@
 (oracle/ref_harness.cpp width_cases()), through the C-ABI:
 
   ac256   AC agent, 2x256 LayerNorm trunks + Beta heads (ac:150-249), HalfCheetah O=17 / A=6
-          -> k_act3 (act), k_upd<256, LN_BETA> + k_dwf (update)
+          -> k_act (API act), k_act3 (rollout act), k_upd<256, LN_BETA> + k_dwf (update)
   ant256  the same agent at Ant-v5 O=105 / A=8 (cfg4)
   hum376  PPO agent, 2x64 tanh + Normal (ppo:120-157), Humanoid-v4 O=376 / A=17 (cfg2)
-          -> k_act2<64, TANH> (act), k_fwdbwd<376> + k_dw (update)
+          -> k_act (API act), k_act4 (rollout act: K-split, wide input), k_upd2 + k_dw2 (update)
   gae_long / gae_t{1,7,33}  k_gae at cfg2's T=2048 (E=1024) and at ragged T (32-step load chunks)
 
 Tolerances (fp32; MFMA f32 chains vs LibTorch's CPU GEMMs, the same bars as test_gpu_parity.py):
@@ -16,6 +16,8 @@ Tolerances (fp32; MFMA f32 chains vs LibTorch's CPU GEMMs, the same bars as test
 """
 import numpy as np
 import pytest
+
+import oracle_lib as O
 
 from golden_inputs import column_fnv, gae_long_inputs, hash_params
 from golden_io import load_case
@@ -66,7 +68,20 @@ def test_act_vs_golden_at_reference_width(pre, kind):
         np.testing.assert_allclose(lpm.numpy(), d["mean_logprob"], rtol=2e-5, atol=1e-4)
     else:
         np.testing.assert_allclose(am.numpy(), d["mean"], rtol=1e-5, atol=2e-6)
-    # the rollout act kernel (the one the trainer launches every step) on the same rows
+    ag.close()
+    # the rollout act kernel (the one the trainer launches every step) on the same rows, as rollout
+    # step 0 of a context with E = n envs: the stored value vs the golden critic output, the sampled
+    # actions and their log-probs vs the oracle drawing the same Philox counters
+    ag = agent_for(meta, n, T=2)
+    ag.load_params(p)
+    done = DeviceArray.from_numpy(np.zeros(n, np.float32))
+    ag.rollout_act(0, 0, n, x, done)
+    np.testing.assert_array_equal(ag.buffer(ppo_amd.BUF_OBS, (2, n, meta["O"])).numpy()[0], d["x"])
+    np.testing.assert_allclose(ag.buffer(ppo_amd.BUF_VALUES, (2, n)).numpy()[0], d["value"], rtol=2e-5, atol=2e-5)
+    L = O.layout_init(meta["kind"], meta["O"], meta["A"], meta["H"])
+    oa, olp, _, _ = O.get_action_and_value(L, p, d["x"], 0, seed=1, rank=0, env_base=0, step_id=0)
+    np.testing.assert_allclose(ag.buffer(ppo_amd.BUF_ACTIONS, (2, n, meta["A"])).numpy()[0], oa, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(ag.buffer(ppo_amd.BUF_LOGPROBS, (2, n)).numpy()[0], olp, rtol=1e-4, atol=1e-3)
     ag.close()
 
 

@@ -322,8 +322,8 @@ def test_full_iteration_vs_oracle(kind):
                                                               ("ret", ppo_amd.BUF_RETURNS),
                                                               ("val", ppo_amd.BUF_VALUES))}
     gpu_act = tr.agent.buffer(ppo_amd.BUF_ACTIONS, (T, E, A)).numpy()
-    # oracle replay
-    oenv = O.SynthEnv(E, O_, A)
+    # oracle replay (the PPO trainer's envs carry the wrapper chain of ppo:41-49, the AC trainer's not)
+    oenv = O.SynthEnv(E, O_, A, wrappers=(kind == 0), gamma=cfg.gamma)
     nobs = oenv.reset(cfg.seed)
     ndone = np.zeros(E, np.float32)
     bo = np.zeros((T, E, O_), np.float32); ba = np.zeros((T, E, A), np.float32)
@@ -499,7 +499,7 @@ def test_cfg1_shape_iteration_vs_oracle():
                                                               ("ret", ppo_amd.BUF_RETURNS),
                                                               ("val", ppo_amd.BUF_VALUES))}
     gpu_act = tr.agent.buffer(ppo_amd.BUF_ACTIONS, (T, E, A)).numpy()
-    oenv = O.SynthEnv(E, O_, A)
+    oenv = O.SynthEnv(E, O_, A, wrappers=True, gamma=cfg.gamma)  # ppo:41-49 wrapper chain, as the Trainer
     nobs = oenv.reset(cfg.seed)
     ndone = np.zeros(E, np.float32)
     bo = np.zeros((T, E, O_), np.float32); ba = np.zeros((T, E, A), np.float32)
@@ -513,6 +513,7 @@ def test_cfg1_shape_iteration_vs_oracle():
         br[t] = r
         ndone = np.maximum(te, trn)
     assert bd.sum() >= 2  # the 1000-step truncation and its autoreset happen inside the rollout
+    np.testing.assert_allclose(tr.agent.buffer(ppo_amd.BUF_REWARDS, (T, E)).numpy(), br, rtol=1e-3, atol=1e-4)
     _, _, _, nv = O.get_action_and_value(L, p, nobs, 2)
     adv, ret = O.gae(br, bv, bd, nv, ndone, 0.99, 0.95)
     np.testing.assert_allclose(gpu_obs, bo, rtol=1e-4, atol=1e-5)

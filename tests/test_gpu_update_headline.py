@@ -1,0 +1,72 @@
+"""The PPO update at the sizes the benchmarks run it, against the C oracle.
+
+At the metric config (AC 2x256 LN/Beta, HalfCheetah O=17 / A=6, E=4096, T=128, 4 minibatches) each
+minibatch is M = 131 072 rows, so every k_upd workgroup walks 16 row tiles and accumulates its slab
+of small gradients across them, and k_dwf sums 128 split-K chunks; the cfg4 shard (Ant O=105 / A=8,
+E=1024 per GPU) runs M = 32 768. Here one update with one minibatch of exactly that size
+(T=32, MB=1, EP=1 gives the same M, tiles per workgroup and chunk count) is compared with the
+oracle's gradient over the same gathered rows (oracle/ppo_oracle.c orc_minibatch_grad_part, row
+chunks on a thread pool, partials added in a fixed order) and with the oracle's clip_grad_norm_ +
+Adam step applied to the oracle's gradient.
+
+Tolerances: raw gradient rel-L2 < 2e-4 overall and < 2e-3 per tensor, loss statistics rtol 2e-4,
+parameters after the Adam step atol 2e-6 (the same bars as the M = 256 golden cases; MFMA fp32
+accumulation order vs the oracle's double sums is the only difference).
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+ppo_amd = pytest.importorskip("ppo_amd")
+from ppo_amd import DeviceArray  # noqa: E402
+from test_gpu_parity import fill_storage, make_agent, random_params, rel  # noqa: E402
+
+
+@pytest.mark.parametrize("name,O_,A,E", [("metric_halfcheetah", 17, 6, 4096), ("cfg4_shard_ant", 105, 8, 1024)])
+def test_headline_minibatch_update_vs_oracle(name, O_, A, E):
+    kind, H, T = 1, 256, 32
+    M = E * T
+    rng = np.random.default_rng(31)
+    L = O.layout_init(kind, O_, A, H)
+    p = random_params(L, rng)
+    x = rng.standard_normal((M, O_)).astype(np.float32)
+    act = rng.uniform(-0.95, 0.95, (M, A)).astype(np.float32)
+    adv = rng.standard_normal(M).astype(np.float32)
+    ret = rng.standard_normal(M).astype(np.float32)
+    # old log-probs / values near the current policy's (the GPU's own forward with the given actions;
+    # the comparison below is of the update only), so the clipped and unclipped branches both occur
+    ag0 = make_agent(kind, O_, A, H, M)
+    ag0.load_params(p)
+    _, lp, _, v = ag0.get_action_and_value(DeviceArray.from_numpy(x), ppo_amd.PPO_GIVEN, DeviceArray.from_numpy(act))
+    lp, v = lp.numpy(), v.numpy()
+    ag0.close()
+    olp = (lp + rng.standard_normal(M) * 0.1).astype(np.float32)
+    ov = (v + rng.standard_normal(M) * 0.1).astype(np.float32)
+    perm = rng.permutation(M).astype(np.int32)
+    clip, lr, mgn, eps = 0.1, 2.5e-4, 0.5, 1e-5
+
+    ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=clip, max_grad_norm=mgn, adam_eps=eps)
+    ag.load_params(p)
+    fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
+    st = ag.update(lr, perms=DeviceArray.from_numpy(perm), want_stats=True)
+    g = ag.last_grad()
+    p1 = ag.params()
+    ag.close()
+
+    cfg = O.LossCfg(clip, 0.01, 0.5, 1, 1)
+    og, ost = O.minibatch_grad_parallel(L, p, x[perm], act[perm], olp[perm], adv[perm], ret[perm], ov[perm], cfg)
+    assert rel(g, og) < 2e-4, rel(g, og)
+    for t in range(L.ntensors):
+        o, n = L.t_off[t], L.t_len[t]
+        if L.t_grad[t]:
+            assert rel(g[o:o + n], og[o:o + n]) < 2e-3, (t, rel(g[o:o + n], og[o:o + n]))
+    np.testing.assert_allclose([st[k] for k in ("pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl",
+                                                 "clipfrac")], ost[:6], rtol=2e-4, atol=2e-6)
+    assert 0.05 < ost[5] < 0.95  # both branches of the clipped surrogate are exercised
+    gc, tn = O.clip_grad_norm(L, og, mgn)
+    np.testing.assert_allclose(st["grad_norm"], tn, rtol=2e-4)
+    op, _, _ = O.adam_step(L, p, gc, np.zeros(L.P, np.float32), np.zeros(L.P, np.float32), 1, lr, eps)
+    np.testing.assert_allclose(p1, op, rtol=0, atol=2e-6)

@@ -295,3 +295,22 @@ def test_e2e_oracle_vs_libtorch_drift():
     np.testing.assert_allclose(rows[:2, :3], want[:2, :3], rtol=2e-5, atol=2e-6)
     drift = np.abs(rows[2, :3] - want[2, :3]) / np.abs(want[2, :3])
     assert drift.max() < 5e-2
+
+
+def test_parallel_minibatch_grad_equals_serial():
+    """The thread-pool form used at the headline minibatch size (test_gpu_update_headline) equals the
+    serial oracle: disjoint row ranges, partials added in double in a fixed order."""
+    L = O.layout_init(1, 17, 6, 256)
+    rng = np.random.default_rng(3)
+    p = (rng.standard_normal(L.P) * 0.05).astype(np.float32)
+    p[L.hi], p[L.lo] = 1.0, -1.0
+    p[L.ostd:L.ostd + 17] = 1.0
+    M = 1500
+    x = rng.standard_normal((M, 17)).astype(np.float32)
+    a = rng.uniform(-0.9, 0.9, (M, 6)).astype(np.float32)
+    z = [rng.standard_normal(M).astype(np.float32) for _ in range(4)]
+    cfg = O.LossCfg(0.1, 0.01, 0.5, 1, 1)
+    g1, s1 = O.minibatch_grad(L, p, x, a, *z, cfg)
+    g2, s2 = O.minibatch_grad_parallel(L, p, x, a, *z, cfg, threads=4, chunk=256)
+    np.testing.assert_allclose(g2, g1, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(s2, s1, rtol=1e-6, atol=1e-9)

@@ -74,3 +74,28 @@ def test_product_wrapper_chain_bit_exact_vs_golden(driver, tmp_path):
     np.testing.assert_array_equal(obs, o_obs)  # product == oracle (both IEEE sqrt), bit for bit
     for i, k in enumerate(("reward", "term", "trunc", "info_ret", "info_len")):
         np.testing.assert_array_equal(rest[i], d[k], err_msg=k)
+
+
+def test_vector_oracle_chain_bit_exact_vs_golden():
+    """orc_vwrap_* (one state per env behind a vector env — the checker of the device chain) fed the
+    scripted env's raw stream reproduces the golden case in every env, bit for bit against the
+    single-env oracle run."""
+    meta, d = load_case("wrappers")
+    Od, T = meta["O"], meta["T"]
+    raw, r, te, tr, rs = O.wrappers_script(Od, T, meta["reset_at"])
+    assert rs.sum() >= 4 and te.sum() >= 3
+    E = 3
+    w = O.VecWrappers(E, Od, meta["gamma"])
+    obs0 = w.reset(np.tile(raw[0], (E, 1)))
+    o_obs, o_out, o_mean, o_var = _oracle_run(Od, T, meta["reset_at"], meta["gamma"])
+    np.testing.assert_array_equal(obs0, np.tile(o_obs[0], (E, 1)))
+    for t in range(T):
+        ob, rw = w.step(np.tile(raw[t + 1], (E, 1)), np.full(E, r[t], np.float32), np.full(E, te[t], np.float32),
+                        np.full(E, rs[t], np.float32))
+        np.testing.assert_array_equal(ob, np.tile(o_obs[t + 1], (E, 1)))
+        np.testing.assert_array_equal(rw, np.full(E, o_out["reward"][t], np.float32))
+        np.testing.assert_array_max_ulp(ob[0], d["obs"][t + 1], maxulp=1)
+        np.testing.assert_array_equal(rw[0], d["reward"][t])
+    st = w.state()
+    np.testing.assert_array_equal(st["obs_mean"][1], d["obs_mean_final"])
+    np.testing.assert_array_equal(st["obs_var"][2], d["obs_var_final"])

@@ -252,7 +252,7 @@ def oracle_trainer(case, iterations):
     L = O.layout_init(kind, 17, 6, 64 if kind == 0 else 256)
     p = hash_params(L, meta["hash_base"])
     m = np.zeros(L.P, np.float32); v = np.zeros(L.P, np.float32); step = 0
-    env = O.SynthEnv(E, 17, 6)
+    env = O.SynthEnv(E, 17, 6, wrappers=meta.get("wrappers", False))
     nobs = env.reset(1); ndone = np.zeros(E, np.float32)
     cfg = O.LossCfg(meta["clip_coef"], meta["ent_coef"], 0.5, 1, 1)
     rows = []
@@ -283,6 +283,21 @@ def test_e2e_oracle_ppo_matches_libtorch_replay():
     np.testing.assert_allclose(rows[:, :5], want[:, :5], rtol=2e-5, atol=1e-6)
     np.testing.assert_allclose(rows[:, 5:], want[:, 6:], rtol=1e-5)
     np.testing.assert_allclose(p, d["params_final"], rtol=0, atol=1e-6)
+
+
+def test_e2e_oracle_ppo_wrapped_matches_libtorch_replay():
+    """The PPO trainer loop with the ppo:41-49 wrapper chain on every env (e2e_ppo_wrapped): the
+    oracle (IEEE sqrtf in NormalizeObservation) against the LibTorch replay (MKL's vsSqrt, 1 ulp low
+    on ~0.65 % of inputs, test_wrappers.py) — the stated bars of the GPU test."""
+    rows, p, d = oracle_trainer("e2e_ppo_wrapped", 8)
+    want = d["stats"].astype(np.float64)
+    print("\nmax rel diff per column:", (np.abs(rows[:, :5] - want[:, :5]) / np.abs(want[:, :5])).max(0),
+          "params max abs diff", np.abs(p - d["params_final"]).max())
+    np.testing.assert_array_equal(rows[:, 6], want[:, 7])
+    np.testing.assert_allclose(rows[:, :3], want[:, :3], rtol=2e-4, atol=1e-6)
+    np.testing.assert_allclose(rows[:, 3:5], want[:, 3:5], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(rows[:, 5], want[:, 6], rtol=1e-5)
+    np.testing.assert_allclose(p, d["params_final"], rtol=0, atol=1e-5)
 
 
 def test_e2e_oracle_vs_libtorch_drift():

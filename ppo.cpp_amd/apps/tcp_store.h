@@ -39,6 +39,7 @@ class TCPStoreServer {
     // bound here (not in the thread) so that a client constructed right after start() finds them
     auto rep = std::make_shared<zmtp::Socket>(zmtp::Type::REP);   // change requests
     auto pub = std::make_shared<zmtp::Socket>(zmtp::Type::PUB);   // current state
+    rep->set_max_msg_size(1 << 16);  // the store's commands are one byte; the port is open to the network
     rep->bind("tcp://*:" + std::to_string(port_));
     pub->bind("tcp://" + rdvz_addr_ + ":" + std::to_string(port_ + 1));
     std::cout << "Server started, waiting for requests..." << std::endl;

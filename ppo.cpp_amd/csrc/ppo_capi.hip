@@ -120,10 +120,11 @@ extern "C" const char* ppo_version(void) { return "ppo_hip 0.1 (gfx950)"; }
 // ------------------------------------------------------------------------------------------
 enum {
   PK_ACT = 0, PK_FWDBWD, PK_DW2, PK_DW1, PK_COLSUM, PK_GRADNORM, PK_ADAM, PK_GAE, PK_PERM, PK_ADV, PK_ALLREDUCE,
-  PK_SYNTH, PK_COUNT
+  PK_SYNTH, PK_ROLLOUT, PK_VALUES, PK_COUNT
 };
 static const char* kProfNames[PK_COUNT] = {"act", "fwdbwd", "dw", "dw_l1", "colsum", "gradnorm",
-                                           "adam", "gae", "perm", "adv_stats", "allreduce", "synth_env"};
+                                           "adam", "gae", "perm", "adv_stats", "allreduce", "synth_env",
+                                           "rollout", "values"};
 
 struct ProfEvent {
   int id;
@@ -174,6 +175,7 @@ struct ppo_ctx {
   int act_kernel = 0;  // 0: the fastest act kernel for the shape; 2 / 4: force k_act2 / k_act4 (PPO_ACT_KERNEL, A/B)
   int upd_trunk_mask = 3, upd_sched = 1;   // k_upd launch options (PPO_UPD_TRUNK: PPO_DIAG builds only)
   int dw_fused = 1;
+  int rollout_mode = PPO_ROLLOUT_AUTO;  // ppo_set_rollout_mode
   // profiling
   unsigned prof_mask = 0;
   std::mutex prof_mu;
@@ -1158,6 +1160,46 @@ extern "C" int ppo_rollout_synth(ppo_t* c, psyn_t* env, float* next_obs, float* 
   const int E = c->cfg.num_envs;
   if (env->a.E != E || env->a.O != c->K.O || env->a.A != c->K.A) return fail("ppo_rollout_synth: env shape mismatch");
   const float lo = env->act_lo, hi = env->act_hi;
+  if (c->rollout_mode == PPO_ROLLOUT_AUTO && !env->a.w.on && rollout_supported(c->K) == 0) {
+    // one persistent launch for all T steps (k_rollout), then the critic over the stored rows
+    RolloutArgs r;
+    memset(&r, 0, sizeof(r));
+    r.P = c->P;
+    r.K = c->K;
+    r.WSW = c->WSW[1];
+    r.E = E;
+    r.T = c->cfg.num_steps;
+    r.step0 = c->iteration * (long)c->cfg.num_steps;
+    r.seed = c->cfg.seed;
+    r.rank = c->rank;
+    r.next_obs = next_obs;
+    r.next_done = next_done;
+    r.s_obs = c->buf[PPO_BUF_OBS];
+    r.s_actions = c->buf[PPO_BUF_ACTIONS];
+    r.s_logp = c->buf[PPO_BUF_LOGPROBS];
+    r.s_dones = c->buf[PPO_BUF_DONES];
+    r.s_rewards = c->buf[PPO_BUF_REWARDS];
+    r.env = env->a;
+    r.lo = lo;
+    r.hi = hi;
+    {
+      ProfScope ps(c, PK_ROLLOUT, c->stream);
+      if (launch_rollout(r, c->stream) != 0) return fail("ppo_rollout_synth: rollout kernel launch failed");
+    }
+    ValuesArgs v;
+    v.P = c->P;
+    v.K = c->K;
+    v.WSW = c->WSW[0];
+    v.obs = c->buf[PPO_BUF_OBS];
+    v.values = c->buf[PPO_BUF_VALUES];
+    v.n = (long)E * c->cfg.num_steps;
+    {
+      ProfScope ps(c, PK_VALUES, c->stream);
+      if (launch_values(v, c->stream) != 0) return fail("ppo_rollout_synth: values kernel launch failed");
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
   for (int t = 0; t < c->cfg.num_steps; ++t) {
     int rc = ppo_rollout_act(c, t, 0, E, next_obs, next_done, act_scratch, nullptr);
     if (rc) return rc;
@@ -1318,5 +1360,12 @@ extern "C" int psyn_attach_wrappers(psyn_t* env, pwrap_t* p) {
   }
   if (p->E != env->a.E || p->O != env->a.O) return fail("psyn_attach_wrappers: shape mismatch");
   env->a.w = p->w;
+  return 0;
+}
+
+extern "C" int ppo_set_rollout_mode(ppo_t* c, int mode) {
+  if (!c) return fail("null ctx");
+  if (mode != PPO_ROLLOUT_AUTO && mode != PPO_ROLLOUT_PER_STEP) return fail("ppo_set_rollout_mode: bad mode");
+  c->rollout_mode = mode;
   return 0;
 }

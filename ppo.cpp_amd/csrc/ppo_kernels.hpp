@@ -186,6 +186,37 @@ struct SynthArgs {
   float* fin_cnt;
 };
 
+// Persistent device-env rollout (ppo_rollout.hip, k_rollout): all T steps of act + env step in one
+// launch, one 16-env block per workgroup, the actor's weights resident in registers.
+struct RolloutArgs {
+  const float* P;
+  PackedLayout K;
+  const float* WSW;     // actor trunk's swizzled W1 | W2 | W2^T
+  int E, T;
+  long step0;           // Philox step counter of step 0 (iteration * T)
+  uint64_t seed;
+  int rank;
+  float* next_obs;      // [E][O] in: the obs of step 0; out: the obs after step T-1
+  float* next_done;     // [E]
+  float *s_obs, *s_actions, *s_logp, *s_dones, *s_rewards;
+  SynthArgs env;
+  float lo, hi;         // the env's action space (clip_actions)
+};
+// Critic forward over n stored rows (ppo_rollout.hip, k_values): values[i] = critic(obs[i]), the
+// same chain as k_act3's critic workgroups, so each value is bitwise the one the per-step act
+// kernel stores.
+struct ValuesArgs {
+  const float* P;
+  PackedLayout K;
+  const float* WSW;     // critic trunk's swizzled copy
+  const float* obs;     // [n][O]
+  float* values;        // [n]
+  long n;
+};
+int rollout_supported(const PackedLayout& K);
+int launch_rollout(const RolloutArgs& a, hipStream_t s);
+int launch_values(const ValuesArgs& a, hipStream_t s);
+
 // sets the thread-local ppo_last_error() message and returns code (ppo_capi.hip)
 int ppo_fail(const std::string& msg, int code);
 

@@ -1,0 +1,454 @@
+// ppo_rollout.hip — the device-env rollout as one persistent launch, and the critic as one pass
+// over the stored observations (ppo:387-434, ac:641-698).
+//
+// A per-step rollout costs two launches per step (agent act, env step), each ~5 us of launch floor
+// plus a cold 256 KB stream of W2 from L2 into every CU ("Why the act launches cost what
+// they cost"). Here:
+//  * k_rollout: one workgroup owns 16 envs for all T steps. The actor's W2 slice of each wave
+//    (32 output features x 256 inputs, 128 VGPRs) and W1 slice stay in registers; obs -> actor ->
+//    Beta sample -> action -> env step -> obs loops inside the kernel with LDS barriers only. The
+//    critic is not on this chain: the value of step t depends only on obs[t], so it is computed
+//    afterwards for all T x E stored rows at once (k_values).
+//  * k_values: the critic forward of n stored rows; the critic's weights resident in registers
+//    the same way, workgroups walk 16-row blocks.
+// Both use the building blocks of k_act3 (ppo_act_common.hpp) in the same order: every action,
+// log-prob, value, reward and observation is bitwise the one the per-step path produces
+// (tests/test_gpu_rollout.py).
+#include "ppo_act_common.hpp"
+
+using namespace act;
+
+namespace {
+
+constexpr int kRows = 16;  // envs (rows) per workgroup
+
+template <int NTO, int NHT>
+struct RollGeo {
+  static constexpr int H = 256, OP = NTO * 16, NHP = 16 * NHT;
+  static constexpr int LDX = ((OP + 63) / 64) * 64 + 4;
+  static constexpr int LDH = H + 4;
+  static constexpr int LDP = NHP + 4;
+  static constexpr int LDQ = OP + 1;                           // env state / obs rows (O <= OP)
+  static constexpr int NSP = 6 * H + NHP * H;
+  static constexpr int oXS = 0;
+  static constexpr int oHB = oXS + kRows * LDX;
+  static constexpr int oSP = oHB + kRows * LDH;
+  static constexpr int oHBIAS = oSP + NSP;
+  static constexpr int oRED = oHBIAS + NHP;
+  static constexpr int oHP = oRED + 2 * kActWaves * kRows;
+  static constexpr int oPRE = oHP + kActWaves * NHP * kRows;
+  static constexpr int oXO = oPRE + kRows * LDP;               // agent input obs of the current step
+  static constexpr int oQ = oXO + kRows * LDQ;                 // env state q
+  static constexpr int oNRM = oQ + kRows * LDQ;                // obs mean | std (OP each)
+  static constexpr int oACT = oNRM + 2 * OP;                   // actions [16][24]
+  static constexpr int oENV = oACT + kRows * 24;               // per-env scalars, 12 x 16
+  static constexpr int total = oENV + 12 * kRows;
+  // distribution scratch in the XS / HB region (dead after layer 2), as in k_act3
+  static constexpr int oITM = 0;
+  static constexpr int oLP = oITM + kRows * 24 * 2 * 4;
+  static_assert(oLP + kRows * 24 * 2 <= oSP, "distribution scratch must fit in the XS/HB region");
+  // staged param vectors inside SP (as ActGeo)
+  static constexpr int sB1 = 0, sG1 = H, sBE1 = 2 * H, sB2 = 3 * H, sG2 = 4 * H, sBE2 = 5 * H, sW3 = 6 * H;
+};
+
+// per-env scalar slots in the oENV region
+enum { EV_DONE = 0, EV_AR, EV_T, EV_RSEED, EV_RCOUNT, EV_EPR, EV_EPL, EV_FR, EV_FL, EV_FC, EV_NSLOT };
+
+// staged small parameters of one trunk into LDS (biases, LayerNorm affine, head rows, head biases)
+template <int NHP>
+PPO_DEV void stage_params(const PackedLayout& K, const TrunkDev& T, PBuf pb, int trunk, float* SP, float* HBIAS,
+                          int tid) {
+  constexpr int H = 256, NSP4 = (6 * H + NHP * H) / 4;
+  for (int q = tid; q < NSP4; q += kActThreads) {
+    const int fl = 4 * q, vec = fl / H, off = fl - vec * H;
+    int src = -1;
+    if (vec < 6) {
+      const int base = vec == 0 ? T.b1 : vec == 1 ? T.g1 : vec == 2 ? T.be1 : vec == 3 ? T.b2 : vec == 4 ? T.g2 : T.be2;
+      src = base >= 0 ? base + off : -1;
+    } else {
+      const int hr = act_head_row(K, trunk, vec - 6);
+      src = hr >= 0 ? hr + off : -1;
+    }
+    *reinterpret_cast<f4*>(SP + fl) = pld4(pb, src >= 0 ? src : K.size, 0);
+  }
+  if (tid < NHP) {
+    const int hbo = act_head_bias(K, trunk, tid);
+    HBIAS[tid] = bld1f(pb, hbo >= 0 ? hbo : K.size);
+  }
+}
+
+// One trunk forward for the 16 rows whose (normalised, zero-padded) inputs are in XS: layer 1,
+// LayerNorm + ReLU, layer 2, LayerNorm + ReLU, heads; leaves the head pre-activations (+ bias) in
+// PRE [16][LDP]. Weights: w1 / w2 register slices of this wave. Same operations, same order as
+// k_act3 (LN_BETA, RT = 1).
+template <int NTO, int NHT>
+PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* lds, int nh, int tid) {
+  using GE = RollGeo<NTO, NHT>;
+  constexpr int H = 256, LDX = GE::LDX, LDH = GE::LDH, LDP = GE::LDP, NHP = GE::NHP, R = kRows;
+  float* XS = lds + GE::oXS;
+  float* HB = lds + GE::oHB;
+  float* SP = lds + GE::oSP;
+  float* HBIAS = lds + GE::oHBIAS;
+  float* RED = lds + GE::oRED;
+  float* HP = lds + GE::oHP;
+  float* PRE = lds + GE::oPRE;
+  const int lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  f4 acc[2][1];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) acc[u][0] = *reinterpret_cast<const f4*>(SP + GE::sB1 + 32 * wave + 16 * u + 4 * g);
+  const float* xin = XS + j * LDX + 4 * g;
+  act_layer_regs<NTO, 1>(acc, w1, [&](int t, int) { return *reinterpret_cast<const f4*>(xin + 16 * t); });
+  act_activate<PPO_NET_LN_BETA, 1>(acc, SP + GE::sG1, SP + GE::sBE1, RED, wave, j, g);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) *reinterpret_cast<f4*>(HB + j * LDH + 32 * wave + 16 * u + 4 * g) = acc[u][0];
+  lds_barrier();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) acc[u][0] = *reinterpret_cast<const f4*>(SP + GE::sB2 + 32 * wave + 16 * u + 4 * g);
+  const float* hin = HB + j * LDH + 4 * g;
+  act_layer_regs<16, 1>(acc, w2, [&](int t, int) { return *reinterpret_cast<const f4*>(hin + 16 * t); });
+  act_activate<PPO_NET_LN_BETA, 1>(acc, SP + GE::sG2, SP + GE::sBE2, RED, wave, j, g);
+#pragma unroll
+  for (int ht = 0; ht < NHT; ++ht) {
+    f4 hp = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const f4 wv = *reinterpret_cast<const f4*>(SP + GE::sW3 + (16 * ht + j) * H + 32 * wave + 16 * u + 4 * g);
+      hp = mfma16(wv.x, acc[u][0].x, hp);
+      hp = mfma16(wv.y, acc[u][0].y, hp);
+      hp = mfma16(wv.z, acc[u][0].z, hp);
+      hp = mfma16(wv.w, acc[u][0].w, hp);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) HP[(wave * NHP + 16 * ht + 4 * g + r) * R + j] = hp[r];
+  }
+  lds_barrier();
+  for (int idx = tid; idx < R * nh; idx += kActThreads) {
+    const int r = idx / nh, h = idx - r * nh;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < kActWaves; ++w) s += HP[(w * NHP + h) * R + r];
+    PRE[r * LDP + h] = s + HBIAS[h];
+  }
+  lds_barrier();
+}
+
+// this wave's register slices of a trunk's W1 (NTO k-blocks) and W2 (16 k-blocks), 2 feature tiles
+template <int NTO>
+PPO_DEV void load_weight_slices(PBuf wsw, int wave, int lane, f4 (&w1)[NTO][2], f4 (&w2)[16][2]) {
+  constexpr int H = 256, OP = NTO * 16;
+  const int l1 = ((2 * wave) * NTO * 64 + lane) * 4;
+  const int l2 = H * OP + ((2 * wave) * 16 * 64 + lane) * 4;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+#pragma unroll
+    for (int t = 0; t < NTO; ++t) w1[t][u] = pld4(wsw, l1, 256 * (NTO * u + t));
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w2[t][u] = pld4(wsw, l2, 256 * (16 * u + t));
+  }
+}
+
+}  // namespace
+
+// =============================================================================================
+// k_rollout: T steps of {actor act + sample, synthetic env step} for 16 envs per workgroup
+// =============================================================================================
+template <int NTO, int NHT>
+__global__ __launch_bounds__(512) void k_rollout(RolloutArgs a) {
+  using GE = RollGeo<NTO, NHT>;
+  constexpr int OP = GE::OP, LDX = GE::LDX, LDP = GE::LDP, LDQ = GE::LDQ, R = kRows;
+  constexpr int NCH = (OP + 31) / 32;  // 32-dim chunks of the env state per env lane group
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* XS = lds + GE::oXS;
+  float* PRE = lds + GE::oPRE;
+  float* ITM = lds + GE::oITM;
+  float* LPE = lds + GE::oLP;
+  float* XO = lds + GE::oXO;
+  float* Q = lds + GE::oQ;
+  float* NRM = lds + GE::oNRM;
+  float* ACT = lds + GE::oACT;
+  float* EV = lds + GE::oENV;
+  int* EVI = reinterpret_cast<int*>(EV);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const PackedLayout& K = a.K;
+  const float* __restrict__ P = a.P;
+  const PBuf pb = make_pbuf(P, K.size);
+  const int O = K.O, A = K.A, E = a.E;
+  const int row0 = blockIdx.x * R;
+  const SynthArgs& sv = a.env;
+
+  // ---- prologue: resident weights, staged parameters, env state of this block ----
+  f4 w1[NTO][2], w2[16][2];
+  load_weight_slices<NTO>(make_pbuf(a.WSW, (int)sw_size(256, OP)), wave, lane, w1, w2);
+  stage_params<GE::NHP>(K, K.tr[1], pb, 1, lds + GE::oSP, lds + GE::oHBIAS, tid);
+  for (int f = tid; f < OP; f += kActThreads) {
+    NRM[f] = f < O ? P[K.omean + f] : 0.0f;
+    NRM[OP + f] = f < O ? P[K.ostd + f] : 1.0f;
+  }
+  for (int idx = tid; idx < R * O; idx += kActThreads) {
+    const int r = idx / O, f = idx - r * O, e = row0 + r;
+    XO[r * LDQ + f] = e < E ? a.next_obs[(long)e * O + f] : 0.0f;
+    Q[r * LDQ + f] = e < E ? sv.q[(long)e * O + f] : 0.0f;
+  }
+  if (tid < R) {
+    const int e = min(row0 + tid, E - 1);
+    EV[EV_DONE * R + tid] = a.next_done[e];
+    EVI[EV_AR * R + tid] = sv.autoreset[e];
+    EVI[EV_T * R + tid] = sv.t[e];
+    EVI[EV_RSEED * R + tid] = (int)sv.rseed[e];
+    EVI[EV_RCOUNT * R + tid] = (int)sv.rcount[e];
+    EV[EV_EPR * R + tid] = sv.ep_ret[e];
+    EVI[EV_EPL * R + tid] = sv.ep_len[e];
+    EV[EV_FR * R + tid] = sv.fin_ret[e];
+    EV[EV_FL * R + tid] = sv.fin_len[e];
+    EV[EV_FC * R + tid] = sv.fin_cnt[e];
+  }
+  lds_barrier();
+  const SampleKey key = sample_key(a.seed, a.rank);
+  const float hi = P[K.hi], lo = P[K.lo];
+
+  for (int t = 0; t < a.T; ++t) {
+    const long step_id = a.step0 + t;
+    // ---- inputs: rollout stores of obs[t] / dones[t]; normalised rows into XS (k_act3 order) ----
+    for (int idx = tid; idx < R * OP; idx += kActThreads) {
+      const int r = idx / OP, f = idx - r * OP, e = row0 + r;
+      const bool valid = e < E && f < O;
+      const float x = valid ? XO[r * LDQ + f] : 0.0f;
+      if (valid) a.s_obs[((long)t * E + e) * O + f] = x;
+      XS[r * LDX + f] = valid ? (x - NRM[f]) / NRM[OP + f] : x;
+    }
+    if (tid < R && row0 + tid < E) a.s_dones[(long)t * E + row0 + tid] = EV[EV_DONE * R + tid];
+    lds_barrier();
+    trunk_rows<NTO, NHT>(w1, w2, lds, 2 * A, tid);
+    // ---- Beta sample + log-prob (k_act3 stage 1 / 2, PPO_SAMPLE) ----
+    for (int idx = tid; idx < R * A * 2; idx += kActThreads) {
+      const int which = idx & 1, ra = idx >> 1, r = ra / A, ai = ra - r * A;
+      const long env = row0 + r;
+      const float c = softplusf_(PRE[r * LDP + ai + which * A]) + 1.0f;
+      const uint32_t db = 0x10000u + (uint32_t)(ai * 2 + which) * 64u;
+      const float gs = gamma_mt(c, key, env, step_id, db);
+      float* it = ITM + ((r * A + ai) * 2 + which) * 4;
+      it[0] = c;
+      it[1] = gs;
+      float tg_unused;
+      lgamma_digamma_trigamma(c, it[2], it[3], tg_unused);
+    }
+    lds_barrier();
+    for (int idx = tid; idx < R * A; idx += kActThreads) {
+      const int r = idx / A, ai = idx - r * A, e = row0 + r;
+      const float* ia = ITM + (idx * 2 + 0) * 4;
+      const float* ib = ITM + (idx * 2 + 1) * 4;
+      const float al = ia[0], be = ib[0];
+      const float s01 = ia[1] / (ia[1] + ib[1]);
+      const float ab = al + be;
+      float lgab, psab, tab_unused;
+      lgamma_digamma_trigamma(ab, lgab, psab, tab_unused);
+      const float lga = ia[2], lgb = ib[2];
+      const float lp = xlogyf_(al - 1.0f, s01) + xlogyf_(be - 1.0f, 1.0f - s01) + (lgab - (lga + lgb));
+      const float act = (s01 - 0.0f) / (1.0f - 0.0f) * (hi - lo) + lo;
+      LPE[idx * 2 + 0] = lp;
+      ACT[r * 24 + ai] = act;
+      if (e < E) a.s_actions[((long)t * E + e) * A + ai] = act;
+    }
+    lds_barrier();
+    if (tid < R && row0 + tid < E) {
+      float lp = 0.f;
+      for (int ai = 0; ai < A; ++ai) lp += LPE[(tid * A + ai) * 2];
+      a.s_logp[(long)t * E + row0 + tid] = lp;
+    }
+    // ---- env step (k_synth_step / k_synth_step_wide arithmetic): 32 lanes per env ----
+    {
+#pragma clang fp contract(off)
+      const int r = tid >> 5, i0 = tid & 31, e = row0 + r;
+      const bool live = e < E;
+      const bool reset = EVI[EV_AR * R + r] != 0;
+      float* q = Q + r * LDQ;
+      float* xo = XO + r * LDQ;
+      const float* ar = ACT + r * 24;
+      if (live && reset) {
+        const uint32_t rs = (uint32_t)EVI[EV_RSEED * R + r], rc = (uint32_t)EVI[EV_RCOUNT * R + r];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int i = 32 * c + i0;
+          if (i < O) {
+            uint32_t rr[4];
+            philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, rr);
+            const float v = (0.1f * ((2.0f * u01(rr[0])) - 1.0f));
+            q[i] = v;
+            xo[i] = v;
+          }
+        }
+        if (i0 == 0) {
+          EVI[EV_RCOUNT * R + r] = (int)(rc + 1);
+          EVI[EV_T * R + r] = 0;
+          EV[EV_EPR * R + r] = 0.0f;
+          EVI[EV_EPL * R + r] = 0;
+          EV[EV_DONE * R + r] = 0.0f;
+          EVI[EV_AR * R + r] = 0;
+          a.s_rewards[(long)t * E + e] = 0.0f;
+        }
+      } else if (live) {
+        float qo[NCH], qn[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int i = 32 * c + i0;
+          qo[c] = i < O ? q[i] : 0.0f;
+          qn[c] = i < O ? q[i + 1 < O ? i + 1 : 0] : 0.0f;
+        }
+        float q0_new = 0.0f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int i = 32 * c + i0;
+          if (i < O) {
+            const float ai = fminf(fmaxf(ar[i % A], a.lo), a.hi);
+            const float nq = __fmaf_rn(0.9f, qo[c], __fmaf_rn(0.1f, ai, (0.05f * qn[c])));
+            q[i] = nq;
+            xo[i] = nq;
+            if (c == 0) q0_new = nq;
+          }
+        }
+        if (i0 == 0) {
+          const float vel = ((q0_new - qo[0]) / 0.05f);
+          float ctrl = 0.0f;
+          for (int k = 0; k < A; ++k) {
+            const float ak = fminf(fmaxf(ar[k], a.lo), a.hi);
+            ctrl = (ctrl + ((0.1f * ak) * ak));
+          }
+          const float rw = (vel - ctrl);
+          const int tt = EVI[EV_T * R + r] + 1;
+          EVI[EV_T * R + r] = tt;
+          const bool tr = tt >= 1000;
+          a.s_rewards[(long)t * E + e] = rw;
+          EV[EV_DONE * R + r] = tr ? 1.0f : 0.0f;
+          const float epr = (EV[EV_EPR * R + r] + rw);
+          EV[EV_EPR * R + r] = epr;
+          const int epl = EVI[EV_EPL * R + r] + 1;
+          EVI[EV_EPL * R + r] = epl;
+          if (tr) {
+            EV[EV_FR * R + r] += epr;
+            EV[EV_FL * R + r] += (float)epl;
+            EV[EV_FC * R + r] += 1.0f;
+          }
+          EVI[EV_AR * R + r] = tr ? 1 : 0;
+        }
+      }
+    }
+    lds_barrier();
+  }
+  // ---- epilogue: next_obs / next_done and the env state back to HBM ----
+  for (int idx = tid; idx < R * O; idx += kActThreads) {
+    const int r = idx / O, f = idx - r * O, e = row0 + r;
+    if (e < E) {
+      a.next_obs[(long)e * O + f] = XO[r * LDQ + f];
+      sv.q[(long)e * O + f] = Q[r * LDQ + f];
+    }
+  }
+  if (tid < R && row0 + tid < E) {
+    const int e = row0 + tid;
+    a.next_done[e] = EV[EV_DONE * R + tid];
+    sv.autoreset[e] = EVI[EV_AR * R + tid];
+    sv.t[e] = EVI[EV_T * R + tid];
+    sv.rseed[e] = (uint32_t)EVI[EV_RSEED * R + tid];
+    sv.rcount[e] = (uint32_t)EVI[EV_RCOUNT * R + tid];
+    sv.ep_ret[e] = EV[EV_EPR * R + tid];
+    sv.ep_len[e] = EVI[EV_EPL * R + tid];
+    sv.fin_ret[e] = EV[EV_FR * R + tid];
+    sv.fin_len[e] = EV[EV_FL * R + tid];
+    sv.fin_cnt[e] = EV[EV_FC * R + tid];
+  }
+}
+
+// =============================================================================================
+// k_values: critic(obs[i]) for n stored rows; workgroups walk 16-row blocks
+// =============================================================================================
+template <int NTO, int NHT>
+__global__ __launch_bounds__(512) void k_values(ValuesArgs a) {
+  using GE = RollGeo<NTO, NHT>;
+  constexpr int OP = GE::OP, LDX = GE::LDX, LDP = GE::LDP, R = kRows;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* XS = lds + GE::oXS;
+  float* PRE = lds + GE::oPRE;
+  float* NRM = lds + GE::oNRM;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const PackedLayout& K = a.K;
+  const float* __restrict__ P = a.P;
+  const PBuf pb = make_pbuf(P, K.size);
+  const int O = K.O;
+  f4 w1[NTO][2], w2[16][2];
+  load_weight_slices<NTO>(make_pbuf(a.WSW, (int)sw_size(256, OP)), wave, lane, w1, w2);
+  stage_params<GE::NHP>(K, K.tr[0], pb, 0, lds + GE::oSP, lds + GE::oHBIAS, tid);
+  for (int f = tid; f < OP; f += kActThreads) {
+    NRM[f] = f < O ? P[K.omean + f] : 0.0f;
+    NRM[OP + f] = f < O ? P[K.ostd + f] : 1.0f;
+  }
+  const long nblk = (a.n + R - 1) / R;
+  for (long b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const long row0 = b * R;
+    lds_barrier();  // previous block's PRE reads done; NRM / SP staged (first pass)
+    for (int idx = tid; idx < R * OP; idx += kActThreads) {
+      const int r = idx / OP, f = idx - r * OP;
+      const long row = row0 + r;
+      const bool valid = row < a.n && f < O;
+      const float x = valid ? a.obs[row * O + f] : 0.0f;
+      XS[r * LDX + f] = valid ? (x - NRM[f]) / NRM[OP + f] : x;
+    }
+    lds_barrier();
+    trunk_rows<NTO, NHT>(w1, w2, lds, 1, tid);
+    if (tid < R && row0 + tid < a.n) a.values[row0 + tid] = PRE[tid * LDP];
+  }
+}
+
+// =============================================================================================
+// launchers
+// =============================================================================================
+int rollout_supported(const PackedLayout& K) {
+  if (K.kind != PPO_NET_LN_BETA || K.H != 256 || 2 * K.A > 16) return -1;
+  const int nto = K.OP / 16;
+  return (nto == 1 || nto == 2 || nto == 7) ? 0 : -1;
+}
+
+template <int NTO, int NHT>
+static int launch_rollout_t(const RolloutArgs& a, hipStream_t s) {
+  using GE = RollGeo<NTO, NHT>;
+  const size_t lds = (size_t)GE::total * sizeof(float);
+  static const bool ok = hipFuncSetAttribute((const void*)k_rollout<NTO, NHT>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+  if (!ok) return -2;
+  hipLaunchKernelGGL((k_rollout<NTO, NHT>), dim3((a.E + kRows - 1) / kRows), dim3(kActThreads), lds, s, a);
+  return 0;
+}
+
+int launch_rollout(const RolloutArgs& a, hipStream_t s) {
+  if (rollout_supported(a.K) != 0 || a.env.w.on) return -1;
+  switch (a.K.OP / 16) {
+    case 1: return launch_rollout_t<1, 1>(a, s);
+    case 2: return launch_rollout_t<2, 1>(a, s);
+    case 7: return launch_rollout_t<7, 1>(a, s);
+  }
+  return -1;
+}
+
+template <int NTO, int NHT>
+static int launch_values_t(const ValuesArgs& a, hipStream_t s) {
+  using GE = RollGeo<NTO, NHT>;
+  const size_t lds = (size_t)GE::total * sizeof(float);
+  static const bool ok = hipFuncSetAttribute((const void*)k_values<NTO, NHT>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+  if (!ok) return -2;
+  const long nblk = (a.n + kRows - 1) / kRows;
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const long grid = nblk < ncu ? nblk : ncu;  // one resident workgroup per CU (registers hold the weights)
+  hipLaunchKernelGGL((k_values<NTO, NHT>), dim3((unsigned)grid), dim3(kActThreads), lds, s, a);
+  return 0;
+}
+
+int launch_values(const ValuesArgs& a, hipStream_t s) {
+  if (rollout_supported(a.K) != 0) return -1;
+  switch (a.K.OP / 16) {
+    case 1: return launch_values_t<1, 1>(a, s);
+    case 2: return launch_values_t<2, 1>(a, s);
+    case 7: return launch_values_t<7, 1>(a, s);
+  }
+  return -1;
+}

@@ -135,10 +135,14 @@ class Socket {
   // SUB options (zmq::sockopt::subscribe / conflate)
   void subscribe(const std::string& prefix) {
     subs_.push_back(prefix);
+    std::vector<Peer*> dead;
     for (auto& p : peers_)
-      if (p->ready) send_raw(*p, encode({std::string(1, '\x01') + prefix}));
+      if (p->ready && !send_raw(*p, encode({std::string(1, '\x01') + prefix}))) dead.push_back(p.get());
+    for (Peer* d : dead) drop(d);
   }
   void set_conflate(bool on) { conflate_ = on; }
+  // ZMQ_MAXMSGSIZE: a peer announcing a larger frame is disconnected (0: no limit, libzmq's default)
+  void set_max_msg_size(size_t bytes) { max_msg_size_ = bytes; }
 
   // "tcp://*:port", "tcp://host:port", "ipc:///path"
   void bind(const std::string& endpoint) {
@@ -163,20 +167,30 @@ class Socket {
   // Send one multipart message. PAIR / REQ wait for the peer (timeout_ms < 0: forever); REP replies
   // to the peer of the last request; PUB fans out to the matching subscribers present (none: dropped,
   // as zmq). Returns false on timeout.
+  // A peer that has gone (EPIPE, ECONNRESET, ...) is dropped, as libzmq does, instead of failing
+  // the socket: PUB keeps serving its other subscribers; REP / REQ / PAIR return false.
   bool send(const Message& m, int timeout_ms = -1) {
     if (type_ == Type::SUB) throw Error("zmtp: SUB sockets do not send");
     if (type_ == Type::PUB) {
       pump(0);
+      const std::string bytes = encode(m);
+      std::vector<Peer*> dead;
       for (auto& p : peers_)
-        if (p->ready && matches(*p, m.empty() ? std::string() : m[0])) send_raw(*p, encode(m));
+        if (p->ready && matches(*p, m.empty() ? std::string() : m[0]) && !send_raw(*p, bytes, true))
+          dead.push_back(p.get());
+      for (Peer* d : dead) drop(d);
       return true;
     }
     if (type_ == Type::REP) {
       if (!reply_to_) throw Error("zmtp: REP send without a pending request");
       Message e = reply_env_;
       e.insert(e.end(), m.begin(), m.end());
-      send_raw(*reply_to_, encode(e));
+      Peer* p = reply_to_;
       reply_to_ = nullptr;
+      if (!send_raw(*p, encode(e))) {
+        drop(p);
+        return false;
+      }
       return true;
     }
     Peer* p = wait_peer(timeout_ms);
@@ -185,11 +199,17 @@ class Socket {
       if (awaiting_reply_) throw Error("zmtp: REQ send while a reply is pending");
       Message e{std::string()};  // empty delimiter frame
       e.insert(e.end(), m.begin(), m.end());
-      send_raw(*p, encode(e));
+      if (!send_raw(*p, encode(e))) {
+        drop(p);
+        return false;
+      }
       awaiting_reply_ = true;
       return true;
     }
-    send_raw(*p, encode(m));
+    if (!send_raw(*p, encode(m))) {
+      drop(p);
+      return false;
+    }
     return true;
   }
   bool send(const std::string& single, int timeout_ms = -1) { return send(Message{single}, timeout_ms); }
@@ -254,6 +274,8 @@ class Socket {
   std::vector<std::unique_ptr<Peer>> peers_;
   std::vector<std::string> subs_;
   bool conflate_ = false, awaiting_reply_ = false;
+  size_t max_msg_size_ = 0;
+  static constexpr int kStallMs = 5000;  // a peer that stops reading in the middle of a message is dropped
   size_t rr_ = 0;  // REP fair queueing
   Peer* reply_to_ = nullptr;
   Message reply_env_;
@@ -360,7 +382,7 @@ class Socket {
     p->fd = fd;
     Peer& r = *p;
     peers_.push_back(std::move(p));
-    send_raw(r, greeting());  // the whole greeting at once (RFC 23 allows it)
+    if (!send_raw(r, greeting())) drop(&r);  // the whole greeting at once (RFC 23 allows it)
   }
   void drop(Peer* d) {
     if (reply_to_ == d) reply_to_ = nullptr;
@@ -373,21 +395,30 @@ class Socket {
     if (type_ == Type::REQ) awaiting_reply_ = false;
   }
 
-  void send_raw(Peer& p, const std::string& bytes) {
+  // Writes one encoded message to a peer. false: the peer is gone (any send error but EAGAIN /
+  // EINTR) or stopped reading for kStallMs in the middle of the message -- the caller drops it.
+  // hwm_drop (PUB): a subscriber whose socket buffer is full when the message starts does not get
+  // it (libzmq drops messages for a subscriber at its high-water mark) and stays connected.
+  bool send_raw(Peer& p, const std::string& bytes, bool hwm_drop = false) {
     size_t off = 0;
+    const auto t0 = std::chrono::steady_clock::now();
     while (off < bytes.size()) {
       const ssize_t n = ::send(p.fd, bytes.data() + off, bytes.size() - off, MSG_NOSIGNAL);
       if (n > 0) {
         off += (size_t)n;
         continue;
       }
-      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR)) {
+      if (n < 0 && errno == EINTR) continue;
+      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        if (hwm_drop && off == 0) return true;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(kStallMs)) return false;
         pollfd f{p.fd, POLLOUT, 0};
         ::poll(&f, 1, 100);
         continue;
       }
-      throw Error(std::string("zmtp: send failed: ") + std::strerror(errno));
+      return false;
     }
+    return true;
   }
 
   // read what is available and parse it; false when the peer closed or broke the protocol
@@ -415,7 +446,7 @@ class Socket {
       if (std::memcmp(&g[12], "NULL", 4) != 0) return false;
       p.greeted = true;
       pos = 64;
-      send_raw(p, ready_command(type_));
+      if (!send_raw(p, ready_command(type_))) return false;
     }
     for (;;) {
       if (p.rbuf.size() - pos < 2) break;
@@ -427,6 +458,7 @@ class Socket {
         for (int i = 0; i < 8; ++i) len = (len << 8) | (uint8_t)p.rbuf[pos + 1 + i];
         hdr = 9;
       }
+      if (max_msg_size_ && len > max_msg_size_) return false;  // ZMQ_MAXMSGSIZE: drop the peer
       if (p.rbuf.size() - pos - hdr < len) break;
       std::string body = p.rbuf.substr(pos + hdr, len);
       pos += hdr + len;
@@ -467,7 +499,8 @@ class Socket {
       if (!compatible(type_, peer_type)) return false;
       p.ready = true;
       if (type_ == Type::SUB)
-        for (const auto& s : subs_) send_raw(p, encode({std::string(1, '\x01') + s}));
+        for (const auto& s : subs_)
+          if (!send_raw(p, encode({std::string(1, '\x01') + s}))) return false;
       return true;
     }
     if (name == "SUBSCRIBE" && type_ == Type::PUB) {  // ZMTP 3.1 form

@@ -178,6 +178,7 @@ SYMBOLS = [
     ("psyn_episode_stats_end", _I, [_VP, C.POINTER(_F), C.POINTER(_F), C.POINTER(_F)]),
     ("ppo_rollout_synth", _I, [_VP, _VP, _FP, _FP, _FP, _FP]),
     ("psyn_set_action_space", _I, [_VP, _F, _F]),
+    ("ppo_set_rollout_mode", _I, [_VP, _I]),
     ("psyn_action_space", _I, [_VP, C.POINTER(_F), C.POINTER(_F)]),
     ("psyn_attach_wrappers", _I, [_VP, _VP]),
     ("pwrap_create", _I, [_I, _I, _F, C.POINTER(_VP)]),
@@ -599,6 +600,10 @@ class Agent:
     def comm_allreduce(self, buf: DeviceArray, average=True):
         check(lib().ppo_comm_allreduce(self.h, buf.ptr, int(np.prod(buf.shape)), int(average)))
         self.sync()
+
+    def set_rollout_mode(self, per_step: bool):
+        """ppo_rollout_synth: one persistent launch (default, where supported) or per-step launches."""
+        check(lib().ppo_set_rollout_mode(self.h, 1 if per_step else 0))
 
     def comm_info(self):
         """(kind, rank, world) of the attached communicator: kind "none" / "rccl" / "host"; for RCCL

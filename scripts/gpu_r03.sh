@@ -16,4 +16,10 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --t
 tail -2 $OUT/gpu_all.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -30 $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log
+if [ -n "$BENCH" ]; then
+  timeout -k 10 300 python bench.py --steps 10 --warmup 2 --profile-all --no-cpu-baseline --no-cli > $OUT/bench_all.log 2>&1 || { echo "bench failed"; tail -30 $OUT/bench_all.log; exit 1; }
+  tail -1 $OUT/bench_all.log | cut -c1-600
+  timeout -k 10 300 python bench.py --num-envs 512 --steps 20 --warmup 3 --profile-all --no-cpu-baseline --no-cli > $OUT/bench_e512.log 2>&1 || { echo "bench e512 failed"; tail -30 $OUT/bench_e512.log; exit 1; }
+  tail -1 $OUT/bench_e512.log | cut -c1-600
+fi
 echo done

@@ -12,10 +12,12 @@ LIB = os.path.join(ROOT, "ppo.cpp_amd", "lib", "libppo_hip.so")
 
 def declared_functions():
     names = []
-    for h in ("ppo_hip.h", "ppo_synth_env.h", "ppo_carla.h", "ppo_pth.h"):
+    hdrs = sorted(h for h in os.listdir(os.path.join(ROOT, "include")) if h.endswith(".h"))
+    assert {"ppo_hip.h", "ppo_synth_env.h", "ppo_env_wrappers.h", "ppo_carla.h", "ppo_pth.h"} <= set(hdrs)
+    for h in hdrs:
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        for m in re.finditer(r"^\s*[A-Za-z_][\w\s\*]*?\b((?:ppo|psyn)_\w+)\s*\(", src, flags=re.M):
+        for m in re.finditer(r"^\s*[A-Za-z_][\w\s\*]*?\b((?:ppo|psyn|pwrap)_\w+)\s*\(", src, flags=re.M):
             if "static" not in m.group(0):  # header-only helpers (static inline layout initialisers)
                 names.append(m.group(1))
     return sorted(set(names))
@@ -24,7 +26,8 @@ def declared_functions():
 def test_headers_declare_the_boundary():
     names = declared_functions()
     for required in ("ppo_create", "ppo_get_action_and_value", "ppo_rollout_act", "ppo_compute_gae", "ppo_update",
-                     "ppo_comm_init", "psyn_step"):
+                     "ppo_comm_init", "ppo_comm_info", "psyn_step", "pwrap_step", "psyn_attach_wrappers",
+                     "ppo_set_rollout_mode"):
         assert required in names
 
 

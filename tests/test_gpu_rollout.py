@@ -1,0 +1,77 @@
+"""The persistent device-env rollout (k_rollout + k_values, csrc/ppo_rollout.hip) against the
+per-step path (k_act3 + k_synth_step launches per step) through the C-ABI (ppo_set_rollout_mode).
+
+The persistent kernel keeps the actor's weights in registers and runs obs -> actor -> Beta sample
+-> env step for all T steps in one launch; the critic runs afterwards over the stored observations.
+Both use the same arithmetic in the same order, so the whole rollout storage (obs, actions,
+log-probs, rewards, dones, values), the env state, the episode statistics and -- after the shared
+update -- the parameters must be bitwise equal. Covers ragged env blocks (E not a multiple of 16),
+three observation widths (Hopper 11, HalfCheetah 17, Ant 105 with the Ant normalisation table) and
+the 1000-step truncation with its next-step autoreset (9 x 128 steps)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ppo_amd = pytest.importorskip("ppo_amd")
+
+BUFS = [("obs", "BUF_OBS", 1), ("actions", "BUF_ACTIONS", 2), ("logp", "BUF_LOGPROBS", 0),
+        ("rewards", "BUF_REWARDS", 0), ("dones", "BUF_DONES", 0), ("values", "BUF_VALUES", 0)]
+
+
+def snapshot(tr):
+    E, T, O, A = tr.hcfg.num_envs, tr.hcfg.num_steps, tr.hcfg.obs_dim, tr.hcfg.act_dim
+    out = {}
+    for name, b, kind in BUFS:
+        shape = (T, E, O) if kind == 1 else (T, E, A) if kind == 2 else (T, E)
+        out[name] = tr.agent.buffer(getattr(ppo_amd, b), shape).numpy()
+    out["next_obs"] = tr.next_obs.numpy()
+    out["next_done"] = tr.next_done.numpy()
+    return out
+
+
+@pytest.mark.parametrize("env_id,E,iters", [("HalfCheetah-v5", 200, 9), ("Hopper-v5", 37, 9), ("Ant-v5", 96, 3)])
+def test_persistent_rollout_bitwise_equals_per_step(env_id, E, iters):
+    T = 128
+    cfg = ppo_amd.ACPPOConfig(env_id=env_id, num_envs=E, num_steps=T, num_minibatches=4, update_epochs=2,
+                              total_timesteps=E * T * iters)
+    trs = [ppo_amd.Trainer(cfg), ppo_amd.Trainer(cfg)]
+    trs[1].agent.set_rollout_mode(per_step=True)
+    n_done = 0.0
+    for it in range(iters):
+        snaps, stats = [], []
+        for tr in trs:
+            tr.rollout()
+            tr.agent.sync()
+            snaps.append(snapshot(tr))
+            stats.append(tr.env.episode_stats())
+            tr.agent.compute_gae(tr.next_obs, tr.next_done)
+            tr.agent.update(tr.lr_now(), want_stats=False)
+            tr.iteration += 1
+        for k in snaps[0]:
+            np.testing.assert_array_equal(snaps[0][k], snaps[1][k], err_msg=f"iteration {it}: {k}")
+        assert stats[0] == stats[1], it
+        np.testing.assert_array_equal(trs[0].agent.params(), trs[1].agent.params(), err_msg=f"iteration {it}")
+        n_done += snaps[0]["dones"].sum()
+    if iters * T >= 1000:
+        assert n_done == E  # the 1000-step truncation (and its autoreset) happened inside a rollout
+    for tr in trs:
+        tr.close()
+
+
+def test_persistent_rollout_metric_shape_properties():
+    """The metric configuration (E=4096, T=128): the persistent path fills the storage with finite
+    values, actions inside the action space, log-probs of the Beta policy, and is deterministic."""
+    cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=4096, total_timesteps=4096 * 128 * 4)
+    res = []
+    for _ in range(2):
+        tr = ppo_amd.Trainer(cfg)
+        tr.rollout()
+        tr.agent.sync()
+        res.append(snapshot(tr))
+        tr.close()
+    for k in res[0]:
+        np.testing.assert_array_equal(res[0][k], res[1][k], err_msg=k)
+    s = res[0]
+    assert np.isfinite(s["values"]).all() and np.isfinite(s["logp"]).all()
+    assert np.abs(s["actions"]).max() <= 1.0

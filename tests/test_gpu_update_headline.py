@@ -9,9 +9,16 @@ oracle's gradient over the same gathered rows (oracle/ppo_oracle.c orc_minibatch
 chunks on a thread pool, partials added in a fixed order) and with the oracle's clip_grad_norm_ +
 Adam step applied to the oracle's gradient.
 
-Tolerances: raw gradient rel-L2 < 2e-4 overall and < 2e-3 per tensor, loss statistics rtol 2e-4,
-parameters after the Adam step atol 2e-6 (the same bars as the M = 256 golden cases; MFMA fp32
-accumulation order vs the oracle's double sums is the only difference).
+Tolerances: raw gradient rel-L2 < 2e-4 overall and < 2e-3 per tensor, loss statistics rtol 2e-4
+(the same bars as the M = 256 golden cases; MFMA fp32 accumulation order vs the oracle's double sums
+is the only difference). Parameters after the Adam step:
+  * against the oracle's clip_grad_norm_ + Adam applied to the GPU's own raw gradient: atol 2e-6
+    (the clip and Adam arithmetic alone);
+  * against the oracle's step of the oracle's gradient: atol 2e-6 + lr |dg| / (|g| + eps) per
+    element. Adam's first step moves every parameter by lr g / (|g| + eps), whose derivative in g is
+    at most 1 / (|g| + eps): an element whose gradient is a near-cancelling sum over 131 072 rows
+    (|g| ~ eps) turns the fp32-vs-double difference of that sum into an lr-sized difference of the
+    step (measured: 30 of 146 225 elements beyond a flat 2e-6, at most 1.3e-5 = 0.05 lr).
 """
 import numpy as np
 import pytest
@@ -68,5 +75,11 @@ def test_headline_minibatch_update_vs_oracle(name, O_, A, E):
     assert 0.05 < ost[5] < 0.95  # both branches of the clipped surrogate are exercised
     gc, tn = O.clip_grad_norm(L, og, mgn)
     np.testing.assert_allclose(st["grad_norm"], tn, rtol=2e-4)
-    op, _, _ = O.adam_step(L, p, gc, np.zeros(L.P, np.float32), np.zeros(L.P, np.float32), 1, lr, eps)
-    np.testing.assert_allclose(p1, op, rtol=0, atol=2e-6)
+    zeros = np.zeros(L.P, np.float32)
+    gg, _ = O.clip_grad_norm(L, g, mgn)
+    pg_, _, _ = O.adam_step(L, p, gg, zeros, zeros, 1, lr, eps)
+    np.testing.assert_allclose(p1, pg_, rtol=0, atol=2e-6)  # clip + Adam of the GPU's gradient
+    op, _, _ = O.adam_step(L, p, gc, zeros, zeros, 1, lr, eps)
+    bound = 2e-6 + lr * np.abs(gg.astype(np.float64) - gc) / (np.abs(gc.astype(np.float64)) + eps)
+    assert (np.abs(p1.astype(np.float64) - op) <= bound).all(), np.abs(p1 - op).max()
+    assert np.mean(np.abs(p1 - op) > 2e-6) < 1e-3  # the sensitive elements are a small minority

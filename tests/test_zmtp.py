@@ -82,6 +82,48 @@ def test_cpp_store_server_python_clients():
         srv.wait()
 
 
+def test_store_server_survives_departed_subscriber_and_oversized_frame():
+    """A subscriber that disconnects (RST) while the server publishes is dropped, not fatal (libzmq's
+    PUB drops a departed subscriber); a client announcing a frame beyond the request socket's maximum
+    message size is disconnected (ZMQ_MAXMSGSIZE); the server keeps serving the others."""
+    import socket
+    port = free_port()
+    srv = subprocess.Popen([TOOL, "store-server", "127.0.0.1", str(port), "20"], stdout=subprocess.PIPE, text=True)
+    try:
+        assert srv.stdout.readline().startswith("Server started")
+        keep = Peer.connect("SUB", f"tcp://127.0.0.1:{port + 1}")
+        keep.subscribe()
+        gone = Peer.connect("SUB", f"tcp://127.0.0.1:{port + 1}")
+        gone.subscribe()
+        time.sleep(0.3)
+        req = Peer.connect("REQ", f"tcp://127.0.0.1:{port}")
+        req.send([b"r"])
+        assert req.recv() == [b" "]
+        assert struct.unpack("<i", keep.recv()[0])[0] == 0
+        # abortive close: the next writes to it fail with EPIPE / ECONNRESET
+        gone.s.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))
+        gone.close()
+        for k in range(1, 6):
+            req.send([b"i"])
+            assert req.recv() == [b" "]
+            assert struct.unpack("<i", keep.recv()[0])[0] == k
+        # a 2**40-byte frame announced to the REP socket: that client is dropped
+        bad = Peer.connect("REQ", f"tcp://127.0.0.1:{port}")
+        bad.s.sendall(bytes([0x02]) + struct.pack(">Q", 1 << 40) + b"x" * 16)
+        time.sleep(0.3)
+        with pytest.raises((ConnectionError, OSError)):
+            bad.s.settimeout(5)
+            bad.send([b"i"])
+            bad.recv()
+        req.send([b"i"])
+        assert req.recv() == [b" "]
+        assert struct.unpack("<i", keep.recv()[0])[0] == 6
+        assert srv.poll() is None  # still running
+    finally:
+        srv.kill()
+        srv.wait()
+
+
 def test_python_store_server_cpp_client():
     """the reference protocol served from Python; the C++ client's increment / reset / get."""
     port = free_port()

@@ -14,7 +14,7 @@ Tolerances: raw gradient rel-L2 < 2e-4 overall and < 2e-3 per tensor, loss stati
 is the only difference). Parameters after the Adam step:
   * against the oracle's clip_grad_norm_ + Adam applied to the GPU's own raw gradient: atol 2e-6
     (the clip and Adam arithmetic alone);
-  * against the oracle's step of the oracle's gradient: atol 2e-6 + lr |dg| / (|g| + eps) per
+  * against the oracle's step of the oracle's gradient: atol 2e-6 + lr |dg| / (min |g| + eps) per
     element. Adam's first step moves every parameter by lr g / (|g| + eps), whose derivative in g is
     at most 1 / (|g| + eps): an element whose gradient is a near-cancelling sum over 131 072 rows
     (|g| ~ eps) turns the fp32-vs-double difference of that sum into an lr-sized difference of the
@@ -80,6 +80,7 @@ def test_headline_minibatch_update_vs_oracle(name, O_, A, E):
     pg_, _, _ = O.adam_step(L, p, gg, zeros, zeros, 1, lr, eps)
     np.testing.assert_allclose(p1, pg_, rtol=0, atol=2e-6)  # clip + Adam of the GPU's gradient
     op, _, _ = O.adam_step(L, p, gc, zeros, zeros, 1, lr, eps)
-    bound = 2e-6 + lr * np.abs(gg.astype(np.float64) - gc) / (np.abs(gc.astype(np.float64)) + eps)
+    g64, c64 = gg.astype(np.float64), gc.astype(np.float64)
+    bound = 2e-6 + lr * np.abs(g64 - c64) / (np.minimum(np.abs(g64), np.abs(c64)) + eps)
     assert (np.abs(p1.astype(np.float64) - op) <= bound).all(), np.abs(p1 - op).max()
     assert np.mean(np.abs(p1 - op) > 2e-6) < 1e-3  # the sensitive elements are a small minority

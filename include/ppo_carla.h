@@ -126,6 +126,9 @@ typedef struct ppo_carla ppo_carla_t;
 
 /* carla_model.h:35-206 (the module) — allocates parameters and activation buffers on `device`. */
 int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_carla_t** out);
+/* options: NULL / "" (defaults), "conv1=staged" (the default: conv1 forward and weight gradient with
+ * the image patch staged in LDS) or "conv1=generic" (the generic implicit-GEMM kernels; A/B tests) */
+int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, const char* options, ppo_carla_t** out);
 int ppo_carla_destroy(ppo_carla_t* c);
 int ppo_carla_get_layout(const ppo_carla_t* c, ppo_carla_layout* out);
 /* host floats in named_parameters() order (torch::load of a model_*.pth, ac_ppo_carla.cpp) */

@@ -79,6 +79,16 @@ int ppo_runtime_check(void);
 int ppo_obs_norm(const char* env_id, const float** mean, const float** std, int* n);
 
 int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
+/* ppo_create with kernel-selection options, "key=value" pairs separated by ',' (NULL or "": the
+ * defaults ppo_create uses). Every choice is a complete, tested kernel path; results differ only in
+ * summation order (A/B comparisons, tests):
+ *   upd_kernel=auto|fwdbwd   minibatch forward/backward: the feature-split k_upd / k_upd2 (auto) or
+ *                            the wave-per-16-rows k_fwdbwd
+ *   act_kernel=auto|2|4      64-wide agent act: by shape (auto), k_act2, or k_act4
+ *   dw_fused=1|0             dW1 / dW2 in one pass (k_dwf) or two (k_dw)
+ *   rollout=auto|per_step    ppo_rollout_synth: persistent launch where supported, or per step
+ * An unknown key or value is an error. */
+int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* options, ppo_t** out);
 int ppo_destroy(ppo_t* ctx);
 int ppo_get_layout(const ppo_t* ctx, ppo_layout* out);
 void* ppo_stream(ppo_t* ctx);

@@ -337,8 +337,12 @@ static int launch_act3_rt(const ActArgs& a, hipStream_t s) {
 // (rollout act): 19.4 us with 16 rows, 20.3 with 32, 32.7 with 64 (profiles/r02/act/act_rt_ab.txt)
 template <int KIND, int NTO, int NHT>
 static int launch_act3_t(const ActArgs& a, hipStream_t s) {
+#ifdef PPO_DIAG
   static const int force = [] { const char* e = getenv("PPO_ACT_RT"); return e ? atoi(e) : 0; }();
   const int rt = force ? force : 1;
+#else
+  const int rt = 1;
+#endif
   if (rt == 4) return launch_act3_rt<KIND, NTO, NHT, 4>(a, s);
   if (rt == 2) return launch_act3_rt<KIND, NTO, NHT, 2>(a, s);
   return launch_act3_rt<KIND, NTO, NHT, 1>(a, s);
@@ -346,8 +350,11 @@ static int launch_act3_t(const ActArgs& a, hipStream_t s) {
 
 // 256-wide agents; returns -1 when the shape is not covered (the caller falls back to k_act2)
 int launch_act3(const ActArgs& a, hipStream_t s) {
+#ifdef PPO_DIAG
   static const bool off = [] { const char* e = getenv("PPO_ACT3"); return e && e[0] == '0'; }();
-  if (off || a.K.H != 256 || a.K.A > 24) return -1;
+  if (off) return -1;
+#endif
+  if (a.K.H != 256 || a.K.A > 24) return -1;
   const int nto = a.K.OP / 16;
   const int nh = a.K.kind == PPO_NET_LN_BETA ? 2 * a.K.A : a.K.A;
   const int nht = (nh + 15) / 16;

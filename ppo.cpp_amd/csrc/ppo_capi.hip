@@ -245,8 +245,44 @@ static int dmalloc(T** p, size_t n) {
   return 0;
 }
 
+// Kernel selection options of ppo_create_ex: "key=value" pairs separated by ',' (include/ppo_hip.h).
+struct CreateOptions {
+  int upd_kernel = 0;   // 0 auto, 1 the wave-per-16-rows k_fwdbwd
+  int act_kernel = 0;   // 0 auto, 2 / 4 force k_act2 / k_act4
+  int dw_fused = 1;
+  int rollout = PPO_ROLLOUT_AUTO;
+};
+static int parse_create_options(const char* opts, CreateOptions* o) {
+  if (!opts) return 0;
+  std::string s(opts);
+  size_t pos = 0;
+  while (pos < s.size()) {
+    size_t end = s.find(',', pos);
+    if (end == std::string::npos) end = s.size();
+    const std::string kv = s.substr(pos, end - pos);
+    pos = end + 1;
+    if (kv.empty()) continue;
+    const size_t eq = kv.find('=');
+    if (eq == std::string::npos) return fail("ppo_create_ex: option without '=': " + kv);
+    const std::string k = kv.substr(0, eq), v = kv.substr(eq + 1);
+    if (k == "upd_kernel" && (v == "auto" || v == "fwdbwd")) o->upd_kernel = v == "fwdbwd";
+    else if (k == "act_kernel" && (v == "auto" || v == "2" || v == "4")) o->act_kernel = v == "auto" ? 0 : v[0] - '0';
+    else if (k == "dw_fused" && (v == "0" || v == "1")) o->dw_fused = v[0] - '0';
+    else if (k == "rollout" && (v == "auto" || v == "per_step"))
+      o->rollout = v == "auto" ? PPO_ROLLOUT_AUTO : PPO_ROLLOUT_PER_STEP;
+    else return fail("ppo_create_ex: unknown option or value: " + kv);
+  }
+  return 0;
+}
+
 extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
+  return ppo_create_ex(cfg, device, nullptr, out);
+}
+
+extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* options, ppo_t** out) {
   if (!cfg || !out) return fail("ppo_create: null argument");
+  CreateOptions opt;
+  if (parse_create_options(options, &opt)) return -1;
   if (int rc = ppo_runtime_check()) return rc;
   ppo_layout L;
   if (ppo_layout_init(&L, cfg->net_kind, cfg->obs_dim, cfg->act_dim, cfg->hidden) != 0)
@@ -282,25 +318,31 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   c->M = (int)(B / cfg->num_minibatches);
   c->rank = cfg->rank;
   c->world = 1;  // statistics and collectives span the communicator attached later (ppo_comm_init*)
-  {  // kernel selection, read once (A/B switches of complete kernels; never read on a launch path)
+  // kernel selection: the options of ppo_create_ex (A/B comparisons of complete, tested kernels);
+  // the diagnostic build (PPO_DIAG) also reads the measurement scripts' environment switches
+  c->act_kernel = opt.act_kernel;
+  c->dw_fused = opt.dw_fused;
+  c->rollout_mode = opt.rollout;
+  int upd_kernel = opt.upd_kernel;
+#ifdef PPO_DIAG
+  {
     const char* es = getenv("PPO_UPD_SCHED");
     if (es && es[0] >= '0' && es[0] <= '3') c->upd_sched = es[0] - '0';
 #ifdef PPO_STAMPS
     if (es) c->upd_sched = atoi(es);  // diagnostic build: bits 4..7 skip stores (ppo_update.hip)
-#endif
-    const char* ea = getenv("PPO_ACT_KERNEL");
-    if (ea && (ea[0] == '2' || ea[0] == '4')) c->act_kernel = ea[0] - '0';
-#ifdef PPO_STAMPS
     const char* eg = getenv("PPO_ACT_DIAG");  // diagnostic build: phases of k_act3 to skip (bits, << 8)
     if (eg) c->act_kernel |= atoi(eg) << 8;
 #endif
+    const char* ea = getenv("PPO_ACT_KERNEL");
+    if (ea && (ea[0] == '2' || ea[0] == '4')) c->act_kernel = ea[0] - '0';
     const char* ed = getenv("PPO_DW_FUSED");
-    c->dw_fused = !(ed && ed[0] == '0');
-#ifdef PPO_DIAG
+    if (ed) c->dw_fused = !(ed[0] == '0');
+    const char* ev = getenv("PPO_UPD_KERNEL");
+    if (ev && ev[0] == '0') upd_kernel = 1;
     const char* et = getenv("PPO_UPD_TRUNK");
     if (et && (et[0] == '0' || et[0] == '1')) c->upd_trunk_mask = 1 << (et[0] - '0');
-#endif
   }
+#endif
   const int H = cfg->hidden, A = cfg->act_dim, O = cfg->obs_dim, OP = c->K.OP;
   c->sg[0] = make_sg(H, 1, A);
   c->sg[1] = make_sg(H, cfg->net_kind == PPO_NET_LN_BETA ? 2 * A : A, A);
@@ -332,15 +374,14 @@ extern "C" int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out) {
   c->tiles_per_block = std::max(1, (tiles + 255) / 256);
   c->nblk = (tiles + c->tiles_per_block - 1) / c->tiles_per_block;
   {
-    const char* ev = getenv("PPO_UPD_KERNEL");  // "0": force the wave-per-16-rows k_fwdbwd
     const int sgmax = std::max(c->sg[0].size, c->sg[1].size);
     // k_upd2 addresses the rollout storage with 32-bit buffer offsets
     const bool fits32 = (double)B * (double)std::max(O, A) * 4.0 < 4294967040.0;
-    if (!(ev && ev[0] == '0') && fits32 && upd2_supported(c->K, &c->upd) == 0) {
+    if (!upd_kernel && fits32 && upd2_supported(c->K, &c->upd) == 0) {
       c->use_upd = c->use_upd2 = true;
       const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
       c->upd_nblk = std::min(ut, 512);  // both trunks per workgroup, 2 workgroups per CU x 256 CUs
-    } else if (!(ev && ev[0] == '0') && upd_supported(c->K, c->sg[1].nh, sgmax, &c->upd) == 0) {
+    } else if (!upd_kernel && upd_supported(c->K, c->sg[1].nh, sgmax, &c->upd) == 0) {
       c->use_upd = true;
       const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
       c->upd_nblk = std::min(ut, 256);  // 2 workgroups per CU x 256 CUs over the two trunks

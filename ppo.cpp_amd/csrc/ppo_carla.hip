@@ -612,7 +612,18 @@ extern "C" int ppo_carla_destroy(ppo_carla_t* c) {
 }
 
 extern "C" int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_carla_t** out) {
+  return ppo_carla_create_ex(cfg, device, nullptr, out);
+}
+
+extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, const char* options, ppo_carla_t** out) {
   if (!cfg || !out) return ppo_fail("ppo_carla_create: null argument", -1);
+  bool conv_img = true;
+  if (options && *options) {
+    const std::string o(options);
+    if (o == "conv1=staged") conv_img = true;
+    else if (o == "conv1=generic") conv_img = false;
+    else return ppo_fail("ppo_carla_create_ex: unknown option " + o, -1);
+  }
   if (int rc = ppo_runtime_check()) return rc;
   ppo_carla_layout L;
   if (ppo_carla_layout_init(&L, cfg->obs_channels, cfg->bev_h, cfg->bev_w, cfg->num_measurements,
@@ -627,10 +638,10 @@ extern "C" int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_car
   c->cfg = *cfg;
   c->L = L;
   c->device = device;
-  {
-    const char* e = getenv("PPO_CARLA_CONV1");
-    c->conv_img = !(e && e[0] == '0');
-  }
+  c->conv_img = conv_img;
+#ifdef PPO_DIAG
+  if (const char* e = getenv("PPO_CARLA_CONV1")) c->conv_img = !(e[0] == '0');
+#endif
   int rc = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess ? 0 : -2;
   const size_t B = (size_t)cfg->max_batch;
   rc |= carla_alloc(&c->P, L.P);

@@ -1584,7 +1584,11 @@ int launch_act(const ActArgs& a, hipStream_t s) {
     constexpr int H = decltype(H_)::value, KIND = decltype(KIND_)::value, NTO = decltype(NTO_)::value;
     if (a.K.A > 20) return -1;
     // 16 rows per workgroup unless that still leaves > 2 workgroups per CU (then 32)
+#ifdef PPO_DIAG
     static const int force_rg = [] { const char* e = getenv("PPO_ACT_RG"); return e ? atoi(e) : 0; }();
+#else
+    constexpr int force_rg = 0;
+#endif
     if (force_rg == 1 || (force_rg == 0 && (a.n + 15) / 16 <= 512)) {
       dim3 grid((a.n + 15) / 16, a.need_actor ? 2 : 1);
       hipLaunchKernelGGL((k_act2<H, KIND, NTO, 1>), grid, dim3(256), 0, s, a);

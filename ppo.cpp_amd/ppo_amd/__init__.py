@@ -129,6 +129,7 @@ SYMBOLS = [
     ("ppo_obs_norm", _I, [C.c_char_p, C.POINTER(C.POINTER(C.c_float)), C.POINTER(C.POINTER(C.c_float)),
                           C.POINTER(_I)]),
     ("ppo_create", _I, [C.POINTER(HipConfig), _I, C.POINTER(_VP)]),
+    ("ppo_create_ex", _I, [C.POINTER(HipConfig), _I, C.c_char_p, C.POINTER(_VP)]),
     ("ppo_destroy", _I, [_VP]),
     ("ppo_get_layout", _I, [_VP, C.POINTER(Layout)]),
     ("ppo_stream", _VP, [_VP]),
@@ -187,6 +188,7 @@ SYMBOLS = [
     ("pwrap_step", _I, [_VP, _I, _I, _FP, _FP, _FP, _FP, _VP]),
     ("pwrap_read_state", _I, [_VP, _FP, _L]),
     ("ppo_carla_create", _I, [C.POINTER(CarlaConfig), _I, C.POINTER(_VP)]),
+    ("ppo_carla_create_ex", _I, [C.POINTER(CarlaConfig), _I, C.c_char_p, C.POINTER(_VP)]),
     ("ppo_carla_destroy", _I, [_VP]),
     ("ppo_carla_get_layout", _I, [_VP, C.POINTER(CarlaLayout)]),
     ("ppo_carla_load_params", _I, [_VP, _FP, _L]),
@@ -466,10 +468,11 @@ def hip_config(cfg: PPOConfig, num_envs_per_device=None, rank=0, world_size=1) -
 class Agent:
     """Owns a ppo_t: the agent parameters, the Adam state and the [T, E, *] rollout storage."""
 
-    def __init__(self, hcfg: HipConfig, device=0):
+    def __init__(self, hcfg: HipConfig, device=0, options: str | None = None):
+        """options: ppo_create_ex kernel selection, e.g. "upd_kernel=fwdbwd,dw_fused=0" (A/B tests)."""
         self.hcfg = hcfg
         h = C.c_void_p()
-        check(lib().ppo_create(C.byref(hcfg), device, C.byref(h)))
+        check(lib().ppo_create_ex(C.byref(hcfg), device, options.encode() if options else None, C.byref(h)))
         self.h = h.value
         self.layout = Layout()
         check(lib().ppo_get_layout(self.h, C.byref(self.layout)))
@@ -621,11 +624,12 @@ class CarlaAgent:
     _MODES = {"sample": PPO_CARLA_SAMPLE, "mean": PPO_CARLA_MEAN, "roach": PPO_CARLA_ROACH}
 
     def __init__(self, max_batch, obs_channels=15, bev=192, num_measurements=8, num_value_measurements=3,
-                 action_dim=2, beta_min=1.0, seed=1, rank=0, device=0):
+                 action_dim=2, beta_min=1.0, seed=1, rank=0, device=0, options: str | None = None):
         self.cfg = CarlaConfig(obs_channels, bev, bev, num_measurements, num_value_measurements, action_dim, beta_min,
                                max_batch, seed, rank)
         self._h = C.c_void_p()
-        check(lib().ppo_carla_create(C.byref(self.cfg), device, C.byref(self._h)))
+        check(lib().ppo_carla_create_ex(C.byref(self.cfg), device, options.encode() if options else None,
+                                        C.byref(self._h)))
         self.layout = CarlaLayout()
         check(lib().ppo_carla_get_layout(self._h, C.byref(self.layout)))
 

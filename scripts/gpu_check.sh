@@ -18,6 +18,4 @@ timeout -k 10 400 python bench.py > $OUT/bench_default.log 2>&1 || { echo "bench
 tail -1 $OUT/bench_default.log
 timeout -k 10 300 python bench.py --steps 5 --warmup 1 --profile-all --no-cpu-baseline > $OUT/bench_all.log 2>&1 || { echo "bench profile-all failed"; tail -30 $OUT/bench_all.log; exit 1; }
 tail -1 $OUT/bench_all.log
-timeout -k 10 300 env PPO_DW_FUSED=0 python bench.py --steps 5 --warmup 1 --profile-all --no-cpu-baseline > $OUT/bench_all_dw2.log 2>&1 || { echo "bench dw2 failed"; tail -30 $OUT/bench_all_dw2.log; exit 1; }
-tail -1 $OUT/bench_all_dw2.log
 echo done

@@ -83,10 +83,10 @@ def test_errors(carla):
         ppo_amd.CarlaAgent(max_batch=4, bev=128)  # roach encoder needs 256 x 2 x 2 at the end
 
 
-def test_staged_conv1_kernels_match_generic(monkeypatch):
+def test_staged_conv1_kernels_match_generic():
     """conv1 runs through k_conv_img2 / k_wgrad_img2 (uint8 patch staged in LDS, ds_read_u8 gathers,
     two output columns per MFMA column for OC = 8) and conv2's input gradient through k_dgrad_s2 (dZ
-    region staged in LDS); with PPO_CARLA_CONV1=0 at create the generic k_conv / k_wgrad / k_dgrad
+    region staged in LDS); with the create option "conv1=generic" the generic k_conv / k_wgrad / k_dgrad
     gather from global memory. Forward: the real taps in k_conv's order, the extra taps with exact
     zero weights (the f32 MFMA accumulates as a sequential fma chain), so every output is bitwise
     equal (n = 7: partial tiles, 94 = 2 x 32 + 30 = 5 x 16 + 14). Update: k_dgrad_s2 keeps k_dgrad's chain (bitwise), so every gradient tensor
@@ -104,9 +104,8 @@ def test_staged_conv1_kernels_match_generic(monkeypatch):
     ret = rng.normal(0.0, 1.0, n).astype(np.float32)
     old_v = rng.normal(0.0, 1.0, n).astype(np.float32)
     outs = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("PPO_CARLA_CONV1", flag)
-        ag = ppo_amd.CarlaAgent(max_batch=16, seed=7)
+    for opt in ("conv1=generic", "conv1=staged"):
+        ag = ppo_amd.CarlaAgent(max_batch=16, seed=7, options=opt)
         ag.load_params(p)
         res = [run(ag, bev, meas, vmeas, mode=m, env_base=3, step_id=5) for m in ("sample", "mean", "roach")]
         res.append(run(ag, bev, meas, vmeas, act))

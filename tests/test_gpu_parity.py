@@ -25,10 +25,10 @@ def rel(a, b):
 
 
 def make_agent(kind, O_, A, H, E, T=1, MB=1, EP=1, clip=0.2, ent=0.01, vf=0.5, max_grad_norm=0.5, adam_eps=1e-5,
-               seed=1, norm_adv=1, clip_vloss=1):
+               seed=1, norm_adv=1, clip_vloss=1, options=None):
     hc = ppo_amd.HipConfig(kind, O_, A, H, E, T, MB, EP, 0.99, 0.95, clip, ent, vf, max_grad_norm, adam_eps,
                            norm_adv, clip_vloss, seed, 0, 1)
-    return ppo_amd.Agent(hc)
+    return ppo_amd.Agent(hc, options=options)
 
 
 def fill_storage(ag, T, E, obs, act, logp, adv, ret, val):
@@ -376,7 +376,7 @@ def test_metric_config_iteration_properties_and_determinism():
 
 @pytest.mark.parametrize("kind,O_,A,H", [(1, 17, 6, 256), (0, 17, 6, 256), (0, 17, 6, 64), (0, 376, 17, 64),
                                          (0, 11, 3, 64)])
-def test_update_kernels_agree(kind, O_, A, H, monkeypatch):
+def test_update_kernels_agree(kind, O_, A, H):
     """The feature-split k_upd (H = 256) / the two-trunk k_upd2 (H = 64) and the wave-per-16-rows
     k_fwdbwd compute the same minibatch gradient (different summation orders only) at a size where
     every workgroup loops several times (M = 12 792 rows, ragged last tile)."""
@@ -396,9 +396,8 @@ def test_update_kernels_agree(kind, O_, A, H, monkeypatch):
     ret = rng.standard_normal(B).astype(np.float32)
     perm = rng.permutation(B).astype(np.int32)
     grads, stats = [], []
-    for env in ("0", "1"):
-        monkeypatch.setenv("PPO_UPD_KERNEL", env)
-        ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.1)
+    for opt in ("upd_kernel=fwdbwd", "upd_kernel=auto"):
+        ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.1, options=opt)
         ag.load_params(p)
         fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
         st = ag.update(2.5e-4, perms=DeviceArray.from_numpy(perm), want_stats=True)
@@ -414,7 +413,7 @@ def test_update_kernels_agree(kind, O_, A, H, monkeypatch):
 
 
 @pytest.mark.parametrize("O_,A,n", [(376, 17, 1000), (17, 6, 777), (11, 3, 5)])
-def test_act_kernels_agree(O_, A, n, monkeypatch):
+def test_act_kernels_agree(O_, A, n):
     """The K-split two-trunk k_act4 and the feature-split k_act2 (64-wide tanh agent) give the same
     forward (summation order only) and, through the shared Philox contract, the same samples."""
     rng = np.random.default_rng(9)
@@ -424,9 +423,8 @@ def test_act_kernels_agree(O_, A, n, monkeypatch):
     x = rng.standard_normal((n, O_)).astype(np.float32)
     given = rng.standard_normal((n, A)).astype(np.float32)
     outs = []
-    for env in ("2", "4"):
-        monkeypatch.setenv("PPO_ACT_KERNEL", env)
-        ag = make_agent(0, O_, A, 64, n)
+    for opt in ("act_kernel=2", "act_kernel=4"):
+        ag = make_agent(0, O_, A, 64, n, options=opt)
         ag.load_params(p)
         xd = DeviceArray.from_numpy(x)
         res = []
@@ -442,7 +440,7 @@ def test_act_kernels_agree(O_, A, n, monkeypatch):
 
 
 @pytest.mark.parametrize("kind,O_,A,H", [(1, 17, 6, 256), (0, 17, 6, 256), (1, 9, 3, 256)])
-def test_fused_dw_matches_two_phase_dw(kind, O_, A, H, monkeypatch):
+def test_fused_dw_matches_two_phase_dw(kind, O_, A, H):
     """k_dwf (dW2 and dW1 in one pass over the rows) and the two-phase k_dw run the same MFMA
     chains over the same rows in the same order: the gradients are bitwise equal (ragged last
     chunk and stage: M = 12 800 - 8 rows)."""
@@ -461,9 +459,8 @@ def test_fused_dw_matches_two_phase_dw(kind, O_, A, H, monkeypatch):
     ret = rng.standard_normal(B).astype(np.float32)
     perm = rng.permutation(B).astype(np.int32)
     grads = []
-    for env in ("0", "1"):
-        monkeypatch.setenv("PPO_DW_FUSED", env)
-        ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.1)
+    for opt in ("dw_fused=0", "dw_fused=1"):
+        ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.1, options=opt)
         ag.load_params(p)
         fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
         ag.update(2.5e-4, perms=DeviceArray.from_numpy(perm), want_stats=True)

@@ -44,10 +44,12 @@ struct ppo_ctx;
 int ppo_rollout_synth(struct ppo_ctx* ctx, psyn_t* env, float* next_obs_dev, float* next_done_dev,
                       float* act_scratch_dev, float* rew_scratch_dev);
 /* How ppo_rollout_synth runs the T steps: PPO_ROLLOUT_AUTO (default) uses one persistent launch
- * (actor weights resident in registers, the env step fused in; then the critic over all stored
- * observations) where the agent shape and env allow it (AC agent, H = 256, no wrapper chain), and
- * per-step launches otherwise; PPO_ROLLOUT_PER_STEP always launches per step. Both produce
- * bitwise identical storage, env state and episode statistics. */
+ * (actor weights resident in registers, the env step and the PPO wrapper chain fused in; then the
+ * critic over all stored observations) for the agent shapes the trainers build (AC agent H = 256
+ * without wrappers, PPO agent H = 64), and per-step launches otherwise; PPO_ROLLOUT_PER_STEP always
+ * launches per step. The persistent kernels run the arithmetic of the per-step act kernels k_act3
+ * (AC) and k_act4 (PPO; the per-step default at O >= 112, option act_kernel=4 otherwise): storage,
+ * env state and episode statistics are then bitwise identical. */
 enum { PPO_ROLLOUT_AUTO = 0, PPO_ROLLOUT_PER_STEP = 1 };
 int ppo_set_rollout_mode(struct ppo_ctx* ctx, int mode);
 

@@ -1201,7 +1201,11 @@ extern "C" int ppo_rollout_synth(ppo_t* c, psyn_t* env, float* next_obs, float* 
   const int E = c->cfg.num_envs;
   if (env->a.E != E || env->a.O != c->K.O || env->a.A != c->K.A) return fail("ppo_rollout_synth: env shape mismatch");
   const float lo = env->act_lo, hi = env->act_hi;
-  if (c->rollout_mode == PPO_ROLLOUT_AUTO && !env->a.w.on && rollout_supported(c->K) == 0) {
+  // the AC kernel has no wrapper chain (the AC trainer's envs carry none, ac:50-53); the PPO kernel
+  // runs k_act4's arithmetic (the per-step path's kernel at O >= 112, or with act_kernel=4)
+  const bool persistent = c->rollout_mode == PPO_ROLLOUT_AUTO && rollout_supported(c->K) == 0 &&
+                          (c->K.kind == PPO_NET_TANH_NORMAL || !env->a.w.on);
+  if (persistent) {
     // one persistent launch for all T steps (k_rollout), then the critic over the stored rows
     RolloutArgs r;
     memset(&r, 0, sizeof(r));

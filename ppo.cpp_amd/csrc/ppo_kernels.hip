@@ -15,6 +15,7 @@
 //   k_synth_*    synthetic HalfCheetah-shaped device env (bench/test env; not the hot path)
 #include "ppo_agent.hpp"
 #include "ppo_kernels.hpp"
+#include "ppo_wrap.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -1317,48 +1318,6 @@ __global__ void k_adv_finalize(AdvArgs a) {
 // same order, as gymcpp/wrappers.h and the oracle (orc_vwrap_*): no contraction, IEEE division and
 // square root, so the chain is bit-exact against both.
 // ---------------------------------------------------------------------------------------------
-// NormalizeObservation::observation for dimension i of env e (stateful_observation.h:64-84: the
-// Welford update with batch_count 1 BEFORE normalising) + TransformObservation clamp +-10 (ppo:44).
-// oc is the env's count_ as read before this step; the caller stores oc + 1 once per env.
-PPO_DEV float wrap_obs_dim(const WrapArgs& w, long e, int O, int i, float oc, float x) {
-#pragma clang fp contract(off)
-  float* om = w.om + e * O + i;
-  float* ov = w.ov + e * O + i;
-  const float batch_count = 1.0f;
-  const float tot_count = oc + batch_count;
-  const float delta = x - *om;
-  const float new_mean = *om + delta * batch_count / tot_count;
-  const float m_a = *ov * oc;
-  const float m_b = 0.0f * batch_count;
-  const float M2 = m_a + m_b + (delta * delta) * oc * batch_count / tot_count;
-  const float new_var = M2 / tot_count;
-  *om = new_mean;
-  *ov = new_var;
-  const float v = (x - new_mean) / sqrtf(new_var + 1e-4f);
-  return v < -10.0f ? -10.0f : (v > 10.0f ? 10.0f : v);
-}
-
-// NormalizeReward::step (stateful_reward.h:55-91; te = termination) + TransformReward clamp +-10
-PPO_DEV float wrap_reward(const WrapArgs& w, long e, float r, float te) {
-#pragma clang fp contract(off)
-  const float racc = w.racc[e] * w.gamma * (1.0f - te) + r;
-  const float rmean = w.rmean[e], rvar = w.rvar[e], rcount = w.rcount[e];
-  const float batch_count = 1.0f;
-  const float delta = racc - rmean;
-  const float tot_count = rcount + batch_count;
-  const float new_mean = rmean + delta * batch_count / tot_count;
-  const float m_a = rvar * rcount;
-  const float m_b = 0.0f * batch_count;
-  const float M2 = m_a + m_b + (delta * delta) * rcount * batch_count / tot_count;
-  const float new_var = M2 / tot_count;
-  w.racc[e] = racc;
-  w.rcount[e] = tot_count;
-  w.rmean[e] = new_mean;
-  w.rvar[e] = new_var;
-  const float rn = r / sqrtf(new_var + 1e-8f);
-  return rn < -10.0f ? -10.0f : (rn > 10.0f ? 10.0f : rn);
-}
-
 // The chain as its own pass over envs [e0, e1) of a vector env's output (pwrap_step / pwrap_reset):
 // one wave per env, lanes over the observation. is_reset[e] != 0 marks the next-step autoreset
 // (gym.h:141-149: the reward, 0, bypasses NormalizeReward); reward == nullptr: observations only.

@@ -15,6 +15,7 @@
 // log-prob, value, reward and observation is bitwise the one the per-step path produces
 // (tests/test_gpu_rollout.py).
 #include "ppo_act_common.hpp"
+#include "ppo_wrap.hpp"
 
 using namespace act;
 
@@ -398,12 +399,387 @@ __global__ __launch_bounds__(512) void k_values(ValuesArgs a) {
 }
 
 // =============================================================================================
+// The PPO agent (two 64-wide tanh trunks, Normal head; ppo:120-157): k_rollout4 / k_values4 run
+// k_act4's arithmetic (ppo_act_narrow.hip: layer 1 split over K across the 4 waves, partial sums met
+// in LDS in a fixed order) with the weights in registers, and the device env with the PPO wrapper
+// chain (ppo:41-49) fused, for all T steps.
+// =============================================================================================
+namespace {
+constexpr int kR4Threads = 256, kR4Rows = 16, kR4H = 64, kR4LDP = kR4Rows + 1, kR4LDH = kR4H + 4;
+
+template <int NTO, int NHT>
+struct Roll4Geo {
+  static constexpr int OP = NTO * 16, NHP = NHT * 16, LDQ = OP + 1;
+};
+
+// this wave's register operands of one trunk, exactly those k_act4 loads at kernel start
+template <int NTO, int NKW>
+PPO_DEV void load4_weights(PBuf wsw, int lane, int ks, f4 (&wa)[NKW][4], f4 (&w2v)[4]) {
+  constexpr int H = kR4H, OP = NTO * 16;
+  const int kb0 = ks * NKW;
+#pragma unroll
+  for (int q = 0; q < NKW; ++q)
+#pragma unroll
+    for (int ft = 0; ft < 4; ++ft) wa[q][ft] = pld4(wsw, 4 * lane, 256 * (ft * NTO + min(kb0 + q, NTO - 1)));
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) w2v[kb] = pld4(wsw, H * OP + 4 * lane, 256 * (4 * ks + kb));
+}
+
+// k_act4's trunk body for the 16 rows whose inputs this lane holds in xv: layer 1 partials (P1),
+// tanh(b1 + sum of the 4 slices) (H1), layer 2 tile ks, tanh; returns h2 (this wave's tile ks)
+template <int NTO, int NKW>
+PPO_DEV f4 trunk4(const f4 (&xv)[NKW], const f4 (&wa)[NKW][4], const f4 (&w2v)[4], f4 b1, f4 b2,
+                  float (*P1)[kR4H][kR4LDP], float (*H1)[kR4LDH], int ks, int j, int g) {
+  const int kb0 = ks * NKW;
+  {
+    f4 acc[4];
+#pragma unroll
+    for (int ft = 0; ft < 4; ++ft) acc[ft] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NKW; ++q) {
+      if (kb0 + q < NTO) {
+#pragma unroll
+        for (int ft = 0; ft < 4; ++ft) {
+          acc[ft] = mfma16(wa[q][ft].x, xv[q].x, acc[ft]);
+          acc[ft] = mfma16(wa[q][ft].y, xv[q].y, acc[ft]);
+          acc[ft] = mfma16(wa[q][ft].z, xv[q].z, acc[ft]);
+          acc[ft] = mfma16(wa[q][ft].w, xv[q].w, acc[ft]);
+        }
+      }
+    }
+#pragma unroll
+    for (int ft = 0; ft < 4; ++ft)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) P1[ks][16 * ft + 4 * g + r][j] = acc[ft][r];
+  }
+  __syncthreads();
+  {
+    f4 h;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * ks + 4 * g + r;
+      const float z = (((P1[0][f][j] + P1[1][f][j]) + P1[2][f][j]) + P1[3][f][j]) + b1[r];
+      h[r] = tanhf(z);
+    }
+    *reinterpret_cast<f4*>(&H1[j][16 * ks + 4 * g]) = h;
+  }
+  __syncthreads();
+  f4 z2 = b2;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    const f4 hb = *reinterpret_cast<const f4*>(&H1[j][16 * kb + 4 * g]);
+    z2 = mfma16(w2v[kb].x, hb.x, z2);
+    z2 = mfma16(w2v[kb].y, hb.y, z2);
+    z2 = mfma16(w2v[kb].z, hb.z, z2);
+    z2 = mfma16(w2v[kb].w, hb.w, z2);
+  }
+  f4 h2;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) h2[r] = tanhf(z2[r]);
+  return h2;
+}
+}  // namespace
+
+template <int NTO, int NHT>
+__global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
+  constexpr int H = kR4H, R = kR4Rows, OP = NTO * 16, NKW = (NTO + 3) / 4, NHP = NHT * 16;
+  constexpr int LDQ = Roll4Geo<NTO, NHT>::LDQ, NCH = (OP + 31) / 32;
+  __shared__ float P1[4][H][kR4LDP];
+  __shared__ __attribute__((aligned(16))) float H1[R][kR4LDH];
+  __shared__ float HP[4][NHP][kR4LDP];
+  __shared__ float ITM[R * NHP][2];
+  __shared__ float XO[R * LDQ];   // the agent's input of the current step (the wrapped obs)
+  __shared__ float Q[R * LDQ];    // env state q
+  __shared__ float ACT[R * 32];
+  __shared__ float EV[EV_NSLOT * R];
+  int* EVI = reinterpret_cast<int*>(EV);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4, ks = wave;
+  const PackedLayout& K = a.K;
+  const TrunkDev& T = K.tr[1];
+  const float* __restrict__ P = a.P;
+  const PBuf pb = make_pbuf(P, K.size);
+  const int row0 = blockIdx.x * R, O = K.O, A = K.A, E = a.E;
+  const int kb0 = ks * NKW;
+  const SynthArgs& sv = a.env;
+  const WrapArgs& w = a.env.w;
+
+  f4 wa[NKW][4], w2v[4], hw[NHT];
+  load4_weights<NTO, NKW>(make_pbuf(a.WSW, (int)sw_size(H, OP)), lane, ks, wa, w2v);
+  const f4 b1 = pld4(pb, T.b1 + 16 * ks + 4 * g, 0);
+  const f4 b2 = pld4(pb, T.b2 + 16 * ks + 4 * g, 0);
+#pragma unroll
+  for (int ht = 0; ht < NHT; ++ht) {
+    const int h = 16 * ht + j;
+    const f4 wv = pld4(pb, K.aW3 + min(h, A - 1) * H + 16 * ks + 4 * g, 0);
+    hw[ht] = h < A ? wv : f4{0.f, 0.f, 0.f, 0.f};
+  }
+  constexpr int NI = (R * NHP + kR4Threads - 1) / kR4Threads;
+  float i_b3[NI], i_lstd[NI];
+#pragma unroll
+  for (int u = 0; u < NI; ++u) {
+    const int idx = min(tid + kR4Threads * u, R * A - 1), ir = idx / A, ia = idx - ir * A;
+    (void)ir;
+    i_b3[u] = P[K.ab3 + ia];
+    i_lstd[u] = P[K.logstd + ia];
+  }
+  for (int idx = tid; idx < R * O; idx += kR4Threads) {
+    const int r = idx / O, f = idx - r * O, e = row0 + r;
+    XO[r * LDQ + f] = e < E ? a.next_obs[(long)e * O + f] : 0.0f;
+    Q[r * LDQ + f] = e < E ? sv.q[(long)e * O + f] : 0.0f;
+  }
+  if (tid < R) {
+    const int e = min(row0 + tid, E - 1);
+    EV[EV_DONE * R + tid] = a.next_done[e];
+    EVI[EV_AR * R + tid] = sv.autoreset[e];
+    EVI[EV_T * R + tid] = sv.t[e];
+    EVI[EV_RSEED * R + tid] = (int)sv.rseed[e];
+    EVI[EV_RCOUNT * R + tid] = (int)sv.rcount[e];
+    EV[EV_EPR * R + tid] = sv.ep_ret[e];
+    EVI[EV_EPL * R + tid] = sv.ep_len[e];
+    EV[EV_FR * R + tid] = sv.fin_ret[e];
+    EV[EV_FL * R + tid] = sv.fin_len[e];
+    EV[EV_FC * R + tid] = sv.fin_cnt[e];
+  }
+  __syncthreads();
+  const SampleKey key = sample_key(a.seed, a.rank);
+  const int row = row0 + j;
+
+  for (int t = 0; t < a.T; ++t) {
+    const long step_id = a.step0 + t;
+    // ---- inputs (k_act4's xv: this wave's k-slice), rollout stores of obs[t] / dones[t] ----
+    f4 xv[NKW];
+#pragma unroll
+    for (int q = 0; q < NKW; ++q) {
+      const int kb = kb0 + q;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int col = 16 * kb + 4 * g + c;
+        const float v = XO[j * LDQ + min(col, O - 1)];
+        xv[q][c] = (kb < NTO && col < O && row < E) ? v : 0.f;
+      }
+    }
+    for (int idx = tid; idx < R * O; idx += kR4Threads) {
+      const int r = idx / O, f = idx - r * O, e = row0 + r;
+      if (e < E) a.s_obs[((long)t * E + e) * O + f] = XO[r * LDQ + f];
+    }
+    if (tid < R && row0 + tid < E) a.s_dones[(long)t * E + row0 + tid] = EV[EV_DONE * R + tid];
+    // the Normal draws of this step (k_act4: computed under the weight fetch)
+    float nz[NI];
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int idx = min(tid + kR4Threads * u, R * A - 1), ir = idx / A, ia = idx - ir * A;
+      uint32_t rr[4];
+      philox_draw(key, (long)(row0 + ir), step_id, (uint32_t)(ia >> 1), rr);
+      float z0, z1;
+      box_muller(rr[0], rr[1], z0, z1);
+      nz[u] = (ia & 1) ? z1 : z0;
+    }
+    const f4 h2 = trunk4<NTO, NKW>(xv, wa, w2v, b1, b2, P1, H1, ks, j, g);
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht) {
+      f4 hp = f4{0.f, 0.f, 0.f, 0.f};
+      hp = mfma16(hw[ht].x, h2.x, hp);
+      hp = mfma16(hw[ht].y, h2.y, hp);
+      hp = mfma16(hw[ht].z, h2.z, hp);
+      hp = mfma16(hw[ht].w, h2.w, hp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) HP[ks][16 * ht + 4 * g + r][j] = hp[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int idx = tid + kR4Threads * u;
+      if (idx < R * A) {
+        const int ir = idx / A, ia = idx - ir * A, irow = row0 + ir;
+        const float mu = (((HP[0][ia][ir] + HP[1][ia][ir]) + HP[2][ia][ir]) + HP[3][ia][ir]) + i_b3[u];
+        const float sd = expf(i_lstd[u]);
+        const float var = sd * sd, lsd = logf(sd);
+        const float act = mu + nz[u] * sd;
+        const float d = act - mu;
+        ITM[idx][0] = -(d * d) / (2.0f * var) - lsd - kLz;
+        ACT[ir * 32 + ia] = act;
+        if (irow < E) a.s_actions[((long)t * E + irow) * A + ia] = act;
+      }
+    }
+    __syncthreads();
+    if (tid < R && row0 + tid < E) {
+      float lp = 0.f;
+      for (int ai = 0; ai < A; ++ai) lp += ITM[tid * A + ai][0];
+      a.s_logp[(long)t * E + row0 + tid] = lp;
+    }
+    // ---- env step (k_synth_step / _wide arithmetic, wrapper chain fused): 32 lanes per env ----
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma clang fp contract(off)
+      const int r = (tid >> 5) + 8 * half, i0 = tid & 31, e = row0 + r;
+      if (e >= E) continue;
+      const bool reset = EVI[EV_AR * R + r] != 0;
+      float* q = Q + r * LDQ;
+      float* xo = XO + r * LDQ;
+      const float* ar = ACT + r * 32;
+      const float oc = w.on ? w.ocount[e] : 0.0f;
+      if (reset) {
+        const uint32_t rs = (uint32_t)EVI[EV_RSEED * R + r], rc = (uint32_t)EVI[EV_RCOUNT * R + r];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int i = 32 * c + i0;
+          if (i < O) {
+            uint32_t rr[4];
+            philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, rr);
+            const float v = (0.1f * ((2.0f * u01(rr[0])) - 1.0f));
+            q[i] = v;
+            xo[i] = w.on ? wrap_obs_dim(w, e, O, i, oc, v) : v;
+          }
+        }
+        if (i0 == 0) {
+          if (w.on) w.ocount[e] = oc + 1.0f;
+          EVI[EV_RCOUNT * R + r] = (int)(rc + 1);
+          EVI[EV_T * R + r] = 0;
+          EV[EV_EPR * R + r] = 0.0f;
+          EVI[EV_EPL * R + r] = 0;
+          EV[EV_DONE * R + r] = 0.0f;
+          EVI[EV_AR * R + r] = 0;
+          a.s_rewards[(long)t * E + e] = 0.0f;
+        }
+      } else {
+        float qo[NCH], qn[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int i = 32 * c + i0;
+          qo[c] = i < O ? q[i] : 0.0f;
+          qn[c] = i < O ? q[i + 1 < O ? i + 1 : 0] : 0.0f;
+        }
+        float q0_new = 0.0f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int i = 32 * c + i0;
+          if (i < O) {
+            const float ai = fminf(fmaxf(ar[i % A], a.lo), a.hi);
+            const float nq = __fmaf_rn(0.9f, qo[c], __fmaf_rn(0.1f, ai, (0.05f * qn[c])));
+            q[i] = nq;
+            xo[i] = w.on ? wrap_obs_dim(w, e, O, i, oc, nq) : nq;
+            if (c == 0) q0_new = nq;
+          }
+        }
+        if (i0 == 0) {
+          if (w.on) w.ocount[e] = oc + 1.0f;
+          const float vel = ((q0_new - qo[0]) / 0.05f);
+          float ctrl = 0.0f;
+          for (int k = 0; k < A; ++k) {
+            const float ak = fminf(fmaxf(ar[k], a.lo), a.hi);
+            ctrl = (ctrl + ((0.1f * ak) * ak));
+          }
+          const float rw = (vel - ctrl);
+          const int tt = EVI[EV_T * R + r] + 1;
+          EVI[EV_T * R + r] = tt;
+          const bool tr = tt >= 1000;
+          a.s_rewards[(long)t * E + e] = w.on ? wrap_reward(w, e, rw, 0.0f) : rw;
+          EV[EV_DONE * R + r] = tr ? 1.0f : 0.0f;
+          const float epr = (EV[EV_EPR * R + r] + rw);
+          EV[EV_EPR * R + r] = epr;
+          const int epl = EVI[EV_EPL * R + r] + 1;
+          EVI[EV_EPL * R + r] = epl;
+          if (tr) {
+            EV[EV_FR * R + r] += epr;
+            EV[EV_FL * R + r] += (float)epl;
+            EV[EV_FC * R + r] += 1.0f;
+          }
+          EVI[EV_AR * R + r] = tr ? 1 : 0;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int idx = tid; idx < R * O; idx += kR4Threads) {
+    const int r = idx / O, f = idx - r * O, e = row0 + r;
+    if (e < E) {
+      a.next_obs[(long)e * O + f] = XO[r * LDQ + f];
+      sv.q[(long)e * O + f] = Q[r * LDQ + f];
+    }
+  }
+  if (tid < R && row0 + tid < E) {
+    const int e = row0 + tid;
+    a.next_done[e] = EV[EV_DONE * R + tid];
+    sv.autoreset[e] = EVI[EV_AR * R + tid];
+    sv.t[e] = EVI[EV_T * R + tid];
+    sv.rseed[e] = (uint32_t)EVI[EV_RSEED * R + tid];
+    sv.rcount[e] = (uint32_t)EVI[EV_RCOUNT * R + tid];
+    sv.ep_ret[e] = EV[EV_EPR * R + tid];
+    sv.ep_len[e] = EVI[EV_EPL * R + tid];
+    sv.fin_ret[e] = EV[EV_FR * R + tid];
+    sv.fin_len[e] = EV[EV_FL * R + tid];
+    sv.fin_cnt[e] = EV[EV_FC * R + tid];
+  }
+}
+
+// the PPO critic over n stored rows (k_act4's critic workgroups: the same chain and partial order)
+template <int NTO>
+__global__ __launch_bounds__(256) void k_values4(ValuesArgs a) {
+  constexpr int H = kR4H, R = kR4Rows, OP = NTO * 16, NKW = (NTO + 3) / 4;
+  __shared__ float P1[4][H][kR4LDP];
+  __shared__ __attribute__((aligned(16))) float H1[R][kR4LDH];
+  __shared__ float VP[4][R];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4, ks = wave;
+  const PackedLayout& K = a.K;
+  const TrunkDev& T = K.tr[0];
+  const float* __restrict__ P = a.P;
+  const PBuf pb = make_pbuf(P, K.size);
+  const int O = K.O, kb0 = ks * NKW;
+  f4 wa[NKW][4], w2v[4];
+  load4_weights<NTO, NKW>(make_pbuf(a.WSW, (int)sw_size(H, OP)), lane, ks, wa, w2v);
+  const f4 b1 = pld4(pb, T.b1 + 16 * ks + 4 * g, 0);
+  const f4 b2 = pld4(pb, T.b2 + 16 * ks + 4 * g, 0);
+  const f4 hv = pld4(pb, K.cW3 + 16 * ks + 4 * g, 0);
+  const float c_b3 = P[K.cb3];
+  const long nblk = (a.n + R - 1) / R;
+  for (long b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const long row0 = b * R, row = row0 + j, rowc = row < a.n ? row : a.n - 1;
+    f4 xv[NKW];
+#pragma unroll
+    for (int q = 0; q < NKW; ++q) {
+      const int kb = kb0 + q;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int col = 16 * kb + 4 * g + c;
+        const float v = a.obs[rowc * O + min(col, O - 1)];
+        xv[q][c] = (kb < NTO && col < O && row < a.n) ? v : 0.f;
+      }
+    }
+    __syncthreads();  // the previous block's VP / P1 / H1 readers are done
+    const f4 h2 = trunk4<NTO, NKW>(xv, wa, w2v, b1, b2, P1, H1, ks, j, g);
+    float p = (hv.x * h2.x + hv.y * h2.y) + (hv.z * h2.z + hv.w * h2.w);
+    p = row_allreduce(p);
+    if (g == 0) VP[ks][j] = p;
+    __syncthreads();
+    if (tid < R && row0 + tid < a.n) a.values[row0 + tid] = (((VP[0][tid] + VP[1][tid]) + VP[2][tid]) + VP[3][tid]) + c_b3;
+  }
+}
+
+// =============================================================================================
 // launchers
 // =============================================================================================
 int rollout_supported(const PackedLayout& K) {
-  if (K.kind != PPO_NET_LN_BETA || K.H != 256 || 2 * K.A > 16) return -1;
   const int nto = K.OP / 16;
-  return (nto == 1 || nto == 2 || nto == 7) ? 0 : -1;
+  if (K.kind == PPO_NET_LN_BETA && K.H == 256 && 2 * K.A <= 16) return (nto == 1 || nto == 2 || nto == 7) ? 0 : -1;
+  if (K.kind == PPO_NET_TANH_NORMAL && K.H == 64 && K.A <= 32)
+    return (nto == 1 || nto == 2 || nto == 7 || nto == 24) ? 0 : -1;
+  return -1;
+}
+
+template <int NTO, int NHT>
+static int launch_rollout4_t(const RolloutArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((k_rollout4<NTO, NHT>), dim3((a.E + kR4Rows - 1) / kR4Rows), dim3(kR4Threads), 0, s, a);
+  return 0;
+}
+template <int NTO>
+static int launch_values4_t(const ValuesArgs& a, hipStream_t s) {
+  const long nblk = (a.n + kR4Rows - 1) / kR4Rows;
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const long grid = nblk < 2L * ncu ? nblk : 2L * ncu;
+  hipLaunchKernelGGL((k_values4<NTO>), dim3((unsigned)grid), dim3(kR4Threads), 0, s, a);
+  return 0;
 }
 
 template <int NTO, int NHT>
@@ -418,7 +794,18 @@ static int launch_rollout_t(const RolloutArgs& a, hipStream_t s) {
 }
 
 int launch_rollout(const RolloutArgs& a, hipStream_t s) {
-  if (rollout_supported(a.K) != 0 || a.env.w.on) return -1;
+  if (rollout_supported(a.K) != 0) return -1;
+  if (a.K.kind == PPO_NET_TANH_NORMAL) {
+    const int nht = (a.K.A + 15) / 16;
+    switch (a.K.OP / 16) {
+      case 1: return nht == 1 ? launch_rollout4_t<1, 1>(a, s) : launch_rollout4_t<1, 2>(a, s);
+      case 2: return nht == 1 ? launch_rollout4_t<2, 1>(a, s) : launch_rollout4_t<2, 2>(a, s);
+      case 7: return nht == 1 ? launch_rollout4_t<7, 1>(a, s) : launch_rollout4_t<7, 2>(a, s);
+      case 24: return nht == 1 ? launch_rollout4_t<24, 1>(a, s) : launch_rollout4_t<24, 2>(a, s);
+    }
+    return -1;
+  }
+  if (a.env.w.on) return -1;
   switch (a.K.OP / 16) {
     case 1: return launch_rollout_t<1, 1>(a, s);
     case 2: return launch_rollout_t<2, 1>(a, s);
@@ -445,6 +832,15 @@ static int launch_values_t(const ValuesArgs& a, hipStream_t s) {
 
 int launch_values(const ValuesArgs& a, hipStream_t s) {
   if (rollout_supported(a.K) != 0) return -1;
+  if (a.K.kind == PPO_NET_TANH_NORMAL) {
+    switch (a.K.OP / 16) {
+      case 1: return launch_values4_t<1>(a, s);
+      case 2: return launch_values4_t<2>(a, s);
+      case 7: return launch_values4_t<7>(a, s);
+      case 24: return launch_values4_t<24>(a, s);
+    }
+    return -1;
+  }
   switch (a.K.OP / 16) {
     case 1: return launch_values_t<1, 1>(a, s);
     case 2: return launch_values_t<2, 1>(a, s);

@@ -788,13 +788,13 @@ class Trainer:
     lr anneal -> rollout (T x act + env step) -> GAE -> update. One call = one iteration."""
 
     def __init__(self, cfg: PPOConfig, num_envs_per_device=None, rank=0, world_size=1, device=0, params=None,
-                 wrappers=None):
+                 wrappers=None, options=None):
         """wrappers: the PPO env wrapper chain (ppo:41-49) on the device env; default = what the
         reference trainer uses: on for the PPO agent (ppo_continuous_action), off for the AC agent
         (ac_ppo_continuous_action wraps its envs in RecordEpisodeStatistics only, ac:50-53)."""
         self.cfg = cfg
         self.hcfg = hip_config(cfg, num_envs_per_device, rank, world_size)
-        self.agent = Agent(self.hcfg, device)
+        self.agent = Agent(self.hcfg, device, options=options)
         if params is None:
             params = init_params(self.agent.layout, seed=cfg.seed, env_id=cfg.env_id)
         self.agent.load_params(params)

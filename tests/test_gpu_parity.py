@@ -513,7 +513,9 @@ def test_cfg1_shape_iteration_vs_oracle():
     np.testing.assert_allclose(tr.agent.buffer(ppo_amd.BUF_REWARDS, (T, E)).numpy(), br, rtol=1e-3, atol=1e-4)
     _, _, _, nv = O.get_action_and_value(L, p, nobs, 2)
     adv, ret = O.gae(br, bv, bd, nv, ndone, 0.99, 0.95)
-    np.testing.assert_allclose(gpu_obs, bo, rtol=1e-4, atol=1e-5)
+    # the obs are normalised by the wrapper chain: 1 / sqrt(var) scales the ulp-level action / dynamics
+    # differences of 2 048 steps up by ~10 where the running variance is small
+    np.testing.assert_allclose(gpu_obs, bo, rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(gpu_adv, adv, rtol=1e-3, atol=1e-3)
     lcfg = O.LossCfg(0.2, 0.0, 0.5, 1, 1)
     lr = float(np.float32(cfg.learning_rate))

@@ -30,13 +30,17 @@ def snapshot(tr):
     return out
 
 
-@pytest.mark.parametrize("env_id,E,iters", [("HalfCheetah-v5", 200, 9), ("Hopper-v5", 37, 9), ("Ant-v5", 96, 3)])
-def test_persistent_rollout_bitwise_equals_per_step(env_id, E, iters):
+@pytest.mark.parametrize("agent,env_id,E,iters", [("ac", "HalfCheetah-v5", 200, 9), ("ac", "Hopper-v5", 37, 9),
+                                                  ("ac", "Ant-v5", 96, 3), ("ppo", "HalfCheetah-v5", 37, 9),
+                                                  ("ppo", "Hopper-v5", 20, 2), ("ppo", "Humanoid-v4", 40, 2)])
+def test_persistent_rollout_bitwise_equals_per_step(agent, env_id, E, iters):
+    """AC agent: k_rollout + k_values vs k_act3 + k_synth_step. PPO agent: k_rollout4 + k_values4 vs
+    k_act4 (act_kernel=4) + k_synth_step(_wide), with the PPO wrapper chain (ppo:41-49) fused into
+    both (Humanoid: O = 376, A = 17, two head tiles, actions clipped to [-0.4, 0.4])."""
     T = 128
-    cfg = ppo_amd.ACPPOConfig(env_id=env_id, num_envs=E, num_steps=T, num_minibatches=4, update_epochs=2,
-                              total_timesteps=E * T * iters)
-    trs = [ppo_amd.Trainer(cfg), ppo_amd.Trainer(cfg)]
-    trs[1].agent.set_rollout_mode(per_step=True)
+    C = ppo_amd.ACPPOConfig if agent == "ac" else ppo_amd.PPOConfig
+    cfg = C(env_id=env_id, num_envs=E, num_steps=T, num_minibatches=4, update_epochs=2, total_timesteps=E * T * iters)
+    trs = [ppo_amd.Trainer(cfg), ppo_amd.Trainer(cfg, options="act_kernel=4,rollout=per_step")]
     n_done = 0.0
     for it in range(iters):
         snaps, stats = [], []
@@ -55,6 +59,9 @@ def test_persistent_rollout_bitwise_equals_per_step(env_id, E, iters):
         n_done += snaps[0]["dones"].sum()
     if iters * T >= 1000:
         assert n_done == E  # the 1000-step truncation (and its autoreset) happened inside a rollout
+    if agent == "ppo":
+        for k, v in trs[0].wrappers.state().items():
+            np.testing.assert_array_equal(v, trs[1].wrappers.state()[k], err_msg=k)
     for tr in trs:
         tr.close()
 

@@ -615,8 +615,21 @@ extern "C" int ppo_compute_gae(ppo_t* c, const float* next_obs, const float* nex
   if (!c || !next_obs || !next_done) return fail("ppo_compute_gae: null argument");
   if (nsteps <= 0 || nsteps > c->cfg.num_steps) return fail("ppo_compute_gae: bad step count");
   hipStream_t s = S(c, stream);
-  int rc = ppo_get_value(c, c->cfg.num_envs, next_obs, c->next_value, s);
-  if (rc) return rc;
+  if (rollout_supported(c->K) == 0) {
+    // the bootstrap value with the critic pass that fills values[t] on the persistent path
+    ValuesArgs v;
+    v.P = c->P;
+    v.K = c->K;
+    v.WSW = c->WSW[0];
+    v.obs = next_obs;
+    v.values = c->next_value;
+    v.n = c->cfg.num_envs;
+    ProfScope ps(c, PK_VALUES, s);
+    if (launch_values(v, s) != 0) return fail("ppo_compute_gae: values kernel launch failed");
+  } else {
+    int rc = ppo_get_value(c, c->cfg.num_envs, next_obs, c->next_value, s);
+    if (rc) return rc;
+  }
   return gae_launch(c, c->next_value, next_done, nsteps, s);
 }
 

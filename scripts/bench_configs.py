@@ -3,7 +3,9 @@
 device-resident synthetic env of each config's shape (random-init agent):
   cfg2  ppo_continuous_action Humanoid-v4 (O=376, A=17), 2x64 tanh MLP, E=1024, T=2048, 32 x 10 updates
   cfg4  ac_ppo_continuous_action Ant-v5 (O=105, A=8), E=8192 over 8 GPUs -> the E=1024 shard of one GPU
-        (no collectives here), T=128, 4 x 4 updates
+        (no collectives here), T=128, 4 x 4 updates of 32 768 rows
+  cfg1  ppo_continuous_action HalfCheetah-v5 defaults (E=1, T=2048, 32 x 10 updates of 64 rows) on the GPU
+        path (the reference runs it on the CPU; its arithmetic is timed as bench.py's cpu_baseline cfg1)
 Prints one JSON line per config: ms per iteration, env steps/s on this GPU and the HIP-event time
 of every kernel class per iteration (the events themselves add a few us per launch)."""
 import argparse
@@ -46,16 +48,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--only", default="", help="cfg2 or cfg4_shard")
+    ap.add_argument("--only", default="", help="cfg2, cfg4_shard or cfg1")
     args = ap.parse_args()
     ppo_amd.set_device(0)
     n = args.iters + args.warmup + 2
-    if args.only != "cfg4_shard":
+    if args.only in ("", "cfg2"):
         run("cfg2", ppo_amd.PPOConfig(env_id="Humanoid-v4", num_envs=1024, num_steps=2048,
                                       total_timesteps=1024 * 2048 * n), args.iters, args.warmup)
-    if args.only != "cfg2":
+    if args.only in ("", "cfg4_shard"):
         run("cfg4_shard", ppo_amd.ACPPOConfig(env_id="Ant-v5", num_envs=1024, num_steps=128,
                                               total_timesteps=1024 * 128 * n), args.iters, args.warmup)
+    if args.only in ("", "cfg1"):
+        run("cfg1", ppo_amd.PPOConfig(env_id="HalfCheetah-v5", num_envs=1, num_steps=2048,
+                                      total_timesteps=2048 * n), args.iters, args.warmup)
 
 
 if __name__ == "__main__":

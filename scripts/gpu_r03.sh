@@ -21,5 +21,7 @@ if [ -n "$BENCH" ]; then
   tail -1 $OUT/bench_all.log | cut -c1-600
   timeout -k 10 300 python bench.py --num-envs 512 --steps 20 --warmup 3 --profile-all --no-cpu-baseline --no-cli > $OUT/bench_e512.log 2>&1 || { echo "bench e512 failed"; tail -30 $OUT/bench_e512.log; exit 1; }
   tail -1 $OUT/bench_e512.log | cut -c1-600
+  timeout -k 10 300 python scripts/bench_configs.py > $OUT/configs.jsonl 2>&1 || { echo "configs failed"; tail -20 $OUT/configs.jsonl; exit 1; }
+  cut -c1-300 $OUT/configs.jsonl
 fi
 echo done

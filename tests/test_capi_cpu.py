@@ -129,3 +129,31 @@ print(json.dumps(out))
     for (field, value, message), (rc, has_ctx, err) in zip(BAD_CONFIGS, got):
         assert rc != 0 and not has_ctx, (field, value)
         assert message in err, (field, value, err)
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libppo_hip.so not built")
+def test_create_ex_rejects_unknown_options():
+    """ppo_create_ex parses its kernel-selection options before touching the GPU: an unknown key or
+    value is refused with a message and no context."""
+    import json
+    import subprocess
+    import sys
+    script = r'''
+import ctypes, json, sys
+sys.path.insert(0, sys.argv[1])
+import ppo_amd
+lib = ppo_amd.lib()
+out = []
+for opt in ("upd_kernel=fast", "act_kernel=3", "bogus=1", "dw_fused", "rollout=sometimes"):
+    cfg = ppo_amd.HipConfig(net_kind=1, obs_dim=17, act_dim=6, hidden=256, num_envs=64, num_steps=8,
+                            num_minibatches=1, update_epochs=1)
+    ctx = ctypes.c_void_p()
+    rc = lib.ppo_create_ex(ctypes.byref(cfg), 0, opt.encode(), ctypes.byref(ctx))
+    out.append([rc, bool(ctx.value), lib.ppo_last_error().decode()])
+print(json.dumps(out))
+'''
+    res = subprocess.run([sys.executable, "-c", script, os.path.join(ROOT, "ppo.cpp_amd")], capture_output=True,
+                         text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-2000:]
+    for rc, has_ctx, err in json.loads(res.stdout.strip().splitlines()[-1]):
+        assert rc != 0 and not has_ctx and "ppo_create_ex" in err, err

@@ -40,7 +40,7 @@ def test_persistent_rollout_bitwise_equals_per_step(agent, env_id, E, iters):
     T = 128
     C = ppo_amd.ACPPOConfig if agent == "ac" else ppo_amd.PPOConfig
     cfg = C(env_id=env_id, num_envs=E, num_steps=T, num_minibatches=4, update_epochs=2, total_timesteps=E * T * iters)
-    trs = [ppo_amd.Trainer(cfg), ppo_amd.Trainer(cfg, options="act_kernel=4,rollout=per_step")]
+    trs = [ppo_amd.Trainer(cfg, options="act_kernel=4"), ppo_amd.Trainer(cfg, options="act_kernel=4,rollout=per_step")]
     n_done = 0.0
     for it in range(iters):
         snaps, stats = [], []

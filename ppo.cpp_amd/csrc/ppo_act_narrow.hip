@@ -229,12 +229,14 @@ __global__ __launch_bounds__(256) void k_act4(ActArgs a) {
   }
 }
 
-// H = 64 tanh-Normal agent with a wide input (OP >= 112: measured on MI355X, scripts/act_micro.py,
-// O = 376: 21.7 vs 21.8 us at E = 1024 and 22.7 vs 35.6 us at E = 4096 against k_act2; at O = 17
-// k_act2's feature split is faster, 6.3 vs 8.0 us). Returns -1 when not covered (caller: k_act2).
+// H = 64 tanh-Normal agent (measured on MI355X, scripts/act_micro.py, O = 376: 21.7 vs 21.8 us at
+// E = 1024 and 22.7 vs 35.6 us at E = 4096 against k_act2; at O = 17 k_act2's feature split is
+// faster per launch, 6.3 vs 8.0 us, but k_act4 is the arithmetic of the persistent device-env
+// rollout (k_rollout4) and of the critic pass, so every shape uses it: one summation order for the
+// rollout, the values and the GAE bootstrap whichever env backend runs). Option act_kernel=2
+// selects k_act2. Returns -1 when not covered (caller: k_act2).
 int launch_act4(const ActArgs& a, hipStream_t s) {
   if (a.K.H != 64 || a.K.kind != PPO_NET_TANH_NORMAL || a.K.A > 32 || a.n <= 0) return -1;
-  if (a.K.OP < 112 && (a.kernel & 0xFF) != 4) return -1;  // kernel 4: forced (tests)
   const int nto = a.K.OP / 16, nht = (a.K.A + 15) / 16;
   const dim3 grid((a.n + kA4Rows - 1) / kA4Rows, a.need_actor ? 2 : 1);
 #define PPO_ACT4_CASE(NTO_, NHT_)                                                    \

@@ -14,7 +14,8 @@ import sys
 
 CLASSES = [("k_fwdbwd", "fwdbwd"), ("k_upd", "fwdbwd"), ("k_dw", "dw"), ("k_act", "act"), ("k_colsum", "colsum"),
            ("k_gradnorm", "gradnorm"), ("k_adam", "adam"), ("k_gae", "gae"), ("k_perm", "perm"),
-           ("k_adv_", "adv_stats"), ("k_synth_step", "synth_env")]
+           ("k_adv_", "adv_stats"), ("k_synth_step", "synth_env"), ("k_rollout", "rollout"),
+           ("k_values", "values")]
 
 
 def klass(name):

@@ -176,6 +176,7 @@ struct ppo_ctx {
   int upd_trunk_mask = 3, upd_sched = 1;   // k_upd launch options (PPO_UPD_TRUNK: PPO_DIAG builds only)
   int dw_fused = 1;
   int rollout_mode = PPO_ROLLOUT_AUTO;  // ppo_set_rollout_mode
+  float* beta_store = nullptr;          // persistent AC rollout: (alpha, beta, sample) per (t, env, action)
   // profiling
   unsigned prof_mask = 0;
   std::mutex prof_mu;
@@ -420,7 +421,7 @@ extern "C" int ppo_destroy(ppo_t* c) {
   prof_drain(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   float* ptrs[] = {c->P, c->G, c->Am, c->Av, c->W2T[0], c->W2T[1], c->WSW[0], c->WSW[1], c->next_value, c->advstats, c->advsq, c->Xn,
-                   c->normout, c->gnpart, c->mbstats};
+                   c->normout, c->gnpart, c->mbstats, c->beta_store};
   for (float* p : ptrs)
     if (p) (void)hipFree(p);
   for (int b = 0; b < PPO_BUF_COUNT; ++b)
@@ -1240,9 +1241,14 @@ extern "C" int ppo_rollout_synth(ppo_t* c, psyn_t* env, float* next_obs, float* 
     r.env = env->a;
     r.lo = lo;
     r.hi = hi;
+    if (c->K.kind == PPO_NET_LN_BETA) {  // Beta log-probs after the rollout (off the env's path)
+      if (!c->beta_store && dmalloc(&c->beta_store, (size_t)E * c->cfg.num_steps * c->K.A * 3)) return -2;
+      r.s_beta = c->beta_store;
+    }
     {
       ProfScope ps(c, PK_ROLLOUT, c->stream);
       if (launch_rollout(r, c->stream) != 0) return fail("ppo_rollout_synth: rollout kernel launch failed");
+      if (r.s_beta) launch_beta_logp(r.s_beta, c->buf[PPO_BUF_LOGPROBS], (long)E * c->cfg.num_steps, c->K.A, c->stream);
     }
     ValuesArgs v;
     v.P = c->P;

@@ -199,6 +199,7 @@ struct RolloutArgs {
   float* next_obs;      // [E][O] in: the obs of step 0; out: the obs after step T-1
   float* next_done;     // [E]
   float *s_obs, *s_actions, *s_logp, *s_dones, *s_rewards;
+  float* s_beta;        // AC: [T][E][A][3] (alpha, beta, sample) for k_beta_logp; null: log-probs in the loop
   SynthArgs env;
   float lo, hi;         // the env's action space (clip_actions)
 };
@@ -216,6 +217,7 @@ struct ValuesArgs {
 int rollout_supported(const PackedLayout& K);
 int launch_rollout(const RolloutArgs& a, hipStream_t s);
 int launch_values(const ValuesArgs& a, hipStream_t s);
+int launch_beta_logp(const float* s_beta, float* logp, long n, int A, hipStream_t s);
 
 // sets the thread-local ppo_last_error() message and returns code (ppo_capi.hip)
 int ppo_fail(const std::string& msg, int code);

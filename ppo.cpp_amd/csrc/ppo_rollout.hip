@@ -17,6 +17,8 @@
 #include "ppo_act_common.hpp"
 #include "ppo_wrap.hpp"
 
+#include <type_traits>
+
 using namespace act;
 
 namespace {
@@ -42,8 +44,8 @@ struct RollGeo {
   static constexpr int oQ = oXO + kRows * LDQ;                 // env state q
   static constexpr int oNRM = oQ + kRows * LDQ;                // obs mean | std (OP each)
   static constexpr int oACT = oNRM + 2 * OP;                   // actions [16][24]
-  static constexpr int oENV = oACT + kRows * 24;               // per-env scalars, 12 x 16
-  static constexpr int total = oENV + 12 * kRows;
+  static constexpr int oENV = oACT + kRows * 24;               // per-env scalars, 16 x 16
+  static constexpr int total = oENV + 16 * kRows;
   // distribution scratch in the XS / HB region (dead after layer 2), as in k_act3
   static constexpr int oITM = 0;
   static constexpr int oLP = oITM + kRows * 24 * 2 * 4;
@@ -53,7 +55,9 @@ struct RollGeo {
 };
 
 // per-env scalar slots in the oENV region
-enum { EV_DONE = 0, EV_AR, EV_T, EV_RSEED, EV_RCOUNT, EV_EPR, EV_EPL, EV_FR, EV_FL, EV_FC, EV_NSLOT };
+// (the wrapper chain's per-env scalars: obs count, return accumulator, reward mean / var / count)
+enum { EV_DONE = 0, EV_AR, EV_T, EV_RSEED, EV_RCOUNT, EV_EPR, EV_EPL, EV_FR, EV_FL, EV_FC,
+       EV_WOC, EV_WRA, EV_WRM, EV_WRV, EV_WRC, EV_NSLOT };
 
 // staged small parameters of one trunk into LDS (biases, LayerNorm affine, head rows, head biases)
 template <int NHP>
@@ -82,8 +86,9 @@ PPO_DEV void stage_params(const PackedLayout& K, const TrunkDev& T, PBuf pb, int
 // LayerNorm + ReLU, layer 2, LayerNorm + ReLU, heads; leaves the head pre-activations (+ bias) in
 // PRE [16][LDP]. Weights: w1 / w2 register slices of this wave. Same operations, same order as
 // k_act3 (LN_BETA, RT = 1).
-template <int NTO, int NHT>
-PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* lds, int nh, int tid) {
+template <int NTO, int NHT, typename PRE_L2 = int>
+PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* lds, int nh, int tid,
+                        PRE_L2 pre_l2 = 0) {
   using GE = RollGeo<NTO, NHT>;
   constexpr int H = 256, LDX = GE::LDX, LDH = GE::LDH, LDP = GE::LDP, NHP = GE::NHP, R = kRows;
   float* XS = lds + GE::oXS;
@@ -106,6 +111,9 @@ PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* ld
 #pragma unroll
   for (int u = 0; u < 2; ++u) acc[u][0] = *reinterpret_cast<const f4*>(SP + GE::sB2 + 32 * wave + 16 * u + 4 * g);
   const float* hin = HB + j * LDH + 4 * g;
+  // independent VALU work placed in the layer-2 block: the scheduler interleaves it with the MFMAs,
+  // whose issue leaves the SIMD's vector pipe mostly free
+  if constexpr (!std::is_same_v<PRE_L2, int>) pre_l2();
   act_layer_regs<16, 1>(acc, w2, [&](int t, int) { return *reinterpret_cast<const f4*>(hin + 16 * t); });
   act_activate<PPO_NET_LN_BETA, 1>(acc, SP + GE::sG2, SP + GE::sBE2, RED, wave, j, g);
 #pragma unroll
@@ -219,19 +227,32 @@ __global__ __launch_bounds__(512) void k_rollout(RolloutArgs a) {
     }
     if (tid < R && row0 + tid < E) a.s_dones[(long)t * E + row0 + tid] = EV[EV_DONE * R + tid];
     lds_barrier();
-    trunk_rows<NTO, NHT>(w1, w2, lds, 2 * A, tid);
-    // ---- Beta sample + log-prob (k_act3 stage 1 / 2, PPO_SAMPLE) ----
+    // the first Marsaglia-Tsang attempt's draws of this thread's item (idx = tid) do not depend on
+    // the network: computed inside layer 2, under its MFMAs (k_act3 computes them under its weight
+    // fetch; gamma_mt_d0 with them is gamma_mt, bitwise)
+    GammaDraw gd0 = GammaDraw{0.f, 0.f};
+    trunk_rows<NTO, NHT>(w1, w2, lds, 2 * A, tid, [&] {
+      if (tid < R * A * 2) {
+        const int which = tid & 1, ra = tid >> 1, r = ra / A, ai = ra - r * A;
+        gd0 = gamma_draw(key, (long)(row0 + r), step_id, 0x10000u + (uint32_t)(ai * 2 + which) * 64u);
+      }
+    });
+    // ---- Beta sample (k_act3 stage 1 / 2, PPO_SAMPLE); the log-prob terms either here (as k_act3)
+    // or, with a.s_beta, stored for k_beta_logp after the rollout (they are not on the env's path) ----
+    const bool defer = a.s_beta != nullptr;
     for (int idx = tid; idx < R * A * 2; idx += kActThreads) {
       const int which = idx & 1, ra = idx >> 1, r = ra / A, ai = ra - r * A;
       const long env = row0 + r;
       const float c = softplusf_(PRE[r * LDP + ai + which * A]) + 1.0f;
       const uint32_t db = 0x10000u + (uint32_t)(ai * 2 + which) * 64u;
-      const float gs = gamma_mt(c, key, env, step_id, db);
+      const float gs = idx == tid ? gamma_mt_d0(c, gd0, key, env, step_id, db) : gamma_mt(c, key, env, step_id, db);
       float* it = ITM + ((r * A + ai) * 2 + which) * 4;
       it[0] = c;
       it[1] = gs;
-      float tg_unused;
-      lgamma_digamma_trigamma(c, it[2], it[3], tg_unused);
+      if (!defer) {
+        float tg_unused;
+        lgamma_digamma_trigamma(c, it[2], it[3], tg_unused);
+      }
     }
     lds_barrier();
     for (int idx = tid; idx < R * A; idx += kActThreads) {
@@ -240,18 +261,26 @@ __global__ __launch_bounds__(512) void k_rollout(RolloutArgs a) {
       const float* ib = ITM + (idx * 2 + 1) * 4;
       const float al = ia[0], be = ib[0];
       const float s01 = ia[1] / (ia[1] + ib[1]);
-      const float ab = al + be;
-      float lgab, psab, tab_unused;
-      lgamma_digamma_trigamma(ab, lgab, psab, tab_unused);
-      const float lga = ia[2], lgb = ib[2];
-      const float lp = xlogyf_(al - 1.0f, s01) + xlogyf_(be - 1.0f, 1.0f - s01) + (lgab - (lga + lgb));
       const float act = (s01 - 0.0f) / (1.0f - 0.0f) * (hi - lo) + lo;
-      LPE[idx * 2 + 0] = lp;
       ACT[r * 24 + ai] = act;
       if (e < E) a.s_actions[((long)t * E + e) * A + ai] = act;
+      if (defer) {
+        if (e < E) {
+          float* d = a.s_beta + (((long)t * E + e) * A + ai) * 3;
+          d[0] = al;
+          d[1] = be;
+          d[2] = s01;
+        }
+      } else {
+        const float ab = al + be;
+        float lgab, psab, tab_unused;
+        lgamma_digamma_trigamma(ab, lgab, psab, tab_unused);
+        const float lga = ia[2], lgb = ib[2];
+        LPE[idx * 2 + 0] = xlogyf_(al - 1.0f, s01) + xlogyf_(be - 1.0f, 1.0f - s01) + (lgab - (lga + lgb));
+      }
     }
     lds_barrier();
-    if (tid < R && row0 + tid < E) {
+    if (!defer && tid < R && row0 + tid < E) {
       float lp = 0.f;
       for (int ai = 0; ai < A; ++ai) lp += LPE[(tid * A + ai) * 2];
       a.s_logp[(long)t * E + row0 + tid] = lp;
@@ -356,6 +385,33 @@ __global__ __launch_bounds__(512) void k_rollout(RolloutArgs a) {
     sv.fin_len[e] = EV[EV_FL * R + tid];
     sv.fin_cnt[e] = EV[EV_FC * R + tid];
   }
+}
+
+// =============================================================================================
+// k_beta_logp: the rollout's Beta log-probs from the stored (alpha, beta, sample) of every
+// (row, action), after the rollout (k_act3's stage-1 / stage-2 terms and row sum, same order)
+// =============================================================================================
+__global__ __launch_bounds__(256) void k_beta_logp(const float* __restrict__ sb, float* __restrict__ logp, long n,
+                                                   int A) {
+  const long row = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= n) return;
+  float lp = 0.f;
+  for (int ai = 0; ai < A; ++ai) {
+    const float* d = sb + (row * A + ai) * 3;
+    const float al = d[0], be = d[1], s01 = d[2];
+    float lga, lgb, lgab, u0, u1;
+    lgamma_digamma_trigamma(al, lga, u0, u1);
+    lgamma_digamma_trigamma(be, lgb, u0, u1);
+    const float ab = al + be;
+    lgamma_digamma_trigamma(ab, lgab, u0, u1);
+    lp += xlogyf_(al - 1.0f, s01) + xlogyf_(be - 1.0f, 1.0f - s01) + (lgab - (lga + lgb));
+  }
+  logp[row] = lp;
+}
+
+int launch_beta_logp(const float* s_beta, float* logp, long n, int A, hipStream_t s) {
+  hipLaunchKernelGGL(k_beta_logp, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, s_beta, logp, n, A);
+  return 0;
 }
 
 // =============================================================================================
@@ -492,6 +548,8 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
   __shared__ float Q[R * LDQ];    // env state q
   __shared__ float ACT[R * 32];
   __shared__ float EV[EV_NSLOT * R];
+  __shared__ float WOM[R * LDQ];  // the wrapper chain's running obs mean / var of the block's envs
+  __shared__ float WOV[R * LDQ];
   int* EVI = reinterpret_cast<int*>(EV);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4, ks = wave;
   const PackedLayout& K = a.K;
@@ -526,9 +584,20 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
     const int r = idx / O, f = idx - r * O, e = row0 + r;
     XO[r * LDQ + f] = e < E ? a.next_obs[(long)e * O + f] : 0.0f;
     Q[r * LDQ + f] = e < E ? sv.q[(long)e * O + f] : 0.0f;
+    if (w.on) {
+      WOM[r * LDQ + f] = e < E ? w.om[(long)e * O + f] : 0.0f;
+      WOV[r * LDQ + f] = e < E ? w.ov[(long)e * O + f] : 1.0f;
+    }
   }
   if (tid < R) {
     const int e = min(row0 + tid, E - 1);
+    if (w.on) {
+      EV[EV_WOC * R + tid] = w.ocount[e];
+      EV[EV_WRA * R + tid] = w.racc[e];
+      EV[EV_WRM * R + tid] = w.rmean[e];
+      EV[EV_WRV * R + tid] = w.rvar[e];
+      EV[EV_WRC * R + tid] = w.rcount[e];
+    }
     EV[EV_DONE * R + tid] = a.next_done[e];
     EVI[EV_AR * R + tid] = sv.autoreset[e];
     EVI[EV_T * R + tid] = sv.t[e];
@@ -616,8 +685,10 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
       const bool reset = EVI[EV_AR * R + r] != 0;
       float* q = Q + r * LDQ;
       float* xo = XO + r * LDQ;
+      float* om = WOM + r * LDQ;
+      float* ov = WOV + r * LDQ;
       const float* ar = ACT + r * 32;
-      const float oc = w.on ? w.ocount[e] : 0.0f;
+      const float oc = EV[EV_WOC * R + r];  // read by every lane before lane 0 stores oc + 1
       if (reset) {
         const uint32_t rs = (uint32_t)EVI[EV_RSEED * R + r], rc = (uint32_t)EVI[EV_RCOUNT * R + r];
 #pragma unroll
@@ -628,11 +699,11 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
             philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, rr);
             const float v = (0.1f * ((2.0f * u01(rr[0])) - 1.0f));
             q[i] = v;
-            xo[i] = w.on ? wrap_obs_dim(w, e, O, i, oc, v) : v;
+            xo[i] = w.on ? wrap_obs_at(om + i, ov + i, oc, v) : v;
           }
         }
         if (i0 == 0) {
-          if (w.on) w.ocount[e] = oc + 1.0f;
+          if (w.on) EV[EV_WOC * R + r] = oc + 1.0f;
           EVI[EV_RCOUNT * R + r] = (int)(rc + 1);
           EVI[EV_T * R + r] = 0;
           EV[EV_EPR * R + r] = 0.0f;
@@ -657,12 +728,12 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
             const float ai = fminf(fmaxf(ar[i % A], a.lo), a.hi);
             const float nq = __fmaf_rn(0.9f, qo[c], __fmaf_rn(0.1f, ai, (0.05f * qn[c])));
             q[i] = nq;
-            xo[i] = w.on ? wrap_obs_dim(w, e, O, i, oc, nq) : nq;
+            xo[i] = w.on ? wrap_obs_at(om + i, ov + i, oc, nq) : nq;
             if (c == 0) q0_new = nq;
           }
         }
         if (i0 == 0) {
-          if (w.on) w.ocount[e] = oc + 1.0f;
+          if (w.on) EV[EV_WOC * R + r] = oc + 1.0f;
           const float vel = ((q0_new - qo[0]) / 0.05f);
           float ctrl = 0.0f;
           for (int k = 0; k < A; ++k) {
@@ -673,7 +744,10 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
           const int tt = EVI[EV_T * R + r] + 1;
           EVI[EV_T * R + r] = tt;
           const bool tr = tt >= 1000;
-          a.s_rewards[(long)t * E + e] = w.on ? wrap_reward(w, e, rw, 0.0f) : rw;
+          a.s_rewards[(long)t * E + e] =
+              w.on ? wrap_reward_at(EV + EV_WRA * R + r, EV + EV_WRM * R + r, EV + EV_WRV * R + r,
+                                    EV + EV_WRC * R + r, w.gamma, rw, 0.0f)
+                   : rw;
           EV[EV_DONE * R + r] = tr ? 1.0f : 0.0f;
           const float epr = (EV[EV_EPR * R + r] + rw);
           EV[EV_EPR * R + r] = epr;
@@ -695,10 +769,21 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
     if (e < E) {
       a.next_obs[(long)e * O + f] = XO[r * LDQ + f];
       sv.q[(long)e * O + f] = Q[r * LDQ + f];
+      if (w.on) {
+        w.om[(long)e * O + f] = WOM[r * LDQ + f];
+        w.ov[(long)e * O + f] = WOV[r * LDQ + f];
+      }
     }
   }
   if (tid < R && row0 + tid < E) {
     const int e = row0 + tid;
+    if (w.on) {
+      w.ocount[e] = EV[EV_WOC * R + tid];
+      w.racc[e] = EV[EV_WRA * R + tid];
+      w.rmean[e] = EV[EV_WRM * R + tid];
+      w.rvar[e] = EV[EV_WRV * R + tid];
+      w.rcount[e] = EV[EV_WRC * R + tid];
+    }
     a.next_done[e] = EV[EV_DONE * R + tid];
     sv.autoreset[e] = EVI[EV_AR * R + tid];
     sv.t[e] = EVI[EV_T * R + tid];

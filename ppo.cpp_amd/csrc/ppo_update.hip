@@ -53,7 +53,8 @@ __device__ unsigned long long g_upd_stamps[1024 * 4 * PPO_STAMP_TILES * PPO_STAM
       }                                                                                              \
     }                                                                                                \
   } while (0)
-// a.sched bits 4..7 skip the H1 / DZ2 / DZ1 / Xn stores (timing experiments only)
+// a.sched bits 4..7 skip the H1 / DZ2 / DZ1 / Xn stores, bit 12 the column sums (bias / LayerNorm-affine /
+// critic head weight gradients) (timing experiments only: the gradient is then wrong)
 #define PPO_DIAG_SKIP(bit) ((a.sched >> (bit)) & 1)
 #else
 #define PPO_STAMP(k) do {} while (0)
@@ -928,7 +929,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) dh[ft][rt][r] = w[r] * gr[rt];
       }
-      col_sums<FT, RT>([&](int ft, int rt, int r) { return gr[rt] * h2_of(ft, rt)[r]; }, acc + sg.hW, fbase, j, g);
+      if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return gr[rt] * h2_of(ft, rt)[r]; }, acc + sg.hW, fbase, j, g);
     } else {
 #pragma unroll
     for (int ht = 0; ht < NHT; ++ht) {
@@ -992,8 +993,8 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       rows_total2<WF, RT, R>(s1, s2, RED0, RED1, wf, rbase, j, g);
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) { s1[rt] *= (1.0f / H); s2[rt] *= (1.0f / H); }
-      col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r]; }, acc + sg.be2, fbase, j, g);
-      col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r] * x2[ft][rt][r]; }, acc + sg.g2, fbase, j, g);
+      if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r]; }, acc + sg.be2, fbase, j, g);
+      if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r] * x2[ft][rt][r]; }, acc + sg.g2, fbase, j, g);
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
         const f4 gm = lds_f4(SG2 + fbase + 4 * g + 16 * ft);
@@ -1007,7 +1008,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
         for (int rt = 0; rt < RT; ++rt) x2[ft][rt] = dh[ft][rt] * (1.0f - x2[ft][rt] * x2[ft][rt]);
     }
     // x2 = dz2
-    col_sums<FT, RT>([&](int ft, int rt, int r) { return x2[ft][rt][r]; }, acc + sg.b2, fbase, j, g);
+    if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return x2[ft][rt][r]; }, acc + sg.b2, fbase, j, g);
     if (!PPO_DIAG_SKIP(5)) store_tile_rows<FT, RT>(a.DZ2[trunk], H, x2, m0, a.M, rbase, fbase, j, g);
     lds_barrier();  // dW3 readers of h2 are done
     lds_store_tile<FT, RT, LDA>(ACT, x2, rbase, fbase, j, g);
@@ -1046,8 +1047,8 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       rows_total2<WF, RT, R>(s1, s2, RED2, RED3, wf, rbase, j, g);
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) { s1[rt] *= (1.0f / H); s2[rt] *= (1.0f / H); }
-      col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r]; }, acc + sg.be1, fbase, j, g);
-      col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r] * z[ft][rt][r]; }, acc + sg.g1, fbase, j, g);
+      if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r]; }, acc + sg.be1, fbase, j, g);
+      if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r] * z[ft][rt][r]; }, acc + sg.g1, fbase, j, g);
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
         const f4 gm = lds_f4(SG1 + fbase + 4 * g + 16 * ft);
@@ -1066,7 +1067,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
           }
     }
     // z = dz1
-    col_sums<FT, RT>([&](int ft, int rt, int r) { return z[ft][rt][r]; }, acc + sg.b1, fbase, j, g);
+    if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return z[ft][rt][r]; }, acc + sg.b1, fbase, j, g);
     if (!PPO_DIAG_SKIP(6)) store_tile_rows<FT, RT>(a.DZ1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
     PPO_STAMP(12);
   }

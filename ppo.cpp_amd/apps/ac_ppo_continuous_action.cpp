@@ -229,8 +229,12 @@ int main(int argc, const char** argv) {
       std::string key;
       for (const char* v : {"PPO_RUN_ID", "TORCHELASTIC_RUN_ID", "OMPI_MCA_ess_base_jobid", "SLURM_JOB_ID"})
         if (const char* e = getenv(v)) { key = e; break; }
+      // torchrun keeps the run id across elastic restarts: the attempt number makes the key per attempt
+      if (const char* rc = getenv("TORCHELASTIC_RESTART_COUNT")) key += std::string("#") + rc;
       char id[PPO_COMM_ID_BYTES];
       if (rank == 0) {
+        std::error_code rm_ec;
+        fs::remove(path, rm_ec);  // a file a crashed earlier attempt left behind is never read again
         check(ppo_comm_unique_id(id), "ppo_comm_unique_id");
         {
           std::ofstream f(path + ".tmp", std::ios::binary | std::ios::trunc);

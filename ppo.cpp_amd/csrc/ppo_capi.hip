@@ -55,7 +55,9 @@ extern "C" const char* ppo_last_error(void) { return g_err.c_str(); }
 // then maps a second HIP runtime, and the two tear each other down at exit (free(): invalid
 // pointer, exit 134). Every runtime-initialising entry point checks for that and fails with a
 // clear message; the first failed check also installs an exit guard that ends the process with
-// status 70 before either runtime's teardown runs.
+// status 70 before either runtime's teardown runs. The guard is permanent for the process (a host
+// that handles the -4 still exits 70: its teardown would crash otherwise); it flushes every stdio
+// stream first.
 static int hip_runtime_paths(std::vector<std::string>* out) {
   out->clear();
   dl_iterate_phdr(
@@ -75,7 +77,7 @@ static int hip_runtime_paths(std::vector<std::string>* out) {
 static std::string g_runtime_msg;
 static void runtime_exit_guard() {
   fprintf(stderr, "libppo_hip: %s -- exiting (70) before the HIP runtimes' teardown\n", g_runtime_msg.c_str());
-  fflush(stderr);
+  fflush(nullptr);  // every stdio stream (stdout, log files) before _exit skips the C library's flush
   _exit(70);
 }
 

@@ -21,6 +21,25 @@
 
 using namespace act;
 
+#ifdef PPO_STAMPS
+// diagnostic build only: shader-clock stamps at the phase ends of the first 16 steps, wave 0 of
+// workgroup 0 (k_rollout: 8 phases, k_rollout4: 8 phases); read with ppo_diag_read_roll_stamps
+__device__ unsigned long long g_roll_stamps[16 * 8];
+#define ROLL_STAMP(t, k)                                                                      \
+  do {                                                                                        \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (t) < 16)                                      \
+      g_roll_stamps[(t) * 8 + (k)] = __builtin_amdgcn_s_memtime();                           \
+  } while (0)
+extern "C" int ppo_diag_read_roll_stamps(unsigned long long* host, long n) {
+  if (n > 16 * 8) n = 16 * 8;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_roll_stamps), n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -2;
+}
+#else
+#define ROLL_STAMP(t, k) do {} while (0)
+#endif
+
 namespace {
 
 constexpr int kRows = 16;  // envs (rows) per workgroup
@@ -214,9 +233,14 @@ __global__ __launch_bounds__(512) void k_rollout(RolloutArgs a) {
   lds_barrier();
   const SampleKey key = sample_key(a.seed, a.rank);
   const float hi = P[K.hi], lo = P[K.lo];
+  // this thread's Beta item (row, action, alpha | beta): the R * 2A items spread evenly over the
+  // waves (2A <= 16: at most 32 per wave), so fewer lanes per wave wait on a rejected gamma attempt
+  const int bper = (R * A * 2 + kActWaves - 1) / kActWaves;
+  const int bitem = lane < bper ? wave * bper + lane : R * A * 2;
 
   for (int t = 0; t < a.T; ++t) {
     const long step_id = a.step0 + t;
+    ROLL_STAMP(t, 0);
     // ---- inputs: rollout stores of obs[t] / dones[t]; normalised rows into XS (k_act3 order) ----
     for (int idx = tid; idx < R * OP; idx += kActThreads) {
       const int r = idx / OP, f = idx - r * OP, e = row0 + r;
@@ -231,21 +255,24 @@ __global__ __launch_bounds__(512) void k_rollout(RolloutArgs a) {
     // the network: computed inside layer 2, under its MFMAs (k_act3 computes them under its weight
     // fetch; gamma_mt_d0 with them is gamma_mt, bitwise)
     GammaDraw gd0 = GammaDraw{0.f, 0.f};
+    ROLL_STAMP(t, 1);
     trunk_rows<NTO, NHT>(w1, w2, lds, 2 * A, tid, [&] {
-      if (tid < R * A * 2) {
-        const int which = tid & 1, ra = tid >> 1, r = ra / A, ai = ra - r * A;
-        gd0 = gamma_draw(key, (long)(row0 + r), step_id, 0x10000u + (uint32_t)(ai * 2 + which) * 64u);
+      if (bitem < R * A * 2) {
+        const int which = bitem & 1, ra = bitem >> 1, r = ra / A, ai = ra - r * A;
+        const uint32_t db = 0x10000u + (uint32_t)(ai * 2 + which) * 64u;
+        gd0 = gamma_draw(key, (long)(row0 + r), step_id, db);
       }
     });
     // ---- Beta sample (k_act3 stage 1 / 2, PPO_SAMPLE); the log-prob terms either here (as k_act3)
     // or, with a.s_beta, stored for k_beta_logp after the rollout (they are not on the env's path) ----
     const bool defer = a.s_beta != nullptr;
-    for (int idx = tid; idx < R * A * 2; idx += kActThreads) {
-      const int which = idx & 1, ra = idx >> 1, r = ra / A, ai = ra - r * A;
+    ROLL_STAMP(t, 2);
+    if (bitem < R * A * 2) {
+      const int idx = bitem, which = idx & 1, ra = idx >> 1, r = ra / A, ai = ra - r * A;
       const long env = row0 + r;
       const float c = softplusf_(PRE[r * LDP + ai + which * A]) + 1.0f;
       const uint32_t db = 0x10000u + (uint32_t)(ai * 2 + which) * 64u;
-      const float gs = idx == tid ? gamma_mt_d0(c, gd0, key, env, step_id, db) : gamma_mt(c, key, env, step_id, db);
+      const float gs = gamma_mt_d0(c, gd0, key, env, step_id, db);
       float* it = ITM + ((r * A + ai) * 2 + which) * 4;
       it[0] = c;
       it[1] = gs;
@@ -285,6 +312,7 @@ __global__ __launch_bounds__(512) void k_rollout(RolloutArgs a) {
       for (int ai = 0; ai < A; ++ai) lp += LPE[(tid * A + ai) * 2];
       a.s_logp[(long)t * E + row0 + tid] = lp;
     }
+    ROLL_STAMP(t, 3);
     // ---- env step (k_synth_step / k_synth_step_wide arithmetic): 32 lanes per env ----
     {
 #pragma clang fp contract(off)
@@ -363,6 +391,7 @@ __global__ __launch_bounds__(512) void k_rollout(RolloutArgs a) {
       }
     }
     lds_barrier();
+    ROLL_STAMP(t, 4);
   }
   // ---- epilogue: next_obs / next_done and the env state back to HBM ----
   for (int idx = tid; idx < R * O; idx += kActThreads) {
@@ -483,9 +512,9 @@ PPO_DEV void load4_weights(PBuf wsw, int lane, int ks, f4 (&wa)[NKW][4], f4 (&w2
 
 // k_act4's trunk body for the 16 rows whose inputs this lane holds in xv: layer 1 partials (P1),
 // tanh(b1 + sum of the 4 slices) (H1), layer 2 tile ks, tanh; returns h2 (this wave's tile ks)
-template <int NTO, int NKW>
+template <int NTO, int NKW, typename PRE_L1>
 PPO_DEV f4 trunk4(const f4 (&xv)[NKW], const f4 (&wa)[NKW][4], const f4 (&w2v)[4], f4 b1, f4 b2,
-                  float (*P1)[kR4H][kR4LDP], float (*H1)[kR4LDH], int ks, int j, int g) {
+                  float (*P1)[kR4H][kR4LDP], float (*H1)[kR4LDH], int ks, int j, int g, PRE_L1 pre_l1) {
   const int kb0 = ks * NKW;
   {
     f4 acc[4];
@@ -503,6 +532,8 @@ PPO_DEV f4 trunk4(const f4 (&xv)[NKW], const f4 (&wa)[NKW][4], const f4 (&w2v)[4
         }
       }
     }
+    // independent VALU work (the step's Normal draws) issued under the layer-1 MFMAs
+    pre_l1();
 #pragma unroll
     for (int ft = 0; ft < 4; ++ft)
 #pragma unroll
@@ -539,7 +570,7 @@ PPO_DEV f4 trunk4(const f4 (&xv)[NKW], const f4 (&wa)[NKW][4], const f4 (&w2v)[4
 template <int NTO, int NHT>
 __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
   constexpr int H = kR4H, R = kR4Rows, OP = NTO * 16, NKW = (NTO + 3) / 4, NHP = NHT * 16;
-  constexpr int LDQ = Roll4Geo<NTO, NHT>::LDQ, NCH = (OP + 31) / 32;
+  constexpr int LDQ = Roll4Geo<NTO, NHT>::LDQ, NC16 = (OP + 15) / 16, kEnvGroup = 12;
   __shared__ float P1[4][H][kR4LDP];
   __shared__ __attribute__((aligned(16))) float H1[R][kR4LDH];
   __shared__ float HP[4][NHP][kR4LDP];
@@ -572,13 +603,18 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
     hw[ht] = h < A ? wv : f4{0.f, 0.f, 0.f, 0.f};
   }
   constexpr int NI = (R * NHP + kR4Threads - 1) / kR4Threads;
-  float i_b3[NI], i_lstd[NI];
+  // per-item parameters of the Normal head: constant over the rollout, so std, var and log std
+  // (k_act4's per-launch arithmetic) are computed once
+  float i_b3[NI], i_sd[NI], i_var[NI], i_lsd[NI];
 #pragma unroll
   for (int u = 0; u < NI; ++u) {
     const int idx = min(tid + kR4Threads * u, R * A - 1), ir = idx / A, ia = idx - ir * A;
     (void)ir;
     i_b3[u] = P[K.ab3 + ia];
-    i_lstd[u] = P[K.logstd + ia];
+    const float sd = expf(P[K.logstd + ia]);
+    i_sd[u] = sd;
+    i_var[u] = sd * sd;
+    i_lsd[u] = logf(sd);
   }
   for (int idx = tid; idx < R * O; idx += kR4Threads) {
     const int r = idx / O, f = idx - r * O, e = row0 + r;
@@ -615,6 +651,7 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
 
   for (int t = 0; t < a.T; ++t) {
     const long step_id = a.step0 + t;
+    ROLL_STAMP(t, 0);
     // ---- inputs (k_act4's xv: this wave's k-slice), rollout stores of obs[t] / dones[t] ----
     f4 xv[NKW];
 #pragma unroll
@@ -627,23 +664,40 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
         xv[q][c] = (kb < NTO && col < O && row < E) ? v : 0.f;
       }
     }
-    for (int idx = tid; idx < R * O; idx += kR4Threads) {
-      const int r = idx / O, f = idx - r * O, e = row0 + r;
-      if (e < E) a.s_obs[((long)t * E + e) * O + f] = XO[r * LDQ + f];
+    // rollout store of obs[t] from the registers it arrived in (k_act4's store): lane (j, g) holds
+    // columns 16 kb + 4 g .. + 3 of row j
+    if (row < E) {
+      float* so = a.s_obs + ((long)t * E + row) * O;
+#pragma unroll
+      for (int q = 0; q < NKW; ++q) {
+        const int col = 16 * (kb0 + q) + 4 * g;
+        if (kb0 + q < NTO && col < O) {
+          if ((O & 3) == 0) {
+            *reinterpret_cast<f4*>(so + col) = xv[q];
+          } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              if (col + c < O) so[col + c] = xv[q][c];
+          }
+        }
+      }
     }
     if (tid < R && row0 + tid < E) a.s_dones[(long)t * E + row0 + tid] = EV[EV_DONE * R + tid];
-    // the Normal draws of this step (k_act4: computed under the weight fetch)
+    ROLL_STAMP(t, 1);
+    // the Normal draws of this step (k_act4: computed under the weight fetch; here under layer 1)
     float nz[NI];
+    const f4 h2 = trunk4<NTO, NKW>(xv, wa, w2v, b1, b2, P1, H1, ks, j, g, [&] {
 #pragma unroll
-    for (int u = 0; u < NI; ++u) {
-      const int idx = min(tid + kR4Threads * u, R * A - 1), ir = idx / A, ia = idx - ir * A;
-      uint32_t rr[4];
-      philox_draw(key, (long)(row0 + ir), step_id, (uint32_t)(ia >> 1), rr);
-      float z0, z1;
-      box_muller(rr[0], rr[1], z0, z1);
-      nz[u] = (ia & 1) ? z1 : z0;
-    }
-    const f4 h2 = trunk4<NTO, NKW>(xv, wa, w2v, b1, b2, P1, H1, ks, j, g);
+      for (int u = 0; u < NI; ++u) {
+        const int idx = min(tid + kR4Threads * u, R * A - 1), ir = idx / A, ia = idx - ir * A;
+        uint32_t rr[4];
+        philox_draw(key, (long)(row0 + ir), step_id, (uint32_t)(ia >> 1), rr);
+        float z0, z1;
+        box_muller(rr[0], rr[1], z0, z1);
+        nz[u] = (ia & 1) ? z1 : z0;
+      }
+    });
+    ROLL_STAMP(t, 2);
 #pragma unroll
     for (int ht = 0; ht < NHT; ++ht) {
       f4 hp = f4{0.f, 0.f, 0.f, 0.f};
@@ -661,8 +715,7 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
       if (idx < R * A) {
         const int ir = idx / A, ia = idx - ir * A, irow = row0 + ir;
         const float mu = (((HP[0][ia][ir] + HP[1][ia][ir]) + HP[2][ia][ir]) + HP[3][ia][ir]) + i_b3[u];
-        const float sd = expf(i_lstd[u]);
-        const float var = sd * sd, lsd = logf(sd);
+        const float sd = i_sd[u], var = i_var[u], lsd = i_lsd[u];
         const float act = mu + nz[u] * sd;
         const float d = act - mu;
         ITM[idx][0] = -(d * d) / (2.0f * var) - lsd - kLz;
@@ -676,93 +729,127 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
       for (int ai = 0; ai < A; ++ai) lp += ITM[tid * A + ai][0];
       a.s_logp[(long)t * E + row0 + tid] = lp;
     }
-    // ---- env step (k_synth_step / _wide arithmetic, wrapper chain fused): 32 lanes per env ----
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
+    ROLL_STAMP(t, 3);
+    // ---- env step (k_synth_step / _wide arithmetic, wrapper chain fused): 16 lanes per env, all
+    // 16 envs at once (the per-env reward / episode bookkeeping of lane 0 runs once per step) ----
+    {
 #pragma clang fp contract(off)
-      const int r = (tid >> 5) + 8 * half, i0 = tid & 31, e = row0 + r;
-      if (e >= E) continue;
-      const bool reset = EVI[EV_AR * R + r] != 0;
-      float* q = Q + r * LDQ;
-      float* xo = XO + r * LDQ;
-      float* om = WOM + r * LDQ;
-      float* ov = WOV + r * LDQ;
-      const float* ar = ACT + r * 32;
-      const float oc = EV[EV_WOC * R + r];  // read by every lane before lane 0 stores oc + 1
-      if (reset) {
-        const uint32_t rs = (uint32_t)EVI[EV_RSEED * R + r], rc = (uint32_t)EVI[EV_RCOUNT * R + r];
+      const int r = tid >> 4, i0 = tid & 15, e = row0 + r;
+      if (e < E) {
+        const bool reset = EVI[EV_AR * R + r] != 0;
+        float* q = Q + r * LDQ;
+        float* xo = XO + r * LDQ;
+        float* om = WOM + r * LDQ;
+        float* ov = WOV + r * LDQ;
+        const float* ar = ACT + r * 32;
+        const float oc = EV[EV_WOC * R + r];  // read by every lane before lane 0 stores oc + 1
+        if (reset) {
+          const uint32_t rs = (uint32_t)EVI[EV_RSEED * R + r], rc = (uint32_t)EVI[EV_RCOUNT * R + r];
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          const int i = 32 * c + i0;
-          if (i < O) {
-            uint32_t rr[4];
-            philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, rr);
-            const float v = (0.1f * ((2.0f * u01(rr[0])) - 1.0f));
-            q[i] = v;
-            xo[i] = w.on ? wrap_obs_at(om + i, ov + i, oc, v) : v;
+          for (int c = 0; c < NC16; ++c) {
+            const int i = 16 * c + i0;
+            if (i < O) {
+              uint32_t rr[4];
+              philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, rr);
+              const float v = (0.1f * ((2.0f * u01(rr[0])) - 1.0f));
+              q[i] = v;
+              xo[i] = w.on ? wrap_obs_at(om + i, ov + i, oc, v) : v;
+            }
           }
-        }
-        if (i0 == 0) {
-          if (w.on) EV[EV_WOC * R + r] = oc + 1.0f;
-          EVI[EV_RCOUNT * R + r] = (int)(rc + 1);
-          EVI[EV_T * R + r] = 0;
-          EV[EV_EPR * R + r] = 0.0f;
-          EVI[EV_EPL * R + r] = 0;
-          EV[EV_DONE * R + r] = 0.0f;
-          EVI[EV_AR * R + r] = 0;
-          a.s_rewards[(long)t * E + e] = 0.0f;
-        }
-      } else {
-        float qo[NCH], qn[NCH];
+          if (i0 == 0) {
+            if (w.on) EV[EV_WOC * R + r] = oc + 1.0f;
+            EVI[EV_RCOUNT * R + r] = (int)(rc + 1);
+            EVI[EV_T * R + r] = 0;
+            EV[EV_EPR * R + r] = 0.0f;
+            EVI[EV_EPL * R + r] = 0;
+            EV[EV_DONE * R + r] = 0.0f;
+            EVI[EV_AR * R + r] = 0;
+            a.s_rewards[(long)t * E + e] = 0.0f;
+          }
+        } else {
+          // Groups of up to 12 elements per lane: every LDS operand of a group is read before any
+          // of its results is written (independent element chains; interleaved loads and stores
+          // through possibly aliasing LDS pointers would serialise them). One env's 16 lanes are in
+          // one wave, so a q[i + 1] read precedes the neighbour's store in program order; the wrap
+          // to q[0] reads the value from before the step.
+          const float q0_old = q[0];
+          float q0_new = 0.0f;
+          int ai = i0 % A;
+          const int astep = 16 % A;
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          const int i = 32 * c + i0;
-          qo[c] = i < O ? q[i] : 0.0f;
-          qn[c] = i < O ? q[i + 1 < O ? i + 1 : 0] : 0.0f;
-        }
-        float q0_new = 0.0f;
+          for (int c0 = 0; c0 < NC16; c0 += kEnvGroup) {
+            float qo[kEnvGroup], qn[kEnvGroup], wm[kEnvGroup], wv[kEnvGroup], ac[kEnvGroup];
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          const int i = 32 * c + i0;
-          if (i < O) {
-            const float ai = fminf(fmaxf(ar[i % A], a.lo), a.hi);
-            const float nq = __fmaf_rn(0.9f, qo[c], __fmaf_rn(0.1f, ai, (0.05f * qn[c])));
-            q[i] = nq;
-            xo[i] = w.on ? wrap_obs_at(om + i, ov + i, oc, nq) : nq;
-            if (c == 0) q0_new = nq;
+            for (int u = 0; u < kEnvGroup; ++u) {
+              if (c0 + u < NC16) {
+                const int i = min(16 * (c0 + u) + i0, O - 1);
+                qo[u] = q[i];
+                qn[u] = i + 1 < O ? q[i + 1] : q0_old;
+                ac[u] = ar[ai];
+                ai += astep;
+                ai = ai >= A ? ai - A : ai;
+                if (w.on) {
+                  wm[u] = om[i];
+                  wv[u] = ov[i];
+                }
+              }
+            }
+            float nq[kEnvGroup], xn[kEnvGroup];
+#pragma unroll
+            for (int u = 0; u < kEnvGroup; ++u) {
+              if (c0 + u < NC16) {
+                const float aic = fminf(fmaxf(ac[u], a.lo), a.hi);
+                nq[u] = __fmaf_rn(0.9f, qo[u], __fmaf_rn(0.1f, aic, (0.05f * qn[u])));
+                xn[u] = w.on ? wrap_obs_at(&wm[u], &wv[u], oc, nq[u]) : nq[u];
+              }
+            }
+            if (c0 == 0) q0_new = nq[0];
+#pragma unroll
+            for (int u = 0; u < kEnvGroup; ++u) {
+              const int i = 16 * (c0 + u) + i0;
+              if (c0 + u < NC16 && i < O) {
+                q[i] = nq[u];
+                xo[i] = xn[u];
+                if (w.on) {
+                  om[i] = wm[u];
+                  ov[i] = wv[u];
+                }
+              }
+            }
           }
-        }
-        if (i0 == 0) {
-          if (w.on) EV[EV_WOC * R + r] = oc + 1.0f;
-          const float vel = ((q0_new - qo[0]) / 0.05f);
-          float ctrl = 0.0f;
-          for (int k = 0; k < A; ++k) {
-            const float ak = fminf(fmaxf(ar[k], a.lo), a.hi);
-            ctrl = (ctrl + ((0.1f * ak) * ak));
+          if (i0 == 0) {
+            if (w.on) EV[EV_WOC * R + r] = oc + 1.0f;
+            const float vel = ((q0_new - q0_old) / 0.05f);
+            float ctrl = 0.0f;
+            for (int k = 0; k < A; ++k) {
+              const float ak = fminf(fmaxf(ar[k], a.lo), a.hi);
+              ctrl = (ctrl + ((0.1f * ak) * ak));
+            }
+            const float rw = (vel - ctrl);
+            const int tt = EVI[EV_T * R + r] + 1;
+            EVI[EV_T * R + r] = tt;
+            const bool tr = tt >= 1000;
+            a.s_rewards[(long)t * E + e] =
+                w.on ? wrap_reward_at(EV + EV_WRA * R + r, EV + EV_WRM * R + r, EV + EV_WRV * R + r,
+                                      EV + EV_WRC * R + r, w.gamma, rw, 0.0f)
+                     : rw;
+            EV[EV_DONE * R + r] = tr ? 1.0f : 0.0f;
+            const float epr = (EV[EV_EPR * R + r] + rw);
+            EV[EV_EPR * R + r] = epr;
+            const int epl = EVI[EV_EPL * R + r] + 1;
+            EVI[EV_EPL * R + r] = epl;
+            if (tr) {
+              EV[EV_FR * R + r] += epr;
+              EV[EV_FL * R + r] += (float)epl;
+              EV[EV_FC * R + r] += 1.0f;
+            }
+            EVI[EV_AR * R + r] = tr ? 1 : 0;
           }
-          const float rw = (vel - ctrl);
-          const int tt = EVI[EV_T * R + r] + 1;
-          EVI[EV_T * R + r] = tt;
-          const bool tr = tt >= 1000;
-          a.s_rewards[(long)t * E + e] =
-              w.on ? wrap_reward_at(EV + EV_WRA * R + r, EV + EV_WRM * R + r, EV + EV_WRV * R + r,
-                                    EV + EV_WRC * R + r, w.gamma, rw, 0.0f)
-                   : rw;
-          EV[EV_DONE * R + r] = tr ? 1.0f : 0.0f;
-          const float epr = (EV[EV_EPR * R + r] + rw);
-          EV[EV_EPR * R + r] = epr;
-          const int epl = EVI[EV_EPL * R + r] + 1;
-          EVI[EV_EPL * R + r] = epl;
-          if (tr) {
-            EV[EV_FR * R + r] += epr;
-            EV[EV_FL * R + r] += (float)epl;
-            EV[EV_FC * R + r] += 1.0f;
-          }
-          EVI[EV_AR * R + r] = tr ? 1 : 0;
         }
       }
     }
     __syncthreads();
+    ROLL_STAMP(t, 4);
   }
   for (int idx = tid; idx < R * O; idx += kR4Threads) {
     const int r = idx / O, f = idx - r * O, e = row0 + r;
@@ -831,7 +918,7 @@ __global__ __launch_bounds__(256) void k_values4(ValuesArgs a) {
       }
     }
     __syncthreads();  // the previous block's VP / P1 / H1 readers are done
-    const f4 h2 = trunk4<NTO, NKW>(xv, wa, w2v, b1, b2, P1, H1, ks, j, g);
+    const f4 h2 = trunk4<NTO, NKW>(xv, wa, w2v, b1, b2, P1, H1, ks, j, g, [] {});
     float p = (hv.x * h2.x + hv.y * h2.y) + (hv.z * h2.z + hv.w * h2.w);
     p = row_allreduce(p);
     if (g == 0) VP[ks][j] = p;

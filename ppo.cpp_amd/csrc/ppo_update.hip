@@ -501,6 +501,9 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
   // wide inputs: the tile's loads go out in chunks of GC items from clamped indices (the chunk's
   // permutation entries, then its observation values), masked afterwards — a load under a per-lane
   // branch would wait for itself, one dependent round trip pair per item
+  // (the tile's permutation entries are in ROWS slot 0, loaded a tile ahead: only the data loads
+  // are on the tile's critical path)
+  auto perm_of = [&](int r) { return __float_as_int(ROWS[r * 8]); };
   auto gather_sync = [&](int itc) {
     const int mb = itc * R;
     constexpr int NGS = (R * OP + 255) / 256, GC = 4;
@@ -511,7 +514,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
 #pragma unroll
       for (int c = 0; c < GC; ++c) {
         const int idx = tid + 256 * (k0 + c), row = min(idx / OP, R - 1);
-        rp[c] = a.perm[min(mb + row, a.M - 1)];
+        rp[c] = perm_of(row);
       }
 #pragma unroll
       for (int c = 0; c < GC; ++c) {
@@ -532,7 +535,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       }
     }
     {
-      const int rrow = a.perm[min(mb + min(tid, R - 1), a.M - 1)];
+      const int rrow = perm_of(min(tid, R - 1));
       const float r1 = trunk == 0 ? a.ret[rrow] : a.logp[rrow];
       const float r2 = trunk == 0 ? a.val[rrow] : a.adv[rrow];
       if (tid < R) {
@@ -547,7 +550,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
 #pragma unroll
       for (int k = 0; k < NAS; ++k) {
         const int idx = tid + 256 * k, row = min(idx / (A > 0 ? A : 1), R - 1);
-        ap[k] = a.perm[min(mb + row, a.M - 1)];
+        ap[k] = perm_of(row);
       }
       float av[NAS];
 #pragma unroll
@@ -566,16 +569,22 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     pref_idx(blockIdx.x);
     pref_data(blockIdx.x);
   }
+  // wide inputs: row tid's permutation entry of the next tile (clamped, as the gather clamps rows)
+  int nperm = 0;
+  if constexpr (!PREF) nperm = tid < R ? a.perm[min((int)blockIdx.x * R + tid, a.M - 1)] : 0;
 
   float lst[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // per-lane loss statistics over this workgroup's tiles
   for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
     const int m0 = it * R;
     PPO_STAMP_START();
+    if constexpr (!PREF)
+      if (tid < R) ROWS[tid * 8] = __int_as_float(nperm);  // slot 0 is read only by gather_sync
     lds_barrier();  // the previous iteration's LDS readers are done
     if constexpr (PREF) {
       commit(it);
       pref_idx(it + gridDim.x);
     } else {
+      if (tid < R) nperm = a.perm[min((it + (int)gridDim.x) * R + tid, a.M - 1)];
       gather_sync(it);
     }
     // one head tile (NHT == 1): its weights, in the layout the head backward reads them (critic: w3

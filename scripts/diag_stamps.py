@@ -19,8 +19,14 @@ NAMES = ["top+gather", "L1 mm", "LN1+st+bar", "L2 mm issue", "LN2", "heads+bar",
          "hbias+head bwd", "LN2bwd+cs+st", "dh1 mm issue", "L1 re mm", "LN1bwd+cs+st"]
 NP = len(NAMES)
 NS, NT = NP + 2, 16
-cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=4096, num_steps=128, total_timesteps=4096 * 128 * 4)
-tr = ppo_amd.Trainer(cfg, num_envs_per_device=4096)
+# --ant: the cfg4 shard (Ant-v5, E = 1 024, 32 768-row minibatches: 4 tiles per workgroup)
+ANT = "--ant" in sys.argv
+sys.argv = [x for x in sys.argv if x != "--ant"]
+if ANT:
+    cfg = ppo_amd.ACPPOConfig(env_id="Ant-v5", num_envs=1024, num_steps=128, total_timesteps=1024 * 128 * 4)
+else:
+    cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=4096, num_steps=128, total_timesteps=4096 * 128 * 4)
+tr = ppo_amd.Trainer(cfg, num_envs_per_device=cfg.num_envs)
 tr.iterate()
 tr.agent.sync()
 lib = ppo_amd.lib()
@@ -32,7 +38,7 @@ raw = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 4, NT, NS).copy()
 if len(sys.argv) > 1:
     np.save(sys.argv[1], raw)
 st = raw[..., :NP + 1].astype(np.int64)
-d = np.diff(st, axis=-1)[:, :, 2:NT - 2]  # [wg, wave, tile, phase]
+d = np.diff(st, axis=-1)[:, :, (0 if ANT else 2):(4 if ANT else NT - 2)]  # [wg, wave, tile, phase]
 for trunk, sl in (("critic", slice(0, 256)), ("actor", slice(512, 768))):
     x = d[sl].reshape(-1, NP)
     x = x[(x > 0).all(axis=1) & (x < 10**7).all(axis=1)]

@@ -384,7 +384,7 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
       c->use_upd = c->use_upd2 = true;
       const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
       c->upd_nblk = std::min(ut, 512);  // both trunks per workgroup, 2 workgroups per CU x 256 CUs
-    } else if (!upd_kernel && upd_supported(c->K, c->sg[1].nh, sgmax, &c->upd) == 0) {
+    } else if (!upd_kernel && upd_supported(c->K, c->sg[1].nh, c->sg[0].size, c->sg[1].size, &c->upd) == 0) {
       c->use_upd = true;
       const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
       c->upd_nblk = std::min(ut, 256);  // 2 workgroups per CU x 256 CUs over the two trunks
@@ -760,6 +760,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   u.actn_off = c->upd.actn_off;
   u.acc_off = c->upd.acc_off;
   u.spar_off = c->upd.spar_off;
+  u.hw_global = c->upd.hw_global;
   u.trunk_mask = c->upd_trunk_mask;
   u.sched = c->upd_sched;
   const int nblk = c->use_upd ? c->upd_nblk : c->nblk;  // workgroups that wrote a slab row

@@ -68,6 +68,7 @@ struct UpdArgs {
   float* DZ2[2];
   float* slab[2];
   int actn_off, acc_off, spar_off;  // k_upd: runtime LDS offsets (floats)
+  int hw_global;                    // k_upd: the actor's dW3 accumulators live in its slab row (UpdGeoOut)
   int trunk_mask;         // k_upd: trunks to run (bit t = trunk t; 3 = both; other values: PPO_DIAG builds only)
   int sched;              // k_upd: bit 0 actor workgroups dispatched first, bit 1 actor wave priority
 };
@@ -77,6 +78,7 @@ struct UpdArgs {
 struct UpdGeoOut {
   size_t lds_bytes;
   int actn_off, acc_off, spar_off, rows;
+  int hw_global;  // 1: the actor's head-weight gradient accumulates in its slab row, not in LDS
 };
 
 struct DwArgs {
@@ -227,7 +229,7 @@ int launch_act3(const ActArgs& a, hipStream_t s);
 int launch_act4(const ActArgs& a, hipStream_t s);  // ppo_act_narrow.hip (H = 64 tanh agent)
 int launch_fwdbwd(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s);
 int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes);
-int upd_supported(const PackedLayout& K, int nh_actor, int sg_size, UpdGeoOut* g);
+int upd_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g);
 int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s);
 int upd2_supported(const PackedLayout& K, UpdGeoOut* g);  // ppo_update_narrow.hip (H = 64 tanh agent)
 int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s);

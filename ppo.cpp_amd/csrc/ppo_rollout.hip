@@ -567,12 +567,18 @@ PPO_DEV f4 trunk4(const f4 (&xv)[NKW], const f4 (&wa)[NKW][4], const f4 (&w2v)[4
 }
 }  // namespace
 
-template <int NTO, int NHT>
+// RR envs per workgroup (4 or 16): the MFMA tiles keep 16 rows (rows RR..15 are zero padding, which
+// no real row's arithmetic sees), the env / wrapper phase gets 256 / RR lanes per env. With RR = 4
+// a 1 024-env rollout spreads over 256 CUs instead of 64: the per-step layer MFMAs cost the same,
+// the VALU-bound wrapper chain a quarter.
+template <int NTO, int NHT, int RR>
 __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
-  constexpr int H = kR4H, R = kR4Rows, OP = NTO * 16, NKW = (NTO + 3) / 4, NHP = NHT * 16;
-  constexpr int LDQ = Roll4Geo<NTO, NHT>::LDQ, NC16 = (OP + 15) / 16, kEnvGroup = 12;
+  constexpr int H = kR4H, R = RR, OP = NTO * 16, NKW = (NTO + 3) / 4, NHP = NHT * 16;
+  constexpr int LPE = kR4Threads / RR;  // env lanes per env (one env within one wave)
+  constexpr int LDQ = Roll4Geo<NTO, NHT>::LDQ, NCE = (OP + LPE - 1) / LPE, kEnvGroup = 12;
+  static_assert(RR == 4 || RR == 16, "k_rollout4: 4 or 16 envs per workgroup");
   __shared__ float P1[4][H][kR4LDP];
-  __shared__ __attribute__((aligned(16))) float H1[R][kR4LDH];
+  __shared__ __attribute__((aligned(16))) float H1[kR4Rows][kR4LDH];
   __shared__ float HP[4][NHP][kR4LDP];
   __shared__ float ITM[R * NHP][2];
   __shared__ float XO[R * LDQ];   // the agent's input of the current step (the wrapped obs)
@@ -648,6 +654,7 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
   __syncthreads();
   const SampleKey key = sample_key(a.seed, a.rank);
   const int row = row0 + j;
+  const bool rvalid = j < R && row < E;  // MFMA tile row j is one of this block's envs
 
   for (int t = 0; t < a.T; ++t) {
     const long step_id = a.step0 + t;
@@ -660,13 +667,13 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int col = 16 * kb + 4 * g + c;
-        const float v = XO[j * LDQ + min(col, O - 1)];
-        xv[q][c] = (kb < NTO && col < O && row < E) ? v : 0.f;
+        const float v = XO[min(j, R - 1) * LDQ + min(col, O - 1)];
+        xv[q][c] = (kb < NTO && col < O && rvalid) ? v : 0.f;
       }
     }
     // rollout store of obs[t] from the registers it arrived in (k_act4's store): lane (j, g) holds
     // columns 16 kb + 4 g .. + 3 of row j
-    if (row < E) {
+    if (rvalid) {
       float* so = a.s_obs + ((long)t * E + row) * O;
 #pragma unroll
       for (int q = 0; q < NKW; ++q) {
@@ -730,11 +737,11 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
       a.s_logp[(long)t * E + row0 + tid] = lp;
     }
     ROLL_STAMP(t, 3);
-    // ---- env step (k_synth_step / _wide arithmetic, wrapper chain fused): 16 lanes per env, all
-    // 16 envs at once (the per-env reward / episode bookkeeping of lane 0 runs once per step) ----
+    // ---- env step (k_synth_step / _wide arithmetic, wrapper chain fused): LPE lanes per env, all
+    // RR envs at once (the per-env reward / episode bookkeeping of lane 0 runs once per step) ----
     {
 #pragma clang fp contract(off)
-      const int r = tid >> 4, i0 = tid & 15, e = row0 + r;
+      const int r = tid / LPE, i0 = tid % LPE, e = row0 + r;
       if (e < E) {
         const bool reset = EVI[EV_AR * R + r] != 0;
         float* q = Q + r * LDQ;
@@ -746,8 +753,8 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
         if (reset) {
           const uint32_t rs = (uint32_t)EVI[EV_RSEED * R + r], rc = (uint32_t)EVI[EV_RCOUNT * R + r];
 #pragma unroll
-          for (int c = 0; c < NC16; ++c) {
-            const int i = 16 * c + i0;
+          for (int c = 0; c < NCE; ++c) {
+            const int i = LPE * c + i0;
             if (i < O) {
               uint32_t rr[4];
               philox4x32(rc, (uint32_t)i, 0u, 0u, rs, 0x5EED5EEDu, rr);
@@ -769,20 +776,21 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
         } else {
           // Groups of up to 12 elements per lane: every LDS operand of a group is read before any
           // of its results is written (independent element chains; interleaved loads and stores
-          // through possibly aliasing LDS pointers would serialise them). One env's 16 lanes are in
+          // through possibly aliasing LDS pointers would serialise them). One env's LPE lanes are in
           // one wave, so a q[i + 1] read precedes the neighbour's store in program order; the wrap
           // to q[0] reads the value from before the step.
           const float q0_old = q[0];
+          const Recip rtot = recip_of(oc + 1.0f);
           float q0_new = 0.0f;
           int ai = i0 % A;
-          const int astep = 16 % A;
+          const int astep = LPE % A;
 #pragma unroll
-          for (int c0 = 0; c0 < NC16; c0 += kEnvGroup) {
+          for (int c0 = 0; c0 < NCE; c0 += kEnvGroup) {
             float qo[kEnvGroup], qn[kEnvGroup], wm[kEnvGroup], wv[kEnvGroup], ac[kEnvGroup];
 #pragma unroll
             for (int u = 0; u < kEnvGroup; ++u) {
-              if (c0 + u < NC16) {
-                const int i = min(16 * (c0 + u) + i0, O - 1);
+              if (c0 + u < NCE) {
+                const int i = min(LPE * (c0 + u) + i0, O - 1);
                 qo[u] = q[i];
                 qn[u] = i + 1 < O ? q[i + 1] : q0_old;
                 ac[u] = ar[ai];
@@ -797,17 +805,17 @@ __global__ __launch_bounds__(256) void k_rollout4(RolloutArgs a) {
             float nq[kEnvGroup], xn[kEnvGroup];
 #pragma unroll
             for (int u = 0; u < kEnvGroup; ++u) {
-              if (c0 + u < NC16) {
+              if (c0 + u < NCE) {
                 const float aic = fminf(fmaxf(ac[u], a.lo), a.hi);
                 nq[u] = __fmaf_rn(0.9f, qo[u], __fmaf_rn(0.1f, aic, (0.05f * qn[u])));
-                xn[u] = w.on ? wrap_obs_at(&wm[u], &wv[u], oc, nq[u]) : nq[u];
+                xn[u] = w.on ? wrap_obs_at_r(&wm[u], &wv[u], oc, rtot, nq[u]) : nq[u];
               }
             }
             if (c0 == 0) q0_new = nq[0];
 #pragma unroll
             for (int u = 0; u < kEnvGroup; ++u) {
-              const int i = 16 * (c0 + u) + i0;
-              if (c0 + u < NC16 && i < O) {
+              const int i = LPE * (c0 + u) + i0;
+              if (c0 + u < NCE && i < O) {
                 q[i] = nq[u];
                 xo[i] = xn[u];
                 if (w.on) {
@@ -938,9 +946,17 @@ int rollout_supported(const PackedLayout& K) {
   return -1;
 }
 
+// 4 envs per workgroup while that still fits one workgroup per CU (the kernel's registers allow
+// one), 16 beyond
 template <int NTO, int NHT>
 static int launch_rollout4_t(const RolloutArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((k_rollout4<NTO, NHT>), dim3((a.E + kR4Rows - 1) / kR4Rows), dim3(kR4Threads), 0, s, a);
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if ((a.E + 3) / 4 <= ncu)
+    hipLaunchKernelGGL((k_rollout4<NTO, NHT, 4>), dim3((a.E + 3) / 4), dim3(kR4Threads), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_rollout4<NTO, NHT, 16>), dim3((a.E + 15) / 16), dim3(kR4Threads), 0, s, a);
   return 0;
 }
 template <int NTO>

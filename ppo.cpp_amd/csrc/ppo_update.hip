@@ -397,9 +397,30 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
   const int O = K.O, A = K.A, nh = sg.nh;
   const float c = a.clip_coef;
   const float adv_mean = a.adv_stats[0], adv_std = a.adv_stats[1];
-  float* acc = ACC + wr * sg.size;
-  for (int i = tid; i < GE::WR * sg.size; i += 256) ACC[i] = 0.f;
+  // sl: the LDS accumulators' layout — sg's, or (hw_global, actor) sg without the head-weight
+  // block, whose nh x H sums then accumulate in this workgroup's slab row (upd_geo)
+  const bool hwg = a.hw_global && trunk == 1;
+  SmallGradLayout sl = sg;
+  if (hwg) {
+    const int d = sg.nh * H;
+    sl.hb -= d; sl.ls -= d; sl.stats -= d; sl.size -= d;
+  }
+  float* slab_row = a.slab[trunk] + (size_t)blockIdx.x * sg.size;
+  float* acc = ACC + wr * sl.size;
+  float* hwacc = hwg ? slab_row + sg.hW : acc + sg.hW;
+  for (int i = tid; i < GE::WR * sl.size; i += 256) ACC[i] = 0.f;
   for (int i = tid; i < R * LDG; i += 256) GG[i] = 0.f;  // padding heads stay exactly 0
+  if (hwg) {  // each owning lane zeroes the slab entries it will accumulate (see the head backward)
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = 16 * ht + 4 * g + r;
+          if (h < nh) hwacc[h * H + fbase + 16 * ft + j] = 0.f;
+        }
+  }
   // the per-tile LayerNorm / head-bias reads come from LDS instead of an L2 round trip each
   for (int i = tid; i < GE::NSPAR; i += 256) {
     const int v = i / H, f = i - v * H;
@@ -913,13 +934,13 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     if (tid < nh) {
       float s = 0.f;
       for (int row = 0; row < R; ++row) s += GG[row * LDG + tid];
-      ACC[sg.hb + tid] += s;
+      ACC[sl.hb + tid] += s;
     }
     if (!LN && trunk == 1 && tid >= 64 && tid < 64 + A) {
       const int ai = tid - 64;
       float s = 0.f;
       for (int row = 0; row < R; ++row) s += ITM[(row * A + ai) * ITS + 4];
-      ACC[sg.ls + ai] += s;
+      ACC[sl.ls + ai] += s;
     }
 
     // ---------------- head backward: dh2 = W3^T G^T, dW3 += G^T h2 ----------------
@@ -972,7 +993,7 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int h = 16 * ht + 4 * g + r;
-          if (h < nh) acc[sg.hW + h * H + fbase + 16 * ft + j] += d3[r];
+          if (h < nh) hwacc[h * H + fbase + 16 * ft + j] += d3[r];
         }
       }
     }
@@ -1095,36 +1116,51 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
     float t[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) t[k] = (RED[k] + RED[8 + k]) + (RED[16 + k] + RED[24 + k]);
-    float* st = ACC + sg.stats;  // row group 0's accumulator
+    float* st = ACC + sl.stats;  // row group 0's accumulator
     st[ST_PG] += t[0]; st[ST_V] += t[1]; st[ST_ENT] += t[2];
     st[ST_OKL] += t[3]; st[ST_KL] += t[4]; st[ST_CF] += t[5];
   }
   lds_barrier();
-  float* out = a.slab[trunk] + (size_t)blockIdx.x * sg.size;
-  for (int i = tid; i < sg.size; i += 256) {
+  // LDS accumulators -> the slab row (sg's layout); with hwg the head-weight block is already there
+  for (int i = tid; i < sl.size; i += 256) {
     float s = ACC[i];
 #pragma unroll
-    for (int w = 1; w < GE::WR; ++w) s += ACC[w * sg.size + i];
-    out[i] = s;
+    for (int w = 1; w < GE::WR; ++w) s += ACC[w * sl.size + i];
+    slab_row[hwg && i >= sg.hW ? i + sg.nh * H : i] = s;
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // host side: geometry, LDS size, dispatch
 // ---------------------------------------------------------------------------------------------
+// LDS of one workgroup; two must fit one CU (160 KB) so that a critic and an actor workgroup
+// share it. Where the actor's accumulators would break that (wide inputs: Ant's O = 105 takes
+// 95 KB), its head-weight gradient (nh x H floats) accumulates in its own slab row instead: every
+// element has one owning lane, which adds the tile contributions in tile order (bitwise the LDS
+// result).
 template <int H, int NTO, int NHT>
-static void upd_geo(const PackedLayout& K, int sg_size, UpdGeoOut* g) {
+static void upd_geo(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g) {
   using GE = Geo<H, NTO, NHT>;
-  const int scr = std::max(GE::WF * GE::NHP * GE::R, GE::R * K.A * GE::ITS);
-  int off = GE::oSCR + scr;
-  g->actn_off = off;
-  off += GE::R * K.A;
-  off = (off + 3) & ~3;
-  g->acc_off = off;
-  off += GE::WR * sg_size;
-  g->spar_off = off;
-  off += GE::NSPAR;
-  g->lds_bytes = (size_t)off * sizeof(float);
+  auto carve = [&](int sg_lds) {
+    const int scr = std::max(GE::WF * GE::NHP * GE::R, GE::R * K.A * GE::ITS);
+    int off = GE::oSCR + scr;
+    g->actn_off = off;
+    off += GE::R * K.A;
+    off = (off + 3) & ~3;
+    g->acc_off = off;
+    off += GE::WR * sg_lds;
+    g->spar_off = off;
+    off += GE::NSPAR;
+    g->lds_bytes = (size_t)off * sizeof(float);
+  };
+  g->hw_global = 0;
+  carve(std::max(sg0_size, sg1_size));
+  if (GE::WR == 1 && 2 * g->lds_bytes > 160 * 1024) {
+    const size_t full = g->lds_bytes;
+    carve(std::max(sg0_size, sg1_size - nh_actor * H));
+    if (2 * g->lds_bytes <= 160 * 1024) g->hw_global = 1;
+    else carve(std::max(sg0_size, sg1_size)), (void)full;  // one workgroup per CU either way
+  }
   g->rows = GE::R;
 }
 
@@ -1146,11 +1182,11 @@ static int dispatch_upd(const PackedLayout& K, int nh, F&& f) {
   return -1;
 }
 
-int upd_supported(const PackedLayout& K, int nh_actor, int sg_size, UpdGeoOut* g) {
+int upd_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g) {
   // both trunks run in one launch: the geometry must cover the actor's head count (critic: 1)
   return dispatch_upd(K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_, auto KL_) {
     (void)KIND_;
-    upd_geo<decltype(H_)::value, decltype(NTO_)::value, decltype(NHT_)::value>(K, sg_size, g);
+    upd_geo<decltype(H_)::value, decltype(NTO_)::value, decltype(NHT_)::value>(K, nh_actor, sg0_size, sg1_size, g);
     const auto k = k_upd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value, decltype(NHT_)::value,
                          decltype(KL_)::value>;
     return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) ==

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Quick GPU check after a rollout / update kernel change: the named -m gpu test files, the rollout
-# phase stamps and one config bench.   bash scripts/gpu_quick.sh <tag> "<test files>" [cfg]
+# phase stamps and one config bench.   bash scripts/gpu_quick.sh <tag> "<test files>" [cfg2|cfg4_shard|cfg1|all]
 set -o pipefail
 TAG=$1; TESTS=$2; CFG=${3:-cfg2}
 R=$GRAFT_REPO_ROOT
@@ -11,5 +11,6 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 tail -2 $OUT/tests.txt
 timeout -k 10 120 python3 scripts/roll_stamps.py > $OUT/roll_stamps.txt 2>&1 || { echo "roll stamps failed"; tail -20 $OUT/roll_stamps.txt; exit 1; }
 grep -v amdgpu.ids $OUT/roll_stamps.txt
-timeout -k 10 300 python3 scripts/bench_configs.py --only $CFG > $OUT/configs.jsonl 2>&1 || { echo "configs failed"; tail -20 $OUT/configs.jsonl; exit 1; }
+ONLY="--only $CFG"; [ "$CFG" = all ] && ONLY=""
+timeout -k 10 300 python3 scripts/bench_configs.py $ONLY > $OUT/configs.jsonl 2>&1 || { echo "configs failed"; tail -20 $OUT/configs.jsonl; exit 1; }
 cut -c1-600 $OUT/configs.jsonl

@@ -133,8 +133,8 @@ print(json.dumps(out))
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libppo_hip.so not built")
 def test_create_ex_rejects_unknown_options():
-    """ppo_create_ex parses its kernel-selection options before touching the GPU: an unknown key or
-    value is refused with a message and no context."""
+    """ppo_create_ex / ppo_carla_create_ex parse their kernel-selection options before touching the
+    GPU: an unknown key or value is refused with a message and no context."""
     import json
     import subprocess
     import sys
@@ -150,10 +150,15 @@ for opt in ("upd_kernel=fast", "act_kernel=3", "bogus=1", "dw_fused", "rollout=s
     ctx = ctypes.c_void_p()
     rc = lib.ppo_create_ex(ctypes.byref(cfg), 0, opt.encode(), ctypes.byref(ctx))
     out.append([rc, bool(ctx.value), lib.ppo_last_error().decode()])
+for opt in ("tail=coop", "conv1=staged,tail=", "conv1=fast"):  # the CaRL agent's options
+    cfg = ppo_amd.CarlaConfig(15, 192, 192, 8, 3, 2, 1.0, 32, 7, 0)
+    ctx = ctypes.c_void_p()
+    rc = lib.ppo_carla_create_ex(ctypes.byref(cfg), 0, opt.encode(), ctypes.byref(ctx))
+    out.append([rc, bool(ctx.value), lib.ppo_last_error().decode()])
 print(json.dumps(out))
 '''
     res = subprocess.run([sys.executable, "-c", script, os.path.join(ROOT, "ppo.cpp_amd")], capture_output=True,
                          text=True, timeout=240)
     assert res.returncode == 0, res.stderr[-2000:]
     for rc, has_ctx, err in json.loads(res.stdout.strip().splitlines()[-1]):
-        assert rc != 0 and not has_ctx and "ppo_create_ex" in err, err
+        assert rc != 0 and not has_ctx and ("ppo_create_ex" in err or "ppo_carla_create_ex" in err), err

@@ -126,8 +126,13 @@ typedef struct ppo_carla ppo_carla_t;
 
 /* carla_model.h:35-206 (the module) — allocates parameters and activation buffers on `device`. */
 int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_carla_t** out);
-/* options: NULL / "" (defaults), "conv1=staged" (the default: conv1 forward and weight gradient with
- * the image patch staged in LDS) or "conv1=generic" (the generic implicit-GEMM kernels; A/B tests) */
+/* options: NULL / "" (defaults) or "key=value" pairs separated by ',':
+ *   conv1=staged|generic       conv1 forward and weight gradient with the image patch staged in LDS
+ *                              (default) or the generic implicit-GEMM kernels (A/B tests)
+ *   tail=staged|fused|layers   forwards of n <= 64 rows: the MLP tail after the CNN as one launch per
+ *                              dependency stage (default), one cooperative launch with a grid barrier
+ *                              between stages, or one k_conv / k_conv_fin pair per layer (the path of
+ *                              larger batches); bitwise equal */
 int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, const char* options, ppo_carla_t** out);
 int ppo_carla_destroy(ppo_carla_t* c);
 int ppo_carla_get_layout(const ppo_carla_t* c, ppo_carla_layout* out);

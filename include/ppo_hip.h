@@ -87,6 +87,9 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *   act_kernel=auto|2|4      64-wide agent act: by shape (auto), k_act2, or k_act4
  *   dw_fused=1|0             dW1 / dW2 in one pass (k_dwf) or two (k_dw)
  *   rollout=auto|per_step    ppo_rollout_synth: persistent launch where supported, or per step
+ *   gradstep=split|fused     clip_grad_norm_ + Adam: two launches (k_gradnorm, k_adam; default) or
+ *                            one cooperative launch (k_gradstep: slower on ROCm 7, whose cooperative
+ *                            launch costs ~30 us); bitwise the same
  * An unknown key or value is an error. */
 int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* options, ppo_t** out);
 int ppo_destroy(ppo_t* ctx);

@@ -455,9 +455,10 @@ struct HeadArgs {
   float* hpre;  // [n][2A] dist_mu / dist_sigma pre-activations (training), may be null
 };
 
-__global__ __launch_bounds__(64) void k_carla_head(HeadArgs h) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= h.n) return;
+// one row of k_carla_head: the dist_mu / dist_sigma dot products (or, with pre != nullptr, their
+// values computed by the same loop elsewhere: pre[ai] = mu, pre[A + ai] = sigma pre-activations),
+// softplus + beta_min, the sample / mean / roach / given value, log_prob, entropy
+PPO_DEV void carla_head_row(const HeadArgs& h, int r, const float* pre, bool copy_value) {
   const float* P = h.P;
   const float* x = h.latent + (long)r * 256;
   const float hi = P[h.hi], lo = P[h.lo];
@@ -465,15 +466,22 @@ __global__ __launch_bounds__(64) void k_carla_head(HeadArgs h) {
   const long env = h.env_base + r;
   float lp = 0.f, ent = 0.f;
   for (int ai = 0; ai < h.A; ++ai) {
-    const float* wm = P + h.mu_w + (long)ai * 256;
-    const float* ws = P + h.sg_w + (long)ai * 256;
-    float pm = 0.f, ps = 0.f;
-    for (int k = 0; k < 256; ++k) {
-      pm = fmaf(wm[k], x[k], pm);
-      ps = fmaf(ws[k], x[k], ps);
+    float pm, ps;
+    if (pre) {
+      pm = pre[ai];
+      ps = pre[h.A + ai];
+    } else {
+      const float* wm = P + h.mu_w + (long)ai * 256;
+      const float* ws = P + h.sg_w + (long)ai * 256;
+      pm = 0.f;
+      ps = 0.f;
+      for (int k = 0; k < 256; ++k) {
+        pm = fmaf(wm[k], x[k], pm);
+        ps = fmaf(ws[k], x[k], ps);
+      }
+      pm += P[h.mu_b + ai];
+      ps += P[h.sg_b + ai];
     }
-    pm += P[h.mu_b + ai];
-    ps += P[h.sg_b + ai];
     if (h.hpre) {
       h.hpre[(long)r * 2 * h.A + ai] = pm;
       h.hpre[(long)r * 2 * h.A + h.A + ai] = ps;
@@ -505,10 +513,180 @@ __global__ __launch_bounds__(64) void k_carla_head(HeadArgs h) {
   }
   if (h.logprob) h.logprob[r] = lp;
   if (h.entropy) h.entropy[r] = ent;
-  if (h.value) h.value[r] = h.val[r];
+  if (copy_value && h.value) h.value[r] = h.val[r];
 }
 
-int launch_conv(const ConvArgs& a, hipStream_t s, bool img = true) {
+__global__ __launch_bounds__(64) void k_carla_head(HeadArgs h) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= h.n) return;
+  carla_head_row(h, r, nullptr, true);
+}
+
+// ==========================================================================================
+// The MLP tail at rollout batch sizes (n <= kTailMaxN): state MLP, linear, value and policy heads
+// and the distribution head after the CNN, as stages of ONE kernel (cooperative launch, a grid
+// barrier between stages) instead of ~20 launches of k_conv / k_conv_fin / k_carla_pack /
+// k_carla_head, whose fixed cost per launch dominated the 32-row forward. Every Linear output is
+// bitwise k_conv's: a work item (16 rows x 16 output channels of one layer) is one workgroup, its
+// waves run the same MFMA chains over the same 128-wide k chunks (same operands, same step order,
+// same masked operands), and the chunk partials are added in z order from 0 as k_conv_fin does
+// (one chunk: acc + bias, as k_conv). The head's dot products run one (row, action) per thread with
+// k_carla_head's loop; the per-row Beta arithmetic is k_carla_head's.
+// ==========================================================================================
+constexpr int kTailThreads = 512, kTailMaxZ = 10, kTailMaxLin = 9, kTailMaxStage = 8, kTailMaxN = 64;
+
+struct TailLin {
+  const float* in;
+  long in_stride;
+  int K;
+  long w, b;  // parameter offsets: W [OC][K], b [OC]
+  float* out;
+  long out_stride;
+  int OC, relu;
+  float* out2;  // optional copy of output column 0 (the value head's last layer -> value), stride 1
+};
+struct TailArgs {
+  const float* P;
+  int n;
+  ConvArgs c6;  // conv6's split-K partials, finished in stage 0 as k_conv_fin (c6_Z > 1)
+  int c6_Z;
+  const float* vmeas;  // value measurements -> feat columns [256, 256 + NV) (stage 0)
+  float* feat;
+  int NV;
+  TailLin lin[kTailMaxLin];
+  int lin_stage[kTailMaxLin];  // stage of each layer (non-decreasing)
+  int nlin, nstage, head_stage;
+  HeadArgs h;
+  unsigned* bar;       // grid barrier counter (monotonic across launches)
+  unsigned bar_base;   // its value when this launch started
+  int stage_lo, stage_hi;  // the stages this launch runs (a barrier between consecutive ones)
+};
+
+PPO_DEV int tail_z(int K) { return K >= 256 ? (K + kSplitKC - 1) / kSplitKC : 1; }
+
+// one Linear work item: rows s0 .. s0 + 15, output channels oc0 .. oc0 + 15 of layer L
+PPO_DEV void tail_lin_item(const float* __restrict__ P, const TailLin& L, int n, int s0, int oc0, float* part) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int K = L.K, Z = tail_z(K), kc = Z > 1 ? kSplitKC : K;
+  const int oc = oc0 + j, s = s0 + j;
+  const float* wrow = P + L.w + (long)(oc < L.OC ? oc : 0) * K;
+  const bool sv = s < n;
+  const float* xrow = L.in + (long)(sv ? s : 0) * L.in_stride;
+  // a chunk is at most 32 k-steps (128 / 4): all 64 operand loads of a lane go out together (one
+  // memory latency per chunk), from clamped addresses, masked afterwards
+  for (int z = wave; z < Z; z += kTailThreads / 64) {
+    const int kbeg = z * kc, kend = min(K, kbeg + kc);
+    const int nsteps = 4 * ((kend - kbeg + 15) / 16);
+    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+    float av[kSplitKC / 4], bv[kSplitKC / 4];
+#pragma unroll
+    for (int u = 0; u < kSplitKC / 4; ++u) {
+      const int k = kbeg + 4 * u + g;
+      // k_conv's staged weight: rows of K % 4 == 0 are read as float4s from min(k, K - 4), so a
+      // masked tap past the end holds W[K - 4 + (k & 3)]; other rows clamp to K - 1
+      const int kw = (K & 3) == 0 ? (k < K ? k : K - 4 + (k & 3)) : min(k, K - 1);
+      av[u] = wrow[kw] * ((oc < L.OC && k < kend) ? 1.0f : 0.0f);
+      const bool ok = sv && k < kend;
+      bv[u] = (ok ? xrow[min(k, K - 1)] : L.in[0]) * (ok ? 1.0f : 0.0f);
+    }
+#pragma unroll
+    for (int u = 0; u < kSplitKC / 4; ++u)
+      if (u < nsteps) acc = mfma16(av[u], bv[u], acc);
+    // lane (j, g) holds output channel oc0 + 4 g + r of row s0 + j
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[(z * 16 + 4 * g + r) * 17 + j] = acc[r];
+  }
+  __syncthreads();
+  if (tid < 256) {
+    const int ocl = tid >> 4, sl = tid & 15, o = oc0 + ocl, r = s0 + sl;
+    if (o < L.OC && r < n) {
+      float y;
+      if (Z == 1) {
+        y = part[ocl * 17 + sl] + P[L.b + o];
+      } else {
+        float v = 0.f;
+        for (int z = 0; z < Z; ++z) v += part[(z * 16 + ocl) * 17 + sl];
+        y = v + P[L.b + o];
+      }
+      if (L.relu) y = y > 0.0f ? y : 0.0f;
+      L.out[(long)r * L.out_stride + o] = y;
+      if (L.out2 && o == 0) L.out2[r] = y;
+    }
+  }
+  __syncthreads();  // part is reused by the next item
+}
+
+__global__ __launch_bounds__(kTailThreads) void k_carla_tail(TailArgs a) {
+  __shared__ float part[kTailMaxZ * 16 * 17];
+  __shared__ float pre[kTailThreads * 2];
+  const int tid = threadIdx.x;
+  const int rt_n = (a.n + 15) / 16;
+  for (int stage = a.stage_lo; stage <= a.stage_hi; ++stage) {
+    if (stage > a.stage_lo) grid_barrier(a.bar, a.bar_base + (unsigned)(stage - a.stage_lo) * gridDim.x);
+    if (stage == 0) {  // conv6's split-K finish (k_conv_fin) and the value measurements
+      const long gt = (long)blockIdx.x * kTailThreads + tid, gs = (long)gridDim.x * kTailThreads;
+      if (a.c6_Z > 1) {
+        const ConvArgs& c = a.c6;
+        const int P6 = c.OH * c.OW;
+        const long Q = (long)c.n * P6;
+        for (long i = gt; i < Q * c.OC; i += gs) {
+          const long q = i / c.OC;
+          const int oc = (int)(i - q * c.OC);
+          float v = 0.f;
+          for (int z = 0; z < a.c6_Z; ++z) v += c.part[(size_t)z * Q * c.OC + i];
+          float y = v + c.b[oc];
+          if (c.relu) y = y > 0.0f ? y : 0.0f;
+          const long smp = q / P6;
+          c.out[smp * c.out_stride + (long)oc * P6 + (q - smp * P6)] = y;
+        }
+      }
+      for (long i = gt; i < (long)a.n * a.NV; i += gs) {
+        const long r = i / a.NV, cc = i - r * a.NV;
+        a.feat[r * (256 + a.NV) + 256 + cc] = a.vmeas[i];
+      }
+    }
+    // Linear work items of this stage, then (head stage) the distribution head
+    int nitems = 0;
+    for (int l = 0; l < a.nlin; ++l)
+      if (a.lin_stage[l] == stage) nitems += rt_n * ((a.lin[l].OC + 15) / 16);
+    const int head_wgs = stage == a.head_stage ? (a.n * a.h.A * 2 + kTailThreads - 1) / kTailThreads : 0;
+    for (int it = blockIdx.x; it < nitems + head_wgs; it += gridDim.x) {
+      if (it < nitems) {
+        int rem = it, l = 0;
+        for (; l < a.nlin; ++l) {
+          if (a.lin_stage[l] != stage) continue;
+          const int cnt = rt_n * ((a.lin[l].OC + 15) / 16);
+          if (rem < cnt) break;
+          rem -= cnt;
+        }
+        const int rt = rem % rt_n, ot = rem / rt_n;
+        tail_lin_item(a.P, a.lin[l], a.n, 16 * rt, 16 * ot, part);
+      } else {
+        // head: thread (row, ai, mu | sigma) runs k_carla_head's dot product loop for its
+        // pre-activation; then one thread per row the rest of k_carla_head
+        const HeadArgs& h = a.h;
+        const int A = h.A, rows = kTailThreads / (2 * A), r0 = (it - nitems) * rows;
+        const int rl = tid / (2 * A), q = tid - rl * 2 * A, r = r0 + rl;
+        if (rl < rows && r < a.n) {
+          const int ai = q < A ? q : q - A;
+          const float* wv = a.P + (q < A ? h.mu_w : h.sg_w) + (long)ai * 256;
+          const float* x = h.latent + (long)r * 256;
+          float p = 0.f;
+          for (int k = 0; k < 256; ++k) p = fmaf(wv[k], x[k], p);
+          pre[rl * 2 * A + q] = p + a.P[(q < A ? h.mu_b : h.sg_b) + ai];
+        }
+        __syncthreads();
+        if (tid < rows && r0 + tid < a.n) carla_head_row(h, r0 + tid, pre + tid * 2 * A, false);
+        __syncthreads();
+      }
+    }
+  }
+}
+
+// fin = false: a split-K layer leaves its partials (k_conv_fin is the caller's, e.g. the fused
+// tail's stage 0); *z_out receives the chunk count (1: not split)
+int launch_conv(const ConvArgs& a, hipStream_t s, bool img = true, bool fin = true, int* z_out = nullptr) {
+  if (z_out) *z_out = 1;
   if (a.IC * a.K * a.K > kMaxKTab) return -1;
   if (img && a.in_u8 && ((uintptr_t)a.in_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 8 && a.IW % 4 == 0 &&
       a.in_stride % 4 == 0 && a.OH <= 16 * 64 && img2_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {
@@ -549,7 +727,8 @@ int launch_conv(const ConvArgs& a, hipStream_t s, bool img = true) {
     else PPO_CONV_LAUNCH(1, 1);
   }
 #undef PPO_CONV_LAUNCH
-  if (Z > 1) hipLaunchKernelGGL(k_conv_fin, dim3((unsigned)((Q * a.OC + 255) / 256)), dim3(256), 0, s, b, Z);
+  if (z_out) *z_out = Z;
+  if (Z > 1 && fin) hipLaunchKernelGGL(k_conv_fin, dim3((unsigned)((Q * a.OC + 255) / 256)), dim3(256), 0, s, b, Z);
   return 0;
 }
 
@@ -581,6 +760,12 @@ struct ppo_carla {
   float* small = nullptr;  // scalars, tensor table and norm slices (carla_train_init)
   long step = 0;
   bool conv_img = true;  // LDS-staged conv1 / conv2 kernels (PPO_CARLA_CONV1=0 at create: generic, for A/B)
+  // MLP tail for n <= kTailMaxN: 1 (default) one launch per stage, 0 one cooperative launch (a grid
+  // barrier between stages: slower here, a cooperative launch costs more than the launches it
+  // saves), 2 one k_conv / k_conv_fin pair per layer
+  int tail_mode = 1;
+  unsigned* tail_bar = nullptr;  // k_carla_tail's grid barrier counter
+  unsigned tail_count = 0;       // arrivals so far (the counter's value between launches)
   // data parallelism (ppo_carla_comm_init): one RCCL communicator, any world >= 1
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
@@ -599,7 +784,7 @@ extern "C" int ppo_carla_destroy(ppo_carla_t* c) {
   float* bufs[] = {c->P,    c->enc,  c->s1,  c->l1,  c->feat,  c->v1,  c->v2,      c->val,  c->p1,
                    c->p2,   c->hpre, c->G,   c->m,   c->v,     c->denc, c->ds1,     c->dl1,  c->dfeat,
                    c->dv1,  c->dv2,  c->dp1, c->dp2, c->dhead, c->dval, c->lp,      c->ent,  c->rowstat,
-                   c->part, c->small,  c->ksplit};
+                   c->part, c->small,  c->ksplit, reinterpret_cast<float*>(c->tail_bar)};
   for (float* b : bufs)
     if (b) (void)hipFree(b);
   for (float* b : c->act)
@@ -618,11 +803,20 @@ extern "C" int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_car
 extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, const char* options, ppo_carla_t** out) {
   if (!cfg || !out) return ppo_fail("ppo_carla_create: null argument", -1);
   bool conv_img = true;
-  if (options && *options) {
-    const std::string o(options);
-    if (o == "conv1=staged") conv_img = true;
-    else if (o == "conv1=generic") conv_img = false;
-    else return ppo_fail("ppo_carla_create_ex: unknown option " + o, -1);
+  int tail_mode = 1;
+  if (options && *options) {  // comma-separated key=value
+    std::string rest(options);
+    while (!rest.empty()) {
+      const size_t cpos = rest.find(',');
+      const std::string o = rest.substr(0, cpos);
+      rest = cpos == std::string::npos ? std::string() : rest.substr(cpos + 1);
+      if (o == "conv1=staged") conv_img = true;
+      else if (o == "conv1=generic") conv_img = false;
+      else if (o == "tail=fused") tail_mode = 0;
+      else if (o == "tail=staged") tail_mode = 1;
+      else if (o == "tail=layers") tail_mode = 2;
+      else return ppo_fail("ppo_carla_create_ex: unknown option " + o, -1);
+    }
   }
   if (int rc = ppo_runtime_check()) return rc;
   ppo_carla_layout L;
@@ -639,6 +833,7 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
   c->L = L;
   c->device = device;
   c->conv_img = conv_img;
+  c->tail_mode = tail_mode;
 #ifdef PPO_DIAG
   if (const char* e = getenv("PPO_CARLA_CONV1")) c->conv_img = !(e[0] == '0');
 #endif
@@ -669,6 +864,7 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
     need(256 + L.NV, 1, 256); need(256, 1, 256); need(256, 1, 1);
     if (m) rc |= carla_alloc(&c->ksplit, m);
   }
+  rc |= carla_alloc(reinterpret_cast<float**>(&c->tail_bar), 1);
   if (rc || hipDeviceSynchronize() != hipSuccess) {
     ppo_carla_destroy(c);
     return ppo_fail("ppo_carla_create: device allocation failed", -2);
@@ -715,6 +911,9 @@ extern "C" int ppo_carla_forward(ppo_carla_t* c, int n, const uint8_t* bev, cons
   auto linear = [&](const float* in, long in_stride, int IN, long w, long b, float* out, long out_stride, int OUT,
                     int relu) { return conv(in, nullptr, in_stride, IN, 1, 1, w, b, out, out_stride, OUT, 1, 1, 1, 1, relu); };
   int rc = 0;
+  const bool fused_tail = c->tail_mode != 2 && n <= kTailMaxN;
+  ConvArgs c6{};
+  int c6_Z = 1;
   // cnn (carla_model.h:66-78, :236): conv1 reads the uint8 image, conv6 writes linear-input columns 0..1023
   const uint8_t* img = bev;
   const float* cur = nullptr;
@@ -723,14 +922,72 @@ extern "C" int ppo_carla_forward(ppo_carla_t* c, int n, const uint8_t* bev, cons
     const bool last = i == PPO_CARLA_NCONV - 1;
     float* out = last ? c->enc : c->act[i];
     const long out_stride = last ? 1280 : (long)L.conv_oc[i] * L.conv_oh[i] * L.conv_ow[i];
-    rc |= conv(cur, img, cur_stride, L.conv_ic[i], L.conv_ih[i], L.conv_iw[i], L.conv_w[i], L.conv_b[i], out,
-               out_stride, L.conv_oc[i], L.conv_oh[i], L.conv_ow[i], L.conv_k[i], L.conv_s[i], 1);
+    if (last && fused_tail) {  // conv6's split-K finish moves into the tail's stage 0
+      c6 = ConvArgs{cur, nullptr, cur_stride, L.conv_ic[i], L.conv_ih[i], L.conv_iw[i], P + L.conv_w[i],
+                    P + L.conv_b[i], out, out_stride, L.conv_oc[i], L.conv_oh[i], L.conv_ow[i], L.conv_k[i],
+                    L.conv_s[i], 1, n, c->ksplit, 0};
+      rc |= launch_conv(c6, s, c->conv_img, false, &c6_Z);
+    } else {
+      rc |= conv(cur, img, cur_stride, L.conv_ic[i], L.conv_ih[i], L.conv_iw[i], L.conv_w[i], L.conv_b[i], out,
+                 out_stride, L.conv_oc[i], L.conv_oh[i], L.conv_ow[i], L.conv_k[i], L.conv_s[i], 1);
+    }
     img = nullptr;
     cur = out;
     cur_stride = out_stride;
   }
-  // state_linear (:238) -> columns 1024..1279; linear (:240) -> features = value-head input columns 0..255
   const long FW = 256 + L.NV;
+  if (fused_tail) {
+    if (rc) return ppo_fail("ppo_carla_forward: no convolution kernel for this shape", -1);
+    TailArgs ta{};
+    ta.P = P;
+    ta.n = n;
+    ta.c6 = c6;
+    ta.c6_Z = c6_Z;
+    ta.vmeas = vmeas;
+    ta.feat = c->feat;
+    ta.NV = L.NV;
+    auto lin = [&](int stage, const float* in, long in_stride, int K, long w, long b, float* out, long out_stride,
+                   int OC, int relu, float* out2) {
+      ta.lin[ta.nlin] = TailLin{in, in_stride, K, w, b, out, out_stride, OC, relu, out2};
+      ta.lin_stage[ta.nlin++] = stage;
+    };
+    // the forward's layers in dependency stages (carla_model.h:238-279)
+    lin(0, meas, L.NM, L.NM, L.st_w[0], L.st_b[0], c->s1, 256, 256, 1, nullptr);
+    lin(1, c->s1, 256, 256, L.st_w[1], L.st_b[1], c->enc + 1024, 1280, 256, 1, nullptr);
+    lin(2, c->enc, 1280, 1280, L.lin_w[0], L.lin_b[0], c->l1, 512, 512, 1, nullptr);
+    lin(3, c->l1, 512, 512, L.lin_w[1], L.lin_b[1], c->feat, FW, 256, 1, nullptr);
+    lin(4, c->feat, FW, (int)FW, L.v_w[0], L.v_b[0], c->v1, 256, 256, 1, nullptr);
+    lin(4, c->feat, FW, 256, L.pi_w[0], L.pi_b[0], c->p1, 256, 256, 1, nullptr);
+    lin(5, c->v1, 256, 256, L.v_w[1], L.v_b[1], c->v2, 256, 256, 1, nullptr);
+    lin(5, c->p1, 256, 256, L.pi_w[1], L.pi_b[1], c->p2, 256, 256, 1, nullptr);
+    lin(6, c->v2, 256, 256, L.v_w[2], L.v_b[2], c->val, 1, 1, 0, value);
+    ta.nstage = 7;
+    ta.head_stage = 6;
+    ta.h = HeadArgs{P,          L.mu_w, L.mu_b,   L.sg_w,    L.sg_b,    L.hi,    L.lo,
+                    c->p2,      c->val, n,        L.A,       sample_type, c->cfg.beta_min, action_in,
+                    c->cfg.seed, c->cfg.rank, env_base, step_id, action, logprob, entropy, value, alpha, beta,
+                    c->hpre};
+    ta.bar = c->tail_bar;
+    const int rt_n = (n + 15) / 16;
+    const unsigned G = (unsigned)(rt_n * 32);  // linear.0's work items (512 / 16 output tiles)
+    if (c->tail_mode == 0) {
+      ta.stage_lo = 0;
+      ta.stage_hi = ta.nstage - 1;
+      ta.bar_base = c->tail_count;
+      void* args[] = {&ta};
+      if (hipLaunchCooperativeKernel((const void*)k_carla_tail, dim3(G), dim3(kTailThreads), args, 0, s) != hipSuccess)
+        return ppo_fail("ppo_carla_forward: cooperative launch of the fused tail failed", -2);
+      c->tail_count += (unsigned)(ta.nstage - 1) * G;
+    } else {
+      for (int st = 0; st < ta.nstage; ++st) {
+        ta.stage_lo = ta.stage_hi = st;
+        hipLaunchKernelGGL(k_carla_tail, dim3(G), dim3(kTailThreads), 0, s, ta);
+      }
+    }
+    if (hipGetLastError() != hipSuccess) return ppo_fail("ppo_carla_forward: launch failed", -2);
+    return 0;
+  }
+  // state_linear (:238) -> columns 1024..1279; linear (:240) -> features = value-head input columns 0..255
   rc |= linear(meas, L.NM, L.NM, L.st_w[0], L.st_b[0], c->s1, 256, 256, 1);
   rc |= linear(c->s1, 256, 256, L.st_w[1], L.st_b[1], c->enc + 1024, 1280, 256, 1);
   rc |= linear(c->enc, 1280, 1280, L.lin_w[0], L.lin_b[0], c->l1, 512, 512, 1);

@@ -896,7 +896,7 @@ __global__ __launch_bounds__(512) void k_dw(DwArgs a) {
 // one 32x32 MFMA per wave and row pair) rides under the MFMA-bound dW2 product (eight per wave)
 // instead of running as a second, load-bound phase. 8 waves: dW2 as a 4 x 2 grid of 64 x 128
 // wave tiles, dW1 as one 32-row o-tile per wave. Slab layout as k_dw.
-template <int H, int OP>
+template <int H, int OP, int NSL>
 __global__ __launch_bounds__(512) void k_dwf(DwArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int KS = 16, NTH = 512;
@@ -907,10 +907,16 @@ __global__ __launch_bounds__(512) void k_dwf(DwArgs a) {
   static_assert(H == 256 && OP <= 32 && N2 % NTH == 0, "k_dwf geometry");
   constexpr int PW = N2 / NTH;                      // f4 per thread per width-H source
   constexpr int NXT = (NX + NTH - 1) / NTH;
-  constexpr int TOW = 2, TIW = 4;                   // dW2 wave tile: 2 x 4 32x32 tiles
+  // dW2 wave tile: TOW x 4 32x32 tiles; with NSL output slices a workgroup owns dW2^T rows
+  // [s H / NSL, (s + 1) H / NSL) and dW1^T's rows in that range (its waves 0 .. 8 / NSL - 1)
+  constexpr int TOW = 2 / NSL, TIW = 4;
+  static_assert(NSL == 1 || NSL == 2, "k_dwf slices");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hs = lane >> 5;
   const int wo = wave & 3, wi = wave >> 2;
-  const int trunk = blockIdx.y;
+  const int trunk = blockIdx.y, slice = NSL > 1 ? (int)blockIdx.z : 0;
+  const int obase = slice * (H / NSL);                       // first dW2^T / dW1^T row of the slice
+  const bool w1_wave = NSL == 1 || wave < 8 / NSL;          // this wave owns a dW1^T row tile
+  const int w1row = obase + wave * 32;                       // its first row
   const long m0 = (long)blockIdx.x * a.rows_per_chunk;
   const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
   if (m0 >= m1) return;
@@ -969,16 +975,16 @@ __global__ __launch_bounds__(512) void k_dwf(DwArgs a) {
       const float* rowp = sb + (k + hs) * LDH;
       float av[TOW], bv[TIW];
 #pragma unroll
-      for (int u = 0; u < TOW; ++u) av[u] = rowp[(wo * TOW + u) * 32 + l32];
+      for (int u = 0; u < TOW; ++u) av[u] = rowp[obase + (wo * TOW + u) * 32 + l32];
 #pragma unroll
       for (int v = 0; v < TIW; ++v) bv[v] = rowp[oH1 + (wi * TIW + v) * 32 + l32];
-      const float a1 = rowp[oDZ1 + wave * 32 + l32];
+      const float a1 = rowp[oDZ1 + (w1_wave ? w1row : 0) + l32];
       const float b1 = l32 < OP ? sb[oXN + (k + hs) * LDX + l32] : 0.0f;
 #pragma unroll
       for (int u = 0; u < TOW; ++u)
 #pragma unroll
         for (int v = 0; v < TIW; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[v], acc[u][v], 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc1, 0, 0, 0);
+      if (w1_wave) acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc1, 0, 0, 0);
     }
     if (sI + 1 < nst) store((sI + 1) & 1);
     lds_barrier();
@@ -993,8 +999,8 @@ __global__ __launch_bounds__(512) void k_dwf(DwArgs a) {
     for (int u = 0; u < TOW; ++u)
 #pragma unroll
       for (int v = 0; v < TIW; ++v)
-        out[(size_t)((wo * TOW + u) * 32 + orow) * H + (wi * TIW + v) * 32 + l32] = acc[u][v][r];
-    if (l32 < OP) out[(size_t)H * H + (size_t)(wave * 32 + orow) * OP + l32] = acc1[r];
+        out[(size_t)(obase + (wo * TOW + u) * 32 + orow) * H + (wi * TIW + v) * 32 + l32] = acc[u][v][r];
+    if (w1_wave && l32 < OP) out[(size_t)H * H + (size_t)(w1row + orow) * OP + l32] = acc1[r];
   }
 }
 
@@ -1088,9 +1094,8 @@ __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
 // =============================================================================================
 // pass 1 (k_gradnorm): grid (tensor, PPO_GN_SPLIT slices) -> partial sums of squares;
 // pass 2 (head of k_adam, every block): per-tensor norms from the slices in order, total, coef.
-__global__ __launch_bounds__(256) void k_gradnorm(NormArgs a) {
-  __shared__ float red[4];
-  const int t = blockIdx.x, sp = blockIdx.y, tid = threadIdx.x;
+PPO_DEV void gradnorm_slice(const NormArgs& a, int t, int sp, float* red) {
+  const int tid = threadIdx.x;
   const int len = a.len[t], sl = (((len + PPO_GN_SPLIT - 1) / PPO_GN_SPLIT) + 3) & ~3;
   const int i0 = sp * sl, i1 = min(len, i0 + sl);
   const float* g = a.grad + a.off[t];
@@ -1113,13 +1118,16 @@ __global__ __launch_bounds__(256) void k_gradnorm(NormArgs a) {
   __syncthreads();
   if (tid == 0) a.part[t * PPO_GN_SPLIT + sp] = (red[0] + red[1]) + (red[2] + red[3]);
 }
+__global__ __launch_bounds__(256) void k_gradnorm(NormArgs a) {
+  __shared__ float red[4];
+  gradnorm_slice(a, blockIdx.x, blockIdx.y, red);
+}
 
 // =============================================================================================
 // k_adam — grad *= clip coef; Adam (bias-corrected, torch::optim::Adam); refresh W2^T copies
 // =============================================================================================
-__global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
-  __shared__ float s_norm[PPO_LAYOUT_MAX_TENSORS];
-  __shared__ float s_coef;
+PPO_DEV void adam_block(const AdamArgs& a, int bid, float* s_norm, float& s_coef) {
+  const int blockIdx_x = bid;
   if (threadIdx.x < a.nt) {
     float q = 0.0f;
 #pragma unroll
@@ -1135,16 +1143,16 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
     float coef = a.max_norm / (total + 1e-6f);
     coef = coef > 1.0f ? 1.0f : coef;
     s_coef = coef;
-    if (blockIdx.x == 0) {
+    if (blockIdx_x == 0) {
       a.norm_out[0] = total;
       a.norm_out[1] = coef;
       if (a.stat_out) a.stat_out[0] = total;
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x < a.nt) a.norm_out[2 + threadIdx.x] = s_norm[threadIdx.x];
+  if (blockIdx_x == 0 && threadIdx.x < a.nt) a.norm_out[2 + threadIdx.x] = s_norm[threadIdx.x];
   __syncthreads();
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.n) return;
+  const long i = (long)blockIdx_x * 256 + threadIdx.x;
+  if (i >= a.n) return;  // (no barrier follows)
   const long p = a.begin + i;
   const float coef = s_coef;
   const float gv = a.grad[p] * coef;
@@ -1170,6 +1178,25 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
     const long o1 = p - a.w1_off[k];
     if (a.wsw[k] && o1 >= 0 && o1 < (long)a.H * a.OP) a.wsw[k][sw_index((int)(o1 / a.OP), (int)(o1 % a.OP), a.OP)] = np;
   }
+}
+
+__global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
+  __shared__ float s_norm[PPO_LAYOUT_MAX_TENSORS];
+  __shared__ float s_coef;
+  adam_block(a, blockIdx.x, s_norm, s_coef);
+}
+
+// k_gradnorm and k_adam as ONE cooperative launch: workgroups 0 .. nt * PPO_GN_SPLIT - 1 first run
+// the norm slices of k_gradnorm, a grid barrier makes the partials visible, then every workgroup
+// runs its k_adam block. Same functions, same partial order: bitwise the two-launch result, one
+// launch floor fewer per minibatch (320 minibatches per iteration at cfg1 / cfg2).
+__global__ __launch_bounds__(256) void k_gradstep(NormArgs na, AdamArgs a, unsigned* bar, unsigned target) {
+  __shared__ float red[4];
+  __shared__ float s_norm[PPO_LAYOUT_MAX_TENSORS];
+  __shared__ float s_coef;
+  if ((int)blockIdx.x < na.nt * PPO_GN_SPLIT) gradnorm_slice(na, blockIdx.x / PPO_GN_SPLIT, blockIdx.x % PPO_GN_SPLIT, red);
+  grid_barrier(bar, target);
+  adam_block(a, blockIdx.x, s_norm, s_coef);
 }
 
 // swizzled copies of one trunk (sw_index): [W1 (H x OP) | W2 (H x H) | W2^T (H x H)]
@@ -1606,23 +1633,23 @@ size_t dw_lds_bytes(int H, int OP) {
   return (size_t)2 * (KS * (H + 4) + KS * m) * sizeof(float);
 }
 
-template <int H, int OP>
+template <int H, int OP, int NSL>
 static int launch_dwf_t(const DwArgs& a, int nchunks, hipStream_t s) {
-  auto k = k_dwf<H, OP>;
+  auto k = k_dwf<H, OP, NSL>;
   constexpr size_t lds = (size_t)2 * (3 * 16 * (H + 4) + 16 * (OP + 4)) * sizeof(float);
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(nchunks, 2), dim3(512), lds, s, a);
+  hipLaunchKernelGGL(k, dim3(nchunks, 2, NSL), dim3(512), lds, s, a);
   return 0;
 }
 
 int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s) {
   if (H == 256 && a.fused) {  // a.fused = 0: the two-phase k_dw (PPO_DW_FUSED=0 at ppo_create)
-    if (OP == 16) return launch_dwf_t<256, 16>(a, nchunks, s);
-    if (OP == 32) return launch_dwf_t<256, 32>(a, nchunks, s);
+    if (OP == 16) return a.slices == 2 ? launch_dwf_t<256, 16, 2>(a, nchunks, s) : launch_dwf_t<256, 16, 1>(a, nchunks, s);
+    if (OP == 32) return a.slices == 2 ? launch_dwf_t<256, 32, 2>(a, nchunks, s) : launch_dwf_t<256, 32, 1>(a, nchunks, s);
   }
   const size_t lds = dw_lds_bytes(H, OP);
   if (H == 256 && OP == 16) return launch_dw_t<256, 16>(a, nchunks, lds, s);
@@ -1650,6 +1677,16 @@ void launch_colsum(const ColsumArgs& a_in, int nseg, long maxlen, hipStream_t s)
 }
 void launch_gradnorm(const NormArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_gradnorm, dim3(a.nt, PPO_GN_SPLIT), dim3(256), 0, s, a);
+}
+int launch_gradstep(const NormArgs& na, const AdamArgs& a, unsigned* bar, unsigned* count, hipStream_t s) {
+  const unsigned g = (unsigned)std::max<long>((a.n + 255) / 256, (long)na.nt * PPO_GN_SPLIT);
+  unsigned target = *count + g;
+  NormArgs n2 = na;
+  AdamArgs a2 = a;
+  void* args[] = {&n2, &a2, &bar, &target};
+  if (hipLaunchCooperativeKernel((const void*)k_gradstep, dim3(g), dim3(256), args, 0, s) != hipSuccess) return -2;
+  *count = target;
+  return 0;
 }
 void launch_adam(const AdamArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_adam, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);

@@ -94,7 +94,13 @@ struct DwArgs {
   int M;
   int rows_per_chunk;
   int fused;          // 1: k_dwf (dW2 and dW1 in one pass) where it applies; 0: two-phase k_dw
+  int slices;         // k_dwf: output-row slices per chunk (grid z); 2 halves the chunks, so the
+                      // split-K partials, for small minibatches (dw_slices)
 };
+// k_dwf output slices and dW row chunks for a minibatch of M rows: 128 chunks per trunk (one
+// workgroup per CU over both trunks); below 32 K rows 64 chunks x 2 output halves instead — the
+// same 256 workgroups, half the split-K partial bytes written by k_dwf and read back by k_colsum
+inline int dw_slices(int M, int H, int OP, bool fused) { return (fused && H == 256 && OP <= 32 && M <= 32768) ? 2 : 1; }
 
 struct ColsumSeg {
   const float* src;
@@ -238,6 +244,25 @@ int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s);
 size_t dw_lds_bytes(int H, int OP);
 void launch_colsum(const ColsumArgs& a, int nseg, long maxlen, hipStream_t s);
 void launch_gradnorm(const NormArgs& a, hipStream_t s);
+// k_gradnorm + k_adam in one cooperative launch (grid barrier on *bar; *count: its arrivals so far)
+int launch_gradstep(const NormArgs& na, const AdamArgs& a, unsigned* bar, unsigned* count, hipStream_t s);
+
+// Grid-wide barrier of a cooperative launch (every workgroup resident): all stores before it are
+// visible to every workgroup after it. bar counts arrivals monotonically across launches; target =
+// its value once every workgroup of this barrier has arrived.
+// __syncthreads orders the workgroup's stores before thread 0's agent-scope release (which writes the
+// XCD's L2 back for the other XCDs); thread 0's acquire invalidates the CU's caches for the loads
+// every thread issues after the second __syncthreads. (A fence in every thread instead costs an L2
+// write-back per wave.)
+PPO_DEV void grid_barrier(unsigned* bar, unsigned target) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    while ((int)(__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - target) < 0)
+      __builtin_amdgcn_s_sleep(2);
+  }
+  __syncthreads();
+}
 void launch_adam(const AdamArgs& a, hipStream_t s);
 void launch_transpose(const float* src, float* dst, int H, hipStream_t s);
 void launch_swizzle(const float* w1, const float* w2, float* dst, int H, int OP, hipStream_t s);

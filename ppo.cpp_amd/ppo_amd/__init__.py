@@ -649,15 +649,18 @@ class CarlaAgent:
         check(lib().ppo_carla_load_params(self._h, flat.ctypes.data_as(C.c_void_p), flat.size))
 
     def forward(self, bev: DeviceArray, meas: DeviceArray, vmeas: DeviceArray, actions: DeviceArray | None = None,
-                sample_type="sample", env_base=0, step_id=0):
+                sample_type="sample", env_base=0, step_id=0, out=None, sync=True):
+        """(action, logprob, entropy, value, alpha, beta); out: preallocated arrays of those shapes."""
         n, A = bev.shape[0], self.layout.A
         mode = PPO_CARLA_GIVEN if actions is not None else self._MODES[sample_type]
-        out = [DeviceArray((n, A)), DeviceArray((n,)), DeviceArray((n,)), DeviceArray((n,)), DeviceArray((n, A)),
-               DeviceArray((n, A))]
+        if out is None:
+            out = [DeviceArray((n, A)), DeviceArray((n,)), DeviceArray((n,)), DeviceArray((n,)), DeviceArray((n, A)),
+                   DeviceArray((n, A))]
         check(lib().ppo_carla_forward(self._h, n, bev.ptr, meas.ptr, vmeas.ptr, mode,
                                       actions.ptr if actions is not None else None, env_base, step_id,
                                       *[o.ptr for o in out], None))
-        check(lib().ppo_device_sync())
+        if sync:
+            check(lib().ppo_device_sync())
         return tuple(out)
 
     def update(self, bev: DeviceArray, meas: DeviceArray, vmeas: DeviceArray, actions: DeviceArray,

@@ -26,24 +26,34 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[32, 256])
     ap.add_argument("--update-batch", type=int, nargs="*", default=[256, 2048])
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--options", default="", help="ppo_carla_create_ex options, e.g. tail=layers")
     args = ap.parse_args()
     ppo_amd.set_device(0)
     L = CI.layout()
     p = CI.params(L)
     for n in args.batch:
-        ag = ppo_amd.CarlaAgent(max_batch=n)
+        ag = ppo_amd.CarlaAgent(max_batch=n, options=args.options or None)
         ag.load_params(p)
         bev, meas, vmeas, _ = CI.inputs(n)
         d = [ppo_amd.DeviceArray.from_numpy(bev, np.uint8), ppo_amd.DeviceArray.from_numpy(meas),
              ppo_amd.DeviceArray.from_numpy(vmeas)]
+        A = ag.layout.A
+        out = [ppo_amd.DeviceArray(sh) for sh in ((n, A), (n,), (n,), (n,), (n, A), (n, A))]
         for _ in range(3):
-            ag.forward(*d, sample_type="sample")
+            ag.forward(*d, sample_type="sample", out=out)
+        # rollout pattern: one forward, then wait for its actions (output buffers preallocated)
         t0 = time.perf_counter()
         for i in range(args.iters):
-            ag.forward(*d, sample_type="sample", step_id=i)
+            ag.forward(*d, sample_type="sample", step_id=i, out=out)
         dt = (time.perf_counter() - t0) / args.iters
-        print(json.dumps({"workload": "carla_forward", "batch": n, "ms_per_forward": round(dt * 1e3, 3),
-                          "samples_per_s": round(n / dt, 1),
+        # device time: forwards back to back, one wait at the end
+        t0 = time.perf_counter()
+        for i in range(args.iters):
+            ag.forward(*d, sample_type="sample", step_id=i, out=out, sync=False)
+        ppo_amd.lib().ppo_device_sync()
+        dd = (time.perf_counter() - t0) / args.iters
+        print(json.dumps({"workload": "carla_forward", "batch": n, "options": args.options, "ms_per_forward": round(dt * 1e3, 3),
+                          "ms_per_forward_back_to_back": round(dd * 1e3, 3), "samples_per_s": round(n / dt, 1),
                           "tflops": round(n * FLOP_PER_SAMPLE / dt / 1e12, 2)}), flush=True)
         ag.close()
     for n in args.update_batch:

@@ -11,7 +11,11 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 tail -2 $OUT/tests.txt
 timeout -k 10 300 python3 scripts/bench_carla.py > $OUT/carla.jsonl 2>&1 || { echo "bench failed"; tail -20 $OUT/carla.jsonl; exit 1; }
 grep -v amdgpu.ids $OUT/carla.jsonl
+for o in tail=layers tail=staged tail=fused; do
+  timeout -k 10 120 python3 scripts/bench_carla.py --batch 32 --update-batch --iters 50 --options $o 2>&1 | grep workload || { echo "bench $o failed"; exit 1; }
+done
+# per-kernel trace of the per-layer path (the cooperative launch is not traced here)
 export TMPDIR=/tmp
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- \
-  python3 $R/scripts/bench_carla.py --batch 32 --update-batch --iters 50 > $OUT/kt.log 2>&1 || { echo "trace failed"; tail -20 $OUT/kt.log; exit 1; }
+  python3 $R/scripts/bench_carla.py --batch 32 --update-batch --iters 50 --options tail=staged > $OUT/kt.log 2>&1 || { echo "trace failed"; tail -20 $OUT/kt.log; exit 1; }
 find $OUT/kt -name "*kernel_stats.csv" | head -1 | xargs -I{} cut -d, -f1-4 {} | head -20

@@ -18,5 +18,11 @@ timeout -k 10 300 python scripts/bench_configs.py > $OUT/configs.jsonl 2>&1 || {
 timeout -k 10 300 python scripts/bench_carla.py > $OUT/carla.jsonl 2>&1 || { echo "carla failed"; exit 1; }
 timeout -k 10 120 python bench.py --num-envs 512 --steps 20 --warmup 3 --profile-all --no-cpu-baseline --no-cli > $OUT/bench_e512.log 2>&1 || { echo "e512 failed"; exit 1; }
 timeout -k 10 120 python bench.py --num-envs 1024 --steps 20 --warmup 3 --profile-all --no-cpu-baseline --no-cli > $OUT/bench_e1024.log 2>&1 || { echo "e1024 failed"; exit 1; }
+# kernel traces of the N = 8 / N = 4 shards (E = 512 / 1 024) for the strong-scaling projection
+export TMPDIR=/tmp
+for E in 512 1024; do
+  (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/scale_e$E -o kt -- \
+    python3 $R/bench.py --num-envs $E --steps 10 --warmup 2 --no-cpu-baseline --no-cli > $OUT/scale_e$E.log 2>&1) || { echo "trace E=$E failed"; exit 1; }
+done
 cut -c1-300 $OUT/configs.jsonl; tail -1 $OUT/bench_e512.log | cut -c1-300
 echo final-done

@@ -144,3 +144,35 @@ def test_unaligned_image_pointer(carla):
     out = ag.forward(shifted, DeviceArray.from_numpy(meas), DeviceArray.from_numpy(vmeas), sample_type="mean")
     for r, o in zip(ref, out):
         np.testing.assert_array_equal(o.numpy(), r)
+
+
+@pytest.mark.parametrize("n", [7, 16, 32])
+def test_fused_tail_matches_layer_kernels(n):
+    """Rollout-sized batches (n <= 64) run the MLP tail after the CNN — state MLP, linear, value and
+    policy heads, the Beta head — as k_carla_tail: one cooperative launch with a grid barrier between
+    dependency stages ("tail=fused", the default), or one launch per stage ("tail=staged"). Each
+    Linear work item repeats k_conv's MFMA chains over the same 128-wide k chunks and adds the chunk
+    partials in k_conv_fin's order, so every output (and the update's forward activations) equals the
+    per-layer kernels' ("tail=layers") bit for bit, in every sampling mode."""
+    L = CI.layout()
+    p = CI.params(L)
+    bev, meas, vmeas, act = CI.inputs(n)
+    outs = {}
+    for opt in ("tail=layers", "tail=fused", "tail=staged"):
+        ag = ppo_amd.CarlaAgent(max_batch=64, seed=7, options=opt)
+        ag.load_params(p)
+        res = [run(ag, bev, meas, vmeas, mode=m, env_base=3, step_id=5) for m in ("sample", "mean", "roach")]
+        res.append(run(ag, bev, meas, vmeas, act))
+        if n <= 16:
+            rng = np.random.default_rng(5)
+            extra = [rng.normal(-2.0, 0.3, n), rng.normal(0.0, 1.0, n), rng.normal(0.0, 1.0, n), rng.normal(0.0, 1.0, n)]
+            d = [DeviceArray.from_numpy(bev, np.uint8)] + [DeviceArray.from_numpy(np.ascontiguousarray(x, np.float32))
+                                                           for x in [meas, vmeas, act] + extra]
+            ag.update(*d, lr=3e-4, clip_coef=0.2, ent_coef=0.01, vf_coef=0.5, max_grad_norm=0.5, adam_eps=1e-5)
+            res.append([ag.last_grad(), ag.params()])
+        outs[opt] = res
+        ag.close()
+    for opt in ("tail=fused", "tail=staged"):
+        for r0, r1 in zip(outs["tail=layers"], outs[opt]):
+            for x0, x1 in zip(r0, r1):
+                np.testing.assert_array_equal(x1, x0)

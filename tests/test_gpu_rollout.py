@@ -82,3 +82,27 @@ def test_persistent_rollout_metric_shape_properties():
     s = res[0]
     assert np.isfinite(s["values"]).all() and np.isfinite(s["logp"]).all()
     assert np.abs(s["actions"]).max() <= 1.0
+
+
+@pytest.mark.parametrize("agent,env_id,E,T,mb", [("ac", "HalfCheetah-v5", 256, 128, 4), ("ppo", "Humanoid-v4", 64, 64, 32),
+                                                 ("ppo", "HalfCheetah-v5", 1, 256, 4)])
+def test_gradstep_fused_equals_split(agent, env_id, E, T, mb):
+    """clip_grad_norm_ + Adam as one cooperative launch (k_gradstep: the norm slices, a grid barrier,
+    the Adam blocks; the default) against the two launches k_gradnorm + k_adam (gradstep=split):
+    the same functions in the same order, so parameters, Adam moments and the per-minibatch total
+    norm are bitwise equal after two iterations (many minibatches: the barrier counter runs across
+    launches)."""
+    C = ppo_amd.ACPPOConfig if agent == "ac" else ppo_amd.PPOConfig
+    cfg = C(env_id=env_id, num_envs=E, num_steps=T, num_minibatches=mb, update_epochs=2, total_timesteps=E * T * 4)
+    trs = [ppo_amd.Trainer(cfg), ppo_amd.Trainer(cfg, options="gradstep=split")]
+    for _ in range(2):
+        st = [tr.iterate(want_stats=True) for tr in trs]
+    np.testing.assert_array_equal(trs[0].agent.params(), trs[1].agent.params())
+    m0, v0, s0 = trs[0].agent.adam_state()
+    m1, v1, s1 = trs[1].agent.adam_state()
+    np.testing.assert_array_equal(m0, m1)
+    np.testing.assert_array_equal(v0, v1)
+    assert s0 == s1
+    assert st[0]["grad_norm"] == st[1]["grad_norm"]
+    for tr in trs:
+        tr.close()

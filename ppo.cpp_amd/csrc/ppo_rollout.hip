@@ -107,7 +107,8 @@ PPO_DEV void stage_params(const PackedLayout& K, const TrunkDev& T, PBuf pb, int
 // k_act3 (LN_BETA, RT = 1).
 template <int NTO, int NHT, typename PRE_L2 = int>
 PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* lds, int nh, int tid,
-                        PRE_L2 pre_l2 = 0) {
+                        PRE_L2 pre_l2 = 0, int stamp_t = -1) {
+  (void)stamp_t;  // ROLL_STAMP step index (stamps build; -1: none)
   using GE = RollGeo<NTO, NHT>;
   constexpr int H = 256, LDX = GE::LDX, LDH = GE::LDH, LDP = GE::LDP, NHP = GE::NHP, R = kRows;
   float* XS = lds + GE::oXS;
@@ -127,6 +128,7 @@ PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* ld
 #pragma unroll
   for (int u = 0; u < 2; ++u) *reinterpret_cast<f4*>(HB + j * LDH + 32 * wave + 16 * u + 4 * g) = acc[u][0];
   lds_barrier();
+  if (stamp_t >= 0) ROLL_STAMP(stamp_t, 5);
 #pragma unroll
   for (int u = 0; u < 2; ++u) acc[u][0] = *reinterpret_cast<const f4*>(SP + GE::sB2 + 32 * wave + 16 * u + 4 * g);
   const float* hin = HB + j * LDH + 4 * g;
@@ -134,7 +136,14 @@ PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* ld
   // whose issue leaves the SIMD's vector pipe mostly free
   if constexpr (!std::is_same_v<PRE_L2, int>) pre_l2();
   act_layer_regs<16, 1>(acc, w2, [&](int t, int) { return *reinterpret_cast<const f4*>(hin + 16 * t); });
+  if (stamp_t >= 0) {
+#ifdef PPO_STAMPS
+    asm volatile("s_nop 0" ::"v"(acc[0][0].x), "v"(acc[1][0].x));  // the layer-2 results exist here
+#endif
+    ROLL_STAMP(stamp_t, 6);
+  }
   act_activate<PPO_NET_LN_BETA, 1>(acc, SP + GE::sG2, SP + GE::sBE2, RED, wave, j, g);
+  if (stamp_t >= 0) ROLL_STAMP(stamp_t, 7);
 #pragma unroll
   for (int ht = 0; ht < NHT; ++ht) {
     f4 hp = f4{0.f, 0.f, 0.f, 0.f};
@@ -251,8 +260,8 @@ __global__ __launch_bounds__(512) void k_rollout(RolloutArgs a) {
     }
     if (tid < R && row0 + tid < E) a.s_dones[(long)t * E + row0 + tid] = EV[EV_DONE * R + tid];
     lds_barrier();
-    // the first Marsaglia-Tsang attempt's draws of this thread's item (idx = tid) do not depend on
-    // the network: computed inside layer 2, under its MFMAs (k_act3 computes them under its weight
+    // the first Marsaglia-Tsang attempt's draws of this thread's item (bitem) do not depend on the
+    // network: computed inside layer 2, under its MFMAs (k_act3 computes them under its weight
     // fetch; gamma_mt_d0 with them is gamma_mt, bitwise)
     GammaDraw gd0 = GammaDraw{0.f, 0.f};
     ROLL_STAMP(t, 1);
@@ -262,7 +271,7 @@ __global__ __launch_bounds__(512) void k_rollout(RolloutArgs a) {
         const uint32_t db = 0x10000u + (uint32_t)(ai * 2 + which) * 64u;
         gd0 = gamma_draw(key, (long)(row0 + r), step_id, db);
       }
-    });
+    }, (int)t);
     // ---- Beta sample (k_act3 stage 1 / 2, PPO_SAMPLE); the log-prob terms either here (as k_act3)
     // or, with a.s_beta, stored for k_beta_logp after the rollout (they are not on the env's path) ----
     const bool defer = a.s_beta != nullptr;

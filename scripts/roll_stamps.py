@@ -2,7 +2,8 @@
 """Phase timing of the persistent rollout kernels (diagnostic stamps build, ROLL_STAMP in
 csrc/ppo_rollout.hip): runs one rollout per config with libppo_hip_stamps.so and prints the mean
 shader-clock cycles per phase over steps 1..15 of workgroup 0:
-  k_rollout  (AC):  0 inputs | 1 trunk (L1, LN, L2, LN, heads) | 2 Beta sample / actions | 3 env step
+  k_rollout  (AC):  0 inputs | 1 trunk (L1, LN, L2, LN, heads; split into sub-phases) | 2 Beta sample /
+                    actions | 3 env step
   k_rollout4 (PPO): 0 inputs + draws | 1 trunk (L1, L2) | 2 heads + actions + log-probs | 3 env + wrappers"""
 import ctypes as C
 import os
@@ -21,8 +22,13 @@ def run(name, cfg):
     tr.agent.sync()
     buf = (C.c_ulonglong * 128)()
     n = ppo_amd.lib().ppo_diag_read_roll_stamps(buf, 128)
-    st = np.array(buf[:n], np.int64).reshape(16, 8)[1:, :5]
+    full = np.array(buf[:n], np.int64).reshape(16, 8)[1:]
+    st = full[:, :5]
     d = np.diff(st, axis=1).mean(0)
+    if name.startswith("ac"):  # k_rollout's trunk: L1 + LayerNorm 1 | layer-2 MFMAs | LayerNorm 2 | heads
+        sub = np.stack([full[:, 5] - full[:, 1], full[:, 6] - full[:, 5], full[:, 7] - full[:, 6],
+                        full[:, 2] - full[:, 7]], 1).mean(0)
+        print(name, "trunk sub-phases [L1+LN1, L2 mm, LN2, heads]", np.round(sub, 1).tolist(), flush=True)
     # s_memtime counts shader clock cycles (22 K per AC step at E = 512 = 9.3 us at 2.4 GHz)
     print(name, "E", cfg.num_envs, "per-step cycles", st[:, 4].mean() - st[:, 0].mean(),
           "phases", np.round(d, 1).tolist(), flush=True)

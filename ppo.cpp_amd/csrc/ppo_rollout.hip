@@ -476,16 +476,33 @@ __global__ __launch_bounds__(512) void k_values(ValuesArgs a) {
     NRM[OP + f] = f < O ? P[K.ostd + f] : 1.0f;
   }
   const long nblk = (a.n + R - 1) / R;
+  // the block's observations (R x OP <= 16 x 112: at most 4 per thread) are loaded one block ahead,
+  // under the previous block's layers
+  constexpr int NXI = (R * OP + kActThreads - 1) / kActThreads;
+  float xnext[NXI];
+  auto load_obs = [&](long b) {
+#pragma unroll
+    for (int u = 0; u < NXI; ++u) {
+      const int idx = tid + kActThreads * u, r = idx / OP, f = idx - r * OP;
+      const long row = b * R + r;
+      const bool valid = b < nblk && idx < R * OP && row < a.n && f < O;
+      const float x = a.obs[(valid ? row : 0) * O + (valid ? f : 0)];
+      xnext[u] = valid ? x : 0.0f;
+    }
+  };
+  load_obs(blockIdx.x);
   for (long b = blockIdx.x; b < nblk; b += gridDim.x) {
     const long row0 = b * R;
     lds_barrier();  // previous block's PRE reads done; NRM / SP staged (first pass)
-    for (int idx = tid; idx < R * OP; idx += kActThreads) {
-      const int r = idx / OP, f = idx - r * OP;
+#pragma unroll
+    for (int u = 0; u < NXI; ++u) {
+      const int idx = tid + kActThreads * u, r = idx / OP, f = idx - r * OP;
       const long row = row0 + r;
       const bool valid = row < a.n && f < O;
-      const float x = valid ? a.obs[row * O + f] : 0.0f;
-      XS[r * LDX + f] = valid ? (x - NRM[f]) / NRM[OP + f] : x;
+      const float x = xnext[u];
+      if (idx < R * OP) XS[r * LDX + f] = valid ? (x - NRM[f]) / NRM[OP + f] : x;
     }
+    load_obs(b + gridDim.x);
     lds_barrier();
     trunk_rows<NTO, NHT>(w1, w2, lds, 1, tid);
     if (tid < R && row0 + tid < a.n) a.values[row0 + tid] = PRE[tid * LDP];
@@ -921,19 +938,28 @@ __global__ __launch_bounds__(256) void k_values4(ValuesArgs a) {
   const f4 hv = pld4(pb, K.cW3 + 16 * ks + 4 * g, 0);
   const float c_b3 = P[K.cb3];
   const long nblk = (a.n + R - 1) / R;
-  for (long b = blockIdx.x; b < nblk; b += gridDim.x) {
-    const long row0 = b * R, row = row0 + j, rowc = row < a.n ? row : a.n - 1;
-    f4 xv[NKW];
+  // this lane's inputs of a block (k_act4's xv), loaded one block ahead under the previous block's layers
+  f4 xnext[NKW];
+  auto load_xv = [&](long b) {
+    const long row = b * R + j, rowc = row < a.n ? row : a.n - 1;
 #pragma unroll
     for (int q = 0; q < NKW; ++q) {
       const int kb = kb0 + q;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int col = 16 * kb + 4 * g + c;
-        const float v = a.obs[rowc * O + min(col, O - 1)];
-        xv[q][c] = (kb < NTO && col < O && row < a.n) ? v : 0.f;
+        const float v = a.obs[(b < nblk ? rowc : 0) * O + min(col, O - 1)];
+        xnext[q][c] = (b < nblk && kb < NTO && col < O && row < a.n) ? v : 0.f;
       }
     }
+  };
+  load_xv(blockIdx.x);
+  for (long b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const long row0 = b * R;
+    f4 xv[NKW];
+#pragma unroll
+    for (int q = 0; q < NKW; ++q) xv[q] = xnext[q];
+    load_xv(b + gridDim.x);
     __syncthreads();  // the previous block's VP / P1 / H1 readers are done
     const f4 h2 = trunk4<NTO, NKW>(xv, wa, w2v, b1, b2, P1, H1, ks, j, g, [] {});
     float p = (hv.x * h2.x + hv.y * h2.y) + (hv.z * h2.z + hv.w * h2.w);

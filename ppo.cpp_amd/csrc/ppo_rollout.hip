@@ -44,8 +44,9 @@ namespace {
 
 constexpr int kRows = 16;  // envs (rows) per workgroup
 
-template <int NTO, int NHT>
+template <int NTO, int NHT, int ROWS = kRows>
 struct RollGeo {
+  static constexpr int kRows = ROWS;  // rows per pass (16: the rollout's env block; 32: k_values)
   static constexpr int H = 256, OP = NTO * 16, NHP = 16 * NHT;
   static constexpr int LDX = ((OP + 63) / 64) * 64 + 4;
   static constexpr int LDH = H + 4;
@@ -105,12 +106,12 @@ PPO_DEV void stage_params(const PackedLayout& K, const TrunkDev& T, PBuf pb, int
 // LayerNorm + ReLU, layer 2, LayerNorm + ReLU, heads; leaves the head pre-activations (+ bias) in
 // PRE [16][LDP]. Weights: w1 / w2 register slices of this wave. Same operations, same order as
 // k_act3 (LN_BETA, RT = 1).
-template <int NTO, int NHT, typename PRE_L2 = int>
+template <int NTO, int NHT, int RT = 1, typename PRE_L2 = int>
 PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* lds, int nh, int tid,
                         PRE_L2 pre_l2 = 0, int stamp_t = -1) {
   (void)stamp_t;  // ROLL_STAMP step index (stamps build; -1: none)
-  using GE = RollGeo<NTO, NHT>;
-  constexpr int H = 256, LDX = GE::LDX, LDH = GE::LDH, LDP = GE::LDP, NHP = GE::NHP, R = kRows;
+  using GE = RollGeo<NTO, NHT, 16 * RT>;
+  constexpr int H = 256, LDX = GE::LDX, LDH = GE::LDH, LDP = GE::LDP, NHP = GE::NHP, R = 16 * RT;
   float* XS = lds + GE::oXS;
   float* HB = lds + GE::oHB;
   float* SP = lds + GE::oSP;
@@ -119,44 +120,58 @@ PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* ld
   float* HP = lds + GE::oHP;
   float* PRE = lds + GE::oPRE;
   const int lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
-  f4 acc[2][1];
+  f4 acc[2][RT];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) acc[u][0] = *reinterpret_cast<const f4*>(SP + GE::sB1 + 32 * wave + 16 * u + 4 * g);
+  for (int u = 0; u < 2; ++u) {
+    const f4 b1 = *reinterpret_cast<const f4*>(SP + GE::sB1 + 32 * wave + 16 * u + 4 * g);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[u][rt] = b1;
+  }
   const float* xin = XS + j * LDX + 4 * g;
-  act_layer_regs<NTO, 1>(acc, w1, [&](int t, int) { return *reinterpret_cast<const f4*>(xin + 16 * t); });
-  act_activate<PPO_NET_LN_BETA, 1>(acc, SP + GE::sG1, SP + GE::sBE1, RED, wave, j, g);
+  act_layer_regs<NTO, RT>(acc, w1, [&](int t, int rt) { return *reinterpret_cast<const f4*>(xin + 16 * rt * LDX + 16 * t); });
+  act_activate<PPO_NET_LN_BETA, RT>(acc, SP + GE::sG1, SP + GE::sBE1, RED, wave, j, g);
 #pragma unroll
-  for (int u = 0; u < 2; ++u) *reinterpret_cast<f4*>(HB + j * LDH + 32 * wave + 16 * u + 4 * g) = acc[u][0];
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+      *reinterpret_cast<f4*>(HB + (16 * rt + j) * LDH + 32 * wave + 16 * u + 4 * g) = acc[u][rt];
   lds_barrier();
   if (stamp_t >= 0) ROLL_STAMP(stamp_t, 5);
 #pragma unroll
-  for (int u = 0; u < 2; ++u) acc[u][0] = *reinterpret_cast<const f4*>(SP + GE::sB2 + 32 * wave + 16 * u + 4 * g);
+  for (int u = 0; u < 2; ++u) {
+    const f4 b2 = *reinterpret_cast<const f4*>(SP + GE::sB2 + 32 * wave + 16 * u + 4 * g);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[u][rt] = b2;
+  }
   const float* hin = HB + j * LDH + 4 * g;
   // independent VALU work placed in the layer-2 block: the scheduler interleaves it with the MFMAs,
   // whose issue leaves the SIMD's vector pipe mostly free
   if constexpr (!std::is_same_v<PRE_L2, int>) pre_l2();
-  act_layer_regs<16, 1>(acc, w2, [&](int t, int) { return *reinterpret_cast<const f4*>(hin + 16 * t); });
+  act_layer_regs<16, RT>(acc, w2, [&](int t, int rt) { return *reinterpret_cast<const f4*>(hin + 16 * rt * LDH + 16 * t); });
   if (stamp_t >= 0) {
 #ifdef PPO_STAMPS
     asm volatile("s_nop 0" ::"v"(acc[0][0].x), "v"(acc[1][0].x));  // the layer-2 results exist here
 #endif
     ROLL_STAMP(stamp_t, 6);
   }
-  act_activate<PPO_NET_LN_BETA, 1>(acc, SP + GE::sG2, SP + GE::sBE2, RED, wave, j, g);
+  act_activate<PPO_NET_LN_BETA, RT>(acc, SP + GE::sG2, SP + GE::sBE2, RED, wave, j, g);
   if (stamp_t >= 0) ROLL_STAMP(stamp_t, 7);
 #pragma unroll
   for (int ht = 0; ht < NHT; ++ht) {
-    f4 hp = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const f4 wv = *reinterpret_cast<const f4*>(SP + GE::sW3 + (16 * ht + j) * H + 32 * wave + 16 * u + 4 * g);
-      hp = mfma16(wv.x, acc[u][0].x, hp);
-      hp = mfma16(wv.y, acc[u][0].y, hp);
-      hp = mfma16(wv.z, acc[u][0].z, hp);
-      hp = mfma16(wv.w, acc[u][0].w, hp);
+    for (int rt = 0; rt < RT; ++rt) {
+      f4 hp = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const f4 wv = *reinterpret_cast<const f4*>(SP + GE::sW3 + (16 * ht + j) * H + 32 * wave + 16 * u + 4 * g);
+        hp = mfma16(wv.x, acc[u][rt].x, hp);
+        hp = mfma16(wv.y, acc[u][rt].y, hp);
+        hp = mfma16(wv.z, acc[u][rt].z, hp);
+        hp = mfma16(wv.w, acc[u][rt].w, hp);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) HP[(wave * NHP + 16 * ht + 4 * g + r) * R + 16 * rt + j] = hp[r];
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) HP[(wave * NHP + 16 * ht + 4 * g + r) * R + j] = hp[r];
   }
   lds_barrier();
   for (int idx = tid; idx < R * nh; idx += kActThreads) {
@@ -455,10 +470,12 @@ int launch_beta_logp(const float* s_beta, float* logp, long n, int A, hipStream_
 // =============================================================================================
 // k_values: critic(obs[i]) for n stored rows; workgroups walk 16-row blocks
 // =============================================================================================
+// 32 rows per pass (two 16-row MFMA tiles per wave): the LayerNorm exchanges and barriers of a pass
+// are shared by twice the rows; every row's arithmetic is the 16-row pass's (bitwise)
 template <int NTO, int NHT>
 __global__ __launch_bounds__(512) void k_values(ValuesArgs a) {
-  using GE = RollGeo<NTO, NHT>;
-  constexpr int OP = GE::OP, LDX = GE::LDX, LDP = GE::LDP, R = kRows;
+  using GE = RollGeo<NTO, NHT, 32>;
+  constexpr int OP = GE::OP, LDX = GE::LDX, LDP = GE::LDP, R = 32;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* XS = lds + GE::oXS;
   float* PRE = lds + GE::oPRE;
@@ -504,7 +521,7 @@ __global__ __launch_bounds__(512) void k_values(ValuesArgs a) {
     }
     load_obs(b + gridDim.x);
     lds_barrier();
-    trunk_rows<NTO, NHT>(w1, w2, lds, 1, tid);
+    trunk_rows<NTO, NHT, 2>(w1, w2, lds, 1, tid);
     if (tid < R && row0 + tid < a.n) a.values[row0 + tid] = PRE[tid * LDP];
   }
 }
@@ -938,28 +955,19 @@ __global__ __launch_bounds__(256) void k_values4(ValuesArgs a) {
   const f4 hv = pld4(pb, K.cW3 + 16 * ks + 4 * g, 0);
   const float c_b3 = P[K.cb3];
   const long nblk = (a.n + R - 1) / R;
-  // this lane's inputs of a block (k_act4's xv), loaded one block ahead under the previous block's layers
-  f4 xnext[NKW];
-  auto load_xv = [&](long b) {
-    const long row = b * R + j, rowc = row < a.n ? row : a.n - 1;
+  for (long b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const long row0 = b * R, row = row0 + j, rowc = row < a.n ? row : a.n - 1;
+    f4 xv[NKW];
 #pragma unroll
     for (int q = 0; q < NKW; ++q) {
       const int kb = kb0 + q;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int col = 16 * kb + 4 * g + c;
-        const float v = a.obs[(b < nblk ? rowc : 0) * O + min(col, O - 1)];
-        xnext[q][c] = (b < nblk && kb < NTO && col < O && row < a.n) ? v : 0.f;
+        const float v = a.obs[rowc * O + min(col, O - 1)];
+        xv[q][c] = (kb < NTO && col < O && row < a.n) ? v : 0.f;
       }
     }
-  };
-  load_xv(blockIdx.x);
-  for (long b = blockIdx.x; b < nblk; b += gridDim.x) {
-    const long row0 = b * R;
-    f4 xv[NKW];
-#pragma unroll
-    for (int q = 0; q < NKW; ++q) xv[q] = xnext[q];
-    load_xv(b + gridDim.x);
     __syncthreads();  // the previous block's VP / P1 / H1 readers are done
     const f4 h2 = trunk4<NTO, NKW>(xv, wa, w2v, b1, b2, P1, H1, ks, j, g, [] {});
     float p = (hv.x * h2.x + hv.y * h2.y) + (hv.z * h2.z + hv.w * h2.w);
@@ -1039,12 +1047,12 @@ int launch_rollout(const RolloutArgs& a, hipStream_t s) {
 
 template <int NTO, int NHT>
 static int launch_values_t(const ValuesArgs& a, hipStream_t s) {
-  using GE = RollGeo<NTO, NHT>;
+  using GE = RollGeo<NTO, NHT, 32>;
   const size_t lds = (size_t)GE::total * sizeof(float);
   static const bool ok = hipFuncSetAttribute((const void*)k_values<NTO, NHT>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
   if (!ok) return -2;
-  const long nblk = (a.n + kRows - 1) / kRows;
+  const long nblk = (a.n + 31) / 32;
   int dev = 0, ncu = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);

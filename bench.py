@@ -189,6 +189,9 @@ def main():
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                     help="N > 1 data path: RCCL (one GPU per rank), or the host transport over gloo with every "
                          "rank on GPU 0 (rehearses this script's multi-rank path on a one-GPU box)")
+    ap.add_argument("--comm-1rank", action="store_true",
+                    help="N = 1 only: attach a one-rank RCCL communicator, so the distributed update sequence "
+                         "(split gradient all-reduce on its side stream) runs and its cost can be timed")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -228,6 +231,8 @@ def main():
             dist.broadcast_object_list(uid, src=0)
             tr.agent.comm_init(uid[0], rank, world)
         tr.agent.comm_broadcast_params(0)
+    if world == 1 and args.comm_1rank:
+        tr.agent.comm_init(ppo_amd.Agent.comm_unique_id(), 0, 1)
     comm_kind, _, comm_world = tr.agent.comm_info()
     if world > 1 and comm_world != world:
         raise SystemExit(f"bench.py: the {comm_kind} communicator reports {comm_world} ranks, expected {world}")

@@ -170,10 +170,6 @@ struct ppo_ctx {
   long adam_step = 0;
   long iteration = 0;
   ncclComm_t comm = nullptr;
-  // overlapped gradient all-reduce (ppo_update with a communicator): the critic's share is reduced
-  // on ar_stream while the actor's dW and column sums run on the context stream
-  hipStream_t ar_stream = nullptr;
-  hipEvent_t ar_ev[3] = {nullptr, nullptr, nullptr};
   ppo_host_allreduce_fn host_ar = nullptr;  // host transport (ppo_comm_init_host)
   void* host_user = nullptr;
   std::vector<float> host_stage;
@@ -455,9 +451,6 @@ extern "C" int ppo_destroy(ppo_t* c) {
   if (c->advpart) (void)hipFree(c->advpart);
   comm_detach(c);
   if (c->snap) (void)hipFree(c->snap);
-  for (hipEvent_t& e : c->ar_ev)
-    if (e) (void)hipEventDestroy(e);
-  if (c->ar_stream) (void)hipStreamDestroy(c->ar_stream);
   if (c->snap_ev) (void)hipEventDestroy(c->snap_ev);
   if (c->snap_stream) (void)hipStreamDestroy(c->snap_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -815,9 +808,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
     maxlen = std::max(maxlen, (long)len);
   };
   const bool ln = cfg.net_kind == PPO_NET_LN_BETA;
-  int ns_critic = 0;  // segments [0, ns_critic) write the critic's gradient only
   for (int k = 0; k < 2; ++k) {
-    if (k == 1) ns_critic = ns;
     const TrunkDev& T = c->K.tr[k];
     seg(c->dwslab[k], dw.slab_stride, c->nchunks, H * H, c->G + T.W2, 1.f);
     seg(c->dwslab[k] + (long)H * H, dw.slab_stride, c->nchunks, H * OP, c->G + T.W1, 1.f);
@@ -884,32 +875,6 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
     ad.wsw[k] = c->WSW[k];
   }
   const long trainable_n = c->K.size - tb;
-  // With a communicator (and the per-trunk dW kernels) the gradient all-reduce is split by trunk so
-  // that the critic's share (packed [critic W1, actor W1): critic.* tensors, reference order) is
-  // reduced on ar_stream under the actor's dW GEMM and column sums; the actor's share (actor_mean.* /
-  // dist_* and, for the tanh agent, actor_logstd in front of the critic) follows. Each element is
-  // reduced by exactly one call, so the result equals the single call's (ac:877-885: one average of
-  // every gradient before the clip).
-  const bool overlap = multi && !c->use_upd2;
-  const long crit0 = c->K.tr[0].W1, crit1 = c->K.tr[1].W1;
-  if (overlap) {
-    if (!(tb <= crit0 && crit0 < crit1 && crit1 < c->K.size))
-      return fail("ppo_update: unexpected packed layout for the split all-reduce");
-    if (!c->ar_stream) {
-      HIP_TRY(hipStreamCreateWithFlags(&c->ar_stream, hipStreamNonBlocking));
-      for (hipEvent_t& e : c->ar_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-  }
-  auto colsum_range = [&](int i0, int i1) {
-    ColsumArgs part;
-    memset(&part, 0, sizeof(part));
-    long ml = 0;
-    for (int i = i0; i < i1; ++i) {
-      part.seg[i - i0] = cs.seg[i];
-      ml = std::max(ml, (long)cs.seg[i].len);
-    }
-    launch_colsum(part, i1 - i0, ml, s);
-  };
 
   for (int e = 0; e < EP; ++e) {
     for (int mb = 0; mb < MB; ++mb) {
@@ -924,42 +889,20 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
                                      : launch_fwdbwd(u, nblk, c->lds_bytes, s);
         if (rc_ != 0) return fail("no update kernel for this configuration");
       }
+      {
+        ProfScope ps(c, PK_DW2, s);
+        const int rc_ = c->use_upd2 ? launch_dw2(dw, OP, c->nchunks, s) : launch_dw(dw, H, OP, c->nchunks, s);
+        if (rc_ != 0) return fail("no dW kernel for this configuration");
+      }
       float* st = c->mbstats + 8 * gi;
       cs.seg[stats_seg0 + 0] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_PG, st + ST_PG, c->sg[1].size, nblk, 1, 1.f / M};
       cs.seg[stats_seg0 + 1] = ColsumSeg{c->slab[0] + c->sg[0].stats + ST_V, st + ST_V, c->sg[0].size, nblk, 1, 0.5f / M};
       cs.seg[stats_seg0 + 2] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_ENT, st + ST_ENT, c->sg[1].size, nblk, 4, 1.f / M};
-      if (overlap) {
-        for (int k = 0; k < 2; ++k) {  // critic: dW + column sums, then the actor's behind them
-          dw.trunk0 = k;
-          {
-            ProfScope ps(c, PK_DW2, s);
-            if (launch_dw(dw, H, OP, c->nchunks, s, 1) != 0) return fail("no dW kernel for this configuration");
-          }
-          ProfScope ps(c, PK_COLSUM, s);
-          if (k == 0) colsum_range(0, ns_critic);
-          else colsum_range(ns_critic, ns);
-          HIP_TRY(hipEventRecord(c->ar_ev[k], s));
-        }
-        dw.trunk0 = 0;
-        HIP_TRY(hipStreamWaitEvent(c->ar_stream, c->ar_ev[0], 0));
-        if (allreduce(c, c->G + crit0, crit1 - crit0, 1, c->ar_stream)) return -3;
-        HIP_TRY(hipStreamWaitEvent(c->ar_stream, c->ar_ev[1], 0));
-        if (crit0 > tb && allreduce(c, c->G + tb, crit0 - tb, 1, c->ar_stream)) return -3;
-        if (allreduce(c, c->G + crit1, (long)c->K.size - crit1, 1, c->ar_stream)) return -3;
-        HIP_TRY(hipEventRecord(c->ar_ev[2], c->ar_stream));
-        HIP_TRY(hipStreamWaitEvent(s, c->ar_ev[2], 0));
-      } else {
-        {
-          ProfScope ps(c, PK_DW2, s);
-          const int rc_ = c->use_upd2 ? launch_dw2(dw, OP, c->nchunks, s) : launch_dw(dw, H, OP, c->nchunks, s);
-          if (rc_ != 0) return fail("no dW kernel for this configuration");
-        }
-        {
-          ProfScope ps(c, PK_COLSUM, s);
-          launch_colsum(cs, ns, maxlen, s);
-        }
-        if (multi && allreduce(c, c->G + tb, trainable_n, 1, s)) return -3;  // ac:877-885, before the clip
+      {
+        ProfScope ps(c, PK_COLSUM, s);
+        launch_colsum(cs, ns, maxlen, s);
       }
+      if (multi && allreduce(c, c->G + tb, trainable_n, 1, s)) return -3;  // ac:877-885, before the clip
       c->adam_step += 1;
       const double bc1 = 1.0 - std::pow(0.9, (double)c->adam_step);
       const double bc2 = 1.0 - std::pow(0.999, (double)c->adam_step);

@@ -877,7 +877,7 @@ __global__ __launch_bounds__(512) void k_dw(DwArgs a) {
   constexpr int TO = H / 32;
   constexpr int WO2 = TO >= 4 ? 4 : TO, WI2 = 8 / WO2;
   constexpr int WO1 = TO >= 8 ? 8 : TO, WI1 = 8 / WO1;
-  const int trunk = a.trunk0 + (int)blockIdx.y;
+  const int trunk = blockIdx.y;
   const long m0 = (long)blockIdx.x * a.rows_per_chunk;
   const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
   float* out = a.slab[trunk] + (size_t)blockIdx.x * a.slab_stride;
@@ -913,7 +913,7 @@ __global__ __launch_bounds__(512) void k_dwf(DwArgs a) {
   static_assert(NSL == 1 || NSL == 2, "k_dwf slices");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hs = lane >> 5;
   const int wo = wave & 3, wi = wave >> 2;
-  const int trunk = a.trunk0 + (int)blockIdx.y, slice = NSL > 1 ? (int)blockIdx.z : 0;
+  const int trunk = blockIdx.y, slice = NSL > 1 ? (int)blockIdx.z : 0;
   const int obase = slice * (H / NSL);                       // first dW2^T / dW1^T row of the slice
   const bool w1_wave = NSL == 1 || wave < 8 / NSL;          // this wave owns a dW1^T row tile
   const int w1row = obase + wave * 32;                       // its first row
@@ -1616,14 +1616,14 @@ int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes) {
 
 // dW of both Linear weight matrices of both trunks, grid = (chunks, 2 trunks)
 template <int H, int OP>
-static int launch_dw_t(const DwArgs& a, int nchunks, size_t lds, hipStream_t s, int ntrunk) {
+static int launch_dw_t(const DwArgs& a, int nchunks, size_t lds, hipStream_t s) {
   auto k = k_dw<H, OP>;
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(nchunks, ntrunk), dim3(512), lds, s, a);
+  hipLaunchKernelGGL(k, dim3(nchunks, 2), dim3(512), lds, s, a);
   return 0;
 }
 
@@ -1634,7 +1634,7 @@ size_t dw_lds_bytes(int H, int OP) {
 }
 
 template <int H, int OP, int NSL>
-static int launch_dwf_t(const DwArgs& a, int nchunks, hipStream_t s, int ntrunk) {
+static int launch_dwf_t(const DwArgs& a, int nchunks, hipStream_t s) {
   auto k = k_dwf<H, OP, NSL>;
   constexpr size_t lds = (size_t)2 * (3 * 16 * (H + 4) + 16 * (OP + 4)) * sizeof(float);
   static bool attr = false;
@@ -1642,25 +1642,24 @@ static int launch_dwf_t(const DwArgs& a, int nchunks, hipStream_t s, int ntrunk)
     if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(nchunks, ntrunk, NSL), dim3(512), lds, s, a);
+  hipLaunchKernelGGL(k, dim3(nchunks, 2, NSL), dim3(512), lds, s, a);
   return 0;
 }
 
-int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s, int ntrunk) {
-  if (ntrunk < 1 || a.trunk0 < 0 || a.trunk0 + ntrunk > 2) return -1;
+int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s) {
   if (H == 256 && a.fused) {  // a.fused = 0: the two-phase k_dw (PPO_DW_FUSED=0 at ppo_create)
-    if (OP == 16) return a.slices == 2 ? launch_dwf_t<256, 16, 2>(a, nchunks, s, ntrunk) : launch_dwf_t<256, 16, 1>(a, nchunks, s, ntrunk);
-    if (OP == 32) return a.slices == 2 ? launch_dwf_t<256, 32, 2>(a, nchunks, s, ntrunk) : launch_dwf_t<256, 32, 1>(a, nchunks, s, ntrunk);
+    if (OP == 16) return a.slices == 2 ? launch_dwf_t<256, 16, 2>(a, nchunks, s) : launch_dwf_t<256, 16, 1>(a, nchunks, s);
+    if (OP == 32) return a.slices == 2 ? launch_dwf_t<256, 32, 2>(a, nchunks, s) : launch_dwf_t<256, 32, 1>(a, nchunks, s);
   }
   const size_t lds = dw_lds_bytes(H, OP);
-  if (H == 256 && OP == 16) return launch_dw_t<256, 16>(a, nchunks, lds, s, ntrunk);
-  if (H == 256 && OP == 32) return launch_dw_t<256, 32>(a, nchunks, lds, s, ntrunk);
-  if (H == 256 && OP == 112) return launch_dw_t<256, 112>(a, nchunks, lds, s, ntrunk);
-  if (H == 256 && OP == 384) return launch_dw_t<256, 384>(a, nchunks, lds, s, ntrunk);
-  if (H == 64 && OP == 16) return launch_dw_t<64, 16>(a, nchunks, lds, s, ntrunk);
-  if (H == 64 && OP == 32) return launch_dw_t<64, 32>(a, nchunks, lds, s, ntrunk);
-  if (H == 64 && OP == 112) return launch_dw_t<64, 112>(a, nchunks, lds, s, ntrunk);
-  if (H == 64 && OP == 384) return launch_dw_t<64, 384>(a, nchunks, lds, s, ntrunk);
+  if (H == 256 && OP == 16) return launch_dw_t<256, 16>(a, nchunks, lds, s);
+  if (H == 256 && OP == 32) return launch_dw_t<256, 32>(a, nchunks, lds, s);
+  if (H == 256 && OP == 112) return launch_dw_t<256, 112>(a, nchunks, lds, s);
+  if (H == 256 && OP == 384) return launch_dw_t<256, 384>(a, nchunks, lds, s);
+  if (H == 64 && OP == 16) return launch_dw_t<64, 16>(a, nchunks, lds, s);
+  if (H == 64 && OP == 32) return launch_dw_t<64, 32>(a, nchunks, lds, s);
+  if (H == 64 && OP == 112) return launch_dw_t<64, 112>(a, nchunks, lds, s);
+  if (H == 64 && OP == 384) return launch_dw_t<64, 384>(a, nchunks, lds, s);
   return -1;
 }
 

@@ -96,9 +96,6 @@ struct DwArgs {
   int fused;          // 1: k_dwf (dW2 and dW1 in one pass) where it applies; 0: two-phase k_dw
   int slices;         // k_dwf: output-row slices per chunk (grid z); 2 halves the chunks, so the
                       // split-K partials, for small minibatches (dw_slices)
-  int trunk0;         // first trunk of the launch (grid y covers ntrunk trunks from here): 0 with both
-                      // trunks in one launch; 0 / 1 for the per-trunk launches of the overlapped
-                      // all-reduce (ppo_update with a communicator)
 };
 // k_dwf output slices and dW row chunks for a minibatch of M rows: 128 chunks per trunk (one
 // workgroup per CU over both trunks); below 32 K rows 64 chunks x 2 output halves instead — the
@@ -243,7 +240,7 @@ int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hi
 int upd2_supported(const PackedLayout& K, UpdGeoOut* g);  // ppo_update_narrow.hip (H = 64 tanh agent)
 int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s);
 int launch_dw2(const DwArgs& a, int OP, int nchunks, hipStream_t s);  // both 64-wide trunks, rows gathered once
-int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s, int ntrunk = 2);
+int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s);
 size_t dw_lds_bytes(int H, int OP);
 void launch_colsum(const ColsumArgs& a, int nseg, long maxlen, hipStream_t s);
 void launch_gradnorm(const NormArgs& a, hipStream_t s);

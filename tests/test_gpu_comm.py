@@ -4,9 +4,7 @@ one GPU through the C-ABI:
 
   * a one-rank RCCL communicator runs the distributed sequence and must give bitwise the same
     parameters, gradient and stats as no communicator (RCCL's one-rank sum / average are exact);
-  * the host-transport communicator (ppo_comm_init_host) likewise at world = 1 — with a
-    communicator the gradient all-reduce is issued per trunk (the critic's share on a side stream
-    under the actor's dW and column sums), which must not change a bit;
+  * the host-transport communicator (ppo_comm_init_host) likewise at world = 1;
   * two ranks (two processes sharing the GPU, all-reduces over torch.distributed gloo) on the two
     halves of the golden ac256 minibatch reproduce the LibTorch two-shard replay (grad_dist2_avg,
     with the distributed advantage statistics dist2_adv_stats) and agree bitwise with each other;
@@ -104,16 +102,11 @@ def test_one_rank_host_transport_equals_no_communicator_bitwise(data):
     np.testing.assert_array_equal(g, g_ref)
     np.testing.assert_array_equal(p, p_ref)
     assert s == s_ref
-    # per update: adv mean (avg) + sum of squares (sum), then per minibatch the gradient average split
-    # by trunk (the critic's share first, reduced under the actor's dW; then the actor's), then stats
+    # per update: adv mean (avg) + sum of squares (sum), then one gradient average per minibatch, then stats
     nmb = 2 * 2
     assert calls[0] == (2 * nmb, True) and calls[1] == (nmb, False)
-    grads = [(n, avg) for n, avg in calls if n > 10_000]  # the packed gradient, 146 K floats in two calls
-    assert len(grads) == 2 * 2 * nmb and all(avg for _, avg in grads)  # two updates, two shares each
-    crit, act = grads[0::2], grads[1::2]
-    assert len(set(crit)) == 1 and len(set(act)) == 1  # the same split every minibatch
-    assert crit[0][0] > 70_000 and act[0][0] > 70_000  # 2x256 LayerNorm trunk + head(s) each
-    assert crit[0][0] + act[0][0] < 160_000
+    grads = [(n, avg) for n, avg in calls if n > 100_000]  # the flat (packed) gradient, 146 K floats
+    assert len(grads) == 2 * nmb and all(avg for _, avg in grads)  # two updates
     ag.close()
 
 

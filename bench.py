@@ -192,6 +192,7 @@ def main():
     ap.add_argument("--comm-1rank", action="store_true",
                     help="N = 1 only: attach a one-rank RCCL communicator, so the distributed update sequence "
                          "(split gradient all-reduce on its side stream) runs and its cost can be timed")
+    ap.add_argument("--options", default=None, help="ppo_create_ex options (kernel / geometry A/B runs)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -215,7 +216,7 @@ def main():
     T = args.num_steps
     cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=E_total, num_steps=T,
                               total_timesteps=E_total * T * (args.steps + args.warmup + 1))
-    tr = ppo_amd.Trainer(cfg, num_envs_per_device=E, rank=rank, world_size=world)
+    tr = ppo_amd.Trainer(cfg, num_envs_per_device=E, rank=rank, world_size=world, options=args.options)
     if world > 1:
         if args.comm == "host":
             import torch

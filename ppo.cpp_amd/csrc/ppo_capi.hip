@@ -261,6 +261,8 @@ struct CreateOptions {
   // cooperative launch costs ~30 us on this stack (measured: cfg1 +8.5 ms per iteration), more
   // than the launch it saves.
   int gradstep = 0;
+  int dw_rows = 0;     // dW split-K rows per chunk (multiple of 16; 0: auto, ~128 chunks per trunk)
+  int dw_slices = 0;   // k_dwf output slices per chunk (1 / 2; 0: auto, dw_slices())
 };
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
@@ -281,6 +283,10 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
     else if (k == "rollout" && (v == "auto" || v == "per_step"))
       o->rollout = v == "auto" ? PPO_ROLLOUT_AUTO : PPO_ROLLOUT_PER_STEP;
     else if (k == "gradstep" && (v == "fused" || v == "split")) o->gradstep = v == "fused";
+    else if (k == "dw_rows" && !v.empty() && v.find_first_not_of("0123456789") == std::string::npos &&
+             std::stoi(v) % 16 == 0 && std::stoi(v) >= 16 && std::stoi(v) <= 65536)
+      o->dw_rows = std::stoi(v);
+    else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
     else return fail("ppo_create_ex: unknown option or value: " + kv);
   }
   return 0;
@@ -407,7 +413,9 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   // dW split-K: ~128 row chunks per trunk (256 workgroups for the two trunks), 16-row multiples
   // (the chunking does not depend on dw_fused, so k_dwf and the two-phase k_dw sum the same chunks)
   c->dw_slices = dw_slices(c->M, H, OP, true);
+  if (opt.dw_slices && H == 256 && OP <= 32) c->dw_slices = opt.dw_slices;  // k_dwf geometry only
   c->rows_per_chunk = std::max(64, (((c->M + 128 / c->dw_slices - 1) / (128 / c->dw_slices)) + 15) & ~15);
+  if (opt.dw_rows && !c->use_upd2) c->rows_per_chunk = opt.dw_rows;
   if (c->use_upd2) c->rows_per_chunk = std::max(32, (((c->M + 255) / 256) + 31) & ~31);  // k_dw2: both trunks
   c->nchunks = (c->M + c->rows_per_chunk - 1) / c->rows_per_chunk;
   for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->dwslab[k], (size_t)c->nchunks * (H * H + H * OP));

@@ -455,13 +455,71 @@ struct HeadArgs {
   float* hpre;  // [n][2A] dist_mu / dist_sigma pre-activations (training), may be null
 };
 
+// A value the compiler may not look through: the per-concentration results (gamma draw, lgamma,
+// digamma) are computed by other threads in the fused tail's head (tail_head_rows) and reach the
+// combining expressions through LDS; the same barrier here keeps the two paths' fp contraction (a
+// producer's final multiply fused into its consumer's add) identical, so they agree bit for bit.
+PPO_DEV float opaque_(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// The Beta head's arithmetic in two pieces shared by k_carla_head (one thread per row) and the fused
+// tail (tail_head_rows: the pieces on different threads, exchanged through LDS). Every value that
+// crosses from one piece to the other, and every transcendental result, passes opaque_, so both
+// paths compile the same expression trees over the same leaves (no contraction into a consumer
+// in one path only) and agree bit for bit.
+struct BetaConc {
+  float conc, draw, lg, dg;  // softplus(pre) + beta_min, its gamma draw (sampling), lgamma, digamma
+};
+PPO_DEV BetaConc beta_conc(const HeadArgs& h, float pre, SampleKey key, long env, int ai, int side) {
+  BetaConc c;
+  c.conc = opaque_(opaque_(softplusf_(pre)) + h.beta_min);
+  c.draw = h.mode == PPO_CARLA_SAMPLE
+               ? opaque_(gamma_mt(c.conc, key, env, h.step_id, 0x10000u + (uint32_t)(ai * 2 + side) * 64u))
+               : 0.0f;
+  c.lg = opaque_(lgammaf(c.conc));
+  c.dg = opaque_(digammaf_(c.conc));
+  return c;
+}
+// action ai of row r: the sample / mean / roach / given value and the action's log-prob and
+// entropy terms (carla_head_row adds them over actions in action order); writes action / alpha / beta
+PPO_DEV void beta_action(const HeadArgs& h, int r, int ai, const BetaConc& ca, const BetaConc& cb, float& lpt,
+                         float& entt) {
+  const float* P = h.P;
+  const float hi = P[h.hi], lo = P[h.lo];
+  const float al = ca.conc, be = cb.conc;
+  float sv;
+  if (h.mode == PPO_CARLA_GIVEN) {
+    sv = (h.action_in[(long)r * h.A + ai] - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+    sv = fminf(fmaxf(sv, 0.0f + 1e-7f), 1.0f + 1e-7f);
+  } else if (h.mode == PPO_CARLA_MEAN) {
+    sv = al / (al + be);
+  } else if (h.mode == PPO_CARLA_ROACH) {
+    if (al > 1.0f && be > 1.0f) sv = (al - 1.0f) / (al + be - 2.0f);
+    else if (al <= 1.0f && be > 1.0f) sv = 0.0f;
+    else if (al > 1.0f && be <= 1.0f) sv = 1.0f;
+    else sv = al / (al + be);
+  } else {
+    sv = ca.draw / (ca.draw + cb.draw);
+  }
+  sv = opaque_(sv);
+  const float ab = al + be;
+  const float lgab = opaque_(lgammaf(ab)), dgab = opaque_(digammaf_(ab));
+  const float xa = opaque_(xlogyf_(al - 1.0f, sv)), xb = opaque_(xlogyf_(be - 1.0f, 1.0f - sv));
+  lpt = opaque_(xa + xb + (lgab - (ca.lg + cb.lg)));
+  entt = opaque_((ca.lg + cb.lg) - lgab - (2.0f - ab) * dgab - ((al - 1.0f) * ca.dg + (be - 1.0f) * cb.dg));
+  if (h.action) h.action[(long)r * h.A + ai] = (sv - 0.0f) / (1.0f - 0.0f) * (hi - lo) + lo;
+  if (h.alpha) h.alpha[(long)r * h.A + ai] = al;
+  if (h.beta) h.beta[(long)r * h.A + ai] = be;
+}
+
 // one row of k_carla_head: the dist_mu / dist_sigma dot products (or, with pre != nullptr, their
 // values computed by the same loop elsewhere: pre[ai] = mu, pre[A + ai] = sigma pre-activations),
 // softplus + beta_min, the sample / mean / roach / given value, log_prob, entropy
 PPO_DEV void carla_head_row(const HeadArgs& h, int r, const float* pre, bool copy_value) {
   const float* P = h.P;
   const float* x = h.latent + (long)r * 256;
-  const float hi = P[h.hi], lo = P[h.lo];
   const SampleKey key = sample_key(h.seed, h.rank);
   const long env = h.env_base + r;
   float lp = 0.f, ent = 0.f;
@@ -486,30 +544,11 @@ PPO_DEV void carla_head_row(const HeadArgs& h, int r, const float* pre, bool cop
       h.hpre[(long)r * 2 * h.A + ai] = pm;
       h.hpre[(long)r * 2 * h.A + h.A + ai] = ps;
     }
-    const float al = softplusf_(pm) + h.beta_min, be = softplusf_(ps) + h.beta_min;
-    float sv;
-    if (h.mode == PPO_CARLA_GIVEN) {
-      sv = (h.action_in[(long)r * h.A + ai] - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
-      sv = fminf(fmaxf(sv, 0.0f + 1e-7f), 1.0f + 1e-7f);
-    } else if (h.mode == PPO_CARLA_MEAN) {
-      sv = al / (al + be);
-    } else if (h.mode == PPO_CARLA_ROACH) {
-      if (al > 1.0f && be > 1.0f) sv = (al - 1.0f) / (al + be - 2.0f);
-      else if (al <= 1.0f && be > 1.0f) sv = 0.0f;
-      else if (al > 1.0f && be <= 1.0f) sv = 1.0f;
-      else sv = al / (al + be);
-    } else {
-      const float ga = gamma_mt(al, key, env, h.step_id, 0x10000u + (uint32_t)(ai * 2 + 0) * 64u);
-      const float gb = gamma_mt(be, key, env, h.step_id, 0x10000u + (uint32_t)(ai * 2 + 1) * 64u);
-      sv = ga / (ga + gb);
-    }
-    const float ab = al + be;
-    const float lga = lgammaf(al), lgb = lgammaf(be), lgab = lgammaf(ab);
-    lp += xlogyf_(al - 1.0f, sv) + xlogyf_(be - 1.0f, 1.0f - sv) + (lgab - (lga + lgb));
-    ent += (lga + lgb) - lgab - (2.0f - ab) * digammaf_(ab) - ((al - 1.0f) * digammaf_(al) + (be - 1.0f) * digammaf_(be));
-    if (h.action) h.action[(long)r * h.A + ai] = (sv - 0.0f) / (1.0f - 0.0f) * (hi - lo) + lo;
-    if (h.alpha) h.alpha[(long)r * h.A + ai] = al;
-    if (h.beta) h.beta[(long)r * h.A + ai] = be;
+    const BetaConc ca = beta_conc(h, pm, key, env, ai, 0), cb = beta_conc(h, ps, key, env, ai, 1);
+    float lpt, entt;
+    beta_action(h, r, ai, ca, cb, lpt, entt);
+    lp += lpt;
+    ent += entt;
   }
   if (h.logprob) h.logprob[r] = lp;
   if (h.entropy) h.entropy[r] = ent;
@@ -534,6 +573,8 @@ __global__ __launch_bounds__(64) void k_carla_head(HeadArgs h) {
 // k_carla_head's loop; the per-row Beta arithmetic is k_carla_head's.
 // ==========================================================================================
 constexpr int kTailThreads = 512, kTailMaxZ = 10, kTailMaxLin = 9, kTailMaxStage = 8, kTailMaxN = 64;
+constexpr int kTailLdx = 256 + 4;  // LDS row stride of a recomputed layer's output (OC <= 256)
+constexpr int kTailPreMaxK = 32;   // widest input of a layer computed inside its consumer's items
 
 struct TailLin {
   const float* in;
@@ -560,27 +601,31 @@ struct TailArgs {
   unsigned* bar;       // grid barrier counter (monotonic across launches)
   unsigned bar_base;   // its value when this launch started
   int stage_lo, stage_hi;  // the stages this launch runs (a barrier between consecutive ones)
+  int pre_lin, pre_for;    // layer pre_lin (K < 256, stage -1) is computed inside layer pre_for's items
+                           // for their rows (LDS), instead of as a stage of its own; -1: none
 };
 
 PPO_DEV int tail_z(int K) { return K >= 256 ? (K + kSplitKC - 1) / kSplitKC : 1; }
 
 // one Linear work item: rows s0 .. s0 + 15, output channels oc0 .. oc0 + 15 of layer L
-PPO_DEV void tail_lin_item(const float* __restrict__ P, const TailLin& L, int n, int s0, int oc0, float* part) {
+// (in_row0: the row of the batch that L.in's row 0 holds — 0 for a global input, s0 for rows staged in LDS)
+PPO_DEV void tail_lin_item(const float* __restrict__ P, const TailLin& L, int n, int s0, int oc0, float* part,
+                           int in_row0 = 0) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
   const int K = L.K, Z = tail_z(K), kc = Z > 1 ? kSplitKC : K;
   const int oc = oc0 + j, s = s0 + j;
   const float* wrow = P + L.w + (long)(oc < L.OC ? oc : 0) * K;
   const bool sv = s < n;
-  const float* xrow = L.in + (long)(sv ? s : 0) * L.in_stride;
+  const float* xrow = L.in + (long)(sv ? s - in_row0 : 0) * L.in_stride;
   // a chunk is at most 32 k-steps (128 / 4): all 64 operand loads of a lane go out together (one
-  // memory latency per chunk), from clamped addresses, masked afterwards
-  for (int z = wave; z < Z; z += kTailThreads / 64) {
+  // memory latency per chunk), from clamped addresses, masked afterwards (issuing a second chunk's
+  // loads before the first chunk's chain, for linear.0's ten chunks on eight waves, measured slower:
+  // 236 VGPRs)
+  constexpr int NW = kTailThreads / 64, NU = kSplitKC / 4;
+  auto load = [&](int z, float (&av)[NU], float (&bv)[NU]) {
     const int kbeg = z * kc, kend = min(K, kbeg + kc);
-    const int nsteps = 4 * ((kend - kbeg + 15) / 16);
-    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-    float av[kSplitKC / 4], bv[kSplitKC / 4];
 #pragma unroll
-    for (int u = 0; u < kSplitKC / 4; ++u) {
+    for (int u = 0; u < NU; ++u) {
       const int k = kbeg + 4 * u + g;
       // k_conv's staged weight: rows of K % 4 == 0 are read as float4s from min(k, K - 4), so a
       // masked tap past the end holds W[K - 4 + (k & 3)]; other rows clamp to K - 1
@@ -589,12 +634,22 @@ PPO_DEV void tail_lin_item(const float* __restrict__ P, const TailLin& L, int n,
       const bool ok = sv && k < kend;
       bv[u] = (ok ? xrow[min(k, K - 1)] : L.in[0]) * (ok ? 1.0f : 0.0f);
     }
+  };
+  auto chain = [&](int z, const float (&av)[NU], const float (&bv)[NU]) {
+    const int kbeg = z * kc, kend = min(K, kbeg + kc);
+    const int nsteps = 4 * ((kend - kbeg + 15) / 16);
+    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < kSplitKC / 4; ++u)
+    for (int u = 0; u < NU; ++u)
       if (u < nsteps) acc = mfma16(av[u], bv[u], acc);
     // lane (j, g) holds output channel oc0 + 4 g + r of row s0 + j
 #pragma unroll
     for (int r = 0; r < 4; ++r) part[(z * 16 + 4 * g + r) * 17 + j] = acc[r];
+  };
+  for (int z = wave; z < Z; z += NW) {
+    float av[NU], bv[NU];
+    load(z, av, bv);
+    chain(z, av, bv);
   }
   __syncthreads();
   if (tid < 256) {
@@ -616,9 +671,95 @@ PPO_DEV void tail_lin_item(const float* __restrict__ P, const TailLin& L, int n,
   __syncthreads();  // part is reused by the next item
 }
 
+// All OC outputs of a one-chunk layer L (K < 256) for rows s0 .. s0 + 15 into LDS xs[16][ldx], with
+// tail_lin_item's arithmetic (per 16x16 tile the same MFMA chain over the same masked operands, then
+// + bias, relu), so a dependent layer's items can take them as their input without a stage of their
+// own (the state MLP's first layer under its second). Optionally also stored to L.out (rows < n).
+PPO_DEV void tail_lin_rows_lds(const float* __restrict__ P, const TailLin& L, int n, int s0, float* xs, int ldx,
+                               bool store) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  constexpr int NU = kTailPreMaxK / 4;  // u-steps a K <= kTailPreMaxK layer can use (tail_lin_item loads
+                                        // kSplitKC / 4 and issues the first nsteps: the same operands)
+  const int K = L.K, kend = K;
+  const int nsteps = 4 * ((K + 15) / 16);
+  const int s = s0 + j;
+  const bool sv = s < n;
+  const float* xrow = L.in + (long)(sv ? s : 0) * L.in_stride;
+#pragma unroll 1
+  for (int ot = wave; ot < (L.OC + 15) / 16; ot += kTailThreads / 64) {
+    const int oc0 = 16 * ot, oc = oc0 + j;
+    const float* wrow = P + L.w + (long)(oc < L.OC ? oc : 0) * K;
+    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+    float av[NU], bv[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int k = 4 * u + g;
+      const int kw = (K & 3) == 0 ? (k < K ? k : K - 4 + (k & 3)) : min(k, K - 1);
+      av[u] = wrow[kw] * ((oc < L.OC && k < kend) ? 1.0f : 0.0f);
+      const bool ok = sv && k < kend;
+      bv[u] = (ok ? xrow[min(k, K - 1)] : L.in[0]) * (ok ? 1.0f : 0.0f);
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+      if (u < nsteps) acc = mfma16(av[u], bv[u], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = oc0 + 4 * g + r;
+      if (o < L.OC) {
+        float y = acc[r] + P[L.b + o];
+        if (L.relu) y = y > 0.0f ? y : 0.0f;
+        xs[j * ldx + o] = y;
+        if (store && sv) L.out[(long)s * L.out_stride + o] = y;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// The tail's Beta head for rows r0 .. r0 + rows - 1 (rows * 2A <= kTailThreads), given the dist_mu /
+// dist_sigma pre-activations pre[row][2A]: carla_head_row's arithmetic spread over threads — one per
+// (row, concentration) for softplus, the gamma draw, lgamma and digamma of that concentration, one
+// per (row, action) for the sample value and the action's log-prob / entropy terms, one per row for
+// the sums over actions in action order (lp = (0 + t_0) + t_1 ..., as carla_head_row's loop adds
+// them) — so the row's serial chain is one concentration plus one action instead of 2A of each.
+PPO_DEV void tail_head_rows(const HeadArgs& h, int r0, int rows, const float* pre, float* hsc) {
+  const int tid = threadIdx.x, A = h.A, n = h.n;
+  const SampleKey key = sample_key(h.seed, h.rank);
+  BetaConc* cs = reinterpret_cast<BetaConc*>(hsc);  // [rows][2A]
+  {  // (row, q): q < A the alpha side of action q, q >= A the beta side of action q - A
+    const int rl = tid / (2 * A), q = tid - rl * 2 * A, r = r0 + rl;
+    if (rl < rows && r < n) {
+      const int side = q < A ? 0 : 1, ai = q - side * A;
+      const float x = pre[rl * 2 * A + q];
+      if (h.hpre) h.hpre[(long)r * 2 * A + q] = x;
+      cs[rl * 2 * A + q] = beta_conc(h, x, key, h.env_base + r, ai, side);
+    }
+  }
+  __syncthreads();
+  float* terms = hsc + kTailThreads * 4;  // [rows][A][2]: log-prob term, entropy term
+  {
+    const int rl = tid / A, ai = tid - rl * A, r = r0 + rl;
+    if (rl < rows && r < n)
+      beta_action(h, r, ai, cs[rl * 2 * A + ai], cs[rl * 2 * A + A + ai], terms[tid * 2], terms[tid * 2 + 1]);
+  }
+  __syncthreads();
+  if (tid < rows && r0 + tid < n) {
+    float lp = 0.f, ent = 0.f;
+    for (int ai = 0; ai < A; ++ai) {
+      lp += terms[(tid * A + ai) * 2 + 0];
+      ent += terms[(tid * A + ai) * 2 + 1];
+    }
+    if (h.logprob) h.logprob[r0 + tid] = lp;
+    if (h.entropy) h.entropy[r0 + tid] = ent;
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(kTailThreads) void k_carla_tail(TailArgs a) {
   __shared__ float part[kTailMaxZ * 16 * 17];
   __shared__ float pre[kTailThreads * 2];
+  __shared__ float xs[16 * kTailLdx];            // rows of layer pre_lin, computed inside pre_for's items
+  __shared__ float hsc[kTailThreads * 4 + kTailThreads * 2];  // head scratch (tail_head_rows)
   const int tid = threadIdx.x;
   const int rt_n = (a.n + 15) / 16;
   for (int stage = a.stage_lo; stage <= a.stage_hi; ++stage) {
@@ -660,7 +801,15 @@ __global__ __launch_bounds__(kTailThreads) void k_carla_tail(TailArgs a) {
           rem -= cnt;
         }
         const int rt = rem % rt_n, ot = rem / rt_n;
-        tail_lin_item(a.P, a.lin[l], a.n, 16 * rt, 16 * ot, part);
+        TailLin lx = a.lin[l];
+        int row0 = 0;
+        if (l == a.pre_for) {  // its input rows first, from the one-chunk layer pre_lin (ot 0 also stores them)
+          tail_lin_rows_lds(a.P, a.lin[a.pre_lin], a.n, 16 * rt, xs, kTailLdx, ot == 0);
+          lx.in = xs;
+          lx.in_stride = kTailLdx;
+          row0 = 16 * rt;
+        }
+        tail_lin_item(a.P, lx, a.n, 16 * rt, 16 * ot, part, row0);
       } else {
         // head: thread (row, ai, mu | sigma) runs k_carla_head's dot product loop for its
         // pre-activation; then one thread per row the rest of k_carla_head
@@ -676,8 +825,7 @@ __global__ __launch_bounds__(kTailThreads) void k_carla_tail(TailArgs a) {
           pre[rl * 2 * A + q] = p + a.P[(q < A ? h.mu_b : h.sg_b) + ai];
         }
         __syncthreads();
-        if (tid < rows && r0 + tid < a.n) carla_head_row(h, r0 + tid, pre + tid * 2 * A, false);
-        __syncthreads();
+        tail_head_rows(h, r0, rows, pre, hsc);
       }
     }
   }
@@ -914,6 +1062,7 @@ extern "C" int ppo_carla_forward(ppo_carla_t* c, int n, const uint8_t* bev, cons
   const bool fused_tail = c->tail_mode != 2 && n <= kTailMaxN;
   ConvArgs c6{};
   int c6_Z = 1;
+  const long FW = 256 + L.NV;
   // cnn (carla_model.h:66-78, :236): conv1 reads the uint8 image, conv6 writes linear-input columns 0..1023
   const uint8_t* img = bev;
   const float* cur = nullptr;
@@ -935,7 +1084,6 @@ extern "C" int ppo_carla_forward(ppo_carla_t* c, int n, const uint8_t* bev, cons
     cur = out;
     cur_stride = out_stride;
   }
-  const long FW = 256 + L.NV;
   if (fused_tail) {
     if (rc) return ppo_fail("ppo_carla_forward: no convolution kernel for this shape", -1);
     TailArgs ta{};
@@ -952,17 +1100,23 @@ extern "C" int ppo_carla_forward(ppo_carla_t* c, int n, const uint8_t* bev, cons
       ta.lin_stage[ta.nlin++] = stage;
     };
     // the forward's layers in dependency stages (carla_model.h:238-279)
-    lin(0, meas, L.NM, L.NM, L.st_w[0], L.st_b[0], c->s1, 256, 256, 1, nullptr);
-    lin(1, c->s1, 256, 256, L.st_w[1], L.st_b[1], c->enc + 1024, 1280, 256, 1, nullptr);
-    lin(2, c->enc, 1280, 1280, L.lin_w[0], L.lin_b[0], c->l1, 512, 512, 1, nullptr);
-    lin(3, c->l1, 512, 512, L.lin_w[1], L.lin_b[1], c->feat, FW, 256, 1, nullptr);
-    lin(4, c->feat, FW, (int)FW, L.v_w[0], L.v_b[0], c->v1, 256, 256, 1, nullptr);
-    lin(4, c->feat, FW, 256, L.pi_w[0], L.pi_b[0], c->p1, 256, 256, 1, nullptr);
-    lin(5, c->v1, 256, 256, L.v_w[1], L.v_b[1], c->v2, 256, 256, 1, nullptr);
-    lin(5, c->p1, 256, 256, L.pi_w[1], L.pi_b[1], c->p2, 256, 256, 1, nullptr);
-    lin(6, c->v2, 256, 256, L.v_w[2], L.v_b[2], c->val, 1, 1, 0, value);
-    ta.nstage = 7;
-    ta.head_stage = 6;
+    // With a narrow measurement vector the state MLP's first layer runs inside its second layer's
+    // items (stage 0, beside conv6's finish): one stage fewer
+    const int d = L.NM <= kTailPreMaxK ? 1 : 0;
+    ta.pre_lin = ta.pre_for = -1;
+    if (d) ta.pre_lin = ta.nlin;
+    lin(d ? -1 : 0, meas, L.NM, L.NM, L.st_w[0], L.st_b[0], c->s1, 256, 256, 1, nullptr);
+    if (d) ta.pre_for = ta.nlin;
+    lin(1 - d, c->s1, 256, 256, L.st_w[1], L.st_b[1], c->enc + 1024, 1280, 256, 1, nullptr);
+    lin(2 - d, c->enc, 1280, 1280, L.lin_w[0], L.lin_b[0], c->l1, 512, 512, 1, nullptr);
+    lin(3 - d, c->l1, 512, 512, L.lin_w[1], L.lin_b[1], c->feat, FW, 256, 1, nullptr);
+    lin(4 - d, c->feat, FW, (int)FW, L.v_w[0], L.v_b[0], c->v1, 256, 256, 1, nullptr);
+    lin(4 - d, c->feat, FW, 256, L.pi_w[0], L.pi_b[0], c->p1, 256, 256, 1, nullptr);
+    lin(5 - d, c->v1, 256, 256, L.v_w[1], L.v_b[1], c->v2, 256, 256, 1, nullptr);
+    lin(5 - d, c->p1, 256, 256, L.pi_w[1], L.pi_b[1], c->p2, 256, 256, 1, nullptr);
+    lin(6 - d, c->v2, 256, 256, L.v_w[2], L.v_b[2], c->val, 1, 1, 0, value);
+    ta.nstage = 7 - d;
+    ta.head_stage = 6 - d;
     ta.h = HeadArgs{P,          L.mu_w, L.mu_b,   L.sg_w,    L.sg_b,    L.hi,    L.lo,
                     c->p2,      c->val, n,        L.A,       sample_type, c->cfg.beta_min, action_in,
                     c->cfg.seed, c->cfg.rank, env_base, step_id, action, logprob, entropy, value, alpha, beta,

@@ -415,8 +415,8 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   c->dw_slices = dw_slices(c->M, H, OP, true);
   if (opt.dw_slices && H == 256 && OP <= 32) c->dw_slices = opt.dw_slices;  // k_dwf geometry only
   c->rows_per_chunk = std::max(64, (((c->M + 128 / c->dw_slices - 1) / (128 / c->dw_slices)) + 15) & ~15);
-  if (opt.dw_rows && !c->use_upd2) c->rows_per_chunk = opt.dw_rows;
   if (c->use_upd2) c->rows_per_chunk = std::max(32, (((c->M + 255) / 256) + 31) & ~31);  // k_dw2: both trunks
+  if (opt.dw_rows && (!c->use_upd2 || opt.dw_rows % 32 == 0)) c->rows_per_chunk = opt.dw_rows;  // k_dw2: 32-row steps
   c->nchunks = (c->M + c->rows_per_chunk - 1) / c->rows_per_chunk;
   for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->dwslab[k], (size_t)c->nchunks * (H * H + H * OP));
   rc |= dmalloc(&c->normout, 2 + PPO_LAYOUT_MAX_TENSORS + 2);

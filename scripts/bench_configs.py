@@ -19,8 +19,8 @@ sys.path.insert(0, os.path.join(ROOT, "ppo.cpp_amd"))
 import ppo_amd  # noqa: E402
 
 
-def run(name, cfg, iters, warmup):
-    tr = ppo_amd.Trainer(cfg)
+def run(name, cfg, iters, warmup, options=None):
+    tr = ppo_amd.Trainer(cfg, options=options)
     for _ in range(warmup):
         tr.iterate()
     tr.agent.sync()
@@ -37,7 +37,7 @@ def run(name, cfg, iters, warmup):
     tr.agent.sync()
     dt = (time.perf_counter() - t0) / iters
     steps = cfg.num_envs * cfg.num_steps
-    out = {"config": name, "num_envs": cfg.num_envs, "num_steps": cfg.num_steps, "env_id": cfg.env_id,
+    out = {"config": name, **({"options": options} if options else {}), "num_envs": cfg.num_envs, "num_steps": cfg.num_steps, "env_id": cfg.env_id,
            "ms_per_iteration": round(dt * 1e3, 3), "env_steps_per_s": round(steps / dt, 1),
            "kernels_ms_per_iteration": {k: round(v[0], 3) for k, v in prof.items()}}
     print(json.dumps(out), flush=True)
@@ -49,18 +49,19 @@ def main():
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--only", default="", help="cfg2, cfg4_shard or cfg1")
+    ap.add_argument("--options", default=None, help="ppo_create_ex options (A/B runs)")
     args = ap.parse_args()
     ppo_amd.set_device(0)
     n = args.iters + args.warmup + 2
     if args.only in ("", "cfg2"):
         run("cfg2", ppo_amd.PPOConfig(env_id="Humanoid-v4", num_envs=1024, num_steps=2048,
-                                      total_timesteps=1024 * 2048 * n), args.iters, args.warmup)
+                                      total_timesteps=1024 * 2048 * n), args.iters, args.warmup, args.options)
     if args.only in ("", "cfg4_shard"):
         run("cfg4_shard", ppo_amd.ACPPOConfig(env_id="Ant-v5", num_envs=1024, num_steps=128,
-                                              total_timesteps=1024 * 128 * n), args.iters, args.warmup)
+                                              total_timesteps=1024 * 128 * n), args.iters, args.warmup, args.options)
     if args.only in ("", "cfg1"):
         run("cfg1", ppo_amd.PPOConfig(env_id="HalfCheetah-v5", num_envs=1, num_steps=2048,
-                                      total_timesteps=2048 * n), args.iters, args.warmup)
+                                      total_timesteps=2048 * n), args.iters, args.warmup, args.options)
 
 
 if __name__ == "__main__":

@@ -86,6 +86,10 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            the wave-per-16-rows k_fwdbwd
  *   act_kernel=auto|2|4      64-wide agent act: by shape (auto), k_act2, or k_act4
  *   dw_fused=1|0             dW1 / dW2 in one pass (k_dwf) or two (k_dw)
+ *   dw_dma=1|0               k_dwf's rows staged by LDS DMA in three buffers (k_dwf_dma, default)
+ *                            or through registers in two (k_dwf); bitwise the same
+ *   dw_rows=<n>, dw_slices=1|2  dW split-K geometry: rows per chunk (multiple of 16; 32 for the
+ *                            64-wide agent) and k_dwf output slices; default: automatic
  *   rollout=auto|per_step    ppo_rollout_synth: persistent launch where supported, or per step
  *   gradstep=split|fused     clip_grad_norm_ + Adam: two launches (k_gradnorm, k_adam; default) or
  *                            one cooperative launch (k_gradstep: slower on ROCm 7, whose cooperative

@@ -177,6 +177,7 @@ struct ppo_ctx {
   int act_kernel = 0;  // 0: the fastest act kernel for the shape; 2 / 4: force k_act2 / k_act4 (PPO_ACT_KERNEL, A/B)
   int upd_trunk_mask = 3, upd_sched = 1;   // k_upd launch options (PPO_UPD_TRUNK: PPO_DIAG builds only)
   int dw_fused = 1;
+  int dw_dma = 1;                       // create option dw_dma: k_dwf stages by LDS DMA (k_dwf_dma)
   int rollout_mode = PPO_ROLLOUT_AUTO;  // ppo_set_rollout_mode
   int gradstep = 0;                     // create option gradstep=fused|split (default split)
   unsigned* gs_bar = nullptr;           // k_gradstep's grid barrier counter
@@ -263,6 +264,7 @@ struct CreateOptions {
   int gradstep = 0;
   int dw_rows = 0;     // dW split-K rows per chunk (multiple of 16; 0: auto, ~128 chunks per trunk)
   int dw_slices = 0;   // k_dwf output slices per chunk (1 / 2; 0: auto, dw_slices())
+  int dw_dma = 1;      // 1 (default): k_dwf_dma (LDS-DMA staging, three stage buffers); 0: k_dwf
 };
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
@@ -287,6 +289,7 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
              std::stoi(v) % 16 == 0 && std::stoi(v) >= 16 && std::stoi(v) <= 65536)
       o->dw_rows = std::stoi(v);
     else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
+    else if (k == "dw_dma" && (v == "0" || v == "1")) o->dw_dma = v[0] - '0';
     else return fail("ppo_create_ex: unknown option or value: " + kv);
   }
   return 0;
@@ -339,6 +342,7 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   // the diagnostic build (PPO_DIAG) also reads the measurement scripts' environment switches
   c->act_kernel = opt.act_kernel;
   c->dw_fused = opt.dw_fused;
+  c->dw_dma = opt.dw_dma;
   c->rollout_mode = opt.rollout;
   c->gradstep = opt.gradstep;
   int upd_kernel = opt.upd_kernel;
@@ -796,6 +800,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   dw.rows_per_chunk = c->rows_per_chunk;
   dw.slices = c->dw_slices;
   dw.fused = c->dw_fused;
+  dw.dma = c->dw_dma;
   dw.xn = c->Xn;
   dw.obs = c->buf[PPO_BUF_OBS];
   dw.O = c->K.O;

@@ -1004,6 +1004,117 @@ __global__ __launch_bounds__(512) void k_dwf(DwArgs a) {
   }
 }
 
+// k_dwf_dma — k_dwf with the stage rows moved by LDS DMA (buffer_load ... lds, 16 bytes a lane: one
+// wave instruction per 1 KB row) into three stage buffers, two stages ahead: no register staging,
+// no ds_write phase between the MFMA blocks, and a stage's loads have two MFMA blocks to land.
+// Rows are unpadded (a 32-lane operand read of two rows meets a 2-way bank conflict, which costs
+// far less than the MFMAs it feeds); the MFMA loop and its operands are k_dwf's, so the result is
+// bitwise k_dwf's. Rows past the chunk read as 0 through an out-of-range offset.
+template <int H, int OP, int NSL>
+__global__ __launch_bounds__(512) void k_dwf_dma(DwArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int KS = 16, NBUF = 3;
+  constexpr int LDH = H, LDX = OP;
+  constexpr int oH1 = KS * LDH, oDZ1 = 2 * KS * LDH, oXN = 3 * KS * LDH;
+  constexpr int STG = 3 * KS * LDH + KS * LDX;
+  static_assert(H == 256 && (OP == 16 || OP == 32), "k_dwf_dma geometry");
+  // DMA instructions per stage: 3 x KS rows of H floats (one each) + the XN rows (KS * OP / 256)
+  constexpr int NXI = KS * OP / 256;
+  static_assert(KS == 16 && NXI <= 8, "k_dwf_dma: 2 rows of each source per wave + XN on waves 0 .. NXI-1");
+  constexpr int TOW = 2 / NSL, TIW = 4;
+  static_assert(NSL == 1 || NSL == 2, "k_dwf slices");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hs = lane >> 5;
+  const int wo = wave & 3, wi = wave >> 2;
+  const int trunk = blockIdx.y, slice = NSL > 1 ? (int)blockIdx.z : 0;
+  const int obase = slice * (H / NSL);
+  const bool w1_wave = NSL == 1 || wave < 8 / NSL;
+  const int w1row = obase + wave * 32;
+  const long m0 = (long)blockIdx.x * a.rows_per_chunk;
+  const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
+  if (m0 >= m1) return;
+  const uint32_t rows_bytes = (uint32_t)((long)a.M * H * 4), xn_bytes = (uint32_t)((long)a.M * OP * 4);
+  const PBuf bdz2 = make_pbuf(a.dz2[trunk], (int)(rows_bytes / 4)), bh1 = make_pbuf(a.h1[trunk], (int)(rows_bytes / 4));
+  const PBuf bdz1 = make_pbuf(a.dz1[trunk], (int)(rows_bytes / 4));
+  const PBuf bxn = make_pbuf(a.xn, (int)(xn_bytes / 4));
+  f16v acc[TOW][TIW], acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc1[r] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < TOW; ++u)
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) acc[u][v][r] = 0.0f;
+  }
+  // stage at rows mb into buffer buf: wave w moves rows 2 w and 2 w + 1 of each of the three
+  // row sources, waves 0 .. NXI-1 one XN instruction each (256 floats = 256 / OP rows)
+  auto issue = [&](long mb, int buf) {
+    float* b = lds + buf * STG;
+#pragma unroll
+    for (int s3 = 0; s3 < 3; ++s3) {
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int r = 2 * wave + rr;
+        const long row = mb + r;
+        const uint32_t voff = row < m1 ? (uint32_t)((row * H) * 4 + lane * 16) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds((s3 == 0 ? bdz2 : s3 == 1 ? bh1 : bdz1).r,
+                                                 (__attribute__((address_space(3))) void*)(b + s3 * KS * LDH + r * LDH), 16,
+                                                 voff, 0, 0, 0);
+      }
+    }
+    if (wave < NXI) {
+      const int e = wave * 256 + lane * 4, r = e / OP;  // 4 floats of row r
+      const long row = mb + r;
+      const uint32_t voff = row < m1 ? (uint32_t)((row * OP + (e - r * OP)) * 4) : 0xFFFFFFF0u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(bxn.r, (__attribute__((address_space(3))) void*)(b + oXN + wave * 256), 16,
+                                               voff, 0, 0, 0);
+    }
+  };
+  // instructions this wave issues per stage: the vmcnt that leaves only the newest stage in flight
+  const bool xw = wave < NXI;
+  const int nst = (int)((m1 - m0 + KS - 1) / KS);
+  issue(m0, 0);
+  if (nst > 1) issue(m0 + KS, 1);
+  for (int sI = 0; sI < nst; ++sI) {
+    if (sI + 1 < nst) {  // stage sI + 1 may stay in flight
+      if (xw) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();  // every wave's stage-sI rows have landed; stage sI - 1's buffer is free
+    if (sI + 2 < nst) issue(m0 + (long)(sI + 2) * KS, (sI + 2) % NBUF);
+    __builtin_amdgcn_sched_barrier(0);
+    const float* sb = lds + (sI % NBUF) * STG;
+#pragma unroll
+    for (int k = 0; k < KS; k += 2) {
+      const float* rowp = sb + (k + hs) * LDH;
+      float av[TOW], bv[TIW];
+#pragma unroll
+      for (int u = 0; u < TOW; ++u) av[u] = rowp[obase + (wo * TOW + u) * 32 + l32];
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) bv[v] = rowp[oH1 + (wi * TIW + v) * 32 + l32];
+      const float a1 = rowp[oDZ1 + (w1_wave ? w1row : 0) + l32];
+      const float b1 = l32 < OP ? sb[oXN + (k + hs) * LDX + l32] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < TOW; ++u)
+#pragma unroll
+        for (int v = 0; v < TIW; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[v], acc[u][v], 0, 0, 0);
+      if (w1_wave) acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc1, 0, 0, 0);
+    }
+  }
+  float* out = a.slab[trunk] + (size_t)blockIdx.x * a.slab_stride;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int orow = (r & 3) + 8 * (r >> 2) + 4 * hs;
+#pragma unroll
+    for (int u = 0; u < TOW; ++u)
+#pragma unroll
+      for (int v = 0; v < TIW; ++v)
+        out[(size_t)(obase + (wo * TOW + u) * 32 + orow) * H + (wi * TIW + v) * 32 + l32] = acc[u][v][r];
+    if (w1_wave && l32 < OP) out[(size_t)H * H + (size_t)(w1row + orow) * OP + l32] = acc1[r];
+  }
+}
+
 // =============================================================================================
 // k_colsum — dst[seg] = sum_{c < C} src[c * stride + seg]   (fixed order => deterministic)
 // =============================================================================================
@@ -1635,6 +1746,17 @@ size_t dw_lds_bytes(int H, int OP) {
 
 template <int H, int OP, int NSL>
 static int launch_dwf_t(const DwArgs& a, int nchunks, hipStream_t s) {
+  if (a.dma) {
+    auto k = k_dwf_dma<H, OP, NSL>;
+    constexpr size_t lds = (size_t)3 * (3 * 16 * H + 16 * OP) * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+      if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
+      attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3(nchunks, 2, NSL), dim3(512), lds, s, a);
+    return 0;
+  }
   auto k = k_dwf<H, OP, NSL>;
   constexpr size_t lds = (size_t)2 * (3 * 16 * (H + 4) + 16 * (OP + 4)) * sizeof(float);
   static bool attr = false;

@@ -96,6 +96,7 @@ struct DwArgs {
   int fused;          // 1: k_dwf (dW2 and dW1 in one pass) where it applies; 0: two-phase k_dw
   int slices;         // k_dwf: output-row slices per chunk (grid z); 2 halves the chunks, so the
                       // split-K partials, for small minibatches (dw_slices)
+  int dma;            // k_dwf: 1 stages the rows by LDS DMA, three buffers (k_dwf_dma), bitwise k_dwf
 };
 // k_dwf output slices and dW row chunks for a minibatch of M rows: 128 chunks per trunk (one
 // workgroup per CU over both trunks); below 32 K rows 64 chunks x 2 output halves instead — the

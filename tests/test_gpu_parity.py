@@ -439,17 +439,19 @@ def test_act_kernels_agree(O_, A, n):
             np.testing.assert_allclose(t4, t2, rtol=1e-5, atol=2e-5)
 
 
-@pytest.mark.parametrize("kind,O_,A,H", [(1, 17, 6, 256), (0, 17, 6, 256), (1, 9, 3, 256)])
-def test_fused_dw_matches_two_phase_dw(kind, O_, A, H):
-    """k_dwf (dW2 and dW1 in one pass over the rows) and the two-phase k_dw run the same MFMA
-    chains over the same rows in the same order: the gradients are bitwise equal (ragged last
-    chunk and stage: M = 12 800 - 8 rows)."""
+@pytest.mark.parametrize("kind,O_,A,H,E", [(1, 17, 6, 256, 1599), (0, 17, 6, 256, 1599), (1, 9, 3, 256, 1599),
+                                           (1, 17, 6, 256, 4100)])
+def test_fused_dw_matches_two_phase_dw(kind, O_, A, H, E):
+    """k_dwf (dW2 and dW1 in one pass over the rows), k_dwf_dma (the same, rows staged by LDS DMA in
+    three buffers: create option dw_dma=1) and the two-phase k_dw run the same MFMA chains over the
+    same rows in the same order: the gradients are bitwise equal (ragged last chunk and stage:
+    M = 12 800 - 8 rows, output halves; M = 32 800, whole rows)."""
     rng = np.random.default_rng(7)
     L = O.layout_init(kind, O_, A, H)
     p = random_params(L, rng)
     if kind == 0:
         p[L.logstd:L.logstd + A] = -0.5
-    E, T = 1599, 8
+    T = 8
     B = T * E
     x = rng.standard_normal((B, O_)).astype(np.float32)
     act = (rng.uniform(-0.95, 0.95, (B, A)) if kind else rng.standard_normal((B, A))).astype(np.float32)
@@ -459,7 +461,7 @@ def test_fused_dw_matches_two_phase_dw(kind, O_, A, H):
     ret = rng.standard_normal(B).astype(np.float32)
     perm = rng.permutation(B).astype(np.int32)
     grads = []
-    for opt in ("dw_fused=0", "dw_fused=1"):
+    for opt in ("dw_fused=0", "dw_dma=0", "dw_dma=1"):
         ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.1, options=opt)
         ag.load_params(p)
         fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
@@ -468,6 +470,7 @@ def test_fused_dw_matches_two_phase_dw(kind, O_, A, H):
         ag.close()
     assert np.isfinite(grads[0]).all()
     np.testing.assert_array_equal(grads[1], grads[0])
+    np.testing.assert_array_equal(grads[2], grads[0])
 
 
 def test_cfg1_shape_iteration_vs_oracle():

@@ -804,6 +804,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   dw.xn = c->Xn;
   dw.obs = c->buf[PPO_BUF_OBS];
   dw.O = c->K.O;
+  dw.obs_n = B * c->K.O;
   dw.slab_stride = (long)H * H + (long)H * OP;
   for (int k = 0; k < 2; ++k) {
     dw.dz2[k] = c->DZ2[k];

@@ -88,6 +88,7 @@ struct DwArgs {
   const float* xn;
   const int32_t* perm;  // non-null: dW1's input rows are gathered as obs[perm[m]] (O wide, zero padded to OP)
   const float* obs;     //   instead of read from xn (k_upd2: no input normalisation, no Xn round trip)
+  long obs_n;           // floats in obs (k_dw2_dma's buffer descriptor)
   int O;
   float* slab[2];     // [nchunks][H*H + H*OP] per trunk
   long slab_stride;

@@ -901,6 +901,141 @@ __global__ __launch_bounds__(512) void k_dw2(DwArgs a) {
   }
 }
 
+// k_dw2_dma — k_dw2 with the stage rows moved by LDS DMA (16 bytes a lane) into three stage buffers,
+// two stages ahead of the MFMAs, instead of through registers into one buffer between two barriers
+// (OP % 128 == 0 and O % 4 == 0: Humanoid's 376 / 384). The gathered X rows are [16][OP] unpadded
+// (columns O .. OP-1 and rows past the chunk read as 0 through out-of-range offsets); DZ1 / DZ2 / H1
+// of each trunk are [16][64] blocks. Each wave issues the same number of DMA instructions per stage
+// (OP / 128 X + 3 row-block instructions) and loads the permutation entries of its X rows four
+// stages ahead, so one constant s_waitcnt keeps exactly the next stage in flight. Every stage past
+// the last is issued too (all out of range) to keep that count; the operand values and the MFMA
+// order are k_dw2's: bitwise k_dw2.
+template <int OP>
+__global__ __launch_bounds__(512) void k_dw2_dma(DwArgs a) {
+  constexpr int H = 64, KS = 16, NBUF = 3;
+  constexpr int TI = (OP + 31) / 32, TIW = (TI + 1) / 2;
+  constexpr int UPR = OP / 4;                      // 16-byte units per X row
+  constexpr int XI = KS * OP / 256, XPW = XI / 8;  // X DMA instructions per stage / per wave
+  static_assert(OP % 128 == 0 && XPW >= 1, "k_dw2_dma: X rows must be whole instructions per wave");
+  constexpr int oZ = KS * OP, STG = oZ + 6 * KS * H;  // X | DZ1 t0,t1 | DZ2 t0,t1 | H1 t0,t1
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hs = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar DMA descriptors
+  const long m0 = (long)blockIdx.x * a.rows_per_chunk;
+  const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
+  if (m0 >= m1) return;
+  const int nst = (int)((m1 - m0 + KS - 1) / KS);
+  const int O = a.O;
+  const int wo = wave & 3, wi = wave >> 2;
+  const int t2 = wave >> 2, ot2 = (wave >> 1) & 1, it2 = wave & 1;
+  const PBuf ob = make_pbuf_b(a.obs, (uint32_t)min(a.obs_n * 4, (long)0xFFFFFFFF));
+  const uint32_t zb = (uint32_t)((long)a.M * H * 4);
+  const PBuf bz0 = make_pbuf_b(a.dz1[0], zb), bz1 = make_pbuf_b(a.dz1[1], zb);
+  const PBuf bz2 = make_pbuf_b(a.dz2[0], zb), bz3 = make_pbuf_b(a.dz2[1], zb);
+  const PBuf bz4 = make_pbuf_b(a.h1[0], zb), bz5 = make_pbuf_b(a.h1[1], zb);
+
+  f16v2 acc1[TIW], acc2;
+#pragma unroll
+  for (int v = 0; v < TIW; ++v)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc1[v][r] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
+
+  // The permutation entries of a stage's 16 rows also arrive by LDS DMA (4 bytes a lane), each wave
+  // fetching those of its own two X rows (2 w, 2 w + 1) into its slot of a three-stage ring, so no
+  // register waits on a load: per stage every wave issues X (XPW) + row-block (3) + entry (1) DMAs.
+  static_assert(XPW * 64 == 2 * UPR, "each wave's X instructions cover its two rows");
+  const PBuf bperm = make_pbuf_b(a.perm, (uint32_t)((long)a.M * 4));
+  int* PR = reinterpret_cast<int*>(lds + NBUF * STG);  // [3 stages][8 waves][64]
+  auto perm_dma = [&](int st) {
+    const long m = m0 + (long)st * KS + 2 * wave + lane;
+    const uint32_t voff = lane < 2 ? (uint32_t)(min(m, m1 - 1) * 4) : kOOB;  // clamped; masked at use
+    dma<4>(bperm, reinterpret_cast<float*>(PR + ((st % NBUF) * 8 + wave) * 64), voff);
+  };
+  auto issue = [&](int st) {
+    float* b = lds + (st % NBUF) * STG;
+    const int* pw = PR + ((st % NBUF) * 8 + wave) * 64;
+#pragma unroll
+    for (int x = 0; x < XPW; ++x) {
+      const int i = wave * XPW + x, u = i * 64 + lane, row = u / UPR, q = u - row * UPR;
+      const long m = m0 + (long)st * KS + row;
+      const int pr = pw[row - 2 * wave];
+      const uint32_t voff = (m < m1 && 4 * q < O) ? (uint32_t)(pr * O + 4 * q) * 4u : kOOB;
+      dma<16>(ob, b + i * 256, voff);
+    }
+#pragma unroll
+    for (int y = 0; y < 3; ++y) {  // row-block instruction i: source i / 4, rows 4 (i % 4) .. + 3
+      const int i = wave * 3 + y, src = i >> 2, r0 = 4 * (i & 3), row = r0 + (lane >> 4);
+      const long m = m0 + (long)st * KS + row;
+      const uint32_t voff = m < m1 ? (uint32_t)((m * H + 4 * (lane & 15)) * 4) : kOOB;
+      const PBuf bs = src == 0 ? bz0 : src == 1 ? bz1 : src == 2 ? bz2 : src == 3 ? bz3 : src == 4 ? bz4 : bz5;
+      dma<16>(bs, b + oZ + src * KS * H + r0 * H, voff);
+    }
+  };
+  perm_dma(0);
+  perm_dma(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // each wave reads only its own entries
+  issue(0);
+  perm_dma(2);
+  issue(1);
+  perm_dma(3);
+  for (int st = 0; st < nst; ++st) {
+    // stage st's rows and stage st + 2's entries have landed; stage st + 1's rows and stage st + 3's
+    // entries may stay in flight
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XPW + 3 + 1) : "memory");
+    lds_barrier();
+    issue(st + 2);
+    perm_dma(st + 4);
+    __builtin_amdgcn_sched_barrier(0);
+    const float* b = lds + (st % NBUF) * STG;
+    const float* XS = b;
+    const float* Z = b + oZ;
+    float opn[TIW + 3];
+    auto rd_ops = [&](int k, float (&o)[TIW + 3]) {
+      const int row = k + hs;
+      o[0] = Z[(wo >> 1) * KS * H + row * H + 32 * (wo & 1) + l32];
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) {
+        const int col = min(32 * (TIW * wi + v) + l32, OP - 1);  // cols >= OP are masked below
+        o[1 + v] = XS[row * OP + col];
+      }
+      o[TIW + 1] = Z[(2 + t2) * KS * H + row * H + 32 * ot2 + l32];
+      o[TIW + 2] = Z[(4 + t2) * KS * H + row * H + 32 * it2 + l32];
+    };
+    rd_ops(0, opn);
+#pragma unroll
+    for (int k = 0; k < KS; k += 2) {
+      float op[TIW + 3];
+#pragma unroll
+      for (int q = 0; q < TIW + 3; ++q) op[q] = opn[q];
+      if (k + 2 < KS) rd_ops(k + 2, opn);
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) {
+        const int col = 32 * (TIW * wi + v) + l32;
+        acc1[v] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[0], col < OP ? op[1 + v] : 0.f, acc1[v], 0, 0, 0);
+      }
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(op[TIW + 1], op[TIW + 2], acc2, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA may land after the workgroup ends
+  // ---- partials of this chunk (k_dw2's layout) ----
+#pragma unroll
+  for (int v = 0; v < TIW; ++v)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = 32 * wo + (r & 3) + 8 * (r >> 2) + 4 * hs, t = o >> 6;
+      const int i = 32 * (TIW * wi + v) + l32;
+      if (i < OP) a.slab[t][(size_t)blockIdx.x * a.slab_stride + H * H + (size_t)(o & 63) * OP + i] = acc1[v][r];
+    }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int o = 32 * ot2 + (r & 3) + 8 * (r >> 2) + 4 * hs, i = 32 * it2 + l32;
+    a.slab[t2][(size_t)blockIdx.x * a.slab_stride + o * H + i] = acc2[r];
+  }
+}
+
 size_t dw2_lds_bytes(int OP) { return (size_t)(16 * (OP + 4) + 3 * 16 * (2 * 64 + 4)) * sizeof(float); }
 
 template <int OP, int VEC>
@@ -915,6 +1050,14 @@ static int launch_dw2_t(const DwArgs& a, int nchunks, hipStream_t s) {
 
 int launch_dw2(const DwArgs& a, int OP, int nchunks, hipStream_t s) {
   const bool v4 = (a.O % 4) == 0;
+  if (a.dma && v4 && OP == 384) {
+    constexpr size_t lds = (size_t)3 * (16 * 384 + 6 * 16 * 64) * sizeof(float) + 3 * 8 * 64 * sizeof(int);
+    static const bool ok = hipFuncSetAttribute((const void*)k_dw2_dma<384>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)lds) == hipSuccess;
+    if (!ok) return -2;
+    hipLaunchKernelGGL((k_dw2_dma<384>), dim3(nchunks), dim3(512), lds, s, a);
+    return 0;
+  }
   if (OP == 16) return v4 ? launch_dw2_t<16, 4>(a, nchunks, s) : launch_dw2_t<16, 1>(a, nchunks, s);
   if (OP == 32) return v4 ? launch_dw2_t<32, 4>(a, nchunks, s) : launch_dw2_t<32, 1>(a, nchunks, s);
   if (OP == 112) return v4 ? launch_dw2_t<112, 4>(a, nchunks, s) : launch_dw2_t<112, 1>(a, nchunks, s);

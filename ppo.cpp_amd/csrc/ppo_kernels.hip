@@ -869,6 +869,121 @@ PPO_DEV void dw_phase(const float* __restrict__ DZ, const float* __restrict__ IN
       }
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 7]
+PPO_DEV void wait_vmcnt_upto7(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+  }
+}
+
+// dw_phase with the stage rows moved by LDS DMA (16 bytes a lane, one 1 KB wave instruction per
+// 256 floats; rows contiguous in HBM, IN rows of LDI floats, no permutation) into three unpadded
+// stage buffers two stages ahead — k_dwf_dma's pipeline for the two-phase k_dw (wide inputs: Ant's
+// OP = 112). Same operands and MFMA order as dw_phase: bitwise.
+template <int NO, int NI, int LDI, int WO, int WI>
+PPO_DEV void dw_phase_dma(const float* __restrict__ DZ, const float* __restrict__ IN, long M, long m0, long m1,
+                          float* __restrict__ out, float* lds, int tid) {
+  constexpr int TO = NO / 32, TI = (NI + 31) / 32;
+  constexpr int TOW = TO / WO, TIW = (TI + WI - 1) / WI;
+  constexpr int KS = 16, NBUF = 3;
+  constexpr int ADZ = KS * NO, STG = ADZ + KS * LDI;
+  constexpr int ND = KS * NO / 256, NIN = KS * LDI / 256, NT = ND + NIN;  // DMA instructions per stage
+  static_assert(KS * NO % 256 == 0 && KS * LDI % 256 == 0, "dw_phase_dma: whole 1 KB instructions");
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wo = wave % WO, wi = wave / WO;
+  const int l32 = lane & 31, hs = lane >> 5;
+  const PBuf bdz = make_pbuf(DZ, (int)(M * NO)), bin = make_pbuf(IN, (int)(M * LDI));
+  f16v acc[TOW][TIW];
+#pragma unroll
+  for (int u = 0; u < TOW; ++u)
+#pragma unroll
+    for (int v = 0; v < TIW; ++v)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[u][v][r] = 0.0f;
+  // wave w moves instructions w, w + 8, ... of a stage: [0, ND) DZ rows, [ND, NT) IN floats
+  const int nmine = (NT - wave + 7) / 8;
+  auto issue = [&](long mb, int buf) {
+    float* b = lds + buf * STG;
+#pragma unroll
+    for (int q = 0; q < (NT + 7) / 8; ++q) {
+      const int i = wave + 8 * q;
+      if (i < ND) {
+        const long row = mb + i / (NO / 256);
+        const uint32_t voff = row < m1 ? (uint32_t)(((long)i * 256 + mb * NO) * 4 + lane * 16) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(bdz.r, (__attribute__((address_space(3))) void*)(b + i * 256), 16,
+                                                 voff, 0, 0, 0);
+      } else if (i < NT) {
+        const int e = (i - ND) * 256 + lane * 4;  // float of the stage's IN block
+        const long row = mb + e / LDI;
+        const uint32_t voff = row < m1 ? (uint32_t)((mb * LDI + e) * 4) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(bin.r, (__attribute__((address_space(3))) void*)(b + ADZ + (i - ND) * 256),
+                                                 16, voff, 0, 0, 0);
+      }
+    }
+  };
+  const int nst = (int)((m1 - m0 + KS - 1) / KS);
+  issue(m0, 0);
+  if (nst > 1) issue(m0 + KS, 1);
+  for (int sI = 0; sI < nst; ++sI) {
+    wait_vmcnt_upto7(sI + 1 < nst ? nmine : 0);  // stage sI landed; sI + 1 may stay in flight
+    lds_barrier();
+    if (sI + 2 < nst) issue(m0 + (long)(sI + 2) * KS, (sI + 2) % NBUF);
+    __builtin_amdgcn_sched_barrier(0);
+    const float* sdz = lds + (sI % NBUF) * STG;
+    const float* sin = sdz + ADZ;
+#pragma unroll
+    for (int k = 0; k < KS; k += 2) {
+      float av[TOW], bv[TIW];
+#pragma unroll
+      for (int u = 0; u < TOW; ++u) av[u] = sdz[(k + hs) * NO + (wo * TOW + u) * 32 + l32];
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) {
+        const int col = (wi * TIW + v) * 32 + l32;
+        bv[v] = (col < LDI) ? sin[(k + hs) * LDI + col] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < TOW; ++u)
+#pragma unroll
+        for (int v = 0; v < TIW; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[v], acc[u][v], 0, 0, 0);
+    }
+  }
+  lds_barrier();  // the buffers are free for the next phase
+#pragma unroll
+  for (int u = 0; u < TOW; ++u)
+#pragma unroll
+    for (int v = 0; v < TIW; ++v)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = (wo * TOW + u) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hs;
+        const int i = (wi * TIW + v) * 32 + l32;
+        if (i < LDI) out[(size_t)o * LDI + i] = acc[u][v][r];
+      }
+}
+
+template <int H, int OP>
+__global__ __launch_bounds__(512) void k_dw_dma(DwArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int TO = H / 32;
+  constexpr int WO2 = TO >= 4 ? 4 : TO, WI2 = 8 / WO2;
+  constexpr int WO1 = TO >= 8 ? 8 : TO, WI1 = 8 / WO1;
+  const int trunk = blockIdx.y;
+  const long m0 = (long)blockIdx.x * a.rows_per_chunk;
+  const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
+  float* out = a.slab[trunk] + (size_t)blockIdx.x * a.slab_stride;
+  if (m0 < m1) {
+    dw_phase_dma<H, H, H, WO2, WI2>(a.dz2[trunk], a.h1[trunk], a.M, m0, m1, out, lds, threadIdx.x);
+    dw_phase_dma<H, OP, OP, WO1, WI1>(a.dz1[trunk], a.xn, a.M, m0, m1, out + H * H, lds, threadIdx.x);
+  }
+}
+
 // 8 waves (two per SIMD): dW2 as a 4 x 2 grid of 64 x 128 wave tiles (128 accumulator registers
 // per wave), then dW1 (H x OP) with the waves split over the output rows.
 template <int H, int OP>
@@ -1768,11 +1883,27 @@ static int launch_dwf_t(const DwArgs& a, int nchunks, hipStream_t s) {
   return 0;
 }
 
+// k_dw_dma: the stage buffers of the larger phase, three of them
+template <int H, int OP>
+static int launch_dw_dma_t(const DwArgs& a, int nchunks, hipStream_t s) {
+  auto k = k_dw_dma<H, OP>;
+  constexpr int big = H > OP ? H : OP;
+  constexpr size_t lds = (size_t)3 * 16 * (H + big) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3(nchunks, 2), dim3(512), lds, s, a);
+  return 0;
+}
+
 int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s) {
   if (H == 256 && a.fused) {  // a.fused = 0: the two-phase k_dw (PPO_DW_FUSED=0 at ppo_create)
     if (OP == 16) return a.slices == 2 ? launch_dwf_t<256, 16, 2>(a, nchunks, s) : launch_dwf_t<256, 16, 1>(a, nchunks, s);
     if (OP == 32) return a.slices == 2 ? launch_dwf_t<256, 32, 2>(a, nchunks, s) : launch_dwf_t<256, 32, 1>(a, nchunks, s);
   }
+  if (a.dma && !a.perm && H == 256 && OP == 112) return launch_dw_dma_t<256, 112>(a, nchunks, s);  // Ant (cfg4)
   const size_t lds = dw_lds_bytes(H, OP);
   if (H == 256 && OP == 16) return launch_dw_t<256, 16>(a, nchunks, lds, s);
   if (H == 256 && OP == 32) return launch_dw_t<256, 32>(a, nchunks, lds, s);

@@ -440,13 +440,14 @@ def test_act_kernels_agree(O_, A, n):
 
 
 @pytest.mark.parametrize("kind,O_,A,H,E", [(1, 17, 6, 256, 1599), (0, 17, 6, 256, 1599), (1, 9, 3, 256, 1599),
-                                           (1, 17, 6, 256, 4100), (0, 376, 17, 64, 1599)])
+                                           (1, 17, 6, 256, 4100), (0, 376, 17, 64, 1599), (1, 105, 8, 256, 1599)])
 def test_fused_dw_matches_two_phase_dw(kind, O_, A, H, E):
     """k_dwf (dW2 and dW1 in one pass over the rows), k_dwf_dma (the same, rows staged by LDS DMA in
     three buffers: create option dw_dma=1) and the two-phase k_dw run the same MFMA chains over the
     same rows in the same order: the gradients are bitwise equal (ragged last chunk and stage:
     M = 12 800 - 8 rows, output halves; M = 32 800, whole rows). The 64-wide agent at Humanoid's
-    O = 376 compares k_dw2 (dw_dma=0) with k_dw2_dma (the default) the same way."""
+    O = 376 compares k_dw2 (dw_dma=0) with k_dw2_dma (the default) the same way, and Ant's O = 105
+    (OP = 112, the two-phase k_dw) k_dw with k_dw_dma."""
     rng = np.random.default_rng(7)
     L = O.layout_init(kind, O_, A, H)
     p = random_params(L, rng)

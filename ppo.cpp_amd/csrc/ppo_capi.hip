@@ -178,7 +178,6 @@ struct ppo_ctx {
   int upd_trunk_mask = 3, upd_sched = 1;   // k_upd launch options (PPO_UPD_TRUNK: PPO_DIAG builds only)
   int dw_fused = 1;
   int dw_dma = 1;                       // create option dw_dma: k_dwf stages by LDS DMA (k_dwf_dma)
-  int dw_sched = 0;                     // create option dw_sched (k_dwf_dma A/B)
   int rollout_mode = PPO_ROLLOUT_AUTO;  // ppo_set_rollout_mode
   int gradstep = 0;                     // create option gradstep=fused|split (default split)
   unsigned* gs_bar = nullptr;           // k_gradstep's grid barrier counter
@@ -266,7 +265,6 @@ struct CreateOptions {
   int dw_rows = 0;     // dW split-K rows per chunk (multiple of 16; 0: auto, ~128 chunks per trunk)
   int dw_slices = 0;   // k_dwf output slices per chunk (1 / 2; 0: auto, dw_slices())
   int dw_dma = 1;      // 1 (default): k_dwf_dma (LDS-DMA staging, three stage buffers); 0: k_dwf
-  int dw_sched = 0;    // k_dwf_dma scheduling A/B bits
 };
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
@@ -292,7 +290,6 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
       o->dw_rows = std::stoi(v);
     else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
     else if (k == "dw_dma" && (v == "0" || v == "1")) o->dw_dma = v[0] - '0';
-    else if (k == "dw_sched" && (v == "0" || v == "1")) o->dw_sched = v[0] - '0';
     else return fail("ppo_create_ex: unknown option or value: " + kv);
   }
   return 0;
@@ -346,7 +343,6 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   c->act_kernel = opt.act_kernel;
   c->dw_fused = opt.dw_fused;
   c->dw_dma = opt.dw_dma;
-  c->dw_sched = opt.dw_sched;
   c->rollout_mode = opt.rollout;
   c->gradstep = opt.gradstep;
   int upd_kernel = opt.upd_kernel;
@@ -805,7 +801,6 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   dw.slices = c->dw_slices;
   dw.fused = c->dw_fused;
   dw.dma = c->dw_dma;
-  dw.sched = c->dw_sched;
   dw.xn = c->Xn;
   dw.obs = c->buf[PPO_BUF_OBS];
   dw.O = c->K.O;

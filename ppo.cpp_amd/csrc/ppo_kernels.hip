@@ -1140,7 +1140,6 @@ __global__ __launch_bounds__(512) void k_dwf_dma(DwArgs a) {
   static_assert(NSL == 1 || NSL == 2, "k_dwf slices");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hs = lane >> 5;
   const int wo = wave & 3, wi = wave >> 2;
-  if ((a.sched & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);  // A/B: the second wave of each SIMD first
   const int trunk = blockIdx.y, slice = NSL > 1 ? (int)blockIdx.z : 0;
   const int obase = slice * (H / NSL);
   const bool w1_wave = NSL == 1 || wave < 8 / NSL;

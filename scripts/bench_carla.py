@@ -23,7 +23,7 @@ FLOP_PER_SAMPLE = 87_907_008  # SURVEY §8d (conv + MLP forward, 2 K N per layer
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, nargs="+", default=[32, 256])
+    ap.add_argument("--batch", type=int, nargs="*", default=[32, 256])
     ap.add_argument("--update-batch", type=int, nargs="*", default=[256, 2048])
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--options", default="", help="ppo_carla_create_ex options, e.g. tail=layers")

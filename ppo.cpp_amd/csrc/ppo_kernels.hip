@@ -1861,7 +1861,8 @@ size_t dw_lds_bytes(int H, int OP) {
 
 template <int H, int OP, int NSL>
 static int launch_dwf_t(const DwArgs& a, int nchunks, hipStream_t s) {
-  if (a.dma) {
+  // the DMA kernels address their sources through 32-bit buffer descriptors (make_pbuf: int floats)
+  if (a.dma && (long)a.M * H < (1L << 29)) {
     auto k = k_dwf_dma<H, OP, NSL>;
     constexpr size_t lds = (size_t)3 * (3 * 16 * H + 16 * OP) * sizeof(float);
     static bool attr = false;
@@ -1903,7 +1904,8 @@ int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s) {
     if (OP == 16) return a.slices == 2 ? launch_dwf_t<256, 16, 2>(a, nchunks, s) : launch_dwf_t<256, 16, 1>(a, nchunks, s);
     if (OP == 32) return a.slices == 2 ? launch_dwf_t<256, 32, 2>(a, nchunks, s) : launch_dwf_t<256, 32, 1>(a, nchunks, s);
   }
-  if (a.dma && !a.perm && H == 256 && OP == 112) return launch_dw_dma_t<256, 112>(a, nchunks, s);  // Ant (cfg4)
+  if (a.dma && !a.perm && H == 256 && OP == 112 && (long)a.M * H < (1L << 29))  // Ant (cfg4); 32-bit descriptors
+    return launch_dw_dma_t<256, 112>(a, nchunks, s);
   const size_t lds = dw_lds_bytes(H, OP);
   if (H == 256 && OP == 16) return launch_dw_t<256, 16>(a, nchunks, lds, s);
   if (H == 256 && OP == 32) return launch_dw_t<256, 32>(a, nchunks, lds, s);

@@ -1050,7 +1050,8 @@ static int launch_dw2_t(const DwArgs& a, int nchunks, hipStream_t s) {
 
 int launch_dw2(const DwArgs& a, int OP, int nchunks, hipStream_t s) {
   const bool v4 = (a.O % 4) == 0;
-  if (a.dma && v4 && OP == 384) {
+  // 32-bit buffer descriptors: the observation buffer and the row blocks must stay below 4 GB
+  if (a.dma && v4 && OP == 384 && a.obs_n * 4 < 0xFFFFFFF0L && (long)a.M * 64 * 4 < 0xFFFFFFF0L) {
     constexpr size_t lds = (size_t)3 * (16 * 384 + 6 * 16 * 64) * sizeof(float) + 3 * 8 * 64 * sizeof(int);
     static const bool ok = hipFuncSetAttribute((const void*)k_dw2_dma<384>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)lds) == hipSuccess;

@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
   using GE = Geo2<NTO, NHT, VEC, NUA>;
   constexpr int OP = GE::OP, CKB = GE::CKB, NCH = GE::NCH, CW = GE::CW, LDX = GE::LDX, NHP = GE::NHP;
   constexpr int LDG = GE::LDG, PERROW = GE::PERROW, NGI = GE::NGI, NU = GE::NU, UPR = GE::UPR, SWZ = GE::SWZ;
-  constexpr int W1D = 2;  // W1 A-operand prefetch depth (k-blocks)
+  constexpr int W1D = 3;  // W1 A-operand prefetch depth (k-blocks; 2 -> 3: cfg2 k_upd2 44.05 -> 43.88 ms)
   constexpr int R = R2, FT = FT2, RT = RT2, LDA = LDA2, H = H2;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* XS = lds + GE::oXS;
@@ -314,9 +314,9 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
 #pragma unroll
       for (int kb = 0; kb < NTO; ++kb) {
         if (kb > 0 && kb % CKB == 0) {
-          // chunk kb / CKB landed: only the W1 loads of k-blocks kb, kb + 1 may still be in flight
-          static_assert(W1D * FT2 == 4, "vmcnt below");
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          // chunk kb / CKB landed: only the W1 loads of k-blocks kb .. kb + 2 may still be in flight
+          static_assert(W1D * FT2 == 6, "vmcnt below");
+          asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
           lds_barrier();
           const int ch = kb / CKB;
           if (ch + 1 < NCH) issue(pcur, ch + 1, tp ^ ((ch + 1) & 1));

@@ -918,6 +918,9 @@ __global__ __launch_bounds__(512) void k_dw2_dma(DwArgs a) {
   constexpr int XI = KS * OP / 256, XPW = XI / 8;  // X DMA instructions per stage / per wave
   static_assert(OP % 128 == 0 && XPW >= 1, "k_dw2_dma: X rows must be whole instructions per wave");
   constexpr int oZ = KS * OP, STG = oZ + 6 * KS * H;  // X | DZ1 t0,t1 | DZ2 t0,t1 | H1 t0,t1
+  // every dW1 column tile is a real one (OP = 32 TI, two waves' TIW tiles cover them exactly): no
+  // operand clamping or masking in the MFMA loop
+  constexpr bool FULL = TI * 32 == OP && 2 * TIW == TI;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hs = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar DMA descriptors
@@ -997,8 +1000,8 @@ __global__ __launch_bounds__(512) void k_dw2_dma(DwArgs a) {
       o[0] = Z[(wo >> 1) * KS * H + row * H + 32 * (wo & 1) + l32];
 #pragma unroll
       for (int v = 0; v < TIW; ++v) {
-        const int col = min(32 * (TIW * wi + v) + l32, OP - 1);  // cols >= OP are masked below
-        o[1 + v] = XS[row * OP + col];
+        const int col = 32 * (TIW * wi + v) + l32;
+        o[1 + v] = XS[row * OP + (FULL ? col : min(col, OP - 1))];  // cols >= OP are masked below
       }
       o[TIW + 1] = Z[(2 + t2) * KS * H + row * H + 32 * ot2 + l32];
       o[TIW + 2] = Z[(4 + t2) * KS * H + row * H + 32 * it2 + l32];
@@ -1013,7 +1016,7 @@ __global__ __launch_bounds__(512) void k_dw2_dma(DwArgs a) {
 #pragma unroll
       for (int v = 0; v < TIW; ++v) {
         const int col = 32 * (TIW * wi + v) + l32;
-        acc1[v] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[0], col < OP ? op[1 + v] : 0.f, acc1[v], 0, 0, 0);
+        acc1[v] = __builtin_amdgcn_mfma_f32_32x32x2f32(op[0], (FULL || col < OP) ? op[1 + v] : 0.f, acc1[v], 0, 0, 0);
       }
       acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(op[TIW + 1], op[TIW + 2], acc2, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);

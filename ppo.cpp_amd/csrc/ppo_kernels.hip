@@ -892,6 +892,7 @@ PPO_DEV void dw_phase_dma(const float* __restrict__ DZ, const float* __restrict_
                           float* __restrict__ out, float* lds, int tid) {
   constexpr int TO = NO / 32, TI = (NI + 31) / 32;
   constexpr int TOW = TO / WO, TIW = (TI + WI - 1) / WI;
+  constexpr bool FULL = TI * 32 == LDI && WI * TIW == TI;  // every input column tile is real: no masking
   constexpr int KS = 16, NBUF = 3;
   constexpr int ADZ = KS * NO, STG = ADZ + KS * LDI;
   constexpr int ND = KS * NO / 256, NIN = KS * LDI / 256, NT = ND + NIN;  // DMA instructions per stage
@@ -947,7 +948,7 @@ PPO_DEV void dw_phase_dma(const float* __restrict__ DZ, const float* __restrict_
 #pragma unroll
       for (int v = 0; v < TIW; ++v) {
         const int col = (wi * TIW + v) * 32 + l32;
-        bv[v] = (col < LDI) ? sin[(k + hs) * LDI + col] : 0.0f;
+        bv[v] = (FULL || col < LDI) ? sin[(k + hs) * LDI + col] : 0.0f;
       }
 #pragma unroll
       for (int u = 0; u < TOW; ++u)
@@ -964,7 +965,7 @@ PPO_DEV void dw_phase_dma(const float* __restrict__ DZ, const float* __restrict_
       for (int r = 0; r < 16; ++r) {
         const int o = (wo * TOW + u) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hs;
         const int i = (wi * TIW + v) * 32 + l32;
-        if (i < LDI) out[(size_t)o * LDI + i] = acc[u][v][r];
+        if (FULL || i < LDI) out[(size_t)o * LDI + i] = acc[u][v][r];
       }
 }
 

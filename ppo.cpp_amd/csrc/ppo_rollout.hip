@@ -468,18 +468,22 @@ int launch_beta_logp(const float* s_beta, float* logp, long n, int A, hipStream_
 }
 
 // =============================================================================================
-// k_values: critic(obs[i]) for n stored rows; workgroups walk 16-row blocks
+// k_values: critic(obs[i]) for n stored rows; workgroups walk R-row blocks
 // =============================================================================================
-// 32 rows per pass (two 16-row MFMA tiles per wave): the LayerNorm exchanges and barriers of a pass
-// are shared by twice the rows; every row's arithmetic is the 16-row pass's (bitwise)
+// 32 or 64 rows per pass (two or four 16-row MFMA tiles per wave): the LayerNorm exchanges and
+// barriers of a pass are shared by more rows; every row's arithmetic is the 16-row pass's (bitwise).
+// 64 only for the narrow observation widths: at NTO = 7 the fourth tile's accumulators spill.
+template <int NTO>
+constexpr int val_rows() { return NTO <= 2 ? 64 : 32; }
 template <int NTO, int NHT>
 __global__ __launch_bounds__(512) void k_values(ValuesArgs a) {
-  using GE = RollGeo<NTO, NHT, 32>;
-  constexpr int OP = GE::OP, LDX = GE::LDX, LDP = GE::LDP, R = 32;
+  constexpr int R = val_rows<NTO>();
+  using GE = RollGeo<NTO, NHT, R>;
+  constexpr int OP = GE::OP, LDX = GE::LDX, LDP = GE::LDP;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* XS = lds + GE::oXS;
   float* PRE = lds + GE::oPRE;
-  float* NRM = lds + GE::oNRM;
+  float* NRM = lds + GE::oXO;  // the env regions from oXO on are unused here: the statistics go there
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const PackedLayout& K = a.K;
   const float* __restrict__ P = a.P;
@@ -493,7 +497,7 @@ __global__ __launch_bounds__(512) void k_values(ValuesArgs a) {
     NRM[OP + f] = f < O ? P[K.ostd + f] : 1.0f;
   }
   const long nblk = (a.n + R - 1) / R;
-  // the block's observations (R x OP <= 16 x 112: at most 4 per thread) are loaded one block ahead,
+  // the block's observations (R x OP <= 64 x 32 or 32 x 112: at most 7 per thread) are loaded one block ahead,
   // under the previous block's layers
   constexpr int NXI = (R * OP + kActThreads - 1) / kActThreads;
   float xnext[NXI];
@@ -521,7 +525,7 @@ __global__ __launch_bounds__(512) void k_values(ValuesArgs a) {
     }
     load_obs(b + gridDim.x);
     lds_barrier();
-    trunk_rows<NTO, NHT, 2>(w1, w2, lds, 1, tid);
+    trunk_rows<NTO, NHT, R / 16>(w1, w2, lds, 1, tid);
     if (tid < R && row0 + tid < a.n) a.values[row0 + tid] = PRE[tid * LDP];
   }
 }
@@ -1047,12 +1051,15 @@ int launch_rollout(const RolloutArgs& a, hipStream_t s) {
 
 template <int NTO, int NHT>
 static int launch_values_t(const ValuesArgs& a, hipStream_t s) {
-  using GE = RollGeo<NTO, NHT, 32>;
-  const size_t lds = (size_t)GE::total * sizeof(float);
+  constexpr int R = val_rows<NTO>();
+  using GE = RollGeo<NTO, NHT, R>;
+  constexpr int total = GE::oXO + 2 * GE::OP;  // trunk regions + the observation statistics
+  static_assert(total * sizeof(float) <= 160 * 1024, "k_values LDS above 160 KB");
+  const size_t lds = (size_t)total * sizeof(float);
   static const bool ok = hipFuncSetAttribute((const void*)k_values<NTO, NHT>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
   if (!ok) return -2;
-  const long nblk = (a.n + 31) / 32;
+  const long nblk = (a.n + R - 1) / R;
   int dev = 0, ncu = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);

@@ -90,6 +90,10 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            or through registers in two (k_dwf); bitwise the same
  *   dw_rows=<n>, dw_slices=1|2  dW split-K geometry: rows per chunk (multiple of 16; 32 for the
  *                            64-wide agent) and k_dwf output slices; default: automatic
+ *   update_graph=0|1       ppo_update's minibatch launches eager (default) or replayed as one
+ *                            hipGraph captured on the second call (one process, gradstep=split,
+ *                            no profiling, no checkpoint snapshots); the Adam step constants come
+ *                            from a device table, so the result is bitwise the eager one
  *   rollout=auto|per_step    ppo_rollout_synth: persistent launch where supported, or per step
  *   gradstep=split|fused     clip_grad_norm_ + Adam: two launches (k_gradnorm, k_adam; default) or
  *                            one cooperative launch (k_gradstep: slower on ROCm 7, whose cooperative

@@ -182,6 +182,12 @@ struct ppo_ctx {
   int gradstep = 0;                     // create option gradstep=fused|split (default split)
   unsigned* gs_bar = nullptr;           // k_gradstep's grid barrier counter
   unsigned gs_count = 0;                // its arrivals so far
+  int update_graph = 0;                 // create option update_graph: replay the minibatch loop as a hipGraph
+  hipGraphExec_t upd_exec = nullptr;    // the captured loop (all epochs x minibatches)
+  const int32_t* upd_exec_perms = nullptr;
+  long upd_calls = 0;
+  float* sched = nullptr;               // per-minibatch (step size, sqrt(bc2)), AdamArgs::sched
+  std::vector<float> sched_host;
   float* beta_store = nullptr;          // persistent AC rollout: (alpha, beta, sample) per (t, env, action)
   // profiling
   unsigned prof_mask = 0;
@@ -265,6 +271,9 @@ struct CreateOptions {
   int dw_rows = 0;     // dW split-K rows per chunk (multiple of 16; 0: auto, ~128 chunks per trunk)
   int dw_slices = 0;   // k_dwf output slices per chunk (1 / 2; 0: auto, dw_slices())
   int dw_dma = 1;      // 1 (default): k_dwf_dma (LDS-DMA staging, three stage buffers); 0: k_dwf
+  // 1: ppo_update replays its minibatch launches as one captured hipGraph; 0 (default): eager. Not the
+  // default: a checkpoint snapshot's cross-stream wait (ppo_snapshot_state) then fails on this stack
+  int update_graph = 0;
 };
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
@@ -290,6 +299,7 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
       o->dw_rows = std::stoi(v);
     else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
     else if (k == "dw_dma" && (v == "0" || v == "1")) o->dw_dma = v[0] - '0';
+    else if (k == "update_graph" && (v == "0" || v == "1")) o->update_graph = v[0] - '0';
     else return fail("ppo_create_ex: unknown option or value: " + kv);
   }
   return 0;
@@ -345,6 +355,7 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   c->dw_dma = opt.dw_dma;
   c->rollout_mode = opt.rollout;
   c->gradstep = opt.gradstep;
+  c->update_graph = opt.update_graph;
   int upd_kernel = opt.upd_kernel;
 #ifdef PPO_DIAG
   {
@@ -460,6 +471,8 @@ extern "C" int ppo_destroy(ppo_t* c) {
   for (int k = 0; k < 4; ++k)
     if (c->dwslab[k]) (void)hipFree(c->dwslab[k]);
   if (c->perms) (void)hipFree(c->perms);
+  if (c->upd_exec) (void)hipGraphExecDestroy(c->upd_exec);
+  if (c->sched) (void)hipFree(c->sched);
   if (c->advpart) (void)hipFree(c->advpart);
   comm_detach(c);
   if (c->snap) (void)hipFree(c->snap);
@@ -890,6 +903,8 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   }
   const long trainable_n = c->K.size - tb;
 
+  // the minibatch launch sequence; with graph, the Adam step constants come from c->sched[gi]
+  auto enqueue = [&](bool graph) -> int {
   for (int e = 0; e < EP; ++e) {
     for (int mb = 0; mb < MB; ++mb) {
       const int gi = e * MB + mb;
@@ -917,11 +932,16 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
         launch_colsum(cs, ns, maxlen, s);
       }
       if (multi && allreduce(c, c->G + tb, trainable_n, 1, s)) return -3;  // ac:877-885, before the clip
-      c->adam_step += 1;
-      const double bc1 = 1.0 - std::pow(0.9, (double)c->adam_step);
-      const double bc2 = 1.0 - std::pow(0.999, (double)c->adam_step);
-      ad.step_size = (float)((double)lr / bc1);
-      ad.sbc2 = (float)std::sqrt(bc2);
+      if (graph) {
+        ad.sched = c->sched;
+        ad.gi = gi;
+      } else {
+        c->adam_step += 1;
+        const double bc1 = 1.0 - std::pow(0.9, (double)c->adam_step);
+        const double bc2 = 1.0 - std::pow(0.999, (double)c->adam_step);
+        ad.step_size = (float)((double)lr / bc1);
+        ad.sbc2 = (float)std::sqrt(bc2);
+      }
       ad.stat_out = st + 6;  // the total norm of this minibatch next to its loss stats
       if (c->gradstep) {  // clip_grad_norm_ + Adam: one cooperative launch (profile class "adam")
         ProfScope ps(c, PK_ADAM, s);
@@ -936,6 +956,51 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
       }
     }
   }
+  return 0;
+  };
+  // hipGraph replay (update_graph=1, one process, split clip + Adam, no profiling events): captured
+  // on the second call (the first warms the launchers' one-time attribute calls), re-captured when
+  // the permutation buffer changes; every captured kernel argument is fixed across iterations
+  const bool use_graph = c->update_graph && !multi && !c->gradstep && c->prof_mask == 0;
+  if (use_graph && c->upd_calls > 0) {
+    const int n = EP * MB;
+    if (!c->sched && dmalloc(&c->sched, 2 * (size_t)n)) return -2;
+    c->sched_host.resize(2 * (size_t)n);
+    for (int gi = 0; gi < n; ++gi) {  // the eager path's per-step constants, same expressions
+      const long t = c->adam_step + 1 + gi;
+      const double bc1 = 1.0 - std::pow(0.9, (double)t);
+      const double bc2 = 1.0 - std::pow(0.999, (double)t);
+      c->sched_host[2 * gi] = (float)((double)lr / bc1);
+      c->sched_host[2 * gi + 1] = (float)std::sqrt(bc2);
+    }
+    HIP_TRY(hipMemcpyAsync(c->sched, c->sched_host.data(), sizeof(float) * 2 * n, hipMemcpyHostToDevice, s));
+    if (!c->upd_exec || c->upd_exec_perms != perms) {
+      if (c->upd_exec) (void)hipGraphExecDestroy(c->upd_exec);
+      c->upd_exec = nullptr;
+      HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      const int rc = enqueue(true);
+      hipGraph_t g = nullptr;
+      const hipError_t ec = hipStreamEndCapture(s, &g);
+      if (rc != 0) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+      }
+      if (ec != hipSuccess) return fail(std::string("ppo_update: graph capture: ") + hipGetErrorString(ec));
+      const hipError_t ei = hipGraphInstantiate(&c->upd_exec, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      if (ei != hipSuccess) {
+        c->upd_exec = nullptr;
+        return fail(std::string("ppo_update: graph instantiate: ") + hipGetErrorString(ei));
+      }
+      c->upd_exec_perms = perms;
+    }
+    HIP_TRY(hipGraphLaunch(c->upd_exec, s));
+    c->adam_step += n;
+  } else {
+    const int rc = enqueue(false);
+    if (rc != 0) return rc;
+  }
+  c->upd_calls += 1;
   HIP_TRY(hipGetLastError());
   c->iteration += 1;
   if (out) {

@@ -1387,8 +1387,10 @@ PPO_DEV void adam_block(const AdamArgs& a, int bid, float* s_norm, float& s_coef
   const float v = a.v[p] * 0.999f + gv * gv * 0.001f;
   a.m[p] = m;
   a.v[p] = v;
-  const float denom = sqrtf(v) / a.sbc2 + a.eps;
-  const float np = a.param[p] - a.step_size * (m / denom);
+  const float sbc2 = a.sched ? a.sched[2 * a.gi + 1] : a.sbc2;
+  const float step_size = a.sched ? a.sched[2 * a.gi] : a.step_size;
+  const float denom = sqrtf(v) / sbc2 + a.eps;
+  const float np = a.param[p] - step_size * (m / denom);
   a.param[p] = np;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {

@@ -147,6 +147,11 @@ struct AdamArgs {
   long w1_off[2];
   float* wsw[2];  // swizzled copies (sw_index), refreshed with the parameters
   int OP;
+  // update graph (create option update_graph=1): the step size and sqrt(1 - 0.999^t) of minibatch gi
+  // come from sched[2 gi], sched[2 gi + 1] (written by the host before every replay) instead of
+  // step_size / sbc2, so the captured launch sequence stays valid across iterations
+  const float* sched;
+  int gi;
 };
 
 struct GaeArgs {

@@ -106,3 +106,27 @@ def test_gradstep_fused_equals_split(agent, env_id, E, T, mb):
     assert st[0]["grad_norm"] == st[1]["grad_norm"]
     for tr in trs:
         tr.close()
+
+
+@pytest.mark.parametrize("agent,env_id,E,T,mb,it", [("ac", "HalfCheetah-v5", 256, 128, 4, 3), ("ppo", "Humanoid-v4", 64, 64, 32, 3),
+                                                    ("ppo", "HalfCheetah-v5", 1, 256, 4, 4), ("ac", "Ant-v5", 96, 64, 2, 3)])
+def test_update_graph_equals_eager(agent, env_id, E, T, mb, it):
+    """ppo_update's minibatch loop replayed as one captured hipGraph (update_graph=1: eager on the
+    first call, captured on the second, replayed after) against the eager launches: the Adam step
+    constants come from a device table written before each replay, everything else is the same
+    launch sequence, so parameters, Adam moments and the per-minibatch stats are bitwise equal over
+    several iterations with the annealed learning rate."""
+    C = ppo_amd.ACPPOConfig if agent == "ac" else ppo_amd.PPOConfig
+    cfg = C(env_id=env_id, num_envs=E, num_steps=T, num_minibatches=mb, update_epochs=2, total_timesteps=E * T * it)
+    trs = [ppo_amd.Trainer(cfg, options="gradstep=split,update_graph=0"), ppo_amd.Trainer(cfg, options="gradstep=split,update_graph=1")]
+    for i in range(it):
+        st = [tr.iterate(want_stats=True) for tr in trs]
+        np.testing.assert_array_equal(trs[0].agent.params(), trs[1].agent.params(), err_msg=f"iteration {i}")
+        assert st[0] == st[1], i
+    m0, v0, s0 = trs[0].agent.adam_state()
+    m1, v1, s1 = trs[1].agent.adam_state()
+    np.testing.assert_array_equal(m0, m1)
+    np.testing.assert_array_equal(v0, v1)
+    assert s0 == s1
+    for tr in trs:
+        tr.close()

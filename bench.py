@@ -190,8 +190,8 @@ def main():
                     help="N > 1 data path: RCCL (one GPU per rank), or the host transport over gloo with every "
                          "rank on GPU 0 (rehearses this script's multi-rank path on a one-GPU box)")
     ap.add_argument("--comm-1rank", action="store_true",
-                    help="N = 1 only: attach a one-rank RCCL communicator, so the distributed update sequence "
-                         "(split gradient all-reduce on its side stream) runs and its cost can be timed")
+                    help="N = 1 only: attach a one-rank RCCL communicator, so the distributed update path "
+                         "(advantage-statistics and in-stream gradient all-reduces) runs and its cost can be timed")
     ap.add_argument("--options", default=None, help="ppo_create_ex options (kernel / geometry A/B runs)")
     args = ap.parse_args()
 
@@ -209,14 +209,29 @@ def main():
     if world > 1:
         import torch.distributed as dist  # gloo (CPU) only for rendezvous, barriers and timing max
         dist.init_process_group("gloo")
-    ppo_amd.set_device(0 if args.comm == "host" else local_rank)
+    # one GPU per rank (the reference's cudaSetDevice(gpu_ids.at(local_rank)), ac:447-448 / :459-460);
+    # only the host-transport rehearsal puts every rank on GPU 0 on purpose
+    device = 0 if args.comm == "host" else local_rank
+    ppo_amd.set_device(device)
 
     E_total = args.num_envs if args.scaling == "strong" else args.num_envs * world
     E = E_total // world
     T = args.num_steps
     cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=E_total, num_steps=T,
                               total_timesteps=E_total * T * (args.steps + args.warmup + 1))
-    tr = ppo_amd.Trainer(cfg, num_envs_per_device=E, rank=rank, world_size=world, options=args.options)
+    tr = ppo_amd.Trainer(cfg, num_envs_per_device=E, rank=rank, world_size=world, device=device,
+                         options=args.options)
+    dev_ord, dev_bus = tr.agent.device()
+    if dev_ord != device:
+        raise SystemExit(f"bench.py: rank {rank} asked for device {device} but its context is on {dev_ord}")
+    devices = [(dev_ord, dev_bus)]
+    if world > 1:
+        devices = [None] * world
+        dist.all_gather_object(devices, (dev_ord, dev_bus))
+        buses = [b for _, b in devices]
+        if args.comm == "rccl" and len(set(buses)) != world:
+            raise SystemExit(f"bench.py: ranks share a GPU under RCCL (PCI bus ids {buses}); one GPU per rank "
+                             f"is required")
     if world > 1:
         if args.comm == "host":
             import torch
@@ -303,6 +318,7 @@ def main():
                        "num_envs": E_total, "num_envs_per_device": E, "num_steps": T,
                        "minibatch_per_device": E * T // cfg.num_minibatches, "parallelism": f"dp{world}",
                        "comm_ranks": comm_world, "comm_kind": comm_kind,
+                       "devices": [d for d, _ in devices], "device_pci_bus_ids": [b for _, b in devices],
                        **({"comm": "host transport (gloo), all ranks on GPU 0: rehearsal, not a scaling number"}
                           if world > 1 and args.comm == "host" else {})},
             "roofline": roof,

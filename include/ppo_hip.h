@@ -92,8 +92,9 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            64-wide agent) and k_dwf output slices; default: automatic
  *   update_graph=0|1       ppo_update's minibatch launches eager (default) or replayed as one
  *                            hipGraph captured on the second call (one process, gradstep=split,
- *                            no profiling, no checkpoint snapshots); the Adam step constants come
- *                            from a device table, so the result is bitwise the eager one
+ *                            no profiling); the Adam step constants come from a device table, so
+ *                            the result is bitwise the eager one. Checkpoint snapshots work with it
+ *                            (ppo_read_snapshot waits on the host, never across streams)
  *   rollout=auto|per_step    ppo_rollout_synth: persistent launch where supported, or per step
  *   gradstep=split|fused     clip_grad_norm_ + Adam: two launches (k_gradnorm, k_adam; default) or
  *                            one cooperative launch (k_gradstep: slower on ROCm 7, whose cooperative
@@ -142,8 +143,10 @@ int ppo_debug_last_grad(ppo_t* ctx, float* host, long n);
 /* Asynchronous checkpoint source (the reference saves agent + optimizer every iteration inside its
  * SPS span, ppo:545-563 / ac:904-927): ppo_snapshot_state enqueues a device-side copy of the
  * parameters and the Adam state on the context stream (ordered after the last update, before the
- * next) and returns at once; ppo_read_snapshot, callable from another host thread, waits for that
- * copy only and unpacks it in the flat reference order. One snapshot buffer: call
+ * next) and returns at once; ppo_read_snapshot, callable from another host thread, waits (on the
+ * host, hipEventSynchronize) for that copy only and unpacks it in the flat reference order — no
+ * cross-stream dependency, so it is safe while the context stream is being captured into a hipGraph
+ * (update_graph=1). One snapshot buffer: call
  * ppo_read_snapshot before the next ppo_snapshot_state. */
 int ppo_snapshot_state(ppo_t* ctx);
 int ppo_read_snapshot(ppo_t* ctx, float* params_host, float* m_host, float* v_host, long n, long* step);
@@ -176,6 +179,11 @@ int ppo_comm_allreduce(ppo_t* ctx, float* buf_dev, long n, int average);
  * (distributed.cpp:66-79). */
 enum { PPO_COMM_NONE = 0, PPO_COMM_RCCL = 1, PPO_COMM_HOST = 2 };
 int ppo_comm_info(const ppo_t* ctx, int* kind, int* rank, int* world);
+/* The HIP device the context lives on (the `device` of ppo_create, the reference's
+ * cudaSetDevice(gpu_ids.at(local_rank)), ac:447-448 / :459-460) and that device's PCI bus id
+ * (hipDeviceGetPCIBusId, e.g. "0000:05:00.0"; pass NULL / 0 to skip). Launchers compare the bus ids
+ * of all ranks: two ranks on one GPU is an error under RCCL. */
+int ppo_get_device(const ppo_t* ctx, int* device, char* pci_bus_id, int len);
 
 /* ---- device memory helpers (so C / ctypes callers need no HIP headers) ---- */
 int ppo_set_device(int device);

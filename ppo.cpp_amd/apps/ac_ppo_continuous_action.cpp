@@ -157,7 +157,14 @@ int main(int argc, const char** argv) {
     return 3;
   }
   // The agent always runs on the MI355X (the reference's cpu options exist for LibTorch CPU runs).
-  const int device = config.gpu_ids.at((size_t)local_rank % config.gpu_ids.size());
+  // gpu_ids.at(local_rank) as the reference indexes it (ac:447-448 / :459-460): a list shorter than
+  // the local rank count is an error, never a silent wrap onto another rank's GPU
+  if ((size_t)local_rank >= config.gpu_ids.size()) {
+    std::cerr << "local rank " << local_rank << " has no entry in --gpu_ids (" << config.gpu_ids.size()
+              << " given): pass one --gpu_ids per local rank\n";
+    return 2;
+  }
+  const int device = config.gpu_ids.at((size_t)local_rank);
 
   const fs::path exe = fs::canonical(argv[0]);
   const fs::path exp_folder = exe.parent_path() / ".." / "models" / config.exp_name;

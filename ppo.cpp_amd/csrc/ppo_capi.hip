@@ -187,7 +187,9 @@ struct ppo_ctx {
   const int32_t* upd_exec_perms = nullptr;
   long upd_calls = 0;
   float* sched = nullptr;               // per-minibatch (step size, sqrt(bc2)), AdamArgs::sched
-  std::vector<float> sched_host;
+  float* sched_host[2] = {};            // pinned staging of that table, alternating per replay
+  hipEvent_t sched_ev[2] = {};          // the H2D copy out of sched_host[i] has completed
+  int sched_flip = 0;
   float* beta_store = nullptr;          // persistent AC rollout: (alpha, beta, sample) per (t, env, action)
   // profiling
   unsigned prof_mask = 0;
@@ -294,9 +296,9 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
     else if (k == "rollout" && (v == "auto" || v == "per_step"))
       o->rollout = v == "auto" ? PPO_ROLLOUT_AUTO : PPO_ROLLOUT_PER_STEP;
     else if (k == "gradstep" && (v == "fused" || v == "split")) o->gradstep = v == "fused";
-    else if (k == "dw_rows" && !v.empty() && v.find_first_not_of("0123456789") == std::string::npos &&
-             std::stoi(v) % 16 == 0 && std::stoi(v) >= 16 && std::stoi(v) <= 65536)
-      o->dw_rows = std::stoi(v);
+    else if (k == "dw_rows" && !v.empty() && v.size() <= 5 && v.find_first_not_of("0123456789") == std::string::npos &&
+             atoi(v.c_str()) % 16 == 0 && atoi(v.c_str()) >= 16 && atoi(v.c_str()) <= 65536)
+      o->dw_rows = atoi(v.c_str());  // at most 5 digits: no overflow, no exception across the C-ABI
     else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
     else if (k == "dw_dma" && (v == "0" || v == "1")) o->dw_dma = v[0] - '0';
     else if (k == "update_graph" && (v == "0" || v == "1")) o->update_graph = v[0] - '0';
@@ -324,6 +326,13 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   const long B = (long)cfg->num_envs * cfg->num_steps;
   if (B % cfg->num_minibatches) return fail("ppo_create: num_steps*num_envs must divide by num_minibatches");
   if (B >= (1L << 31)) return fail("ppo_create: batch too large");
+  {
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev)  // the reference's gpu_ids.at(local_rank) throws here (ac:447)
+      return fail("ppo_create: device " + std::to_string(device) + " requested but " + std::to_string(ndev) +
+                  " HIP device(s) are visible");
+  }
   HIP_TRY(hipSetDevice(device));
   ppo_t* c = new ppo_t();
   c->cfg = *cfg;
@@ -473,6 +482,10 @@ extern "C" int ppo_destroy(ppo_t* c) {
   if (c->perms) (void)hipFree(c->perms);
   if (c->upd_exec) (void)hipGraphExecDestroy(c->upd_exec);
   if (c->sched) (void)hipFree(c->sched);
+  for (int i = 0; i < 2; ++i) {
+    if (c->sched_host[i]) (void)hipHostFree(c->sched_host[i]);
+    if (c->sched_ev[i]) (void)hipEventDestroy(c->sched_ev[i]);
+  }
   if (c->advpart) (void)hipFree(c->advpart);
   comm_detach(c);
   if (c->snap) (void)hipFree(c->snap);
@@ -964,16 +977,27 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   const bool use_graph = c->update_graph && !multi && !c->gradstep && c->prof_mask == 0;
   if (use_graph && c->upd_calls > 0) {
     const int n = EP * MB;
-    if (!c->sched && dmalloc(&c->sched, 2 * (size_t)n)) return -2;
-    c->sched_host.resize(2 * (size_t)n);
+    if (!c->sched) {
+      if (dmalloc(&c->sched, 2 * (size_t)n)) return -2;
+      for (int i = 0; i < 2; ++i) {
+        HIP_TRY(hipHostMalloc((void**)&c->sched_host[i], sizeof(float) * 2 * n, hipHostMallocDefault));
+        HIP_TRY(hipEventCreateWithFlags(&c->sched_ev[i], hipEventDisableTiming));
+      }
+    }
+    // the staging buffer alternates per replay; before refilling one, wait until the copy that last
+    // read it (two replays ago) has completed — back-to-back replays never overwrite a pending copy
+    float* sh = c->sched_host[c->sched_flip];
+    HIP_TRY(hipEventSynchronize(c->sched_ev[c->sched_flip]));
     for (int gi = 0; gi < n; ++gi) {  // the eager path's per-step constants, same expressions
       const long t = c->adam_step + 1 + gi;
       const double bc1 = 1.0 - std::pow(0.9, (double)t);
       const double bc2 = 1.0 - std::pow(0.999, (double)t);
-      c->sched_host[2 * gi] = (float)((double)lr / bc1);
-      c->sched_host[2 * gi + 1] = (float)std::sqrt(bc2);
+      sh[2 * gi] = (float)((double)lr / bc1);
+      sh[2 * gi + 1] = (float)std::sqrt(bc2);
     }
-    HIP_TRY(hipMemcpyAsync(c->sched, c->sched_host.data(), sizeof(float) * 2 * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->sched, sh, sizeof(float) * 2 * n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(c->sched_ev[c->sched_flip], s));
+    c->sched_flip ^= 1;
     if (!c->upd_exec || c->upd_exec_perms != perms) {
       if (c->upd_exec) (void)hipGraphExecDestroy(c->upd_exec);
       c->upd_exec = nullptr;
@@ -1057,7 +1081,9 @@ extern "C" int ppo_read_snapshot(ppo_t* c, float* p, float* m, float* v, long n,
   HIP_TRY(hipSetDevice(c->device));
   const size_t K = c->K.size;
   std::vector<float> h(3 * K);
-  HIP_TRY(hipStreamWaitEvent(c->snap_stream, c->snap_ev, 0));
+  // a host wait, not hipStreamWaitEvent: a cross-stream dependency on the context stream is refused
+  // while the owner thread captures that stream into the update hipGraph (update_graph=1)
+  HIP_TRY(hipEventSynchronize(c->snap_ev));
   HIP_TRY(hipMemcpyAsync(h.data(), c->snap, 3 * K * sizeof(float), hipMemcpyDeviceToHost, c->snap_stream));
   HIP_TRY(hipStreamSynchronize(c->snap_stream));
   if (p) unpack_params(c->K, c->L, h.data(), p);
@@ -1170,8 +1196,20 @@ extern "C" int ppo_comm_info(const ppo_t* c, int* kind, int* rank, int* world) {
 // ------------------------------------------------------------------------------------------
 // device helpers
 // ------------------------------------------------------------------------------------------
+extern "C" int ppo_get_device(const ppo_t* c, int* device, char* pci_bus_id, int len) {
+  if (!c || !device) return fail("ppo_get_device: null argument");
+  *device = c->device;
+  if (pci_bus_id && len > 0) HIP_TRY(hipDeviceGetPCIBusId(pci_bus_id, len, c->device));
+  return 0;
+}
+
 extern "C" int ppo_set_device(int d) {
   if (int rc = ppo_runtime_check()) return rc;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (d < 0 || d >= ndev)
+    return fail("ppo_set_device: device " + std::to_string(d) + " requested but " + std::to_string(ndev) +
+                " HIP device(s) are visible");
   HIP_TRY(hipSetDevice(d));
   return 0;
 }

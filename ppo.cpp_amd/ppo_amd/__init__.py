@@ -158,6 +158,7 @@ SYMBOLS = [
     ("ppo_comm_broadcast_params", _I, [_VP, _I]),
     ("ppo_comm_allreduce", _I, [_VP, _FP, _L, _I]),
     ("ppo_comm_info", _I, [_VP, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
+    ("ppo_get_device", _I, [_VP, C.POINTER(_I), C.c_char_p, _I]),
     ("ppo_set_device", _I, [_I]),
     ("ppo_device_count", _I, [C.POINTER(_I)]),
     ("ppo_dev_malloc", _I, [C.POINTER(_VP), _SZ]),
@@ -603,6 +604,13 @@ class Agent:
     def comm_allreduce(self, buf: DeviceArray, average=True):
         check(lib().ppo_comm_allreduce(self.h, buf.ptr, int(np.prod(buf.shape)), int(average)))
         self.sync()
+
+    def device(self):
+        """(device ordinal, PCI bus id) the context runs on (ppo_get_device)."""
+        d = C.c_int(-1)
+        bus = C.create_string_buffer(64)
+        check(lib().ppo_get_device(self.h, C.byref(d), bus, 64))
+        return d.value, bus.value.decode()
 
     def set_rollout_mode(self, per_step: bool):
         """ppo_rollout_synth: one persistent launch (default, where supported) or per-step launches."""

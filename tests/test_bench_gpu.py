@@ -28,6 +28,32 @@ def test_bench_single_rank_line():
     roof = d["roofline"]
     assert roof["bound"] == "mfma" and 0 < roof["frac"] < 1 and roof["peak"] == 157.3
     assert abs(d["value"] - 512 * 128 / (d["ms_per_step"] / 1e3)) / d["value"] < 0.01
+    assert d["config"]["devices"] == [0] and len(d["config"]["device_pci_bus_ids"]) == 1
+
+
+def test_bench_one_rank_rccl_reports_its_device():
+    """`--comm-1rank`: a one-rank RCCL communicator on the rank's own device; the line names it."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--comm-1rank",
+                        "--no-cli", "--no-cpu-baseline", "--num-envs", "512"], capture_output=True, text=True,
+                       timeout=300, cwd=ROOT, check=True)
+    d = last_json(r.stdout)
+    assert d["config"]["devices"] == [0]
+    assert d["config"]["comm_kind"] == "rccl" and d["config"]["comm_ranks"] == 1
+
+
+def test_bench_rank_without_its_gpu_fails_loudly():
+    """Rank k runs on GPU k (the reference's cudaSetDevice(gpu_ids.at(local_rank)), ac:447-448). A
+    rank whose LOCAL_RANK names a GPU the box does not have must fail with a message naming that
+    device -- never fall back silently onto GPU 0."""
+    import ppo_amd
+    n = ppo_amd.device_count()
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK=str(n))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0", "--no-cli",
+                        "--no-cpu-baseline", "--num-envs", "512"], capture_output=True, text=True, timeout=300,
+                       cwd=ROOT, env=env)
+    assert r.returncode != 0
+    assert f"device {n} requested but {n} HIP device(s) are visible" in r.stderr, r.stderr[-2000:]
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
 
 
 def test_bench_two_ranks_host_transport():
@@ -41,6 +67,7 @@ def test_bench_two_ranks_host_transport():
         assert k in d, k
     assert d["n_gpus"] == 2 and d["config"]["num_envs_per_device"] == 512 and d["config"]["parallelism"] == "dp2"
     assert d["value"] > 0 and "comm" in d["config"]
+    assert d["config"]["devices"] == [0, 0] and d["config"]["comm_ranks"] == 2  # the rehearsal: both on GPU 0
 
 
 def test_bench_gpus_flag_starts_the_ranks_itself():

@@ -26,7 +26,7 @@ def declared_functions():
 def test_headers_declare_the_boundary():
     names = declared_functions()
     for required in ("ppo_create", "ppo_get_action_and_value", "ppo_rollout_act", "ppo_compute_gae", "ppo_update",
-                     "ppo_comm_init", "ppo_comm_info", "psyn_step", "pwrap_step", "psyn_attach_wrappers",
+                     "ppo_comm_init", "ppo_comm_info", "ppo_get_device", "psyn_step", "pwrap_step", "psyn_attach_wrappers",
                      "ppo_set_rollout_mode"):
         assert required in names
 
@@ -145,7 +145,7 @@ import ppo_amd
 lib = ppo_amd.lib()
 out = []
 for opt in ("upd_kernel=fast", "act_kernel=3", "bogus=1", "dw_fused", "rollout=sometimes", "dw_dma=2",
-            "dw_rows=24", "dw_rows=0", "dw_rows=x", "dw_slices=3", "update_graph=2"):
+            "dw_rows=24", "dw_rows=0", "dw_rows=x", "dw_rows=99999999999", "dw_slices=3", "update_graph=2"):
     cfg = ppo_amd.HipConfig(net_kind=1, obs_dim=17, act_dim=6, hidden=256, num_envs=64, num_steps=8,
                             num_minibatches=1, update_epochs=1)
     ctx = ctypes.c_void_p()
@@ -163,3 +163,20 @@ print(json.dumps(out))
     assert res.returncode == 0, res.stderr[-2000:]
     for rc, has_ctx, err in json.loads(res.stdout.strip().splitlines()[-1]):
         assert rc != 0 and not has_ctx and ("ppo_create_ex" in err or "ppo_carla_create_ex" in err), err
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "ppo.cpp_amd", "bin", "ac_ppo_continuous_action")),
+                    reason="CLI not built")
+def test_ac_cli_refuses_a_rank_without_a_gpu_id(tmp_path):
+    """The reference picks its GPU as gpu_ids.at(local_rank) (ac:447-448 / :459-460), which throws
+    for a rank without an entry; the drop-in CLI refuses such a rank with a message and exit code 2
+    before any HIP call (so this runs without a GPU), instead of wrapping onto another rank's GPU."""
+    import subprocess
+    exe = os.path.join(ROOT, "ppo.cpp_amd", "bin", "ac_ppo_continuous_action")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "OMPI_COMM_WORLD_RANK",
+                                                             "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK")}
+    env["LOCAL_RANK"] = "1"
+    r = subprocess.run([exe, "--env_backend", "device", "--total_timesteps", "1024", "--exp_name_stem", "refuse"],
+                       capture_output=True, text=True, timeout=60, env=env, cwd=tmp_path)
+    assert r.returncode == 2, (r.returncode, r.stdout, r.stderr)
+    assert "local rank 1 has no entry in --gpu_ids" in r.stderr

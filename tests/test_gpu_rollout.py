@@ -87,14 +87,14 @@ def test_persistent_rollout_metric_shape_properties():
 @pytest.mark.parametrize("agent,env_id,E,T,mb", [("ac", "HalfCheetah-v5", 256, 128, 4), ("ppo", "Humanoid-v4", 64, 64, 32),
                                                  ("ppo", "HalfCheetah-v5", 1, 256, 4)])
 def test_gradstep_fused_equals_split(agent, env_id, E, T, mb):
-    """clip_grad_norm_ + Adam as one cooperative launch (k_gradstep: the norm slices, a grid barrier,
-    the Adam blocks; the default) against the two launches k_gradnorm + k_adam (gradstep=split):
-    the same functions in the same order, so parameters, Adam moments and the per-minibatch total
-    norm are bitwise equal after two iterations (many minibatches: the barrier counter runs across
-    launches)."""
+    """clip_grad_norm_ + Adam as one cooperative launch (k_gradstep, gradstep=fused: the norm slices,
+    a grid barrier, the Adam blocks) against the two launches k_gradnorm + k_adam (gradstep=split,
+    the default): the same functions in the same order, so parameters, Adam moments and the
+    per-minibatch total norm are bitwise equal after two iterations (many minibatches: the barrier
+    counter runs across launches)."""
     C = ppo_amd.ACPPOConfig if agent == "ac" else ppo_amd.PPOConfig
     cfg = C(env_id=env_id, num_envs=E, num_steps=T, num_minibatches=mb, update_epochs=2, total_timesteps=E * T * 4)
-    trs = [ppo_amd.Trainer(cfg), ppo_amd.Trainer(cfg, options="gradstep=split")]
+    trs = [ppo_amd.Trainer(cfg, options="gradstep=fused"), ppo_amd.Trainer(cfg, options="gradstep=split")]
     for _ in range(2):
         st = [tr.iterate(want_stats=True) for tr in trs]
     np.testing.assert_array_equal(trs[0].agent.params(), trs[1].agent.params())
@@ -129,4 +129,54 @@ def test_update_graph_equals_eager(agent, env_id, E, T, mb, it):
     np.testing.assert_array_equal(v0, v1)
     assert s0 == s1
     for tr in trs:
+        tr.close()
+
+
+@pytest.mark.parametrize("agent,env_id,E,T,mb", [("ac", "HalfCheetah-v5", 256, 128, 4), ("ppo", "HalfCheetah-v5", 1, 256, 4)])
+def test_update_graph_back_to_back_and_snapshots(agent, env_id, E, T, mb):
+    """update_graph=1 without a host sync between replays (want_stats=False: the Adam step table is
+    restaged every replay while earlier copies may still be pending), and the checkpoint snapshot the
+    CLI takes every iteration (ppo_snapshot_state on the context stream, ppo_read_snapshot from a
+    writer thread while the next update is captured / replayed: ac:904-927). Parameters and Adam
+    state are bitwise the eager run's, and every snapshot holds exactly the state after its iteration."""
+    import ctypes
+    import threading
+    C = ppo_amd.ACPPOConfig if agent == "ac" else ppo_amd.PPOConfig
+    it = 5
+    cfg = C(env_id=env_id, num_envs=E, num_steps=T, num_minibatches=mb, update_epochs=2, total_timesteps=E * T * it)
+    eager = ppo_amd.Trainer(cfg, options="update_graph=0")
+    graph = ppo_amd.Trainer(cfg, options="update_graph=1")
+    lib = ppo_amd.lib()
+    P = graph.agent.num_params
+    ref, snaps, errs = [], [], []
+    for i in range(it):
+        eager.iterate(want_stats=False)
+        ref.append(eager.agent.params())
+    graph.iterate(want_stats=False)
+    for k in range(it):
+        ppo_amd.check(lib.ppo_snapshot_state(graph.agent.h))
+        p = np.zeros(P, np.float32)
+
+        def reader(p=p):
+            st = ctypes.c_long()
+            if lib.ppo_read_snapshot(graph.agent.h, p.ctypes.data, None, None,
+                                     P, ctypes.byref(st)) != 0:
+                errs.append(lib.ppo_last_error().decode())
+        th = threading.Thread(target=reader)
+        th.start()
+        if k + 1 < it:  # the next iteration (its update captured on the second call) beside the reader
+            graph.iterate(want_stats=False)
+        th.join()
+        snaps.append(p)
+    assert not errs, errs
+    for k in range(it):
+        np.testing.assert_array_equal(snaps[k], ref[k], err_msg=f"snapshot after iteration {k}")
+    graph.agent.sync()
+    np.testing.assert_array_equal(graph.agent.params(), eager.agent.params())
+    m0, v0, s0 = eager.agent.adam_state()
+    m1, v1, s1 = graph.agent.adam_state()
+    np.testing.assert_array_equal(m0, m1)
+    np.testing.assert_array_equal(v0, v1)
+    assert s0 == s1
+    for tr in (eager, graph):
         tr.close()

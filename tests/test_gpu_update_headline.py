@@ -3,8 +3,10 @@
 At the metric config (AC 2x256 LN/Beta, HalfCheetah O=17 / A=6, E=4096, T=128, 4 minibatches) each
 minibatch is M = 131 072 rows, so every k_upd workgroup walks 16 row tiles and accumulates its slab
 of small gradients across them, and k_dwf sums 128 split-K chunks; the cfg4 shard (Ant O=105 / A=8,
-E=1024 per GPU) runs M = 32 768. Here one update with one minibatch of exactly that size
-(T=32, MB=1, EP=1 gives the same M, tiles per workgroup and chunk count) is compared with the
+E=1024 per GPU) runs M = 32 768; cfg2 (PPO 2x64 tanh / Normal, Humanoid O=376 / A=17, E=1024,
+T=2048, 32 minibatches) runs M = 65 536 through k_upd2 and k_dw2_dma. Here one update with one
+minibatch of exactly that size (T x E with MB=1, EP=1 gives the same M, tiles per workgroup and
+chunk count) is compared with the
 oracle's gradient over the same gathered rows (oracle/ppo_oracle.c orc_minibatch_grad_part, row
 chunks on a thread pool, partials added in a fixed order) and with the oracle's clip_grad_norm_ +
 Adam step applied to the oracle's gradient.
@@ -32,9 +34,14 @@ from ppo_amd import DeviceArray  # noqa: E402
 from test_gpu_parity import fill_storage, make_agent, random_params, rel  # noqa: E402
 
 
-@pytest.mark.parametrize("name,O_,A,E", [("metric_halfcheetah", 17, 6, 4096), ("cfg4_shard_ant", 105, 8, 1024)])
-def test_headline_minibatch_update_vs_oracle(name, O_, A, E):
-    kind, H, T = 1, 256, 32
+@pytest.mark.parametrize("name,kind,H,O_,A,E,T,clip,ent,lr", [
+    ("metric_halfcheetah", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4),
+    ("cfg4_shard_ant", 1, 256, 105, 8, 1024, 32, 0.1, 0.01, 2.5e-4),
+    # cfg2: ppo_continuous_action Humanoid-v4, E=1024, T=2048, 32 minibatches -> M = 65 536 rows
+    # (ppo:489-542; clip 0.2, ent_coef 0, lr 3e-4, ppo:60-67): k_upd2 walks 128 32-row tiles per
+    # workgroup pair and k_dw2_dma sums 256 split-K chunks of 256 rows
+    ("cfg2_humanoid", 0, 64, 376, 17, 1024, 64, 0.2, 0.0, 3e-4)])
+def test_headline_minibatch_update_vs_oracle(name, kind, H, O_, A, E, T, clip, ent, lr):
     M = E * T
     rng = np.random.default_rng(31)
     L = O.layout_init(kind, O_, A, H)
@@ -50,12 +57,12 @@ def test_headline_minibatch_update_vs_oracle(name, O_, A, E):
     _, lp, _, v = ag0.get_action_and_value(DeviceArray.from_numpy(x), ppo_amd.PPO_GIVEN, DeviceArray.from_numpy(act))
     lp, v = lp.numpy(), v.numpy()
     ag0.close()
-    olp = (lp + rng.standard_normal(M) * 0.1).astype(np.float32)
+    olp = (lp + rng.standard_normal(M) * clip).astype(np.float32)
     ov = (v + rng.standard_normal(M) * 0.1).astype(np.float32)
     perm = rng.permutation(M).astype(np.int32)
-    clip, lr, mgn, eps = 0.1, 2.5e-4, 0.5, 1e-5
+    mgn, eps = 0.5, 1e-5
 
-    ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=clip, max_grad_norm=mgn, adam_eps=eps)
+    ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=clip, ent=ent, max_grad_norm=mgn, adam_eps=eps)
     ag.load_params(p)
     fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
     st = ag.update(lr, perms=DeviceArray.from_numpy(perm), want_stats=True)
@@ -63,7 +70,7 @@ def test_headline_minibatch_update_vs_oracle(name, O_, A, E):
     p1 = ag.params()
     ag.close()
 
-    cfg = O.LossCfg(clip, 0.01, 0.5, 1, 1)
+    cfg = O.LossCfg(clip, ent, 0.5, 1, 1)
     og, ost = O.minibatch_grad_parallel(L, p, x[perm], act[perm], olp[perm], adv[perm], ret[perm], ov[perm], cfg)
     assert rel(g, og) < 2e-4, rel(g, og)
     for t in range(L.ntensors):

@@ -51,17 +51,17 @@ PPO_DEV void act_layer(f4 (&acc)[2][RT], PBuf wb, int wlane, BF bfrag) {
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int t = 0; t < NKB; ++t) {
+    f4 b[RT];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const f4 b = bfrag(t, rt);
+    for (int rt = 0; rt < RT; ++rt) b[rt] = bfrag(t, rt);
+    // k-step c outermost: 2 RT independent accumulator chains interleaved (16x16x4 f32: 40-cycle
+    // dependent latency against a 32-cycle issue); each chain's order is unchanged
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        acc[u][rt] = mfma16(w[t % D][u].x, b.x, acc[u][rt]);
-        acc[u][rt] = mfma16(w[t % D][u].y, b.y, acc[u][rt]);
-        acc[u][rt] = mfma16(w[t % D][u].z, b.z, acc[u][rt]);
-        acc[u][rt] = mfma16(w[t % D][u].w, b.w, acc[u][rt]);
-      }
-    }
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[u][rt] = mfma16(w[t % D][u][c], b[rt][c], acc[u][rt]);
     if (t + D < NKB) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) w[t % D][u] = pld4(wb, wlane, 256 * (NKB * u + t + D));
@@ -161,17 +161,15 @@ template <int NKB, int RT, typename BF>
 PPO_DEV void act_layer_regs(f4 (&acc)[2][RT], const f4 (&w)[NKB][2], BF bfrag) {
 #pragma unroll
   for (int t = 0; t < NKB; ++t) {
+    f4 b[RT];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const f4 b = bfrag(t, rt);
+    for (int rt = 0; rt < RT; ++rt) b[rt] = bfrag(t, rt);
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        acc[u][rt] = mfma16(w[t][u].x, b.x, acc[u][rt]);
-        acc[u][rt] = mfma16(w[t][u].y, b.y, acc[u][rt]);
-        acc[u][rt] = mfma16(w[t][u].z, b.z, acc[u][rt]);
-        acc[u][rt] = mfma16(w[t][u].w, b.w, acc[u][rt]);
-      }
-    }
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[u][rt] = mfma16(w[t][u][c], b[rt][c], acc[u][rt]);
   }
 }
 

@@ -117,12 +117,9 @@ __global__ __launch_bounds__(256) void k_act4(ActArgs a) {
     for (int q = 0; q < NKW; ++q) {
       if (kb0 + q < NTO) {
 #pragma unroll
-        for (int ft = 0; ft < 4; ++ft) {
-          acc[ft] = mfma16(wa[q][ft].x, xv[q].x, acc[ft]);
-          acc[ft] = mfma16(wa[q][ft].y, xv[q].y, acc[ft]);
-          acc[ft] = mfma16(wa[q][ft].z, xv[q].z, acc[ft]);
-          acc[ft] = mfma16(wa[q][ft].w, xv[q].w, acc[ft]);
-        }
+        for (int c = 0; c < 4; ++c)  // 4 independent chains interleaved, each in its own order
+#pragma unroll
+          for (int ft = 0; ft < 4; ++ft) acc[ft] = mfma16(wa[q][ft][c], xv[q][c], acc[ft]);
       }
     }
 #pragma unroll

@@ -42,14 +42,13 @@ PPO_DEV void mm_layer(f4 (&out)[NT_OUT], const f4 (&in)[NT_IN], const float* __r
   }
 #pragma unroll
   for (int t = 0; t < NT_IN; ++t) {
+    f4 w[NT_OUT];
 #pragma unroll
-    for (int ot = 0; ot < NT_OUT; ++ot) {
-      const f4 w = pld4(wb, lo, 16 * ot * LDW + 16 * t);
-      out[ot] = mfma16(w.x, in[t].x, out[ot]);
-      out[ot] = mfma16(w.y, in[t].y, out[ot]);
-      out[ot] = mfma16(w.z, in[t].z, out[ot]);
-      out[ot] = mfma16(w.w, in[t].w, out[ot]);
-    }
+    for (int ot = 0; ot < NT_OUT; ++ot) w[ot] = pld4(wb, lo, 16 * ot * LDW + 16 * t);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)  // independent chains interleaved, each in its own order
+#pragma unroll
+      for (int ot = 0; ot < NT_OUT; ++ot) out[ot] = mfma16(w[ot][c], in[t][c], out[ot]);
   }
 }
 
@@ -100,14 +99,13 @@ PPO_DEV void mm_layer_lds(f4 (&out)[NT_OUT], const f4 (&in)[NT_IN], const float*
 #pragma unroll
   for (int t = 0; t < NT_IN; ++t) {
     const float* sb = wlds + (t & 1) * SLAB + i * 16 + 4 * g;
+    f4 w[NT_OUT];
 #pragma unroll
-    for (int ot = 0; ot < NT_OUT; ++ot) {
-      const f4 w = *reinterpret_cast<const f4*>(sb + ot * 256);
-      out[ot] = mfma16(w.x, in[t].x, out[ot]);
-      out[ot] = mfma16(w.y, in[t].y, out[ot]);
-      out[ot] = mfma16(w.z, in[t].z, out[ot]);
-      out[ot] = mfma16(w.w, in[t].w, out[ot]);
-    }
+    for (int ot = 0; ot < NT_OUT; ++ot) w[ot] = *reinterpret_cast<const f4*>(sb + ot * 256);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int ot = 0; ot < NT_OUT; ++ot) out[ot] = mfma16(w[ot][c], in[t][c], out[ot]);
     if (t + 1 < NT_IN) store((t + 1) & 1);
     lds_barrier();
     if (t + 2 < NT_IN) load(t + 2);

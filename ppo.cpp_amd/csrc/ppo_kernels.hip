@@ -181,17 +181,15 @@ __global__ __launch_bounds__(256) void k_act2(ActArgs a) {
       for (int u = 0; u < NTW; ++u) dst[u] = pld4(wb, (16 * (wave * NTW + u) + j) * ldw + 4 * g, 16 * t);
     };
     auto step = [&](const f4 (&wt)[NTW], int t) {
+      f4 b[RG];
 #pragma unroll
-      for (int rg = 0; rg < RG; ++rg) {
-        const f4 b = bfrag(rg, t);
+      for (int rg = 0; rg < RG; ++rg) b[rg] = bfrag(rg, t);
 #pragma unroll
-        for (int u = 0; u < NTW; ++u) {
-          acc[rg][u] = mfma16(wt[u].x, b.x, acc[rg][u]);
-          acc[rg][u] = mfma16(wt[u].y, b.y, acc[rg][u]);
-          acc[rg][u] = mfma16(wt[u].z, b.z, acc[rg][u]);
-          acc[rg][u] = mfma16(wt[u].w, b.w, acc[rg][u]);
-        }
-      }
+      for (int c = 0; c < 4; ++c)  // independent chains interleaved, each in its own order
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+          for (int u = 0; u < NTW; ++u) acc[rg][u] = mfma16(wt[u][c], b[rg][c], acc[rg][u]);
     };
     wload(w[0], 0);
     if (NTIN > 1) wload(w[1], 1);

@@ -571,12 +571,9 @@ PPO_DEV f4 trunk4(const f4 (&xv)[NKW], const f4 (&wa)[NKW][4], const f4 (&w2v)[4
     for (int q = 0; q < NKW; ++q) {
       if (kb0 + q < NTO) {
 #pragma unroll
-        for (int ft = 0; ft < 4; ++ft) {
-          acc[ft] = mfma16(wa[q][ft].x, xv[q].x, acc[ft]);
-          acc[ft] = mfma16(wa[q][ft].y, xv[q].y, acc[ft]);
-          acc[ft] = mfma16(wa[q][ft].z, xv[q].z, acc[ft]);
-          acc[ft] = mfma16(wa[q][ft].w, xv[q].w, acc[ft]);
-        }
+        for (int c = 0; c < 4; ++c)  // 4 independent chains interleaved, each in its own order
+#pragma unroll
+          for (int ft = 0; ft < 4; ++ft) acc[ft] = mfma16(wa[q][ft][c], xv[q][c], acc[ft]);
       }
     }
     // independent VALU work (the step's Normal draws) issued under the layer-1 MFMAs

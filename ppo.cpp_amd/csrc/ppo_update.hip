@@ -124,17 +124,17 @@ PPO_DEV void mm_fr(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* in) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) b[rt] = lds_f4(in + 16 * rt * LDI + 16 * kb);
     const bool full = kb + 1 < NKB || KL >= 4;
+    // k-step c outermost: consecutive MFMAs go to different accumulators (FT x RT independent
+    // chains), so none waits out the 40-cycle dependent latency of 16x16x4 f32 (32-cycle issue)
+    // when the partner wave is not streaming MFMAs; each accumulator's chain order is unchanged
 #pragma unroll
-    for (int ft = 0; ft < FT; ++ft)
+    for (int c = 0; c < 4; ++c) {
+      if (c > 0 && !full) break;
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        out[ft][rt] = mfma16(w[kb & 1][ft].x, b[rt].x, out[ft][rt]);
-        if (full) {
-          out[ft][rt] = mfma16(w[kb & 1][ft].y, b[rt].y, out[ft][rt]);
-          out[ft][rt] = mfma16(w[kb & 1][ft].z, b[rt].z, out[ft][rt]);
-          out[ft][rt] = mfma16(w[kb & 1][ft].w, b[rt].w, out[ft][rt]);
-        }
-      }
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) out[ft][rt] = mfma16(w[kb & 1][ft][c], b[rt][c], out[ft][rt]);
+    }
   }
 }
 
@@ -734,18 +734,18 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
       for (int ht = 0; ht < NHT; ++ht) {
         wv[ht] = hrow_f[ht] >= 0 ? pld4(pb, hrow_f[ht] + fbase + 4 * g, 16 * ft) : f4{0.f, 0.f, 0.f, 0.f};
       }
+      f4 h2v[RT];
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
-        const f4 h2 = h2_of(ft, rt);
-        lds_st4(ACT + (rbase + 16 * rt + j) * LDA + fbase + 16 * ft + 4 * g, h2);
-#pragma unroll
-        for (int ht = 0; ht < NHT; ++ht) {
-          hp[ht][rt] = mfma16(wv[ht].x, h2.x, hp[ht][rt]);
-          hp[ht][rt] = mfma16(wv[ht].y, h2.y, hp[ht][rt]);
-          hp[ht][rt] = mfma16(wv[ht].z, h2.z, hp[ht][rt]);
-          hp[ht][rt] = mfma16(wv[ht].w, h2.w, hp[ht][rt]);
-        }
+        h2v[rt] = h2_of(ft, rt);
+        lds_st4(ACT + (rbase + 16 * rt + j) * LDA + fbase + 16 * ft + 4 * g, h2v[rt]);
       }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int ht = 0; ht < NHT; ++ht) hp[ht][rt] = mfma16(wv[ht][c], h2v[rt][c], hp[ht][rt]);
     }
     // partial head sums -> SCR[wf][head][row]
 #pragma unroll
@@ -973,14 +973,13 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
           for (int r = 0; r < 4; ++r)
             wT[r] = hrow_b[ht][r] >= 0 ? bld1(pb, hrow_b[ht][r] + fbase + j, 16 * ft) : 0.0f;
         }
+        f4 gvv[RT];
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          const f4 gv = lds_f4(GG + (rbase + 16 * rt + j) * LDG + 16 * ht + 4 * g);
-          dh[ft][rt] = mfma16(wT.x, gv.x, dh[ft][rt]);
-          dh[ft][rt] = mfma16(wT.y, gv.y, dh[ft][rt]);
-          dh[ft][rt] = mfma16(wT.z, gv.z, dh[ft][rt]);
-          dh[ft][rt] = mfma16(wT.w, gv.w, dh[ft][rt]);
-        }
+        for (int rt = 0; rt < RT; ++rt) gvv[rt] = lds_f4(GG + (rbase + 16 * rt + j) * LDG + 16 * ht + 4 * g);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) dh[ft][rt] = mfma16(wT[c], gvv[rt][c], dh[ft][rt]);
         // dW3 tile (heads 16 ht.., features fbase + 16 ft ..): contract over this wave's rows
         f4 d3 = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll

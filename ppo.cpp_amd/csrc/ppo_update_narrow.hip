@@ -25,6 +25,34 @@
 #include "ppo_agent.hpp"
 #include "ppo_kernels.hpp"
 
+#ifdef PPO_STAMPS
+// diagnostic build only: per-wave shader-clock stamps at the phase ends of the first 16 tiles of
+// every workgroup ([wg][wave][tile][start, 12 phase ends, hardware wave id]), read by
+// ppo_diag_read_stamps2 (scripts/diag_stamps2.py)
+#define PPO2_NSTAMP 12
+#define PPO2_TILES 16
+#define PPO2_REC (PPO2_NSTAMP + 2)
+__device__ unsigned long long g_upd2_stamps[512 * 4 * PPO2_TILES * PPO2_REC];
+#define PPO2_STAMP(k)                                                                                \
+  do {                                                                                               \
+    const int tt_ = (it - (int)blockIdx.x) / (int)gridDim.x;                                         \
+    if (tt_ >= 0 && tt_ < PPO2_TILES && blockIdx.x < 512 && lane == 0)                              \
+      g_upd2_stamps[((blockIdx.x * 4 + wave) * PPO2_TILES + tt_) * PPO2_REC + (k)] =                \
+          __builtin_amdgcn_s_memtime();                                                              \
+  } while (0)
+#define PPO2_STAMP_ID()                                                                              \
+  do {                                                                                               \
+    const int tt_ = (it - (int)blockIdx.x) / (int)gridDim.x;                                         \
+    if (tt_ >= 0 && tt_ < PPO2_TILES && blockIdx.x < 512 && lane == 0)                              \
+      g_upd2_stamps[((blockIdx.x * 4 + wave) * PPO2_TILES + tt_) * PPO2_REC + PPO2_NSTAMP + 1] =    \
+          (unsigned long long)__builtin_amdgcn_s_getreg(0xF804) |                                    \
+          ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32);                             \
+  } while (0)
+#else
+#define PPO2_STAMP(k) do {} while (0)
+#define PPO2_STAMP_ID() do {} while (0)
+#endif
+
 namespace {
 
 // tanh of the update's forward recompute: (1 - e) / (1 + e) with e = exp(-2|x|) on v_exp_f32 /
@@ -126,14 +154,11 @@ PPO_DEV void mm64(f4 (&out)[FT2][RT2], PBuf wb, int wlane, const float* in) {
 #pragma unroll
     for (int rt = 0; rt < RT2; ++rt) b[rt] = lf4(in + 16 * rt * LDA2 + 16 * kb);
 #pragma unroll
-    for (int ft = 0; ft < FT2; ++ft)
+    for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int rt = 0; rt < RT2; ++rt) {
-        out[ft][rt] = mfma16(w[kb & 1][ft].x, b[rt].x, out[ft][rt]);
-        out[ft][rt] = mfma16(w[kb & 1][ft].y, b[rt].y, out[ft][rt]);
-        out[ft][rt] = mfma16(w[kb & 1][ft].z, b[rt].z, out[ft][rt]);
-        out[ft][rt] = mfma16(w[kb & 1][ft].w, b[rt].w, out[ft][rt]);
-      }
+      for (int ft = 0; ft < FT2; ++ft)
+#pragma unroll
+        for (int rt = 0; rt < RT2; ++rt) out[ft][rt] = mfma16(w[kb & 1][ft][c], b[rt][c], out[ft][rt]);
   }
 }
 
@@ -290,9 +315,12 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
   int tp = 0;  // buffer of this tile's chunk 0: the running chunk count's parity
   for (int it = blockIdx.x; it < ntiles; it += gridDim.x, tp ^= NCH & 1) {
     const int m0 = it * R;
+    PPO2_STAMP(0);
+    PPO2_STAMP_ID();
     // chunk 0 and the row data of this tile were DMA'd during the previous tile
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
+    PPO2_STAMP(1);
     perms_of(it + gridDim.x, pnext);
     row_perms(it + gridDim.x);
     // ---------------- layer 1 (both trunks share the staged rows) ----------------
@@ -334,17 +362,17 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) b[rt] = lf4(xs + 16 * rt * LDX);  // (16 rt + j) & (SWZ - 1) = j & (SWZ - 1)
         const int wq = kb % (W1D + 1);
+        // k-step c outermost: 4 independent accumulator chains back to back (16x16x4 f32: 32-cycle
+        // issue, 40-cycle dependent latency); each chain's order is unchanged
 #pragma unroll
-        for (int ft = 0; ft < FT; ++ft)
+        for (int c = 0; c < 4; ++c)
 #pragma unroll
-          for (int rt = 0; rt < RT; ++rt) {
-            z[ft][rt] = mfma16(w[wq][ft].x, b[rt].x, z[ft][rt]);
-            z[ft][rt] = mfma16(w[wq][ft].y, b[rt].y, z[ft][rt]);
-            z[ft][rt] = mfma16(w[wq][ft].z, b[rt].z, z[ft][rt]);
-            z[ft][rt] = mfma16(w[wq][ft].w, b[rt].w, z[ft][rt]);
-          }
+          for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) z[ft][rt] = mfma16(w[wq][ft][c], b[rt][c], z[ft][rt]);
       }
     }
+    PPO2_STAMP(2);
 #pragma unroll
     for (int u = 0; u < NGI; ++u) pcur[u] = pnext[u];
     // h1 = tanh(z1): kept in registers for the backward, stored for dW2 and as layer 2's input
@@ -359,6 +387,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
         if (m < M) st4(a.H1[trunk] + (size_t)m * H + fbase + 16 * ft + 4 * g, z[ft][rt]);
       }
     lds_barrier();
+    PPO2_STAMP(3);
 
     // ---------------- layer 2 ----------------
     f4 h2[FT][RT];
@@ -380,6 +409,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
     for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) sf4(ACT + (16 * rt + j) * LDA + fbase + 16 * ft + 4 * g, h2[ft][rt]);
+    PPO2_STAMP(4);
 
     // ---------------- heads: partial sums over this wave's 32 features ----------------
     if (trunk == 0) {
@@ -404,16 +434,13 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
 #pragma unroll
         for (int ft = 0; ft < FT; ++ft) hw[ft] = head_fwd(ht, ft);
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          hp[ht][rt] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int rt = 0; rt < RT; ++rt) hp[ht][rt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int ft = 0; ft < FT; ++ft) {
-            hp[ht][rt] = mfma16(hw[ft].x, h2[ft][rt].x, hp[ht][rt]);
-            hp[ht][rt] = mfma16(hw[ft].y, h2[ft][rt].y, hp[ht][rt]);
-            hp[ht][rt] = mfma16(hw[ft].z, h2[ft][rt].z, hp[ht][rt]);
-            hp[ht][rt] = mfma16(hw[ft].w, h2[ft][rt].w, hp[ht][rt]);
-          }
-        }
+        for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) hp[ht][rt] = mfma16(hw[ft][c], h2[ft][rt][c], hp[ht][rt]);
       }
 #pragma unroll
       for (int ht = 0; ht < NHT; ++ht)
@@ -423,6 +450,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
           for (int r = 0; r < 4; ++r) SCR[(wf * NHP + 16 * ht + 4 * g + r) * R + 16 * rt + j] = hp[ht][rt][r];
     }
     lds_barrier();
+    PPO2_STAMP(5);
 
     // ---------------- loss, pass 1: per (row, action) Normal log-prob / entropy terms ----------------
 #pragma unroll
@@ -467,6 +495,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
       lst[1] += sv;
     }
     lds_barrier();
+    PPO2_STAMP(6);
     // ---------------- loss, per row: clipped surrogate (ppo:497-513) ----------------
     if (tid < R) {
       const bool valid = m0 + tid < M;
@@ -500,6 +529,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
       ROWS[tid * 8 + 5] = g_ent;
     }
     lds_barrier();
+    PPO2_STAMP(7);
     // every read of this tile's RD / ACTN is done: DMA the next tile's
     row_dma();
     // ---------------- loss, pass 2: d loss / d mu and d loss / d logstd ----------------
@@ -517,6 +547,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
       }
     }
     lds_barrier();
+    PPO2_STAMP(8);
 
     // ---------------- head backward: dh2, dW3 ----------------
     f4 dh[FT][RT];
@@ -547,14 +578,13 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
 #pragma unroll
         for (int ht = 0; ht < NHT; ++ht) {
           const f4 hw = head_bwd(ht, ft);
+          f4 gvv[RT];
 #pragma unroll
-          for (int rt = 0; rt < RT; ++rt) {
-            const f4 gv = lf4(GG + (16 * rt + j) * LDG + 16 * ht + 4 * g);
-            dh[ft][rt] = mfma16(hw.x, gv.x, dh[ft][rt]);
-            dh[ft][rt] = mfma16(hw.y, gv.y, dh[ft][rt]);
-            dh[ft][rt] = mfma16(hw.z, gv.z, dh[ft][rt]);
-            dh[ft][rt] = mfma16(hw.w, gv.w, dh[ft][rt]);
-          }
+          for (int rt = 0; rt < RT; ++rt) gvv[rt] = lf4(GG + (16 * rt + j) * LDG + 16 * ht + 4 * g);
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) dh[ft][rt] = mfma16(hw[c], gvv[rt][c], dh[ft][rt]);
           // dW3 tile (heads 16 ht.., features fbase + 16 ft ..), contracted over the tile's rows
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt)
@@ -567,6 +597,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
         }
       }
     }
+    PPO2_STAMP(9);
     // dz2 = dh2 * (1 - h2^2)
     {
       float x[8];
@@ -590,6 +621,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) sf4(ACT + (16 * rt + j) * LDA + fbase + 16 * ft + 4 * g, dh[ft][rt]);
     lds_barrier();
+    PPO2_STAMP(10);
 
     // ---------------- dh1 = W2^T dz2, dz1 = dh1 * (1 - h1^2) ----------------
     f4 d1[FT][RT];
@@ -598,6 +630,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) d1[ft][rt] = f4{0.f, 0.f, 0.f, 0.f};
     mm64(d1, wsw, w2tlane, act_in);
+    PPO2_STAMP(11);
     {
       float x[8];
 #pragma unroll
@@ -613,6 +646,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
       }
       acc_b1 += colsum8(x, j);
     }
+    PPO2_STAMP(12);
   }
 
   // ---------------- workgroup result: one slab row per trunk (fixed-order reductions) ----------------
@@ -714,6 +748,16 @@ int upd2_supported(const PackedLayout& K, UpdGeoOut* g) {
                : -2;
   });
 }
+
+#ifdef PPO_STAMPS
+extern "C" int ppo_diag_read_stamps2(unsigned long long* host, long n) {
+  const long cap = (long)(sizeof(g_upd2_stamps) / sizeof(g_upd2_stamps[0]));
+  if (n > cap) n = cap;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_upd2_stamps), n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -2;
+}
+#endif
 
 int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s) {
   return dispatch_upd2(a.K, [&](auto NTO_, auto NHT_, auto VEC_, auto NU_) {

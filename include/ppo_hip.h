@@ -95,6 +95,10 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            no profiling); the Adam step constants come from a device table, so
  *                            the result is bitwise the eager one. Checkpoint snapshots work with it
  *                            (ppo_read_snapshot waits on the host, never across streams)
+ *   upd2_split=auto|0|2|3    64-wide agent with wide inputs (O % 4 == 0, OP = 384: Humanoid): layer 1
+ *                            of both trunks as one gathered GEMM (k_l1g) and k_upd2's tail in its own
+ *                            launch at 2 / 3 workgroups per CU, or the single k_upd2 (0; auto: the
+ *                            single kernel, measured faster)
  *   rollout=auto|per_step    ppo_rollout_synth: persistent launch where supported, or per step
  *   gradstep=split|fused     clip_grad_norm_ + Adam: two launches (k_gradnorm, k_adam; default) or
  *                            one cooperative launch (k_gradstep: slower on ROCm 7, whose cooperative

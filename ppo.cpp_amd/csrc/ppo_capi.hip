@@ -122,11 +122,11 @@ extern "C" const char* ppo_version(void) { return "ppo_hip 0.1 (gfx950)"; }
 // ------------------------------------------------------------------------------------------
 enum {
   PK_ACT = 0, PK_FWDBWD, PK_DW2, PK_DW1, PK_COLSUM, PK_GRADNORM, PK_ADAM, PK_GAE, PK_PERM, PK_ADV, PK_ALLREDUCE,
-  PK_SYNTH, PK_ROLLOUT, PK_VALUES, PK_COUNT
+  PK_SYNTH, PK_ROLLOUT, PK_VALUES, PK_L1G, PK_COUNT
 };
 static const char* kProfNames[PK_COUNT] = {"act", "fwdbwd", "dw", "dw_l1", "colsum", "gradnorm",
                                            "adam", "gae", "perm", "adv_stats", "allreduce", "synth_env",
-                                           "rollout", "values"};
+                                           "rollout", "values", "l1g"};
 
 struct ProfEvent {
   int id;
@@ -154,6 +154,8 @@ struct ppo_ctx {
   int tiles_per_block = 1, nblk = 1;
   bool use_upd = false;  // feature-split k_upd (ppo_update.hip) instead of k_fwdbwd
   bool use_upd2 = false;  // two-trunk k_upd2 (ppo_update_narrow.hip, H = 64 tanh agent)
+  int upd2_split = 0;       // k_l1g (layer 1 as a gathered GEMM into Z1) + k_upd2's split form at 2 / 3 per CU
+  float* Z1 = nullptr;      // [Mr][128] layer-1 pre-activations of the minibatch (split form)
   UpdGeoOut upd = {};
   int upd_nblk = 0;
   size_t lds_bytes = 0;
@@ -276,7 +278,11 @@ struct CreateOptions {
   // 1: ppo_update replays its minibatch launches as one captured hipGraph; 0 (default): eager. Not the
   // default: a checkpoint snapshot's cross-stream wait (ppo_snapshot_state) then fails on this stack
   int update_graph = 0;
+  int upd2_split = -1;  // -1 auto (wide inputs: k_l1g + split k_upd2), 0 one k_upd2, 2 / 3 split at 2 / 3 workgroups per CU
 };
+// auto = the single k_upd2: the split form measured slower on cfg2 (round 4, profiles/r04/cfg2_split/:
+// 101.3 vs 92.9 ms per iteration; k_l1g 66 us = 0.61 of peak per launch, the tail 94 us at 3 per CU)
+static constexpr int kUpd2SplitAuto = 0;
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
   std::string s(opts);
@@ -302,6 +308,7 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
     else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
     else if (k == "dw_dma" && (v == "0" || v == "1")) o->dw_dma = v[0] - '0';
     else if (k == "update_graph" && (v == "0" || v == "1")) o->update_graph = v[0] - '0';
+    else if (k == "upd2_split" && (v == "auto" || v == "0" || v == "2" || v == "3")) o->upd2_split = v == "auto" ? -1 : v[0] - '0';
     else return fail("ppo_create_ex: unknown option or value: " + kv);
   }
   return 0;
@@ -419,10 +426,17 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
     const int sgmax = std::max(c->sg[0].size, c->sg[1].size);
     // k_upd2 addresses the rollout storage with 32-bit buffer offsets
     const bool fits32 = (double)B * (double)std::max(O, A) * 4.0 < 4294967040.0;
-    if (!upd_kernel && fits32 && upd2_supported(c->K, &c->upd) == 0) {
+    const int split = !fits32 ? 0 : opt.upd2_split >= 0 ? opt.upd2_split : upd2_split_supported(c->K) ? kUpd2SplitAuto : 0;
+    if (opt.upd2_split > 0 && (upd_kernel || !upd2_split_supported(c->K))) {
+      delete c;
+      return fail("ppo_create: upd2_split needs the 64-wide agent with O % 4 == 0 and OP = 384");
+    }
+    if (!upd_kernel && fits32 && upd2_supported(c->K, &c->upd, split) == 0) {
       c->use_upd = c->use_upd2 = true;
+      c->upd2_split = split;
       const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
-      c->upd_nblk = std::min(ut, 512);  // both trunks per workgroup, 2 workgroups per CU x 256 CUs
+      // both trunks per workgroup, 2 workgroups per CU x 256 CUs (split form: 3 per CU)
+      c->upd_nblk = std::min(ut, split ? 256 * split : 512);
     } else if (!upd_kernel && upd_supported(c->K, c->sg[1].nh, c->sg[0].size, c->sg[1].size, &c->upd) == 0) {
       c->use_upd = true;
       const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
@@ -443,6 +457,7 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   if (opt.dw_rows && (!c->use_upd2 || opt.dw_rows % 32 == 0)) c->rows_per_chunk = opt.dw_rows;  // k_dw2: 32-row steps
   c->nchunks = (c->M + c->rows_per_chunk - 1) / c->rows_per_chunk;
   for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->dwslab[k], (size_t)c->nchunks * (H * H + H * OP));
+  if (c->upd2_split) rc |= dmalloc(&c->Z1, Mr * 128);
   rc |= dmalloc(&c->normout, 2 + PPO_LAYOUT_MAX_TENSORS + 2);
   rc |= dmalloc(&c->gnpart, (size_t)PPO_LAYOUT_MAX_TENSORS * PPO_GN_SPLIT);
   rc |= dmalloc(reinterpret_cast<float**>(&c->gs_bar), 1);
@@ -466,7 +481,7 @@ extern "C" int ppo_destroy(ppo_t* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   prof_drain(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
-  float* ptrs[] = {c->P, c->G, c->Am, c->Av, c->W2T[0], c->W2T[1], c->WSW[0], c->WSW[1], c->next_value, c->advstats, c->advsq, c->Xn,
+  float* ptrs[] = {c->P, c->G, c->Am, c->Av, c->W2T[0], c->W2T[1], c->WSW[0], c->WSW[1], c->next_value, c->advstats, c->advsq, c->Xn, c->Z1,
                    c->normout, c->gnpart, c->mbstats, c->beta_store, reinterpret_cast<float*>(c->gs_bar)};
   for (float* p : ptrs)
     if (p) (void)hipFree(p);
@@ -807,6 +822,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
   u.clip_vloss = cfg.clip_vloss;
   u.norm_adv = cfg.norm_adv;
   u.Xn = c->Xn;
+  u.Z1 = c->Z1;
   u.actn_off = c->upd.actn_off;
   u.acc_off = c->upd.acc_off;
   u.spar_off = c->upd.spar_off;
@@ -924,9 +940,13 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
       u.perm = perms + (size_t)e * B + (size_t)mb * M;
       u.adv_stats = c->advstats + 2 * gi;
       if (c->use_upd2) dw.perm = u.perm;  // k_dw gathers dW1's input rows itself
+      if (c->upd2_split) {
+        ProfScope ps(c, PK_L1G, s);
+        if (launch_l1g(u, s) != 0) return fail("k_l1g: unsupported configuration");
+      }
       {
         ProfScope ps(c, PK_FWDBWD, s);
-        const int rc_ = c->use_upd2  ? launch_upd2(u, c->upd_nblk, c->upd.lds_bytes, s)
+        const int rc_ = c->use_upd2  ? launch_upd2(u, c->upd_nblk, c->upd.lds_bytes, s, c->upd2_split)
                         : c->use_upd ? launch_upd(u, c->sg[1].nh, c->upd_nblk, c->upd.lds_bytes, s)
                                      : launch_fwdbwd(u, nblk, c->lds_bytes, s);
         if (rc_ != 0) return fail("no update kernel for this configuration");

@@ -69,6 +69,7 @@ struct UpdArgs {
   float* slab[2];
   int actn_off, acc_off, spar_off;  // k_upd: runtime LDS offsets (floats)
   int hw_global;                    // k_upd: the actor's dW3 accumulators live in its slab row (UpdGeoOut)
+  float* Z1;              // k_l1g -> k_upd2 (split form): layer-1 pre-activations [M][128], critic | actor
   int trunk_mask;         // k_upd: trunks to run (bit t = trunk t; 3 = both; other values: PPO_DIAG builds only)
   int sched;              // k_upd: bit 0 actor workgroups dispatched first, bit 1 actor wave priority
 };
@@ -244,8 +245,12 @@ int launch_fwdbwd(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s
 int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes);
 int upd_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g);
 int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s);
-int upd2_supported(const PackedLayout& K, UpdGeoOut* g);  // ppo_update_narrow.hip (H = 64 tanh agent)
-int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s);
+// ppo_update_narrow.hip (H = 64 tanh agent); split form: k_l1g computes layer 1 (a.Z1), k_upd2 the rest
+bool upd2_split_supported(const PackedLayout& K);
+// split: 0 one kernel; 2 / 3 the split form at 2 / 3 workgroups per CU
+int upd2_supported(const PackedLayout& K, UpdGeoOut* g, int split);
+int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s, int split);
+int launch_l1g(const UpdArgs& a, hipStream_t s);
 int launch_dw2(const DwArgs& a, int OP, int nchunks, hipStream_t s);  // both 64-wide trunks, rows gathered once
 int launch_dw(const DwArgs& a, int H, int OP, int nchunks, hipStream_t s);
 size_t dw_lds_bytes(int H, int OP);

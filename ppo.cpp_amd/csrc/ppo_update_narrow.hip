@@ -53,6 +53,8 @@ __device__ unsigned long long g_upd2_stamps[512 * 4 * PPO2_TILES * PPO2_REC];
 #define PPO2_STAMP_ID() do {} while (0)
 #endif
 
+typedef float f16v2 __attribute__((ext_vector_type(16)));
+
 namespace {
 
 // tanh of the update's forward recompute: (1 - e) / (1 + e) with e = exp(-2|x|) on v_exp_f32 /
@@ -69,7 +71,7 @@ PPO_DEV float tanh_upd(float x) {
 
 constexpr int H2 = 64, FT2 = 2, RT2 = 2, R2 = 32, LDA2 = H2 + 4;
 
-template <int NTO, int NHT, int VEC, int NUA>
+template <int NTO, int NHT, int VEC, int NUA, int SPLIT = 0>
 struct Geo2 {
   static constexpr int OP = NTO * 16;
   static constexpr int CKB = NTO < 8 ? NTO : 8;      // k-blocks (16 columns) per staged X chunk
@@ -86,7 +88,8 @@ struct Geo2 {
   static constexpr int NU = NUA;                         // (row, action) items per thread: ceil(R A / 256)
   // LDS carve (floats); the (row, action) item and action regions follow at runtime offsets
   static constexpr int oXS = 0;
-  static constexpr int oACT = oXS + NB * R2 * LDX;     // [2 trunks][R][LDA]: h1, then h2, then dz2
+  // split form (k_l1g computed layer 1): no X staging
+  static constexpr int oACT = oXS + (SPLIT ? 0 : NB * R2 * LDX);  // [2 trunks][R][LDA]: h1, then h2, then dz2
   static constexpr int oSCR = oACT + 2 * R2 * LDA2;    // actor head partials [2][NHP][R] | critic [2][R]
   static constexpr int oGG = oSCR + 2 * NHP * R2 + 2 * R2;  // [R][LDG] d loss / d mu
   static constexpr int oROWS = oGG + R2 * LDG;          // [R][8] per-row scalars computed by the loss
@@ -164,9 +167,12 @@ PPO_DEV void mm64(f4 (&out)[FT2][RT2], PBuf wb, int wlane, const float* in) {
 
 }  // namespace
 
-template <int NTO, int NHT, int VEC, int NUA>
-__global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
-  using GE = Geo2<NTO, NHT, VEC, NUA>;
+// SPLIT (2 or 3: workgroups per CU): layer 1's pre-activations come from k_l1g (a.Z1 rows, bias
+// included) instead of the staged X chunks and W1: the kernel is the tail only (tanh onwards), with
+// a smaller LDS / register footprint (3 per CU: 168 VGPRs, a few spilled registers).
+template <int NTO, int NHT, int VEC, int NUA, int SPLIT>
+__global__ __launch_bounds__(256, SPLIT ? SPLIT : 2) void k_upd2(UpdArgs a) {
+  using GE = Geo2<NTO, NHT, VEC, NUA, SPLIT>;
   constexpr int OP = GE::OP, CKB = GE::CKB, NCH = GE::NCH, CW = GE::CW, LDX = GE::LDX, NHP = GE::NHP;
   constexpr int LDG = GE::LDG, PERROW = GE::PERROW, NGI = GE::NGI, NU = GE::NU, UPR = GE::UPR, SWZ = GE::SWZ;
   constexpr int W1D = 3;  // W1 A-operand prefetch depth (k-blocks; 2 -> 3: cfg2 k_upd2 44.05 -> 43.88 ms)
@@ -307,8 +313,24 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
   float cbacc = 0.f;                        // critic head bias (tid < R)
   float lst[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // pg, v, ent, old kl, kl, clipfrac (tid < R)
 
-  perms_of(blockIdx.x, pcur);
-  issue(pcur, 0, 0);
+  // split form: this lane's layer-1 pre-activations of a tile (rows 16 rt + j, clamped; masked at use)
+  auto z1_load = [&](int itn, f4 (&zz)[FT][RT]) {
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const long m = min((long)itn * R + 16 * rt + j, (long)M - 1);
+        zz[ft][rt] = ld4(a.Z1 + m * 128 + 64 * trunk + fbase + 16 * ft + 4 * g);
+      }
+  };
+  f4 zn[FT][RT];
+  constexpr bool PREF_Z = false;  // next tile's Z1 rows prefetched mid-tile (16 VGPRs: spills at 3 WGs / CU)
+  if constexpr (SPLIT) {
+    if constexpr (PREF_Z) z1_load(blockIdx.x, zn);
+  } else {
+    perms_of(blockIdx.x, pcur);
+    issue(pcur, 0, 0);
+  }
   row_perms(blockIdx.x);
   row_dma();
 
@@ -321,10 +343,17 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
     PPO2_STAMP(1);
-    perms_of(it + gridDim.x, pnext);
+    if constexpr (!SPLIT) perms_of(it + gridDim.x, pnext);
     row_perms(it + gridDim.x);
     // ---------------- layer 1 (both trunks share the staged rows) ----------------
     f4 z[FT][RT];
+    if constexpr (SPLIT) {
+      if constexpr (!PREF_Z) z1_load(it, zn);
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) z[ft][rt] = zn[ft][rt];
+    } else {
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft) {
       const f4 bv = pld4(pb, T.b1 + fbase + 4 * g, 16 * ft);
@@ -372,9 +401,10 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
             for (int rt = 0; rt < RT; ++rt) z[ft][rt] = mfma16(w[wq][ft][c], b[rt][c], z[ft][rt]);
       }
     }
-    PPO2_STAMP(2);
 #pragma unroll
     for (int u = 0; u < NGI; ++u) pcur[u] = pnext[u];
+    }  // !SPLIT
+    PPO2_STAMP(2);
     // h1 = tanh(z1): kept in registers for the backward, stored for dW2 and as layer 2's input
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft)
@@ -451,6 +481,7 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
     }
     lds_barrier();
     PPO2_STAMP(5);
+    if constexpr (SPLIT && PREF_Z) z1_load(it + gridDim.x, zn);  // the next tile's rows, a half tile ahead
 
     // ---------------- loss, pass 1: per (row, action) Normal log-prob / entropy terms ----------------
 #pragma unroll
@@ -711,18 +742,152 @@ __global__ __launch_bounds__(256, 2) void k_upd2(UpdArgs a) {
   }
 }
 
+// =============================================================================================
+// k_l1g — layer 1 of BOTH 64-wide trunks over the minibatch's gathered observation rows, as one
+// GEMM: Z1[m][o] = b1[o] + sum_k X[perm[m]][k] W1[o][k], o < 64 the critic, o >= 64 the actor
+// (ppo:124-135: actor_mean.0 / critic.0), for wide inputs (cfg2 Humanoid: K = 376 of 384 padded).
+// k_upd2 then runs in its split form (SPLIT): tanh of these rows onwards, no X staging, no W1.
+// At K = 384 layer 1 is 73 % of the update forward/backward's MFMAs; inside k_upd2 it ran beside
+// the tail's barrier / VALU phases of the co-resident workgroup at ~0.8 of the pipe while the
+// tails themselves left it idle. Here it is a plain GEMM, and the tail kernel gets occupancy of its
+// own.
+//  * workgroup: 128 rows x 128 outputs, 4 waves; wave w: trunk w >> 1, rows 64 (w & 1) .. + 64
+//    (2 tiles of 32), outputs 64 trunk .. + 64 (2 tiles of 32): 4 accumulators of
+//    v_mfma_f32_32x32x2_f32 (64-cycle issue = dependent latency: no chain stalls);
+//  * D[m][o] orientation: A = X rows (lane = row), B = W1^T (lane = output), so a result register
+//    holds 32 consecutive outputs of one row (128-byte row segments on store);
+//  * k in groups of 8: lane half h holds k = 8 q + 4 h .. + 3 as one f4 of each operand; MFMA step
+//    c takes component c (k = 8 q + c and 8 q + 4 + c);
+//  * X: 32-column chunks of the 128 gathered rows by LDS DMA (16 bytes a lane; columns >= O and
+//    rows >= M out of range, hence 0) into three buffers, two chunks ahead; 16-byte unit u of row r
+//    stored at unit u ^ ((r >> 1) & 7): conflict-free ds_read_b128 A operands (64 banks, 32-float
+//    rows, the b128 lane groups of MI355X_MICROARCH.md's LDS table);
+//  * W1^T: f4 buffer loads from the packed parameters (L2-resident), one chunk ahead;
+//  * one s_waitcnt vmcnt(4) per chunk: everything but the newest chunk's 4 DMAs has landed.
+// =============================================================================================
+template <int OP>
+__global__ __launch_bounds__(256, 2) void k_l1g(UpdArgs a) {
+  constexpr int H = 64, RW = 128, CK = 32, NCH = OP / CK, NBUF = 3, UPR = CK / 4;
+  static_assert(OP % CK == 0, "k_l1g: OP must be a multiple of 32");
+  constexpr int DPW = RW * UPR / 64 / 4;  // DMA instructions per wave per chunk (4)
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int trunk = wave >> 1, rh = wave & 1;
+  const int M = a.M, O = a.K.O;
+  const long m0 = (long)blockIdx.x * RW;
+  const PBuf ob = make_pbuf_b(a.obs, (uint32_t)min(a.obs_n * 4, (long)0xFFFFFFFF));
+  const PBuf pb = make_pbuf(a.P, a.K.size);
+  // this lane's rows of its DMA instructions (the same rows every chunk): instruction i covers rows
+  // 8 i .. 8 i + 7, lane -> row 8 i + (lane >> 3), physical unit lane & 7
+  int prow[DPW];
+#pragma unroll
+  for (int d = 0; d < DPW; ++d) {
+    const int row = 8 * (wave * DPW + d) + (lane >> 3);
+    const long m = m0 + row;
+    const int p = a.perm[min(m, (long)M - 1)];
+    prow[d] = m < M ? p : -1;
+  }
+  auto issue = [&](int ch) {
+    float* b = lds + (ch % NBUF) * RW * CK;
+#pragma unroll
+    for (int d = 0; d < DPW; ++d) {
+      const int i = wave * DPW + d, row = 8 * i + (lane >> 3), pu = lane & 7;
+      const int u = pu ^ ((row >> 1) & 7), col = ch * CK + 4 * u;
+      const uint32_t voff = (ch < NCH && prow[d] >= 0 && col < O) ? (uint32_t)(prow[d] * O + col) * 4u : kOOB;
+      dma<16>(ob, b + i * 256, voff);
+    }
+  };
+  // W1^T operands: lane (output j, half h): W1[64 trunk + 32 ot + j][8 q + 4 h .. + 3]
+  const int wl = (a.K.tr[trunk].W1 + l32 * OP + 4 * h);
+  f4 wc[2][4][2];  // [chunk parity][q][ot]
+  auto wload = [&](int ch, f4 (&w)[4][2]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int ot = 0; ot < 2; ++ot)
+        w[q][ot] = ch < NCH ? pld4(pb, wl, 32 * ot * OP + ch * CK + 8 * q) : f4{0.f, 0.f, 0.f, 0.f};
+  };
+  f16v2 acc[2][2];  // [rt][ot]
+#pragma unroll
+  for (int ot = 0; ot < 2; ++ot) {
+    const float bv = a.P[a.K.tr[trunk].b1 + 32 * ot + l32];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[rt][ot][r] = bv;
+  }
+  wload(0, wc[0]);
+  issue(0);
+  issue(1);
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    // chunk ch's rows (every wave's DMAs) and W1 of chunk ch have landed; chunk ch + 1's DMAs may
+    // stay in flight
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+    lds_barrier();
+    wload(ch + 1, wc[(ch + 1) & 1]);
+    issue(ch + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    const float* b = lds + (ch % NBUF) * RW * CK;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f4 x[2];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int row = 64 * rh + 32 * rt + l32, u = 2 * q + h;
+        x[rt] = *reinterpret_cast<const f4*>(b + row * CK + 4 * (u ^ ((row >> 1) & 7)));
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+          for (int ot = 0; ot < 2; ++ot)
+            acc[rt][ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(x[rt][c], wc[ch & 1][q][ot][c], acc[rt][ot], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA may land after the workgroup ends
+  // result register r of tile (rt, ot): row 64 rh + 32 rt + (r & 3) + 8 (r >> 2) + 4 h, output 32 ot + l32
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const long m = m0 + 64 * rh + 32 * rt + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (m < M) {
+#pragma unroll
+        for (int ot = 0; ot < 2; ++ot) a.Z1[m * 128 + 64 * trunk + 32 * ot + l32] = acc[rt][ot][r];
+      }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
+size_t l1g_lds_bytes();
+
+// the split form (k_l1g + the tail) where layer 1 is wide: OP a multiple of 32 from 128 on, whole
+// 16-byte units per row (O % 4 == 0) — cfg2's Humanoid O = 376 / OP = 384
+bool upd2_split_supported(const PackedLayout& K) { return K.H == 64 && K.OP == 384 && K.O % 4 == 0; }
+
 template <typename F>
-static int dispatch_upd2(const PackedLayout& K, F&& f) {
+static int dispatch_upd2(const PackedLayout& K, int split, F&& f) {
   if (K.H != 64 || K.kind != PPO_NET_TANH_NORMAL || K.A > 32) return -1;
+  if (split && !upd2_split_supported(K)) return -1;
   const int nto = K.OP / 16, nht = (K.A + 15) / 16, nu = (R2 * K.A + 255) / 256;
   const int vec = (K.O % 4 == 0 && nto >= 2) ? 4 : 1;  // 16-byte DMA needs >= 8 units per row (256 per chunk)
+  if (split && nto == 24 && nht == 2 && vec == 4 && nu == 3) {
+    if (split == 3)
+      return f(std::integral_constant<int, 24>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 4>{},
+               std::integral_constant<int, 3>{}, std::integral_constant<int, 3>{});
+    return f(std::integral_constant<int, 24>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 4>{},
+             std::integral_constant<int, 3>{}, std::integral_constant<int, 2>{});
+  }
+  if (split) return -1;
 #define PPO_UPD2_CASE(NTO_, NHT_, VEC_, NU_)                                                         \
   if (nto == NTO_ && nht == NHT_ && vec == VEC_ && nu == NU_)                                        \
     return f(std::integral_constant<int, NTO_>{}, std::integral_constant<int, NHT_>{},               \
-             std::integral_constant<int, VEC_>{}, std::integral_constant<int, NU_>{});
+             std::integral_constant<int, VEC_>{}, std::integral_constant<int, NU_>{}, std::integral_constant<int, 0>{});
   // NU = 1: A <= 8; 2: A <= 16; 3: A <= 24; 4: A <= 32
   PPO_UPD2_CASE(1, 1, 1, 1) PPO_UPD2_CASE(2, 1, 1, 1) PPO_UPD2_CASE(2, 1, 1, 2) PPO_UPD2_CASE(7, 1, 1, 1)
   PPO_UPD2_CASE(24, 2, 4, 3) PPO_UPD2_CASE(2, 2, 1, 3) PPO_UPD2_CASE(24, 2, 1, 3)
@@ -731,9 +896,16 @@ static int dispatch_upd2(const PackedLayout& K, F&& f) {
   return -1;
 }
 
-int upd2_supported(const PackedLayout& K, UpdGeoOut* g) {
-  return dispatch_upd2(K, [&](auto NTO_, auto NHT_, auto VEC_, auto NU_) {
-    using GE = Geo2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value, decltype(NU_)::value>;
+int upd2_supported(const PackedLayout& K, UpdGeoOut* g, int split) {
+  if (split) {
+    const auto k = k_l1g<384>;
+    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1g_lds_bytes()) !=
+        hipSuccess)
+      return -2;
+  }
+  return dispatch_upd2(K, split, [&](auto NTO_, auto NHT_, auto VEC_, auto NU_, auto SP_) {
+    using GE = Geo2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value, decltype(NU_)::value,
+                    decltype(SP_)::value>;
     int off = GE::oITM + 4 * R2 * K.A;
     g->actn_off = off;
     off += 64 * ((R2 * K.A + 63) / 64);
@@ -741,7 +913,8 @@ int upd2_supported(const PackedLayout& K, UpdGeoOut* g) {
     g->spar_off = 0;
     g->lds_bytes = (size_t)off * sizeof(float);
     g->rows = R2;
-    const auto k = k_upd2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value, decltype(NU_)::value>;
+    const auto k = k_upd2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value, decltype(NU_)::value,
+                          decltype(SP_)::value>;
     return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) ==
                    hipSuccess
                ? 0
@@ -759,13 +932,21 @@ extern "C" int ppo_diag_read_stamps2(unsigned long long* host, long n) {
 }
 #endif
 
-int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s) {
-  return dispatch_upd2(a.K, [&](auto NTO_, auto NHT_, auto VEC_, auto NU_) {
+int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s, int split) {
+  return dispatch_upd2(a.K, split, [&](auto NTO_, auto NHT_, auto VEC_, auto NU_, auto SP_) {
     hipLaunchKernelGGL((k_upd2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value,
-                               decltype(NU_)::value>),
+                               decltype(NU_)::value, decltype(SP_)::value>),
                        dim3(nblocks), dim3(256), lds_bytes, s, a);
     return 0;
   });
+}
+
+size_t l1g_lds_bytes() { return (size_t)3 * 128 * 32 * sizeof(float); }
+
+int launch_l1g(const UpdArgs& a, hipStream_t s) {
+  if (!upd2_split_supported(a.K)) return -1;
+  hipLaunchKernelGGL((k_l1g<384>), dim3((a.M + 127) / 128), dim3(256), l1g_lds_bytes(), s, a);
+  return 0;
 }
 
 // =============================================================================================
@@ -778,8 +959,6 @@ int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s) 
 // are in flight in registers under the current stage's MFMAs. Partials per chunk go to the slab
 // (k_colsum adds the chunks in a fixed order).
 // =============================================================================================
-typedef float f16v2 __attribute__((ext_vector_type(16)));
-
 template <int OP, int VEC>
 __global__ __launch_bounds__(512) void k_dw2(DwArgs a) {
   constexpr int H = 64, KS = 16, NTH = 512;

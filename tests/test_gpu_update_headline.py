@@ -91,3 +91,37 @@ def test_headline_minibatch_update_vs_oracle(name, kind, H, O_, A, E, T, clip, e
     bound = 2e-6 + lr * np.abs(g64 - c64) / (np.minimum(np.abs(g64), np.abs(c64)) + eps)
     assert (np.abs(p1.astype(np.float64) - op) <= bound).all(), np.abs(p1 - op).max()
     assert np.mean(np.abs(p1 - op) > 2e-6) < 1e-3  # the sensitive elements are a small minority
+
+
+@pytest.mark.parametrize("split", ["2", "3"])
+def test_cfg2_split_update_matches_single_kernel(split):
+    """cfg2's update in its split form (k_l1g: layer 1 of both trunks as one gathered GEMM into Z1,
+    then k_upd2's tail at 2 / 3 workgroups per CU) against the single k_upd2 (upd2_split=0) on the
+    same minibatch (M = 16 384, ragged last tile: 16 383 rows): the layer-1 sums are the same products
+    in another order (32x32x2 chains over k pairs instead of 16x16x4 chains), so gradients agree to
+    fp32 accumulation noise (rel-L2 < 1e-5) and the loss statistics to rtol 1e-5."""
+    kind, H, O_, A, E, T = 0, 64, 376, 17, 16383, 1
+    M = E * T
+    rng = np.random.default_rng(5)
+    L = O.layout_init(kind, O_, A, H)
+    p = random_params(L, rng)
+    x = rng.standard_normal((M, O_)).astype(np.float32)
+    act = rng.standard_normal((M, A)).astype(np.float32) * 0.5
+    olp = rng.standard_normal(M).astype(np.float32) - 20.0
+    adv = rng.standard_normal(M).astype(np.float32)
+    ret = rng.standard_normal(M).astype(np.float32)
+    ov = rng.standard_normal(M).astype(np.float32)
+    perm = rng.permutation(M).astype(np.int32)
+    out = []
+    for opt in ("upd2_split=0", f"upd2_split={split}"):
+        ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.2, ent=0.0, options=opt)
+        ag.load_params(p)
+        fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
+        st = ag.update(3e-4, perms=DeviceArray.from_numpy(perm), want_stats=True)
+        out.append((ag.last_grad(), st, ag.params()))
+        ag.close()
+    (g0, s0, p0), (g1, s1, p1) = out
+    assert rel(g1, g0) < 1e-5, rel(g1, g0)
+    for k in ("pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac", "grad_norm"):
+        np.testing.assert_allclose(s1[k], s0[k], rtol=1e-5, atol=1e-7, err_msg=k)
+    assert np.abs(p1 - p0).max() < 1e-5

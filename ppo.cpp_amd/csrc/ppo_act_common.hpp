@@ -90,13 +90,16 @@ PPO_DEV void act_activate(f4 (&acc)[2][RT], const float* sp_g, const float* sp_b
 #pragma unroll
       for (int w = 0; w < kActWaves; ++w) t += red[w * R + 16 * rt + j];
       mu[rt] = t * (1.0f / 256);
+      // explicit FMAs: `q += d * d` leaves the contraction to the compiler, which fused some
+      // terms and not others (a different choice per kernel breaks the bitwise contract with
+      // k_rollout_v's statistics lanes)
       float q = 0.f;
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float d = acc[u][rt][r] - mu[rt];
-          q += d * d;
+          q = __fmaf_rn(d, d, q);
         }
       q = row_allreduce(q);
       if (g == 0) red[(kActWaves + wave) * R + 16 * rt + j] = q;
@@ -107,7 +110,7 @@ PPO_DEV void act_activate(f4 (&acc)[2][RT], const float* sp_g, const float* sp_b
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < kActWaves; ++w) v += red[(kActWaves + w) * R + 16 * rt + j];
-      rs[rt] = 1.0f / sqrtf(v * (1.0f / 256) + 1e-5f);
+      rs[rt] = 1.0f / sqrtf(__fmaf_rn(v, 1.0f / 256, 1e-5f));
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {

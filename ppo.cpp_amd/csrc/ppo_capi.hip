@@ -154,6 +154,7 @@ struct ppo_ctx {
   int tiles_per_block = 1, nblk = 1;
   bool use_upd = false;  // feature-split k_upd (ppo_update.hip) instead of k_fwdbwd
   bool use_upd2 = false;  // two-trunk k_upd2 (ppo_update_narrow.hip, H = 64 tanh agent)
+  int rollout_kernel = 0;   // AC persistent rollout: 0 auto, 1 k_rollout (MFMA), 2 k_rollout_v (VALU)
   int upd2_split = 0;       // k_l1g (layer 1 as a gathered GEMM into Z1) + k_upd2's split form at 2 / 3 per CU
   float* Z1 = nullptr;      // [Mr][128] layer-1 pre-activations of the minibatch (split form)
   UpdGeoOut upd = {};
@@ -278,6 +279,7 @@ struct CreateOptions {
   // 1: ppo_update replays its minibatch launches as one captured hipGraph; 0 (default): eager. Not the
   // default: a checkpoint snapshot's cross-stream wait (ppo_snapshot_state) then fails on this stack
   int update_graph = 0;
+  int rollout_kernel = 0;  // 0 auto, 1 mfma (k_rollout), 2 valu (k_rollout_v)
   int upd2_split = -1;  // -1 auto (wide inputs: k_l1g + split k_upd2), 0 one k_upd2, 2 / 3 split at 2 / 3 workgroups per CU
 };
 // auto = the single k_upd2: the split form measured slower on cfg2 (round 4, profiles/r04/cfg2_split/:
@@ -308,6 +310,8 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
     else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
     else if (k == "dw_dma" && (v == "0" || v == "1")) o->dw_dma = v[0] - '0';
     else if (k == "update_graph" && (v == "0" || v == "1")) o->update_graph = v[0] - '0';
+    else if (k == "rollout_kernel" && (v == "auto" || v == "mfma" || v == "valu"))
+      o->rollout_kernel = v == "auto" ? 0 : v == "mfma" ? 1 : 2;
     else if (k == "upd2_split" && (v == "auto" || v == "0" || v == "2" || v == "3")) o->upd2_split = v == "auto" ? -1 : v[0] - '0';
     else return fail("ppo_create_ex: unknown option or value: " + kv);
   }
@@ -372,6 +376,7 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   c->rollout_mode = opt.rollout;
   c->gradstep = opt.gradstep;
   c->update_graph = opt.update_graph;
+  c->rollout_kernel = opt.rollout_kernel;
   int upd_kernel = opt.upd_kernel;
 #ifdef PPO_DIAG
   {
@@ -522,6 +527,13 @@ extern "C" int ppo_set_iteration(ppo_t* c, long it) {
   if (!c) return fail("null ctx");
   c->iteration = it;
   return 0;
+}
+// debug hook (not part of the C-ABI header): internal device buffers by name ("beta_store": the AC
+// rollout's (alpha, beta, sample) per (t, env, action))
+extern "C" float* ppo_debug_buffer(ppo_t* c, const char* name) {
+  if (!c || !name) return nullptr;
+  if (!strcmp(name, "beta_store")) return c->beta_store;
+  return nullptr;
 }
 extern "C" float* ppo_buffer(ppo_t* c, int which) {
   if (!c || which < 0 || which >= PPO_BUF_COUNT) return nullptr;
@@ -1397,6 +1409,7 @@ extern "C" int ppo_rollout_synth(ppo_t* c, psyn_t* env, float* next_obs, float* 
     r.env = env->a;
     r.lo = lo;
     r.hi = hi;
+    r.variant = c->rollout_kernel;
     if (c->K.kind == PPO_NET_LN_BETA) {  // Beta log-probs after the rollout (off the env's path)
       if (!c->beta_store && dmalloc(&c->beta_store, (size_t)E * c->cfg.num_steps * c->K.A * 3)) return -2;
       r.s_beta = c->beta_store;

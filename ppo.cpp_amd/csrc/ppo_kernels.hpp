@@ -218,6 +218,7 @@ struct RolloutArgs {
   float* s_beta;        // AC: [T][E][A][3] (alpha, beta, sample) for k_beta_logp; null: log-probs in the loop
   SynthArgs env;
   float lo, hi;         // the env's action space (clip_actions)
+  int variant;          // AC rollout kernel: 0 auto, 1 k_rollout (MFMA, 16 envs per workgroup), 2 k_rollout_v (VALU)
 };
 // Critic forward over n stored rows (ppo_rollout.hip, k_values): values[i] = critic(obs[i]), the
 // same chain as k_act3's critic workgroups, so each value is bitwise the one the per-step act

@@ -36,6 +36,15 @@ extern "C" int ppo_diag_read_roll_stamps(unsigned long long* host, long n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_roll_stamps), n * sizeof(unsigned long long), 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -2;
 }
+// intermediate values of one env (g_rdbg_env) at step 0: [0] k_rollout, [1] k_rollout_v; slots
+// layer-1 out 0.., h1 260.., layer-2 out 516.., h2 776.., head partials [8][16] 1032.., pre 1160..
+__device__ float g_rdbg[2][1280];
+#define RDBG(k, i, v) (g_rdbg[k][i] = (v))
+extern "C" int ppo_diag_read_rdbg(float* host) {
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rdbg), sizeof(g_rdbg), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+constexpr int kRdbgEnv = 26;
 #else
 #define ROLL_STAMP(t, k) do {} while (0)
 #endif
@@ -106,7 +115,9 @@ PPO_DEV void stage_params(const PackedLayout& K, const TrunkDev& T, PBuf pb, int
 // LayerNorm + ReLU, layer 2, LayerNorm + ReLU, heads; leaves the head pre-activations (+ bias) in
 // PRE [16][LDP]. Weights: w1 / w2 register slices of this wave. Same operations, same order as
 // k_act3 (LN_BETA, RT = 1).
-template <int NTO, int NHT, int RT = 1, typename PRE_L2 = int>
+// PRE_PASS false: stop once the per-wave head partials are in HP (after the barrier); the caller
+// adds them itself (the same adds in the same order: bitwise the PRE values).
+template <int NTO, int NHT, int RT = 1, bool PRE_PASS = true, typename PRE_L2 = int>
 PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* lds, int nh, int tid,
                         PRE_L2 pre_l2 = 0, int stamp_t = -1) {
   (void)stamp_t;  // ROLL_STAMP step index (stamps build; -1: none)
@@ -129,7 +140,19 @@ PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* ld
   }
   const float* xin = XS + j * LDX + 4 * g;
   act_layer_regs<NTO, RT>(acc, w1, [&](int t, int rt) { return *reinterpret_cast<const f4*>(xin + 16 * rt * LDX + 16 * t); });
+#ifdef PPO_STAMPS
+  const bool dbg = stamp_t == 0 && RT == 1 && (int)blockIdx.x * 16 + j == kRdbgEnv;
+  auto dump = [&](int base) {
+    if (dbg)
+      for (int u = 0; u < 2; ++u)
+        for (int r = 0; r < 4; ++r) RDBG(0, base + 32 * wave + 16 * u + 4 * g + r, acc[u][0][r]);
+  };
+#else
+  auto dump = [](int) {};
+#endif
+  dump(0);
   act_activate<PPO_NET_LN_BETA, RT>(acc, SP + GE::sG1, SP + GE::sBE1, RED, wave, j, g);
+  dump(260);
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -154,7 +177,9 @@ PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* ld
 #endif
     ROLL_STAMP(stamp_t, 6);
   }
+  dump(516);
   act_activate<PPO_NET_LN_BETA, RT>(acc, SP + GE::sG2, SP + GE::sBE2, RED, wave, j, g);
+  dump(776);
   if (stamp_t >= 0) ROLL_STAMP(stamp_t, 7);
 #pragma unroll
   for (int ht = 0; ht < NHT; ++ht) {
@@ -171,9 +196,14 @@ PPO_DEV void trunk_rows(const f4 (&w1)[NTO][2], const f4 (&w2)[16][2], float* ld
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) HP[(wave * NHP + 16 * ht + 4 * g + r) * R + 16 * rt + j] = hp[r];
+#ifdef PPO_STAMPS
+      if (dbg && ht == 0)
+        for (int r = 0; r < 4; ++r) RDBG(0, 1032 + wave * 16 + 4 * g + r, hp[r]);
+#endif
     }
   }
   lds_barrier();
+  if constexpr (!PRE_PASS) return;
   for (int idx = tid; idx < R * nh; idx += kActThreads) {
     const int r = idx / nh, h = idx - r * nh;
     float s = 0.f;
@@ -261,6 +291,7 @@ __global__ __launch_bounds__(512) void k_rollout(RolloutArgs a) {
   // waves (2A <= 16: at most 32 per wave), so fewer lanes per wave wait on a rejected gamma attempt
   const int bper = (R * A * 2 + kActWaves - 1) / kActWaves;
   const int bitem = lane < bper ? wave * bper + lane : R * A * 2;
+  const bool defer = a.s_beta != nullptr;
 
   for (int t = 0; t < a.T; ++t) {
     const long step_id = a.step0 + t;
@@ -280,21 +311,39 @@ __global__ __launch_bounds__(512) void k_rollout(RolloutArgs a) {
     // fetch; gamma_mt_d0 with them is gamma_mt, bitwise)
     GammaDraw gd0 = GammaDraw{0.f, 0.f};
     ROLL_STAMP(t, 1);
-    trunk_rows<NTO, NHT>(w1, w2, lds, 2 * A, tid, [&] {
+    // deferred log-probs (a.s_beta, the AC rollout): no PRE pass — each Beta item adds its head's
+    // per-wave partials itself (the same adds in the same order as the pass: bitwise its PRE), one
+    // LDS pass and one barrier fewer per step
+    const auto draw0 = [&] {
       if (bitem < R * A * 2) {
         const int which = bitem & 1, ra = bitem >> 1, r = ra / A, ai = ra - r * A;
         const uint32_t db = 0x10000u + (uint32_t)(ai * 2 + which) * 64u;
         gd0 = gamma_draw(key, (long)(row0 + r), step_id, db);
       }
-    }, (int)t);
+    };
+    if (defer) trunk_rows<NTO, NHT, 1, false>(w1, w2, lds, 2 * A, tid, draw0, (int)t);
+    else trunk_rows<NTO, NHT>(w1, w2, lds, 2 * A, tid, draw0, (int)t);
     // ---- Beta sample (k_act3 stage 1 / 2, PPO_SAMPLE); the log-prob terms either here (as k_act3)
     // or, with a.s_beta, stored for k_beta_logp after the rollout (they are not on the env's path) ----
-    const bool defer = a.s_beta != nullptr;
     ROLL_STAMP(t, 2);
     if (bitem < R * A * 2) {
       const int idx = bitem, which = idx & 1, ra = idx >> 1, r = ra / A, ai = ra - r * A;
       const long env = row0 + r;
-      const float c = softplusf_(PRE[r * LDP + ai + which * A]) + 1.0f;
+      float pre;
+      if (defer) {
+        const int h = ai + which * A;
+        const float* HP = lds + GE::oHP;
+        float sm = 0.f;
+#pragma unroll
+        for (int w = 0; w < kActWaves; ++w) sm += HP[(w * GE::NHP + h) * R + r];
+        pre = sm + lds[GE::oHBIAS + h];
+      } else {
+        pre = PRE[r * LDP + ai + which * A];
+      }
+#ifdef PPO_STAMPS
+      if (t == 0 && env == kRdbgEnv) RDBG(0, 1160 + ai + which * A, pre);
+#endif
+      const float c = softplusf_(pre) + 1.0f;
       const uint32_t db = 0x10000u + (uint32_t)(ai * 2 + which) * 64u;
       const float gs = gamma_mt_d0(c, gd0, key, env, step_id, db);
       float* it = ITM + ((r * A + ai) * 2 + which) * 4;
@@ -980,6 +1029,473 @@ __global__ __launch_bounds__(256) void k_values4(ValuesArgs a) {
 }
 
 // =============================================================================================
+// k_rollout_v: the AC rollout for few envs per GPU (the E = 4096 / N shards of N = 4 and 8), on the
+// VALU instead of MFMA, R = 2 or 4 envs per workgroup.
+//
+// k_rollout's step is bounded by layer 2 on one CU: 1 024 16x16x4 MFMAs for its 16-env block
+// (8.2 K cycles per SIMD), whatever number of those 16 rows is real — at E = 512 its 32 workgroups
+// leave 224 CUs idle and every step still pays the 16-row layer. Here a workgroup owns R envs (all
+// CUs busy at E = 512 with R = 2) and the layers run as packed-f32 FMA chains (v_pk_fma_f32, one
+// lane per output feature, R / 2 row pairs per lane), the f32 VALU's rate equal to the MFMA's.
+// Results are bitwise k_act3's: an f32 MFMA is a k-ordered fmaf chain (MI355X guide;
+// scripts/probe/fma_chain_probe: 0 mismatches, also for v_pk_fma_f32), so each layer runs the
+// k_act3 chain order k = 16 t + 4 g + c (t, c outer, g inner) from the bias; the LayerNorm
+// statistics, head partials and their sums repeat k_act3's partial-sum trees exactly (lane
+// partials over the same 8 features, the g-butterfly, the wave-order sums).
+//  * 8 waves: feature quarter w & 3 (lane = feature 64 (w & 3) + lane), k half w >> 2: layer 2's
+//    chain runs k-blocks 0..7 in waves 0-3 and continues 8..15 in waves 4-7 (accumulators handed
+//    over through LDS), so each lane keeps 128 W2 values (chain order) in registers for the whole
+//    rollout; W1 (K <= 32) sits in LDS transposed (lane = feature: conflict-free) for waves 0-3;
+//  * B operands (the layer inputs) sit in LDS in chain order, R floats per k, read as broadcast
+//    ds_read_b128 (every lane the same address);
+//  * LayerNorm statistics: the layer's outputs go to LDS and 8 R x 4 "stats lanes" (old wave, row,
+//    lane group g) recompute k_act3's lane partials from there;
+//  * heads: one lane per (head, old wave, row) runs that wave's 32-feature MFMA chain order;
+//  * Beta sampling, the env step and the episode bookkeeping are k_rollout's, for R envs; the
+//    first Marsaglia-Tsang draws run in waves 4-7 during layer 1 (waves 0-3);
+//  * log-probs deferred to k_beta_logp (a.s_beta) only.
+// =============================================================================================
+namespace {
+template <int NTO, int R>
+struct RollVGeo {
+  static constexpr int H = 256, OP = NTO * 16, NHP = 16, LDZ = H + 4, LDQ = OP + 1;
+  static constexpr int oXV = 0;                     // layer-1 input, chain order: [OP][R]
+  static constexpr int oHV = oXV + OP * R;          // layer-2 input, chain order: [H][R]
+  static constexpr int oACH = oHV + H * R;          // layer-2 accumulators k half 0 -> 1: [H][R]
+  static constexpr int oZL = oACH + H * R;          // layer outputs, natural order: [R][LDZ]
+  static constexpr int oH2 = oZL + R * LDZ;         // head inputs h2: [R][LDZ]
+  static constexpr int oRS = oH2 + R * LDZ;         // stats partials: sums [8][R], squares [8][R]
+  static constexpr int oW3 = oRS + 16 * R;          // head rows [NHP][H]
+  static constexpr int oHB = oW3 + NHP * H;         // head biases [NHP]
+  static constexpr int oHP = oHB + NHP;             // head partials [8][NHP][R]
+  static constexpr int oITM = oHP + 8 * NHP * R;    // Beta items [R][24][2][4]
+  static constexpr int oXO = oITM + R * 24 * 2 * 4;  // agent input obs of the step [R][LDQ]
+  static constexpr int oQ = oXO + R * LDQ;          // env state q [R][LDQ]
+  static constexpr int oNRM = oQ + R * LDQ;         // obs mean | std [2][OP]
+  static constexpr int oACT = oNRM + 2 * OP;        // actions [R][24]
+  static constexpr int oENV = oACT + R * 24;        // per-env scalars [16][R]
+  static constexpr int oW1 = oENV + 16 * R;         // W1 transposed, chain order: [OP][H]
+  static constexpr int total = oW1 + OP * H;
+};
+// chain position of input k in a 16x16x4 layer chain: k-block t, k-step c, lane group g
+PPO_DEV int chain_pos(int k) { return (k & ~15) | ((k & 3) << 2) | ((k >> 2) & 3); }
+typedef float f2v __attribute__((ext_vector_type(2)));
+// acc = fma(w, x, acc) as one v_fma_f32 (single rounding: the MFMA chain's step). Written as asm so
+// the SLP vectorizer cannot pack the per-row FMAs of one weight into v_pk_fma_f32 with the weight
+// duplicated into a register pair (2 VGPRs per resident weight: the layer's 128 no longer fit)
+PPO_DEV void fma_v(float& acc, float w, float x) { asm("v_fma_f32 %0, %1, %2, %0" : "+v"(acc) : "v"(w), "v"(x)); }
+template <int R>
+PPO_DEV void fma_rows(float (&acc)[R], float w, const float* x) {  // x: the R rows' inputs
+#pragma unroll
+  for (int i = 0; i < R; ++i) fma_v(acc[i], w, x[i]);
+}
+}  // namespace
+
+constexpr int kRVThreads = 512;
+template <int NTO, int R>
+__global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
+  using GE = RollVGeo<NTO, R>;
+  constexpr int H = 256, OP = GE::OP, NHP = GE::NHP, LDZ = GE::LDZ, LDQ = GE::LDQ;
+  constexpr int NCH = (OP + 31) / 32;
+  static_assert(R == 2 || R == 4, "k_rollout_v: 2 or 4 envs per workgroup");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* XV = lds + GE::oXV;
+  float* HV = lds + GE::oHV;
+  float* ACH = lds + GE::oACH;
+  float* ZL = lds + GE::oZL;
+  float* H2 = lds + GE::oH2;
+  float* RS = lds + GE::oRS;
+  float* W3 = lds + GE::oW3;
+  float* HBIAS = lds + GE::oHB;
+  float* HP = lds + GE::oHP;
+  float* ITM = lds + GE::oITM;
+  float* XO = lds + GE::oXO;
+  float* Q = lds + GE::oQ;
+  float* NRM = lds + GE::oNRM;
+  float* ACT = lds + GE::oACT;
+  float* EV = lds + GE::oENV;
+  int* EVI = reinterpret_cast<int*>(EV);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kh = wave >> 2, f = 64 * (wave & 3) + lane;  // this lane's output feature, k half
+  const PackedLayout& K = a.K;
+  const TrunkDev& T = K.tr[1];
+  const float* __restrict__ P = a.P;
+  const int O = K.O, A = K.A, E = a.E, nh = 2 * A;
+  const int row0 = blockIdx.x * R;
+  const SynthArgs& sv = a.env;
+
+  // ---- prologue: this lane's weights in chain order, staged head rows, env state of the block ----
+  float w2r[128];
+  float* W1T = lds + GE::oW1;
+  for (int i = tid; i < OP * H; i += kRVThreads) {
+    const int p = i / H, ff = i - p * H;
+    W1T[i] = P[T.W1 + (long)ff * OP + chain_pos(p)];  // chain_pos is its own inverse
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f4 v = ld4(P + T.W2 + (long)f * H + 16 * (8 * kh + t) + 4 * g);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) w2r[16 * t + 4 * c + g] = v[c];
+    }
+  const float b1 = P[T.b1 + f], b2 = P[T.b2 + f];
+  const float g1 = P[T.g1 + f], be1 = P[T.be1 + f], g2 = P[T.g2 + f], be2 = P[T.be2 + f];
+  for (int i = tid; i < NHP * H; i += kRVThreads) {
+    const int h = i / H, k = i - h * H;
+    const int hr = act_head_row(K, 1, h);
+    W3[i] = hr >= 0 ? P[hr + k] : 0.0f;
+  }
+  if (tid < NHP) {
+    const int hbo = act_head_bias(K, 1, tid);
+    HBIAS[tid] = hbo >= 0 ? P[hbo] : 0.0f;
+  }
+  for (int i = tid; i < OP; i += kRVThreads) {
+    NRM[i] = i < O ? P[K.omean + i] : 0.0f;
+    NRM[OP + i] = i < O ? P[K.ostd + i] : 1.0f;
+  }
+  for (int idx = tid; idx < R * O; idx += kRVThreads) {
+    const int r = idx / O, ff = idx - r * O, e = row0 + r;
+    XO[r * LDQ + ff] = e < E ? a.next_obs[(long)e * O + ff] : 0.0f;
+    Q[r * LDQ + ff] = e < E ? sv.q[(long)e * O + ff] : 0.0f;
+  }
+  if (tid < R) {
+    const int e = min(row0 + tid, E - 1);
+    EV[EV_DONE * R + tid] = a.next_done[e];
+    EVI[EV_AR * R + tid] = sv.autoreset[e];
+    EVI[EV_T * R + tid] = sv.t[e];
+    EVI[EV_RSEED * R + tid] = (int)sv.rseed[e];
+    EVI[EV_RCOUNT * R + tid] = (int)sv.rcount[e];
+    EV[EV_EPR * R + tid] = sv.ep_ret[e];
+    EVI[EV_EPL * R + tid] = sv.ep_len[e];
+    EV[EV_FR * R + tid] = sv.fin_ret[e];
+    EV[EV_FL * R + tid] = sv.fin_len[e];
+    EV[EV_FC * R + tid] = sv.fin_cnt[e];
+  }
+  lds_barrier();
+  const SampleKey key = sample_key(a.seed, a.rank);
+  const float hi = P[K.hi], lo = P[K.lo];
+  // Beta items (row, action, alpha | beta) in waves 4-7 (idle during layer 1, where their first
+  // Marsaglia-Tsang draws are computed), spread evenly
+  const int bper = (R * A * 2 + 3) / 4;
+  const int bitem = (kh == 1 && lane < bper) ? (wave - 4) * bper + lane : R * A * 2;
+  auto draw0 = [&](long step) {
+    GammaDraw d = GammaDraw{0.f, 0.f};
+    if (bitem < R * A * 2) {
+      const int which = bitem & 1, ra = bitem >> 1, r = ra / A, ai = ra - r * A;
+      d = gamma_draw(key, (long)(row0 + r), step, 0x10000u + (uint32_t)(ai * 2 + which) * 64u);
+    }
+    return d;
+  };
+  GammaDraw gd0 = GammaDraw{0.f, 0.f};
+  // LayerNorm statistics lanes: (old wave ow, row r, lane group g), 8 R x 4 of them (waves 0 ..)
+  constexpr int NSL = 8 * R * 4;
+  const int sg = tid & 3, sr = (tid >> 2) & (R - 1), sow = tid / (4 * R);
+  // LayerNorm of the layer outputs in ZL (k_act3 act_activate's statistics, bitwise): mean and
+  // 1 / std of row r, every thread; 3 barriers
+  auto ln_stats = [&](float (&mu)[R], float (&rs)[R]) {
+    f4 va = f4{0.f, 0.f, 0.f, 0.f}, vb = va;
+    if (tid < NSL) {
+      va = *reinterpret_cast<const f4*>(ZL + sr * LDZ + 32 * sow + 4 * sg);
+      vb = *reinterpret_cast<const f4*>(ZL + sr * LDZ + 32 * sow + 16 + 4 * sg);
+      float s = (va.x + va.y) + (va.z + va.w) + ((vb.x + vb.y) + (vb.z + vb.w));
+      s = s + dpp_f<kDppQuadXor1>(s);
+      s = s + dpp_f<kDppQuadXor2>(s);
+      if (sg == 0) RS[sow * R + sr] = s;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < kActWaves; ++w) t += RS[w * R + r];
+      mu[r] = t * (1.0f / 256);
+    }
+    if (tid < NSL) {
+      float q = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float d = (u ? vb : va)[c] - mu[sr];
+          q = __fmaf_rn(d, d, q);
+        }
+      q = q + dpp_f<kDppQuadXor1>(q);
+      q = q + dpp_f<kDppQuadXor2>(q);
+      if (sg == 0) RS[(8 + sow) * R + sr] = q;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < kActWaves; ++w) v += RS[(8 + w) * R + r];
+      rs[r] = 1.0f / sqrtf(__fmaf_rn(v, 1.0f / 256, 1e-5f));
+    }
+    lds_barrier();  // RS is reused by the next statistics
+  };
+  for (int t = 0; t < a.T; ++t) {
+    const long step_id = a.step0 + t;
+    ROLL_STAMP(t, 0);
+#ifdef PPO_STAMPS
+    const int dbg_r = (t == 0 && kRdbgEnv >= row0 && kRdbgEnv < row0 + R) ? kRdbgEnv - row0 : -1;
+#endif
+    // ---- inputs: rollout stores of obs[t] / dones[t]; normalised rows into XV (chain order) ----
+    for (int idx = tid; idx < R * OP; idx += kRVThreads) {
+      const int r = idx / OP, ff = idx - r * OP, e = row0 + r;
+      const bool valid = e < E && ff < O;
+      const float x = valid ? XO[r * LDQ + ff] : 0.0f;
+      if (valid) a.s_obs[((long)t * E + e) * O + ff] = x;
+      XV[chain_pos(ff) * R + r] = valid ? (x - NRM[ff]) / NRM[OP + ff] : x;
+    }
+    if (tid < R && row0 + tid < E) a.s_dones[(long)t * E + row0 + tid] = EV[EV_DONE * R + tid];
+    lds_barrier();
+    ROLL_STAMP(t, 1);
+    // ---- layer 1 (waves 0-3; k_act3's chain from the bias) ----
+    float acc[R];
+    if (kh == 0) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) acc[i] = b1;
+#pragma unroll
+      for (int p = 0; p < OP; p += 2) {
+        float x[2 * R];  // positions p, p + 1: R inputs each
+        *reinterpret_cast<f4*>(x) = *reinterpret_cast<const f4*>(XV + R * p);
+        if constexpr (R == 4) *reinterpret_cast<f4*>(x + 4) = *reinterpret_cast<const f4*>(XV + R * p + 4);
+        fma_rows<R>(acc, W1T[p * H + f], x);
+        fma_rows<R>(acc, W1T[(p + 1) * H + f], x + R);
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) ZL[i * LDZ + f] = acc[i];
+#ifdef PPO_STAMPS
+      if (dbg_r >= 0) RDBG(1, f, acc[dbg_r]);
+#endif
+    } else {
+      gd0 = draw0(step_id);
+    }
+    lds_barrier();
+    float mu[R], rs[R];
+    ln_stats(mu, rs);
+    if (kh == 0) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const float y = __fmaf_rn(g1, (acc[i] - mu[i]) * rs[i], be1);
+        HV[chain_pos(f) * R + i] = y > 0.0f ? y : 0.0f;
+#ifdef PPO_STAMPS
+        if (i == dbg_r) RDBG(1, 260 + f, y > 0.0f ? y : 0.0f);
+#endif
+      }
+    }
+    lds_barrier();
+    ROLL_STAMP(t, 5);
+    // ---- layer 2: k-blocks 0..7 in waves 0-3 from the bias, handed over, 8..15 in waves 4-7 ----
+    if (kh == 1) {
+      lds_barrier();  // waves 0-3 stored their accumulators
+#pragma unroll
+      for (int i = 0; i < R; ++i) acc[i] = ACH[f * R + i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < R; ++i) acc[i] = b2;
+    }
+    {
+      const int p0 = 128 * kh;
+#pragma unroll
+      for (int p = 0; p < 128; p += 2) {
+        // bound the broadcast reads in flight (the compiler otherwise hoists the whole layer's)
+        if (p % 16 == 0) __builtin_amdgcn_sched_barrier(0);
+        float x[2 * R];
+        *reinterpret_cast<f4*>(x) = *reinterpret_cast<const f4*>(HV + R * (p0 + p));
+        if constexpr (R == 4) *reinterpret_cast<f4*>(x + 4) = *reinterpret_cast<const f4*>(HV + R * (p0 + p) + 4);
+        fma_rows<R>(acc, w2r[p], x);
+        fma_rows<R>(acc, w2r[p + 1], x + R);
+      }
+      if (kh == 0) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) ACH[f * R + i] = acc[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < R; ++i) ZL[i * LDZ + f] = acc[i];
+#ifdef PPO_STAMPS
+        if (dbg_r >= 0) RDBG(1, 516 + f, acc[dbg_r]);
+#endif
+      }
+    }
+    if (kh == 0) lds_barrier();  // pairs with the k-half-1 waves' barrier above
+    lds_barrier();
+    ROLL_STAMP(t, 6);
+    ln_stats(mu, rs);
+    if (kh == 1) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const float y = __fmaf_rn(g2, (acc[i] - mu[i]) * rs[i], be2);
+        H2[i * LDZ + f] = y > 0.0f ? y : 0.0f;
+#ifdef PPO_STAMPS
+        if (i == dbg_r) RDBG(1, 776 + f, y > 0.0f ? y : 0.0f);
+#endif
+      }
+    }
+    lds_barrier();
+    ROLL_STAMP(t, 7);
+    // ---- heads: (head, old wave, row) partials in the MFMA chain order of that wave's features ----
+    for (int idx = tid; idx < nh * 8 * R; idx += kRVThreads) {
+      const int r = idx % R, ow = (idx / R) & 7, h = idx / (8 * R);
+      float hp = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int ff = 32 * ow + 16 * u + 4 * g + c;
+            hp = __builtin_fmaf(W3[h * H + ff], H2[r * LDZ + ff], hp);
+            if (g == 3 && (c & 1)) __builtin_amdgcn_sched_barrier(0);  // bound the reads in flight
+          }
+      HP[(ow * NHP + h) * R + r] = hp;
+#ifdef PPO_STAMPS
+      if (r == dbg_r) RDBG(1, 1032 + ow * 16 + h, hp);
+#endif
+    }
+    lds_barrier();
+    ROLL_STAMP(t, 2);
+    // ---- Beta sample (k_rollout / k_act3 stages 1 and 2) ----
+    if (bitem < R * A * 2) {
+      const int which = bitem & 1, ra = bitem >> 1, r = ra / A, ai = ra - r * A, h = ai + which * A;
+      float sm = 0.f;
+#pragma unroll
+      for (int w = 0; w < kActWaves; ++w) sm += HP[(w * NHP + h) * R + r];
+      const float c = softplusf_(sm + HBIAS[h]) + 1.0f;
+#ifdef PPO_STAMPS
+      if (r == dbg_r) RDBG(1, 1160 + h, sm + HBIAS[h]);
+#endif
+      const uint32_t db = 0x10000u + (uint32_t)(ai * 2 + which) * 64u;
+      const float gs = gamma_mt_d0(c, gd0, key, (long)(row0 + r), step_id, db);
+      float* it = ITM + ((r * A + ai) * 2 + which) * 4;
+      it[0] = c;
+      it[1] = gs;
+    }
+    lds_barrier();
+    if (tid < R * A) {
+      const int idx = tid, r = idx / A, ai = idx - r * A, e = row0 + r;
+      const float* ia = ITM + (idx * 2 + 0) * 4;
+      const float* ib = ITM + (idx * 2 + 1) * 4;
+      const float al = ia[0], be = ib[0];
+      const float s01 = ia[1] / (ia[1] + ib[1]);
+      const float act = (s01 - 0.0f) / (1.0f - 0.0f) * (hi - lo) + lo;
+      ACT[r * 24 + ai] = act;
+      if (e < E) {
+        a.s_actions[((long)t * E + e) * A + ai] = act;
+        float* d = a.s_beta + (((long)t * E + e) * A + ai) * 3;
+        d[0] = al;
+        d[1] = be;
+        d[2] = s01;
+      }
+    }
+    lds_barrier();
+    ROLL_STAMP(t, 3);
+    // ---- env step (k_rollout's: 32 lanes per env) ----
+    if (tid < 32 * R) {
+#pragma clang fp contract(off)
+      const int r = tid >> 5, i0 = tid & 31, e = row0 + r;
+      const bool live = e < E;
+      const bool reset = EVI[EV_AR * R + r] != 0;
+      float* q = Q + r * LDQ;
+      float* xo = XO + r * LDQ;
+      const float* ar = ACT + r * 24;
+      if (live && reset) {
+        const uint32_t rsd = (uint32_t)EVI[EV_RSEED * R + r], rc = (uint32_t)EVI[EV_RCOUNT * R + r];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int i = 32 * c + i0;
+          if (i < O) {
+            uint32_t rr[4];
+            philox4x32(rc, (uint32_t)i, 0u, 0u, rsd, 0x5EED5EEDu, rr);
+            const float v = (0.1f * ((2.0f * u01(rr[0])) - 1.0f));
+            q[i] = v;
+            xo[i] = v;
+          }
+        }
+        if (i0 == 0) {
+          EVI[EV_RCOUNT * R + r] = (int)(rc + 1);
+          EVI[EV_T * R + r] = 0;
+          EV[EV_EPR * R + r] = 0.0f;
+          EVI[EV_EPL * R + r] = 0;
+          EV[EV_DONE * R + r] = 0.0f;
+          EVI[EV_AR * R + r] = 0;
+          a.s_rewards[(long)t * E + e] = 0.0f;
+        }
+      } else if (live) {
+        float qo[NCH], qn[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int i = 32 * c + i0;
+          qo[c] = i < O ? q[i] : 0.0f;
+          qn[c] = i < O ? q[i + 1 < O ? i + 1 : 0] : 0.0f;
+        }
+        float q0_new = 0.0f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const int i = 32 * c + i0;
+          if (i < O) {
+            const float ai = fminf(fmaxf(ar[i % A], a.lo), a.hi);
+            const float nq = __fmaf_rn(0.9f, qo[c], __fmaf_rn(0.1f, ai, (0.05f * qn[c])));
+            q[i] = nq;
+            xo[i] = nq;
+            if (c == 0) q0_new = nq;
+          }
+        }
+        if (i0 == 0) {
+          const float vel = ((q0_new - qo[0]) / 0.05f);
+          float ctrl = 0.0f;
+          for (int k = 0; k < A; ++k) {
+            const float ak = fminf(fmaxf(ar[k], a.lo), a.hi);
+            ctrl = (ctrl + ((0.1f * ak) * ak));
+          }
+          const float rw = (vel - ctrl);
+          const int tt = EVI[EV_T * R + r] + 1;
+          EVI[EV_T * R + r] = tt;
+          const bool tr = tt >= 1000;
+          a.s_rewards[(long)t * E + e] = rw;
+          EV[EV_DONE * R + r] = tr ? 1.0f : 0.0f;
+          const float epr = (EV[EV_EPR * R + r] + rw);
+          EV[EV_EPR * R + r] = epr;
+          const int epl = EVI[EV_EPL * R + r] + 1;
+          EVI[EV_EPL * R + r] = epl;
+          if (tr) {
+            EV[EV_FR * R + r] += epr;
+            EV[EV_FL * R + r] += (float)epl;
+            EV[EV_FC * R + r] += 1.0f;
+          }
+          EVI[EV_AR * R + r] = tr ? 1 : 0;
+        }
+      }
+    }
+    lds_barrier();
+    ROLL_STAMP(t, 4);
+  }
+  // ---- epilogue: next_obs / next_done and the env state back to HBM ----
+  for (int idx = tid; idx < R * O; idx += kRVThreads) {
+    const int r = idx / O, ff = idx - r * O, e = row0 + r;
+    if (e < E) {
+      a.next_obs[(long)e * O + ff] = XO[r * LDQ + ff];
+      sv.q[(long)e * O + ff] = Q[r * LDQ + ff];
+    }
+  }
+  if (tid < R && row0 + tid < E) {
+    const int e = row0 + tid;
+    a.next_done[e] = EV[EV_DONE * R + tid];
+    sv.autoreset[e] = EVI[EV_AR * R + tid];
+    sv.t[e] = EVI[EV_T * R + tid];
+    sv.rseed[e] = (uint32_t)EVI[EV_RSEED * R + tid];
+    sv.rcount[e] = (uint32_t)EVI[EV_RCOUNT * R + tid];
+    sv.ep_ret[e] = EV[EV_EPR * R + tid];
+    sv.ep_len[e] = EVI[EV_EPL * R + tid];
+    sv.fin_ret[e] = EV[EV_FR * R + tid];
+    sv.fin_len[e] = EV[EV_FL * R + tid];
+    sv.fin_cnt[e] = EV[EV_FC * R + tid];
+  }
+}
+
+// =============================================================================================
 // launchers
 // =============================================================================================
 int rollout_supported(const PackedLayout& K) {
@@ -1021,12 +1537,33 @@ static int launch_rollout_t(const RolloutArgs& a, hipStream_t s) {
   static const bool ok = hipFuncSetAttribute((const void*)k_rollout<NTO, NHT>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
   if (!ok) return -2;
-  hipLaunchKernelGGL((k_rollout<NTO, NHT>), dim3((a.E + kRows - 1) / kRows), dim3(kActThreads), lds, s, a);
+  hipLaunchKernelGGL((k_rollout<NTO, NHT>), dim3((a.E + kRows - 1) / kRows), dim3(kRVThreads), lds, s, a);
   return 0;
+}
+
+template <int NTO, int R>
+static int launch_rollout_v_t(const RolloutArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)RollVGeo<NTO, R>::total * sizeof(float);
+  hipLaunchKernelGGL((k_rollout_v<NTO, R>), dim3((a.E + R - 1) / R), dim3(kRVThreads), lds, s, a);
+  return 0;
+}
+
+// the VALU rollout where it applies: AC agent, O <= 32, and few envs (auto: E <= 1024, the N >= 4
+// shards of the metric config); a.variant 1 forces k_rollout, 2 k_rollout_v
+static int rollout_v_rows(const RolloutArgs& a) {
+  if (a.K.kind != PPO_NET_LN_BETA || a.K.OP > 32 || a.env.w.on || !a.s_beta || a.variant == 1) return 0;
+  if (a.variant == 2) return a.E <= 512 ? 2 : 4;
+  // auto: R = 2 at E <= 512 (rollout 1.23 -> 1.01 ms per iteration); R = 4 at E = 1 024 measured
+  // slower than k_rollout (1.42 vs 1.19 ms, profiles/r04/rollout_v/), so only variant 2 selects it
+  return a.E <= 512 ? 2 : 0;
 }
 
 int launch_rollout(const RolloutArgs& a, hipStream_t s) {
   if (rollout_supported(a.K) != 0) return -1;
+  if (const int rv = rollout_v_rows(a)) {
+    if (a.K.OP == 16) return rv == 2 ? launch_rollout_v_t<1, 2>(a, s) : launch_rollout_v_t<1, 4>(a, s);
+    return rv == 2 ? launch_rollout_v_t<2, 2>(a, s) : launch_rollout_v_t<2, 4>(a, s);
+  }
   if (a.K.kind == PPO_NET_TANH_NORMAL) {
     const int nht = (a.K.A + 15) / 16;
     switch (a.K.OP / 16) {

@@ -9,10 +9,10 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd $R
-if [ -x scripts/probe/fma_chain_probe ]; then
-  timeout -k 10 60 scripts/probe/fma_chain_probe > $OUT/fma_chain_probe.jsonl 2>&1 || { echo "probe failed"; cat $OUT/fma_chain_probe.jsonl; exit 1; }
-  cat $OUT/fma_chain_probe.jsonl
-fi
+for PR in ${PROBES:-}; do
+  timeout -k 10 60 scripts/probe/$PR > $OUT/$PR.jsonl 2>&1 || { echo "probe $PR failed"; cat $OUT/$PR.jsonl; exit 1; }
+  cat $OUT/$PR.jsonl
+done
 if [ "$TESTS" != none ]; then
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu $TESTS > $OUT/tests.txt 2>&1 || { echo "tests failed"; tail -40 $OUT/tests.txt; exit 1; }
 tail -2 $OUT/tests.txt

@@ -31,10 +31,13 @@ def snapshot(tr):
 
 
 @pytest.mark.parametrize("agent,env_id,E,iters", [("ac", "HalfCheetah-v5", 200, 9), ("ac", "Hopper-v5", 37, 9),
-                                                  ("ac", "Ant-v5", 96, 3), ("ppo", "HalfCheetah-v5", 37, 9),
+                                                  ("ac", "HalfCheetah-v5", 998, 2), ("ac", "Ant-v5", 96, 3),
+                                                  ("ppo", "HalfCheetah-v5", 37, 9),
                                                   ("ppo", "Hopper-v5", 20, 2), ("ppo", "Humanoid-v4", 40, 2)])
 def test_persistent_rollout_bitwise_equals_per_step(agent, env_id, E, iters):
-    """AC agent: k_rollout + k_values vs k_act3 + k_synth_step. PPO agent: k_rollout4 + k_values4 vs
+    """AC agent: the persistent rollout (k_rollout_v, the VALU form with 2 / 4 envs per workgroup, at
+    E <= 1024 and O <= 32 — E = 200 / 37 / 998 here; k_rollout, 16 envs per workgroup on MFMA, for
+    Ant's O = 105) + k_values vs k_act3 + k_synth_step. PPO agent: k_rollout4 + k_values4 vs
     k_act4 (act_kernel=4) + k_synth_step(_wide), with the PPO wrapper chain (ppo:41-49) fused into
     both (Humanoid: O = 376, A = 17, two head tiles, actions clipped to [-0.4, 0.4])."""
     T = 128
@@ -62,6 +65,33 @@ def test_persistent_rollout_bitwise_equals_per_step(agent, env_id, E, iters):
     if agent == "ppo":
         for k, v in trs[0].wrappers.state().items():
             np.testing.assert_array_equal(v, trs[1].wrappers.state()[k], err_msg=k)
+    for tr in trs:
+        tr.close()
+
+
+@pytest.mark.parametrize("E", [512, 1024])
+def test_valu_rollout_bitwise_equals_mfma_rollout(E):
+    """The N = 8 / N = 4 shards of the metric config (AC HalfCheetah, E = 512 / 1 024): the VALU
+    rollout (rollout_kernel=valu: 2 / 4 envs per workgroup, v_fma_f32 chains in the MFMA's k order,
+    k_act3's LayerNorm / head partial-sum trees) against the MFMA rollout (rollout_kernel=mfma):
+    every stored buffer, the env state and, after the shared update, the parameters bitwise equal over
+    two iterations."""
+    cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=E, num_steps=128, num_minibatches=4,
+                              update_epochs=1, total_timesteps=E * 128 * 2)
+    trs = [ppo_amd.Trainer(cfg, options="rollout_kernel=valu"), ppo_amd.Trainer(cfg, options="rollout_kernel=mfma")]
+    for it in range(2):
+        snaps = []
+        for tr in trs:
+            tr.rollout()
+            tr.agent.sync()
+            snaps.append(snapshot(tr))
+            tr.agent.compute_gae(tr.next_obs, tr.next_done)
+            tr.agent.update(tr.lr_now(), want_stats=False)
+            tr.iteration += 1
+        for k in snaps[0]:
+            np.testing.assert_array_equal(snaps[0][k], snaps[1][k], err_msg=f"iteration {it}: {k}")
+        assert trs[0].env.episode_stats() == trs[1].env.episode_stats()
+        np.testing.assert_array_equal(trs[0].agent.params(), trs[1].agent.params())
     for tr in trs:
         tr.close()
 

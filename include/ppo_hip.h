@@ -99,10 +99,13 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            of both trunks as one gathered GEMM (k_l1g) and k_upd2's tail in its own
  *                            launch at 2 / 3 workgroups per CU, or the single k_upd2 (0; auto: the
  *                            single kernel, measured faster)
+ *   upd_mfma=auto|16|32      LayerNorm-Beta agent at hidden 256: the fused minibatch kernel on
+ *                            16x16x4 MFMAs (k_upd; auto) or on 32x32x2 MFMAs (k_upd32); the same
+ *                            results up to summation order
  *   rollout=auto|per_step    ppo_rollout_synth: persistent launch where supported, or per step
  *   rollout_kernel=auto|mfma|valu  the AC agent's persistent rollout: k_rollout (16 envs per
- *                            workgroup, MFMA) or k_rollout_v (2 / 4 envs per workgroup, VALU; O <= 32);
- *                            auto: k_rollout_v at E <= 512 (R = 2). Bitwise the same results
+ *                            workgroup, MFMA) or k_rollout_v (2 envs per workgroup, VALU; O <= 32);
+ *                            auto: k_rollout_v at E <= 512. Bitwise the same results
  *   gradstep=split|fused     clip_grad_norm_ + Adam: two launches (k_gradnorm, k_adam; default) or
  *                            one cooperative launch (k_gradstep: slower on ROCm 7, whose cooperative
  *                            launch costs ~30 us); bitwise the same

@@ -1029,40 +1029,38 @@ __global__ __launch_bounds__(256) void k_values4(ValuesArgs a) {
 }
 
 // =============================================================================================
-// k_rollout_v: the AC rollout for few envs per GPU (the E = 4096 / N shards of N = 4 and 8), on the
-// VALU instead of MFMA, R = 2 or 4 envs per workgroup.
+// k_rollout_v: the AC rollout for few envs per GPU (E <= 512: the E = 4096 / 8 shard), on the VALU
+// instead of MFMA, 2 envs per workgroup.
 //
 // k_rollout's step is bounded by layer 2 on one CU: 1 024 16x16x4 MFMAs for its 16-env block
 // (8.2 K cycles per SIMD), whatever number of those 16 rows is real — at E = 512 its 32 workgroups
-// leave 224 CUs idle and every step still pays the 16-row layer. Here a workgroup owns R envs (all
-// CUs busy at E = 512 with R = 2) and the layers run as packed-f32 FMA chains (v_pk_fma_f32, one
-// lane per output feature, R / 2 row pairs per lane), the f32 VALU's rate equal to the MFMA's.
-// Results are bitwise k_act3's: an f32 MFMA is a k-ordered fmaf chain (MI355X guide;
-// scripts/probe/fma_chain_probe: 0 mismatches, also for v_pk_fma_f32), so each layer runs the
-// k_act3 chain order k = 16 t + 4 g + c (t, c outer, g inner) from the bias; the LayerNorm
-// statistics, head partials and their sums repeat k_act3's partial-sum trees exactly (lane
+// leave 224 CUs idle and every step still pays the 16-row layer. Here a workgroup owns 2 envs (all
+// CUs busy at E = 512) and the layers run as v_fma_f32 chains, one lane per (row, output feature),
+// the f32 VALU's rate equal to the MFMA's. Results are bitwise k_act3's: an f32 MFMA is a k-ordered
+// fmaf chain (MI355X guide; scripts/probe/fma_chain_probe, fma_chain_big_probe: 0 mismatches), so
+// each layer runs the k_act3 chain order k = 16 t + 4 g + c (t, c outer, g inner) from the bias; the
+// LayerNorm statistics, head partials and their sums repeat k_act3's partial-sum trees exactly (lane
 // partials over the same 8 features, the g-butterfly, the wave-order sums).
-//  * 8 waves: feature quarter w & 3 (lane = feature 64 (w & 3) + lane), k half w >> 2: layer 2's
-//    chain runs k-blocks 0..7 in waves 0-3 and continues 8..15 in waves 4-7 (accumulators handed
-//    over through LDS), so each lane keeps 128 W2 values (chain order) in registers for the whole
-//    rollout; W1 (K <= 32) sits in LDS transposed (lane = feature: conflict-free) for waves 0-3;
-//  * B operands (the layer inputs) sit in LDS in chain order, R floats per k, read as broadcast
-//    ds_read_b128 (every lane the same address);
-//  * LayerNorm statistics: the layer's outputs go to LDS and 8 R x 4 "stats lanes" (old wave, row,
+//  * 8 waves: row w >> 2, feature quarter w & 3 (lane = feature 64 (w & 3) + lane); each lane keeps
+//    its W1 row and W2 chain positions 0..127 in registers (160 VGPRs) for the whole rollout, and
+//    positions 128..255 come from one 128 KB LDS copy shared by the two rows (float4 per 4
+//    positions, lane-consecutive: conflict-free);
+//  * B operands (the layer inputs) sit in LDS in chain order per row, read as broadcast ds_read_b128;
+//  * LayerNorm statistics: the layer's outputs go to LDS and 8 x 2 x 4 "stats lanes" (old wave, row,
 //    lane group g) recompute k_act3's lane partials from there;
-//  * heads: one lane per (head, old wave, row) runs that wave's 32-feature MFMA chain order;
-//  * Beta sampling, the env step and the episode bookkeeping are k_rollout's, for R envs; the
-//    first Marsaglia-Tsang draws run in waves 4-7 during layer 1 (waves 0-3);
+//  * heads: one lane per (head, old wave, row) runs that wave's 32-feature MFMA chain order from
+//    float4 reads;
+//  * Beta sampling, the env step and the episode bookkeeping are k_rollout's, for 2 envs;
 //  * log-probs deferred to k_beta_logp (a.s_beta) only.
 // =============================================================================================
 namespace {
-template <int NTO, int R>
+template <int NTO>
 struct RollVGeo {
-  static constexpr int H = 256, OP = NTO * 16, NHP = 16, LDZ = H + 4, LDQ = OP + 1;
-  static constexpr int oXV = 0;                     // layer-1 input, chain order: [OP][R]
-  static constexpr int oHV = oXV + OP * R;          // layer-2 input, chain order: [H][R]
-  static constexpr int oACH = oHV + H * R;          // layer-2 accumulators k half 0 -> 1: [H][R]
-  static constexpr int oZL = oACH + H * R;          // layer outputs, natural order: [R][LDZ]
+  static constexpr int R = 2, H = 256, OP = NTO * 16, NHP = 16, LDZ = H + 4, LDQ = OP + 1;
+  static constexpr int oW2L = 0;                    // W2 chain positions 128..255: [32][H] float4s
+  static constexpr int oXV = oW2L + 128 * H;        // layer-1 input, chain order: [R][OP]
+  static constexpr int oHV = oXV + R * OP;          // layer-2 input, chain order: [R][H]
+  static constexpr int oZL = oHV + R * H;           // layer outputs, natural order: [R][LDZ]
   static constexpr int oH2 = oZL + R * LDZ;         // head inputs h2: [R][LDZ]
   static constexpr int oRS = oH2 + R * LDZ;         // stats partials: sums [8][R], squares [8][R]
   static constexpr int oW3 = oRS + 16 * R;          // head rows [NHP][H]
@@ -1074,34 +1072,26 @@ struct RollVGeo {
   static constexpr int oNRM = oQ + R * LDQ;         // obs mean | std [2][OP]
   static constexpr int oACT = oNRM + 2 * OP;        // actions [R][24]
   static constexpr int oENV = oACT + R * 24;        // per-env scalars [16][R]
-  static constexpr int oW1 = oENV + 16 * R;         // W1 transposed, chain order: [OP][H]
-  static constexpr int total = oW1 + OP * H;
+  static constexpr int total = oENV + 16 * R;
 };
 // chain position of input k in a 16x16x4 layer chain: k-block t, k-step c, lane group g
 PPO_DEV int chain_pos(int k) { return (k & ~15) | ((k & 3) << 2) | ((k >> 2) & 3); }
-typedef float f2v __attribute__((ext_vector_type(2)));
 // acc = fma(w, x, acc) as one v_fma_f32 (single rounding: the MFMA chain's step). Written as asm so
-// the SLP vectorizer cannot pack the per-row FMAs of one weight into v_pk_fma_f32 with the weight
-// duplicated into a register pair (2 VGPRs per resident weight: the layer's 128 no longer fit)
+// the SLP vectorizer cannot pack FMAs of one weight into v_pk_fma_f32 with the weight duplicated
+// into a register pair (2 VGPRs per resident weight: the layer's 160 no longer fit)
 PPO_DEV void fma_v(float& acc, float w, float x) { asm("v_fma_f32 %0, %1, %2, %0" : "+v"(acc) : "v"(w), "v"(x)); }
-template <int R>
-PPO_DEV void fma_rows(float (&acc)[R], float w, const float* x) {  // x: the R rows' inputs
-#pragma unroll
-  for (int i = 0; i < R; ++i) fma_v(acc[i], w, x[i]);
-}
 }  // namespace
 
 constexpr int kRVThreads = 512;
-template <int NTO, int R>
+template <int NTO>
 __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
-  using GE = RollVGeo<NTO, R>;
-  constexpr int H = 256, OP = GE::OP, NHP = GE::NHP, LDZ = GE::LDZ, LDQ = GE::LDQ;
+  using GE = RollVGeo<NTO>;
+  constexpr int R = GE::R, H = 256, OP = GE::OP, NHP = GE::NHP, LDZ = GE::LDZ, LDQ = GE::LDQ;
   constexpr int NCH = (OP + 31) / 32;
-  static_assert(R == 2 || R == 4, "k_rollout_v: 2 or 4 envs per workgroup");
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* W2L = lds + GE::oW2L;
   float* XV = lds + GE::oXV;
   float* HV = lds + GE::oHV;
-  float* ACH = lds + GE::oACH;
   float* ZL = lds + GE::oZL;
   float* H2 = lds + GE::oH2;
   float* RS = lds + GE::oRS;
@@ -1117,7 +1107,7 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
   int* EVI = reinterpret_cast<int*>(EV);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kh = wave >> 2, f = 64 * (wave & 3) + lane;  // this lane's output feature, k half
+  const int rg = wave >> 2, f = 64 * (wave & 3) + lane;  // this lane's row and output feature
   const PackedLayout& K = a.K;
   const TrunkDev& T = K.tr[1];
   const float* __restrict__ P = a.P;
@@ -1125,21 +1115,29 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
   const int row0 = blockIdx.x * R;
   const SynthArgs& sv = a.env;
 
-  // ---- prologue: this lane's weights in chain order, staged head rows, env state of the block ----
-  float w2r[128];
-  float* W1T = lds + GE::oW1;
-  for (int i = tid; i < OP * H; i += kRVThreads) {
-    const int p = i / H, ff = i - p * H;
-    W1T[i] = P[T.W1 + (long)ff * OP + chain_pos(p)];  // chain_pos is its own inverse
-  }
+  // ---- prologue: this lane's weights in chain order (W1 row, W2 row positions 0..127 in
+  // registers, 128..255 in LDS shared by the two rows), staged head rows, env state ----
+  float w1r[OP], w2r[128];
+#pragma unroll
+  for (int t = 0; t < NTO; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f4 v = ld4(P + T.W1 + (long)f * OP + 16 * t + 4 * g);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) w1r[16 * t + 4 * c + g] = v[c];
+    }
 #pragma unroll
   for (int t = 0; t < 8; ++t)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const f4 v = ld4(P + T.W2 + (long)f * H + 16 * (8 * kh + t) + 4 * g);
+      const f4 v = ld4(P + T.W2 + (long)f * H + 16 * t + 4 * g);
 #pragma unroll
       for (int c = 0; c < 4; ++c) w2r[16 * t + 4 * c + g] = v[c];
     }
+  for (int i = tid; i < 128 * H; i += kRVThreads) {
+    const int pp = i / H, ff = i - pp * H;  // chain position 128 + pp of feature ff's row
+    W2L[((pp >> 2) * H + ff) * 4 + (pp & 3)] = P[T.W2 + (long)ff * H + 128 + chain_pos(pp)];
+  }
   const float b1 = P[T.b1 + f], b2 = P[T.b2 + f];
   const float g1 = P[T.g1 + f], be1 = P[T.be1 + f], g2 = P[T.g2 + f], be2 = P[T.be2 + f];
   for (int i = tid; i < NHP * H; i += kRVThreads) {
@@ -1176,20 +1174,10 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
   lds_barrier();
   const SampleKey key = sample_key(a.seed, a.rank);
   const float hi = P[K.hi], lo = P[K.lo];
-  // Beta items (row, action, alpha | beta) in waves 4-7 (idle during layer 1, where their first
-  // Marsaglia-Tsang draws are computed), spread evenly
-  const int bper = (R * A * 2 + 3) / 4;
-  const int bitem = (kh == 1 && lane < bper) ? (wave - 4) * bper + lane : R * A * 2;
-  auto draw0 = [&](long step) {
-    GammaDraw d = GammaDraw{0.f, 0.f};
-    if (bitem < R * A * 2) {
-      const int which = bitem & 1, ra = bitem >> 1, r = ra / A, ai = ra - r * A;
-      d = gamma_draw(key, (long)(row0 + r), step, 0x10000u + (uint32_t)(ai * 2 + which) * 64u);
-    }
-    return d;
-  };
-  GammaDraw gd0 = GammaDraw{0.f, 0.f};
-  // LayerNorm statistics lanes: (old wave ow, row r, lane group g), 8 R x 4 of them (waves 0 ..)
+  // Beta items (row, action, alpha | beta) spread evenly over the 8 waves
+  const int bper = (R * A * 2 + 7) / 8;
+  const int bitem = lane < bper ? wave * bper + lane : R * A * 2;
+  // LayerNorm statistics lanes: (old wave ow, row r, lane group g), 8 R x 4 of them (wave 0)
   constexpr int NSL = 8 * R * 4;
   const int sg = tid & 3, sr = (tid >> 2) & (R - 1), sow = tid / (4 * R);
   // LayerNorm of the layer outputs in ZL (k_act3 act_activate's statistics, bitwise): mean and
@@ -1235,11 +1223,13 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
     }
     lds_barrier();  // RS is reused by the next statistics
   };
+  const float* xv = XV + rg * OP;
+  const float* hv = HV + rg * H;
   for (int t = 0; t < a.T; ++t) {
     const long step_id = a.step0 + t;
     ROLL_STAMP(t, 0);
 #ifdef PPO_STAMPS
-    const int dbg_r = (t == 0 && kRdbgEnv >= row0 && kRdbgEnv < row0 + R) ? kRdbgEnv - row0 : -1;
+    const int dbg_r = (t == 0 && kRdbgEnv == row0 + rg) ? rg : -1;
 #endif
     // ---- inputs: rollout stores of obs[t] / dones[t]; normalised rows into XV (chain order) ----
     for (int idx = tid; idx < R * OP; idx += kRVThreads) {
@@ -1247,92 +1237,71 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
       const bool valid = e < E && ff < O;
       const float x = valid ? XO[r * LDQ + ff] : 0.0f;
       if (valid) a.s_obs[((long)t * E + e) * O + ff] = x;
-      XV[chain_pos(ff) * R + r] = valid ? (x - NRM[ff]) / NRM[OP + ff] : x;
+      XV[r * OP + chain_pos(ff)] = valid ? (x - NRM[ff]) / NRM[OP + ff] : x;
     }
     if (tid < R && row0 + tid < E) a.s_dones[(long)t * E + row0 + tid] = EV[EV_DONE * R + tid];
+    // the first Marsaglia-Tsang attempt's draws of this thread's item: independent of the network
+    GammaDraw gd0 = GammaDraw{0.f, 0.f};
+    if (bitem < R * A * 2) {
+      const int which = bitem & 1, ra = bitem >> 1, r = ra / A, ai = ra - r * A;
+      gd0 = gamma_draw(key, (long)(row0 + r), step_id, 0x10000u + (uint32_t)(ai * 2 + which) * 64u);
+    }
     lds_barrier();
     ROLL_STAMP(t, 1);
-    // ---- layer 1 (waves 0-3; k_act3's chain from the bias) ----
-    float acc[R];
-    if (kh == 0) {
+    // ---- layer 1 (k_act3's chain from the bias), one row per 4 waves ----
+    float acc = b1;
 #pragma unroll
-      for (int i = 0; i < R; ++i) acc[i] = b1;
+    for (int p = 0; p < OP; p += 4) {
+      const f4 x = *reinterpret_cast<const f4*>(xv + p);
 #pragma unroll
-      for (int p = 0; p < OP; p += 2) {
-        float x[2 * R];  // positions p, p + 1: R inputs each
-        *reinterpret_cast<f4*>(x) = *reinterpret_cast<const f4*>(XV + R * p);
-        if constexpr (R == 4) *reinterpret_cast<f4*>(x + 4) = *reinterpret_cast<const f4*>(XV + R * p + 4);
-        fma_rows<R>(acc, W1T[p * H + f], x);
-        fma_rows<R>(acc, W1T[(p + 1) * H + f], x + R);
-      }
-#pragma unroll
-      for (int i = 0; i < R; ++i) ZL[i * LDZ + f] = acc[i];
-#ifdef PPO_STAMPS
-      if (dbg_r >= 0) RDBG(1, f, acc[dbg_r]);
-#endif
-    } else {
-      gd0 = draw0(step_id);
+      for (int c = 0; c < 4; ++c) fma_v(acc, w1r[p + c], x[c]);
     }
+    ZL[rg * LDZ + f] = acc;
+#ifdef PPO_STAMPS
+    if (dbg_r >= 0) RDBG(1, f, acc);
+#endif
     lds_barrier();
     float mu[R], rs[R];
     ln_stats(mu, rs);
-    if (kh == 0) {
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const float y = __fmaf_rn(g1, (acc[i] - mu[i]) * rs[i], be1);
-        HV[chain_pos(f) * R + i] = y > 0.0f ? y : 0.0f;
+    {
+      const float y = __fmaf_rn(g1, (acc - mu[rg]) * rs[rg], be1);
+      HV[rg * H + chain_pos(f)] = y > 0.0f ? y : 0.0f;
 #ifdef PPO_STAMPS
-        if (i == dbg_r) RDBG(1, 260 + f, y > 0.0f ? y : 0.0f);
+      if (dbg_r >= 0) RDBG(1, 260 + f, y > 0.0f ? y : 0.0f);
 #endif
-      }
     }
     lds_barrier();
     ROLL_STAMP(t, 5);
-    // ---- layer 2: k-blocks 0..7 in waves 0-3 from the bias, handed over, 8..15 in waves 4-7 ----
-    if (kh == 1) {
-      lds_barrier();  // waves 0-3 stored their accumulators
+    // ---- layer 2: chain positions 0..127 from registers, 128..255 from LDS ----
+    acc = b2;
 #pragma unroll
-      for (int i = 0; i < R; ++i) acc[i] = ACH[f * R + i];
-    } else {
+    for (int p = 0; p < 128; p += 4) {
+      if (p % 32 == 0) __builtin_amdgcn_sched_barrier(0);  // bound the broadcast reads in flight
+      const f4 x = *reinterpret_cast<const f4*>(hv + p);
 #pragma unroll
-      for (int i = 0; i < R; ++i) acc[i] = b2;
+      for (int c = 0; c < 4; ++c) fma_v(acc, w2r[p + c], x[c]);
     }
-    {
-      const int p0 = 128 * kh;
 #pragma unroll
-      for (int p = 0; p < 128; p += 2) {
-        // bound the broadcast reads in flight (the compiler otherwise hoists the whole layer's)
-        if (p % 16 == 0) __builtin_amdgcn_sched_barrier(0);
-        float x[2 * R];
-        *reinterpret_cast<f4*>(x) = *reinterpret_cast<const f4*>(HV + R * (p0 + p));
-        if constexpr (R == 4) *reinterpret_cast<f4*>(x + 4) = *reinterpret_cast<const f4*>(HV + R * (p0 + p) + 4);
-        fma_rows<R>(acc, w2r[p], x);
-        fma_rows<R>(acc, w2r[p + 1], x + R);
-      }
-      if (kh == 0) {
+    for (int p = 0; p < 128; p += 4) {
+      if (p % 32 == 0) __builtin_amdgcn_sched_barrier(0);
+      const f4 w = *reinterpret_cast<const f4*>(W2L + ((p >> 2) * H + f) * 4);
+      const f4 x = *reinterpret_cast<const f4*>(hv + 128 + p);
 #pragma unroll
-        for (int i = 0; i < R; ++i) ACH[f * R + i] = acc[i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < R; ++i) ZL[i * LDZ + f] = acc[i];
+      for (int c = 0; c < 4; ++c) fma_v(acc, w[c], x[c]);
+    }
+    ZL[rg * LDZ + f] = acc;
 #ifdef PPO_STAMPS
-        if (dbg_r >= 0) RDBG(1, 516 + f, acc[dbg_r]);
+    if (dbg_r >= 0) RDBG(1, 516 + f, acc);
 #endif
-      }
-    }
-    if (kh == 0) lds_barrier();  // pairs with the k-half-1 waves' barrier above
     lds_barrier();
     ROLL_STAMP(t, 6);
     ln_stats(mu, rs);
-    if (kh == 1) {
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const float y = __fmaf_rn(g2, (acc[i] - mu[i]) * rs[i], be2);
-        H2[i * LDZ + f] = y > 0.0f ? y : 0.0f;
+    {
+      const float y = __fmaf_rn(g2, (acc - mu[rg]) * rs[rg], be2);
+      H2[rg * LDZ + f] = y > 0.0f ? y : 0.0f;
 #ifdef PPO_STAMPS
-        if (i == dbg_r) RDBG(1, 776 + f, y > 0.0f ? y : 0.0f);
+      if (dbg_r >= 0) RDBG(1, 776 + f, y > 0.0f ? y : 0.0f);
 #endif
-      }
     }
     lds_barrier();
     ROLL_STAMP(t, 7);
@@ -1341,18 +1310,21 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
       const int r = idx % R, ow = (idx / R) & 7, h = idx / (8 * R);
       float hp = 0.f;
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u) {
+        f4 wq[4], xq[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          wq[g] = *reinterpret_cast<const f4*>(W3 + h * H + 32 * ow + 16 * u + 4 * g);
+          xq[g] = *reinterpret_cast<const f4*>(H2 + r * LDZ + 32 * ow + 16 * u + 4 * g);
+        }
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int ff = 32 * ow + 16 * u + 4 * g + c;
-            hp = __builtin_fmaf(W3[h * H + ff], H2[r * LDZ + ff], hp);
-            if (g == 3 && (c & 1)) __builtin_amdgcn_sched_barrier(0);  // bound the reads in flight
-          }
+          for (int g = 0; g < 4; ++g) hp = __builtin_fmaf(wq[g][c], xq[g][c], hp);
+      }
       HP[(ow * NHP + h) * R + r] = hp;
 #ifdef PPO_STAMPS
-      if (r == dbg_r) RDBG(1, 1032 + ow * 16 + h, hp);
+      if (t == 0 && kRdbgEnv == row0 + r) RDBG(1, 1032 + ow * 16 + h, hp);
 #endif
     }
     lds_barrier();
@@ -1365,7 +1337,7 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
       for (int w = 0; w < kActWaves; ++w) sm += HP[(w * NHP + h) * R + r];
       const float c = softplusf_(sm + HBIAS[h]) + 1.0f;
 #ifdef PPO_STAMPS
-      if (r == dbg_r) RDBG(1, 1160 + h, sm + HBIAS[h]);
+      if (t == 0 && kRdbgEnv == row0 + r) RDBG(1, 1160 + h, sm + HBIAS[h]);
 #endif
       const uint32_t db = 0x10000u + (uint32_t)(ai * 2 + which) * 64u;
       const float gs = gamma_mt_d0(c, gd0, key, (long)(row0 + r), step_id, db);
@@ -1541,29 +1513,26 @@ static int launch_rollout_t(const RolloutArgs& a, hipStream_t s) {
   return 0;
 }
 
-template <int NTO, int R>
+template <int NTO>
 static int launch_rollout_v_t(const RolloutArgs& a, hipStream_t s) {
-  const size_t lds = (size_t)RollVGeo<NTO, R>::total * sizeof(float);
-  hipLaunchKernelGGL((k_rollout_v<NTO, R>), dim3((a.E + R - 1) / R), dim3(kRVThreads), lds, s, a);
+  const size_t lds = (size_t)RollVGeo<NTO>::total * sizeof(float);
+  static const bool ok = hipFuncSetAttribute((const void*)k_rollout_v<NTO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds) == hipSuccess;
+  if (!ok) return -2;
+  hipLaunchKernelGGL((k_rollout_v<NTO>), dim3((a.E + 1) / 2), dim3(kRVThreads), lds, s, a);
   return 0;
 }
 
-// the VALU rollout where it applies: AC agent, O <= 32, and few envs (auto: E <= 1024, the N >= 4
-// shards of the metric config); a.variant 1 forces k_rollout, 2 k_rollout_v
-static int rollout_v_rows(const RolloutArgs& a) {
-  if (a.K.kind != PPO_NET_LN_BETA || a.K.OP > 32 || a.env.w.on || !a.s_beta || a.variant == 1) return 0;
-  if (a.variant == 2) return a.E <= 512 ? 2 : 4;
-  // auto: R = 2 at E <= 512 (rollout 1.23 -> 1.01 ms per iteration); R = 4 at E = 1 024 measured
-  // slower than k_rollout (1.42 vs 1.19 ms, profiles/r04/rollout_v/), so only variant 2 selects it
-  return a.E <= 512 ? 2 : 0;
+// the VALU rollout where it applies: AC agent, O <= 32, and few envs (auto: E <= 512, the N = 8
+// shard of the metric config); a.variant 1 forces k_rollout, 2 k_rollout_v
+static bool use_rollout_v(const RolloutArgs& a) {
+  if (a.K.kind != PPO_NET_LN_BETA || a.K.OP > 32 || a.env.w.on || !a.s_beta || a.variant == 1) return false;
+  return a.variant == 2 || a.E <= 512;
 }
 
 int launch_rollout(const RolloutArgs& a, hipStream_t s) {
   if (rollout_supported(a.K) != 0) return -1;
-  if (const int rv = rollout_v_rows(a)) {
-    if (a.K.OP == 16) return rv == 2 ? launch_rollout_v_t<1, 2>(a, s) : launch_rollout_v_t<1, 4>(a, s);
-    return rv == 2 ? launch_rollout_v_t<2, 2>(a, s) : launch_rollout_v_t<2, 4>(a, s);
-  }
+  if (use_rollout_v(a)) return a.K.OP == 16 ? launch_rollout_v_t<1>(a, s) : launch_rollout_v_t<2>(a, s);
   if (a.K.kind == PPO_NET_TANH_NORMAL) {
     const int nht = (a.K.A + 15) / 16;
     switch (a.K.OP / 16) {

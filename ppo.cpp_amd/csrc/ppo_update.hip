@@ -1129,6 +1129,851 @@ __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
   }
 }
 
+// =============================================================================================
+// k_upd32: k_upd on v_mfma_f32_32x32x2_f32 (create option upd_mfma=32; LayerNorm-Beta agent, H = 256).
+//
+// Same contract, LDS carve, gather, loss and accumulators as k_upd; the three 256-wide GEMMs of a
+// tile (layer 2, dh1 = W2^T dz2, layer 1 twice) and the actor's head backward run as 32 x 32 x 2
+// MFMAs on a 32-row tile per wave, so every activation is 2 feature tiles x 16 registers per lane:
+// lane (j = row, h = lane >> 5), register r of tile ft = feature fbase + 32 ft + 8 (r >> 2) + 4 h + (r & 3).
+// Why: a 32x32x2 f32 MFMA issues for 64 cycles, and a partner wave on the same SIMD co-issues 6.2
+// VALU instructions beside it against 2.2 beside a 16x16x4 (32 cycles) — 1.4x the VALU per FLOP
+// (profiles/r02/probe/mfma_valu_coissue.jsonl), and k_upd's latency-bound phases (LayerNorm
+// backward, loss, column sums) run beside the partner trunk's GEMMs. Row statistics are in-lane
+// sums over 32 features plus one v_permlane32_swap; column sums a 32-lane reduce-scatter (one
+// v_permlane16_swap stage ahead of k_upd's four DPP stages). The A operands come from the same
+// swizzled copies (16-byte pieces of the 16 x 16 blocks, four 256-byte runs per wave-load); the B
+// operand of a k-block is one ds_read_b128 of the lane's row (conflict-free at row stride 4 mod 64).
+// The forward heads and the head-weight gradient stay 16x16x4 MFMAs reading h2 from LDS (padding the
+// 12 heads to 32 would double them). Summation orders differ from k_upd (not bitwise equal to it);
+// the parity tests compare both with the oracle.
+// =============================================================================================
+namespace {
+typedef float f16v __attribute__((ext_vector_type(16)));
+PPO_DEV f16v mfma32(float a, float b, f16v c) { return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0); }
+PPO_DEV f4 quad(const f16v& v, int q) { return f4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]}; }
+PPO_DEV void set_quad(f16v& v, int q, f4 x) {
+  v[4 * q] = x.x;
+  v[4 * q + 1] = x.y;
+  v[4 * q + 2] = x.z;
+  v[4 * q + 3] = x.w;
+}
+
+// out[ft] (+)= sum_k W[fbase + 32 ft + i][k] IN[j][k] over NKB 8-wide k-blocks (the last one: KLAST
+// k-steps). alane: this lane's float offset of the wave's first A piece in the swizzled copy (the
+// matrix base, the wave's 32-row block, (i >> 4) NC/16 blocks, lane group h, row i & 15);
+// in = IN + j LDI + 4 h. Step c of k-block kb covers columns 8 kb + c (h = 0) and 8 kb + 4 + c.
+template <int NKB, int KLAST, int NC>
+PPO_DEV void mm32(f16v (&out)[2], PBuf wb, int alane, const float* in) {
+  constexpr int FS = 32 * NC;  // floats between the wave's two 32-row feature tiles
+  constexpr int PD = 2;        // A pieces requested two k-blocks (2 x 512 MFMA cycles) ahead
+  auto ko = [](int kb) { return (kb >> 1) * 256 + (kb & 1) * 128; };
+  f4 w[PD + 1][2];
+#pragma unroll
+  for (int p = 0; p < PD && p < NKB; ++p)
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft) w[p][ft] = pld4(wb, alane, FS * ft + ko(p));
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    if (kb + PD < NKB) {
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft) w[(kb + PD) % (PD + 1)][ft] = pld4(wb, alane, FS * ft + ko(kb + PD));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const f4 b = lds_f4(in + 8 * kb);
+    const int nc = kb + 1 < NKB ? 4 : KLAST;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c >= nc) break;
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft) out[ft] = mfma32(w[kb % (PD + 1)][ft][c], b[c], out[ft]);
+    }
+  }
+}
+
+// out = the bias vector in the 32x32 layout (boff_lane = bias + fbase + 4 h)
+PPO_DEV void init_bias32(f16v (&out)[2], PBuf pb, int boff_lane) {
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) set_quad(out[ft], q, pld4(pb, boff_lane, 32 * ft + 8 * q));
+}
+
+PPO_DEV float lane_sum32(const f16v (&v)[2]) {
+  float t = 0.f;
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t += (v[ft][4 * q] + v[ft][4 * q + 1]) + (v[ft][4 * q + 2] + v[ft][4 * q + 3]);
+  return t;
+}
+
+// row j's total over the 256 features from the lane partials: + the other lane half, then the four
+// waves through LDS (red: [4][32]); contains a barrier
+PPO_DEV float rows32(float s, float* red, int wave, int j, int h) {
+  s = xor32_sum(s);
+  if (h == 0) red[wave * 32 + j] = s;
+  lds_barrier();
+  float t = 0.f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) t += red[w * 32 + j];
+  return t;
+}
+PPO_DEV void rows32x2(float& s, float& q, float* red0, float* red1, int wave, int j, int h) {
+  s = xor32_sum(s);
+  q = xor32_sum(q);
+  if (h == 0) {
+    red0[wave * 32 + j] = s;
+    red1[wave * 32 + j] = q;
+  }
+  lds_barrier();
+  float t = 0.f, u = 0.f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    t += red0[w * 32 + j];
+    u += red1[w * 32 + j];
+  }
+  s = t;
+  q = u;
+}
+
+// LayerNorm statistics of row j (two-pass, eps 1e-5, biased variance as torch::layer_norm)
+PPO_DEV void ln32(const f16v (&z)[2], float& mu, float& rs, float* red0, float* red1, int wave, int j, int h) {
+  mu = rows32(lane_sum32(z), red0, wave, j, h) * (1.0f / 256);
+  float t = 0.f;
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float d = z[ft][r] - mu;
+      t = __fmaf_rn(d, d, t);
+    }
+  rs = 1.0f / sqrtf(__fmaf_rn(rows32(t, red1, wave, j, h), 1.0f / 256, 1e-5f));
+}
+
+// column sums over the tile's 32 rows of v(ft, r), added to acc[feature]: the j / j + 16 halves by
+// v_permlane16_swap (rows 0 | 2 keep tile 0, rows 1 | 3 tile 1), then k_upd's 16-lane
+// reduce-scatter; lane j ends with register j & 15 of tile j >> 4 summed over all rows
+template <typename Fn>
+PPO_DEV void col_sums32(Fn v, float* acc, int fbase, int j, int h) {
+  float x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const auto p = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v(0, i)),
+                                                    __builtin_bit_cast(unsigned, v(1, i)), false, false);
+    x[i] = __builtin_bit_cast(float, (unsigned)p[0]) + __builtin_bit_cast(float, (unsigned)p[1]);
+  }
+  const int jj = j & 15;
+  rs_stage_banked(x);
+  rs_stage<kDppQuadMirror, 4, 2>(x, jj);
+  rs_stage<kDppQuadXor1, 2, 1>(x, jj);
+  acc[fbase + 32 * (j >> 4) + 8 * (jj >> 2) + 4 * h + (jj & 3)] += x[0];
+}
+
+PPO_DEV void store_rows32(float* __restrict__ dst, int ld, const f16v (&v)[2], int m, int M, int fh) {
+  if (m < M) {
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) st4(dst + (size_t)m * ld + fh + 32 * ft + 8 * q, quad(v[ft], q));
+  }
+}
+template <int LDA>
+PPO_DEV void lds_store32(float* act, const f16v (&v)[2], int j, int fh) {
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) lds_st4(act + j * LDA + fh + 32 * ft + 8 * q, quad(v[ft], q));
+}
+PPO_DEV void zero32(f16v (&v)[2]) {
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[ft][r] = 0.f;
+}
+}  // namespace
+
+template <int NTO, int NHT, int KL1>
+__global__ __launch_bounds__(256, 2) void k_upd32(UpdArgs a) {
+  constexpr int H = 256;
+  using GE = Geo<H, NTO, NHT>;
+  constexpr int R = GE::R, OP = GE::OP, NHP = GE::NHP, ITS = GE::ITS;
+  constexpr int LDX = GE::LDX, LDA = GE::LDA, LDG = GE::LDG;
+  static_assert(R == 32 && GE::WF == 4, "k_upd32: 32-row tiles, 4 feature waves");
+  // layer 1's 8-wide k-blocks: with K = 16 (NTO - 1) + 1 (KL1 == 1) only column 16 (NTO - 1) of the
+  // last 16-wide block is real, i.e. step 0 of its first 8-wide block
+  constexpr int NKB1 = KL1 == 1 ? 2 * (NTO - 1) + 1 : 2 * NTO, KLAST1 = KL1 == 1 ? 1 : 4;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* XN = lds + GE::oXN;
+  float* ACT = lds + GE::oACT;
+  float* RED = lds + GE::oRED;
+  float* PRE = lds + GE::oPRE;
+  float* GG = lds + GE::oG;
+  float* ROWS = lds + GE::oROW;
+  float* SCR = lds + GE::oSCR;
+  float* ACTN = lds + a.actn_off;
+  float* ACC = lds + a.acc_off;
+  float* SPAR = lds + a.spar_off;  // gamma1 | beta1 | gamma2 | beta2 | head biases | obs mean | std
+  float* SG1 = SPAR;
+  float* SBE1 = SPAR + H;
+  float* SG2 = SPAR + 2 * H;
+  float* SBE2 = SPAR + 3 * H;
+  float* SHB = SPAR + 4 * H;
+  float* SOM = SHB + NHP;
+  float* SOS = SOM + OP;
+  float* RED0 = RED;
+  float* RED1 = RED + 4 * R;
+  float* RED2 = RED + 8 * R;
+  float* RED3 = RED + 12 * R;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;    // 32x32 layout: row, lane half
+  const int j16 = lane & 15, g = lane >> 4;  // 16x16 layout (forward heads, head-weight gradient)
+  const int fbase = 64 * wave, fh = fbase + 4 * h;
+  const int trunk = (a.sched & 1) ? 1 - (int)blockIdx.y : (int)blockIdx.y;
+  if (!((a.trunk_mask >> trunk) & 1)) return;
+  if ((a.sched & 2) && trunk == 1) __builtin_amdgcn_s_setprio(1);
+  const PackedLayout& K = a.K;
+  const TrunkDev& T = K.tr[trunk];
+  const float* __restrict__ P = a.P;
+  const PBuf pb = make_pbuf(P, K.size);
+  const PBuf wsw = make_pbuf(a.WSW[trunk], (int)sw_size(H, OP));
+  const SmallGradLayout sg = a.sg[trunk];
+  const int O = K.O, A = K.A, nh = sg.nh;
+  const float c = a.clip_coef;
+  const float adv_mean = a.adv_stats[0], adv_std = a.adv_stats[1];
+  const bool hwg = a.hw_global && trunk == 1;
+  SmallGradLayout sl = sg;
+  if (hwg) {
+    const int d = sg.nh * H;
+    sl.hb -= d; sl.ls -= d; sl.stats -= d; sl.size -= d;
+  }
+  float* slab_row = a.slab[trunk] + (size_t)blockIdx.x * sg.size;
+  float* acc = ACC;
+  float* hwacc = hwg ? slab_row + sg.hW : acc + sg.hW;
+  for (int i = tid; i < sl.size; i += 256) ACC[i] = 0.f;
+  for (int i = tid; i < R * LDG; i += 256) GG[i] = 0.f;
+  if (hwg) {  // each owning lane zeroes the slab entries it accumulates (head-weight gradient, 16x16)
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+      for (int ft = 0; ft < 4; ++ft)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int hh = 16 * ht + 4 * g + r;
+          if (hh < nh) hwacc[hh * H + fbase + 16 * ft + j16] = 0.f;
+        }
+  }
+  for (int i = tid; i < GE::NSPAR; i += 256) {
+    const int v = i / H, f = i - v * H;
+    float x = 0.f;
+    if (v < 4) {
+      x = P[(v == 0 ? T.g1 : v == 1 ? T.be1 : v == 2 ? T.g2 : T.be2) + f];
+    } else if (i < 4 * H + NHP) {
+      if (i - 4 * H < nh) x = P[head_bias(K, trunk, i - 4 * H)];
+    } else {
+      const int q = i - 4 * H - NHP, o = q % OP;
+      x = q < OP ? 0.f : 1.f;
+      if (o < O) x = P[(q < OP ? K.omean : K.ostd) + o];
+    }
+    SPAR[i] = x;
+  }
+
+  // A-operand lane offsets into the swizzled W1 | W2 | W2^T (mm32)
+  const int w1lane = (fbase / 32) * 32 * OP + ((j >> 4) * (OP / 16) * 64 + h * 16 + (j & 15)) * 4;
+  const int w2lane = H * OP + (fbase / 32) * 32 * H + ((j >> 4) * 16 * 64 + h * 16 + (j & 15)) * 4;
+  const int w2tlane = w2lane + H * H;
+  const float* xn_in = XN + j * LDX + 4 * h;
+  const float* act_in = ACT + j * LDA + 4 * h;
+  // forward head rows (16x16: A = W3[16 ht + j16][..]); head-backward rows (32x32: heads
+  // 16 ht + 8 q2 + 4 h + c of feature fbase + 32 ft + j)
+  int hrow_f[NHT], hrow_b[NHT][2][4];
+#pragma unroll
+  for (int ht = 0; ht < NHT; ++ht) {
+    hrow_f[ht] = head_row(K, trunk, 16 * ht + j16, H);
+#pragma unroll
+    for (int q2 = 0; q2 < 2; ++q2)
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) hrow_b[ht][q2][cc] = head_row(K, trunk, 16 * ht + 8 * q2 + 4 * h + cc, H);
+  }
+  const int ntiles = (a.M + R - 1) / R;
+
+  // ---- gather (as k_upd) ----
+  constexpr bool PREF = (R * OP + 255) / 256 <= 4;
+  constexpr int NG = PREF ? (R * OP + 255) / 256 : 1;
+  constexpr int NAI = PREF ? (R * PPO_UPD_MAXA + 255) / 256 : 1;
+  int pg[NG], pra, pac[NAI];
+  float vg[NG], vr1 = 0.f, vr2 = 0.f, vac[NAI];
+  auto pref_idx = [&](int itn) {
+    const int mb = itn * R;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int idx = tid + 256 * k, row = idx / OP, f = idx - row * OP, m = mb + row;
+      pg[k] = (itn < ntiles && idx < R * OP && m < a.M && f < O) ? a.perm[m] : -1;
+    }
+    pra = (itn < ntiles && tid < R && mb + tid < a.M) ? a.perm[mb + tid] : -1;
+#pragma unroll
+    for (int k = 0; k < NAI; ++k) {
+      const int idx = tid + 256 * k, row = idx / (A > 0 ? A : 1), m = mb + row;
+      pac[k] = (trunk == 1 && itn < ntiles && idx < R * A && m < a.M) ? a.perm[m] : -1;
+    }
+  };
+  auto pref_data = [&]() {
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int idx = tid + 256 * k, f = idx - (idx / OP) * OP;
+      vg[k] = pg[k] >= 0 ? a.obs[(long)pg[k] * O + f] : 0.f;
+    }
+    if (pra >= 0) {
+      if (trunk == 0) { vr1 = a.ret[pra]; vr2 = a.val[pra]; }
+      else { vr1 = a.logp[pra]; vr2 = a.adv[pra]; }
+    } else {
+      vr1 = 0.f; vr2 = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NAI; ++k) {
+      const int idx = tid + 256 * k, ai = idx - (idx / (A > 0 ? A : 1)) * A;
+      vac[k] = pac[k] >= 0 ? a.actions[(long)pac[k] * A + ai] : 0.f;
+    }
+  };
+  auto commit = [&](int itc) {
+    const int mb = itc * R;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int idx = tid + 256 * k, row = idx / OP, f = idx - row * OP, m = mb + row;
+      if (idx < R * OP) {
+        float v = vg[k];
+        if (pg[k] >= 0) v = (v - SOM[f]) / SOS[f];
+        XN[row * LDX + f] = v;
+        if (trunk == 0 && m < a.M) a.Xn[(size_t)m * OP + f] = v;
+      }
+    }
+    if (tid < R) {
+      ROWS[tid * 8 + 1] = vr1;
+      ROWS[tid * 8 + 2] = vr2;
+    }
+#pragma unroll
+    for (int k = 0; k < NAI; ++k) {
+      const int idx = tid + 256 * k;
+      if (trunk == 1 && idx < R * A) ACTN[idx] = vac[k];
+    }
+  };
+  auto perm_of = [&](int r) { return __float_as_int(ROWS[r * 8]); };
+  auto gather_sync = [&](int itc) {
+    const int mb = itc * R;
+    constexpr int NGS = (R * OP + 255) / 256, GC = 4;
+#pragma unroll 1
+    for (int k0 = 0; k0 < NGS; k0 += GC) {
+      int rp[GC];
+      float v[GC];
+#pragma unroll
+      for (int cc = 0; cc < GC; ++cc) {
+        const int idx = tid + 256 * (k0 + cc), row = min(idx / OP, R - 1);
+        rp[cc] = perm_of(row);
+      }
+#pragma unroll
+      for (int cc = 0; cc < GC; ++cc) {
+        const int idx = tid + 256 * (k0 + cc), f = idx - (idx / OP) * OP;
+        v[cc] = a.obs[(long)rp[cc] * O + min(f, O - 1)];
+      }
+#pragma unroll
+      for (int cc = 0; cc < GC; ++cc) {
+        const int idx = tid + 256 * (k0 + cc), row = idx / OP, f = idx - row * OP, m = mb + row;
+        if (k0 + cc < NGS && idx < R * OP) {
+          const bool ok = m < a.M && f < O;
+          float x = ok ? v[cc] : 0.f;
+          if (ok) x = (x - SOM[f]) / SOS[f];
+          XN[row * LDX + f] = x;
+          if (trunk == 0 && m < a.M) a.Xn[(size_t)m * OP + f] = x;
+        }
+      }
+    }
+    {
+      const int rrow = perm_of(min(tid, R - 1));
+      const float r1 = trunk == 0 ? a.ret[rrow] : a.logp[rrow];
+      const float r2 = trunk == 0 ? a.val[rrow] : a.adv[rrow];
+      if (tid < R) {
+        const bool ok = mb + tid < a.M;
+        ROWS[tid * 8 + 1] = ok ? r1 : 0.f;
+        ROWS[tid * 8 + 2] = ok ? r2 : 0.f;
+      }
+    }
+    if (trunk == 1) {
+      constexpr int NAS = (R * PPO_UPD_MAXA + 255) / 256;
+      int ap[NAS];
+#pragma unroll
+      for (int k = 0; k < NAS; ++k) {
+        const int idx = tid + 256 * k, row = min(idx / (A > 0 ? A : 1), R - 1);
+        ap[k] = perm_of(row);
+      }
+      float av[NAS];
+#pragma unroll
+      for (int k = 0; k < NAS; ++k) {
+        const int idx = tid + 256 * k, ai = idx - (idx / (A > 0 ? A : 1)) * A;
+        av[k] = a.actions[(long)ap[k] * A + ai];
+      }
+#pragma unroll
+      for (int k = 0; k < NAS; ++k) {
+        const int idx = tid + 256 * k, m = mb + idx / (A > 0 ? A : 1);
+        if (idx < R * A) ACTN[idx] = m < a.M ? av[k] : 0.f;
+      }
+    }
+  };
+  if constexpr (PREF) {
+    pref_idx(blockIdx.x);
+    pref_data();
+  }
+  int nperm = 0;
+  if constexpr (!PREF) nperm = tid < R ? a.perm[min((int)blockIdx.x * R + tid, a.M - 1)] : 0;
+
+  float lst[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
+    const int m0 = it * R, m = m0 + j;
+    PPO_STAMP_START();
+    if constexpr (!PREF)
+      if (tid < R) ROWS[tid * 8] = __int_as_float(nperm);
+    lds_barrier();
+    if constexpr (PREF) {
+      commit(it);
+      pref_idx(it + gridDim.x);
+    } else {
+      if (tid < R) nperm = a.perm[min((it + (int)gridDim.x) * R + tid, a.M - 1)];
+      gather_sync(it);
+    }
+    // the actor's head-backward A operands (one head tile), requested a forward pass ahead
+    f4 hwb[2][2];
+    if constexpr (NHT == 1) {
+      if (trunk == 1) {
+#pragma unroll
+        for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+          for (int q2 = 0; q2 < 2; ++q2)
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc)
+              hwb[ft][q2][cc] = hrow_b[0][q2][cc] >= 0 ? bld1(pb, hrow_b[0][q2][cc] + fbase + j, 32 * ft) : 0.0f;
+      }
+    }
+    lds_barrier();
+    PPO_STAMP(0);
+
+    // ---------------- layer 1 ----------------
+    f16v z[2];
+    init_bias32(z, pb, T.b1 + fh);
+    mm32<NKB1, KLAST1, OP>(z, wsw, w1lane, xn_in);
+    PPO_STAMP(1);
+    float mu1, rs1;
+    ln32(z, mu1, rs1, RED0, RED1, wave, j, h);
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f4 gm = lds_f4(SG1 + fh + 32 * ft + 8 * q), bt = lds_f4(SBE1 + fh + 32 * ft + 8 * q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float xh = (z[ft][4 * q + r] - mu1) * rs1;
+          const float y = __fmaf_rn(gm[r], xh, bt[r]);
+          z[ft][4 * q + r] = y > 0.0f ? y : 0.0f;
+        }
+      }
+    store_rows32(a.H1[trunk], H, z, m, a.M, fh);
+    lds_store32<LDA>(ACT, z, j, fh);
+    lds_barrier();
+    PPO_STAMP(2);
+
+    // ---------------- layer 2 ----------------
+    f16v x2[2];  // x_hat2
+    init_bias32(x2, pb, T.b2 + fh);
+    mm32<32, 4, H>(x2, wsw, w2lane, act_in);
+    PPO_STAMP(3);
+    if constexpr (PREF) pref_data();
+    float mu2, rs2;
+    ln32(x2, mu2, rs2, RED2, RED3, wave, j, h);
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft) x2[ft] = (x2[ft] - mu2) * rs2;
+    auto h2_of = [&](int ft, int q) -> f4 {
+      const f4 gm = lds_f4(SG2 + fh + 32 * ft + 8 * q), bt = lds_f4(SBE2 + fh + 32 * ft + 8 * q);
+      f4 y;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = __fmaf_rn(gm[r], x2[ft][4 * q + r], bt[r]);
+        y[r] = v > 0.0f ? v : 0.0f;
+      }
+      return y;
+    };
+    PPO_STAMP(4);
+    // ---------------- heads ----------------
+    lds_barrier();  // every wave is done reading h1 from ACT
+    if (trunk == 0) {
+      // critic: one real head — per-row dot product over the lane's 32 features, + the other half
+      float pv = 0.f;
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 w = pld4(pb, K.cW3 + fh, 32 * ft + 8 * q);
+          const f4 h2 = h2_of(ft, q);
+          lds_st4(ACT + j * LDA + fh + 32 * ft + 8 * q, h2);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pv = __fmaf_rn(w[r], h2[r], pv);
+        }
+      pv = xor32_sum(pv);
+      if (h == 0) SCR[(wave * NHP) * R + j] = pv;
+    } else {
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lds_st4(ACT + j * LDA + fh + 32 * ft + 8 * q, h2_of(ft, q));
+      // 16x16x4 heads over this wave's 64 features, h2 read back from ACT (the wave's own columns:
+      // LDS keeps one wave's accesses in order)
+      f4 hp[NHT][2];
+#pragma unroll
+      for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) hp[ht][rt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ft = 0; ft < 4; ++ft) {
+        f4 wv[NHT];
+#pragma unroll
+        for (int ht = 0; ht < NHT; ++ht)
+          wv[ht] = hrow_f[ht] >= 0 ? pld4(pb, hrow_f[ht] + fbase + 4 * g, 16 * ft) : f4{0.f, 0.f, 0.f, 0.f};
+        f4 h2v[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) h2v[rt] = lds_f4(ACT + (16 * rt + j16) * LDA + fbase + 16 * ft + 4 * g);
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int ht = 0; ht < NHT; ++ht) hp[ht][rt] = mfma16(wv[ht][cc], h2v[rt][cc], hp[ht][rt]);
+      }
+#pragma unroll
+      for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) SCR[(wave * NHP + 16 * ht + 4 * g + r) * R + 16 * rt + j16] = hp[ht][rt][r];
+    }
+    lds_barrier();
+    PPO_STAMP(5);
+    for (int idx = tid; idx < R * nh; idx += 256) {
+      const int row = idx / nh, hh = idx - row * nh;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) s += SCR[(w * NHP + hh) * R + row];
+      PRE[row * LDG + hh] = s + SHB[hh];
+    }
+    lds_barrier();
+    PPO_STAMP(6);
+
+    // ---------------- loss and its gradient wrt the head pre-activations (k_upd's) ----------------
+    float* ITM = SCR;
+    float st_a = 0.f, st_b = 0.f, st_c = 0.f, st_d = 0.f, st_e = 0.f, st_f = 0.f;
+    if (trunk == 0) {
+      if (tid < R) {
+        const bool valid = m0 + tid < a.M;
+        const float v = PRE[tid * LDG];
+        const float rt_ = ROWS[tid * 8 + 1], ov = ROWS[tid * 8 + 2];
+        float gv, sv;
+        if (a.clip_vloss) {
+          const float vu = (v - rt_) * (v - rt_);
+          const float dv = v - ov;
+          const float vcl = ov + fminf(fmaxf(dv, -c), c);
+          const float vc = (vcl - rt_) * (vcl - rt_);
+          sv = fmaxf(vu, vc);
+          const float w1 = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
+          const float inr = (dv >= -c && dv <= c) ? 1.0f : 0.0f;
+          gv = 0.5f * a.vf_coef * a.inv_m * (w1 * 2.0f * (v - rt_) + (1.0f - w1) * 2.0f * (vcl - rt_) * inr);
+        } else {
+          sv = (v - rt_) * (v - rt_);
+          gv = 0.5f * a.vf_coef * a.inv_m * 2.0f * (v - rt_);
+        }
+        if (!valid) { gv = 0.f; sv = 0.f; }
+        GG[tid * LDG] = gv;
+        st_b = sv;
+      }
+    } else if (A <= 8) {
+      const int row = tid >> 3, ai = tid & 7;
+      const bool item = ai < A;
+      const bool valid = m0 + row < a.M;
+      const int ac = item ? ai : 0;
+      const float hi = P[K.hi], lo = P[K.lo];
+      const float pa = PRE[row * LDG + ac], pbv = PRE[row * LDG + A + ac];
+      const float al = softplusf_(pa) + 1.0f, be = softplusf_(pbv) + 1.0f;
+      const float av = valid ? ACTN[row * A + ac] : 0.5f * (hi + lo);
+      float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+      s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
+      const float ab = al + be;
+      float lga, lgb, lgab, psa, psb, psab, ta, tb, tab;
+      lgamma_digamma_trigamma(al, lga, psa, ta);
+      lgamma_digamma_trigamma(be, lgb, psb, tb);
+      lgamma_digamma_trigamma(ab, lgab, psab, tab);
+      const float lpi = xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
+      const float eni = (lga + lgb) - lgab - (2.0f - ab) * psab - ((al - 1.0f) * psa + (be - 1.0f) * psb);
+      const float lp = group8_sum(item ? lpi : 0.0f), ent = group8_sum(item ? eni : 0.0f);
+      const float oldlp = valid ? ROWS[row * 8 + 1] : lp;
+      const float logratio = lp - oldlp;
+      const float ratio = expf(logratio);
+      float an = valid ? ROWS[row * 8 + 2] : 0.f;
+      if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
+      const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
+      const float pg1 = -an * ratio, pg2 = -an * rc;
+      const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+      const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
+      float g_logp = a.inv_m * (w1 * (-an) + (1.0f - w1) * (-an) * inr) * ratio;
+      float g_ent = -a.ent_coef * a.inv_m;
+      if (!valid) { g_logp = 0.f; g_ent = 0.f; }
+      if (ai == 0 && valid) {
+        st_a = fmaxf(pg1, pg2);
+        st_c = ent;
+        st_d = -logratio;
+        st_e = (ratio - 1.0f) - logratio;
+        st_f = fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
+      }
+      if (item) {
+        const float dla = ((al - 1.0f) != 0.0f ? logf(s) : 0.0f) + psab - psa;
+        const float dea = (ab - 2.0f) * tab - (al - 1.0f) * ta;
+        const float dlb = ((be - 1.0f) != 0.0f ? logf(1.0f - s) : 0.0f) + psab - psb;
+        const float deb = (ab - 2.0f) * tab - (be - 1.0f) * tb;
+        GG[row * LDG + ai] = (g_logp * dla + g_ent * dea) * softplus_d(pa);
+        GG[row * LDG + A + ai] = (g_logp * dlb + g_ent * deb) * softplus_d(pbv);
+      }
+    } else {
+      for (int idx = tid; idx < R * A; idx += 256) {
+        const int row = idx / A, ai = idx - row * A;
+        const bool valid = m0 + row < a.M;
+        float* it_ = ITM + idx * ITS;
+        const float hi = P[K.hi], lo = P[K.lo];
+        const float pa = PRE[row * LDG + ai], pbv = PRE[row * LDG + A + ai];
+        const float al = softplusf_(pa) + 1.0f, be = softplusf_(pbv) + 1.0f;
+        const float av = valid ? ACTN[idx] : 0.5f * (hi + lo);
+        float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+        s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
+        const float ab = al + be;
+        float lga, lgb, lgab, psa, psb, psab, ta, tb, tab;
+        lgamma_digamma_trigamma(al, lga, psa, ta);
+        lgamma_digamma_trigamma(be, lgb, psb, tb);
+        lgamma_digamma_trigamma(ab, lgab, psab, tab);
+        it_[0] = xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
+        it_[1] = (lga + lgb) - lgab - (2.0f - ab) * psab - ((al - 1.0f) * psa + (be - 1.0f) * psb);
+        it_[2] = ((al - 1.0f) != 0.0f ? logf(s) : 0.0f) + psab - psa;
+        it_[3] = (ab - 2.0f) * tab - (al - 1.0f) * ta;
+        it_[4] = softplus_d(pa);
+        it_[5] = ((be - 1.0f) != 0.0f ? logf(1.0f - s) : 0.0f) + psab - psb;
+        it_[6] = (ab - 2.0f) * tab - (be - 1.0f) * tb;
+        it_[7] = softplus_d(pbv);
+      }
+      lds_barrier();
+      if (tid < R) {
+        const bool valid = m0 + tid < a.M;
+        float lp = 0.f, ent = 0.f;
+        for (int ai = 0; ai < A; ++ai) {
+          lp += ITM[(tid * A + ai) * ITS + 0];
+          ent += ITM[(tid * A + ai) * ITS + 1];
+        }
+        const float oldlp = valid ? ROWS[tid * 8 + 1] : lp;
+        const float logratio = lp - oldlp;
+        const float ratio = expf(logratio);
+        float an = valid ? ROWS[tid * 8 + 2] : 0.f;
+        if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
+        const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
+        const float pg1 = -an * ratio, pg2 = -an * rc;
+        const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+        const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
+        float g_logp = a.inv_m * (w1 * (-an) + (1.0f - w1) * (-an) * inr) * ratio;
+        float g_ent = -a.ent_coef * a.inv_m;
+        st_a = fmaxf(pg1, pg2);
+        st_c = ent;
+        st_d = -logratio;
+        st_e = (ratio - 1.0f) - logratio;
+        st_f = fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
+        if (!valid) { g_logp = 0.f; g_ent = 0.f; st_a = st_c = st_d = st_e = st_f = 0.f; }
+        ROWS[tid * 8 + 3] = g_logp;
+        ROWS[tid * 8 + 4] = g_ent;
+      }
+      lds_barrier();
+      for (int idx = tid; idx < R * A; idx += 256) {
+        const int row = idx / A, ai = idx - row * A;
+        const float g_logp = ROWS[row * 8 + 3], g_ent = ROWS[row * 8 + 4];
+        float* it_ = ITM + idx * ITS;
+        GG[row * LDG + ai] = (g_logp * it_[2] + g_ent * it_[3]) * it_[4];
+        GG[row * LDG + A + ai] = (g_logp * it_[5] + g_ent * it_[6]) * it_[7];
+      }
+    }
+    lst[0] += st_a; lst[1] += st_b; lst[2] += st_c; lst[3] += st_d; lst[4] += st_e; lst[5] += st_f;
+    lds_barrier();
+    PPO_STAMP(7);
+    if (tid < nh) {
+      float s = 0.f;
+      for (int row = 0; row < R; ++row) s += GG[row * LDG + tid];
+      ACC[sl.hb + tid] += s;
+    }
+
+    // ---------------- head backward: dh2 = W3^T G^T, dW3 += G^T h2 ----------------
+    f16v dh[2];
+    zero32(dh);
+    if (trunk == 0) {
+      const float gr = lds_f(GG + j * LDG);
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 w = pld4(pb, K.cW3 + fh, 32 * ft + 8 * q);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dh[ft][4 * q + r] = w[r] * gr;
+        }
+      f16v hv[2];  // h2 back from ACT (stored by this lane above)
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) set_quad(hv[ft], q, lds_f4(ACT + j * LDA + fh + 32 * ft + 8 * q));
+      col_sums32([&](int ft, int r) { return gr * hv[ft][r]; }, acc + sg.hW, fbase, j, h);
+    } else {
+#pragma unroll
+      for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+        for (int q2 = 0; q2 < 2; ++q2) {
+          const f4 gq = lds_f4(GG + j * LDG + 16 * ht + 8 * q2 + 4 * h);
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+            for (int ft = 0; ft < 2; ++ft) {
+              float wv;
+              if constexpr (NHT == 1) wv = hwb[ft][q2][cc];
+              else wv = hrow_b[ht][q2][cc] >= 0 ? bld1(pb, hrow_b[ht][q2][cc] + fbase + j, 32 * ft) : 0.0f;
+              dh[ft] = mfma32(wv, gq[cc], dh[ft]);
+            }
+        }
+      // dW3 tiles (heads 16 ht .., features fbase + 16 ft ..), 16x16x4 over the 32 rows from LDS
+#pragma unroll
+      for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+        for (int ft = 0; ft < 4; ++ft) {
+          f4 d3 = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 16 * rt + 4 * g + r;
+              d3 = mfma16(lds_f(GG + row * LDG + 16 * ht + j16), lds_f(ACT + row * LDA + fbase + 16 * ft + j16), d3);
+            }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int hh = 16 * ht + 4 * g + r;
+            if (hh < nh) hwacc[hh * H + fbase + 16 * ft + j16] += d3[r];
+          }
+        }
+    }
+    PPO_STAMP(8);
+
+    // ---------------- layer-2 backward: dz2 ----------------
+    {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 gm = lds_f4(SG2 + fh + 32 * ft + 8 * q), bt = lds_f4(SBE2 + fh + 32 * ft + 8 * q);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k = 4 * q + r;
+            const float y = __fmaf_rn(gm[r], x2[ft][k], bt[r]);
+            const float dy = y > 0.0f ? dh[ft][k] : 0.0f;
+            dh[ft][k] = dy;
+            const float dx = dy * gm[r];
+            s1 += dx;
+            s2 += dx * x2[ft][k];
+          }
+        }
+      rows32x2(s1, s2, RED0, RED1, wave, j, h);
+      s1 *= (1.0f / H);
+      s2 *= (1.0f / H);
+      col_sums32([&](int ft, int r) { return dh[ft][r]; }, acc + sg.be2, fbase, j, h);
+      col_sums32([&](int ft, int r) { return dh[ft][r] * x2[ft][r]; }, acc + sg.g2, fbase, j, h);
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 gm = lds_f4(SG2 + fh + 32 * ft + 8 * q);
+          set_quad(x2[ft], q, rs2 * (quad(dh[ft], q) * gm - s1 - quad(x2[ft], q) * s2));
+        }
+    }
+    // x2 = dz2
+    col_sums32([&](int ft, int r) { return x2[ft][r]; }, acc + sg.b2, fbase, j, h);
+    store_rows32(a.DZ2[trunk], H, x2, m, a.M, fh);
+    lds_barrier();  // dW3 readers of h2 are done
+    lds_store32<LDA>(ACT, x2, j, fh);
+    lds_barrier();
+    PPO_STAMP(9);
+
+    // ---------------- dh1 = W2^T dz2 ----------------
+    zero32(dh);
+    mm32<32, 4, H>(dh, wsw, w2tlane, act_in);
+    PPO_STAMP(10);
+    // ---------------- recompute layer 1, layer-1 backward ----------------
+    init_bias32(z, pb, T.b1 + fh);
+    mm32<NKB1, KLAST1, OP>(z, wsw, w1lane, xn_in);
+    PPO_STAMP(11);
+    {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 gm = lds_f4(SG1 + fh + 32 * ft + 8 * q), bt = lds_f4(SBE1 + fh + 32 * ft + 8 * q);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k = 4 * q + r;
+            const float xh = (z[ft][k] - mu1) * rs1;
+            z[ft][k] = xh;
+            const float y = __fmaf_rn(gm[r], xh, bt[r]);
+            const float dy = y > 0.0f ? dh[ft][k] : 0.0f;
+            dh[ft][k] = dy;
+            const float dx = dy * gm[r];
+            s1 += dx;
+            s2 += dx * xh;
+          }
+        }
+      rows32x2(s1, s2, RED2, RED3, wave, j, h);
+      s1 *= (1.0f / H);
+      s2 *= (1.0f / H);
+      col_sums32([&](int ft, int r) { return dh[ft][r]; }, acc + sg.be1, fbase, j, h);
+      col_sums32([&](int ft, int r) { return dh[ft][r] * z[ft][r]; }, acc + sg.g1, fbase, j, h);
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 gm = lds_f4(SG1 + fh + 32 * ft + 8 * q);
+          set_quad(z[ft], q, rs1 * (quad(dh[ft], q) * gm - s1 - quad(z[ft], q) * s2));
+        }
+    }
+    // z = dz1
+    col_sums32([&](int ft, int r) { return z[ft][r]; }, acc + sg.b1, fbase, j, h);
+    store_rows32(a.DZ1[trunk], H, z, m, a.M, fh);
+    PPO_STAMP(12);
+  }
+  // ---------------- workgroup result ----------------
+#pragma unroll
+  for (int mm = 32; mm >= 1; mm >>= 1)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) lst[k] += shfl_xor(lst[k], mm);
+  lds_barrier();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) RED[wave * 8 + k] = lst[k];
+  }
+  lds_barrier();
+  if (tid == 0) {
+    float t[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) t[k] = (RED[k] + RED[8 + k]) + (RED[16 + k] + RED[24 + k]);
+    float* st = ACC + sl.stats;
+    st[ST_PG] += t[0]; st[ST_V] += t[1]; st[ST_ENT] += t[2];
+    st[ST_OKL] += t[3]; st[ST_KL] += t[4]; st[ST_CF] += t[5];
+  }
+  lds_barrier();
+  for (int i = tid; i < sl.size; i += 256) slab_row[hwg && i >= sg.hW ? i + sg.nh * H : i] = ACC[i];
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side: geometry, LDS size, dispatch
 // ---------------------------------------------------------------------------------------------
@@ -1192,6 +2037,44 @@ int upd_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_siz
                    hipSuccess
                ? 0
                : -2;
+  });
+}
+
+// k_upd32: the LayerNorm-Beta agent at H = 256 (the instantiations k_upd has for it)
+template <typename F>
+static int dispatch_upd32(const PackedLayout& K, int nh, F&& f) {
+  const int nto = K.OP / 16, nht = (nh + 15) / 16;
+  const int kl = (K.O == 16 * (nto - 1) + 1) ? 1 : 4;
+  if (K.H != 256 || K.kind != PPO_NET_LN_BETA) return -1;
+#define PPO_UPD32_CASE(NTO_, NHT_, KL_)                                                              \
+  if (nto == NTO_ && nht == NHT_ && kl == KL_)                                                       \
+    return f(std::integral_constant<int, NTO_>{}, std::integral_constant<int, NHT_>{}, std::integral_constant<int, KL_>{});
+  PPO_UPD32_CASE(1, 1, 4) PPO_UPD32_CASE(2, 1, 4) PPO_UPD32_CASE(2, 1, 1) PPO_UPD32_CASE(7, 1, 4)
+  PPO_UPD32_CASE(24, 3, 4) PPO_UPD32_CASE(2, 3, 4) PPO_UPD32_CASE(2, 3, 1)
+#undef PPO_UPD32_CASE
+  return -1;
+}
+
+int upd32_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g) {
+  return dispatch_upd32(K, nh_actor, [&](auto NTO_, auto NHT_, auto KL_) {
+    upd_geo<256, decltype(NTO_)::value, decltype(NHT_)::value>(K, nh_actor, sg0_size, sg1_size, g);
+    const auto k = k_upd32<decltype(NTO_)::value, decltype(NHT_)::value, decltype(KL_)::value>;
+    return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) ==
+                   hipSuccess
+               ? 0
+               : -2;
+  });
+}
+
+int launch_upd32(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s) {
+  UpdArgs b = a;
+#ifndef PPO_DIAG
+  b.trunk_mask = 3;
+#endif
+  return dispatch_upd32(a.K, nh_actor, [&](auto NTO_, auto NHT_, auto KL_) {
+    hipLaunchKernelGGL((k_upd32<decltype(NTO_)::value, decltype(NHT_)::value, decltype(KL_)::value>), dim3(nblocks, 2),
+                       dim3(256), lds_bytes, s, b);
+    return 0;
   });
 }
 

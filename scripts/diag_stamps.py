@@ -26,7 +26,8 @@ if ANT:
     cfg = ppo_amd.ACPPOConfig(env_id="Ant-v5", num_envs=1024, num_steps=128, total_timesteps=1024 * 128 * 4)
 else:
     cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=4096, num_steps=128, total_timesteps=4096 * 128 * 4)
-tr = ppo_amd.Trainer(cfg, num_envs_per_device=cfg.num_envs)
+# PPO_OPTS: ppo_create_ex options (e.g. upd_mfma=32: the same phases of k_upd32)
+tr = ppo_amd.Trainer(cfg, num_envs_per_device=cfg.num_envs, options=os.environ.get("PPO_OPTS") or None)
 tr.iterate()
 tr.agent.sync()
 lib = ppo_amd.lib()

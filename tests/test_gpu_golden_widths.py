@@ -39,7 +39,7 @@ def agent_for(meta, E, T=1, MB=1, EP=1, **kw):
     hc = ppo_amd.HipConfig(meta["kind"], meta["O"], meta["A"], meta["H"], E, T, MB, EP, 0.99, 0.95,
                            kw.get("clip", 0.2), kw.get("ent", 0.01), kw.get("vf", 0.5), kw.get("mgn", 0.5),
                            kw.get("eps", 1e-5), 1, 1, 1, 0, 1)
-    return ppo_amd.Agent(hc)
+    return ppo_amd.Agent(hc, options=kw.get("options"))
 
 
 def golden_params(pre):
@@ -85,13 +85,16 @@ def test_act_vs_golden_at_reference_width(pre, kind):
     ag.close()
 
 
-@pytest.mark.parametrize("pre,kind", WIDTH_CASES)
-def test_update_vs_golden_at_reference_width(pre, kind):
+@pytest.mark.parametrize("pre,kind,opts", [c + (None,) for c in WIDTH_CASES] +
+                         [("ac256", 1, "upd_mfma=32"), ("ant256", 1, "upd_mfma=32")])
+def test_update_vs_golden_at_reference_width(pre, kind, opts):
+    """The update at the reference widths against the LibTorch golden; the AC agent also through
+    k_upd32 (create option upd_mfma=32)."""
     meta, p = golden_params(pre)
     mu, d = load_case(pre + "_update")
     M = mu["M"]
     ag = agent_for(meta, M, clip=mu["clip_coef"], ent=mu["ent_coef"], vf=mu["vf_coef"], mgn=mu["max_grad_norm"],
-                   eps=mu["adam_eps"])
+                   eps=mu["adam_eps"], options=opts)
     ag.load_params(p)
     O_, A = meta["O"], meta["A"]
     ag.buffer(ppo_amd.BUF_OBS, (1, M, O_)).upload(d["x"].reshape(1, M, O_))

@@ -34,14 +34,17 @@ from ppo_amd import DeviceArray  # noqa: E402
 from test_gpu_parity import fill_storage, make_agent, random_params, rel  # noqa: E402
 
 
-@pytest.mark.parametrize("name,kind,H,O_,A,E,T,clip,ent,lr", [
-    ("metric_halfcheetah", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4),
-    ("cfg4_shard_ant", 1, 256, 105, 8, 1024, 32, 0.1, 0.01, 2.5e-4),
+@pytest.mark.parametrize("name,kind,H,O_,A,E,T,clip,ent,lr,opts", [
+    ("metric_halfcheetah", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, None),
+    ("cfg4_shard_ant", 1, 256, 105, 8, 1024, 32, 0.1, 0.01, 2.5e-4, None),
+    # the same two through k_upd32 (32x32x2 MFMA layout, create option upd_mfma=32)
+    ("metric_halfcheetah_mfma32", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=32"),
+    ("cfg4_shard_ant_mfma32", 1, 256, 105, 8, 1024, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=32"),
     # cfg2: ppo_continuous_action Humanoid-v4, E=1024, T=2048, 32 minibatches -> M = 65 536 rows
     # (ppo:489-542; clip 0.2, ent_coef 0, lr 3e-4, ppo:60-67): k_upd2 walks 128 32-row tiles per
     # workgroup pair and k_dw2_dma sums 256 split-K chunks of 256 rows
-    ("cfg2_humanoid", 0, 64, 376, 17, 1024, 64, 0.2, 0.0, 3e-4)])
-def test_headline_minibatch_update_vs_oracle(name, kind, H, O_, A, E, T, clip, ent, lr):
+    ("cfg2_humanoid", 0, 64, 376, 17, 1024, 64, 0.2, 0.0, 3e-4, None)])
+def test_headline_minibatch_update_vs_oracle(name, kind, H, O_, A, E, T, clip, ent, lr, opts):
     M = E * T
     rng = np.random.default_rng(31)
     L = O.layout_init(kind, O_, A, H)
@@ -62,7 +65,8 @@ def test_headline_minibatch_update_vs_oracle(name, kind, H, O_, A, E, T, clip, e
     perm = rng.permutation(M).astype(np.int32)
     mgn, eps = 0.5, 1e-5
 
-    ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=clip, ent=ent, max_grad_norm=mgn, adam_eps=eps)
+    ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=clip, ent=ent, max_grad_norm=mgn, adam_eps=eps,
+                    options=opts)
     ag.load_params(p)
     fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
     st = ag.update(lr, perms=DeviceArray.from_numpy(perm), want_stats=True)
@@ -125,3 +129,44 @@ def test_cfg2_split_update_matches_single_kernel(split):
     for k in ("pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac", "grad_norm"):
         np.testing.assert_allclose(s1[k], s0[k], rtol=1e-5, atol=1e-7, err_msg=k)
     assert np.abs(p1 - p0).max() < 1e-5
+
+
+@pytest.mark.parametrize("O_,A,E", [(17, 6, 999), (105, 8, 777), (16, 8, 333)])
+def test_upd32_matches_upd(O_, A, E):
+    """k_upd32 (upd_mfma=32) against k_upd on the same minibatch, ragged last tile (E = M not a
+    multiple of 32; O = 17: the one-column last k-block, 105: the synchronous wide gather, 16: one
+    full k-block, A = 8: a full head tile): the same products summed in another order (32x32x2 chains and 32-lane reductions),
+    so gradients agree to fp32 accumulation noise (rel-L2 < 2e-5) and the loss statistics to 2e-5."""
+    kind, H, T = 1, 256, 1
+    M = E * T
+    rng = np.random.default_rng(11)
+    L = O.layout_init(kind, O_, A, H)
+    p = random_params(L, rng)
+    x = rng.standard_normal((M, O_)).astype(np.float32)
+    act = rng.uniform(-0.95, 0.95, (M, A)).astype(np.float32)
+    olp = rng.standard_normal(M).astype(np.float32)
+    adv = rng.standard_normal(M).astype(np.float32)
+    ret = rng.standard_normal(M).astype(np.float32)
+    ov = rng.standard_normal(M).astype(np.float32)
+    perm = rng.permutation(M).astype(np.int32)
+    out = []
+    for opt in ("upd_mfma=16", "upd_mfma=32"):
+        ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.2, ent=0.01, options=opt)
+        ag.load_params(p)
+        fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
+        st = ag.update(2.5e-4, perms=DeviceArray.from_numpy(perm), want_stats=True)
+        out.append((ag.last_grad(), st))
+        ag.close()
+    (g0, s0), (g1, s1) = out
+    assert rel(g1, g0) < 2e-5, rel(g1, g0)
+    for t in range(L.ntensors):
+        o, n = L.t_off[t], L.t_len[t]
+        if L.t_grad[t]:
+            assert rel(g1[o:o + n], g0[o:o + n]) < 2e-4, (t, rel(g1[o:o + n], g0[o:o + n]))
+    for k in ("pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac", "grad_norm"):
+        np.testing.assert_allclose(s1[k], s0[k], rtol=2e-5, atol=1e-7, err_msg=k)
+
+
+def test_upd32_refused_for_the_ppo_agent():
+    with pytest.raises(ppo_amd.PPOError, match="upd_mfma=32"):
+        make_agent(0, 17, 6, 64, 64, options="upd_mfma=32")

@@ -1058,9 +1058,14 @@ template <int NTO>
 struct RollVGeo {
   static constexpr int R = 2, H = 256, OP = NTO * 16, NHP = 16, LDZ = H + 4, LDQ = OP + 1;
   static constexpr int oW2L = 0;                    // W2 chain positions 128..255: [32][H] float4s
-  static constexpr int oXV = oW2L + 128 * H;        // layer-1 input, chain order: [R][OP]
-  static constexpr int oHV = oXV + R * OP;          // layer-2 input, chain order: [R][H]
-  static constexpr int oZL = oHV + R * H;           // layer outputs, natural order: [R][LDZ]
+  // layer inputs by chain position p = 16 i + k, k-major so that lane k of every 16-lane row loads
+  // positions k, 16 + k, ... as one contiguous run (row_newbcast then broadcasts position p from
+  // lane k): layer 1 [R][16][4] (i < OP / 16 <= 2), layer 2 [R][16][LDK] (i < 16, stride 20:
+  // conflict-free ds_read_b128)
+  static constexpr int LDK = 20;
+  static constexpr int oXV = oW2L + 128 * H;
+  static constexpr int oHV = oXV + R * 16 * 4;
+  static constexpr int oZL = oHV + R * 16 * LDK;    // layer outputs, natural order: [R][LDZ]
   static constexpr int oH2 = oZL + R * LDZ;         // head inputs h2: [R][LDZ]
   static constexpr int oRS = oH2 + R * LDZ;         // stats partials: sums [8][R], squares [8][R]
   static constexpr int oW3 = oRS + 16 * R;          // head rows [NHP][H]
@@ -1080,6 +1085,23 @@ PPO_DEV int chain_pos(int k) { return (k & ~15) | ((k & 3) << 2) | ((k >> 2) & 3
 // the SLP vectorizer cannot pack FMAs of one weight into v_pk_fma_f32 with the weight duplicated
 // into a register pair (2 VGPRs per resident weight: the layer's 160 no longer fit)
 PPO_DEV void fma_v(float& acc, float w, float x) { asm("v_fma_f32 %0, %1, %2, %0" : "+v"(acc) : "v"(w), "v"(x)); }
+// acc = fma(x from lane K of this lane's 16-lane row, w, acc): v_fmac_f32 with a row_newbcast DPP
+// source — one rounding, so bitwise fma(w, x, acc); the layer input reaches every lane without an
+// LDS broadcast read per position (4 LDS cycles per ds_read_b128 however many lanes share the
+// address). x is never written by a VALU instruction right before (loaded from LDS; an s_nop 1
+// precedes each chain), so the DPP read-after-VALU-write hazard cannot occur.
+template <int K>
+PPO_DEV void fmac_bc(float& acc, float x, float w) {
+  asm volatile("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x), "v"(w), "n"(K));
+}
+template <int... Is, typename F>
+PPO_DEV void static_for_impl(std::integer_sequence<int, Is...>, F&& f) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+PPO_DEV void static_for(F&& f) {
+  static_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
 }  // namespace
 
 constexpr int kRVThreads = 512;
@@ -1174,9 +1196,19 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
   lds_barrier();
   const SampleKey key = sample_key(a.seed, a.rank);
   const float hi = P[K.hi], lo = P[K.lo];
-  // Beta items (row, action, alpha | beta) spread evenly over the 8 waves
-  const int bper = (R * A * 2 + 7) / 8;
-  const int bitem = lane < bper ? wave * bper + lane : R * A * 2;
+  // Beta items (row, action, alpha | beta) spread evenly over waves 1-7, which are idle during the
+  // env step (wave 0): the next step's first Marsaglia-Tsang draws are computed there
+  const int bper = (R * A * 2 + 6) / 7;
+  const int bitem = (wave > 0 && lane < bper) ? (wave - 1) * bper + lane : R * A * 2;
+  auto draw0 = [&](long step) {
+    GammaDraw d = GammaDraw{0.f, 0.f};
+    if (bitem < R * A * 2) {
+      const int which = bitem & 1, ra = bitem >> 1, r = ra / A, ai = ra - r * A;
+      d = gamma_draw(key, (long)(row0 + r), step, 0x10000u + (uint32_t)(ai * 2 + which) * 64u);
+    }
+    return d;
+  };
+  GammaDraw gd0 = draw0(a.step0);
   // LayerNorm statistics lanes: (old wave ow, row r, lane group g), 8 R x 4 of them (wave 0)
   constexpr int NSL = 8 * R * 4;
   const int sg = tid & 3, sr = (tid >> 2) & (R - 1), sow = tid / (4 * R);
@@ -1223,8 +1255,9 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
     }
     lds_barrier();  // RS is reused by the next statistics
   };
-  const float* xv = XV + rg * OP;
-  const float* hv = HV + rg * H;
+  const int kl = lane & 15;  // this lane's position in its 16-lane row
+  const float* xv = XV + rg * 64 + kl * 4;
+  const float* hv = HV + rg * 16 * GE::LDK + kl * GE::LDK;
   for (int t = 0; t < a.T; ++t) {
     const long step_id = a.step0 + t;
     ROLL_STAMP(t, 0);
@@ -1237,24 +1270,21 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
       const bool valid = e < E && ff < O;
       const float x = valid ? XO[r * LDQ + ff] : 0.0f;
       if (valid) a.s_obs[((long)t * E + e) * O + ff] = x;
-      XV[r * OP + chain_pos(ff)] = valid ? (x - NRM[ff]) / NRM[OP + ff] : x;
+      const int p = chain_pos(ff);
+      XV[r * 64 + (p & 15) * 4 + (p >> 4)] = valid ? (x - NRM[ff]) / NRM[OP + ff] : x;
     }
     if (tid < R && row0 + tid < E) a.s_dones[(long)t * E + row0 + tid] = EV[EV_DONE * R + tid];
-    // the first Marsaglia-Tsang attempt's draws of this thread's item: independent of the network
-    GammaDraw gd0 = GammaDraw{0.f, 0.f};
-    if (bitem < R * A * 2) {
-      const int which = bitem & 1, ra = bitem >> 1, r = ra / A, ai = ra - r * A;
-      gd0 = gamma_draw(key, (long)(row0 + r), step_id, 0x10000u + (uint32_t)(ai * 2 + which) * 64u);
-    }
     lds_barrier();
     ROLL_STAMP(t, 1);
     // ---- layer 1 (k_act3's chain from the bias), one row per 4 waves ----
     float acc = b1;
-#pragma unroll
-    for (int p = 0; p < OP; p += 4) {
-      const f4 x = *reinterpret_cast<const f4*>(xv + p);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) fma_v(acc, w1r[p + c], x[c]);
+    {
+      const f4 x = *reinterpret_cast<const f4*>(xv);  // positions kl, 16 + kl
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 1" ::: "memory");
+      static_for<OP>([&](auto P) {
+        constexpr int p = decltype(P)::value;
+        fmac_bc<p & 15>(acc, x[p >> 4], w1r[p]);
+      });
     }
     ZL[rg * LDZ + f] = acc;
 #ifdef PPO_STAMPS
@@ -1265,29 +1295,35 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
     ln_stats(mu, rs);
     {
       const float y = __fmaf_rn(g1, (acc - mu[rg]) * rs[rg], be1);
-      HV[rg * H + chain_pos(f)] = y > 0.0f ? y : 0.0f;
+      const int p = chain_pos(f);
+      HV[rg * 16 * GE::LDK + (p & 15) * GE::LDK + (p >> 4)] = y > 0.0f ? y : 0.0f;
 #ifdef PPO_STAMPS
       if (dbg_r >= 0) RDBG(1, 260 + f, y > 0.0f ? y : 0.0f);
 #endif
     }
     lds_barrier();
     ROLL_STAMP(t, 5);
-    // ---- layer 2: chain positions 0..127 from registers, 128..255 from LDS ----
+    // ---- layer 2: weights of chain positions 0..127 from registers, 128..255 from LDS; the
+    // inputs (this row's 256 h1 values, 16 per lane, the same in every 16-lane row) by row_newbcast ----
     acc = b2;
+    {
+      float x[16];
 #pragma unroll
-    for (int p = 0; p < 128; p += 4) {
-      if (p % 32 == 0) __builtin_amdgcn_sched_barrier(0);  // bound the broadcast reads in flight
-      const f4 x = *reinterpret_cast<const f4*>(hv + p);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) fma_v(acc, w2r[p + c], x[c]);
-    }
-#pragma unroll
-    for (int p = 0; p < 128; p += 4) {
-      if (p % 32 == 0) __builtin_amdgcn_sched_barrier(0);
-      const f4 w = *reinterpret_cast<const f4*>(W2L + ((p >> 2) * H + f) * 4);
-      const f4 x = *reinterpret_cast<const f4*>(hv + 128 + p);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) fma_v(acc, w[c], x[c]);
+      for (int i = 0; i < 16; i += 4) *reinterpret_cast<f4*>(x + i) = *reinterpret_cast<const f4*>(hv + i);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 1" ::: "memory");
+      static_for<128>([&](auto P) {
+        constexpr int p = decltype(P)::value;
+        fmac_bc<p & 15>(acc, x[p >> 4], w2r[p]);
+      });
+      static_for<32>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        if constexpr (q % 8 == 0) __builtin_amdgcn_sched_barrier(0);  // bound the weight reads in flight
+        const f4 w = *reinterpret_cast<const f4*>(W2L + (q * H + f) * 4);
+        static_for<4>([&](auto C) {
+          constexpr int c = decltype(C)::value, p = 128 + 4 * q + c;
+          fmac_bc<p & 15>(acc, x[p >> 4], w[c]);
+        });
+      });
     }
     ZL[rg * LDZ + f] = acc;
 #ifdef PPO_STAMPS
@@ -1441,6 +1477,8 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
         }
       }
     }
+    // the first Marsaglia-Tsang attempt's draws of the next step (independent of the network)
+    if (wave > 0 && t + 1 < a.T) gd0 = draw0(step_id + 1);
     lds_barrier();
     ROLL_STAMP(t, 4);
   }

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Copy one gpu_final_r03.sh run (gpurun_out/<tag>, gpurun_out/prof_<tag>) into profiles/r03/<tag>.
-#   bash scripts/collect_final.sh <tag>
+# Copy one gpu_final_r0N.sh run (gpurun_out/<tag>, gpurun_out/prof_<tag>) into profiles/<round>/<tag>.
+#   ROUND=r04 bash scripts/collect_final.sh <tag>
 set -e
-T=$1; S=gpurun_out/$T; P=gpurun_out/prof_$T; D=profiles/r03/$T
+T=$1; S=gpurun_out/$T; P=gpurun_out/prof_$T; D=profiles/${ROUND:-r04}/$T
 mkdir -p $D/scale
 tail -1 $S/bench_default.log > $D/bench_default.json
 tail -1 $S/bench_all.log > $D/bench_all.json

@@ -51,4 +51,32 @@ for trunk, sl in (("critic", slice(0, 256)), ("actor", slice(512, 768))):
     print(f"{trunk}: {len(x)} wave-tiles, median tile {tot:.0f} cycles")
     for k, nm in enumerate(NAMES):
         print(f"  {k:2d} {nm:16s} {med[k]:8.0f}  {100 * med[k] / tot:5.1f}%")
+# co-residency: each workgroup's span (wave 0, first tile start .. last stamped tile end) and its CU
+# (HW_ID bits 8..15: CU / SH / SE, XCC id in the upper word); the critic and actor workgroups of a CU
+# run side by side only if their spans overlap
+ntile = int(min(NT, (cfg.num_envs * cfg.num_steps // 4 + 31) // 32 // 256))
+span0 = raw[:, 0, 0, 0].astype(np.int64)
+span1 = raw[:, 0, ntile - 1, NP].astype(np.int64)
+cuk = ((raw[:, 0, 0, NP + 1] >> np.uint64(8)) & np.uint64(0xFF)) | ((raw[:, 0, 0, NP + 1] >> np.uint64(32)) << np.uint64(8))
+ok = (span0 > 0) & (span1 > span0)
+wgs = [w for w in list(range(256)) + list(range(512, 768)) if ok[w]]
+if wgs:
+    t0 = min(span0[w] for w in wgs)
+    print(f"launch span {max(span1[w] for w in wgs) - t0} cycles over {ntile} tiles per workgroup; "
+          f"median workgroup span critic {np.median([span1[w] - span0[w] for w in wgs if w < 512]):.0f}, "
+          f"actor {np.median([span1[w] - span0[w] for w in wgs if w >= 512]):.0f}")
+    bycu = {}
+    for w in wgs:
+        bycu.setdefault(int(cuk[w]), []).append(w)
+    ov = []
+    for ws in bycu.values():
+        c = [w for w in ws if w < 512]
+        a_ = [w for w in ws if w >= 512]
+        for wc in c:
+            for wa in a_:
+                inter = min(span1[wc], span1[wa]) - max(span0[wc], span0[wa])
+                ov.append(max(0, inter) / max(span1[wc] - span0[wc], span1[wa] - span0[wa]))
+    print(f"CU keys {len(bycu)}; critic/actor pairs on one CU {len(ov)}, "
+          f"mean overlap of their spans {np.mean(ov) if ov else 0:.2f}; start offsets (median) "
+          f"critic {np.median([span0[w] - t0 for w in wgs if w < 512]):.0f} actor {np.median([span0[w] - t0 for w in wgs if w >= 512]):.0f}")
 tr.close()

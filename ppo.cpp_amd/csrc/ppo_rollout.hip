@@ -1071,8 +1071,7 @@ struct RollVGeo {
   static constexpr int oW3 = oRS + 16 * R;          // head rows [NHP][H]
   static constexpr int oHB = oW3 + NHP * H;         // head biases [NHP]
   static constexpr int oHP = oHB + NHP;             // head partials [8][NHP][R]
-  static constexpr int oITM = oHP + 8 * NHP * R;    // Beta items [R][24][2][4]
-  static constexpr int oXO = oITM + R * 24 * 2 * 4;  // agent input obs of the step [R][LDQ]
+  static constexpr int oXO = oHP + 8 * NHP * R;     // agent input obs of the step [R][LDQ]
   static constexpr int oQ = oXO + R * LDQ;          // env state q [R][LDQ]
   static constexpr int oNRM = oQ + R * LDQ;         // obs mean | std [2][OP]
   static constexpr int oACT = oNRM + 2 * OP;        // actions [R][24]
@@ -1120,7 +1119,6 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
   float* W3 = lds + GE::oW3;
   float* HBIAS = lds + GE::oHB;
   float* HP = lds + GE::oHP;
-  float* ITM = lds + GE::oITM;
   float* XO = lds + GE::oXO;
   float* Q = lds + GE::oQ;
   float* NRM = lds + GE::oNRM;
@@ -1197,8 +1195,9 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
   const SampleKey key = sample_key(a.seed, a.rank);
   const float hi = P[K.hi], lo = P[K.lo];
   // Beta items (row, action, alpha | beta) spread evenly over waves 1-7, which are idle during the
-  // env step (wave 0): the next step's first Marsaglia-Tsang draws are computed there
-  const int bper = (R * A * 2 + 6) / 7;
+  // env step (wave 0): the next step's first Marsaglia-Tsang draws are computed there. An even
+  // count per wave keeps an action's alpha and beta items in adjacent lanes (2 m, 2 m + 1)
+  const int bper = 2 * ((R * A + 6) / 7);
   const int bitem = (wave > 0 && lane < bper) ? (wave - 1) * bper + lane : R * A * 2;
   auto draw0 = [&](long step) {
     GammaDraw d = GammaDraw{0.f, 0.f};
@@ -1365,37 +1364,37 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
     }
     lds_barrier();
     ROLL_STAMP(t, 2);
-    // ---- Beta sample (k_rollout / k_act3 stages 1 and 2) ----
+    // ---- Beta sample (k_rollout / k_act3 stages 1 and 2): the alpha and beta items of an action
+    // sit in adjacent lanes, so stage 2 takes the partner's concentration and gamma sample by DPP
+    // (quad xor 1) instead of a round trip through LDS and a barrier ----
+    float bc = 1.0f, bg = 1.0f;
     if (bitem < R * A * 2) {
       const int which = bitem & 1, ra = bitem >> 1, r = ra / A, ai = ra - r * A, h = ai + which * A;
       float sm = 0.f;
 #pragma unroll
       for (int w = 0; w < kActWaves; ++w) sm += HP[(w * NHP + h) * R + r];
-      const float c = softplusf_(sm + HBIAS[h]) + 1.0f;
+      bc = softplusf_(sm + HBIAS[h]) + 1.0f;
 #ifdef PPO_STAMPS
       if (t == 0 && kRdbgEnv == row0 + r) RDBG(1, 1160 + h, sm + HBIAS[h]);
 #endif
       const uint32_t db = 0x10000u + (uint32_t)(ai * 2 + which) * 64u;
-      const float gs = gamma_mt_d0(c, gd0, key, (long)(row0 + r), step_id, db);
-      float* it = ITM + ((r * A + ai) * 2 + which) * 4;
-      it[0] = c;
-      it[1] = gs;
+      bg = gamma_mt_d0(bc, gd0, key, (long)(row0 + r), step_id, db);
     }
-    lds_barrier();
-    if (tid < R * A) {
-      const int idx = tid, r = idx / A, ai = idx - r * A, e = row0 + r;
-      const float* ia = ITM + (idx * 2 + 0) * 4;
-      const float* ib = ITM + (idx * 2 + 1) * 4;
-      const float al = ia[0], be = ib[0];
-      const float s01 = ia[1] / (ia[1] + ib[1]);
-      const float act = (s01 - 0.0f) / (1.0f - 0.0f) * (hi - lo) + lo;
-      ACT[r * 24 + ai] = act;
-      if (e < E) {
-        a.s_actions[((long)t * E + e) * A + ai] = act;
-        float* d = a.s_beta + (((long)t * E + e) * A + ai) * 3;
-        d[0] = al;
-        d[1] = be;
-        d[2] = s01;
+    {
+      const float pc = dpp_f<kDppQuadXor1>(bc), pg = dpp_f<kDppQuadXor1>(bg);  // every lane of the wave
+      if (bitem < R * A * 2 && (bitem & 1) == 0) {
+        const int ra = bitem >> 1, r = ra / A, ai = ra - r * A, e = row0 + r;
+        const float al = bc, be = pc;
+        const float s01 = bg / (bg + pg);
+        const float act = (s01 - 0.0f) / (1.0f - 0.0f) * (hi - lo) + lo;
+        ACT[r * 24 + ai] = act;
+        if (e < E) {
+          a.s_actions[((long)t * E + e) * A + ai] = act;
+          float* d = a.s_beta + (((long)t * E + e) * A + ai) * 3;
+          d[0] = al;
+          d[1] = be;
+          d[2] = s01;
+        }
       }
     }
     lds_barrier();

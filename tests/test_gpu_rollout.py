@@ -69,14 +69,16 @@ def test_persistent_rollout_bitwise_equals_per_step(agent, env_id, E, iters):
         tr.close()
 
 
-@pytest.mark.parametrize("E", [512, 1024])
-def test_valu_rollout_bitwise_equals_mfma_rollout(E):
-    """The N = 8 / N = 4 shards of the metric config (AC HalfCheetah, E = 512 / 1 024): the VALU
-    rollout (rollout_kernel=valu: 2 / 4 envs per workgroup, v_fma_f32 chains in the MFMA's k order,
-    k_act3's LayerNorm / head partial-sum trees) against the MFMA rollout (rollout_kernel=mfma):
-    every stored buffer, the env state and, after the shared update, the parameters bitwise equal over
-    two iterations."""
-    cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=E, num_steps=128, num_minibatches=4,
+@pytest.mark.parametrize("env_id,E", [("HalfCheetah-v5", 512), ("HalfCheetah-v5", 1024), ("HalfCheetah-v5", 333),
+                                      ("Hopper-v5", 64)])
+def test_valu_rollout_bitwise_equals_mfma_rollout(env_id, E):
+    """The N = 8 / N = 4 shards of the metric config (AC HalfCheetah, E = 512 / 1 024), an odd E (the
+    last workgroup's second env absent) and Hopper (O = 11: one 16-wide input block, observation
+    normalisation tables): the VALU rollout (rollout_kernel=valu: 2 envs per workgroup, v_fma_f32 /
+    row_newbcast chains in the MFMA's k order, k_act3's LayerNorm / head partial-sum trees) against
+    the MFMA rollout (rollout_kernel=mfma): every stored buffer, the env state and, after the shared
+    update, the parameters bitwise equal over two iterations."""
+    cfg = ppo_amd.ACPPOConfig(env_id=env_id, num_envs=E, num_steps=128, num_minibatches=1 if E % 4 else 4,
                               update_epochs=1, total_timesteps=E * 128 * 2)
     trs = [ppo_amd.Trainer(cfg, options="rollout_kernel=valu"), ppo_amd.Trainer(cfg, options="rollout_kernel=mfma")]
     for it in range(2):

@@ -99,9 +99,10 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            of both trunks as one gathered GEMM (k_l1g) and k_upd2's tail in its own
  *                            launch at 2 / 3 workgroups per CU, or the single k_upd2 (0; auto: the
  *                            single kernel, measured faster)
- *   upd_mfma=auto|16|32      LayerNorm-Beta agent at hidden 256: the fused minibatch kernel on
- *                            16x16x4 MFMAs (k_upd; auto) or on 32x32x2 MFMAs (k_upd32); the same
- *                            results up to summation order
+ *   upd_mfma=auto|16|32|mix  LayerNorm-Beta agent at hidden 256: the fused minibatch kernel on
+ *                            16x16x4 MFMAs (k_upd; auto), on 32x32x2 MFMAs (k_upd32), or mixed
+ *                            (critic trunk 32x32x2, actor 16x16x4); the same results up to
+ *                            summation order
  *   rollout=auto|per_step    ppo_rollout_synth: persistent launch where supported, or per step
  *   rollout_kernel=auto|mfma|valu  the AC agent's persistent rollout: k_rollout (16 envs per
  *                            workgroup, MFMA) or k_rollout_v (2 envs per workgroup, VALU; O <= 32);

@@ -154,6 +154,7 @@ struct ppo_ctx {
   int tiles_per_block = 1, nblk = 1;
   bool use_upd = false;  // feature-split k_upd (ppo_update.hip) instead of k_fwdbwd
   bool use_upd32 = false;  // k_upd32 (32x32x2 MFMAs) instead of k_upd (create option upd_mfma)
+  int upd32_mix = 0;       // k_upd32 with the actor trunk on k_upd's body (upd_mfma=mix)
   bool use_upd2 = false;  // two-trunk k_upd2 (ppo_update_narrow.hip, H = 64 tanh agent)
   int rollout_kernel = 0;   // AC persistent rollout: 0 auto, 1 k_rollout (MFMA), 2 k_rollout_v (VALU)
   int upd2_split = 0;       // k_l1g (layer 1 as a gathered GEMM into Z1) + k_upd2's split form at 2 / 3 per CU
@@ -282,7 +283,8 @@ struct CreateOptions {
   int update_graph = 0;
   int rollout_kernel = 0;  // 0 auto, 1 mfma (k_rollout), 2 valu (k_rollout_v)
   int upd2_split = -1;  // -1 auto (wide inputs: k_l1g + split k_upd2), 0 one k_upd2, 2 / 3 split at 2 / 3 workgroups per CU
-  int upd_mfma = 0;     // 0 auto, 16: k_upd (16x16x4 MFMAs), 32: k_upd32 (32x32x2; LayerNorm-Beta agent, H = 256)
+  int upd_mfma = 0;     // 0 auto, 16: k_upd (16x16x4 MFMAs), 32: k_upd32 (32x32x2; LayerNorm-Beta agent, H = 256),
+                        // 1: k_upd32's mixed form (critic 32x32x2, actor 16x16x4)
 };
 // auto = the single k_upd2: the split form measured slower on cfg2 (round 4, profiles/r04/cfg2_split/:
 // 101.3 vs 92.9 ms per iteration; k_l1g 66 us = 0.61 of peak per launch, the tail 94 us at 3 per CU)
@@ -315,7 +317,8 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
     else if (k == "rollout_kernel" && (v == "auto" || v == "mfma" || v == "valu"))
       o->rollout_kernel = v == "auto" ? 0 : v == "mfma" ? 1 : 2;
     else if (k == "upd2_split" && (v == "auto" || v == "0" || v == "2" || v == "3")) o->upd2_split = v == "auto" ? -1 : v[0] - '0';
-    else if (k == "upd_mfma" && (v == "auto" || v == "16" || v == "32")) o->upd_mfma = v == "auto" ? 0 : atoi(v.c_str());
+    else if (k == "upd_mfma" && (v == "auto" || v == "16" || v == "32" || v == "mix"))
+      o->upd_mfma = v == "auto" ? 0 : v == "mix" ? 1 : atoi(v.c_str());
     else return fail("ppo_create_ex: unknown option or value: " + kv);
   }
   return 0;
@@ -435,9 +438,9 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
     // k_upd2 addresses the rollout storage with 32-bit buffer offsets
     const bool fits32 = (double)B * (double)std::max(O, A) * 4.0 < 4294967040.0;
     const int split = !fits32 ? 0 : opt.upd2_split >= 0 ? opt.upd2_split : upd2_split_supported(c->K) ? kUpd2SplitAuto : 0;
-    if (opt.upd_mfma == 32 && (H != 256 || cfg->net_kind != PPO_NET_LN_BETA)) {
+    if ((opt.upd_mfma == 32 || opt.upd_mfma == 1) && (H != 256 || cfg->net_kind != PPO_NET_LN_BETA)) {
       delete c;
-      return fail("ppo_create: upd_mfma=32 needs the LayerNorm-Beta agent at hidden 256");
+      return fail("ppo_create: upd_mfma=32 / mix needs the LayerNorm-Beta agent at hidden 256");
     }
     if (opt.upd2_split > 0 && (upd_kernel || !upd2_split_supported(c->K))) {
       delete c;
@@ -449,10 +452,11 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
       const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
       // both trunks per workgroup, 2 workgroups per CU x 256 CUs (split form: 3 per CU)
       c->upd_nblk = std::min(ut, split ? 256 * split : 512);
-    } else if (opt.upd_mfma == 32) {
-      if (upd_kernel || upd32_supported(c->K, c->sg[1].nh, c->sg[0].size, c->sg[1].size, &c->upd) != 0) {
+    } else if (opt.upd_mfma == 32 || opt.upd_mfma == 1) {
+      c->upd32_mix = opt.upd_mfma == 1;
+      if (upd_kernel || upd32_supported(c->K, c->sg[1].nh, c->sg[0].size, c->sg[1].size, &c->upd, c->upd32_mix) != 0) {
         delete c;
-        return fail("ppo_create: upd_mfma=32 needs the LayerNorm-Beta agent at hidden 256");
+        return fail("ppo_create: upd_mfma=32 / mix needs the LayerNorm-Beta agent at hidden 256");
       }
       c->use_upd = c->use_upd32 = true;
       c->upd_nblk = std::min((c->M + c->upd.rows - 1) / c->upd.rows, 256);
@@ -542,13 +546,15 @@ extern "C" int ppo_set_iteration(ppo_t* c, long it) {
   c->iteration = it;
   return 0;
 }
-// debug hook (not part of the C-ABI header): internal device buffers by name ("beta_store": the AC
-// rollout's (alpha, beta, sample) per (t, env, action))
+#ifdef PPO_DIAG
+// diagnostic build only (not part of the C-ABI header): internal device buffers by name
+// ("beta_store": the AC rollout's (alpha, beta, sample) per (t, env, action); scripts/debug_rollout_v.py)
 extern "C" float* ppo_debug_buffer(ppo_t* c, const char* name) {
   if (!c || !name) return nullptr;
   if (!strcmp(name, "beta_store")) return c->beta_store;
   return nullptr;
 }
+#endif
 extern "C" float* ppo_buffer(ppo_t* c, int which) {
   if (!c || which < 0 || which >= PPO_BUF_COUNT) return nullptr;
   return c->buf[which];
@@ -973,7 +979,7 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
       {
         ProfScope ps(c, PK_FWDBWD, s);
         const int rc_ = c->use_upd2  ? launch_upd2(u, c->upd_nblk, c->upd.lds_bytes, s, c->upd2_split)
-                        : c->use_upd32 ? launch_upd32(u, c->sg[1].nh, c->upd_nblk, c->upd.lds_bytes, s)
+                        : c->use_upd32 ? launch_upd32(u, c->sg[1].nh, c->upd_nblk, c->upd.lds_bytes, s, c->upd32_mix)
                         : c->use_upd ? launch_upd(u, c->sg[1].nh, c->upd_nblk, c->upd.lds_bytes, s)
                                      : launch_fwdbwd(u, nblk, c->lds_bytes, s);
         if (rc_ != 0) return fail("no update kernel for this configuration");

@@ -246,9 +246,10 @@ int launch_fwdbwd(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s
 int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes);
 int upd_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g);
 int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s);
-// k_upd32 (create option upd_mfma=32): k_upd on 32x32x2 MFMAs, LayerNorm-Beta agent at H = 256
-int upd32_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g);
-int launch_upd32(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s);
+// k_upd32 (create option upd_mfma=32 | mix): k_upd on 32x32x2 MFMAs, LayerNorm-Beta agent at
+// H = 256; mix = 1: only the critic trunk on 32x32x2, the actor on k_upd's body
+int upd32_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g, int mix);
+int launch_upd32(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s, int mix);
 // ppo_update_narrow.hip (H = 64 tanh agent); split form: k_l1g computes layer 1 (a.Z1), k_upd2 the rest
 bool upd2_split_supported(const PackedLayout& K);
 // split: 0 one kernel; 2 / 3 the split form at 2 / 3 workgroups per CU

@@ -345,8 +345,9 @@ PPO_DEV int head_bias(const PackedLayout& K, int trunk, int h) {
 
 }  // namespace
 
+// k_upd's body (a device function so that k_upd32's mixed form can run it for the actor trunk)
 template <int H, int KIND, int NTO, int NHT, int KL1>
-__global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
+PPO_DEV void upd16_body(const UpdArgs& a) {
   using GE = Geo<H, NTO, NHT>;
   constexpr int FT = GE::FT, RT = GE::RT, WF = GE::WF, R = GE::R, NT = GE::NT, OP = GE::OP;
   constexpr int LDX = GE::LDX, LDA = GE::LDA, LDG = GE::LDG, NHP = GE::NHP, ITS = GE::ITS;
@@ -1294,7 +1295,7 @@ PPO_DEV void zero32(f16v (&v)[2]) {
 }  // namespace
 
 template <int NTO, int NHT, int KL1>
-__global__ __launch_bounds__(256, 2) void k_upd32(UpdArgs a) {
+PPO_DEV void upd32_body(const UpdArgs& a) {
   constexpr int H = 256;
   using GE = Geo<H, NTO, NHT>;
   constexpr int R = GE::R, OP = GE::OP, NHP = GE::NHP, ITS = GE::ITS;
@@ -1974,6 +1975,21 @@ __global__ __launch_bounds__(256, 2) void k_upd32(UpdArgs a) {
   for (int i = tid; i < sl.size; i += 256) slab_row[hwg && i >= sg.hW ? i + sg.nh * H : i] = ACC[i];
 }
 
+template <int H, int KIND, int NTO, int NHT, int KL1>
+__global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
+  upd16_body<H, KIND, NTO, NHT, KL1>(a);
+}
+
+// MIX = 0: both trunks on 32x32x2 MFMAs; MIX = 1: the critic on 32x32x2, the actor on k_upd's
+// 16x16x4 body (the actor's loss and LayerNorm phases are VALU chains that co-issue beside the
+// partner's MFMAs: 6.2 VALU per 32x32x2 against 2.2 per 16x16x4)
+template <int NTO, int NHT, int KL1, int MIX>
+__global__ __launch_bounds__(256, 2) void k_upd32(UpdArgs a) {
+  const int trunk = (a.sched & 1) ? 1 - (int)blockIdx.y : (int)blockIdx.y;
+  if (MIX && trunk == 1) upd16_body<256, PPO_NET_LN_BETA, NTO, NHT, KL1>(a);
+  else upd32_body<NTO, NHT, KL1>(a);
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side: geometry, LDS size, dispatch
 // ---------------------------------------------------------------------------------------------
@@ -2055,25 +2071,24 @@ static int dispatch_upd32(const PackedLayout& K, int nh, F&& f) {
   return -1;
 }
 
-int upd32_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g) {
+int upd32_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g, int mix) {
   return dispatch_upd32(K, nh_actor, [&](auto NTO_, auto NHT_, auto KL_) {
     upd_geo<256, decltype(NTO_)::value, decltype(NHT_)::value>(K, nh_actor, sg0_size, sg1_size, g);
-    const auto k = k_upd32<decltype(NTO_)::value, decltype(NHT_)::value, decltype(KL_)::value>;
-    return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) ==
-                   hipSuccess
-               ? 0
-               : -2;
+    constexpr int N = decltype(NTO_)::value, T = decltype(NHT_)::value, L = decltype(KL_)::value;
+    const void* k = mix ? (const void*)k_upd32<N, T, L, 1> : (const void*)k_upd32<N, T, L, 0>;
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) == hipSuccess ? 0 : -2;
   });
 }
 
-int launch_upd32(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s) {
+int launch_upd32(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s, int mix) {
   UpdArgs b = a;
 #ifndef PPO_DIAG
   b.trunk_mask = 3;
 #endif
   return dispatch_upd32(a.K, nh_actor, [&](auto NTO_, auto NHT_, auto KL_) {
-    hipLaunchKernelGGL((k_upd32<decltype(NTO_)::value, decltype(NHT_)::value, decltype(KL_)::value>), dim3(nblocks, 2),
-                       dim3(256), lds_bytes, s, b);
+    constexpr int N = decltype(NTO_)::value, T = decltype(NHT_)::value, L = decltype(KL_)::value;
+    if (mix) hipLaunchKernelGGL((k_upd32<N, T, L, 1>), dim3(nblocks, 2), dim3(256), lds_bytes, s, b);
+    else hipLaunchKernelGGL((k_upd32<N, T, L, 0>), dim3(nblocks, 2), dim3(256), lds_bytes, s, b);
     return 0;
   });
 }

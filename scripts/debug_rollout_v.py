@@ -5,9 +5,9 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RDBG = os.environ.get("RDBG") == "1"  # stamps build: per-layer dumps of env 26 at step 0 (g_rdbg)
-if RDBG:
-    os.environ["PPO_HIP_LIB"] = os.path.join(ROOT, "ppo.cpp_amd", "lib", "libppo_hip_stamps.so")
+RDBG = os.environ.get("RDBG") == "1"  # also the per-layer dumps of env 26 at step 0 (g_rdbg)
+# the diagnostic build (make -C ppo.cpp_amd stamps): ppo_debug_buffer, ppo_diag_read_rdbg
+os.environ["PPO_HIP_LIB"] = os.path.join(ROOT, "ppo.cpp_amd", "lib", "libppo_hip_stamps.so")
 sys.path.insert(0, os.path.join(ROOT, "ppo.cpp_amd"))
 import numpy as np  # noqa: E402
 

@@ -40,6 +40,7 @@ from test_gpu_parity import fill_storage, make_agent, random_params, rel  # noqa
     # the same two through k_upd32 (32x32x2 MFMA layout, create option upd_mfma=32)
     ("metric_halfcheetah_mfma32", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=32"),
     ("cfg4_shard_ant_mfma32", 1, 256, 105, 8, 1024, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=32"),
+    ("metric_halfcheetah_mix", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=mix"),
     # cfg2: ppo_continuous_action Humanoid-v4, E=1024, T=2048, 32 minibatches -> M = 65 536 rows
     # (ppo:489-542; clip 0.2, ent_coef 0, lr 3e-4, ppo:60-67): k_upd2 walks 128 32-row tiles per
     # workgroup pair and k_dw2_dma sums 256 split-K chunks of 256 rows
@@ -131,8 +132,9 @@ def test_cfg2_split_update_matches_single_kernel(split):
     assert np.abs(p1 - p0).max() < 1e-5
 
 
-@pytest.mark.parametrize("O_,A,E", [(17, 6, 999), (105, 8, 777), (16, 8, 333)])
-def test_upd32_matches_upd(O_, A, E):
+@pytest.mark.parametrize("O_,A,E,opt32", [(17, 6, 999, "upd_mfma=32"), (105, 8, 777, "upd_mfma=32"),
+                                          (16, 8, 333, "upd_mfma=32"), (17, 6, 999, "upd_mfma=mix")])
+def test_upd32_matches_upd(O_, A, E, opt32):
     """k_upd32 (upd_mfma=32) against k_upd on the same minibatch, ragged last tile (E = M not a
     multiple of 32; O = 17: the one-column last k-block, 105: the synchronous wide gather, 16: one
     full k-block, A = 8: a full head tile): the same products summed in another order (32x32x2 chains and 32-lane reductions),
@@ -150,7 +152,7 @@ def test_upd32_matches_upd(O_, A, E):
     ov = rng.standard_normal(M).astype(np.float32)
     perm = rng.permutation(M).astype(np.int32)
     out = []
-    for opt in ("upd_mfma=16", "upd_mfma=32"):
+    for opt in ("upd_mfma=16", opt32):
         ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.2, ent=0.01, options=opt)
         ag.load_params(p)
         fill_storage(ag, T, E, x, act, olp, adv, ret, ov)

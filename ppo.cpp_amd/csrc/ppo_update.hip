@@ -345,6 +345,176 @@ PPO_DEV int head_bias(const PackedLayout& K, int trunk, int h) {
 
 }  // namespace
 
+// The PPO loss of one tile and its gradient wrt the head pre-activations: PRE -> GG (critic: the
+// clipped value loss, ppo:520-533; actor: Beta or Normal log-prob / entropy, the clipped surrogate,
+// ppo:497-519, ac:815-875), the per-lane loss statistics added to lst. Shared by k_upd and k_upd32.
+template <bool LN, int R, int ITS, int LDG>
+PPO_DEV void upd_loss(const UpdArgs& a, int trunk, int tid, int m0, float c, float adv_mean, float adv_std,
+                      const float* PRE, float* GG, float* ROWS, const float* ACTN, float* ITM, float (&lst)[6]) {
+  const PackedLayout& K = a.K;
+  const float* __restrict__ P = a.P;
+  const int A = K.A;
+  float st_a = 0.f, st_b = 0.f, st_c = 0.f, st_d = 0.f, st_e = 0.f, st_f = 0.f;  // per-row stats (tid < R)
+  if (trunk == 0) {
+    if (tid < R) {
+      const bool valid = m0 + tid < a.M;
+      const float v = PRE[tid * LDG];
+      const float rt_ = ROWS[tid * 8 + 1], ov = ROWS[tid * 8 + 2];
+      float gv, sv;
+      if (a.clip_vloss) {
+        const float vu = (v - rt_) * (v - rt_);
+        const float dv = v - ov;
+        const float vcl = ov + fminf(fmaxf(dv, -c), c);
+        const float vc = (vcl - rt_) * (vcl - rt_);
+        sv = fmaxf(vu, vc);
+        const float w1 = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
+        const float inr = (dv >= -c && dv <= c) ? 1.0f : 0.0f;
+        gv = 0.5f * a.vf_coef * a.inv_m * (w1 * 2.0f * (v - rt_) + (1.0f - w1) * 2.0f * (vcl - rt_) * inr);
+      } else {
+        sv = (v - rt_) * (v - rt_);
+        gv = 0.5f * a.vf_coef * a.inv_m * 2.0f * (v - rt_);
+      }
+      if (!valid) { gv = 0.f; sv = 0.f; }
+      GG[tid * LDG] = gv;
+      st_b = sv;
+    }
+  } else if (LN && R == 32 && A <= 8) {
+    // Beta actor, one row per 8-lane group (32 rows x 8 lanes = the workgroup), one (row, action)
+    // item per lane: the row's log-prob / entropy sums are DPP sums inside the group, every lane
+    // of the group evaluates the row's surrogate, and the head gradients are written straight to
+    // GG — no item scratch in LDS and one barrier instead of three
+    const int row = tid >> 3, ai = tid & 7;
+    const bool item = ai < A;
+    const bool valid = m0 + row < a.M;
+    const int ac = item ? ai : 0;  // lanes past A evaluate item 0 and drop it (uniform control flow)
+    const float hi = P[K.hi], lo = P[K.lo];
+    const float pa = PRE[row * LDG + ac], pbv = PRE[row * LDG + A + ac];
+    const float al = softplusf_(pa) + 1.0f, be = softplusf_(pbv) + 1.0f;
+    const float av = valid ? ACTN[row * A + ac] : 0.5f * (hi + lo);
+    float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+    s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
+    const float ab = al + be;
+    float lga, lgb, lgab, psa, psb, psab, ta, tb, tab;
+    lgamma_digamma_trigamma(al, lga, psa, ta);
+    lgamma_digamma_trigamma(be, lgb, psb, tb);
+    lgamma_digamma_trigamma(ab, lgab, psab, tab);
+    const float lpi = xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
+    const float eni = (lga + lgb) - lgab - (2.0f - ab) * psab - ((al - 1.0f) * psa + (be - 1.0f) * psb);
+    const float lp = group8_sum(item ? lpi : 0.0f), ent = group8_sum(item ? eni : 0.0f);
+    const float oldlp = valid ? ROWS[row * 8 + 1] : lp;
+    const float logratio = lp - oldlp;
+    const float ratio = expf(logratio);
+    float an = valid ? ROWS[row * 8 + 2] : 0.f;
+    if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
+    const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
+    const float pg1 = -an * ratio, pg2 = -an * rc;
+    const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+    const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
+    float g_logp = a.inv_m * (w1 * (-an) + (1.0f - w1) * (-an) * inr) * ratio;
+    float g_ent = -a.ent_coef * a.inv_m;
+    if (!valid) { g_logp = 0.f; g_ent = 0.f; }
+    if (ai == 0 && valid) {  // the row's statistics, once per row
+      st_a = fmaxf(pg1, pg2);
+      st_c = ent;
+      st_d = -logratio;
+      st_e = (ratio - 1.0f) - logratio;
+      st_f = fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
+    }
+    if (item) {
+      const float dla = ((al - 1.0f) != 0.0f ? logf(s) : 0.0f) + psab - psa;         // d lp / d alpha
+      const float dea = (ab - 2.0f) * tab - (al - 1.0f) * ta;                         // d ent / d alpha
+      const float dlb = ((be - 1.0f) != 0.0f ? logf(1.0f - s) : 0.0f) + psab - psb;  // d lp / d beta
+      const float deb = (ab - 2.0f) * tab - (be - 1.0f) * tb;                         // d ent / d beta
+      GG[row * LDG + ai] = (g_logp * dla + g_ent * dea) * softplus_d(pa);
+      GG[row * LDG + A + ai] = (g_logp * dlb + g_ent * deb) * softplus_d(pbv);
+    }
+  } else {
+    // pass 1: per (row, action) log-prob / entropy terms and derivative pieces
+    for (int idx = tid; idx < R * A; idx += 256) {
+      const int row = idx / A, ai = idx - row * A;
+      const bool valid = m0 + row < a.M;
+      float* it_ = ITM + idx * ITS;
+      if constexpr (LN) {
+        const float hi = P[K.hi], lo = P[K.lo];
+        const float pa = PRE[row * LDG + ai], pbv = PRE[row * LDG + A + ai];
+        const float al = softplusf_(pa) + 1.0f, be = softplusf_(pbv) + 1.0f;
+        const float av = valid ? ACTN[idx] : 0.5f * (hi + lo);
+        float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
+        s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
+        const float ab = al + be;
+        float lga, lgb, lgab, psa, psb, psab, ta, tb, tab;
+        lgamma_digamma_trigamma(al, lga, psa, ta);
+        lgamma_digamma_trigamma(be, lgb, psb, tb);
+        lgamma_digamma_trigamma(ab, lgab, psab, tab);
+        it_[0] = xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
+        it_[1] = (lga + lgb) - lgab - (2.0f - ab) * psab - ((al - 1.0f) * psa + (be - 1.0f) * psb);
+        it_[2] = ((al - 1.0f) != 0.0f ? logf(s) : 0.0f) + psab - psa;            // d lp / d alpha
+        it_[3] = (ab - 2.0f) * tab - (al - 1.0f) * ta;                            // d ent / d alpha
+        it_[4] = softplus_d(pa);
+        it_[5] = ((be - 1.0f) != 0.0f ? logf(1.0f - s) : 0.0f) + psab - psb;     // d lp / d beta
+        it_[6] = (ab - 2.0f) * tab - (be - 1.0f) * tb;                            // d ent / d beta
+        it_[7] = softplus_d(pbv);
+      } else {
+        const float mu = PRE[row * LDG + ai];
+        const float sd = expf(P[K.logstd + ai]);
+        const float var = sd * sd, lsd = logf(sd);
+        const float act = valid ? ACTN[idx] : mu;
+        const float d = act - mu;
+        it_[0] = -(d * d) / (2.0f * var) - lsd - kLz;
+        it_[1] = kEntC + lsd;
+        it_[2] = d / var;
+        it_[3] = d * d / var - 1.0f;
+      }
+    }
+    lds_barrier();
+    // per row: log-prob / entropy sums, clipped surrogate, d loss / d logp, d loss / d ent
+    if (tid < R) {
+      const bool valid = m0 + tid < a.M;
+      float lp = 0.f, ent = 0.f;
+      for (int ai = 0; ai < A; ++ai) {
+        lp += ITM[(tid * A + ai) * ITS + 0];
+        ent += ITM[(tid * A + ai) * ITS + 1];
+      }
+      const float oldlp = valid ? ROWS[tid * 8 + 1] : lp;
+      const float logratio = lp - oldlp;
+      const float ratio = expf(logratio);
+      float an = valid ? ROWS[tid * 8 + 2] : 0.f;
+      if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
+      const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
+      const float pg1 = -an * ratio, pg2 = -an * rc;
+      const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
+      const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
+      float g_logp = a.inv_m * (w1 * (-an) + (1.0f - w1) * (-an) * inr) * ratio;
+      float g_ent = -a.ent_coef * a.inv_m;
+      st_a = fmaxf(pg1, pg2);
+      st_c = ent;
+      st_d = -logratio;
+      st_e = (ratio - 1.0f) - logratio;
+      st_f = fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
+      if (!valid) { g_logp = 0.f; g_ent = 0.f; st_a = st_c = st_d = st_e = st_f = 0.f; }
+      ROWS[tid * 8 + 3] = g_logp;
+      ROWS[tid * 8 + 4] = g_ent;
+    }
+    lds_barrier();
+    // pass 2: head gradients
+    for (int idx = tid; idx < R * A; idx += 256) {
+      const int row = idx / A, ai = idx - row * A;
+      const float g_logp = ROWS[row * 8 + 3], g_ent = ROWS[row * 8 + 4];
+      float* it_ = ITM + idx * ITS;
+      if constexpr (LN) {
+        GG[row * LDG + ai] = (g_logp * it_[2] + g_ent * it_[3]) * it_[4];
+        GG[row * LDG + A + ai] = (g_logp * it_[5] + g_ent * it_[6]) * it_[7];
+      } else {
+        GG[row * LDG + ai] = g_logp * it_[2];
+        it_[4] = g_logp * it_[3] + g_ent;  // d loss / d logstd (per row)
+      }
+    }
+  }
+  // loss statistics: summed per lane over the tiles, reduced across lanes and waves once after
+  // the tile loop (reported values only, no gradient depends on them)
+  lst[0] += st_a; lst[1] += st_b; lst[2] += st_c; lst[3] += st_d; lst[4] += st_e; lst[5] += st_f;
+}
+
 // k_upd's body (a device function so that k_upd32's mixed form can run it for the actor trunk)
 template <int H, int KIND, int NTO, int NHT, int KL1>
 PPO_DEV void upd16_body(const UpdArgs& a) {
@@ -770,165 +940,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
 
     // ---------------- loss and its gradient wrt the head pre-activations ----------------
     float* ITM = SCR;  // R x A x ITS (head partials are consumed)
-    float st_a = 0.f, st_b = 0.f, st_c = 0.f, st_d = 0.f, st_e = 0.f, st_f = 0.f;  // per-row stats (tid < R)
-    if (trunk == 0) {
-      if (tid < R) {
-        const bool valid = m0 + tid < a.M;
-        const float v = PRE[tid * LDG];
-        const float rt_ = ROWS[tid * 8 + 1], ov = ROWS[tid * 8 + 2];
-        float gv, sv;
-        if (a.clip_vloss) {
-          const float vu = (v - rt_) * (v - rt_);
-          const float dv = v - ov;
-          const float vcl = ov + fminf(fmaxf(dv, -c), c);
-          const float vc = (vcl - rt_) * (vcl - rt_);
-          sv = fmaxf(vu, vc);
-          const float w1 = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
-          const float inr = (dv >= -c && dv <= c) ? 1.0f : 0.0f;
-          gv = 0.5f * a.vf_coef * a.inv_m * (w1 * 2.0f * (v - rt_) + (1.0f - w1) * 2.0f * (vcl - rt_) * inr);
-        } else {
-          sv = (v - rt_) * (v - rt_);
-          gv = 0.5f * a.vf_coef * a.inv_m * 2.0f * (v - rt_);
-        }
-        if (!valid) { gv = 0.f; sv = 0.f; }
-        GG[tid * LDG] = gv;
-        st_b = sv;
-      }
-    } else if (LN && R == 32 && A <= 8) {
-      // Beta actor, one row per 8-lane group (32 rows x 8 lanes = the workgroup), one (row, action)
-      // item per lane: the row's log-prob / entropy sums are DPP sums inside the group, every lane
-      // of the group evaluates the row's surrogate, and the head gradients are written straight to
-      // GG — no item scratch in LDS and one barrier instead of three
-      const int row = tid >> 3, ai = tid & 7;
-      const bool item = ai < A;
-      const bool valid = m0 + row < a.M;
-      const int ac = item ? ai : 0;  // lanes past A evaluate item 0 and drop it (uniform control flow)
-      const float hi = P[K.hi], lo = P[K.lo];
-      const float pa = PRE[row * LDG + ac], pbv = PRE[row * LDG + A + ac];
-      const float al = softplusf_(pa) + 1.0f, be = softplusf_(pbv) + 1.0f;
-      const float av = valid ? ACTN[row * A + ac] : 0.5f * (hi + lo);
-      float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
-      s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
-      const float ab = al + be;
-      float lga, lgb, lgab, psa, psb, psab, ta, tb, tab;
-      lgamma_digamma_trigamma(al, lga, psa, ta);
-      lgamma_digamma_trigamma(be, lgb, psb, tb);
-      lgamma_digamma_trigamma(ab, lgab, psab, tab);
-      const float lpi = xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
-      const float eni = (lga + lgb) - lgab - (2.0f - ab) * psab - ((al - 1.0f) * psa + (be - 1.0f) * psb);
-      const float lp = group8_sum(item ? lpi : 0.0f), ent = group8_sum(item ? eni : 0.0f);
-      const float oldlp = valid ? ROWS[row * 8 + 1] : lp;
-      const float logratio = lp - oldlp;
-      const float ratio = expf(logratio);
-      float an = valid ? ROWS[row * 8 + 2] : 0.f;
-      if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
-      const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
-      const float pg1 = -an * ratio, pg2 = -an * rc;
-      const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
-      const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
-      float g_logp = a.inv_m * (w1 * (-an) + (1.0f - w1) * (-an) * inr) * ratio;
-      float g_ent = -a.ent_coef * a.inv_m;
-      if (!valid) { g_logp = 0.f; g_ent = 0.f; }
-      if (ai == 0 && valid) {  // the row's statistics, once per row
-        st_a = fmaxf(pg1, pg2);
-        st_c = ent;
-        st_d = -logratio;
-        st_e = (ratio - 1.0f) - logratio;
-        st_f = fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
-      }
-      if (item) {
-        const float dla = ((al - 1.0f) != 0.0f ? logf(s) : 0.0f) + psab - psa;         // d lp / d alpha
-        const float dea = (ab - 2.0f) * tab - (al - 1.0f) * ta;                         // d ent / d alpha
-        const float dlb = ((be - 1.0f) != 0.0f ? logf(1.0f - s) : 0.0f) + psab - psb;  // d lp / d beta
-        const float deb = (ab - 2.0f) * tab - (be - 1.0f) * tb;                         // d ent / d beta
-        GG[row * LDG + ai] = (g_logp * dla + g_ent * dea) * softplus_d(pa);
-        GG[row * LDG + A + ai] = (g_logp * dlb + g_ent * deb) * softplus_d(pbv);
-      }
-    } else {
-      // pass 1: per (row, action) log-prob / entropy terms and derivative pieces
-      for (int idx = tid; idx < R * A; idx += 256) {
-        const int row = idx / A, ai = idx - row * A;
-        const bool valid = m0 + row < a.M;
-        float* it_ = ITM + idx * ITS;
-        if constexpr (LN) {
-          const float hi = P[K.hi], lo = P[K.lo];
-          const float pa = PRE[row * LDG + ai], pbv = PRE[row * LDG + A + ai];
-          const float al = softplusf_(pa) + 1.0f, be = softplusf_(pbv) + 1.0f;
-          const float av = valid ? ACTN[idx] : 0.5f * (hi + lo);
-          float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
-          s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
-          const float ab = al + be;
-          float lga, lgb, lgab, psa, psb, psab, ta, tb, tab;
-          lgamma_digamma_trigamma(al, lga, psa, ta);
-          lgamma_digamma_trigamma(be, lgb, psb, tb);
-          lgamma_digamma_trigamma(ab, lgab, psab, tab);
-          it_[0] = xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
-          it_[1] = (lga + lgb) - lgab - (2.0f - ab) * psab - ((al - 1.0f) * psa + (be - 1.0f) * psb);
-          it_[2] = ((al - 1.0f) != 0.0f ? logf(s) : 0.0f) + psab - psa;            // d lp / d alpha
-          it_[3] = (ab - 2.0f) * tab - (al - 1.0f) * ta;                            // d ent / d alpha
-          it_[4] = softplus_d(pa);
-          it_[5] = ((be - 1.0f) != 0.0f ? logf(1.0f - s) : 0.0f) + psab - psb;     // d lp / d beta
-          it_[6] = (ab - 2.0f) * tab - (be - 1.0f) * tb;                            // d ent / d beta
-          it_[7] = softplus_d(pbv);
-        } else {
-          const float mu = PRE[row * LDG + ai];
-          const float sd = expf(P[K.logstd + ai]);
-          const float var = sd * sd, lsd = logf(sd);
-          const float act = valid ? ACTN[idx] : mu;
-          const float d = act - mu;
-          it_[0] = -(d * d) / (2.0f * var) - lsd - kLz;
-          it_[1] = kEntC + lsd;
-          it_[2] = d / var;
-          it_[3] = d * d / var - 1.0f;
-        }
-      }
-      lds_barrier();
-      // per row: log-prob / entropy sums, clipped surrogate, d loss / d logp, d loss / d ent
-      if (tid < R) {
-        const bool valid = m0 + tid < a.M;
-        float lp = 0.f, ent = 0.f;
-        for (int ai = 0; ai < A; ++ai) {
-          lp += ITM[(tid * A + ai) * ITS + 0];
-          ent += ITM[(tid * A + ai) * ITS + 1];
-        }
-        const float oldlp = valid ? ROWS[tid * 8 + 1] : lp;
-        const float logratio = lp - oldlp;
-        const float ratio = expf(logratio);
-        float an = valid ? ROWS[tid * 8 + 2] : 0.f;
-        if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
-        const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
-        const float pg1 = -an * ratio, pg2 = -an * rc;
-        const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
-        const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
-        float g_logp = a.inv_m * (w1 * (-an) + (1.0f - w1) * (-an) * inr) * ratio;
-        float g_ent = -a.ent_coef * a.inv_m;
-        st_a = fmaxf(pg1, pg2);
-        st_c = ent;
-        st_d = -logratio;
-        st_e = (ratio - 1.0f) - logratio;
-        st_f = fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
-        if (!valid) { g_logp = 0.f; g_ent = 0.f; st_a = st_c = st_d = st_e = st_f = 0.f; }
-        ROWS[tid * 8 + 3] = g_logp;
-        ROWS[tid * 8 + 4] = g_ent;
-      }
-      lds_barrier();
-      // pass 2: head gradients
-      for (int idx = tid; idx < R * A; idx += 256) {
-        const int row = idx / A, ai = idx - row * A;
-        const float g_logp = ROWS[row * 8 + 3], g_ent = ROWS[row * 8 + 4];
-        float* it_ = ITM + idx * ITS;
-        if constexpr (LN) {
-          GG[row * LDG + ai] = (g_logp * it_[2] + g_ent * it_[3]) * it_[4];
-          GG[row * LDG + A + ai] = (g_logp * it_[5] + g_ent * it_[6]) * it_[7];
-        } else {
-          GG[row * LDG + ai] = g_logp * it_[2];
-          it_[4] = g_logp * it_[3] + g_ent;  // d loss / d logstd (per row)
-        }
-      }
-    }
-    // loss statistics: summed per lane over the tiles, reduced across lanes and waves once after
-    // the tile loop (reported values only, no gradient depends on them)
-    lst[0] += st_a; lst[1] += st_b; lst[2] += st_c; lst[3] += st_d; lst[4] += st_e; lst[5] += st_f;
+    upd_loss<LN, R, ITS, LDG>(a, trunk, tid, m0, c, adv_mean, adv_std, PRE, GG, ROWS, ACTN, ITM, lst);
     lds_barrier();
     PPO_STAMP(7);
     // head bias (and logstd) gradients: fixed-order sums over the workgroup's rows
@@ -1668,139 +1680,7 @@ PPO_DEV void upd32_body(const UpdArgs& a) {
 
     // ---------------- loss and its gradient wrt the head pre-activations (k_upd's) ----------------
     float* ITM = SCR;
-    float st_a = 0.f, st_b = 0.f, st_c = 0.f, st_d = 0.f, st_e = 0.f, st_f = 0.f;
-    if (trunk == 0) {
-      if (tid < R) {
-        const bool valid = m0 + tid < a.M;
-        const float v = PRE[tid * LDG];
-        const float rt_ = ROWS[tid * 8 + 1], ov = ROWS[tid * 8 + 2];
-        float gv, sv;
-        if (a.clip_vloss) {
-          const float vu = (v - rt_) * (v - rt_);
-          const float dv = v - ov;
-          const float vcl = ov + fminf(fmaxf(dv, -c), c);
-          const float vc = (vcl - rt_) * (vcl - rt_);
-          sv = fmaxf(vu, vc);
-          const float w1 = vu > vc ? 1.0f : (vu == vc ? 0.5f : 0.0f);
-          const float inr = (dv >= -c && dv <= c) ? 1.0f : 0.0f;
-          gv = 0.5f * a.vf_coef * a.inv_m * (w1 * 2.0f * (v - rt_) + (1.0f - w1) * 2.0f * (vcl - rt_) * inr);
-        } else {
-          sv = (v - rt_) * (v - rt_);
-          gv = 0.5f * a.vf_coef * a.inv_m * 2.0f * (v - rt_);
-        }
-        if (!valid) { gv = 0.f; sv = 0.f; }
-        GG[tid * LDG] = gv;
-        st_b = sv;
-      }
-    } else if (A <= 8) {
-      const int row = tid >> 3, ai = tid & 7;
-      const bool item = ai < A;
-      const bool valid = m0 + row < a.M;
-      const int ac = item ? ai : 0;
-      const float hi = P[K.hi], lo = P[K.lo];
-      const float pa = PRE[row * LDG + ac], pbv = PRE[row * LDG + A + ac];
-      const float al = softplusf_(pa) + 1.0f, be = softplusf_(pbv) + 1.0f;
-      const float av = valid ? ACTN[row * A + ac] : 0.5f * (hi + lo);
-      float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
-      s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
-      const float ab = al + be;
-      float lga, lgb, lgab, psa, psb, psab, ta, tb, tab;
-      lgamma_digamma_trigamma(al, lga, psa, ta);
-      lgamma_digamma_trigamma(be, lgb, psb, tb);
-      lgamma_digamma_trigamma(ab, lgab, psab, tab);
-      const float lpi = xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
-      const float eni = (lga + lgb) - lgab - (2.0f - ab) * psab - ((al - 1.0f) * psa + (be - 1.0f) * psb);
-      const float lp = group8_sum(item ? lpi : 0.0f), ent = group8_sum(item ? eni : 0.0f);
-      const float oldlp = valid ? ROWS[row * 8 + 1] : lp;
-      const float logratio = lp - oldlp;
-      const float ratio = expf(logratio);
-      float an = valid ? ROWS[row * 8 + 2] : 0.f;
-      if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
-      const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
-      const float pg1 = -an * ratio, pg2 = -an * rc;
-      const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
-      const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
-      float g_logp = a.inv_m * (w1 * (-an) + (1.0f - w1) * (-an) * inr) * ratio;
-      float g_ent = -a.ent_coef * a.inv_m;
-      if (!valid) { g_logp = 0.f; g_ent = 0.f; }
-      if (ai == 0 && valid) {
-        st_a = fmaxf(pg1, pg2);
-        st_c = ent;
-        st_d = -logratio;
-        st_e = (ratio - 1.0f) - logratio;
-        st_f = fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
-      }
-      if (item) {
-        const float dla = ((al - 1.0f) != 0.0f ? logf(s) : 0.0f) + psab - psa;
-        const float dea = (ab - 2.0f) * tab - (al - 1.0f) * ta;
-        const float dlb = ((be - 1.0f) != 0.0f ? logf(1.0f - s) : 0.0f) + psab - psb;
-        const float deb = (ab - 2.0f) * tab - (be - 1.0f) * tb;
-        GG[row * LDG + ai] = (g_logp * dla + g_ent * dea) * softplus_d(pa);
-        GG[row * LDG + A + ai] = (g_logp * dlb + g_ent * deb) * softplus_d(pbv);
-      }
-    } else {
-      for (int idx = tid; idx < R * A; idx += 256) {
-        const int row = idx / A, ai = idx - row * A;
-        const bool valid = m0 + row < a.M;
-        float* it_ = ITM + idx * ITS;
-        const float hi = P[K.hi], lo = P[K.lo];
-        const float pa = PRE[row * LDG + ai], pbv = PRE[row * LDG + A + ai];
-        const float al = softplusf_(pa) + 1.0f, be = softplusf_(pbv) + 1.0f;
-        const float av = valid ? ACTN[idx] : 0.5f * (hi + lo);
-        float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
-        s = fminf(fmaxf(s, 1e-7f), 1.0f + 1e-7f);
-        const float ab = al + be;
-        float lga, lgb, lgab, psa, psb, psab, ta, tb, tab;
-        lgamma_digamma_trigamma(al, lga, psa, ta);
-        lgamma_digamma_trigamma(be, lgb, psb, tb);
-        lgamma_digamma_trigamma(ab, lgab, psab, tab);
-        it_[0] = xlogyf_(al - 1.0f, s) + xlogyf_(be - 1.0f, 1.0f - s) + (lgab - (lga + lgb));
-        it_[1] = (lga + lgb) - lgab - (2.0f - ab) * psab - ((al - 1.0f) * psa + (be - 1.0f) * psb);
-        it_[2] = ((al - 1.0f) != 0.0f ? logf(s) : 0.0f) + psab - psa;
-        it_[3] = (ab - 2.0f) * tab - (al - 1.0f) * ta;
-        it_[4] = softplus_d(pa);
-        it_[5] = ((be - 1.0f) != 0.0f ? logf(1.0f - s) : 0.0f) + psab - psb;
-        it_[6] = (ab - 2.0f) * tab - (be - 1.0f) * tb;
-        it_[7] = softplus_d(pbv);
-      }
-      lds_barrier();
-      if (tid < R) {
-        const bool valid = m0 + tid < a.M;
-        float lp = 0.f, ent = 0.f;
-        for (int ai = 0; ai < A; ++ai) {
-          lp += ITM[(tid * A + ai) * ITS + 0];
-          ent += ITM[(tid * A + ai) * ITS + 1];
-        }
-        const float oldlp = valid ? ROWS[tid * 8 + 1] : lp;
-        const float logratio = lp - oldlp;
-        const float ratio = expf(logratio);
-        float an = valid ? ROWS[tid * 8 + 2] : 0.f;
-        if (a.norm_adv) an = (an - adv_mean) / (adv_std + 1e-8f);
-        const float rc = fminf(fmaxf(ratio, 1.0f - c), 1.0f + c);
-        const float pg1 = -an * ratio, pg2 = -an * rc;
-        const float w1 = pg1 > pg2 ? 1.0f : (pg1 == pg2 ? 0.5f : 0.0f);
-        const float inr = (ratio >= 1.0f - c && ratio <= 1.0f + c) ? 1.0f : 0.0f;
-        float g_logp = a.inv_m * (w1 * (-an) + (1.0f - w1) * (-an) * inr) * ratio;
-        float g_ent = -a.ent_coef * a.inv_m;
-        st_a = fmaxf(pg1, pg2);
-        st_c = ent;
-        st_d = -logratio;
-        st_e = (ratio - 1.0f) - logratio;
-        st_f = fabsf(ratio - 1.0f) > c ? 1.0f : 0.0f;
-        if (!valid) { g_logp = 0.f; g_ent = 0.f; st_a = st_c = st_d = st_e = st_f = 0.f; }
-        ROWS[tid * 8 + 3] = g_logp;
-        ROWS[tid * 8 + 4] = g_ent;
-      }
-      lds_barrier();
-      for (int idx = tid; idx < R * A; idx += 256) {
-        const int row = idx / A, ai = idx - row * A;
-        const float g_logp = ROWS[row * 8 + 3], g_ent = ROWS[row * 8 + 4];
-        float* it_ = ITM + idx * ITS;
-        GG[row * LDG + ai] = (g_logp * it_[2] + g_ent * it_[3]) * it_[4];
-        GG[row * LDG + A + ai] = (g_logp * it_[5] + g_ent * it_[6]) * it_[7];
-      }
-    }
-    lst[0] += st_a; lst[1] += st_b; lst[2] += st_c; lst[3] += st_d; lst[4] += st_e; lst[5] += st_f;
+    upd_loss<true, R, ITS, LDG>(a, trunk, tid, m0, c, adv_mean, adv_std, PRE, GG, ROWS, ACTN, ITM, lst);
     lds_barrier();
     PPO_STAMP(7);
     if (tid < nh) {

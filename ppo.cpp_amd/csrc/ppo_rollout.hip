@@ -1212,7 +1212,7 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
   constexpr int NSL = 8 * R * 4;
   const int sg = tid & 3, sr = (tid >> 2) & (R - 1), sow = tid / (4 * R);
   // LayerNorm of the layer outputs in ZL (k_act3 act_activate's statistics, bitwise): mean and
-  // 1 / std of row r, every thread; 3 barriers
+  // 1 / std of row r, every thread; 2 barriers
   auto ln_stats = [&](float (&mu)[R], float (&rs)[R]) {
     f4 va = f4{0.f, 0.f, 0.f, 0.f}, vb = va;
     if (tid < NSL) {
@@ -1252,7 +1252,8 @@ __global__ __launch_bounds__(kRVThreads) void k_rollout_v(RolloutArgs a) {
       for (int w = 0; w < kActWaves; ++w) v += RS[(8 + w) * R + r];
       rs[r] = 1.0f / sqrtf(__fmaf_rn(v, 1.0f / 256, 1e-5f));
     }
-    lds_barrier();  // RS is reused by the next statistics
+    // no barrier for RS's reuse: the next call writes the sums only after other barriers, and the
+    // squares only after its own first barrier, which every reader of these squares passes first
   };
   const int kl = lane & 15;  // this lane's position in its 16-lane row
   const float* xv = XV + rg * 64 + kl * 4;

@@ -10,8 +10,11 @@
 //    critic is not on this chain: the value of step t depends only on obs[t], so it is computed
 //    afterwards for all T x E stored rows at once (k_values).
 //  * k_values: the critic forward of n stored rows; the critic's weights resident in registers
-//    the same way, workgroups walk 16-row blocks.
-// Both use the building blocks of k_act3 (ppo_act_common.hpp) in the same order: every action,
+//    the same way, workgroups walk 32- / 64-row blocks.
+//  * k_rollout_v (AC agent, E <= 512): 2 envs per workgroup on the VALU, each layer output one
+//    fmaf chain in the MFMA's k order, so bitwise k_rollout's results.
+//  * k_rollout4 / k_values4: the same for the 64-wide PPO agent (k_act4's arithmetic).
+// They use the building blocks of k_act3 (ppo_act_common.hpp) in the same order: every action,
 // log-prob, value, reward and observation is bitwise the one the per-step path produces
 // (tests/test_gpu_rollout.py).
 #include "ppo_act_common.hpp"

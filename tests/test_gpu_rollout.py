@@ -35,9 +35,9 @@ def snapshot(tr):
                                                   ("ppo", "HalfCheetah-v5", 37, 9),
                                                   ("ppo", "Hopper-v5", 20, 2), ("ppo", "Humanoid-v4", 40, 2)])
 def test_persistent_rollout_bitwise_equals_per_step(agent, env_id, E, iters):
-    """AC agent: the persistent rollout (k_rollout_v, the VALU form with 2 / 4 envs per workgroup, at
-    E <= 1024 and O <= 32 — E = 200 / 37 / 998 here; k_rollout, 16 envs per workgroup on MFMA, for
-    Ant's O = 105) + k_values vs k_act3 + k_synth_step. PPO agent: k_rollout4 + k_values4 vs
+    """AC agent: the persistent rollout (k_rollout_v, the VALU form with 2 envs per workgroup, at
+    E <= 512 and O <= 32 — E = 200 / 37 here; k_rollout, 16 envs per workgroup on MFMA, at E = 998
+    and for Ant's O = 105) + k_values vs k_act3 + k_synth_step. PPO agent: k_rollout4 + k_values4 vs
     k_act4 (act_kernel=4) + k_synth_step(_wide), with the PPO wrapper chain (ppo:41-49) fused into
     both (Humanoid: O = 376, A = 17, two head tiles, actions clipped to [-0.4, 0.4])."""
     T = 128
@@ -94,6 +94,36 @@ def test_valu_rollout_bitwise_equals_mfma_rollout(env_id, E):
             np.testing.assert_array_equal(snaps[0][k], snaps[1][k], err_msg=f"iteration {it}: {k}")
         assert trs[0].env.episode_stats() == trs[1].env.episode_stats()
         np.testing.assert_array_equal(trs[0].agent.params(), trs[1].agent.params())
+    for tr in trs:
+        tr.close()
+
+
+def test_valu_rollout_bitwise_across_episode_ends():
+    """The VALU rollout against the MFMA rollout over 1 152 steps per env (9 iterations of 128; the
+    synthetic env truncates at 1 000 steps), so every env's autoreset branch (Philox reset of the
+    state, episode bookkeeping) runs inside k_rollout_v: stored buffers, env state, episode
+    statistics and parameters bitwise equal after every iteration."""
+    E, T = 64, 128
+    cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=E, num_steps=T, num_minibatches=2,
+                              update_epochs=1, total_timesteps=E * T * 9)
+    trs = [ppo_amd.Trainer(cfg, options="rollout_kernel=valu"), ppo_amd.Trainer(cfg, options="rollout_kernel=mfma")]
+    finished = 0.0
+    for it in range(9):
+        snaps = []
+        for tr in trs:
+            tr.rollout()
+            tr.agent.sync()
+            snaps.append(snapshot(tr))
+            tr.agent.compute_gae(tr.next_obs, tr.next_done)
+            tr.agent.update(tr.lr_now(), want_stats=False)
+            tr.iteration += 1
+        for k in snaps[0]:
+            np.testing.assert_array_equal(snaps[0][k], snaps[1][k], err_msg=f"iteration {it}: {k}")
+        st = [tr.env.episode_stats() for tr in trs]  # (return sum, length sum, count); read-out resets them
+        assert st[0] == st[1]
+        finished += st[0][2]
+        np.testing.assert_array_equal(trs[0].agent.params(), trs[1].agent.params())
+    assert finished == E  # every env finished one episode (and was reset) inside the rollout
     for tr in trs:
         tr.close()
 

@@ -226,12 +226,16 @@ def main():
         raise SystemExit(f"bench.py: rank {rank} asked for device {device} but its context is on {dev_ord}")
     devices = [(dev_ord, dev_bus)]
     if world > 1:
-        devices = [None] * world
-        dist.all_gather_object(devices, (dev_ord, dev_bus))
-        buses = [b for _, b in devices]
-        if args.comm == "rccl" and len(set(buses)) != world:
-            raise SystemExit(f"bench.py: ranks share a GPU under RCCL (PCI bus ids {buses}); one GPU per rank "
-                             f"is required")
+        import socket
+        hosts = [None] * world
+        dist.all_gather_object(hosts, (socket.gethostname(), dev_ord, dev_bus))
+        devices = [(d, b) for _, d, b in hosts]
+        # bus ids repeat across hosts (local rank 0 of every node is usually the same bus): a shared GPU
+        # is the same (host, bus) pair
+        shared = [hb for hb in set((h, b) for h, _, b in hosts) if sum((h, b) == hb for h, _, b in hosts) > 1]
+        if args.comm == "rccl" and shared:
+            raise SystemExit(f"bench.py: ranks share a GPU under RCCL ((host, PCI bus id) {sorted(shared)}); one GPU "
+                             f"per rank is required")
     if world > 1:
         if args.comm == "host":
             import torch

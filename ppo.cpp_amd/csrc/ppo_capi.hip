@@ -278,11 +278,11 @@ struct CreateOptions {
   int dw_rows = 0;     // dW split-K rows per chunk (multiple of 16; 0: auto, ~128 chunks per trunk)
   int dw_slices = 0;   // k_dwf output slices per chunk (1 / 2; 0: auto, dw_slices())
   int dw_dma = 1;      // 1 (default): k_dwf_dma (LDS-DMA staging, three stage buffers); 0: k_dwf
-  // 1: ppo_update replays its minibatch launches as one captured hipGraph; 0 (default): eager. Not the
-  // default: a checkpoint snapshot's cross-stream wait (ppo_snapshot_state) then fails on this stack
+  // 1: ppo_update replays its minibatch launches as one captured hipGraph; 0 (default): eager.
+  // Snapshots work with it on (ppo_read_snapshot waits for the snapshot's event on the host).
   int update_graph = 0;
   int rollout_kernel = 0;  // 0 auto, 1 mfma (k_rollout), 2 valu (k_rollout_v)
-  int upd2_split = -1;  // -1 auto (wide inputs: k_l1g + split k_upd2), 0 one k_upd2, 2 / 3 split at 2 / 3 workgroups per CU
+  int upd2_split = -1;  // -1 auto (= kUpd2SplitAuto: the single k_upd2), 0 one k_upd2, 2 / 3 split at 2 / 3 workgroups per CU
   int upd_mfma = 0;     // 0 auto, 16: k_upd (16x16x4 MFMAs), 32: k_upd32 (32x32x2; LayerNorm-Beta agent, H = 256),
                         // 1: k_upd32's mixed form (critic 32x32x2, actor 16x16x4)
 };
@@ -383,6 +383,10 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   c->gradstep = opt.gradstep;
   c->update_graph = opt.update_graph;
   c->rollout_kernel = opt.rollout_kernel;
+  if (opt.rollout_kernel == 2 && (cfg->net_kind != PPO_NET_LN_BETA || c->K.OP > 32)) {
+    delete c;  // nothing allocated yet
+    return fail("ppo_create: rollout_kernel=valu needs the LayerNorm-Beta agent with obs_dim <= 32");
+  }
   int upd_kernel = opt.upd_kernel;
 #ifdef PPO_DIAG
   {
@@ -439,12 +443,12 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
     const bool fits32 = (double)B * (double)std::max(O, A) * 4.0 < 4294967040.0;
     const int split = !fits32 ? 0 : opt.upd2_split >= 0 ? opt.upd2_split : upd2_split_supported(c->K) ? kUpd2SplitAuto : 0;
     if ((opt.upd_mfma == 32 || opt.upd_mfma == 1) && (H != 256 || cfg->net_kind != PPO_NET_LN_BETA)) {
-      delete c;
+      ppo_destroy(c);
       return fail("ppo_create: upd_mfma=32 / mix needs the LayerNorm-Beta agent at hidden 256");
     }
-    if (opt.upd2_split > 0 && (upd_kernel || !upd2_split_supported(c->K))) {
-      delete c;
-      return fail("ppo_create: upd2_split needs the 64-wide agent with O % 4 == 0 and OP = 384");
+    if (opt.upd2_split > 0 && (upd_kernel || !fits32 || !upd2_split_supported(c->K))) {
+      ppo_destroy(c);
+      return fail("ppo_create: upd2_split needs the 64-wide agent with O % 4 == 0, OP = 384 and 32-bit storage offsets");
     }
     if (!upd_kernel && fits32 && upd2_supported(c->K, &c->upd, split) == 0) {
       c->use_upd = c->use_upd2 = true;
@@ -455,7 +459,7 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
     } else if (opt.upd_mfma == 32 || opt.upd_mfma == 1) {
       c->upd32_mix = opt.upd_mfma == 1;
       if (upd_kernel || upd32_supported(c->K, c->sg[1].nh, c->sg[0].size, c->sg[1].size, &c->upd, c->upd32_mix) != 0) {
-        delete c;
+        ppo_destroy(c);
         return fail("ppo_create: upd_mfma=32 / mix needs the LayerNorm-Beta agent at hidden 256");
       }
       c->use_upd = c->use_upd32 = true;
@@ -1437,7 +1441,10 @@ extern "C" int ppo_rollout_synth(ppo_t* c, psyn_t* env, float* next_obs, float* 
     }
     {
       ProfScope ps(c, PK_ROLLOUT, c->stream);
-      if (launch_rollout(r, c->stream) != 0) return fail("ppo_rollout_synth: rollout kernel launch failed");
+      if (const int lrc = launch_rollout(r, c->stream))
+        return fail(lrc == -3 ? "ppo_rollout_synth: rollout_kernel=valu needs the LayerNorm-Beta agent, O <= 32 and no "
+                                "device env wrappers"
+                              : "ppo_rollout_synth: rollout kernel launch failed");
       if (r.s_beta) launch_beta_logp(r.s_beta, c->buf[PPO_BUF_LOGPROBS], (long)E * c->cfg.num_steps, c->K.A, c->stream);
     }
     ValuesArgs v;

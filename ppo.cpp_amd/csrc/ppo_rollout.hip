@@ -1550,7 +1550,7 @@ static int launch_rollout_t(const RolloutArgs& a, hipStream_t s) {
   static const bool ok = hipFuncSetAttribute((const void*)k_rollout<NTO, NHT>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
   if (!ok) return -2;
-  hipLaunchKernelGGL((k_rollout<NTO, NHT>), dim3((a.E + kRows - 1) / kRows), dim3(kRVThreads), lds, s, a);
+  hipLaunchKernelGGL((k_rollout<NTO, NHT>), dim3((a.E + kRows - 1) / kRows), dim3(kActThreads), lds, s, a);
   return 0;
 }
 
@@ -1573,6 +1573,8 @@ static bool use_rollout_v(const RolloutArgs& a) {
 
 int launch_rollout(const RolloutArgs& a, hipStream_t s) {
   if (rollout_supported(a.K) != 0) return -1;
+  // an explicit rollout_kernel=valu that cannot apply is an error, not a silent k_rollout
+  if (a.variant == 2 && !use_rollout_v(a)) return -3;
   if (use_rollout_v(a)) return a.K.OP == 16 ? launch_rollout_v_t<1>(a, s) : launch_rollout_v_t<2>(a, s);
   if (a.K.kind == PPO_NET_TANH_NORMAL) {
     const int nht = (a.K.A + 15) / 16;

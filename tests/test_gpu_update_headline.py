@@ -172,3 +172,21 @@ def test_upd32_matches_upd(O_, A, E, opt32):
 def test_upd32_refused_for_the_ppo_agent():
     with pytest.raises(ppo_amd.PPOError, match="upd_mfma=32"):
         make_agent(0, 17, 6, 64, 64, options="upd_mfma=32")
+
+
+def test_refused_options_free_the_context():
+    """A create refused for an option that cannot apply (upd_mfma=32 / upd2_split on the wrong agent)
+    releases every device buffer it had allocated (the refusal paths used to `delete`
+    the context after its stream and buffers existed). Device memory must not grow over repeated
+    refusals at a metric-sized batch; rollout_kernel=valu on the PPO agent is refused up front."""
+    import torch
+    free0 = torch.cuda.mem_get_info(0)[0]
+    for _ in range(6):
+        with pytest.raises(ppo_amd.PPOError, match="upd_mfma=32"):
+            make_agent(0, 17, 6, 64, 4096, T=128, MB=4, options="upd_mfma=32")
+        with pytest.raises(ppo_amd.PPOError, match="upd2_split"):
+            make_agent(1, 17, 6, 256, 4096, T=128, MB=4, options="upd2_split=2")
+    free1 = torch.cuda.mem_get_info(0)[0]
+    assert free0 - free1 < 64 << 20, (free0, free1)
+    with pytest.raises(ppo_amd.PPOError, match="rollout_kernel=valu"):
+        make_agent(0, 17, 6, 64, 64, options="rollout_kernel=valu")

@@ -137,7 +137,10 @@ int ppo_get_value(ppo_t* ctx, int n, const float* x_dev, float* value_dev, void*
 int ppo_rollout_act(ppo_t* ctx, int step, int env_begin, int env_end, const float* next_obs_dev,
                     const float* next_done_dev, float* action_out_dev, void* stream);
 int ppo_rollout_reward(ppo_t* ctx, int step, int env_begin, int env_end, const float* reward_dev, void* stream);
-/* GAE over steps [0, num_steps_collected) using next_obs/next_done after the last step. */
+/* GAE over steps [0, num_steps_collected) using next_obs/next_done after the last step (ac:759-779).
+ * num_steps_collected < num_steps (DD-PPO preemption): the last collected step is bootstrapped from
+ * the stored step num_steps_collected (values / dones), as the reference's loop does; next_obs and
+ * next_done are then unused. */
 int ppo_compute_gae(ppo_t* ctx, const float* next_obs_dev, const float* next_done_dev, int num_steps_collected,
                     void* stream);
 /* GAE with a caller-supplied bootstrap value next_value[E] (skips the critic call). */
@@ -148,6 +151,13 @@ int ppo_gae_from_values(ppo_t* ctx, const float* next_value_dev, const float* ne
  * counter used by the rollout RNG. perms_dev (optional, int32 [epochs][T*E]) overrides the
  * Philox/Feistel minibatch permutation (tests inject the reference's randperm). */
 int ppo_update(ppo_t* ctx, float lr, const int32_t* perms_dev, ppo_update_stats* stats);
+/* ppo_update over a partial collection (DD-PPO preemption, ac:803-810): the first
+ * num_steps_collected steps of every env are the samples; each epoch's permutation runs over those
+ * num_steps_collected * E samples and is repeated and truncated to T * E (b_inds.repeat(...)[:B]),
+ * so the minibatch count and size are those of a full collection. GAE for such a collection:
+ * ppo_compute_gae with the same step count, which bootstraps from the stored step
+ * num_steps_collected as the reference does (ac:765-774). ppo_update = ppo_update_ex(..., T, ...). */
+int ppo_update_ex(ppo_t* ctx, float lr, int num_steps_collected, const int32_t* perms_dev, ppo_update_stats* stats);
 int ppo_sync(ppo_t* ctx);
 /* test hook: raw (pre-clip, post all-reduce) gradient of the last minibatch, flat reference order */
 int ppo_debug_last_grad(ppo_t* ctx, float* host, long n);

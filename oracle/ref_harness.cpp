@@ -686,7 +686,7 @@ struct VecWrap {
 // ---------------------------------------------------------------------------------------------
 template <typename AgentT>
 static void e2e_case(const std::string& cname, AgentT& agent, int kind, int E, int T, int MB, int EP, int NIT,
-                     float lr0, const LossCfg& c, uint32_t base, bool wrappers = false) {
+                     float lr0, const LossCfg& c, uint32_t base, bool wrappers = false, bool teacher = false) {
   const int O = 17, A = 6;
   std::string names;
   hash_params(*agent, base, 1.0f, -1.0f, names);
@@ -708,7 +708,17 @@ static void e2e_case(const std::string& cname, AgentT& agent, int kind, int E, i
   Tensor next_done = torch::zeros({E});
   const long B = (long)E * T, M = B / MB;
   std::vector<float> stats;   // per iteration: pg, v, ent, old_kl, kl (last minibatch), clipfrac (mean), ret_sum, n_ep
+  // teacher forcing (verdict r04 item 1): the state every iteration starts from (parameters and Adam
+  // moments for it >= 1), the rollout it collects, and its last minibatch's pre-clip gradient and
+  // total norm, so the GPU trainer can run each iteration from the replay's own state
+  std::vector<Tensor> tf_p, tf_m, tf_v, tf_obs, tf_act, tf_lp, tf_rew, tf_done, tf_val, tf_nv, tf_nd, tf_grad;
+  std::vector<float> tf_gn;
   for (int it = 0; it < NIT; ++it) {
+    if (teacher && it > 0) {
+      tf_p.push_back(flat_params(*agent));
+      tf_m.push_back(flat_state(opt, false));
+      tf_v.push_back(flat_state(opt, true));
+    }
     const float frac = 1.0f - static_cast<float>(it) / static_cast<float>(NIT);
     const float lrnow = frac * lr0;
     static_cast<torch::optim::AdamOptions&>(opt.param_groups()[0].options()).set_lr(lrnow);
@@ -773,6 +783,11 @@ static void e2e_case(const std::string& cname, AgentT& agent, int kind, int E, i
       else next_value = agent->critic->forward((next_obs - agent->mean_) / agent->std_).flatten();
     }
     auto [adv, ret] = gae_ref(rewards, values, dones, next_value, next_done, 0.99f, 0.95f);
+    if (teacher) {
+      tf_obs.push_back(obs.clone()); tf_act.push_back(actions.clone()); tf_lp.push_back(logprobs.clone());
+      tf_rew.push_back(rewards.clone()); tf_done.push_back(dones.clone()); tf_val.push_back(values.clone());
+      tf_nv.push_back(next_value.clone()); tf_nd.push_back(next_done.clone());
+    }
     if (const char* dbg = std::getenv("E2E_DEBUG_DIR")) {  // diagnostics: the rollout of every iteration
       const std::string pre = std::string(dbg) + "/" + cname + "_it" + std::to_string(it);
       for (auto& [nm, tt] : std::vector<std::pair<std::string, Tensor>>{{"actions", actions}, {"logprobs", logprobs},
@@ -816,7 +831,10 @@ static void e2e_case(const std::string& cname, AgentT& agent, int kind, int E, i
         auto& [loss, st] = res;
         opt.zero_grad();
         loss.backward();
-        torch::nn::utils::clip_grad_norm_(agent->parameters(), 0.5);
+        const bool last_mb = ep == EP - 1 && start + M >= B;
+        if (teacher && last_mb && (it & 1)) tf_grad.push_back(flat_grads(*agent));
+        const double tn = torch::nn::utils::clip_grad_norm_(agent->parameters(), 0.5);
+        if (teacher && last_mb) tf_gn.push_back((float)tn);
         opt.step();
         st_last = st;
         cf_sum += st[5];
@@ -834,6 +852,15 @@ static void e2e_case(const std::string& cname, AgentT& agent, int kind, int E, i
                         "\"old_approx_kl\", \"approx_kl\", \"clipfrac_mean\", \"episodic_return_sum\", \"episodes\"]}");
   dump(cname, "stats", torch::tensor(stats).view({NIT, 8}));
   dump(cname, "params_final", flat_params(*agent));
+  if (teacher) {  // tf_* [it] = iteration it (tf_params / tf_adam_*: iterations 1.., tf_grad: odd iterations)
+    dump(cname, "tf_params", torch::stack(tf_p)); dump(cname, "tf_adam_m", torch::stack(tf_m));
+    dump(cname, "tf_adam_v", torch::stack(tf_v));
+    dump(cname, "tf_obs", torch::stack(tf_obs)); dump(cname, "tf_actions", torch::stack(tf_act));
+    dump(cname, "tf_logprobs", torch::stack(tf_lp)); dump(cname, "tf_rewards", torch::stack(tf_rew));
+    dump(cname, "tf_dones", torch::stack(tf_done)); dump(cname, "tf_values", torch::stack(tf_val));
+    dump(cname, "tf_next_value", torch::stack(tf_nv)); dump(cname, "tf_next_done", torch::stack(tf_nd));
+    dump(cname, "tf_grad_last_mb", torch::stack(tf_grad)); dump(cname, "tf_grad_norm", torch::tensor(tf_gn));
+  }
   end_case();
 }
 
@@ -849,7 +876,7 @@ static void e2e_cases() {
   }
   {
     ACAgent agent(17, 6, 256, 1.0f, -1.0f, torch::zeros({17}), torch::ones({17}));
-    e2e_case("e2e_ac", agent, 1, E, T, MB, EP, NIT, 2.5e-4f, LossCfg{0.1f, 0.01f, 0.5f, true, true}, 3400);
+    e2e_case("e2e_ac", agent, 1, E, T, MB, EP, NIT, 2.5e-4f, LossCfg{0.1f, 0.01f, 0.5f, true, true}, 3400, false, true);
   }
 }
 

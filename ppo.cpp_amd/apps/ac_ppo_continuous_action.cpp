@@ -11,10 +11,24 @@
 // inference of one group overlaps the CPU env stepping of the others. Per-env trajectories are
 // identical to the reference's per-env threads (counter-based Philox sampling is independent of
 // grouping). --env_backend device runs the device-resident synthetic env instead (no PCIe).
+// --num_collect_groups 0 (default) = two groups per host thread, so one group's GPU round trip hides
+// under another's CPU stepping; --host_step_us gives the host env a per-step CPU cost (the MuJoCo
+// physics it stands in for), and each group's env stepping is a roctx range ("host_env_step"), so a
+// rocprofv3 --kernel-trace --marker-trace timeline shows the act kernels under the stepping.
+//
+// DD-PPO preemption (--use_dd_ppo_preempt 1, ac:568-583, :629, :680-693, :803-810): rank 0 serves the
+// TCP store (apps/tcp_store.h), every collection group has a client; a group stops collecting once
+// more than dd_ppo_preempt_threshold of all groups (over all ranks) are done and it is past
+// dd_ppo_min_perc of the steps. A group stands in for the reference's per-env thread: the store
+// counts finished groups. The update trains on the minimum step count over the groups, its
+// permutations repeated and truncated to the full batch (ppo_update_ex).
 //
 // Launch: one process per GPU with RANK / WORLD_SIZE / LOCAL_RANK (torchrun or any launcher) or
 // OMPI_COMM_WORLD_{RANK,SIZE,LOCAL_RANK} (mpirun); the RCCL id is exchanged through --rdzv_file.
 #include "trainer_common.h"
+#include "tcp_store.h"
+
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <atomic>
 #include <iomanip>
@@ -59,7 +73,9 @@ struct GlobalConfig {  // ac_ppo_continuous_action.cpp:55-148
   bool estimate_mean_std = false;
   // MI355X build additions
   std::string env_backend = "host";  // host | device
-  int num_collect_groups = 8;
+  int num_collect_groups = 0;        // 0: two per host thread
+  float host_step_us = 0.0f;         // host env: CPU time per env step (busy wait)
+  float straggler_us = 0.0f;         // host env: extra CPU time per env step for the last group (test knob)
   std::string rdzv_file = "";
   unsigned num_devices = 1, num_envs_per_device = 0, batch_size = 0, minibatch_size = 0, num_iterations = 0;
   unsigned batch_size_per_device = 0, minibatch_per_device = 0;
@@ -115,10 +131,12 @@ int main(int argc, const char** argv) {
   flags.add("dd_ppo_min_perc", "Percentage of envs that need to finish before preemtion.", &config.dd_ppo_min_perc);
   flags.add("dd_ppo_preempt_threshold", "Percentage of envs that need to finish before preemtion.",
             &config.dd_ppo_preempt_threshold);
-  flags.add("estimate_mean_std", "Estimate obs mean/std of env 0 (no-op here)", &config.estimate_mean_std);
+  flags.add("estimate_mean_std", "Print the mean / std of env 0's observations at the end", &config.estimate_mean_std);
   flags.add("env_backend", "host (gymcpp envs on the CPU) or device (synthetic env in HBM)", &config.env_backend);
-  flags.add("num_collect_groups", "host envs: number of async collection groups (threads + HIP streams)",
-            &config.num_collect_groups);
+  flags.add("num_collect_groups", "host envs: number of async collection groups (threads + HIP streams); 0: two "
+            "per host thread", &config.num_collect_groups);
+  flags.add("host_step_us", "host envs: CPU time burnt per env step (stands in for the physics)", &config.host_step_us);
+  flags.add("straggler_us", "host envs: extra CPU time per env step in the last collection group", &config.straggler_us);
   flags.add("rdzv_file", "file used to exchange the RCCL id between ranks", &config.rdzv_file);
   try {
     flags.parse(argc, argv);
@@ -130,8 +148,9 @@ int main(int argc, const char** argv) {
     flags.print_help(std::cerr);
     return 1;
   }
-  if (config.use_dd_ppo_preempt) {
-    std::cerr << "use_dd_ppo_preempt is not supported by this build (disabled in every reference config)\n";
+  if (config.use_dd_ppo_preempt && config.env_backend == "device") {
+    std::cerr << "use_dd_ppo_preempt needs host envs (--env_backend host): the device rollout has no per-env "
+                 "collection threads to preempt\n";
     return 1;
   }
   // derived fields (ac:398-407)
@@ -173,14 +192,31 @@ int main(int argc, const char** argv) {
 
   const int E = (int)config.num_envs_per_device, T = (int)config.num_steps;
   const bool device_env = config.env_backend == "device";
+  // DD-PPO store (ac:568-573): rank 0 serves it from before the communicator exists, so the other
+  // ranks' clients (created once every rank has joined) always find it
+  std::unique_ptr<TCPStoreServer> store_server;
+  if (config.use_dd_ppo_preempt && rank == 0) {
+    store_server = std::make_unique<TCPStoreServer>(config.rdzv_addr, config.tcp_store_port, (int)config.num_envs);
+    store_server->start();
+  }
   int O = 17, A = 6;
   float act_lo = -1.f, act_hi = 1.f;
   std::vector<std::shared_ptr<gymcpp::SeqVectorEnv>> envs;  // one SeqVectorEnv per env, as the reference
   if (!device_env) {
     try {
+      const int G0 = config.num_collect_groups > 0 ? config.num_collect_groups : 2 * host_threads();
+      const int Gs = std::max(1, std::min(G0, E));
       for (int i = 0; i < E; ++i) {
+        auto base = make_base_env(config.env_id);
+        // the last collection group (envs [E (G-1) / G, E)) carries the straggler cost
+        const float us = config.host_step_us + (i >= (long)E * (Gs - 1) / Gs ? config.straggler_us : 0.0f);
+        if (us > 0.0f) {
+          auto sc = std::dynamic_pointer_cast<gymcpp::SyntheticCheetah>(base);
+          if (!sc) throw std::invalid_argument("host_step_us / straggler_us apply to SyntheticCheetah-v0 only");
+          sc->set_step_cost_ns((int64_t)std::llround(us * 1000.0));
+        }
         std::vector<std::shared_ptr<gymcpp::EnvironmentWrapper>> arr{
-            std::make_shared<gymcpp::RecordEpisodeStatistics>(make_base_env(config.env_id))};
+            std::make_shared<gymcpp::RecordEpisodeStatistics>(base)};
         envs.push_back(std::make_shared<gymcpp::SeqVectorEnv>(arr, config.clip_actions));
       }
     } catch (const std::invalid_argument& e) {
@@ -285,7 +321,16 @@ int main(int argc, const char** argv) {
     HIPCHECK(hipMalloc(&d_rew, sizeof(float) * E));
     HIPCHECK(hipMemset(d_done, 0, sizeof(float) * E));
     float *h_obs = nullptr, *h_act = nullptr, *h_rew = nullptr, *h_done = nullptr;
-    const int G = std::max(1, std::min(config.num_collect_groups, E));
+    const int G = std::max(1, std::min(config.num_collect_groups > 0 ? config.num_collect_groups : 2 * host_threads(), E));
+    if (!device_env && rank == 0)
+      std::cout << "collection groups: " << G << " (" << host_threads() << " host threads)" << std::endl;
+    std::vector<std::unique_ptr<TCPStoreClient>> store_clients;  // one per group (ac:576-582: one per env thread)
+    if (config.use_dd_ppo_preempt)
+      for (int gi = 0; gi < G; ++gi)
+        store_clients.push_back(std::make_unique<TCPStoreClient>(config.rdzv_addr, config.tcp_store_port));
+    const long dd_min_steps = std::lround(config.dd_ppo_min_perc * static_cast<float>(config.num_steps));
+    const int dd_groups = G * world_size;  // every rank runs G groups
+    std::vector<float> obs_mean_std;       // env 0's observations (ac:663, estimate_mean_std)
     std::vector<hipStream_t> gstreams(G);
     if (device_env) {
       check(psyn_create(E, O, A, &denv), "psyn_create");
@@ -319,8 +364,27 @@ int main(int argc, const char** argv) {
         lrnow = frac * config.learning_rate;
       }
       double sum_r = 0, sum_l = 0, n_ep = 0;
+      int steps_collected = T;  // min over the collection groups (ac:703-707, :723)
+      if (config.use_dd_ppo_preempt) {
+        if (rank == 0) store_clients[0]->reset();  // ac:628-630
+        if (world_size > 1) {  // comm->allreduce(sychronize) (ac:631): every rank starts after the reset
+          HIPCHECK(hipMemsetAsync(d_stats, 0, sizeof(float), s));
+          check(ppo_comm_allreduce(agent, d_stats, 1, 0), "ppo_comm_allreduce");
+          HIPCHECK(hipStreamSynchronize(s));
+        }
+      }
       if (device_env) {
         check(ppo_rollout_synth(agent, denv, d_obs, d_done, d_act, d_rew), "ppo_rollout_synth");
+        if (config.estimate_mean_std) {  // env 0's next observation after every step: obs[1..T-1][0], next_obs[0]
+          const float* sobs = ppo_buffer(agent, PPO_BUF_OBS);
+          std::vector<float> o((size_t)T * O);
+          for (int t = 1; t < T; ++t)
+            HIPCHECK(hipMemcpyAsync(o.data() + (size_t)(t - 1) * O, sobs + (size_t)t * E * O, sizeof(float) * O,
+                                    hipMemcpyDeviceToHost, s));
+          HIPCHECK(hipMemcpyAsync(o.data() + (size_t)(T - 1) * O, d_obs, sizeof(float) * O, hipMemcpyDeviceToHost, s));
+          HIPCHECK(hipStreamSynchronize(s));
+          obs_mean_std.insert(obs_mean_std.end(), o.begin(), o.end());
+        }
         // episode sums read out behind the rollout, without a device-wide sync; collected after
         // the update has been enqueued (the values are those of this rollout)
         check(psyn_episode_stats_begin(denv, s), "psyn_episode_stats_begin");
@@ -328,20 +392,24 @@ int main(int argc, const char** argv) {
         // asynchronous collection: one host thread + HIP stream per env group
         std::vector<std::thread> th;
         std::vector<double> gr(G, 0), gl(G, 0), gn(G, 0);
+        std::vector<int> gsteps(G, T);
         std::atomic<int> failed{0};
         for (int gi = 0; gi < G; ++gi) {
           th.emplace_back([&, gi] {
             const int e0 = E * gi / G, e1 = E * (gi + 1) / G, n = e1 - e0;
             hipStream_t gs = gstreams[gi];
             try {
-              for (int step = 0; step < T; ++step) {
+              int step;
+              for (step = 0; step < T; ++step) {
                 check(ppo_rollout_act(agent, step, e0, e1, d_obs + (size_t)e0 * O, d_done + e0, d_act + (size_t)e0 * A, gs),
                       "ppo_rollout_act");
                 HIPCHECK(hipMemcpyAsync(h_act + (size_t)e0 * A, d_act + (size_t)e0 * A, sizeof(float) * n * A,
                                         hipMemcpyDeviceToHost, gs));
                 HIPCHECK(hipStreamSynchronize(gs));
+                roctxRangePushA("host_env_step");
                 for (int i = e0; i < e1; ++i) {
                   gymcpp::VecStep r = envs[i]->step(h_act + (size_t)i * A);
+                  if (i == 0 && config.estimate_mean_std) obs_mean_std.insert(obs_mean_std.end(), r.obs, r.obs + O);
                   std::copy(r.obs, r.obs + O, h_obs + (size_t)i * O);
                   h_rew[i] = r.rewards[0];
                   h_done[i] = (r.terminations[0] != 0.f || r.truncations[0] != 0.f) ? 1.f : 0.f;
@@ -351,13 +419,22 @@ int main(int argc, const char** argv) {
                     gn[gi] += 1;
                   }
                 }
+                roctxRangePop();
                 HIPCHECK(hipMemcpyAsync(d_rew + e0, h_rew + e0, sizeof(float) * n, hipMemcpyHostToDevice, gs));
                 check(ppo_rollout_reward(agent, step, e0, e1, d_rew + e0, gs), "ppo_rollout_reward");
                 HIPCHECK(hipMemcpyAsync(d_obs + (size_t)e0 * O, h_obs + (size_t)e0 * O, sizeof(float) * n * O,
                                         hipMemcpyHostToDevice, gs));
                 HIPCHECK(hipMemcpyAsync(d_done + e0, h_done + e0, sizeof(float) * n, hipMemcpyHostToDevice, gs));
+                if (config.use_dd_ppo_preempt) {  // ac:680-689 (the step just taken is stored, not trained on)
+                  const int num_done = store_clients[gi]->get();
+                  if (static_cast<float>(num_done) / static_cast<float>(dd_groups) > config.dd_ppo_preempt_threshold &&
+                      step > dd_min_steps)
+                    break;
+                }
               }
               HIPCHECK(hipStreamSynchronize(gs));
+              if (config.use_dd_ppo_preempt) store_clients[gi]->increment();  // ac:692-694
+              gsteps[gi] = step;
             } catch (const std::exception& e) {
               std::cerr << e.what() << std::endl;
               failed = 1;
@@ -366,10 +443,17 @@ int main(int argc, const char** argv) {
         }
         for (auto& t : th) t.join();
         if (failed) throw std::runtime_error("collection failed");
-        for (int gi = 0; gi < G; ++gi) { sum_r += gr[gi]; sum_l += gl[gi]; n_ep += gn[gi]; }
+        for (int gi = 0; gi < G; ++gi) {
+          sum_r += gr[gi]; sum_l += gl[gi]; n_ep += gn[gi];
+          steps_collected = std::min(steps_collected, gsteps[gi]);
+        }
+        if (steps_collected < T)
+          std::cout << "dd_ppo: rank " << rank << " trains on " << steps_collected << " of " << T
+                    << " steps per env (preempted)" << std::endl;
       }
-      check(ppo_compute_gae(agent, d_obs, d_done, T, s), "ppo_compute_gae");
-      check(ppo_update(agent, lrnow, nullptr, &st), "ppo_update");  // stats are rank-averaged inside
+      check(ppo_compute_gae(agent, d_obs, d_done, steps_collected, s), "ppo_compute_gae");
+      // a preempted collection: the permutations over the collected samples, repeated to the batch (ac:803-810)
+      check(ppo_update_ex(agent, lrnow, steps_collected, nullptr, &st), "ppo_update");  // stats rank-averaged inside
       if (device_env) {
         float r, l, n;
         check(psyn_episode_stats_end(denv, &r, &l, &n), "psyn_episode_stats_end");
@@ -417,6 +501,23 @@ int main(int argc, const char** argv) {
     }
     ckpt.finish();
     if (rank == 0) save_state(agent, exp_folder, "model_final.pth", "optimizer_final.pth", last_lr, config.adam_eps);
+    if (config.estimate_mean_std && !obs_mean_std.empty()) {  // ac:954-963: mean and population std of env 0's obs
+      const size_t n = obs_mean_std.size() / O;
+      std::vector<double> mu(O, 0.0), var(O, 0.0);
+      for (size_t k = 0; k < n; ++k)
+        for (int f = 0; f < O; ++f) mu[f] += obs_mean_std[k * O + f];
+      for (int f = 0; f < O; ++f) mu[f] /= (double)n;
+      for (size_t k = 0; k < n; ++k)
+        for (int f = 0; f < O; ++f) {
+          const double d = obs_mean_std[k * O + f] - mu[f];
+          var[f] += d * d;
+        }
+      std::cout << "Mean obs:\n";
+      for (int f = 0; f < O; ++f) std::cout << std::setprecision(6) << " " << (float)mu[f] << "\n";
+      std::cout << "[ CPUFloatType{" << O << "} ]\n\nStd obs:\n";
+      for (int f = 0; f < O; ++f) std::cout << " " << (float)std::sqrt(var[f] / (double)n) << "\n";
+      std::cout << "[ CPUFloatType{" << O << "} ]\n" << std::endl;
+    }
     // rank 0 evaluation with the Beta mean action on env 0 (ac:965-1001)
     if (rank == 0 && !device_env) {
       std::vector<float> episodic_returns;

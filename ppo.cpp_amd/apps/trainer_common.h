@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -375,6 +376,18 @@ inline std::shared_ptr<gymcpp::Environment> make_base_env(const std::string& env
                                 " needs MuJoCo 3.2.0, which this build does not link; use SyntheticCheetah-v0 "
                                 "or the device env (--env_backend device)");
   throw std::invalid_argument("env_id: " + env_id + " is not implemented.");
+}
+
+// Host threads this process may use: the launcher's thread budget (OMP_NUM_THREADS, set to the box's
+// CPU share), else the cgroup CPU quota, else the hardware concurrency.
+inline int host_threads() {
+  if (const char* v = std::getenv("OMP_NUM_THREADS"))
+    if (std::atoi(v) > 0) return std::atoi(v);
+  std::ifstream f("/sys/fs/cgroup/cpu.max");
+  std::string q, per;
+  if (f >> q >> per && q != "max" && std::atol(per.c_str()) > 0)
+    return std::max(1L, std::atol(q.c_str()) / std::atol(per.c_str()));
+  return std::max(1u, std::thread::hardware_concurrency());
 }
 
 inline double seconds_since(std::chrono::high_resolution_clock::time_point t0) {

@@ -745,6 +745,14 @@ extern "C" int ppo_gae_from_values(ppo_t* c, const float* next_value, const floa
 }
 
 static int gae_launch(ppo_t* c, const float* next_value, const float* next_done, int nsteps, hipStream_t s) {
+  // a partial collection (DD-PPO preemption, nsteps < num_steps): the reference's recurrence bootstraps
+  // the last collected step from the STORED step nsteps (values[t + 1], dones[t + 1] whenever
+  // t != num_steps - 1, ac:765-774), which every env executed before it stopped; next_value and
+  // next_done are not read then
+  if (nsteps < c->cfg.num_steps) {
+    next_value = c->buf[PPO_BUF_VALUES] + (size_t)nsteps * c->cfg.num_envs;
+    next_done = c->buf[PPO_BUF_DONES] + (size_t)nsteps * c->cfg.num_envs;
+  }
   GaeArgs g;
   g.rewards = c->buf[PPO_BUF_REWARDS];
   g.values = c->buf[PPO_BUF_VALUES];
@@ -791,6 +799,12 @@ static int allreduce(ppo_t* c, float* buf, long n, int average, hipStream_t s) {
 
 extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_update_stats* out) {
   if (!c) return fail("ppo_update: null ctx");
+  return ppo_update_ex(c, lr, c->cfg.num_steps, perms_dev, out);
+}
+
+extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perms_dev, ppo_update_stats* out) {
+  if (!c) return fail("ppo_update: null ctx");
+  if (nsteps <= 0 || nsteps > c->cfg.num_steps) return fail("ppo_update: bad collected step count");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
   const ppo_hip_config& cfg = c->cfg;
@@ -801,12 +815,22 @@ extern "C" int ppo_update(ppo_t* c, float lr, const int32_t* perms_dev, ppo_upda
     return fail("ppo_update: world_size " + std::to_string(cfg.world_size) +
                 " but no communicator attached (ppo_comm_init / ppo_comm_init_host)");
   // ---- permutations (torch::randperm per epoch, ppo:490 / ac:804) ----
+  // A partial collection of nsteps < num_steps (DD-PPO preemption, ac:803-810): the permutation runs
+  // over the Bc = nsteps * E collected samples (the first nsteps rows of the [T, E] storage) and is
+  // repeated and truncated to the per-device batch, b_inds.repeat(ceil(B / Bc))[:B]
   const int32_t* perms = perms_dev;
   if (!perms) {
     ProfScope ps(c, PK_PERM, s);
-    for (int e = 0; e < EP; ++e)
-      launch_perm(c->perms + (size_t)e * B, (uint32_t)B,
-                  make_perm_key(cfg.seed, c->rank, c->iteration * (long)EP + e, B), s);
+    const long Bc = (long)nsteps * cfg.num_envs;
+    for (int e = 0; e < EP; ++e) {
+      int32_t* dst = c->perms + (size_t)e * B;
+      launch_perm(dst, (uint32_t)Bc, make_perm_key(cfg.seed, c->rank, c->iteration * (long)EP + e, Bc), s);
+      for (long have = Bc; have < B;) {  // doubling copies of the periodic prefix
+        const long n = std::min(have, B - have);
+        HIP_TRY(hipMemcpyAsync(dst + have, dst, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+        have += n;
+      }
+    }
     perms = c->perms;
   }
   // ---- advantage statistics of every minibatch (ppo:511; distributed ac:833-846) ----

@@ -5,6 +5,7 @@
 // -ffp-contract=off), Philox4x32-10 reset noise keyed (seed, 0x5EED5EED), counter (resets, i).
 #pragma once
 
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <vector>
@@ -30,8 +31,14 @@ class SyntheticCheetah final : public Environment {
   std::vector<float> q_ = std::vector<float>(kO, 0.0f), nq_ = std::vector<float>(kO, 0.0f);
   uint32_t rseed_ = 1, rcount_ = 0;
   int elapsed_ = kMaxSteps + 1;
+  int64_t step_cost_ns_ = 0;
 
  public:
+  // Host CPU time each step() burns before it returns (a busy wait): stands in for the physics of the
+  // MuJoCo env this replaces ("per-step host cost configurable"), so the async
+  // collection's overlap of CPU stepping with GPU inference can be measured. 0: no cost.
+  void set_step_cost_ns(int64_t ns) { step_cost_ns_ = ns; }
+  int64_t step_cost_ns() const { return step_cost_ns_; }
   ObsView reset(int seed) override {
     if (seed > 0) { rseed_ = (uint32_t)seed; rcount_ = 0; }
     for (int i = 0; i < kO; ++i) {
@@ -45,6 +52,11 @@ class SyntheticCheetah final : public Environment {
     return ObsView{q_.data(), kO};
   }
   std::tuple<ObsView, float, bool, bool> step(const float* a) override {
+    if (step_cost_ns_ > 0) {
+      const auto until = std::chrono::steady_clock::now() + std::chrono::nanoseconds(step_cost_ns_);
+      while (std::chrono::steady_clock::now() < until) {
+      }
+    }
     const float xb = q_[0];
     for (int i = 0; i < kO; ++i) nq_[i] = std::fma(0.9f, q_[i], std::fma(0.1f, a[i % kA], 0.05f * q_[(i + 1) % kO]));
     q_.swap(nq_);

@@ -144,6 +144,7 @@ SYMBOLS = [
     ("ppo_compute_gae", _I, [_VP, _FP, _FP, _I, _VP]),
     ("ppo_gae_from_values", _I, [_VP, _FP, _FP, _I, _VP]),
     ("ppo_update", _I, [_VP, _F, _VP, C.POINTER(UpdateStats)]),
+    ("ppo_update_ex", _I, [_VP, _F, _I, _VP, C.POINTER(UpdateStats)]),
     ("ppo_sync", _I, [_VP]),
     ("ppo_debug_last_grad", _I, [_VP, _FP, _L]),
     ("ppo_snapshot_state", _I, [_VP]),
@@ -508,6 +509,11 @@ class Agent:
         check(lib().ppo_save_adam(self.h, m.ctypes.data, v.ctypes.data, m.size, C.byref(st)))
         return m, v, st.value
 
+    def load_adam(self, m, v, step):
+        """Set the Adam moments (flat, unpadded named_parameters() order) and the step count."""
+        m, v = np.ascontiguousarray(m, np.float32), np.ascontiguousarray(v, np.float32)
+        check(lib().ppo_load_adam(self.h, m.ctypes.data, v.ctypes.data, m.size, int(step)))
+
     # -- agent calls (device arrays in / out) ----------------------------------------------------
     def get_action_and_value(self, x: DeviceArray, sample_type=PPO_SAMPLE, action: DeviceArray | None = None,
                              env_base=0, step_id=0):
@@ -539,9 +545,11 @@ class Agent:
     def gae_from_values(self, next_value: DeviceArray, next_done: DeviceArray, nsteps=None):
         check(lib().ppo_gae_from_values(self.h, next_value.ptr, next_done.ptr, nsteps or self.hcfg.num_steps, None))
 
-    def update(self, lr, perms: DeviceArray | None = None, want_stats=True):
+    def update(self, lr, perms: DeviceArray | None = None, want_stats=True, num_steps_collected=None):
+        """num_steps_collected < num_steps: a DD-PPO partial collection (ppo_update_ex)."""
         st = UpdateStats()
-        check(lib().ppo_update(self.h, lr, perms.ptr if perms else None, C.byref(st) if want_stats else None))
+        check(lib().ppo_update_ex(self.h, lr, num_steps_collected or self.hcfg.num_steps, perms.ptr if perms else None,
+                                  C.byref(st) if want_stats else None))
         return st.as_dict() if want_stats else None
 
     def sync(self):

@@ -58,18 +58,80 @@ def test_ppo_cli_runs():
 
 
 @pytest.mark.gpu
-def test_ac_cli_host_equals_device_env():
-    common = ["--num_envs", "64", "--num_steps", "16", "--total_timesteps", str(64 * 16 * 2), "--seed", "4",
+@pytest.mark.parametrize("E,T,groups,host_us", [(64, 16, "5", "0"), (4096, 8, "0", "0"), (512, 8, "0", "2")])
+def test_ac_cli_host_equals_device_env(E, T, groups, host_us):
+    """Host envs in async collection groups (5 groups; the default two per host thread at cfg3's
+    E = 4096; with a per-step host cost) vs the device env: bit-identical weights."""
+    tag = f"{E}_{T}_{groups}_{host_us}".replace(".", "p")
+    common = ["--num_envs", str(E), "--num_steps", str(T), "--total_timesteps", str(E * T * 2), "--seed", "4",
               "--num_eval_runs", "1"]
-    _run([_exe("ac_ppo_continuous_action"), "--env_id", "SyntheticCheetah-v0", "--env_backend", "host",
-          "--num_collect_groups", "5", "--exp_name_stem", "t_ac_host"] + common)
+    out = _run([_exe("ac_ppo_continuous_action"), "--env_id", "SyntheticCheetah-v0", "--env_backend", "host",
+                "--num_collect_groups", groups, "--host_step_us", host_us, "--exp_name_stem", f"t_ac_host{tag}"] + common)
+    assert "collection groups: " in out
     _run([_exe("ac_ppo_continuous_action"), "--env_id", "SyntheticCheetah-v0", "--env_backend", "device",
-          "--exp_name_stem", "t_ac_dev"] + common)
+          "--exp_name_stem", f"t_ac_dev{tag}"] + common)
     L = P.agent_layout(P.PPO_NET_LN_BETA, 17, 6, 256)
-    a = P.load_agent_pth(L, os.path.join(MODELS, "t_ac_host_4", "model_final.pth"))
-    b = P.load_agent_pth(L, os.path.join(MODELS, "t_ac_dev_4", "model_final.pth"))
+    a = P.load_agent_pth(L, os.path.join(MODELS, f"t_ac_host{tag}_4", "model_final.pth"))
+    b = P.load_agent_pth(L, os.path.join(MODELS, f"t_ac_dev{tag}_4", "model_final.pth"))
     assert a.size == b.size and a.size > 146189
     np.testing.assert_array_equal(a, b)
+
+
+def _free_port_pair():
+    import socket
+    for _ in range(50):
+        with socket.socket() as s0:
+            s0.bind(("127.0.0.1", 0))
+            p = s0.getsockname()[1]
+        try:
+            with socket.socket() as s1:
+                s1.bind(("127.0.0.1", p + 1))
+            return p
+        except OSError:
+            continue
+    raise RuntimeError("no free port pair")
+
+
+@pytest.mark.gpu
+def test_ac_cli_dd_ppo_preemption_with_a_straggler_group():
+    """DD-PPO preemption (ac:568-583, :680-693, :803-810) through the drop-in CLI: 4 collection groups,
+    the last one 200 us per env step slower. The other three finish all 64 steps while the straggler
+    is still early, so once it is past dd_ppo_min_perc (0.25 x 64 = 16 steps) it sees 3 of 4 groups
+    done (> 0.6) and stops after step 17: both iterations train on 17 steps per env (the step at
+    which it stops is stored but not trained on, as in the reference), the batch padded by repeating
+    the permutation (the index rule itself: test_gpu_ddppo.py)."""
+    port = _free_port_pair()
+    out = _run([_exe("ac_ppo_continuous_action"), "--env_id", "SyntheticCheetah-v0", "--env_backend", "host",
+                "--num_envs", "64", "--num_steps", "64", "--total_timesteps", str(64 * 64 * 2), "--seed", "6",
+                "--num_eval_runs", "1", "--num_collect_groups", "4", "--straggler_us", "200",
+                "--use_dd_ppo_preempt", "1", "--dd_ppo_min_perc", "0.25", "--dd_ppo_preempt_threshold", "0.6",
+                "--rdzv_addr", "127.0.0.1", "--tcp_store_port", str(port), "--exp_name_stem", "t_ac_ddppo"])
+    assert out.count("dd_ppo: rank 0 trains on 17 of 64 steps per env (preempted)") == 2, out[-3000:]
+    L = P.agent_layout(P.PPO_NET_LN_BETA, 17, 6, 256)
+    p = P.load_agent_pth(L, os.path.join(MODELS, "t_ac_ddppo_6", "model_final.pth"))
+    assert np.isfinite(p).all()
+    # without preemption the same run trains on all 64 steps
+    out = _run([_exe("ac_ppo_continuous_action"), "--env_id", "SyntheticCheetah-v0", "--env_backend", "host",
+                "--num_envs", "64", "--num_steps", "64", "--total_timesteps", str(64 * 64 * 2), "--seed", "6",
+                "--num_eval_runs", "1", "--num_collect_groups", "4", "--exp_name_stem", "t_ac_noddppo"])
+    assert "dd_ppo:" not in out
+
+
+@pytest.mark.gpu
+def test_ac_cli_estimate_mean_std_host_equals_device():
+    """--estimate_mean_std (ac:663, :954-963): mean and population std of env 0's observations over the
+    run, printed at the end; the host and the device env give the same trajectories, so the same numbers."""
+    outs = []
+    for backend in ("host", "device"):
+        out = _run([_exe("ac_ppo_continuous_action"), "--env_id", "SyntheticCheetah-v0", "--env_backend", backend,
+                    "--num_envs", "8", "--num_steps", "16", "--total_timesteps", str(8 * 16 * 2), "--seed", "2",
+                    "--num_eval_runs", "1", "--estimate_mean_std", "1", "--exp_name_stem", f"t_ac_ems_{backend}"])
+        tail = out[out.index("Mean obs:"):]
+        tail = tail[:tail.index("]", tail.index("Std obs:"))]
+        vals = [float(x) for x in tail.split() if x.replace(".", "").replace("-", "").replace("e", "").isdigit()]
+        outs.append(vals)
+    assert len(outs[0]) == 34 and outs[0] == outs[1]
+    assert all(v >= 0 for v in outs[0][17:])
 
 
 @pytest.mark.gpu

@@ -112,6 +112,37 @@ def test_update_larger_batch_vs_torch(agent):
     assert st2["approx_kl"] >= 0.0
 
 
+def test_update_cfg5_minibatch_2048_vs_torch():
+    """cfg5's per-GPU minibatch: 256 envs x num_steps 2048 / 32 minibatches / 8 GPUs = 2 048 rows
+    (carla_config.h:28,31,133-138). Hundreds of wgrad chunks per layer and conv1's reductions over
+    2 048 x 8 836 output pixels, against the fp32 PyTorch reference at the per-tensor bars of
+    _check_grad; stats rtol 1e-4, total norm rtol 1e-4, parameters after the clipped Adam step atol
+    2e-6. The reference takes ~12 s and ~11 GB of host memory on 8 threads."""
+    torch.set_num_threads(16)
+    L = CI.layout()
+    p = CI.params(L)
+    n = 2048
+    rng = np.random.default_rng(11)
+    bev = rng.integers(0, 256, size=(n, 15, 192, 192), dtype=np.uint8)
+    f = lambda *shape: rng.uniform(-1, 1, shape).astype(np.float32)  # noqa: E731
+    batch = (bev, f(n, 8), f(n, 3), f(n, 2) * 0.95, f(n) * 0.2, rng.standard_normal(n).astype(np.float32),
+             rng.standard_normal(n).astype(np.float32), f(n) * 0.1)
+    ag = ppo_amd.CarlaAgent(max_batch=n, seed=7)
+    try:
+        ag.load_params(p)
+        ag.load_adam(np.zeros(L.P, np.float32), np.zeros(L.P, np.float32), 0)
+        st, grad, newp = _run_update(ag, *batch)
+    finally:
+        ag.close()
+    ref_g, ref_st, ref_total, ref_p, _, _ = TR.update(L, p, *batch, **CFG)
+    stats = np.array([st[k] for k in ("pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac")])
+    np.testing.assert_allclose(stats[:5], ref_st[:5], rtol=1e-4, atol=2e-6)
+    assert abs(stats[5] - ref_st[5]) <= 1.5 / n  # clipfrac: at most one row on the other side of the clip
+    np.testing.assert_allclose(st["grad_norm"], ref_total, rtol=1e-4)
+    _check_grad(L, grad, ref_g)
+    np.testing.assert_allclose(newp, ref_p, rtol=0, atol=2e-6)
+
+
 def test_update_argument_errors(agent):
     x = DeviceArray.from_numpy(np.zeros((1, 2), np.float32))
     with pytest.raises(ppo_amd.PPOError, match="n >= 2"):

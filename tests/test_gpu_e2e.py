@@ -18,6 +18,9 @@ Tolerances (stated; fp32 on both sides, MFMA vs LibTorch CPU accumulation orders
     sample flips (tests/test_oracle_golden.py::test_e2e_oracle_vs_libtorch_drift measures it on CPU).
     So: iterations 0-1 losses rtol 2e-4; later iterations rtol 5e-2 (atol 2e-3); clipfrac atol 3e-2;
     episodic returns rtol 2e-3 (measured 6.5e-4); final parameters relative L2 < 2e-2.
+    This is the free-running check only: tests/test_gpu_e2e_teacher.py re-runs each of the 8
+    iterations from the replay's own state (parameters, Adam moments, rollout buffers) at
+    one-iteration bars (parameters within 1.2e-7 of the replay after every iteration).
   PPO agent behind the ppo:41-49 wrapper chain (e2e_ppo_wrapped; the device chain fused into the env
     kernels): the replay's NormalizeObservation uses LibTorch's CPU torch::sqrt, 1 ulp low on ~0.65 %
     of inputs (test_wrappers.py), so observations differ by an ulp here and there and the run by a

@@ -183,6 +183,7 @@ struct ppo_ctx {
   int upd_trunk_mask = 3, upd_sched = 1;   // k_upd launch options (PPO_UPD_TRUNK: PPO_DIAG builds only)
   int dw_fused = 1;
   int dw_dma = 1;                       // create option dw_dma: k_dwf stages by LDS DMA (k_dwf_dma)
+  int dw_bx = 0;                        // create option dw_mfma: 0 fp32 MFMA, 8 / 9 exact bf16 piece products (k_dwf_bx)
   int rollout_mode = PPO_ROLLOUT_AUTO;  // ppo_set_rollout_mode
   int gradstep = 0;                     // create option gradstep=fused|split (default split)
   unsigned* gs_bar = nullptr;           // k_gradstep's grid barrier counter
@@ -278,6 +279,7 @@ struct CreateOptions {
   int dw_rows = 0;     // dW split-K rows per chunk (multiple of 16; 0: auto, ~128 chunks per trunk)
   int dw_slices = 0;   // k_dwf output slices per chunk (1 / 2; 0: auto, dw_slices())
   int dw_dma = 1;      // 1 (default): k_dwf_dma (LDS-DMA staging, three stage buffers); 0: k_dwf
+  int dw_bx = -1;      // dw_mfma: -1 auto, 0 f32 (fp32 MFMA), 9 bf16x9 / 8 bf16x8 (k_dwf_bx: exact bf16 splits)
   // 1: ppo_update replays its minibatch launches as one captured hipGraph; 0 (default): eager.
   // Snapshots work with it on (ppo_read_snapshot waits for the snapshot's event on the host).
   int update_graph = 0;
@@ -289,6 +291,8 @@ struct CreateOptions {
 // auto = the single k_upd2: the split form measured slower on cfg2 (round 4, profiles/r04/cfg2_split/:
 // 101.3 vs 92.9 ms per iteration; k_l1g 66 us = 0.61 of peak per launch, the tail 94 us at 3 per CU)
 static constexpr int kUpd2SplitAuto = 0;
+// dw_mfma=auto: the fused dW on fp32 MFMAs (k_dwf_dma) until the split-bf16 form is measured
+static constexpr int kDwBxAuto = 0;
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
   std::string s(opts);
@@ -313,6 +317,8 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
       o->dw_rows = atoi(v.c_str());  // at most 5 digits: no overflow, no exception across the C-ABI
     else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
     else if (k == "dw_dma" && (v == "0" || v == "1")) o->dw_dma = v[0] - '0';
+    else if (k == "dw_mfma" && (v == "auto" || v == "f32" || v == "bf16x9" || v == "bf16x8"))
+      o->dw_bx = v == "auto" ? -1 : v == "f32" ? 0 : v == "bf16x9" ? 9 : 8;
     else if (k == "update_graph" && (v == "0" || v == "1")) o->update_graph = v[0] - '0';
     else if (k == "rollout_kernel" && (v == "auto" || v == "mfma" || v == "valu"))
       o->rollout_kernel = v == "auto" ? 0 : v == "mfma" ? 1 : 2;
@@ -379,6 +385,7 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   c->act_kernel = opt.act_kernel;
   c->dw_fused = opt.dw_fused;
   c->dw_dma = opt.dw_dma;
+  c->dw_bx = opt.dw_bx >= 0 ? opt.dw_bx : kDwBxAuto;
   c->rollout_mode = opt.rollout;
   c->gradstep = opt.gradstep;
   c->update_graph = opt.update_graph;
@@ -903,6 +910,7 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
   dw.slices = c->dw_slices;
   dw.fused = c->dw_fused;
   dw.dma = c->dw_dma;
+  dw.bx = c->dw_dma ? c->dw_bx : 0;
   dw.xn = c->Xn;
   dw.obs = c->buf[PPO_BUF_OBS];
   dw.O = c->K.O;

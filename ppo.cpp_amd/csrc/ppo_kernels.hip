@@ -1230,6 +1230,185 @@ __global__ __launch_bounds__(512) void k_dwf_dma(DwArgs a) {
 }
 
 // =============================================================================================
+// k_dwf_bx — k_dwf_dma's products on BF16 MFMAs with every fp32 operand split exactly in three
+// (create option dw_mfma=bf16x9 / bf16x8; the default: see ppo_capi.hip).
+//
+// On gfx950 the fp32 MFMA runs at 1/16 of the BF16 rate (MI355X_MICROARCH.md: 157 vs ~2 500
+// TF/s), and k_dwf_dma is MFMA-bound (matrix pipe 0.77 busy, 1.9 VALU per MFMA). Every fp32 x is
+// the exact sum of three bf16 numbers: hi = x with the low 16 bits cleared (truncation), r = x - hi
+// (exact: a prefix of x's significand is removed), mid = r truncated the same way, lo = r - mid
+// (exact, at most 8 significant bits: a bf16). So a.b = sum over the nine piece products, each
+// product of two 8-bit significands exact in fp32, and the MFMA accumulates them in fp32 like the
+// fp32 MFMA accumulates a.b: NP = 9 keeps every piece product (an exact-product fp32 GEMM in a
+// different summation order), NP = 8 drops lo.lo (< 2^-30 |a.b|: 64x below an fp32 rounding). The
+// passes of one k-block run smallest first. v_mfma_f32_32x32x16_bf16 takes 32 cycles for 16 k
+// against 8 x 64 cycles of v_mfma_f32_32x32x2_f32: 9 passes are 0.56 of the fp32 MFMA time, 8 0.50.
+// Operand layout (cdna_hip_programming.md): lane (r = l & 31, h = l >> 5) holds A[r][8 h + e] and
+// B[8 h + e][r] in element e = 0..7; the accumulator layout is the 32x32x2 one, so the slab stores
+// are k_dwf_dma's. Per 16-row stage a lane reads its column of rows 8 h .. 8 h + 7 (ds_read_b32,
+// the same count as k_dwf_dma's 8 k-steps) and splits each value once (v_and / v_sub / v_perm).
+// Staging (LDS DMA, three buffers, two stages ahead) is k_dwf_dma's.
+// =============================================================================================
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+struct Split3 {
+  u32x4 hi, mid, lo;
+};
+// two fp32 values -> their (hi, mid, lo) bf16 pieces, packed (x0 in the low half)
+PPO_DEV void split3_pair(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
+  const unsigned u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
+  const float r0 = x0 - __uint_as_float(u0 & 0xffff0000u), r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
+  const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
+  const float l0 = r0 - __uint_as_float(v0 & 0xffff0000u), l1 = r1 - __uint_as_float(v1 & 0xffff0000u);
+  hi = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+  mid = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
+  lo = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
+}
+PPO_DEV Split3 split3(const float (&x)[8]) {
+  Split3 s;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    unsigned h, m, l;
+    split3_pair(x[2 * p], x[2 * p + 1], h, m, l);
+    s.hi[p] = h;
+    s.mid[p] = m;
+    s.lo[p] = l;
+  }
+  return s;
+}
+PPO_DEV f16v mfma_bx(u32x4 a, u32x4 b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+// acc += A.B over one 16-k block as NP piece products, smallest first
+template <int NP>
+PPO_DEV f16v mfma_split(const Split3& A, const Split3& B, f16v acc) {
+  if constexpr (NP >= 9) acc = mfma_bx(A.lo, B.lo, acc);
+  acc = mfma_bx(A.lo, B.mid, acc);
+  acc = mfma_bx(A.mid, B.lo, acc);
+  acc = mfma_bx(A.lo, B.hi, acc);
+  acc = mfma_bx(A.mid, B.mid, acc);
+  acc = mfma_bx(A.hi, B.lo, acc);
+  acc = mfma_bx(A.mid, B.hi, acc);
+  acc = mfma_bx(A.hi, B.mid, acc);
+  acc = mfma_bx(A.hi, B.hi, acc);
+  return acc;
+}
+
+template <int H, int OP, int NSL, int NP>
+__global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int KS = 16, NBUF = 3;
+  constexpr int LDH = H, LDX = OP;
+  constexpr int oH1 = KS * LDH, oDZ1 = 2 * KS * LDH, oXN = 3 * KS * LDH;
+  constexpr int STG = 3 * KS * LDH + KS * LDX;
+  static_assert(H == 256 && (OP == 16 || OP == 32), "k_dwf_bx geometry");
+  constexpr int NXI = KS * OP / 256;
+  constexpr int TOW = 2 / NSL, TIW = 4;
+  static_assert(NSL == 1 || NSL == 2, "k_dwf slices");
+  static_assert(NP == 8 || NP == 9, "k_dwf_bx passes");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hs = lane >> 5;
+  const int wo = wave & 3, wi = wave >> 2;
+  const int trunk = blockIdx.y, slice = NSL > 1 ? (int)blockIdx.z : 0;
+  const int obase = slice * (H / NSL);
+  const bool w1_wave = NSL == 1 || wave < 8 / NSL;
+  const int w1row = obase + wave * 32;
+  const long m0 = (long)blockIdx.x * a.rows_per_chunk;
+  const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
+  if (m0 >= m1) return;
+  const uint32_t rows_bytes = (uint32_t)((long)a.M * H * 4), xn_bytes = (uint32_t)((long)a.M * OP * 4);
+  const PBuf bdz2 = make_pbuf(a.dz2[trunk], (int)(rows_bytes / 4)), bh1 = make_pbuf(a.h1[trunk], (int)(rows_bytes / 4));
+  const PBuf bdz1 = make_pbuf(a.dz1[trunk], (int)(rows_bytes / 4));
+  const PBuf bxn = make_pbuf(a.xn, (int)(xn_bytes / 4));
+  f16v acc[TOW][TIW], acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc1[r] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < TOW; ++u)
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) acc[u][v][r] = 0.0f;
+  }
+  auto issue = [&](long mb, int buf) {
+    float* b = lds + buf * STG;
+#pragma unroll
+    for (int s3 = 0; s3 < 3; ++s3) {
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int r = 2 * wave + rr;
+        const long row = mb + r;
+        const uint32_t voff = row < m1 ? (uint32_t)((row * H) * 4 + lane * 16) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds((s3 == 0 ? bdz2 : s3 == 1 ? bh1 : bdz1).r,
+                                                 (__attribute__((address_space(3))) void*)(b + s3 * KS * LDH + r * LDH), 16,
+                                                 voff, 0, 0, 0);
+      }
+    }
+    if (wave < NXI) {
+      const int e = wave * 256 + lane * 4, r = e / OP;
+      const long row = mb + r;
+      const uint32_t voff = row < m1 ? (uint32_t)((row * OP + (e - r * OP)) * 4) : 0xFFFFFFF0u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(bxn.r, (__attribute__((address_space(3))) void*)(b + oXN + wave * 256), 16,
+                                               voff, 0, 0, 0);
+    }
+  };
+  const bool xw = wave < NXI;
+  const int nst = (int)((m1 - m0 + KS - 1) / KS);
+  issue(m0, 0);
+  if (nst > 1) issue(m0 + KS, 1);
+  for (int sI = 0; sI < nst; ++sI) {
+    if (sI + 1 < nst) {
+      if (xw) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();
+    if (sI + 2 < nst) issue(m0 + (long)(sI + 2) * KS, (sI + 2) % NBUF);
+    __builtin_amdgcn_sched_barrier(0);
+    const float* sb = lds + (sI % NBUF) * STG + (8 * hs) * LDH;  // this lane's rows 8 hs .. 8 hs + 7
+    Split3 as[TOW], a1s, b1s;
+    {
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < TOW; ++u) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = sb[e * LDH + obase + (wo * TOW + u) * 32 + l32];
+        as[u] = split3(x);
+      }
+      if (w1_wave) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = sb[oDZ1 + e * LDH + w1row + l32];
+        a1s = split3(x);
+        const float* xb = lds + (sI % NBUF) * STG + oXN + (8 * hs) * LDX;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = l32 < OP ? xb[e * LDX + l32] : 0.0f;
+        b1s = split3(x);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < TIW; ++v) {
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = sb[oH1 + e * LDH + (wi * TIW + v) * 32 + l32];
+      const Split3 bs = split3(x);
+#pragma unroll
+      for (int u = 0; u < TOW; ++u) acc[u][v] = mfma_split<NP>(as[u], bs, acc[u][v]);
+    }
+    if (w1_wave) acc1 = mfma_split<NP>(a1s, b1s, acc1);
+  }
+  float* out = a.slab[trunk] + (size_t)blockIdx.x * a.slab_stride;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int orow = (r & 3) + 8 * (r >> 2) + 4 * hs;
+#pragma unroll
+    for (int u = 0; u < TOW; ++u)
+#pragma unroll
+      for (int v = 0; v < TIW; ++v)
+        out[(size_t)(obase + (wo * TOW + u) * 32 + orow) * H + (wi * TIW + v) * 32 + l32] = acc[u][v][r];
+    if (w1_wave && l32 < OP) out[(size_t)H * H + (size_t)(w1row + orow) * OP + l32] = acc1[r];
+  }
+}
+
+// =============================================================================================
 // k_colsum — dst[seg] = sum_{c < C} src[c * stride + seg]   (fixed order => deterministic)
 // =============================================================================================
 // The segments are cut into 64-float column tiles, numbered consecutively over all segments
@@ -1863,6 +2042,17 @@ size_t dw_lds_bytes(int H, int OP) {
 template <int H, int OP, int NSL>
 static int launch_dwf_t(const DwArgs& a, int nchunks, hipStream_t s) {
   // the DMA kernels address their sources through 32-bit buffer descriptors (make_pbuf: int floats)
+  if (a.bx && (long)a.M * H < (1L << 29)) {
+    auto k = a.bx == 9 ? k_dwf_bx<H, OP, NSL, 9> : k_dwf_bx<H, OP, NSL, 8>;
+    constexpr size_t lds = (size_t)3 * (3 * 16 * H + 16 * OP) * sizeof(float);
+    static bool attr[2] = {false, false};
+    if (!attr[a.bx == 9]) {
+      if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
+      attr[a.bx == 9] = true;
+    }
+    hipLaunchKernelGGL(k, dim3(nchunks, 2, NSL), dim3(512), lds, s, a);
+    return 0;
+  }
   if (a.dma && (long)a.M * H < (1L << 29)) {
     auto k = k_dwf_dma<H, OP, NSL>;
     constexpr size_t lds = (size_t)3 * (3 * 16 * H + 16 * OP) * sizeof(float);

@@ -99,6 +99,7 @@ struct DwArgs {
   int slices;         // k_dwf: output-row slices per chunk (grid z); 2 halves the chunks, so the
                       // split-K partials, for small minibatches (dw_slices)
   int dma;            // k_dwf: 1 stages the rows by LDS DMA, three buffers (k_dwf_dma), bitwise k_dwf
+  int bx;             // k_dwf: 8 / 9 runs the products as exact bf16 piece products (k_dwf_bx); 0 fp32 MFMA
 };
 // k_dwf output slices and dW row chunks for a minibatch of M rows: 128 chunks per trunk (one
 // workgroup per CU over both trunks); below 32 K rows 64 chunks x 2 output halves instead — the

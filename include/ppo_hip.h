@@ -88,6 +88,10 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *   dw_fused=1|0             dW1 / dW2 in one pass (k_dwf) or two (k_dw)
  *   dw_dma=1|0               k_dwf's rows staged by LDS DMA in three buffers (k_dwf_dma, default)
  *                            or through registers in two (k_dwf); bitwise the same
+ *   dw_mfma=auto|f32|bf16x9|bf16x8  k_dwf_dma's products on fp32 MFMAs (auto) or as exact three-way
+ *                            bf16 splits of every fp32 operand on 32x32x16 bf16 MFMAs (k_dwf_bx: all 9
+ *                            piece products, or 8 without lo*lo < 2^-30 |ab|); fp32 accumulation, not
+ *                            bitwise the fp32 path (rounding of the bf16 MFMA's internal sums)
  *   dw_rows=<n>, dw_slices=1|2  dW split-K geometry: rows per chunk (multiple of 16; 32 for the
  *                            64-wide agent) and k_dwf output slices; default: automatic
  *   update_graph=0|1       ppo_update's minibatch launches eager (default) or replayed as one
@@ -106,11 +110,14 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *   rollout=auto|per_step    ppo_rollout_synth: persistent launch where supported, or per step
  *   rollout_kernel=auto|mfma|valu  the AC agent's persistent rollout: k_rollout (16 envs per
  *                            workgroup, MFMA) or k_rollout_v (2 envs per workgroup, VALU; O <= 32);
- *                            auto: k_rollout_v at E <= 512. Bitwise the same results
+ *                            auto: k_rollout_v at E <= 512. Bitwise the same results. valu on an
+ *                            agent it cannot serve (the PPO agent, O > 32, device env wrappers) fails
  *   gradstep=split|fused     clip_grad_norm_ + Adam: two launches (k_gradnorm, k_adam; default) or
  *                            one cooperative launch (k_gradstep: slower on ROCm 7, whose cooperative
  *                            launch costs ~30 us); bitwise the same
- * An unknown key or value is an error. */
+ * An unknown key or value is an error, and so is an option the agent cannot use (upd_mfma=32 / mix
+ * off the LayerNorm-Beta agent, upd2_split > 0 off the 64-wide Humanoid shape): such a create
+ * fails and releases everything it had allocated. */
 int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* options, ppo_t** out);
 int ppo_destroy(ppo_t* ctx);
 int ppo_get_layout(const ppo_t* ctx, ppo_layout* out);

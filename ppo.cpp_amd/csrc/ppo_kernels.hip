@@ -1163,6 +1163,9 @@ __global__ __launch_bounds__(512) void k_dwf_dma(DwArgs a) {
   // row sources, waves 0 .. NXI-1 one XN instruction each (256 floats = 256 / OP rows)
   auto issue = [&](long mb, int buf) {
     float* b = lds + buf * STG;
+#ifdef PPO_DIAG
+    if (a.hot) mb = m0;  // diagnostic: L2-hot rows (bandwidth bound or not)
+#endif
 #pragma unroll
     for (int s3 = 0; s3 < 3; ++s3) {
 #pragma unroll
@@ -1330,6 +1333,9 @@ __global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
   }
   auto issue = [&](long mb, int buf) {
     float* b = lds + buf * STG;
+#ifdef PPO_DIAG
+    if (a.hot) mb = m0;  // diagnostic: L2-hot rows (bandwidth bound or not)
+#endif
 #pragma unroll
     for (int s3 = 0; s3 < 3; ++s3) {
 #pragma unroll
@@ -2040,7 +2046,12 @@ size_t dw_lds_bytes(int H, int OP) {
 }
 
 template <int H, int OP, int NSL>
-static int launch_dwf_t(const DwArgs& a, int nchunks, hipStream_t s) {
+static int launch_dwf_t(const DwArgs& a0, int nchunks, hipStream_t s) {
+  DwArgs a = a0;
+#ifdef PPO_DIAG
+  static const int hot = [] { const char* e = getenv("PPO_DW_HOT"); return e ? atoi(e) : 0; }();
+  a.hot = hot;
+#endif
   // the DMA kernels address their sources through 32-bit buffer descriptors (make_pbuf: int floats)
   if (a.bx && (long)a.M * H < (1L << 29)) {
     auto k = a.bx == 9 ? k_dwf_bx<H, OP, NSL, 9> : k_dwf_bx<H, OP, NSL, 8>;

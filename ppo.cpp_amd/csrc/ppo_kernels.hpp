@@ -100,6 +100,7 @@ struct DwArgs {
                       // split-K partials, for small minibatches (dw_slices)
   int dma;            // k_dwf: 1 stages the rows by LDS DMA, three buffers (k_dwf_dma), bitwise k_dwf
   int bx;             // k_dwf: 8 / 9 runs the products as exact bf16 piece products (k_dwf_bx); 0 fp32 MFMA
+  int hot;            // diagnostic build only (PPO_DW_HOT): every stage re-reads the chunk's first rows (L2-hot)
 };
 // k_dwf output slices and dW row chunks for a minibatch of M rows: 128 chunks per trunk (one
 // workgroup per CU over both trunks); below 32 K rows 64 chunks x 2 output halves instead — the

@@ -896,6 +896,12 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
   u.hw_global = c->upd.hw_global;
   u.trunk_mask = c->upd_trunk_mask;
   u.sched = c->upd_sched;
+#ifdef PPO_DIAG
+  {
+    static const int hot = [] { const char* e = getenv("PPO_UPD2_HOT"); return e ? atoi(e) : 0; }();
+    u.hot = hot;
+  }
+#endif
   const int nblk = c->use_upd ? c->upd_nblk : c->nblk;  // workgroups that wrote a slab row
   for (int k = 0; k < 2; ++k) {
     u.H1[k] = c->H1[k];

@@ -44,6 +44,7 @@ struct ConvArgs {
   int n;
   float* part;  // split-K partial sums [Z][n * OH * OW][OC] (launch_conv sets kc and part)
   int kc;       // k-range per blockIdx.z (0: no split)
+  float* wprep = nullptr;  // conv1 packed form (k_conv_img3): its A operands, [kImg3Blocks][4][16][4]
 };
 
 constexpr int kConvWaves = 4;
@@ -427,6 +428,143 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a) {
         float y = acc[u][r] + a.b[oc];
         if (a.relu) y = y > 0.0f ? y : 0.0f;
         a.out[(size_t)smp * a.out_stride + (size_t)oc * P + (size_t)oy * a.OW + ox] = y;
+      }
+    }
+  }
+}
+
+// ---- conv1, packed taps (k_conv_img3; create option conv1=packed) -------------------------------
+// k_conv_img2 spends 7.3 VALU and 1.6 LDS instructions per MFMA (SQ counters, profiles/r05/carla):
+// every B operand is its own ds_read_u8 + convert + scale, every A operand an index lookup + select.
+// Here the taps of one 16-wide MFMA k block are ordered so that lane group g's four k-steps are four
+// CONSECUTIVE taps of one kernel row: tap (16 kb + 4 g + st) = extended column kx' = 4 (g & 1) + st of
+// kernel row r = 2 kb + (g >> 1) (r = ic K + ky; kx' in [0, 8): k_conv_img2's K + S = 7 columns
+// padded to 8 with a zero-weight tap). Then a lane's B operands for the four steps are the four bytes
+// of ONE aligned dword of the patch row (ds_read_b32 + v_cvt_f32_ubyte0..3), and its A operands the
+// four floats of one 16-byte piece of a pre-arranged weight table (wprep, built by k_conv1_wprep from
+// W each call: A row i = oc + 8 dx holds W[oc][ic][ky][kx' - S dx], 0 outside the kernel), read from
+// L2 one k block ahead. 38 blocks x 4 steps x 4 row tiles = 608 MFMAs per wave (k_conv_img2: 528) for
+// ~8x fewer VALU and 5x fewer LDS instructions. Each product is k_conv's (x = u8 / 255, the same
+// weight); only the order of the k chain differs (not bitwise k_conv's; tolerance tests).
+constexpr int kImg3KX = 8;  // extended taps per kernel row, padded
+constexpr int kConv1Auto = 2;  // the default conv1 form (ppo_carla_create_ex option conv1): packed (measured faster)
+template <int K, int S>
+struct Img3Geo {
+  static constexpr int TI = (kImgTile - 1) * S + K;          // patch rows
+  static constexpr int TW = (kImg2W - 1) * S + K;            // patch columns used by real taps
+  static constexpr int TIP = ((2 * S * (kImg2W / 2 - 1) + kImg3KX) + 3) & ~3;  // incl. the padding tap
+};
+__host__ __device__ inline int img3_blocks(int IC, int K) { return (IC * K + 1) / 2; }
+static size_t img3_lds_bytes(int IC, int K, int S) {
+  const int TI = (kImgTile - 1) * S + K, TIP = ((2 * S * (kImg2W / 2 - 1) + kImg3KX) + 3) & ~3;
+  return ((size_t)IC * TI * TIP + 15) & ~(size_t)15;
+}
+// wprep[((kb * 4 + g) * 16 + i) * 4 + st] = A[i][tap 16 kb + 4 g + st]
+__global__ void k_conv1_wprep(const float* __restrict__ W, float* __restrict__ wp, int IC, int K, int S, int OC,
+                              int nblk) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nblk * 256) return;
+  const int st = e & 3, i = (e >> 2) & 15, g = (e >> 6) & 3, kb = e >> 8;
+  const int r = 2 * kb + (g >> 1), kxp = 4 * (g & 1) + st;
+  const int oc = i & 7, dx = i >> 3, kx = kxp - S * dx;
+  float w = 0.0f;
+  if (oc < OC && r < IC * K && kx >= 0 && kx < K) w = W[((size_t)oc * IC * K + r) * K + kx];  // W[oc][ic][ky][kx]
+  wp[e] = w * (1.0f / 255.0f);  // the image's 1 / 255 moves onto the weights: B is the raw byte value
+}
+
+// A workgroup walks tiles [t0, t1) (sample-major, 18 per 192 x 192 sample) with the A-operand table
+// staged in LDS once (38 KB) and one patch buffer (35 KB), refilled per tile by LDS DMA (one dword a
+// lane); two workgroups per CU, so one's patch fetch runs under the other's MFMAs. The k loop issues
+// no vector-memory instruction: an A operand in global memory made the compiler wait vmcnt(0) at
+// every k block (the ring index is not static), a full L2 round trip per 16 MFMAs.
+constexpr int kImg3WG = 512;  // workgroups: two per CU
+__host__ __device__ inline size_t img3_patch_bytes(int IC, int K, int S) {
+  const int TI = (kImgTile - 1) * S + K, TIP = ((2 * S * (kImg2W / 2 - 1) + kImg3KX) + 3) & ~3;
+  return ((size_t)IC * TI * TIP + 1023) & ~(size_t)1023;  // whole 4-wave DMA rounds (1 KB)
+}
+template <int K, int S>
+__global__ __launch_bounds__(256, 2) void k_conv_img3(ConvArgs a, int tiles, int tpc) {
+  using G = Img3Geo<K, S>;
+  constexpr int TI = G::TI, TIP = G::TIP, DW = TIP / 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int nblk = img3_blocks(a.IC, K), nrow = a.IC * K;
+  const int pbytes = (int)img3_patch_bytes(a.IC, K, S), ndma = pbytes / 1024;  // DMA instructions per wave
+  unsigned char* tile = smem;
+  float* wl = reinterpret_cast<float*>(smem + pbytes);  // [nblk][4][16][4]
+  const int tiles_x = (a.OW + kImg2W - 1) / kImg2W, tps = tiles_x * ((a.OH + kImgTile - 1) / kImgTile);
+  const int t0 = blockIdx.x * tpc, t1 = min(tiles, t0 + tpc);
+  if (t0 >= t1) return;
+  for (int e = tid; e < nblk * 64; e += 256)
+    reinterpret_cast<f4*>(wl)[e] = reinterpret_cast<const f4*>(a.wprep)[e];
+  const int plane = a.IH * a.IW, total = a.IC * TI * DW;
+  const float* wlane = wl + (g * 16 + j) * 4;  // this lane's piece of an A block
+  const int P = a.OH * a.OW;
+  int pix[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) pix[u] = S * (4 * wave + u) * TIP + 2 * S * j + 4 * (g & 1);
+  // row 2 m + (g >> 1) of a ten-row step: channel (2 m + (g >> 1)) / K of the pair, kernel row % K
+  int rowoff[5], rowq[5];
+#pragma unroll
+  for (int m = 0; m < 5; ++m) {
+    const int rr = 2 * m + (g >> 1), q = rr / K, ky = rr - q * K;
+    rowq[m] = q;
+    rowoff[m] = (q * TI + ky) * TIP;
+  }
+  for (int t = t0; t < t1; ++t) {
+    const int smp = t / tps, tt = t - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    __syncthreads();  // every wave is done with the previous tile's patch
+    {  // wave w moves dwords (w ndma + q) 64 + lane of the patch, q < ndma
+      const int x0 = tx * kImg2W * S, y0 = ty * kImgTile * S;
+      const size_t sb = (size_t)smp * a.in_stride, left = (size_t)a.n * a.in_stride - sb;
+      const PBuf ib{__builtin_amdgcn_make_buffer_rsrc((void*)(a.in_u8 + sb), (short)0,
+                                                      (int)(left < 0xFFFFFFF0u ? left : 0xFFFFFFF0u), 0x00020000)};
+      for (int q = 0; q < ndma; ++q) {
+        const int e0 = (wave * ndma + q) * 64, e = e0 + lane;
+        const int ic = e / (TI * DW), rem = e - ic * (TI * DW), r = rem / DW, d = rem - r * DW;
+        const uint32_t voff = e < total ? (uint32_t)(ic * plane + (y0 + r) * a.IW + x0 + 4 * d) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ib.r, (__attribute__((address_space(3))) void*)(tile + 4 * e0), 4,
+                                                 voff, 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    f4 acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = f4{0.f, 0.f, 0.f, 0.f};
+    // Five k blocks = ten kernel rows = two input channels per step: the patch offset of every row is
+    // a per-lane constant plus 2 TI TIP per step (rows past the last channel read channel 0: their
+    // weights are 0). The operands of block kb + 1 are read from LDS under block kb's MFMAs.
+    for (int c2 = 0; c2 < (a.IC + 1) / 2; ++c2) {
+      const unsigned char* cbase = tile + (size_t)min(2 * c2, a.IC - 1) * TI * TIP;
+#pragma unroll
+      for (int m = 0; m < 5; ++m) {
+        const int kb = 5 * c2 + m;
+        if (kb >= nblk) break;
+        const unsigned char* prow = (2 * c2 + 1 < a.IC || rowq[m] == 0) ? cbase + rowoff[m] : tile + rowoff[m] % (TI * TIP);
+        unsigned xb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) xb[u] = *reinterpret_cast<const unsigned*>(prow + pix[u]);
+        const f4 wv = *reinterpret_cast<const f4*>(wlane + kb * 256);
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc[u] = mfma16(wv[st], (float)((xb[u] >> (8 * st)) & 255u), acc[u]);
+      }
+    }
+    // lane (j, g), register r: channel (4 g + r) & 7 of output column 2 j + ((4 g + r) >> 3) (k_conv_img2's)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int oy = ty * kImgTile + 4 * wave + u;
+      if (oy >= a.OH) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ocp = 4 * g + r, oc = ocp & 7, ox = tx * kImg2W + 2 * j + (ocp >> 3);
+        if (oc < a.OC && ox < a.OW) {
+          float y = acc[u][r] + a.b[oc];
+          if (a.relu) y = y > 0.0f ? y : 0.0f;
+          a.out[(size_t)smp * a.out_stride + (size_t)oc * P + (size_t)oy * a.OW + ox] = y;
+        }
       }
     }
   }
@@ -833,9 +971,24 @@ __global__ __launch_bounds__(kTailThreads) void k_carla_tail(TailArgs a) {
 
 // fin = false: a split-K layer leaves its partials (k_conv_fin is the caller's, e.g. the fused
 // tail's stage 0); *z_out receives the chunk count (1: not split)
-int launch_conv(const ConvArgs& a, hipStream_t s, bool img = true, bool fin = true, int* z_out = nullptr) {
+int launch_conv(const ConvArgs& a, hipStream_t s, int img = 1, bool fin = true, int* z_out = nullptr) {
   if (z_out) *z_out = 1;
   if (a.IC * a.K * a.K > kMaxKTab) return -1;
+  if (img == 2 && a.wprep && a.in_u8 && ((uintptr_t)a.in_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 8 &&
+      a.IW % 4 == 0 && a.in_stride % 4 == 0 && a.OH <= 16 * 64 &&
+      img3_patch_bytes(a.IC, a.K, a.S) + (size_t)img3_blocks(a.IC, a.K) * 1024 <= 80 * 1024) {
+    const int nblk = img3_blocks(a.IC, a.K);
+    hipLaunchKernelGGL(k_conv1_wprep, dim3((nblk * 256 + 255) / 256), dim3(256), 0, s, a.W, a.wprep, a.IC, a.K, a.S,
+                       a.OC, nblk);
+    const int tiles = ((a.OW + kImg2W - 1) / kImg2W) * ((a.OH + kImgTile - 1) / kImgTile) * a.n;
+    const int grid = std::min(tiles, kImg3WG), tpc = (tiles + grid - 1) / grid;
+    const size_t lds = img3_patch_bytes(a.IC, a.K, a.S) + (size_t)nblk * 256 * sizeof(float);
+    static const bool attr = hipFuncSetAttribute((const void*)k_conv_img3<5, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)lds) == hipSuccess;
+    if (!attr) return -2;
+    hipLaunchKernelGGL((k_conv_img3<5, 2>), dim3((tiles + tpc - 1) / tpc), dim3(256), lds, s, a, tiles, tpc);
+    return 0;
+  }
   if (img && a.in_u8 && ((uintptr_t)a.in_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 8 && a.IW % 4 == 0 &&
       a.in_stride % 4 == 0 && a.OH <= 16 * 64 && img2_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {
     const int tiles = ((a.OW + kImg2W - 1) / kImg2W) * ((a.OH + kImgTile - 1) / kImgTile);
@@ -907,7 +1060,11 @@ struct ppo_carla {
   size_t part_floats = 0;
   float* small = nullptr;  // scalars, tensor table and norm slices (carla_train_init)
   long step = 0;
-  bool conv_img = true;  // LDS-staged conv1 / conv2 kernels (PPO_CARLA_CONV1=0 at create: generic, for A/B)
+  // conv1 / conv2 kernels: 2 packed conv1 taps (k_conv_img3), 1 LDS-staged (k_conv_img2 and the staged
+  // wgrad / dgrad kernels), 0 generic (create option conv1=packed|staged|generic; PPO_CARLA_CONV1 in the
+  // diagnostic build). The backward's staged kernels run for 1 and 2.
+  int conv_img = kConv1Auto;
+  float* c1w = nullptr;  // k_conv_img3's A-operand table
   // MLP tail for n <= kTailMaxN: 1 (default) one launch per stage, 0 one cooperative launch (a grid
   // barrier between stages: slower here, a cooperative launch costs more than the launches it
   // saves), 2 one k_conv / k_conv_fin pair per layer
@@ -932,7 +1089,7 @@ extern "C" int ppo_carla_destroy(ppo_carla_t* c) {
   float* bufs[] = {c->P,    c->enc,  c->s1,  c->l1,  c->feat,  c->v1,  c->v2,      c->val,  c->p1,
                    c->p2,   c->hpre, c->G,   c->m,   c->v,     c->denc, c->ds1,     c->dl1,  c->dfeat,
                    c->dv1,  c->dv2,  c->dp1, c->dp2, c->dhead, c->dval, c->lp,      c->ent,  c->rowstat,
-                   c->part, c->small,  c->ksplit, reinterpret_cast<float*>(c->tail_bar)};
+                   c->part, c->small,  c->ksplit, c->c1w, reinterpret_cast<float*>(c->tail_bar)};
   for (float* b : bufs)
     if (b) (void)hipFree(b);
   for (float* b : c->act)
@@ -950,7 +1107,7 @@ extern "C" int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_car
 
 extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, const char* options, ppo_carla_t** out) {
   if (!cfg || !out) return ppo_fail("ppo_carla_create: null argument", -1);
-  bool conv_img = true;
+  int conv_img = kConv1Auto;
   int tail_mode = 1;
   if (options && *options) {  // comma-separated key=value
     std::string rest(options);
@@ -958,8 +1115,9 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
       const size_t cpos = rest.find(',');
       const std::string o = rest.substr(0, cpos);
       rest = cpos == std::string::npos ? std::string() : rest.substr(cpos + 1);
-      if (o == "conv1=staged") conv_img = true;
-      else if (o == "conv1=generic") conv_img = false;
+      if (o == "conv1=packed") conv_img = 2;
+      else if (o == "conv1=staged") conv_img = 1;
+      else if (o == "conv1=generic") conv_img = 0;
       else if (o == "tail=fused") tail_mode = 0;
       else if (o == "tail=staged") tail_mode = 1;
       else if (o == "tail=layers") tail_mode = 2;
@@ -983,7 +1141,7 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
   c->conv_img = conv_img;
   c->tail_mode = tail_mode;
 #ifdef PPO_DIAG
-  if (const char* e = getenv("PPO_CARLA_CONV1")) c->conv_img = !(e[0] == '0');
+  if (const char* e = getenv("PPO_CARLA_CONV1")) c->conv_img = e[0] - '0';
 #endif
   int rc = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess ? 0 : -2;
   const size_t B = (size_t)cfg->max_batch;
@@ -1012,6 +1170,7 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
     need(256 + L.NV, 1, 256); need(256, 1, 256); need(256, 1, 1);
     if (m) rc |= carla_alloc(&c->ksplit, m);
   }
+  rc |= carla_alloc(&c->c1w, (size_t)img3_blocks(L.C, L.conv_k[0]) * 256);
   rc |= carla_alloc(reinterpret_cast<float**>(&c->tail_bar), 1);
   if (rc || hipDeviceSynchronize() != hipSuccess) {
     ppo_carla_destroy(c);
@@ -1054,6 +1213,7 @@ extern "C" int ppo_carla_forward(ppo_carla_t* c, int n, const uint8_t* bev, cons
                   float* out, long out_stride, int OC, int OH, int OW, int K, int S, int relu) {
     ConvArgs a{in_f, in_u8, in_stride, IC, IH, IW, P + w, P + b, out, out_stride, OC, OH, OW, K, S, relu, n,
                c->ksplit, 0};
+    a.wprep = c->c1w;
     return launch_conv(a, s, c->conv_img);
   };
   auto linear = [&](const float* in, long in_stride, int IN, long w, long b, float* out, long out_stride, int OUT,

@@ -72,6 +72,7 @@ struct UpdArgs {
   float* Z1;              // k_l1g -> k_upd2 (split form): layer-1 pre-activations [M][128], critic | actor
   int trunk_mask;         // k_upd: trunks to run (bit t = trunk t; 3 = both; other values: PPO_DIAG builds only)
   int sched;              // k_upd: bit 0 actor workgroups dispatched first, bit 1 actor wave priority
+  int hot;                // diagnostic build only (PPO_UPD2_HOT): k_upd2 gathers the rows of its first 8 tiles only
 };
 
 // k_upd geometry (ppo_update.hip)

@@ -246,7 +246,11 @@ __global__ __launch_bounds__(256, SPLIT ? SPLIT : 2) void k_upd2(UpdArgs a) {
 #pragma unroll
     for (int u = 0; u < NGI; ++u) {
       const int e = (wave * NGI + u) * 64 + lane, row = e / PERROW, m = itn * R + row;
+#ifdef PPO_DIAG
+      const int p = a.perm[min(a.hot ? m % (8 * R) : m, M - 1)];  // diagnostic: L2-resident rows
+#else
       const int p = a.perm[min(m, M - 1)];  // unconditional (clamped), masked below
+#endif
       pm[u] = (itn < ntiles && m < M) ? p : -1;
     }
   };

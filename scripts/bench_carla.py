@@ -57,7 +57,7 @@ def main():
                           "tflops": round(n * FLOP_PER_SAMPLE / dt / 1e12, 2)}), flush=True)
         ag.close()
     for n in args.update_batch:
-        ag = ppo_amd.CarlaAgent(max_batch=n)
+        ag = ppo_amd.CarlaAgent(max_batch=n, options=args.options or None)
         ag.load_params(p)
         rng = np.random.default_rng(1)
         bev = rng.integers(0, 256, size=(n, 15, 192, 192), dtype=np.uint8)
@@ -73,7 +73,7 @@ def main():
             ag.update(*d, want_stats=False)
         ppo_amd.lib().ppo_device_sync()
         dt = (time.perf_counter() - t0) / its
-        print(json.dumps({"workload": "carla_update", "batch": n, "ms_per_update": round(dt * 1e3, 3),
+        print(json.dumps({"workload": "carla_update", "batch": n, "options": args.options, "ms_per_update": round(dt * 1e3, 3),
                           "samples_per_s": round(n / dt, 1),
                           "tflops": round(3 * n * FLOP_PER_SAMPLE / dt / 1e12, 2)}), flush=True)
         ag.close()

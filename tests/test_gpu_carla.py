@@ -130,13 +130,64 @@ def test_staged_conv1_kernels_match_generic():
     np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-7)
 
 
+def test_packed_conv1_matches_staged():
+    """conv1=packed (k_conv_img3: the taps of a 16-wide MFMA k block ordered so that each lane group's
+    four k-steps are four consecutive patch bytes of one kernel row, one ds_read_b32 per B quadruple,
+    A operands from a pre-arranged weight table) computes every product as k_conv_img2 does (u8 / 255
+    times the same weight) in another k order: forward outputs within fp32 summation noise of the
+    staged kernel (n = 7, partial tiles; every sampling mode), the update's gradients per tensor
+    within rel-L2 1e-5, the stepped parameters within 1e-6. Golden / oracle / torch parity of the
+    packed path itself: the module tests above run on the default conv1 form."""
+    import carla_torch_ref  # noqa: F401
+    n = 7
+    L = CI.layout()
+    p = CI.params(L)
+    bev, meas, vmeas, act = CI.inputs(n)
+    rng = np.random.default_rng(4)
+    old_logp = rng.normal(-2.0, 0.3, n).astype(np.float32)
+    adv = rng.normal(0.0, 1.0, n).astype(np.float32)
+    ret = rng.normal(0.0, 1.0, n).astype(np.float32)
+    old_v = rng.normal(0.0, 1.0, n).astype(np.float32)
+    outs = []
+    for opt in ("conv1=staged", "conv1=packed"):
+        ag = ppo_amd.CarlaAgent(max_batch=16, seed=7, options=opt)
+        ag.load_params(p)
+        res = [run(ag, bev, meas, vmeas, mode=m, env_base=3, step_id=5) for m in ("sample", "mean", "roach")]
+        res.append(run(ag, bev, meas, vmeas, act))
+        d = [DeviceArray.from_numpy(bev, np.uint8)] + [DeviceArray.from_numpy(np.ascontiguousarray(x, np.float32))
+                                                       for x in (meas, vmeas, act, old_logp, adv, ret, old_v)]
+        ag.update(*d, lr=3e-4, clip_coef=0.2, ent_coef=0.01, vf_coef=0.5, max_grad_norm=0.5, adam_eps=1e-5)
+        res.append([ag.last_grad(), ag.params()])
+        outs.append(res)
+        ag.close()
+    for r0, r1 in zip(outs[0][:4], outs[1][:4]):
+        for x0, x1 in zip(r0, r1):
+            np.testing.assert_allclose(x1, x0, rtol=2e-5, atol=2e-6)
+    (g0, p0), (g1, p1) = outs[0][4], outs[1][4]
+    for t in range(L.ntensors):
+        o, m = L.t_off[t], L.t_len[t]
+        nr = np.linalg.norm(g0[o:o + m])
+        if nr > 0:
+            r = np.linalg.norm((g1[o:o + m] - g0[o:o + m]).astype(np.float64)) / nr
+            assert r < 1e-5, (t, r)
+    # Adam's first step normalises g / |g|: a few near-zero gradient entries move by up to ~lr / 1000
+    np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-6)
+
+
 def test_unaligned_image_pointer(carla):
-    """The staged first-layer kernels load the uint8 image as dwords: an image pointer that is not
-    4-byte aligned takes the generic gather path and gives the same outputs, bitwise."""
-    ag = carla[0]
+    """The staged / packed first-layer kernels load the uint8 image as dwords: an image pointer that is
+    not 4-byte aligned takes the generic gather path. It gives the staged kernel's outputs bitwise
+    (conv1=staged keeps k_conv's MFMA chains), and the default (packed) outputs within fp32 noise."""
+    ag, L, p = carla[0], carla[1], carla[2]
     n = 3
     bev, meas, vmeas, _ = CI.inputs(n)
-    ref = run(ag, bev, meas, vmeas, mode="mean")
+    packed = run(ag, bev, meas, vmeas, mode="mean")
+    ag_s = ppo_amd.CarlaAgent(max_batch=16, seed=7, options="conv1=staged")
+    ag_s.load_params(p)
+    ref = run(ag_s, bev, meas, vmeas, mode="mean")
+    ag_s.close()
+    for r, o in zip(ref, packed):
+        np.testing.assert_allclose(o, r, rtol=2e-5, atol=2e-6)
     raw = np.zeros(bev.size + 4, np.uint8)
     raw[1:1 + bev.size] = bev.ravel()
     buf = DeviceArray.from_numpy(raw, np.uint8)

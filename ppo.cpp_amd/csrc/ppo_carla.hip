@@ -2125,6 +2125,8 @@ WgradPlan plan_wgrad(int OC, int Kt, long Q) {
 // dW[oc][ic, ky, kx] = D[oc][(ic, ky, kx)] + D[oc + 8][(ic, ky, kx + S)] (bias: both halves).
 // 25 % fewer MFMAs than k_wgrad_img; the pixel sum is split into its even and odd halves, so the
 // result differs from k_wgrad's in rounding only. The combine runs once per workgroup through LDS.
+// The B operands are the raw byte values (exact in fp32) and the workgroup's tap sums are scaled by
+// 1 / 255 once in the combine (round 5: one VALU fewer per MFMA; the bias column is not scaled).
 constexpr int kWimg2CT = 9;  // column tiles per wave: 4 x 9 x 16 = 576 >= IC K (K + S) + 1 = 526
 static size_t wimg2_lds_bytes(int IC, int K, int S, int OC) {
   const int TI = (kImgTile - 1) * S + K, TIP = (TI + 3) & ~3;
@@ -2195,7 +2197,7 @@ __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, in
 #pragma unroll
       for (int u = 0; u < kWimg2CT; ++u) {
         const int raw = tile[ko[u] + po];
-        const float xv = (float)raw * (1.0f / 255.0f);
+        const float xv = (float)raw;  // the image's 1 / 255 is applied once, in the combine below
         // the bias and padding columns lie in the last 4 tiles of the last wave (launch condition)
         const float bv = u >= kWimg2CT - 4 ? (cb[u] < 0.0f ? xv : cb[u]) : xv;
         acc[u] = mfma16(av, bv, acc[u]);
@@ -2220,7 +2222,7 @@ __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, in
     } else {
       const int ic = k / (K * K), rem = k - ic * (K * K), ky = rem / K, kx = rem - ky * K;
       const int c = (ic * K + ky) * KX + kx;
-      v = dl[oc * NC + c] + dl[(oc + 8) * NC + c + S];
+      v = (dl[oc * NC + c] + dl[(oc + 8) * NC + c + S]) * (1.0f / 255.0f);
     }
     out[e] = v;
   }

@@ -1623,6 +1623,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
     kc[u] = k < a.Kt ? 0 : (k == a.Kt ? 1 : 2);
     ko[u] = k < a.Kt ? koff[k] : 0;
   }
+  // fp32 input: the gathers go through a buffer descriptor with 32-bit byte offsets (the whole
+  // minibatch's activations are < 4 GB, launch condition): column byte offsets ko4 (a value far past
+  // the buffer for the bias / padding columns) plus the pixel's byte offset xb4 (also far past the
+  // buffer for pixels past the chunk), so a column reads 0 out of range instead of through a select
+  // and 64-bit address arithmetic (round 5: 15 VALU per MFMA before, SQ counters)
+  constexpr uint32_t kFar = 0x70000000u;
+  uint32_t ko4[NKT];
+#pragma unroll
+  for (int u = 0; u < NKT; ++u) ko4[u] = kc[u] == 0 ? (uint32_t)ko[u] * 4u : kFar;
+  const PBuf xbuf{__builtin_amdgcn_make_buffer_rsrc((void*)(U8 ? (const void*)a.x_u8 : (const void*)a.x_f), (short)0,
+                                                    (int)(U8 ? 0 : (uint32_t)min((long)a.n * a.x_stride * 4, (long)kFar)),
+                                                    0x00020000)};
   // The dZ operand (the A side) is the same for the workgroup's 4 waves: each iteration's
   // 16 NOT x 4 U tile is loaded once per workgroup (element e = tid + 256 h: channel e / (4 U),
   // pixel qb + e % (4 U), consecutive threads on consecutive pixels) and staged in LDS in A-operand
@@ -1680,19 +1692,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
 #pragma unroll
     for (int st = 0; st < U; ++st) {
       const bool qv = q < qe;
-      const long xb = s * a.x_stride + (qv ? pbase[p] : 0);
+      if constexpr (U8) {
+        const long xb = s * a.x_stride + (qv ? pbase[p] : 0);
 #pragma unroll
-      for (int u = 0; u < NKT; ++u) {
-        const bool ok = qv && kc[u] == 0;
-        const long off = ok ? xb + ko[u] : 0;
-        float v;
-        if constexpr (U8) {
+        for (int u = 0; u < NKT; ++u) {
+          const bool ok = qv && kc[u] == 0;
+          const long off = ok ? xb + ko[u] : 0;
           const int raw = a.x_u8[off];
-          v = (float)(ok ? raw : 0) * (1.0f / 255.0f);
-        } else {
-          v = a.x_f[off] * (ok ? 1.0f : 0.0f);
+          const float v = (float)(ok ? raw : 0) * (1.0f / 255.0f);
+          bv[st][u] = (qv && kc[u] == 1) ? 1.0f : v;
         }
-        bv[st][u] = (qv && kc[u] == 1) ? 1.0f : v;
+      } else {
+        const uint32_t xb4 = qv ? (uint32_t)(s * a.x_stride + pbase[p]) * 4u : kFar;
+#pragma unroll
+        for (int u = 0; u < NKT; ++u) {
+          const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xbuf.r, xb4 + ko4[u], 0, 0));
+          bv[st][u] = (qv && kc[u] == 1) ? 1.0f : v;
+        }
       }
       q += 4;
       p += 4;
@@ -2230,6 +2246,7 @@ __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, in
 
 int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap, hipStream_t s, bool img = true) {
   if (a.Kt > kMaxKTab || a.OP > kMaxPTab) return -1;
+  if (!a.x_u8 && (long)a.n * a.x_stride * 4 >= 0x70000000L) return -1;  // k_wgrad's 32-bit buffer offsets
   const long per = (long)a.OC * (a.Kt + 1);
   const int OH = a.OP / a.OW;
   if (img && a.x_u8 && ((uintptr_t)a.x_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 8 &&

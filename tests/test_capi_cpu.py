@@ -146,7 +146,7 @@ lib = ppo_amd.lib()
 out = []
 for opt in ("upd_kernel=fast", "act_kernel=3", "bogus=1", "dw_fused", "rollout=sometimes", "dw_dma=2",
             "dw_rows=24", "dw_rows=0", "dw_rows=x", "dw_rows=99999999999", "dw_slices=3", "update_graph=2",
-            "upd2_split=1", "rollout_kernel=fast", "upd_mfma=8"):
+            "upd2_split=1", "rollout_kernel=fast", "upd_mfma=8", "dw_mfma=bf16", "dw_mfma=x9"):
     cfg = ppo_amd.HipConfig(net_kind=1, obs_dim=17, act_dim=6, hidden=256, num_envs=64, num_steps=8,
                             num_minibatches=1, update_epochs=1)
     ctx = ctypes.c_void_p()
@@ -181,3 +181,25 @@ def test_ac_cli_refuses_a_rank_without_a_gpu_id(tmp_path):
                        capture_output=True, text=True, timeout=60, env=env, cwd=tmp_path)
     assert r.returncode == 2, (r.returncode, r.stdout, r.stderr)
     assert "local rank 1 has no entry in --gpu_ids" in r.stderr
+
+
+def test_ac_cli_refuses_dd_ppo_on_the_device_env(tmp_path):
+    """DD-PPO preemption stops per-env collection threads early (ac:680-689); the device-resident
+    rollout has none, so the CLI refuses the combination before any HIP call (exit 1)."""
+    import subprocess
+    exe = os.path.join(ROOT, "ppo.cpp_amd", "bin", "ac_ppo_continuous_action")
+    r = subprocess.run([exe, "--env_backend", "device", "--use_dd_ppo_preempt", "1", "--total_timesteps", "1024",
+                        "--exp_name_stem", "refuse_dd"], capture_output=True, text=True, timeout=60, cwd=tmp_path)
+    assert r.returncode == 1, (r.returncode, r.stdout, r.stderr)
+    assert "use_dd_ppo_preempt needs host envs" in r.stderr
+
+
+def test_ac_cli_flags_of_round_5(tmp_path):
+    """The AC CLI lists the collection flags (host cost per env step, straggler cost, group count with
+    its automatic default) and estimate_mean_std in its --help, as args.hxx prints flags."""
+    import subprocess
+    exe = os.path.join(ROOT, "ppo.cpp_amd", "bin", "ac_ppo_continuous_action")
+    r = subprocess.run([exe, "--help"], capture_output=True, text=True, timeout=60, cwd=tmp_path)
+    assert r.returncode == 0
+    for flag in ("host_step_us", "straggler_us", "num_collect_groups", "estimate_mean_std", "use_dd_ppo_preempt"):
+        assert flag in r.stdout, flag

@@ -154,6 +154,7 @@ struct ppo_ctx {
   int tiles_per_block = 1, nblk = 1;
   bool use_upd = false;  // feature-split k_upd (ppo_update.hip) instead of k_fwdbwd
   bool use_upd32 = false;  // k_upd32 (32x32x2 MFMAs) instead of k_upd (create option upd_mfma)
+  int upd_bx = 0;          // 1: k_upd's 256-wide GEMMs as split-bf16 piece products (upd_mfma=bx6)
   int upd32_mix = 0;       // k_upd32 with the actor trunk on k_upd's body (upd_mfma=mix)
   bool use_upd2 = false;  // two-trunk k_upd2 (ppo_update_narrow.hip, H = 64 tanh agent)
   int rollout_kernel = 0;   // AC persistent rollout: 0 auto, 1 k_rollout (MFMA), 2 k_rollout_v (VALU)
@@ -286,7 +287,8 @@ struct CreateOptions {
   int rollout_kernel = 0;  // 0 auto, 1 mfma (k_rollout), 2 valu (k_rollout_v)
   int upd2_split = -1;  // -1 auto (= kUpd2SplitAuto: the single k_upd2), 0 one k_upd2, 2 / 3 split at 2 / 3 workgroups per CU
   int upd_mfma = 0;     // 0 auto, 16: k_upd (16x16x4 MFMAs), 32: k_upd32 (32x32x2; LayerNorm-Beta agent, H = 256),
-                        // 1: k_upd32's mixed form (critic 32x32x2, actor 16x16x4)
+                        // 1: k_upd32's mixed form (critic 32x32x2, actor 16x16x4),
+                        // 6: bx6, k_upd with its 256-wide GEMMs as split-bf16 piece products (k_upd<.., BX>)
 };
 // auto = the single k_upd2: the split form measured slower on cfg2 (round 4, profiles/r04/cfg2_split/:
 // 101.3 vs 92.9 ms per iteration; k_l1g 66 us = 0.61 of peak per launch, the tail 94 us at 3 per CU)
@@ -323,8 +325,8 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
     else if (k == "rollout_kernel" && (v == "auto" || v == "mfma" || v == "valu"))
       o->rollout_kernel = v == "auto" ? 0 : v == "mfma" ? 1 : 2;
     else if (k == "upd2_split" && (v == "auto" || v == "0" || v == "2" || v == "3")) o->upd2_split = v == "auto" ? -1 : v[0] - '0';
-    else if (k == "upd_mfma" && (v == "auto" || v == "16" || v == "32" || v == "mix"))
-      o->upd_mfma = v == "auto" ? 0 : v == "mix" ? 1 : atoi(v.c_str());
+    else if (k == "upd_mfma" && (v == "auto" || v == "16" || v == "32" || v == "mix" || v == "bx6"))
+      o->upd_mfma = v == "auto" ? 0 : v == "mix" ? 1 : v == "bx6" ? 6 : atoi(v.c_str());
     else return fail("ppo_create_ex: unknown option or value: " + kv);
   }
   return 0;
@@ -422,7 +424,8 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   const size_t PS = c->K.size;
   rc |= dmalloc(&c->P, PS); rc |= dmalloc(&c->G, PS); rc |= dmalloc(&c->Am, PS); rc |= dmalloc(&c->Av, PS);
   for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->W2T[k], (size_t)H * H);
-  for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->WSW[k], (size_t)sw_size(H, c->K.OP));
+  // H = 256: room for the split-bf16 pieces of W2 | W2^T after the fp32 copies (upd_mfma=bx6)
+  for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->WSW[k], (size_t)(sw_size(H, c->K.OP) + (H == 256 ? bx_size(H) : 0)));
   const size_t E = cfg->num_envs, T = cfg->num_steps;
   rc |= dmalloc(&c->buf[PPO_BUF_OBS], T * E * O);
   rc |= dmalloc(&c->buf[PPO_BUF_ACTIONS], T * E * A);
@@ -453,6 +456,10 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
       ppo_destroy(c);
       return fail("ppo_create: upd_mfma=32 / mix needs the LayerNorm-Beta agent at hidden 256");
     }
+    if (opt.upd_mfma == 6 && (H != 256 || cfg->net_kind != PPO_NET_LN_BETA)) {
+      ppo_destroy(c);
+      return fail("ppo_create: upd_mfma=bx6 needs the LayerNorm-Beta agent at hidden 256 with at most 16 heads");
+    }
     if (opt.upd2_split > 0 && (upd_kernel || !fits32 || !upd2_split_supported(c->K))) {
       ppo_destroy(c);
       return fail("ppo_create: upd2_split needs the 64-wide agent with O % 4 == 0, OP = 384 and 32-bit storage offsets");
@@ -470,6 +477,14 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
         return fail("ppo_create: upd_mfma=32 / mix needs the LayerNorm-Beta agent at hidden 256");
       }
       c->use_upd = c->use_upd32 = true;
+      c->upd_nblk = std::min((c->M + c->upd.rows - 1) / c->upd.rows, 256);
+    } else if (opt.upd_mfma == 6) {
+      if (upd_kernel || upd_supported(c->K, c->sg[1].nh, c->sg[0].size, c->sg[1].size, &c->upd, 1) != 0) {
+        ppo_destroy(c);
+        return fail("ppo_create: upd_mfma=bx6 needs the LayerNorm-Beta agent at hidden 256 with at most 16 heads");
+      }
+      c->use_upd = true;
+      c->upd_bx = 1;
       c->upd_nblk = std::min((c->M + c->upd.rows - 1) / c->upd.rows, 256);
     } else if (!upd_kernel && upd_supported(c->K, c->sg[1].nh, c->sg[0].size, c->sg[1].size, &c->upd) == 0) {
       c->use_upd = true;
@@ -577,7 +592,7 @@ extern "C" float* ppo_buffer(ppo_t* c, int which) {
 static int refresh_weight_copies(ppo_t* c) {
   for (int k = 0; k < 2; ++k) launch_transpose(c->P + c->K.tr[k].W2, c->W2T[k], c->K.H, c->stream);
   for (int k = 0; k < 2; ++k)
-    launch_swizzle(c->P + c->K.tr[k].W1, c->P + c->K.tr[k].W2, c->WSW[k], c->K.H, c->K.OP, c->stream);
+    launch_swizzle(c->P + c->K.tr[k].W1, c->P + c->K.tr[k].W2, c->WSW[k], c->K.H, c->K.OP, c->upd_bx, c->stream);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -868,6 +883,7 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
   u.W2T[1] = c->W2T[1];
   u.WSW[0] = c->WSW[0];
   u.WSW[1] = c->WSW[1];
+  u.bx = c->upd_bx;
   u.K = c->K;
   u.sg[0] = c->sg[0];
   u.sg[1] = c->sg[1];
@@ -1004,6 +1020,7 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
     ad.w1_off[k] = c->K.tr[k].W1;
     ad.wsw[k] = c->WSW[k];
   }
+  ad.bx = c->upd_bx;
   const long trainable_n = c->K.size - tb;
 
   // the minibatch launch sequence; with graph, the Adam step constants come from c->sched[gi]

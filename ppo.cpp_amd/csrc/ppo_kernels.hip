@@ -1252,21 +1252,9 @@ __global__ __launch_bounds__(512) void k_dwf_dma(DwArgs a) {
 // the same count as k_dwf_dma's 8 k-steps) and splits each value once (v_and / v_sub / v_perm).
 // Staging (LDS DMA, three buffers, two stages ahead) is k_dwf_dma's.
 // =============================================================================================
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 struct Split3 {
   u32x4 hi, mid, lo;
 };
-// two fp32 values -> their (hi, mid, lo) bf16 pieces, packed (x0 in the low half)
-PPO_DEV void split3_pair(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
-  const unsigned u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
-  const float r0 = x0 - __uint_as_float(u0 & 0xffff0000u), r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
-  const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
-  const float l0 = r0 - __uint_as_float(v0 & 0xffff0000u), l1 = r1 - __uint_as_float(v1 & 0xffff0000u);
-  hi = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
-  mid = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
-  lo = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
-}
 PPO_DEV Split3 split3(const float (&x)[8]) {
   Split3 s;
 #pragma unroll
@@ -1585,6 +1573,16 @@ PPO_DEV void adam_block(const AdamArgs& a, int bid, float* s_norm, float& s_coef
         float* w = a.wsw[k] + (long)a.H * a.OP;
         w[sw_index(r, cI, a.H)] = np;
         w[(long)a.H * a.H + sw_index(cI, r, a.H)] = np;
+        if (a.bx) {  // split-bf16 pieces of W2 | W2^T (bx_index), after the fp32 copies
+          uint16_t* pw = reinterpret_cast<uint16_t*>(a.wsw[k] + sw_size(a.H, a.OP));
+          uint16_t pc[3];
+          split3_bits(np, pc);
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            pw[bx_index(r, cI, a.H, q)] = pc[q];
+            pw[3L * a.H * a.H + bx_index(cI, r, a.H, q)] = pc[q];
+          }
+        }
       }
     }
     const long o1 = p - a.w1_off[k];
@@ -1612,8 +1610,9 @@ __global__ __launch_bounds__(256) void k_gradstep(NormArgs na, AdamArgs a, unsig
 }
 
 // swizzled copies of one trunk (sw_index): [W1 (H x OP) | W2 (H x H) | W2^T (H x H)]
+// bx: also the split-bf16 pieces of W2 | W2^T (bx_index) after them
 __global__ void k_swizzle(const float* __restrict__ w1, const float* __restrict__ w2, float* __restrict__ dst, int H,
-                          int OP) {
+                          int OP, int bx) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long n1 = (long)H * OP, n2 = (long)H * H;
   if (i < n1) {
@@ -1623,6 +1622,15 @@ __global__ void k_swizzle(const float* __restrict__ w1, const float* __restrict_
     const int r = (int)(o / H), c = (int)(o % H);
     dst[n1 + sw_index(r, c, H)] = w2[o];
     dst[n1 + n2 + sw_index(c, r, H)] = w2[o];
+    if (bx) {
+      uint16_t* pw = reinterpret_cast<uint16_t*>(dst + sw_size(H, OP));
+      uint16_t pc[3];
+      split3_bits(w2[o], pc);
+      for (int q = 0; q < 3; ++q) {
+        pw[bx_index(r, c, H, q)] = pc[q];
+        pw[3 * n2 + bx_index(c, r, H, q)] = pc[q];
+      }
+    }
   }
 }
 
@@ -2151,9 +2159,9 @@ void launch_adam(const AdamArgs& a, hipStream_t s) {
 void launch_transpose(const float* src, float* dst, int H, hipStream_t s) {
   hipLaunchKernelGGL(k_transpose, dim3((H * H + 255) / 256), dim3(256), 0, s, src, dst, H);
 }
-void launch_swizzle(const float* w1, const float* w2, float* dst, int H, int OP, hipStream_t s) {
+void launch_swizzle(const float* w1, const float* w2, float* dst, int H, int OP, int bx, hipStream_t s) {
   const long n = (long)H * OP + (long)H * H;
-  hipLaunchKernelGGL(k_swizzle, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w1, w2, dst, H, OP);
+  hipLaunchKernelGGL(k_swizzle, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w1, w2, dst, H, OP, bx);
 }
 void launch_gae(const GaeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_gae, dim3((a.E + 255) / 256), dim3(256), 0, s, a);

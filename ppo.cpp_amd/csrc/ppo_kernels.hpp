@@ -47,6 +47,45 @@ PPO_DEV_HOST inline long sw_index(int r, int c, int ncols) {
 }
 PPO_DEV_HOST inline long sw_size(int H, int OP) { return (long)H * OP + 2L * H * H; }
 
+// Split-bf16 pieces. Every fp32 x is the exact sum of three bf16 numbers: hi = x with the low 16
+// bits cleared (truncation), r = x - hi (exact: a prefix of x's significand is removed), mid = r
+// truncated the same way, lo = r - mid (exact, at most 8 significant bits: a bf16). A product a.b is
+// then a sum of piece products, each exact in fp32.
+PPO_DEV_HOST inline void split3_bits(float x, uint16_t (&pc)[3]) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, x);
+  const float r = x - __builtin_bit_cast(float, u & 0xffff0000u);
+  const uint32_t v = __builtin_bit_cast(uint32_t, r);
+  const float l = r - __builtin_bit_cast(float, v & 0xffff0000u);
+  pc[0] = (uint16_t)(u >> 16);
+  pc[1] = (uint16_t)(v >> 16);
+  pc[2] = (uint16_t)(__builtin_bit_cast(uint32_t, l) >> 16);
+}
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// two fp32 values -> their (hi, mid, lo) pieces, packed (x0 in the low half); split3_bits per value
+PPO_DEV void split3_pair(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
+  const unsigned u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
+  const float r0 = x0 - __uint_as_float(u0 & 0xffff0000u), r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
+  const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
+  const float l0 = r0 - __uint_as_float(v0 & 0xffff0000u), l1 = r1 - __uint_as_float(v1 & 0xffff0000u);
+  hi = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+  mid = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
+  lo = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
+}
+
+// Piece copies of W2 | W2^T for k_upd's split-bf16 GEMMs (create option upd_mfma=bx6), stored after a
+// trunk's fp32 swizzled copies (H = 256 contexts). Element (r, c) of an [NR][NC] matrix, piece p, sits
+// (in bf16 units) where lane (j, g) = j + 16 g reads it as the v_mfma_f32_16x16x32_bf16 A operand of
+// feature block r >> 4 and 32-wide k block c >> 5: element e = 4 ((c >> 4) & 1) + (c & 3) of the
+// lane's 16-byte piece p, i.e. lane k slot 8 g + e holds column 32 kk + 16 (e >> 2) + 4 g + (e & 3) —
+// the columns k_upd's 16x16x4 form gives lane group g in its two k-blocks 2 kk, 2 kk + 1. One
+// wave-load of a piece is 1 KB contiguous.
+PPO_DEV_HOST inline long bx_index(int r, int c, int ncols, int p) {
+  const int lane = (r & 15) + 16 * ((c & 15) >> 2), e = 4 * ((c >> 4) & 1) + (c & 3);
+  return ((((long)(r >> 4) * (ncols >> 5) + (c >> 5)) * 3 + p) * 64 + lane) * 8 + e;
+}
+PPO_DEV_HOST inline long bx_size(int H) { return 3L * H * H; }  // floats: W2 | W2^T pieces
+
 struct UpdArgs {
   const float* P;
   const float* W2T[2];
@@ -73,6 +112,7 @@ struct UpdArgs {
   int trunk_mask;         // k_upd: trunks to run (bit t = trunk t; 3 = both; other values: PPO_DIAG builds only)
   int sched;              // k_upd: bit 0 actor workgroups dispatched first, bit 1 actor wave priority
   int hot;                // diagnostic build only (PPO_UPD2_HOT): k_upd2 gathers the rows of its first 8 tiles only
+  int bx;                 // k_upd: 1 runs the 256-wide GEMMs as split-bf16 piece products (upd_mfma=bx6)
 };
 
 // k_upd geometry (ppo_update.hip)
@@ -156,6 +196,7 @@ struct AdamArgs {
   // step_size / sbc2, so the captured launch sequence stays valid across iterations
   const float* sched;
   int gi;
+  int bx;  // 1: also refresh the split-bf16 pieces of W2 | W2^T (bx_index) after each wsw copy
 };
 
 struct GaeArgs {
@@ -247,7 +288,8 @@ int launch_act3(const ActArgs& a, hipStream_t s);
 int launch_act4(const ActArgs& a, hipStream_t s);  // ppo_act_narrow.hip (H = 64 tanh agent)
 int launch_fwdbwd(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s);
 int fwdbwd_set_lds(const PackedLayout& K, size_t lds_bytes);
-int upd_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g);
+// bx = 1: the split-bf16 form (k_upd<..., BX = 1>; LayerNorm-Beta agent, H = 256, one head tile)
+int upd_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g, int bx = 0);
 int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s);
 // k_upd32 (create option upd_mfma=32 | mix): k_upd on 32x32x2 MFMAs, LayerNorm-Beta agent at
 // H = 256; mix = 1: only the critic trunk on 32x32x2, the actor on k_upd's body
@@ -285,7 +327,7 @@ PPO_DEV void grid_barrier(unsigned* bar, unsigned target) {
 }
 void launch_adam(const AdamArgs& a, hipStream_t s);
 void launch_transpose(const float* src, float* dst, int H, hipStream_t s);
-void launch_swizzle(const float* w1, const float* w2, float* dst, int H, int OP, hipStream_t s);
+void launch_swizzle(const float* w1, const float* w2, float* dst, int H, int OP, int bx, hipStream_t s);
 void launch_gae(const GaeArgs& a, hipStream_t s);
 void launch_perm(int32_t* out, uint32_t B, const PermKey& pk, hipStream_t s);
 void launch_adv_sum(const AdvArgs& a, hipStream_t s);

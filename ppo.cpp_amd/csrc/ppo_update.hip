@@ -64,9 +64,10 @@ __device__ unsigned long long g_upd_stamps[1024 * 4 * PPO_STAMP_TILES * PPO_STAM
 
 namespace {
 
-template <int H_, int NTO_, int NHT_>
+template <int H_, int NTO_, int NHT_, bool BX_ = false>
 struct Geo {
   static constexpr int H = H_, NT = H / 16;
+  static constexpr bool BX = BX_;
   static constexpr int WF = (H >= 256) ? 4 : 1;  // wave feature groups
   static constexpr int WR = 4 / WF;              // wave row groups
   static constexpr int FT = NT / WF;             // 16-feature tiles per wave
@@ -78,17 +79,29 @@ struct Geo {
   static constexpr int LDA = ((H + 63) / 64) * 64 + 4;
   static constexpr int LDG = NHP + 4;
   static constexpr int ITS = 10;  // floats per (row, action) item
+  // BX: split-bf16 activation rows (3 pieces x H bf16 + 16 B, row stride 4 mod 64 banks like LDA),
+  // in the same region as the fp32 h2 rows the actor's head backward reads
+  static constexpr int LDB = 3 * (H / 2) + 4;
+  static constexpr int LDU = (BX && LDB > LDA) ? LDB : LDA;
   // static part of the LDS carve (floats); the runtime part (items, rows, accumulators) follows
   static constexpr int oXN = 0;
   static constexpr int oACT = oXN + R * LDX;
-  static constexpr int oRED = oACT + R * LDA;        // 4 slots x WF x R
-  static constexpr int oPRE = oRED + 4 * WF * R;     // R x LDG head pre-activations
-  static constexpr int oG = oPRE + R * LDG;          // R x LDG head gradients
-  static constexpr int oROW = oG + R * LDG;          // R x 8 per-row scalars
-  static constexpr int oSCR = oROW + R * 8;          // head partials (WF x NHP x R) / items (R x A x ITS)
+  static constexpr int oRED = oACT + R * LDU;        // 4 slots x WF x R
+  // BX: the per-tile regions whose lifetime lies between the layer-2 GEMM's last piece read and the
+  // dz2 piece writes — head partials / loss items (SCR), head pre-activations (PRE) and gradients
+  // (GG, re-zeroed every tile) — sit in the activation region behind the fp32 h2 rows, which keeps
+  // two workgroups and the LDS accumulators on a CU
+  static constexpr int SCRB = (WF * NHP * R > R * (NHP / 2) * ITS) ? WF * NHP * R : R * (NHP / 2) * ITS;
+  static constexpr int oSCR = BX ? oACT + R * LDA : oRED + 4 * WF * R + 2 * R * LDG + R * 8;
+  static constexpr int oPRE = BX ? oSCR + SCRB : oRED + 4 * WF * R;  // R x LDG head pre-activations
+  static constexpr int oG = oPRE + R * LDG;                          // R x LDG head gradients
+  static constexpr int oROW = BX ? oRED + 4 * WF * R : oG + R * LDG; // R x 8 per-row scalars
+  static constexpr int SCR_MAX = BX ? SCRB : 1 << 30;  // floats SCR (head partials / items) may take
   // staged small parameters: LayerNorm gamma/beta of both layers, head biases, observation
   // mean / std (placed after the runtime-sized regions)
   static constexpr int NSPAR = 4 * H + NHP + 2 * OP;
+  static_assert(!BX || oG + R * LDG <= oACT + R * LDU, "BX: SCR / PRE / GG must fit behind the h2 rows");
+  static_assert(BX || oSCR == oROW + R * 8, "carve");
 };
 
 PPO_DEV float lds_f(const float* p) { return *p; }
@@ -136,6 +149,89 @@ PPO_DEV void mm_fr(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* in) {
         for (int rt = 0; rt < RT; ++rt) out[ft][rt] = mfma16(w[kb & 1][ft][c], b[rt][c], out[ft][rt]);
     }
   }
+}
+
+// Split-bf16 form of the 256-wide GEMMs (create option upd_mfma=bx6, BX = 1): out[ft][rt] (+)= the
+// same sum as mm_fr over k in [0, 16 NKB), as v_mfma_f32_16x16x32_bf16 piece products. A = the
+// weights' pieces (bx_index copies: hi, mid, lo of every fp32 weight, written by k_adam), B = the
+// activations' pieces (split once when the tile is written to LDS, lds_store_pieces). Of the nine
+// piece products six are kept: lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi (smallest first); the
+// dropped mid.lo + lo.mid + lo.lo are < 2^-23 |a b| (below the rounding of an fp32 accumulation over
+// K = 256 terms). One 16x16x32 MFMA takes 16 cycles for 32 k against 8 x 32 cycles of 16x16x4 f32:
+// six are 0.375 of the fp32 MFMA time. Lane (j, g) k slot 8 g + e <-> column 32 kk + 16 (e >> 2) +
+// 4 g + (e & 3), the columns mm_fr gives lane group g in k-blocks 2 kk and 2 kk + 1, so the
+// accumulator layout is mm_fr's.
+//   inb = ACTB + (rbase + j) LDB + 4 g (floats; row = 3 pieces x H bf16 + 16 B, piece p at 128 p floats)
+//   weight unit (kk, ft): 3 x 16 B per lane at wlane + 256 ((ft NKK + kk) 3 + p) floats
+// A pieces stream through a ring of NS units (D = NS - 1 ahead, ~ one 32-k block of every feature tile).
+#ifndef PPO_BX_D
+#define PPO_BX_D 3
+#endif
+#ifndef PPO_HWG_FORCE
+#define PPO_HWG_FORCE 0
+#endif
+PPO_DEV f4 mfma16bx(u32x4 a, u32x4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+PPO_DEV u32x4 pld4u(PBuf b, int lane_floats, int uni_floats) { return __builtin_bit_cast(u32x4, pld4(b, lane_floats, uni_floats)); }
+template <int FT, int RT, int NKB, int LDB>
+PPO_DEV void mm_bx(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* inb) {
+  static_assert(NKB % 2 == 0, "mm_bx: 32-wide k blocks");
+  constexpr int NKK = NKB / 2, U = NKK * FT, D = PPO_BX_D, NS = D + 1, PS = 8 * NKB;
+  u32x4 ar[NS][3];
+  auto load_unit = [&](int u, u32x4 (&dst)[3]) {
+    const int kk = u / FT, ft = u - kk * FT;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) dst[p] = pld4u(wb, wlane, 256 * ((ft * NKK + kk) * 3 + p));
+  };
+#pragma unroll
+  for (int u = 0; u < D; ++u) load_unit(u, ar[u]);
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) {
+    u32x4 bs[RT][3];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bs[rt][p] = __builtin_bit_cast(u32x4, lds_f4(inb + 16 * rt * LDB + PS * p + 16 * kk));
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      const int u = kk * FT + ft;
+      if (u + D < U) load_unit(u + D, ar[(u + D) % NS]);
+      // pin the prefetch here: the scheduler otherwise sinks it next to its use
+      __builtin_amdgcn_sched_barrier(0);
+      const u32x4(&av)[3] = ar[u % NS];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        f4 acc = out[ft][rt];
+        acc = mfma16bx(av[2], bs[rt][0], acc);
+        acc = mfma16bx(av[0], bs[rt][2], acc);
+        acc = mfma16bx(av[1], bs[rt][1], acc);
+        acc = mfma16bx(av[1], bs[rt][0], acc);
+        acc = mfma16bx(av[0], bs[rt][1], acc);
+        out[ft][rt] = mfma16bx(av[0], bs[rt][0], acc);
+      }
+    }
+  }
+}
+// the tile's activations as split-bf16 pieces: lane (j, g) holds row rbase + 16 rt + j, features
+// f = fbase + 16 ft + 4 g + r; feature f of a row sits at bf16 position 32 (f >> 5) + 8 g + 4 ((f >> 4) & 1)
+// + r of each piece (mm_bx's k slots), so a lane writes 8 bytes per piece
+template <int FT, int RT, int LDB, int PS>
+PPO_DEV void lds_store_pieces(float* actb, const f4 (&v)[FT][RT], int rbase, int fbase, int j, int g) {
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      const int f0 = fbase + 16 * ft;
+      float* q = actb + (rbase + 16 * rt + j) * LDB + 16 * (f0 >> 5) + 4 * g + 2 * ((f0 >> 4) & 1);
+      unsigned h0, m0, l0, h1, m1, l1;
+      split3_pair(v[ft][rt][0], v[ft][rt][1], h0, m0, l0);
+      split3_pair(v[ft][rt][2], v[ft][rt][3], h1, m1, l1);
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2*>(q) = u32x2{h0, h1};
+      *reinterpret_cast<u32x2*>(q + PS) = u32x2{m0, m1};
+      *reinterpret_cast<u32x2*>(q + 2 * PS) = u32x2{l0, l1};
+    }
 }
 
 // bias init: out[ft][rt] = b[fbase + 16 ft + 4 g + r]
@@ -516,9 +612,10 @@ PPO_DEV void upd_loss(const UpdArgs& a, int trunk, int tid, int m0, float c, flo
 }
 
 // k_upd's body (a device function so that k_upd32's mixed form can run it for the actor trunk)
-template <int H, int KIND, int NTO, int NHT, int KL1>
+template <int H, int KIND, int NTO, int NHT, int KL1, bool BX = false>
 PPO_DEV void upd16_body(const UpdArgs& a) {
-  using GE = Geo<H, NTO, NHT>;
+  using GE = Geo<H, NTO, NHT, BX>;
+  static_assert(!BX || (H == 256 && KIND == PPO_NET_LN_BETA), "split-bf16 form: LayerNorm-Beta agent, H = 256");
   constexpr int FT = GE::FT, RT = GE::RT, WF = GE::WF, R = GE::R, NT = GE::NT, OP = GE::OP;
   constexpr int LDX = GE::LDX, LDA = GE::LDA, LDG = GE::LDG, NHP = GE::NHP, ITS = GE::ITS;
   constexpr bool LN = KIND == PPO_NET_LN_BETA;
@@ -615,6 +712,12 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
   const int w2tlane = H * OP + H * H + ((fbase >> 4) * NT * 64 + lane) * 4;
   const float* xn_in = XN + (rbase + j) * LDX + 4 * g;
   const float* act_in = ACT + (rbase + j) * LDA + 4 * g;
+  // BX: the pieces of W2 | W2^T (bx_index, after the fp32 copies) and of the activation rows
+  constexpr int LDB = GE::LDB;
+  const PBuf wbx = make_pbuf(a.WSW[trunk] + sw_size(H, OP), BX ? (int)bx_size(H) : 0);
+  const int w2blane = ((fbase >> 4) * (NT / 2) * 3 * 64 + lane) * 4;
+  const int w2tblane = 3 * H * H / 2 + w2blane;
+  const float* actb_in = ACT + (rbase + j) * LDB + 4 * g;
   // head rows for the forward (A = W3[16 ht + i][..]) and the backward (A = W3^T: heads 16 ht + 4 g + r)
   int hrow_f[NHT], hrow_b[NHT][4];
 #pragma unroll
@@ -827,14 +930,16 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
           for (int r = 0; r < 4; ++r) z[ft][rt][r] = tanhf(z[ft][rt][r]);
     }
     if (!PPO_DIAG_SKIP(4)) store_tile_rows<FT, RT>(a.H1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
-    lds_store_tile<FT, RT, LDA>(ACT, z, rbase, fbase, j, g);
+    if constexpr (BX) lds_store_pieces<FT, RT, LDB, H / 2>(ACT, z, rbase, fbase, j, g);
+    else lds_store_tile<FT, RT, LDA>(ACT, z, rbase, fbase, j, g);
     lds_barrier();
     PPO_STAMP(2);
 
     // ---------------- layer 2 ----------------
     f4 x2[FT][RT];  // LN: x_hat2; tanh: h2
     init_bias<FT, RT>(x2, pb, T.b2 + fbase + 4 * g);
-    mm_fr<FT, RT, NT, LDA>(x2, wsw, w2lane, act_in);
+    if constexpr (BX) mm_bx<FT, RT, NT, LDB>(x2, wbx, w2blane, actb_in);
+    else mm_fr<FT, RT, NT, LDA>(x2, wsw, w2lane, act_in);
     PPO_STAMP(3);
     if constexpr (PREF) pref_data(it + gridDim.x);
     float rs2[RT];
@@ -875,6 +980,9 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) hp[ht][rt] = f4{0.f, 0.f, 0.f, 0.f};
     lds_barrier();  // every wave is done reading h1 from ACT
+    if constexpr (BX) {  // GG shares the activation region: padding heads must read exactly 0
+      for (int i = tid; i < R * LDG; i += 256) GG[i] = 0.f;
+    }
     if (trunk == 0) {
       // critic: one real head of NHP — a per-row dot product on the VALU (in-lane over the wave's
       // features, then the 4 lane groups) instead of 15/16-padding MFMAs
@@ -1053,13 +1161,15 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
     if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return x2[ft][rt][r]; }, acc + sg.b2, fbase, j, g);
     if (!PPO_DIAG_SKIP(5)) store_tile_rows<FT, RT>(a.DZ2[trunk], H, x2, m0, a.M, rbase, fbase, j, g);
     lds_barrier();  // dW3 readers of h2 are done
-    lds_store_tile<FT, RT, LDA>(ACT, x2, rbase, fbase, j, g);
+    if constexpr (BX) lds_store_pieces<FT, RT, LDB, H / 2>(ACT, x2, rbase, fbase, j, g);
+    else lds_store_tile<FT, RT, LDA>(ACT, x2, rbase, fbase, j, g);
     lds_barrier();
     PPO_STAMP(9);
 
     // ---------------- dh1 = W2^T dz2 ----------------
     zero<FT, RT>(dh);
-    mm_fr<FT, RT, NT, LDA>(dh, wsw, w2tlane, act_in);
+    if constexpr (BX) mm_bx<FT, RT, NT, LDB>(dh, wbx, w2tblane, actb_in);
+    else mm_fr<FT, RT, NT, LDA>(dh, wsw, w2tlane, act_in);
     PPO_STAMP(10);
     // ---------------- recompute layer 1, layer-1 backward ----------------
     init_bias<FT, RT>(z, pb, T.b1 + fbase + 4 * g);
@@ -1855,10 +1965,13 @@ PPO_DEV void upd32_body(const UpdArgs& a) {
   for (int i = tid; i < sl.size; i += 256) slab_row[hwg && i >= sg.hW ? i + sg.nh * H : i] = ACC[i];
 }
 
-template <int H, int KIND, int NTO, int NHT, int KL1>
+template <int H, int KIND, int NTO, int NHT, int KL1, bool BX>
 __global__ __launch_bounds__(256, 2) void k_upd(UpdArgs a) {
-  upd16_body<H, KIND, NTO, NHT, KL1>(a);
+  upd16_body<H, KIND, NTO, NHT, KL1, BX>(a);
 }
+// the split-bf16 form is instantiated for the LayerNorm-Beta agent at H = 256 with one head tile
+template <int H, int KIND, int NHT>
+constexpr bool upd_bx_ok() { return H == 256 && KIND == PPO_NET_LN_BETA && NHT == 1; }
 
 // MIX = 0: both trunks on 32x32x2 MFMAs; MIX = 1: the critic on 32x32x2, the actor on k_upd's
 // 16x16x4 body (the actor's loss and LayerNorm phases are VALU chains that co-issue beside the
@@ -1878,12 +1991,13 @@ __global__ __launch_bounds__(256, 2) void k_upd32(UpdArgs a) {
 // 95 KB), its head-weight gradient (nh x H floats) accumulates in its own slab row instead: every
 // element has one owning lane, which adds the tile contributions in tile order (bitwise the LDS
 // result).
-template <int H, int NTO, int NHT>
+template <int H, int NTO, int NHT, bool BX = false>
 static void upd_geo(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g) {
-  using GE = Geo<H, NTO, NHT>;
+  using GE = Geo<H, NTO, NHT, BX>;
   auto carve = [&](int sg_lds) {
     const int scr = std::max(GE::WF * GE::NHP * GE::R, GE::R * K.A * GE::ITS);
-    int off = GE::oSCR + scr;
+    int off = GE::BX ? GE::oROW + GE::R * 8 : GE::oSCR + scr;
+    if (scr > GE::SCR_MAX) off = 1 << 20;  // BX: SCR does not fit its region (refused)
     g->actn_off = off;
     off += GE::R * K.A;
     off = (off + 3) & ~3;
@@ -1895,7 +2009,7 @@ static void upd_geo(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_s
   };
   g->hw_global = 0;
   carve(std::max(sg0_size, sg1_size));
-  if (GE::WR == 1 && 2 * g->lds_bytes > 160 * 1024) {
+  if (GE::WR == 1 && (PPO_HWG_FORCE || 2 * g->lds_bytes > 160 * 1024)) {
     const size_t full = g->lds_bytes;
     carve(std::max(sg0_size, sg1_size - nh_actor * H));
     if (2 * g->lds_bytes <= 160 * 1024) g->hw_global = 1;
@@ -1922,17 +2036,25 @@ static int dispatch_upd(const PackedLayout& K, int nh, F&& f) {
   return -1;
 }
 
-int upd_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g) {
+int upd_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_size, UpdGeoOut* g, int bx) {
   // both trunks run in one launch: the geometry must cover the actor's head count (critic: 1)
   return dispatch_upd(K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_, auto KL_) {
-    (void)KIND_;
-    upd_geo<decltype(H_)::value, decltype(NTO_)::value, decltype(NHT_)::value>(K, nh_actor, sg0_size, sg1_size, g);
-    const auto k = k_upd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value, decltype(NHT_)::value,
-                         decltype(KL_)::value>;
-    return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) ==
-                   hipSuccess
-               ? 0
-               : -2;
+    constexpr int H = decltype(H_)::value, KIND = decltype(KIND_)::value, NTO = decltype(NTO_)::value,
+                  NHT = decltype(NHT_)::value, KL = decltype(KL_)::value;
+    const void* k = nullptr;
+    if (bx) {
+      if constexpr (upd_bx_ok<H, KIND, NHT>()) {
+        upd_geo<H, NTO, NHT, true>(K, nh_actor, sg0_size, sg1_size, g);
+        if (2 * g->lds_bytes > 160 * 1024) return -1;  // one workgroup per CU: not this form
+        k = (const void*)k_upd<H, KIND, NTO, NHT, KL, true>;
+      } else {
+        return -1;
+      }
+    } else {
+      upd_geo<H, NTO, NHT>(K, nh_actor, sg0_size, sg1_size, g);
+      k = (const void*)k_upd<H, KIND, NTO, NHT, KL, false>;
+    }
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) == hipSuccess ? 0 : -2;
   });
 }
 
@@ -1982,9 +2104,16 @@ int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hi
 #endif
   const dim3 grid(nblocks, 2);
   return dispatch_upd(a.K, nh_actor, [&](auto H_, auto KIND_, auto NTO_, auto NHT_, auto KL_) {
-    hipLaunchKernelGGL((k_upd<decltype(H_)::value, decltype(KIND_)::value, decltype(NTO_)::value,
-                              decltype(NHT_)::value, decltype(KL_)::value>),
-                       grid, dim3(256), lds_bytes, s, b);
+    constexpr int H = decltype(H_)::value, KIND = decltype(KIND_)::value, NTO = decltype(NTO_)::value,
+                  NHT = decltype(NHT_)::value, KL = decltype(KL_)::value;
+    if (a.bx) {
+      if constexpr (upd_bx_ok<H, KIND, NHT>()) {
+        hipLaunchKernelGGL((k_upd<H, KIND, NTO, NHT, KL, true>), grid, dim3(256), lds_bytes, s, b);
+        return 0;
+      }
+      return -1;
+    }
+    hipLaunchKernelGGL((k_upd<H, KIND, NTO, NHT, KL, false>), grid, dim3(256), lds_bytes, s, b);
     return 0;
   });
 }

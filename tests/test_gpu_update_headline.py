@@ -41,6 +41,9 @@ from test_gpu_parity import fill_storage, make_agent, random_params, rel  # noqa
     ("metric_halfcheetah_mfma32", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=32"),
     ("cfg4_shard_ant_mfma32", 1, 256, 105, 8, 1024, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=32"),
     ("metric_halfcheetah_mix", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=mix"),
+    # k_upd with its 256-wide GEMMs as split-bf16 piece products (create option upd_mfma=bx6)
+    ("metric_halfcheetah_bx6", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=bx6"),
+    ("cfg4_shard_ant_bx6", 1, 256, 105, 8, 1024, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=bx6"),
     # the fused dW on exact bf16 piece products (k_dwf_bx, create option dw_mfma): all nine, and eight
     ("metric_halfcheetah_dw_bf16x9", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "dw_mfma=bf16x9"),
     ("metric_halfcheetah_dw_bf16x8", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "dw_mfma=bf16x8"),
@@ -245,3 +248,58 @@ def test_split_bf16_dw_is_as_accurate_as_fp32_mfma(E, T):
             e32, eb = rel(g32, og[o:o + n]), rel(gb, og[o:o + n])
             print(f"tensor {t} ({n}): {opt} vs f32 {rel(gb, g32):.2e}; vs oracle f32 {e32:.2e} {opt} {eb:.2e}")
             assert eb <= 4.0 * e32 + 1e-7, (t, opt, e32, eb)
+
+
+@pytest.mark.parametrize("O_,A,E", [(17, 6, 999), (105, 8, 777), (16, 8, 333), (17, 6, 4096)])
+def test_upd_bx6_is_as_accurate_as_fp32_mfma(O_, A, E):
+    """k_upd's split-bf16 form (upd_mfma=bx6: layer 2 and dh1 = W2^T dz2 as six bf16 piece products
+    per fp32 product on v_mfma_f32_16x16x32_bf16, fp32 accumulation) against the fp32-MFMA k_upd on
+    the same minibatch (ragged last tiles; O = 17 / 105 (the synchronous wide gather) / 16; A = 8: a full head tile) and both
+    against the oracle's gradient (fp64 accumulation). The dropped piece products are below 2^-23 of
+    each product, so the split form must be as close to the oracle as the fp32 MFMA form: per
+    gradient tensor within 1.5x its error + 1e-6 (a few ulps: one-element tensors), and within 2e-5 rel-L2 of it overall; loss
+    statistics rtol 2e-5."""
+    kind, H, T = 1, 256, 1
+    M = E * T
+    rng = np.random.default_rng(13)
+    L = O.layout_init(kind, O_, A, H)
+    p = random_params(L, rng)
+    x = rng.standard_normal((M, O_)).astype(np.float32)
+    act = rng.uniform(-0.95, 0.95, (M, A)).astype(np.float32)
+    olp = (rng.standard_normal(M) * 0.3 - 3.0).astype(np.float32)
+    adv = rng.standard_normal(M).astype(np.float32)
+    ret = rng.standard_normal(M).astype(np.float32)
+    ov = (rng.standard_normal(M) * 0.1).astype(np.float32)
+    perm = rng.permutation(M).astype(np.int32)
+    out = {}
+    for opt in ("upd_mfma=16", "upd_mfma=bx6"):
+        ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.2, ent=0.01, options=opt)
+        ag.load_params(p)
+        fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
+        st = ag.update(2.5e-4, perms=DeviceArray.from_numpy(perm), want_stats=True)
+        out[opt] = (ag.last_grad(), st, ag.params())
+        ag.close()
+    (g0, s0, p0), (g1, s1, p1) = out["upd_mfma=16"], out["upd_mfma=bx6"]
+    cfg = O.LossCfg(0.2, 0.01, 0.5, 1, 1)
+    og, _ = O.minibatch_grad_parallel(L, p, x[perm], act[perm], olp[perm], adv[perm], ret[perm], ov[perm], cfg)
+    print(f"\nbx6 vs f32 {rel(g1, g0):.2e}; vs oracle: f32 {rel(g0, og):.2e} bx6 {rel(g1, og):.2e}")
+    assert rel(g1, g0) < 2e-5, rel(g1, g0)
+    worst = 0.0
+    for t in range(L.ntensors):
+        o, n = L.t_off[t], L.t_len[t]
+        if L.t_grad[t]:
+            e0, e1 = rel(g0[o:o + n], og[o:o + n]), rel(g1[o:o + n], og[o:o + n])
+            worst = max(worst, e1 / max(e0, 1e-12))
+            print(f"  tensor {t:2d} ({n:6d}): f32 {e0:.2e} bx6 {e1:.2e}")
+            assert e1 <= 1.5 * e0 + 1e-6, (t, e0, e1)
+    print(f"worst per-tensor error ratio bx6 / f32: {worst:.2f}")
+    for k in ("pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac", "grad_norm"):
+        np.testing.assert_allclose(s1[k], s0[k], rtol=2e-5, atol=1e-7, err_msg=k)
+    assert np.abs(p1 - p0).max() < 1e-5
+
+
+def test_upd_bx6_refused_where_it_does_not_apply():
+    with pytest.raises(ppo_amd.PPOError, match="upd_mfma=bx6"):
+        make_agent(0, 17, 6, 64, 64, options="upd_mfma=bx6")
+    with pytest.raises(ppo_amd.PPOError, match="upd_mfma=bx6"):
+        make_agent(1, 376, 17, 256, 64, options="upd_mfma=bx6")  # 34 heads: three head tiles

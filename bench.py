@@ -45,6 +45,21 @@ def algorithmic_work(O, A, H, E, T, MB, nh):
     }
 
 
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense (no sparsity)
+
+
+def bx6_mix_peak(O, A, H):
+    """k_upd with upd_mfma=bx6: the share of its algorithmic FLOPs that run as split-bf16 piece
+    products (layer 2 forward and dh1 = W2^T dz2 of both trunks: 4 x 2 H^2 per row) and the peak of
+    that instruction mix: fp32 products on 16x16x4 f32 MFMAs at 157.3 TF/s, the rest at six bf16 piece
+    products each on the 2.5 PF/s bf16 MFMA (417 TF/s of fp32 products)."""
+    nh = 2 * A
+    fwd_row = (2 * O * H + 2 * H * H + 2 * H) + (2 * O * H + 2 * H * H + 2 * nh * H)
+    bwd_row = (2 * H + 2 * H * H + 2 * H) + (2 * nh * H + 2 * H * H + 2 * nh * H)
+    share = 4 * 2 * H * H / (fwd_row + bwd_row)
+    return share, 1.0 / (share / (PEAK_BF16_MFMA_TFLOPS / 6) + (1 - share) / PEAK_F32_MFMA_TFLOPS)
+
+
 def host_cores():
     """CPU threads this job may use: the launcher's thread budget (OMP_NUM_THREADS, set to the box's
     CPU share), else the cgroup quota, else the affinity mask."""
@@ -287,6 +302,7 @@ def main():
     if rank == 0:
         H, O_, A = 256, 17, 6
         work = algorithmic_work(O_, A, H, E, T, cfg.num_minibatches, 2 * A)
+        kinfo = tr.agent.kernel_info()
         roof = None
         if prof:
             name = max(prof, key=lambda k: prof[k][0])
@@ -298,7 +314,14 @@ def main():
                 roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_F32_MFMA_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4), "traffic": None,
                         "kernel": name, "avg_launch_ms": round(ms / cnt, 4), "launches": cnt,
-                        "algorithmic_per_launch": amount}
+                        "algorithmic_per_launch": amount, "kernels": kinfo}
+                if name == "fwdbwd" and "bx6" in kinfo:
+                    # the fp32 products of layer 2 and dh1 run as six bf16 piece products on the bf16
+                    # MFMA (2.5 PF/s dense): the peak of the kernel's actual instruction mix
+                    frac_bx, peak_mix = bx6_mix_peak(O_, A, H)
+                    roof["bx6_flop_share"] = round(frac_bx, 4)
+                    roof["peak_instruction_mix"] = round(peak_mix, 1)
+                    roof["frac_instruction_mix"] = round(achieved / peak_mix, 4)
             else:
                 achieved = amount / avg_s / 1e9
                 roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -212,6 +212,11 @@ int ppo_comm_info(const ppo_t* ctx, int* kind, int* rank, int* world);
  * (hipDeviceGetPCIBusId, e.g. "0000:05:00.0"; pass NULL / 0 to skip). Launchers compare the bus ids
  * of all ranks: two ranks on one GPU is an error under RCCL. */
 int ppo_get_device(const ppo_t* ctx, int* device, char* pci_bus_id, int len);
+/* The kernels the context selected for its update (create options and shape; no reference
+ * counterpart — a report for benchmarks and logs), as "update=<kernel>[/<form>] dw=<kernel>[/<form>]",
+ * e.g. "update=k_upd/bx6 dw=k_dwf_dma/f32" (bx6: k_upd's 256-wide GEMMs as split-bf16 piece
+ * products, upd_mfma). NUL-terminated, truncated to len. */
+int ppo_kernel_info(const ppo_t* ctx, char* buf, int len);
 
 /* ---- device memory helpers (so C / ctypes callers need no HIP headers) ---- */
 int ppo_set_device(int device);

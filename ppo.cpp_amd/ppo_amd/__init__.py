@@ -160,6 +160,7 @@ SYMBOLS = [
     ("ppo_comm_allreduce", _I, [_VP, _FP, _L, _I]),
     ("ppo_comm_info", _I, [_VP, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
     ("ppo_get_device", _I, [_VP, C.POINTER(_I), C.c_char_p, _I]),
+    ("ppo_kernel_info", _I, [_VP, C.c_char_p, _I]),
     ("ppo_set_device", _I, [_I]),
     ("ppo_device_count", _I, [C.POINTER(_I)]),
     ("ppo_dev_malloc", _I, [C.POINTER(_VP), _SZ]),
@@ -619,6 +620,12 @@ class Agent:
         bus = C.create_string_buffer(64)
         check(lib().ppo_get_device(self.h, C.byref(d), bus, 64))
         return d.value, bus.value.decode()
+
+    def kernel_info(self):
+        """The update / dW kernels this context selected (ppo_kernel_info)."""
+        buf = C.create_string_buffer(256)
+        check(lib().ppo_kernel_info(self.h, buf, 256))
+        return buf.value.decode()
 
     def set_rollout_mode(self, per_step: bool):
         """ppo_rollout_synth: one persistent launch (default, where supported) or per-step launches."""

@@ -349,7 +349,13 @@ def test_full_iteration_vs_oracle(kind):
                               gb["logp"].reshape(-1), gpu_adv.reshape(-1), gb["ret"].reshape(-1),
                               gb["val"].reshape(-1), EP, MB, lr, 0.5, 1e-5, lcfg, seed=cfg.seed, rank=0,
                               epoch_counter0=0)
-    np.testing.assert_allclose(gpu_p, op, rtol=0, atol=2e-5)
+    # Adam's first steps move a parameter by ~ lr g / (|g| + eps): an element whose minibatch gradient
+    # is a near-cancelling sum (|g| ~ eps) turns an fp32 rounding difference of that sum into an
+    # lr-sized step difference (test_gpu_update_headline's per-element bound). Such elements must
+    # stay a tiny minority (measured: 0 with fp32 MFMAs, 2 of 146 225 with k_upd's split-bf16 GEMMs,
+    # 3.7e-5 = 0.15 lr), every other parameter within 2e-5.
+    d = np.abs(gpu_p.astype(np.float64) - op)
+    assert (d > 2e-5).mean() < 1e-4 and d.max() < 0.5 * lr, ((d > 2e-5).sum(), d.max())
 
 
 # ------------------------------------------------------------------------------------------------
@@ -543,7 +549,8 @@ def test_weight_copies_track_adam(net_kind, hidden, env_id, O_):
     (swizzled) copies that k_adam rewrites next to every parameter update. After a full iteration
     (16 or 64 Adam steps), act and value outputs computed from the incrementally maintained copies
     must equal, bitwise, those after the copies are rebuilt from the parameters (ppo_load_params
-    -> k_transpose / k_swizzle)."""
+    -> k_transpose / k_swizzle), and so must one more update from the same parameters and Adam state
+    (which also reads the split-bf16 pieces of the AC agent's k_upd)."""
     E, T = 256, 16
     C = ppo_amd.ACPPOConfig if net_kind == 1 else ppo_amd.PPOConfig
     cfg = C(num_envs=E, num_steps=T, num_minibatches=4, update_epochs=4, env_id=env_id, net_kind=net_kind,
@@ -553,14 +560,24 @@ def test_weight_copies_track_adam(net_kind, hidden, env_id, O_):
     tr.iterate()
     p1 = tr.agent.params()
     assert not np.array_equal(p0, p1)
+    m1, v1, s1 = tr.agent.adam_state()
     x = DeviceArray.from_numpy(np.random.default_rng(9).standard_normal((E, O_)).astype(np.float32))
-    outs = []
+    outs, upd = [], []
     for rebuild in (False, True):
         if rebuild:
             tr.agent.load_params(p1)
+            tr.agent.load_adam(m1, v1, s1)
         m, lp, ent, v = tr.agent.get_action_and_value(x, sample_type=ppo_amd.PPO_MEAN)
         outs.append([m.numpy(), lp.numpy(), ent.numpy(), v.numpy(), tr.agent.get_value(x).numpy()])
+        # one more update over the stored rollout from the same state: k_upd / k_upd2 read the copies
+        # too (the AC agent's default k_upd also the split-bf16 pieces of W2 | W2^T, bx_index)
+        tr.agent.set_iteration(1)
+        upd.append((tr.agent.update(1e-4), tr.agent.params()))
     for a, b in zip(*outs):
         assert np.isfinite(a).all()
         np.testing.assert_array_equal(a, b)
+    (sa, pa), (sb, pb) = upd
+    assert not np.array_equal(pa, p1)
+    np.testing.assert_array_equal(pa, pb)
+    assert sa == sb
     tr.close()

@@ -41,9 +41,10 @@ from test_gpu_parity import fill_storage, make_agent, random_params, rel  # noqa
     ("metric_halfcheetah_mfma32", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=32"),
     ("cfg4_shard_ant_mfma32", 1, 256, 105, 8, 1024, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=32"),
     ("metric_halfcheetah_mix", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=mix"),
-    # k_upd with its 256-wide GEMMs as split-bf16 piece products (create option upd_mfma=bx6)
-    ("metric_halfcheetah_bx6", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=bx6"),
-    ("cfg4_shard_ant_bx6", 1, 256, 105, 8, 1024, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=bx6"),
+    # the default k_upd of these two runs its 256-wide GEMMs as split-bf16 piece products (upd_mfma=bx6);
+    # the same two on fp32 16x16x4 MFMAs throughout (upd_mfma=16)
+    ("metric_halfcheetah_f32", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=16"),
+    ("cfg4_shard_ant_f32", 1, 256, 105, 8, 1024, 32, 0.1, 0.01, 2.5e-4, "upd_mfma=16"),
     # the fused dW on exact bf16 piece products (k_dwf_bx, create option dw_mfma): all nine, and eight
     ("metric_halfcheetah_dw_bf16x9", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "dw_mfma=bf16x9"),
     ("metric_halfcheetah_dw_bf16x8", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "dw_mfma=bf16x8"),

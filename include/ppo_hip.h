@@ -81,17 +81,20 @@ int ppo_obs_norm(const char* env_id, const float** mean, const float** std, int*
 int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
 /* ppo_create with kernel-selection options, "key=value" pairs separated by ',' (NULL or "": the
  * defaults ppo_create uses). Every choice is a complete, tested kernel path; results differ only in
- * summation order (A/B comparisons, tests):
+ * summation order (A/B comparisons, tests). Split-bf16 forms: every fp32 operand x is the exact sum
+ * of three bf16 pieces (hi = x truncated to bf16, mid = (x - hi) truncated, lo = the rest), so an
+ * fp32 product is a sum of exact piece products, accumulated in fp32 on the bf16 MFMA (16x the fp32
+ * MFMA rate); the fp32 math of the reference, not a reduced-precision variant of it:
  *   upd_kernel=auto|fwdbwd   minibatch forward/backward: the feature-split k_upd / k_upd2 (auto) or
  *                            the wave-per-16-rows k_fwdbwd
  *   act_kernel=auto|2|4      64-wide agent act: by shape (auto), k_act2, or k_act4
  *   dw_fused=1|0             dW1 / dW2 in one pass (k_dwf) or two (k_dw)
  *   dw_dma=1|0               k_dwf's rows staged by LDS DMA in three buffers (k_dwf_dma, default)
  *                            or through registers in two (k_dwf); bitwise the same
- *   dw_mfma=auto|f32|bf16x9|bf16x8  k_dwf_dma's products on fp32 MFMAs (auto) or as exact three-way
- *                            bf16 splits of every fp32 operand on 32x32x16 bf16 MFMAs (k_dwf_bx: all 9
- *                            piece products, or 8 without lo*lo < 2^-30 |ab|); fp32 accumulation, not
- *                            bitwise the fp32 path (rounding of the bf16 MFMA's internal sums)
+ *   dw_mfma=auto|f32|bf16x9|bf16x8  the fused dW's products as split-bf16 piece products on 32x32x16
+ *                            bf16 MFMAs (k_dwf_bx: all 9, auto = bf16x9; or 8 without lo*lo
+ *                            < 2^-30 |ab|) or on fp32 MFMAs (k_dwf_dma, f32); not bitwise the fp32
+ *                            path (rounding of the bf16 MFMA's internal sums)
  *   dw_rows=<n>, dw_slices=1|2  dW split-K geometry: rows per chunk (multiple of 16; 32 for the
  *                            64-wide agent) and k_dwf output slices; default: automatic
  *   update_graph=0|1       ppo_update's minibatch launches eager (default) or replayed as one
@@ -103,10 +106,13 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            of both trunks as one gathered GEMM (k_l1g) and k_upd2's tail in its own
  *                            launch at 2 / 3 workgroups per CU, or the single k_upd2 (0; auto: the
  *                            single kernel, measured faster)
- *   upd_mfma=auto|16|32|mix  LayerNorm-Beta agent at hidden 256: the fused minibatch kernel on
- *                            16x16x4 MFMAs (k_upd; auto), on 32x32x2 MFMAs (k_upd32), or mixed
- *                            (critic trunk 32x32x2, actor 16x16x4); the same results up to
- *                            summation order
+ *   upd_mfma=auto|bx6|16|32|mix  LayerNorm-Beta agent at hidden 256: the fused minibatch kernel
+ *                            with its 256-wide GEMMs (layer 2, dh1 = W2^T dz2) as six split-bf16
+ *                            piece products per fp32 product on 16x16x32 bf16 MFMAs (k_upd bx6;
+ *                            auto where it applies: at most 16 heads; the dropped mid*lo + lo*mid +
+ *                            lo*lo are < 2^-21 |ab|), on 16x16x4 fp32 MFMAs (k_upd, 16), on 32x32x2
+ *                            (k_upd32), or mixed (critic trunk 32x32x2, actor 16x16x4); the same
+ *                            results up to summation order
  *   rollout=auto|per_step    ppo_rollout_synth: persistent launch where supported, or per step
  *   rollout_kernel=auto|mfma|valu  the AC agent's persistent rollout: k_rollout (16 envs per
  *                            workgroup, MFMA) or k_rollout_v (2 envs per workgroup, VALU; O <= 32);
@@ -115,8 +121,8 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *   gradstep=split|fused     clip_grad_norm_ + Adam: two launches (k_gradnorm, k_adam; default) or
  *                            one cooperative launch (k_gradstep: slower on ROCm 7, whose cooperative
  *                            launch costs ~30 us); bitwise the same
- * An unknown key or value is an error, and so is an option the agent cannot use (upd_mfma=32 / mix
- * off the LayerNorm-Beta agent, upd2_split > 0 off the 64-wide Humanoid shape): such a create
+ * An unknown key or value is an error, and so is an option the agent cannot use (upd_mfma=32 / mix /
+ * bx6 off the LayerNorm-Beta agent, upd2_split > 0 off the 64-wide Humanoid shape): such a create
  * fails and releases everything it had allocated. */
 int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* options, ppo_t** out);
 int ppo_destroy(ppo_t* ctx);

@@ -294,8 +294,11 @@ struct CreateOptions {
 // auto = the single k_upd2: the split form measured slower on cfg2 (round 4, profiles/r04/cfg2_split/:
 // 101.3 vs 92.9 ms per iteration; k_l1g 66 us = 0.61 of peak per launch, the tail 94 us at 3 per CU)
 static constexpr int kUpd2SplitAuto = 0;
-// dw_mfma=auto: the fused dW on fp32 MFMAs (k_dwf_dma) until the split-bf16 form is measured
-static constexpr int kDwBxAuto = 0;
+// dw_mfma=auto: the fused dW as all nine exact bf16 piece products (k_dwf_bx, bf16x9). With k_upd on
+// its split-bf16 form too, the metric iteration runs 17.32 (fp32 MFMA dW) -> 16.65 ms
+// (profiles/r05/bx6/); against the fp64 oracle its dW is 2.6x the fp32 MFMA's rounding on the
+// best-conditioned tensor (2.25e-7 vs 8.6e-8 rel-L2), test_split_bf16_dw_is_as_accurate_as_fp32_mfma
+static constexpr int kDwBxAuto = 9;
 // upd_mfma=auto: k_upd's split-bf16 form (bx6) wherever it is instantiated (LayerNorm-Beta agent,
 // H = 256, one head tile): as exact as the fp32 MFMA form against the oracle
 // (test_upd_bx6_is_as_accurate_as_fp32_mfma), k_upd 0.775 -> 0.606 ms per launch at the metric config

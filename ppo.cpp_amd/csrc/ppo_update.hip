@@ -156,8 +156,9 @@ PPO_DEV void mm_fr(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* in) {
 // weights' pieces (bx_index copies: hi, mid, lo of every fp32 weight, written by k_adam), B = the
 // activations' pieces (split once when the tile is written to LDS, lds_store_pieces). Of the nine
 // piece products six are kept: lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi (smallest first); the
-// dropped mid.lo + lo.mid + lo.lo are < 2^-23 |a b| (below the rounding of an fp32 accumulation over
-// K = 256 terms). One 16x16x32 MFMA takes 16 cycles for 32 k against 8 x 32 cycles of 16x16x4 f32:
+// dropped mid.lo + lo.mid + lo.lo are < 2^-21 |a b| (|mid| < 2^-7 |x|, |lo| < 2^-15 |x|): the order of
+// an fp32 accumulation's rounding over K = 256 terms, and measured as exact as the fp32 MFMA form
+// against the fp64 oracle (test_upd_bx6_is_as_accurate_as_fp32_mfma). One 16x16x32 MFMA takes 16 cycles for 32 k against 8 x 32 cycles of 16x16x4 f32:
 // six are 0.375 of the fp32 MFMA time. Lane (j, g) k slot 8 g + e <-> column 32 kk + 16 (e >> 2) +
 // 4 g + (e & 3), the columns mm_fr gives lane group g in k-blocks 2 kk and 2 kk + 1, so the
 // accumulator layout is mm_fr's.

@@ -209,9 +209,9 @@ def test_split_bf16_dw_is_as_accurate_as_fp32_mfma(E, T):
     bf16x8 alike. Against the oracle's gradient (fp64 accumulation) the split form is measurably
     less exact than the fp32 MFMA on the well-conditioned tensors (critic dW2: 2.25e-7 against
     8.6e-8, the bf16 MFMA's internal accumulation) and equal where the k_upd hand-off dominates
-    (actor: 2.4e-6 both): bar 4x the fp32 path's error + 1e-7. This (and a 1-3 % gain) is
-    why it is not the default. Every other gradient entry comes from k_upd / k_colsum and is
-    bitwise the fp32 path's."""
+    (actor: 2.4e-6 both): bar 4x the fp32 path's error + 1e-7 (bf16x9 is the default dW since k_upd
+    runs its split-bf16 form too: 17.3 -> 16.7 ms per metric iteration). Every other
+    gradient entry comes from k_upd / k_colsum and is bitwise the fp32 path's."""
     rng = np.random.default_rng(41)
     kind, O_, A, H = 1, 17, 6, 256
     M = E * T

@@ -91,10 +91,11 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *   dw_fused=1|0             dW1 / dW2 in one pass (k_dwf) or two (k_dw)
  *   dw_dma=1|0               k_dwf's rows staged by LDS DMA in three buffers (k_dwf_dma, default)
  *                            or through registers in two (k_dwf); bitwise the same
- *   dw_mfma=auto|f32|bf16x9|bf16x8  the fused dW's products as split-bf16 piece products on 32x32x16
- *                            bf16 MFMAs (k_dwf_bx: all 9, auto = bf16x9; or 8 without lo*lo
- *                            < 2^-30 |ab|) or on fp32 MFMAs (k_dwf_dma, f32); not bitwise the fp32
- *                            path (rounding of the bf16 MFMA's internal sums)
+ *   dw_mfma=auto|f32|bf16x9|bf16x8|bf16x6  the fused dW's products as split-bf16 piece products on
+ *                            32x32x16 bf16 MFMAs (k_dwf_bx: all 9; 8 without lo*lo < 2^-30 |ab|; 6
+ *                            without mid*lo + lo*mid + lo*lo < 2^-21 |ab|, auto) or on fp32 MFMAs
+ *                            (k_dwf_dma, f32); not bitwise the fp32 path (rounding of the bf16 MFMA's
+ *                            internal sums)
  *   dw_rows=<n>, dw_slices=1|2  dW split-K geometry: rows per chunk (multiple of 16; 32 for the
  *                            64-wide agent) and k_dwf output slices; default: automatic
  *   update_graph=0|1       ppo_update's minibatch launches eager (default) or replayed as one

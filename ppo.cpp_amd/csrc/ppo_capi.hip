@@ -280,7 +280,7 @@ struct CreateOptions {
   int dw_rows = 0;     // dW split-K rows per chunk (multiple of 16; 0: auto, ~128 chunks per trunk)
   int dw_slices = 0;   // k_dwf output slices per chunk (1 / 2; 0: auto, dw_slices())
   int dw_dma = 1;      // 1 (default): k_dwf_dma (LDS-DMA staging, three stage buffers); 0: k_dwf
-  int dw_bx = -1;      // dw_mfma: -1 auto, 0 f32 (fp32 MFMA), 9 bf16x9 / 8 bf16x8 (k_dwf_bx: exact bf16 splits)
+  int dw_bx = -1;      // dw_mfma: -1 auto, 0 f32 (fp32 MFMA), 9 / 8 / 6 bf16x9 / x8 / x6 (k_dwf_bx: exact bf16 splits)
   // 1: ppo_update replays its minibatch launches as one captured hipGraph; 0 (default): eager.
   // Snapshots work with it on (ppo_read_snapshot waits for the snapshot's event on the host).
   int update_graph = 0;
@@ -294,11 +294,12 @@ struct CreateOptions {
 // auto = the single k_upd2: the split form measured slower on cfg2 (round 4, profiles/r04/cfg2_split/:
 // 101.3 vs 92.9 ms per iteration; k_l1g 66 us = 0.61 of peak per launch, the tail 94 us at 3 per CU)
 static constexpr int kUpd2SplitAuto = 0;
-// dw_mfma=auto: the fused dW as all nine exact bf16 piece products (k_dwf_bx, bf16x9). With k_upd on
-// its split-bf16 form too, the metric iteration runs 17.32 (fp32 MFMA dW) -> 16.65 ms
-// (profiles/r05/bx6/); against the fp64 oracle its dW is 2.6x the fp32 MFMA's rounding on the
-// best-conditioned tensor (2.25e-7 vs 8.6e-8 rel-L2), test_split_bf16_dw_is_as_accurate_as_fp32_mfma
-static constexpr int kDwBxAuto = 9;
+// dw_mfma=auto: the fused dW as six exact bf16 piece products (k_dwf_bx, bf16x6: k_upd's six; the
+// dropped mid.lo + lo.mid + lo.lo are < 2^-21 of each product). With k_upd on its split-bf16 form the
+// metric iteration runs 17.32 (fp32 MFMA dW) -> 16.65 (bf16x9) ms, and bf16x9 17.02 -> bf16x6 16.55 ms
+// on another box (profiles/r05/bx6/); against the fp64 oracle every dW tensor stays within 1.5x of the
+// fp32 MFMA's error (test_split_bf16_dw_is_as_accurate_as_fp32_mfma)
+static constexpr int kDwBxAuto = 6;
 // upd_mfma=auto: k_upd's split-bf16 form (bx6) wherever it is instantiated (LayerNorm-Beta agent,
 // H = 256, one head tile): as exact as the fp32 MFMA form against the oracle
 // (test_upd_bx6_is_as_accurate_as_fp32_mfma), k_upd 0.775 -> 0.606 ms per launch at the metric config
@@ -327,8 +328,8 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
       o->dw_rows = atoi(v.c_str());  // at most 5 digits: no overflow, no exception across the C-ABI
     else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
     else if (k == "dw_dma" && (v == "0" || v == "1")) o->dw_dma = v[0] - '0';
-    else if (k == "dw_mfma" && (v == "auto" || v == "f32" || v == "bf16x9" || v == "bf16x8"))
-      o->dw_bx = v == "auto" ? -1 : v == "f32" ? 0 : v == "bf16x9" ? 9 : 8;
+    else if (k == "dw_mfma" && (v == "auto" || v == "f32" || v == "bf16x9" || v == "bf16x8" || v == "bf16x6"))
+      o->dw_bx = v == "auto" ? -1 : v == "f32" ? 0 : v == "bf16x9" ? 9 : v == "bf16x8" ? 8 : 6;
     else if (k == "update_graph" && (v == "0" || v == "1")) o->update_graph = v[0] - '0';
     else if (k == "rollout_kernel" && (v == "auto" || v == "mfma" || v == "valu"))
       o->rollout_kernel = v == "auto" ? 0 : v == "mfma" ? 1 : 2;

@@ -1271,11 +1271,14 @@ PPO_DEV f16v mfma_bx(u32x4 a, u32x4 b, f16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 // acc += A.B over one 16-k block as NP piece products, smallest first
+// (NP = 6: k_upd's six, without mid.lo + lo.mid + lo.lo < 2^-21 |a.b|)
 template <int NP>
 PPO_DEV f16v mfma_split(const Split3& A, const Split3& B, f16v acc) {
   if constexpr (NP >= 9) acc = mfma_bx(A.lo, B.lo, acc);
-  acc = mfma_bx(A.lo, B.mid, acc);
-  acc = mfma_bx(A.mid, B.lo, acc);
+  if constexpr (NP >= 8) {
+    acc = mfma_bx(A.lo, B.mid, acc);
+    acc = mfma_bx(A.mid, B.lo, acc);
+  }
   acc = mfma_bx(A.lo, B.hi, acc);
   acc = mfma_bx(A.mid, B.mid, acc);
   acc = mfma_bx(A.hi, B.lo, acc);
@@ -1296,7 +1299,7 @@ __global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
   constexpr int NXI = KS * OP / 256;
   constexpr int TOW = 2 / NSL, TIW = 4;
   static_assert(NSL == 1 || NSL == 2, "k_dwf slices");
-  static_assert(NP == 8 || NP == 9, "k_dwf_bx passes");
+  static_assert(NP == 6 || NP == 8 || NP == 9, "k_dwf_bx passes");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hs = lane >> 5;
   const int wo = wave & 3, wi = wave >> 2;
   const int trunk = blockIdx.y, slice = NSL > 1 ? (int)blockIdx.z : 0;
@@ -2062,12 +2065,13 @@ static int launch_dwf_t(const DwArgs& a0, int nchunks, hipStream_t s) {
 #endif
   // the DMA kernels address their sources through 32-bit buffer descriptors (make_pbuf: int floats)
   if (a.bx && (long)a.M * H < (1L << 29)) {
-    auto k = a.bx == 9 ? k_dwf_bx<H, OP, NSL, 9> : k_dwf_bx<H, OP, NSL, 8>;
+    auto k = a.bx == 9 ? k_dwf_bx<H, OP, NSL, 9> : a.bx == 8 ? k_dwf_bx<H, OP, NSL, 8> : k_dwf_bx<H, OP, NSL, 6>;
     constexpr size_t lds = (size_t)3 * (3 * 16 * H + 16 * OP) * sizeof(float);
-    static bool attr[2] = {false, false};
-    if (!attr[a.bx == 9]) {
+    static bool attr[3] = {false, false, false};
+    const int ai = a.bx == 9 ? 2 : a.bx == 8 ? 1 : 0;
+    if (!attr[ai]) {
       if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
-      attr[a.bx == 9] = true;
+      attr[ai] = true;
     }
     hipLaunchKernelGGL(k, dim3(nchunks, 2, NSL), dim3(512), lds, s, a);
     return 0;

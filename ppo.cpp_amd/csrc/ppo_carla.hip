@@ -448,6 +448,7 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a) {
 // weight); only the order of the k chain differs (not bitwise k_conv's; tolerance tests).
 constexpr int kImg3KX = 8;  // extended taps per kernel row, padded
 constexpr int kConv1Auto = 2;  // the default conv1 form (ppo_carla_create_ex option conv1): packed (measured faster)
+constexpr int kConv1BxAuto = 0;  // conv1_mfma=auto: fp32 MFMAs until the split-bf16 form is measured
 template <int K, int S>
 struct Img3Geo {
   static constexpr int TI = (kImgTile - 1) * S + K;          // patch rows
@@ -1064,6 +1065,9 @@ struct ppo_carla {
   // wgrad / dgrad kernels), 0 generic (create option conv1=packed|staged|generic; PPO_CARLA_CONV1 in the
   // diagnostic build). The backward's staged kernels run for 1 and 2.
   int conv_img = kConv1Auto;
+  // conv1 (raw-byte input) as split-bf16 products on bf16 MFMAs (create option conv1_mfma=bx3|f32):
+  // k_wgrad_img2<.., BX> and k_conv_img3<.., BX>
+  int c1bx = kConv1BxAuto;
   float* c1w = nullptr;  // k_conv_img3's A-operand table
   // MLP tail for n <= kTailMaxN: 1 (default) one launch per stage, 0 one cooperative launch (a grid
   // barrier between stages: slower here, a cooperative launch costs more than the launches it
@@ -1109,6 +1113,7 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
   if (!cfg || !out) return ppo_fail("ppo_carla_create: null argument", -1);
   int conv_img = kConv1Auto;
   int tail_mode = 1;
+  int c1bx = kConv1BxAuto;
   if (options && *options) {  // comma-separated key=value
     std::string rest(options);
     while (!rest.empty()) {
@@ -1121,6 +1126,9 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
       else if (o == "tail=fused") tail_mode = 0;
       else if (o == "tail=staged") tail_mode = 1;
       else if (o == "tail=layers") tail_mode = 2;
+      else if (o == "conv1_mfma=bx3") c1bx = 1;
+      else if (o == "conv1_mfma=f32") c1bx = 0;
+      else if (o == "conv1_mfma=auto") c1bx = kConv1BxAuto;
       else return ppo_fail("ppo_carla_create_ex: unknown option " + o, -1);
     }
   }
@@ -1140,6 +1148,7 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
   c->device = device;
   c->conv_img = conv_img;
   c->tail_mode = tail_mode;
+  c->c1bx = c1bx;
 #ifdef PPO_DIAG
   if (const char* e = getenv("PPO_CARLA_CONV1")) c->conv_img = e[0] - '0';
 #endif
@@ -2151,7 +2160,12 @@ static size_t wimg2_lds_bytes(int IC, int K, int S, int OC) {
   return stage > comb ? stage : comb;
 }
 
-template <int K, int S>
+// BX (create option conv1_mfma=bx3): the pixel sums as v_mfma_f32_16x16x32_bf16 — the B operands
+// (raw bytes 0..255, and the bias column's 1) are exact bf16 numbers, so every fp32 product dZ.x is
+// the exact sum of three: dZ's split-bf16 pieces (hi, mid, lo; split3_pair) times x. Three 16-cycle
+// MFMAs per 32 pixel pairs instead of eight 32-cycle 16x16x4 f32 ones; lane group g's k slot e of
+// step q is pixel pair 32 q + 4 e + g (the f32 loop's step 8 q + e).
+template <int K, int S, bool BX = false>
 __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, int tps, int tiles, int tpc) {
   using G = ImgGeo<K, S>;
   constexpr int TI = G::TI, TIP = G::TIP, DW = TIP / 4, DZP = 260, KX = K + S, NC = 4 * kWimg2CT * 16;
@@ -2205,6 +2219,34 @@ __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, in
       }
     }
     __syncthreads();
+    if constexpr (BX) {
+#pragma unroll 1
+      for (int q = 0; q < 4; ++q) {
+        u32x4 ah, amd, al;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {  // slots e = 2 w, 2 w + 1: rows 4 q + w, column pairs g, 4 + g
+          const float* ar = arow + 16 * (4 * q + w) + 2 * g;
+          unsigned h, md, l;
+          split3_pair(ar[0] * am, ar[8] * am, h, md, l);
+          ah[w] = h; amd[w] = md; al[w] = l;
+        }
+        const int po0 = S * 4 * q * TIP + 2 * S * g;
+#pragma unroll
+        for (int u = 0; u < kWimg2CT; ++u) {
+          u32x4 b;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const int po = po0 + S * w * TIP;  // slot 2 w: column pair g; slot 2 w + 1: pair 4 + g
+            float x0 = (float)tile[ko[u] + po], x1 = (float)tile[ko[u] + po + 8 * S];
+            if (u >= kWimg2CT - 4 && cb[u] >= 0.0f) { x0 = cb[u]; x1 = cb[u]; }
+            b[w] = pack_bf16_exact(x0, x1);
+          }
+          acc[u] = mfma16bx(al, b, acc[u]);
+          acc[u] = mfma16bx(amd, b, acc[u]);
+          acc[u] = mfma16bx(ah, b, acc[u]);
+        }
+      }
+    } else {
 #pragma unroll 4
     for (int st = 0; st < 32; ++st) {
       const int m = 4 * st + g, ly = m >> 3, lx2 = m & 7;  // column pair (2 lx2, 2 lx2 + 1) of row ly
@@ -2218,6 +2260,7 @@ __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, in
         const float bv = u >= kWimg2CT - 4 ? (cb[u] < 0.0f ? xv : cb[u]) : xv;
         acc[u] = mfma16(av, bv, acc[u]);
       }
+    }
     }
   }
   // combine through LDS: D[16][NC] (row 4 g + r, column (wave 9 + u) 16 + j), then
@@ -2244,7 +2287,8 @@ __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, in
   }
 }
 
-int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap, hipStream_t s, bool img = true) {
+int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap, hipStream_t s, bool img = true,
+                 bool bx = false) {
   if (a.Kt > kMaxKTab || a.OP > kMaxPTab) return -1;
   if (!a.x_u8 && (long)a.n * a.x_stride * 4 >= 0x70000000L) return -1;  // k_wgrad's 32-bit buffer offsets
   const long per = (long)a.OC * (a.Kt + 1);
@@ -2261,8 +2305,12 @@ int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap
     const int groups = (chunks + kSumGroup - 1) / kSumGroup;
     if ((size_t)(chunks + (chunks > kSumGroup ? groups : 0)) * per <= part_cap) {
       a.part = part;
-      hipLaunchKernelGGL((k_wgrad_img2<5, 2>), dim3(chunks), dim3(256), wimg2_lds_bytes(a.IC, a.K, a.S, a.OC), s, a,
-                         tiles_x, tiles_x * tiles_y, tiles, tpc);
+      if (bx)
+        hipLaunchKernelGGL((k_wgrad_img2<5, 2, true>), dim3(chunks), dim3(256), wimg2_lds_bytes(a.IC, a.K, a.S, a.OC),
+                           s, a, tiles_x, tiles_x * tiles_y, tiles, tpc);
+      else
+        hipLaunchKernelGGL((k_wgrad_img2<5, 2, false>), dim3(chunks), dim3(256), wimg2_lds_bytes(a.IC, a.K, a.S, a.OC),
+                           s, a, tiles_x, tiles_x * tiles_y, tiles, tpc);
       const unsigned gb = (unsigned)((per + 255) / 256);
       if (chunks > kSumGroup) {
         float* lvl = part + (size_t)chunks * per;
@@ -2471,7 +2519,7 @@ extern "C" int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc
     WgradArgs wa{dz,          dzs,         L.conv_oc[i], L.conv_oh[i] * L.conv_ow[i], L.conv_ow[i], xf,
                  i ? nullptr : bev, xs,    L.conv_ic[i], L.conv_ih[i],                L.conv_iw[i], L.conv_k[i],
                  L.conv_s[i], n,           L.conv_ic[i] * L.conv_k[i] * L.conv_k[i], 0, nullptr};
-    bad |= launch_wgrad(wa, G + L.conv_w[i], G + L.conv_b[i], c->part, c->part_floats, s, c->conv_img);
+    bad |= launch_wgrad(wa, G + L.conv_w[i], G + L.conv_b[i], c->part, c->part_floats, s, c->conv_img, c->c1bx);
     if (i > 0) {
       DgradArgs da{dz,           dzs,          P + L.conv_w[i], L.conv_ic[i], xf,           xs,
                    c->dact[i - 1], xs,         L.conv_ic[i],    L.conv_ih[i], L.conv_iw[i], L.conv_oc[i],

@@ -243,6 +243,27 @@ PPO_DEV float xlogyf_(float a, float b) {
 // MFMA + cross-lane helpers
 // ------------------------------------------------------------------------------------------
 PPO_DEV f4 mfma16(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+// split-bf16 operands (ppo_kernels.hpp split3_bits): 8 bf16 per lane as 4 dwords
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+PPO_DEV f4 mfma16bx(u32x4 a, u32x4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+// two fp32 values -> their (hi, mid, lo) split-bf16 pieces, packed (x0 in the low half): hi = x with
+// the low 16 bits cleared, mid = (x - hi) the same way, lo = the exact rest (at most 8 significant bits)
+PPO_DEV void split3_pair(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
+  const unsigned u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
+  const float r0 = x0 - __uint_as_float(u0 & 0xffff0000u), r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
+  const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
+  const float l0 = r0 - __uint_as_float(v0 & 0xffff0000u), l1 = r1 - __uint_as_float(v1 & 0xffff0000u);
+  hi = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+  mid = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
+  lo = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
+}
+// two fp32 values exact in bf16 (e.g. byte values 0..255) packed as bf16 (x0 in the low half)
+PPO_DEV unsigned pack_bf16_exact(float x0, float x1) {
+  return __builtin_amdgcn_perm(__float_as_uint(x1), __float_as_uint(x0), 0x07060302u);
+}
 
 PPO_DEV float shfl_xor(float v, int m) { return __shfl_xor(v, m, 64); }
 

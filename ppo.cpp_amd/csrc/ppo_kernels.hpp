@@ -60,19 +60,6 @@ PPO_DEV_HOST inline void split3_bits(float x, uint16_t (&pc)[3]) {
   pc[1] = (uint16_t)(v >> 16);
   pc[2] = (uint16_t)(__builtin_bit_cast(uint32_t, l) >> 16);
 }
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-// two fp32 values -> their (hi, mid, lo) pieces, packed (x0 in the low half); split3_bits per value
-PPO_DEV void split3_pair(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
-  const unsigned u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
-  const float r0 = x0 - __uint_as_float(u0 & 0xffff0000u), r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
-  const unsigned v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
-  const float l0 = r0 - __uint_as_float(v0 & 0xffff0000u), l1 = r1 - __uint_as_float(v1 & 0xffff0000u);
-  hi = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
-  mid = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
-  lo = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
-}
-
 // Piece copies of W2 | W2^T for k_upd's split-bf16 GEMMs (create option upd_mfma=bx6), stored after a
 // trunk's fp32 swizzled copies (H = 256 contexts). Element (r, c) of an [NR][NC] matrix, piece p, sits
 // (in bf16 units) where lane (j, g) = j + 16 g reads it as the v_mfma_f32_16x16x32_bf16 A operand of

@@ -171,9 +171,6 @@ PPO_DEV void mm_fr(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* in) {
 #ifndef PPO_HWG_FORCE
 #define PPO_HWG_FORCE 0
 #endif
-PPO_DEV f4 mfma16bx(u32x4 a, u32x4 b, f4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
-}
 PPO_DEV u32x4 pld4u(PBuf b, int lane_floats, int uni_floats) { return __builtin_bit_cast(u32x4, pld4(b, lane_floats, uni_floats)); }
 template <int FT, int RT, int NKB, int LDB>
 PPO_DEV void mm_bx(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* inb) {

@@ -178,3 +178,46 @@ def test_update_with_one_rank_communicator_is_bit_identical():
         np.testing.assert_array_equal(g0, g1)
         np.testing.assert_array_equal(p0, p1)
         assert st0 == st1
+
+
+@pytest.mark.parametrize("opt", ["conv1_mfma=bx3"])
+def test_conv1_split_bf16_is_as_accurate_as_fp32_mfma(opt):
+    """conv1 (raw-byte input) with its products as split-bf16 MFMAs (conv1_mfma=bx3: the byte operand
+    is exact in bf16, the fp32 operand's three pieces make every product exact; fp32 accumulation)
+    against the fp32-MFMA form (conv1_mfma=f32) and both against the fp32 PyTorch reference, n = 64
+    rows: per gradient tensor the split form's rel-L2 error within 1.5x the fp32 form's + 1e-6, the
+    total norm and the stats rtol 2e-5 of the fp32 form's."""
+    torch.set_num_threads(16)
+    L = CI.layout()
+    p = CI.params(L)
+    n = 64
+    rng = np.random.default_rng(23)
+    bev = rng.integers(0, 256, size=(n, 15, 192, 192), dtype=np.uint8)
+    f = lambda *shape: rng.uniform(-1, 1, shape).astype(np.float32)  # noqa: E731
+    batch = (bev, f(n, 8), f(n, 3), f(n, 2) * 0.95, f(n) * 0.2, rng.standard_normal(n).astype(np.float32),
+             rng.standard_normal(n).astype(np.float32), f(n) * 0.1)
+    out = {}
+    for o in ("conv1_mfma=f32", opt):
+        ag = ppo_amd.CarlaAgent(max_batch=n, seed=7, options=o)
+        try:
+            ag.load_params(p)
+            ag.load_adam(np.zeros(L.P, np.float32), np.zeros(L.P, np.float32), 0)
+            out[o] = _run_update(ag, *batch)
+        finally:
+            ag.close()
+    ref_g = TR.update(L, p, *batch, **CFG)[0]
+    (s0, g0, _), (s1, g1, _) = out["conv1_mfma=f32"], out[opt]
+    rel = lambda a, b: np.linalg.norm(a.astype(np.float64) - b) / max(np.linalg.norm(b.astype(np.float64)), 1e-30)  # noqa: E731
+    worst = 0.0
+    for t in range(L.ntensors):
+        o_, n_ = L.t_off[t], L.t_len[t]
+        r = ref_g[o_:o_ + n_]
+        if np.linalg.norm(r) == 0:
+            continue
+        e0, e1 = rel(g0[o_:o_ + n_], r), rel(g1[o_:o_ + n_], r)
+        worst = max(worst, e1 / max(e0, 1e-12))
+        assert e1 <= 1.5 * e0 + 1e-6, (t, e0, e1)
+    print(f"\n{opt}: grad vs f32 form {rel(g1, g0):.2e}, vs torch f32 {rel(g0, ref_g):.2e} {opt} {rel(g1, ref_g):.2e}; "
+          f"worst per-tensor error ratio {worst:.2f}")
+    for k in ("pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac", "grad_norm"):
+        np.testing.assert_allclose(s1[k], s0[k], rtol=2e-5, atol=1e-7, err_msg=k)

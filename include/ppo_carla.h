@@ -127,8 +127,14 @@ typedef struct ppo_carla ppo_carla_t;
 /* carla_model.h:35-206 (the module) — allocates parameters and activation buffers on `device`. */
 int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_carla_t** out);
 /* options: NULL / "" (defaults) or "key=value" pairs separated by ',':
- *   conv1=staged|generic       conv1 forward and weight gradient with the image patch staged in LDS
- *                              (default) or the generic implicit-GEMM kernels (A/B tests)
+ *   conv1=packed|staged|generic  conv1 forward with packed taps (k_conv_img3, default), conv1 forward
+ *                              and weight gradient with the image patch staged in LDS (staged; the
+ *                              weight gradient's form for packed too), or the generic implicit-GEMM
+ *                              kernels (A/B tests)
+ *   conv1_mfma=auto|bx3|f32    the packed conv1 forward and the staged conv1 weight gradient with their
+ *                              products as split-bf16 MFMAs (bx3, auto: the raw byte operand is exact
+ *                              in bf16, the fp32 operand's three bf16 pieces make every product exact;
+ *                              fp32 accumulation on 16x16x32 bf16 MFMAs) or on 16x16x4 fp32 MFMAs
  *   tail=staged|fused|layers   forwards of n <= 64 rows: the MLP tail after the CNN as one launch per
  *                              dependency stage (default), one cooperative launch with a grid barrier
  *                              between stages, or one k_conv / k_conv_fin pair per layer (the path of

@@ -45,6 +45,7 @@ struct ConvArgs {
   float* part;  // split-K partial sums [Z][n * OH * OW][OC] (launch_conv sets kc and part)
   int kc;       // k-range per blockIdx.z (0: no split)
   float* wprep = nullptr;  // conv1 packed form (k_conv_img3): its A operands, [kImg3Blocks][4][16][4]
+  int bx = 0;              // conv1 packed form: 1 runs its products as split-bf16 MFMAs (k_conv_img3<.., BX>)
 };
 
 constexpr int kConvWaves = 4;
@@ -448,7 +449,10 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a) {
 // weight); only the order of the k chain differs (not bitwise k_conv's; tolerance tests).
 constexpr int kImg3KX = 8;  // extended taps per kernel row, padded
 constexpr int kConv1Auto = 2;  // the default conv1 form (ppo_carla_create_ex option conv1): packed (measured faster)
-constexpr int kConv1BxAuto = 0;  // conv1_mfma=auto: fp32 MFMAs until the split-bf16 form is measured
+// conv1_mfma=auto: the split-bf16 form (bx3). cfg5's 2 048-row update 12.33 -> 10.63 ms, batch-256
+// forward 0.69 -> 0.58 ms (profiles/r05/carla_bx/); gradient vs the fp32 torch reference 6.7e-7 rel-L2
+// (test_conv1_split_bf16_update_vs_torch)
+constexpr int kConv1BxAuto = 1;
 template <int K, int S>
 struct Img3Geo {
   static constexpr int TI = (kImgTile - 1) * S + K;          // patch rows
@@ -483,7 +487,12 @@ __host__ __device__ inline size_t img3_patch_bytes(int IC, int K, int S) {
   const int TI = (kImgTile - 1) * S + K, TIP = ((2 * S * (kImg2W / 2 - 1) + kImg3KX) + 3) & ~3;
   return ((size_t)IC * TI * TIP + 1023) & ~(size_t)1023;  // whole 4-wave DMA rounds (1 KB)
 }
-template <int K, int S>
+// BX (conv1_mfma=bx3): the k loop as v_mfma_f32_16x16x32_bf16 over block pairs (2 kk, 2 kk + 1): a
+// lane's slots e < 4 are block 2 kk's taps st = e, slots 4 + st block 2 kk + 1's. The byte operands
+// are exact bf16 numbers; the weights (fp32, 1/255 folded in) are split into their three pieces as
+// they are read (split3_pair), so every product is exact and three 16-cycle MFMAs replace eight
+// 32-cycle 16x16x4 f32 ones per row tile.
+template <int K, int S, bool BX = false>
 __global__ __launch_bounds__(256, 2) void k_conv_img3(ConvArgs a, int tiles, int tpc) {
   using G = Img3Geo<K, S>;
   constexpr int TI = G::TI, TIP = G::TIP, DW = TIP / 4;
@@ -533,6 +542,47 @@ __global__ __launch_bounds__(256, 2) void k_conv_img3(ConvArgs a, int tiles, int
     f4 acc[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[u] = f4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (BX) {
+      // ten blocks (four channels) per step: five block pairs whose row offsets are per-lane constants
+      for (int c4 = 0; c4 < (nblk + 9) / 10; ++c4) {
+#pragma unroll
+        for (int h5 = 0; h5 < 5; ++h5) {
+          const int kk = 5 * c4 + h5;
+          if (2 * kk >= nblk) break;
+          unsigned xb[2][4];
+          f4 wv[2];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const int mm = 2 * h5 + t, c2 = 2 * c4 + (mm >= 5 ? 1 : 0), m = mm >= 5 ? mm - 5 : mm;
+            const unsigned char* cbase = tile + (size_t)min(2 * c2, a.IC - 1) * TI * TIP;
+            const unsigned char* prow =
+                (2 * c2 + 1 < a.IC || rowq[m] == 0) ? cbase + rowoff[m] : tile + rowoff[m] % (TI * TIP);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) xb[t][u] = *reinterpret_cast<const unsigned*>(prow + pix[u]);
+            wv[t] = *reinterpret_cast<const f4*>(wlane + (2 * kk + t) * 256);
+          }
+          u32x4 ah, amd, al;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            unsigned h, md, l;
+            split3_pair(wv[w >> 1][2 * (w & 1)], wv[w >> 1][2 * (w & 1) + 1], h, md, l);
+            ah[w] = h; amd[w] = md; al[w] = l;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            u32x4 b;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              const unsigned x = xb[w >> 1][u], sh = 16 * (w & 1);
+              b[w] = pack_bf16_exact((float)((x >> sh) & 255u), (float)((x >> (sh + 8)) & 255u));
+            }
+            acc[u] = mfma16bx(al, b, acc[u]);
+            acc[u] = mfma16bx(amd, b, acc[u]);
+            acc[u] = mfma16bx(ah, b, acc[u]);
+          }
+        }
+      }
+    } else
     // Five k blocks = ten kernel rows = two input channels per step: the patch offset of every row is
     // a per-lane constant plus 2 TI TIP per step (rows past the last channel read channel 0: their
     // weights are 0). The operands of block kb + 1 are read from LDS under block kb's MFMAs.
@@ -984,10 +1034,16 @@ int launch_conv(const ConvArgs& a, hipStream_t s, int img = 1, bool fin = true, 
     const int tiles = ((a.OW + kImg2W - 1) / kImg2W) * ((a.OH + kImgTile - 1) / kImgTile) * a.n;
     const int grid = std::min(tiles, kImg3WG), tpc = (tiles + grid - 1) / grid;
     const size_t lds = img3_patch_bytes(a.IC, a.K, a.S) + (size_t)nblk * 256 * sizeof(float);
-    static const bool attr = hipFuncSetAttribute((const void*)k_conv_img3<5, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 (int)lds) == hipSuccess;
+    static const bool attr =
+        hipFuncSetAttribute((const void*)k_conv_img3<5, 2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) ==
+            hipSuccess &&
+        hipFuncSetAttribute((const void*)k_conv_img3<5, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) ==
+            hipSuccess;
     if (!attr) return -2;
-    hipLaunchKernelGGL((k_conv_img3<5, 2>), dim3((tiles + tpc - 1) / tpc), dim3(256), lds, s, a, tiles, tpc);
+    if (a.bx)
+      hipLaunchKernelGGL((k_conv_img3<5, 2, true>), dim3((tiles + tpc - 1) / tpc), dim3(256), lds, s, a, tiles, tpc);
+    else
+      hipLaunchKernelGGL((k_conv_img3<5, 2, false>), dim3((tiles + tpc - 1) / tpc), dim3(256), lds, s, a, tiles, tpc);
     return 0;
   }
   if (img && a.in_u8 && ((uintptr_t)a.in_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 8 && a.IW % 4 == 0 &&
@@ -1223,6 +1279,7 @@ extern "C" int ppo_carla_forward(ppo_carla_t* c, int n, const uint8_t* bev, cons
     ConvArgs a{in_f, in_u8, in_stride, IC, IH, IW, P + w, P + b, out, out_stride, OC, OH, OW, K, S, relu, n,
                c->ksplit, 0};
     a.wprep = c->c1w;
+    a.bx = c->c1bx;
     return launch_conv(a, s, c->conv_img);
   };
   auto linear = [&](const float* in, long in_stride, int IN, long w, long b, float* out, long out_stride, int OUT,

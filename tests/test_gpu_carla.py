@@ -130,14 +130,18 @@ def test_staged_conv1_kernels_match_generic():
     np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-7)
 
 
-def test_packed_conv1_matches_staged():
+@pytest.mark.parametrize("opts", [("conv1=staged", "conv1=packed,conv1_mfma=f32"),
+                                  ("conv1=packed,conv1_mfma=f32", "conv1=packed,conv1_mfma=bx3")])
+def test_packed_conv1_matches_staged(opts):
     """conv1=packed (k_conv_img3: the taps of a 16-wide MFMA k block ordered so that each lane group's
     four k-steps are four consecutive patch bytes of one kernel row, one ds_read_b32 per B quadruple,
     A operands from a pre-arranged weight table) computes every product as k_conv_img2 does (u8 / 255
     times the same weight) in another k order: forward outputs within fp32 summation noise of the
     staged kernel (n = 7, partial tiles; every sampling mode), the update's gradients per tensor
     within rel-L2 1e-5, the stepped parameters within 1e-6. Golden / oracle / torch parity of the
-    packed path itself: the module tests above run on the default conv1 form."""
+    packed path itself: the module tests above run on the default conv1 form. The same bars hold
+    between conv1's fp32-MFMA and split-bf16 forms (conv1_mfma=bx3: exact products of the byte operand
+    and the weights' three bf16 pieces on 16x16x32 bf16 MFMAs, forward and weight gradient)."""
     import carla_torch_ref  # noqa: F401
     n = 7
     L = CI.layout()
@@ -149,7 +153,7 @@ def test_packed_conv1_matches_staged():
     ret = rng.normal(0.0, 1.0, n).astype(np.float32)
     old_v = rng.normal(0.0, 1.0, n).astype(np.float32)
     outs = []
-    for opt in ("conv1=staged", "conv1=packed"):
+    for opt in opts:
         ag = ppo_amd.CarlaAgent(max_batch=16, seed=7, options=opt)
         ag.load_params(p)
         res = [run(ag, bev, meas, vmeas, mode=m, env_base=3, step_id=5) for m in ("sample", "mean", "roach")]

@@ -260,6 +260,44 @@ PPO_DEV void split3_pair(float x0, float x1, unsigned& hi, unsigned& mid, unsign
   mid = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
   lo = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
 }
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+// eight fp32 values (one lane's k slots of a bf16 MFMA operand) -> their three pieces
+struct Split3 {
+  u32x4 hi, mid, lo;
+};
+PPO_DEV Split3 split3(const float (&x)[8]) {
+  Split3 s;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    unsigned h, m, l;
+    split3_pair(x[2 * p], x[2 * p + 1], h, m, l);
+    s.hi[p] = h;
+    s.mid[p] = m;
+    s.lo[p] = l;
+  }
+  return s;
+}
+PPO_DEV f32x16 mfma_bx(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+// acc += A.B over one 16-k block as NP piece products, smallest first
+// (NP = 6: k_upd's six, without mid.lo + lo.mid + lo.lo < 2^-21 |a.b|)
+template <int NP>
+PPO_DEV f32x16 mfma_split(const Split3& A, const Split3& B, f32x16 acc) {
+  if constexpr (NP >= 9) acc = mfma_bx(A.lo, B.lo, acc);
+  if constexpr (NP >= 8) {
+    acc = mfma_bx(A.lo, B.mid, acc);
+    acc = mfma_bx(A.mid, B.lo, acc);
+  }
+  acc = mfma_bx(A.lo, B.hi, acc);
+  acc = mfma_bx(A.mid, B.mid, acc);
+  acc = mfma_bx(A.hi, B.lo, acc);
+  acc = mfma_bx(A.mid, B.hi, acc);
+  acc = mfma_bx(A.hi, B.mid, acc);
+  acc = mfma_bx(A.hi, B.hi, acc);
+  return acc;
+}
+
 // two fp32 values exact in bf16 (e.g. byte values 0..255) packed as bf16 (x0 in the low half)
 PPO_DEV unsigned pack_bf16_exact(float x0, float x1) {
   return __builtin_amdgcn_perm(__float_as_uint(x1), __float_as_uint(x0), 0x07060302u);

@@ -1252,42 +1252,6 @@ __global__ __launch_bounds__(512) void k_dwf_dma(DwArgs a) {
 // the same count as k_dwf_dma's 8 k-steps) and splits each value once (v_and / v_sub / v_perm).
 // Staging (LDS DMA, three buffers, two stages ahead) is k_dwf_dma's.
 // =============================================================================================
-struct Split3 {
-  u32x4 hi, mid, lo;
-};
-PPO_DEV Split3 split3(const float (&x)[8]) {
-  Split3 s;
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    unsigned h, m, l;
-    split3_pair(x[2 * p], x[2 * p + 1], h, m, l);
-    s.hi[p] = h;
-    s.mid[p] = m;
-    s.lo[p] = l;
-  }
-  return s;
-}
-PPO_DEV f16v mfma_bx(u32x4 a, u32x4 b, f16v c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
-}
-// acc += A.B over one 16-k block as NP piece products, smallest first
-// (NP = 6: k_upd's six, without mid.lo + lo.mid + lo.lo < 2^-21 |a.b|)
-template <int NP>
-PPO_DEV f16v mfma_split(const Split3& A, const Split3& B, f16v acc) {
-  if constexpr (NP >= 9) acc = mfma_bx(A.lo, B.lo, acc);
-  if constexpr (NP >= 8) {
-    acc = mfma_bx(A.lo, B.mid, acc);
-    acc = mfma_bx(A.mid, B.lo, acc);
-  }
-  acc = mfma_bx(A.lo, B.hi, acc);
-  acc = mfma_bx(A.mid, B.mid, acc);
-  acc = mfma_bx(A.hi, B.lo, acc);
-  acc = mfma_bx(A.mid, B.hi, acc);
-  acc = mfma_bx(A.hi, B.mid, acc);
-  acc = mfma_bx(A.hi, B.hi, acc);
-  return acc;
-}
-
 template <int H, int OP, int NSL, int NP>
 __global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];

@@ -1137,7 +1137,11 @@ __global__ __launch_bounds__(512) void k_dw2(DwArgs a) {
 // stages ahead, so one constant s_waitcnt keeps exactly the next stage in flight. Every stage past
 // the last is issued too (all out of range) to keep that count; the operand values and the MFMA
 // order are k_dw2's: bitwise k_dw2.
-template <int OP>
+// BX (dw_mfma=bf16x6 / x9 / x8, k_dwf_bx's scheme): a 16-row stage is one v_mfma_f32_32x32x16_bf16
+// k block; lane (l32, hs) reads its operand column at rows 8 hs .. 8 hs + 7 (the same LDS reads as
+// the eight 32x32x2 steps) and splits each value into its three bf16 pieces; NP piece products per
+// stage and accumulator, fp32 accumulation. Not bitwise the fp32 form (the bf16 MFMA's internal sums).
+template <int OP, int BX = 0>
 __global__ __launch_bounds__(512) void k_dw2_dma(DwArgs a) {
   constexpr int H = 64, KS = 16, NBUF = 3;
   constexpr int TI = (OP + 31) / 32, TIW = (TI + 1) / 2;
@@ -1221,6 +1225,30 @@ __global__ __launch_bounds__(512) void k_dw2_dma(DwArgs a) {
     const float* b = lds + (st % NBUF) * STG;
     const float* XS = b;
     const float* Z = b + oZ;
+    if constexpr (BX) {
+      float v8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v8[e] = Z[(wo >> 1) * KS * H + (8 * hs + e) * H + 32 * (wo & 1) + l32];
+      const Split3 az = split3(v8);
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) {
+        const int col = 32 * (TIW * wi + v) + l32;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = XS[(8 * hs + e) * OP + (FULL ? col : min(col, OP - 1))];
+          v8[e] = (FULL || col < OP) ? x : 0.f;
+        }
+        acc1[v] = mfma_split<BX>(az, split3(v8), acc1[v]);
+      }
+      float w8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v8[e] = Z[(2 + t2) * KS * H + (8 * hs + e) * H + 32 * ot2 + l32];
+        w8[e] = Z[(4 + t2) * KS * H + (8 * hs + e) * H + 32 * it2 + l32];
+      }
+      acc2 = mfma_split<BX>(split3(v8), split3(w8), acc2);
+      continue;
+    }
     float opn[TIW + 3];
     auto rd_ops = [&](int k, float (&o)[TIW + 3]) {
       const int row = k + hs;
@@ -1283,10 +1311,20 @@ int launch_dw2(const DwArgs& a, int OP, int nchunks, hipStream_t s) {
   // 32-bit buffer descriptors: the observation buffer and the row blocks must stay below 4 GB
   if (a.dma && v4 && OP == 384 && a.obs_n * 4 < 0xFFFFFFF0L && (long)a.M * 64 * 4 < 0xFFFFFFF0L) {
     constexpr size_t lds = (size_t)3 * (16 * 384 + 6 * 16 * 64) * sizeof(float) + 3 * 8 * 64 * sizeof(int);
-    static const bool ok = hipFuncSetAttribute((const void*)k_dw2_dma<384>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)lds) == hipSuccess;
-    if (!ok) return -2;
-    hipLaunchKernelGGL((k_dw2_dma<384>), dim3(nchunks), dim3(512), lds, s, a);
+    const void* k = a.bx == 6   ? (const void*)k_dw2_dma<384, 6>
+                    : a.bx == 8 ? (const void*)k_dw2_dma<384, 8>
+                    : a.bx == 9 ? (const void*)k_dw2_dma<384, 9>
+                                : (const void*)k_dw2_dma<384, 0>;
+    static bool attr[10] = {};
+    const int ai = a.bx >= 0 && a.bx < 10 ? a.bx : 0;
+    if (!attr[ai]) {
+      if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
+      attr[ai] = true;
+    }
+    if (a.bx == 6) hipLaunchKernelGGL((k_dw2_dma<384, 6>), dim3(nchunks), dim3(512), lds, s, a);
+    else if (a.bx == 8) hipLaunchKernelGGL((k_dw2_dma<384, 8>), dim3(nchunks), dim3(512), lds, s, a);
+    else if (a.bx == 9) hipLaunchKernelGGL((k_dw2_dma<384, 9>), dim3(nchunks), dim3(512), lds, s, a);
+    else hipLaunchKernelGGL((k_dw2_dma<384, 0>), dim3(nchunks), dim3(512), lds, s, a);
     return 0;
   }
   if (OP == 16) return v4 ? launch_dw2_t<16, 4>(a, nchunks, s) : launch_dw2_t<16, 1>(a, nchunks, s);

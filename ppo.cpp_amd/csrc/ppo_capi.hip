@@ -1334,9 +1334,10 @@ extern "C" int ppo_kernel_info(const ppo_t* c, char* buf, int len) {
                                    : "k_fwdbwd";
   const int H = c->K.H, OP = c->K.OP;
   const bool fused = c->dw_fused && H == 256 && (OP == 16 || OP == 32);  // launch_dw's dispatch
-  std::string dw = c->use_upd2 ? "k_dw2_dma"
+  const std::string bxs = c->dw_bx ? "/bf16x" + std::to_string(c->dw_bx) : "/f32";
+  std::string dw = c->use_upd2 ? (c->dw_dma && OP == 384 && c->K.O % 4 == 0 ? "k_dw2_dma" + bxs : "k_dw2")
                    : fused ? (!c->dw_dma ? "k_dwf" : c->dw_bx ? "k_dwf_bx/bf16x" + std::to_string(c->dw_bx) : "k_dwf_dma/f32")
-                   : (c->dw_dma && H == 256 && OP == 112) ? "k_dw_dma"
+                   : (c->dw_dma && H == 256 && OP == 112) ? "k_dw_dma" + bxs
                                                           : "k_dw";
   const std::string s = "update=" + upd + " dw=" + dw;
   snprintf(buf, (size_t)len, "%s", s.c_str());

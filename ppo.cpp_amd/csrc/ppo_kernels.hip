@@ -884,8 +884,10 @@ PPO_DEV void wait_vmcnt_upto7(int n) {
 // dw_phase with the stage rows moved by LDS DMA (16 bytes a lane, one 1 KB wave instruction per
 // 256 floats; rows contiguous in HBM, IN rows of LDI floats, no permutation) into three unpadded
 // stage buffers two stages ahead — k_dwf_dma's pipeline for the two-phase k_dw (wide inputs: Ant's
-// OP = 112). Same operands and MFMA order as dw_phase: bitwise.
-template <int NO, int NI, int LDI, int WO, int WI>
+// OP = 112). Same operands and MFMA order as dw_phase: bitwise. NP > 0 (dw_mfma=bf16x6 / x8 / x9):
+// a 16-row stage is one v_mfma_f32_32x32x16_bf16 k block of NP split-bf16 piece products (k_dwf_bx's
+// scheme; each lane splits its column of rows 8 hs .. 8 hs + 7 as read).
+template <int NO, int NI, int LDI, int WO, int WI, int NP = 0>
 PPO_DEV void dw_phase_dma(const float* __restrict__ DZ, const float* __restrict__ IN, long M, long m0, long m1,
                           float* __restrict__ out, float* lds, int tid) {
   constexpr int TO = NO / 32, TI = (NI + 31) / 32;
@@ -938,6 +940,28 @@ PPO_DEV void dw_phase_dma(const float* __restrict__ DZ, const float* __restrict_
     __builtin_amdgcn_sched_barrier(0);
     const float* sdz = lds + (sI % NBUF) * STG;
     const float* sin = sdz + ADZ;
+    if constexpr (NP > 0) {
+      Split3 as[TOW];
+#pragma unroll
+      for (int u = 0; u < TOW; ++u) {
+        float v8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v8[e] = sdz[(8 * hs + e) * NO + (wo * TOW + u) * 32 + l32];
+        as[u] = split3(v8);
+      }
+#pragma unroll
+      for (int v = 0; v < TIW; ++v) {
+        const int col = (wi * TIW + v) * 32 + l32;
+        float w8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          w8[e] = (FULL || col < LDI) ? sin[(8 * hs + e) * LDI + (FULL ? col : min(col, LDI - 1))] : 0.0f;
+        const Split3 bs = split3(w8);
+#pragma unroll
+        for (int u = 0; u < TOW; ++u) acc[u][v] = mfma_split<NP>(as[u], bs, acc[u][v]);
+      }
+      continue;
+    }
 #pragma unroll
     for (int k = 0; k < KS; k += 2) {
       float av[TOW], bv[TIW];
@@ -967,7 +991,7 @@ PPO_DEV void dw_phase_dma(const float* __restrict__ DZ, const float* __restrict_
       }
 }
 
-template <int H, int OP>
+template <int H, int OP, int NP = 0>
 __global__ __launch_bounds__(512) void k_dw_dma(DwArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int TO = H / 32;
@@ -978,8 +1002,8 @@ __global__ __launch_bounds__(512) void k_dw_dma(DwArgs a) {
   const long m1 = min((long)a.M, m0 + a.rows_per_chunk);
   float* out = a.slab[trunk] + (size_t)blockIdx.x * a.slab_stride;
   if (m0 < m1) {
-    dw_phase_dma<H, H, H, WO2, WI2>(a.dz2[trunk], a.h1[trunk], a.M, m0, m1, out, lds, threadIdx.x);
-    dw_phase_dma<H, OP, OP, WO1, WI1>(a.dz1[trunk], a.xn, a.M, m0, m1, out + H * H, lds, threadIdx.x);
+    dw_phase_dma<H, H, H, WO2, WI2, NP>(a.dz2[trunk], a.h1[trunk], a.M, m0, m1, out, lds, threadIdx.x);
+    dw_phase_dma<H, OP, OP, WO1, WI1, NP>(a.dz1[trunk], a.xn, a.M, m0, m1, out + H * H, lds, threadIdx.x);
   }
 }
 
@@ -2065,13 +2089,14 @@ static int launch_dwf_t(const DwArgs& a0, int nchunks, hipStream_t s) {
 // k_dw_dma: the stage buffers of the larger phase, three of them
 template <int H, int OP>
 static int launch_dw_dma_t(const DwArgs& a, int nchunks, hipStream_t s) {
-  auto k = k_dw_dma<H, OP>;
+  auto k = a.bx == 6 ? k_dw_dma<H, OP, 6> : a.bx == 8 ? k_dw_dma<H, OP, 8> : a.bx == 9 ? k_dw_dma<H, OP, 9> : k_dw_dma<H, OP, 0>;
   constexpr int big = H > OP ? H : OP;
   constexpr size_t lds = (size_t)3 * 16 * (H + big) * sizeof(float);
-  static bool attr = false;
-  if (!attr) {
+  static bool attr[10] = {};
+  const int ai = a.bx >= 0 && a.bx < 10 ? a.bx : 0;
+  if (!attr[ai]) {
     if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
-    attr = true;
+    attr[ai] = true;
   }
   hipLaunchKernelGGL(k, dim3(nchunks, 2), dim3(512), lds, s, a);
   return 0;

@@ -470,7 +470,7 @@ def test_fused_dw_matches_two_phase_dw(kind, O_, A, H, E):
     perm = rng.permutation(B).astype(np.int32)
     grads = []
     # (fp32 MFMAs throughout: the default fused dW runs split-bf16 products, dw_mfma)
-    for opt in ("dw_fused=0", "dw_dma=0", "dw_dma=1,dw_mfma=f32"):
+    for opt in ("dw_fused=0,dw_mfma=f32", "dw_dma=0", "dw_dma=1,dw_mfma=f32"):
         ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.1, options=opt)
         ag.load_params(p)
         fill_storage(ag, T, E, x, act, olp, adv, ret, ov)

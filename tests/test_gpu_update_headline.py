@@ -201,7 +201,8 @@ def test_refused_options_free_the_context():
 
 
 @pytest.mark.parametrize("kind,O_,A,H,E,T", [(1, 17, 6, 256, 1024, 32), (1, 17, 6, 256, 1599, 8),
-                                             (0, 376, 17, 64, 1024, 16), (0, 376, 17, 64, 1599, 8)])
+                                             (0, 376, 17, 64, 1024, 16), (0, 376, 17, 64, 1599, 8),
+                                             (1, 105, 8, 256, 1024, 8)])
 def test_split_bf16_dw_is_as_accurate_as_fp32_mfma(kind, O_, A, H, E, T):
     """k_dwf_bx (dW as exact bf16 piece products on v_mfma_f32_32x32x16_bf16, fp32 accumulation;
     opt-in create option dw_mfma=bf16x9 / bf16x8) against k_dwf_dma (v_mfma_f32_32x32x2_f32) on the
@@ -215,7 +216,7 @@ def test_split_bf16_dw_is_as_accurate_as_fp32_mfma(kind, O_, A, H, E, T):
     §8) measured 1.16e-7 against 7.7e-8 there. Every other gradient entry comes from k_upd / k_colsum
     and is bitwise the fp32 path's. The 64-wide agent (cfg2's Humanoid shape) runs the same three forms
     in k_dw2_dma (dW1 over the gathered 376-wide observation rows, dW2; one 16-row stage per
-    32x32x16 bf16 MFMA k block)."""
+    32x32x16 bf16 MFMA k block), Ant's O = 105 (OP = 112) in the two-phase k_dw_dma the same way."""
     rng = np.random.default_rng(41)
     M = E * T
     L = O.layout_init(kind, O_, A, H)

@@ -1636,42 +1636,63 @@ __global__ void k_transpose(const float* __restrict__ src, float* __restrict__ d
 // k_gae — one thread per env, t = T-1 .. 0; op-for-op fp32 (no contraction), ppo:447-467.
 // The recurrence stays serial per env (bit-exact with the reference's order); its inputs are not:
 // rewards / values / dones of kGaeChunk steps are loaded together (coalesced over envs, loads
-// unconditional with a clamped step), so T steps cost T / kGaeChunk memory round trips.
+// unconditional with a clamped step), and the next chunk's loads are issued before the current
+// chunk's recurrence runs (two register buffers), so the memory round trips overlap the serial
+// chain instead of alternating with it. 64-thread workgroups spread few envs over many CUs (cfg2:
+// E = 1 024 envs on 16 CUs instead of 4).
 // =============================================================================================
 constexpr int kGaeChunk = 32;
-__global__ __launch_bounds__(256) void k_gae(GaeArgs a) {
+struct GaeChunk {
+  float r[kGaeChunk], v[kGaeChunk], d[kGaeChunk];
+};
+PPO_DEV void gae_load(const GaeArgs& a, int e, int t1, GaeChunk& c) {
+  const long E = a.E;
+#pragma unroll
+  for (int k = 0; k < kGaeChunk; ++k) {
+    const int t = t1 - k >= 0 ? t1 - k : 0;
+    const long idx = (long)t * E + e;
+    c.r[k] = a.rewards[idx];
+    c.v[k] = a.values[idx];
+    c.d[k] = a.dones[idx];
+  }
+}
+PPO_DEV void gae_run(const GaeArgs& a, int e, int t1, const GaeChunk& c, float& last, float& nnt, float& nv) {
 #pragma clang fp contract(off)
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= a.E) return;
   const long E = a.E;
   const float gl = (a.gamma * a.lam);
+#pragma unroll
+  for (int k = 0; k < kGaeChunk; ++k) {
+    if (t1 - k < 0) break;
+    const long idx = (long)(t1 - k) * E + e;
+    const float r = c.r[k], v = c.v[k];
+    const float gnv = (a.gamma * nv);
+    const float delta = ((r + (gnv * nnt)) - v);
+    const float adv = (delta + ((gl * nnt) * last));
+    a.adv[idx] = adv;
+    a.ret[idx] = (adv + v);
+    last = adv;
+    nnt = (1.0f - c.d[k]);
+    nv = v;
+  }
+}
+__global__ __launch_bounds__(64) void k_gae(GaeArgs a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.E) return;
   float last = 0.0f;
   float nnt = (1.0f - a.next_done[e]);
   float nv = a.next_value[e];
-  for (int t1 = a.T - 1; t1 >= 0; t1 -= kGaeChunk) {
-    float rr[kGaeChunk], vv[kGaeChunk], dd[kGaeChunk];
-#pragma unroll
-    for (int k = 0; k < kGaeChunk; ++k) {
-      const int t = t1 - k >= 0 ? t1 - k : 0;
-      const long idx = (long)t * E + e;
-      rr[k] = a.rewards[idx];
-      vv[k] = a.values[idx];
-      dd[k] = a.dones[idx];
-    }
-#pragma unroll
-    for (int k = 0; k < kGaeChunk; ++k) {
-      if (t1 - k < 0) break;
-      const long idx = (long)(t1 - k) * E + e;
-      const float r = rr[k], v = vv[k];
-      const float gnv = (a.gamma * nv);
-      const float delta = ((r + (gnv * nnt)) - v);
-      const float adv = (delta + ((gl * nnt) * last));
-      a.adv[idx] = adv;
-      a.ret[idx] = (adv + v);
-      last = adv;
-      nnt = (1.0f - dd[k]);
-      nv = v;
-    }
+  GaeChunk c0, c1;
+  int t1 = a.T - 1;
+  gae_load(a, e, t1, c0);
+  while (t1 >= 0) {
+    const int t2 = t1 - kGaeChunk;
+    if (t2 >= 0) gae_load(a, e, t2, c1);
+    gae_run(a, e, t1, c0, last, nnt, nv);
+    if (t2 < 0) break;
+    const int t3 = t2 - kGaeChunk;
+    if (t3 >= 0) gae_load(a, e, t3, c0);
+    gae_run(a, e, t2, c1, last, nnt, nv);
+    t1 = t3;
   }
 }
 
@@ -2157,7 +2178,7 @@ void launch_swizzle(const float* w1, const float* w2, float* dst, int H, int OP,
   hipLaunchKernelGGL(k_swizzle, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w1, w2, dst, H, OP, bx);
 }
 void launch_gae(const GaeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_gae, dim3((a.E + 255) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_gae, dim3((a.E + 63) / 64), dim3(64), 0, s, a);
 }
 void launch_perm(int32_t* out, uint32_t B, const PermKey& pk, hipStream_t s) {
   hipLaunchKernelGGL(k_perm, dim3((B + 255) / 256), dim3(256), 0, s, out, B, pk);

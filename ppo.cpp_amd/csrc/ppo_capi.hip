@@ -304,6 +304,8 @@ static constexpr int kDwBxAuto = 6;
 // H = 256, one head tile): as exact as the fp32 MFMA form against the oracle
 // (test_upd_bx6_is_as_accurate_as_fp32_mfma), k_upd 0.775 -> 0.606 ms per launch at the metric config
 static constexpr int kUpdBxAuto = 1;
+// upd_mfma=auto for the 64-wide agent: k_upd2's layer 1 as split-bf16 piece products where instantiated
+static constexpr int kUpd2BxAuto = 1;
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
   std::string s(opts);
@@ -433,8 +435,8 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   const size_t PS = c->K.size;
   rc |= dmalloc(&c->P, PS); rc |= dmalloc(&c->G, PS); rc |= dmalloc(&c->Am, PS); rc |= dmalloc(&c->Av, PS);
   for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->W2T[k], (size_t)H * H);
-  // H = 256: room for the split-bf16 pieces of W2 | W2^T after the fp32 copies (upd_mfma=bx6)
-  for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->WSW[k], (size_t)(sw_size(H, c->K.OP) + (H == 256 ? bx_size(H) : 0)));
+  // room for the split-bf16 pieces after the fp32 copies (upd_mfma=bx6): W2 | W2^T at H = 256, W1 at 64
+  for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->WSW[k], (size_t)(sw_size(H, c->K.OP) + bx_region(H, c->K.OP)));
   const size_t E = cfg->num_envs, T = cfg->num_steps;
   rc |= dmalloc(&c->buf[PPO_BUF_OBS], T * E * O);
   rc |= dmalloc(&c->buf[PPO_BUF_ACTIONS], T * E * A);
@@ -465,9 +467,11 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
       ppo_destroy(c);
       return fail("ppo_create: upd_mfma=32 / mix needs the LayerNorm-Beta agent at hidden 256");
     }
-    if (opt.upd_mfma == 6 && (H != 256 || cfg->net_kind != PPO_NET_LN_BETA)) {
+    const char* bx_refusal = "ppo_create: upd_mfma=bx6 needs the LayerNorm-Beta agent at hidden 256 with at most 16 "
+                             "heads, or the 64-wide agent's single k_upd2 at OP = 384";
+    if (opt.upd_mfma == 6 && !((H == 256 && cfg->net_kind == PPO_NET_LN_BETA) || H == 64)) {
       ppo_destroy(c);
-      return fail("ppo_create: upd_mfma=bx6 needs the LayerNorm-Beta agent at hidden 256 with at most 16 heads");
+      return fail(bx_refusal);
     }
     if (opt.upd2_split > 0 && (upd_kernel || !fits32 || !upd2_split_supported(c->K))) {
       ppo_destroy(c);
@@ -476,6 +480,16 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
     if (!upd_kernel && fits32 && upd2_supported(c->K, &c->upd, split) == 0) {
       c->use_upd = c->use_upd2 = true;
       c->upd2_split = split;
+      // layer 1 as split-bf16 piece products (the single kernel at cfg2's shape)
+      const bool want_bx = opt.upd_mfma == 6 || (opt.upd_mfma == 0 && kUpd2BxAuto);
+      if (want_bx && split == 0 && upd2_supported(c->K, &c->upd, 0, 1) == 0) {
+        c->upd_bx = 2;
+      } else if (opt.upd_mfma == 6) {
+        ppo_destroy(c);
+        return fail(bx_refusal);
+      } else if (want_bx) {
+        upd2_supported(c->K, &c->upd, split);  // the fp32 form's geometry again
+      }
       const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
       // both trunks per workgroup, 2 workgroups per CU x 256 CUs (split form: 3 per CU)
       c->upd_nblk = std::min(ut, split ? 256 * split : 512);
@@ -492,7 +506,7 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
                 upd_supported(c->K, c->sg[1].nh, c->sg[0].size, c->sg[1].size, &c->upd, 1) == 0)) {
       if (upd_kernel || upd_supported(c->K, c->sg[1].nh, c->sg[0].size, c->sg[1].size, &c->upd, 1) != 0) {
         ppo_destroy(c);
-        return fail("ppo_create: upd_mfma=bx6 needs the LayerNorm-Beta agent at hidden 256 with at most 16 heads");
+        return fail(bx_refusal);
       }
       c->use_upd = true;
       c->upd_bx = 1;
@@ -1328,7 +1342,7 @@ extern "C" int ppo_get_device(const ppo_t* c, int* device, char* pci_bus_id, int
 
 extern "C" int ppo_kernel_info(const ppo_t* c, char* buf, int len) {
   if (!c || !buf || len <= 0) return fail("ppo_kernel_info: null argument");
-  std::string upd = c->use_upd2    ? (c->upd2_split ? "k_l1g+k_upd2" : "k_upd2")
+  std::string upd = c->use_upd2    ? (c->upd2_split ? "k_l1g+k_upd2" : c->upd_bx ? "k_upd2/bx6" : "k_upd2/f32")
                     : c->use_upd32 ? (c->upd32_mix ? "k_upd32/mix" : "k_upd32")
                     : c->use_upd   ? (c->upd_bx ? "k_upd/bx6" : "k_upd/f32")
                                    : "k_fwdbwd";

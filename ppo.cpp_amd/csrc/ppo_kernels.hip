@@ -1564,7 +1564,7 @@ PPO_DEV void adam_block(const AdamArgs& a, int bid, float* s_norm, float& s_coef
         float* w = a.wsw[k] + (long)a.H * a.OP;
         w[sw_index(r, cI, a.H)] = np;
         w[(long)a.H * a.H + sw_index(cI, r, a.H)] = np;
-        if (a.bx) {  // split-bf16 pieces of W2 | W2^T (bx_index), after the fp32 copies
+        if (a.bx == 1) {  // split-bf16 pieces of W2 | W2^T (bx_index), after the fp32 copies
           uint16_t* pw = reinterpret_cast<uint16_t*>(a.wsw[k] + sw_size(a.H, a.OP));
           uint16_t pc[3];
           split3_bits(np, pc);
@@ -1577,7 +1577,17 @@ PPO_DEV void adam_block(const AdamArgs& a, int bid, float* s_norm, float& s_coef
       }
     }
     const long o1 = p - a.w1_off[k];
-    if (a.wsw[k] && o1 >= 0 && o1 < (long)a.H * a.OP) a.wsw[k][sw_index((int)(o1 / a.OP), (int)(o1 % a.OP), a.OP)] = np;
+    if (a.wsw[k] && o1 >= 0 && o1 < (long)a.H * a.OP) {
+      const int r = (int)(o1 / a.OP), cI = (int)(o1 % a.OP);
+      a.wsw[k][sw_index(r, cI, a.OP)] = np;
+      if (a.bx == 2) {  // split-bf16 pieces of W1 (bx_index), after the fp32 copies
+        uint16_t* pw = reinterpret_cast<uint16_t*>(a.wsw[k] + sw_size(a.H, a.OP));
+        uint16_t pc[3];
+        split3_bits(np, pc);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) pw[bx_index(r, cI, a.OP, q)] = pc[q];
+      }
+    }
   }
 }
 
@@ -1601,19 +1611,26 @@ __global__ __launch_bounds__(256) void k_gradstep(NormArgs na, AdamArgs a, unsig
 }
 
 // swizzled copies of one trunk (sw_index): [W1 (H x OP) | W2 (H x H) | W2^T (H x H)]
-// bx: also the split-bf16 pieces of W2 | W2^T (bx_index) after them
+// bx: also the split-bf16 pieces (bx_index) after them: 1 of W2 | W2^T, 2 of W1
 __global__ void k_swizzle(const float* __restrict__ w1, const float* __restrict__ w2, float* __restrict__ dst, int H,
                           int OP, int bx) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long n1 = (long)H * OP, n2 = (long)H * H;
   if (i < n1) {
-    dst[sw_index((int)(i / OP), (int)(i % OP), OP)] = w1[i];
+    const int r = (int)(i / OP), c = (int)(i % OP);
+    dst[sw_index(r, c, OP)] = w1[i];
+    if (bx == 2) {
+      uint16_t* pw = reinterpret_cast<uint16_t*>(dst + sw_size(H, OP));
+      uint16_t pc[3];
+      split3_bits(w1[i], pc);
+      for (int q = 0; q < 3; ++q) pw[bx_index(r, c, OP, q)] = pc[q];
+    }
   } else if (i < n1 + n2) {
     const long o = i - n1;
     const int r = (int)(o / H), c = (int)(o % H);
     dst[n1 + sw_index(r, c, H)] = w2[o];
     dst[n1 + n2 + sw_index(c, r, H)] = w2[o];
-    if (bx) {
+    if (bx == 1) {
       uint16_t* pw = reinterpret_cast<uint16_t*>(dst + sw_size(H, OP));
       uint16_t pc[3];
       split3_bits(w2[o], pc);

@@ -72,6 +72,10 @@ PPO_DEV_HOST inline long bx_index(int r, int c, int ncols, int p) {
   return ((((long)(r >> 4) * (ncols >> 5) + (c >> 5)) * 3 + p) * 64 + lane) * 8 + e;
 }
 PPO_DEV_HOST inline long bx_size(int H) { return 3L * H * H; }  // floats: W2 | W2^T pieces
+// the 64-wide agent (k_upd2's split-bf16 layer 1): the pieces of W1 (H x OP) instead, same layout
+PPO_DEV_HOST inline long bx_w1_size(int H, int OP) { return 3L * H * OP / 2; }
+// floats of a trunk's piece region (after its fp32 swizzled copies)
+PPO_DEV_HOST inline long bx_region(int H, int OP) { return H == 256 ? bx_size(H) : H == 64 ? bx_w1_size(H, OP) : 0; }
 
 struct UpdArgs {
   const float* P;
@@ -99,7 +103,8 @@ struct UpdArgs {
   int trunk_mask;         // k_upd: trunks to run (bit t = trunk t; 3 = both; other values: PPO_DIAG builds only)
   int sched;              // k_upd: bit 0 actor workgroups dispatched first, bit 1 actor wave priority
   int hot;                // diagnostic build only (PPO_UPD2_HOT): k_upd2 gathers the rows of its first 8 tiles only
-  int bx;                 // k_upd: 1 runs the 256-wide GEMMs as split-bf16 piece products (upd_mfma=bx6)
+  int bx;                 // k_upd: 1 runs the 256-wide GEMMs as split-bf16 piece products (upd_mfma=bx6);
+                          // k_upd2: 2 runs layer 1 that way
 };
 
 // k_upd geometry (ppo_update.hip)
@@ -183,7 +188,7 @@ struct AdamArgs {
   // step_size / sbc2, so the captured launch sequence stays valid across iterations
   const float* sched;
   int gi;
-  int bx;  // 1: also refresh the split-bf16 pieces of W2 | W2^T (bx_index) after each wsw copy
+  int bx;  // also refresh the split-bf16 pieces (bx_index) after each wsw copy: 1 of W2 | W2^T, 2 of W1
 };
 
 struct GaeArgs {
@@ -284,8 +289,9 @@ int upd32_supported(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_s
 int launch_upd32(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hipStream_t s, int mix);
 // ppo_update_narrow.hip (H = 64 tanh agent); split form: k_l1g computes layer 1 (a.Z1), k_upd2 the rest
 bool upd2_split_supported(const PackedLayout& K);
-// split: 0 one kernel; 2 / 3 the split form at 2 / 3 workgroups per CU
-int upd2_supported(const PackedLayout& K, UpdGeoOut* g, int split);
+// split: 0 one kernel; 2 / 3 the split form at 2 / 3 workgroups per CU; bx: layer 1 as split-bf16
+// piece products (cfg2's Humanoid shape)
+int upd2_supported(const PackedLayout& K, UpdGeoOut* g, int split, int bx = 0);
 int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s, int split);
 int launch_l1g(const UpdArgs& a, hipStream_t s);
 int launch_dw2(const DwArgs& a, int OP, int nchunks, hipStream_t s);  // both 64-wide trunks, rows gathered once

@@ -98,6 +98,9 @@ struct Geo2 {
   static constexpr int oITM = oSP + 4 * NHP + 4;        // [R*A][4] items, then [64 ceil(R*A / 64)] actions
 };
 
+#ifndef PPO_BX2_D
+#define PPO_BX2_D 1
+#endif
 PPO_DEV float lf(const float* p) { return *p; }
 PPO_DEV f4 lf4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 PPO_DEV void sf4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
@@ -170,9 +173,16 @@ PPO_DEV void mm64(f4 (&out)[FT2][RT2], PBuf wb, int wlane, const float* in) {
 // SPLIT (2 or 3: workgroups per CU): layer 1's pre-activations come from k_l1g (a.Z1 rows, bias
 // included) instead of the staged X chunks and W1: the kernel is the tail only (tanh onwards), with
 // a smaller LDS / register footprint (3 per CU: 168 VGPRs, a few spilled registers).
-template <int NTO, int NHT, int VEC, int NUA, int SPLIT>
+// BX: layer 1 as split-bf16 piece products (upd_mfma=bx6, k_upd's scheme): each staged
+// 128-column chunk is split ONCE into bf16 pieces (XP: [32 rows][3 pieces x 128 bf16 + 16 B], in the
+// space of ACT and SCR, which layer 1 does not use) by all 256 threads between two barriers; the MFMAs
+// then read 3 ds_read_b128 per row tile and 32 k, the W1 pieces come from their bx_index copy
+// (k_adam), and six v_mfma_f32_16x16x32_bf16 replace eight x four 16x16x4 f32 ones per (feature
+// tile, row tile) and 32 k.
+template <int NTO, int NHT, int VEC, int NUA, int SPLIT, int BX = 0>
 __global__ __launch_bounds__(256, SPLIT ? SPLIT : 2) void k_upd2(UpdArgs a) {
   using GE = Geo2<NTO, NHT, VEC, NUA, SPLIT>;
+  static_assert(!BX || (GE::CW == 128 && NTO % 8 == 0 && !SPLIT), "k_upd2 BX: whole 128-column chunks");
   constexpr int OP = GE::OP, CKB = GE::CKB, NCH = GE::NCH, CW = GE::CW, LDX = GE::LDX, NHP = GE::NHP;
   constexpr int LDG = GE::LDG, PERROW = GE::PERROW, NGI = GE::NGI, NU = GE::NU, UPR = GE::UPR, SWZ = GE::SWZ;
   constexpr int W1D = 3;  // W1 A-operand prefetch depth (k-blocks; 2 -> 3: cfg2 k_upd2 44.05 -> 43.88 ms)
@@ -364,7 +374,85 @@ __global__ __launch_bounds__(256, SPLIT ? SPLIT : 2) void k_upd2(UpdArgs a) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) z[ft][rt] = bv;
     }
-    {
+    if constexpr (BX) {
+      constexpr int LDB = 3 * (CW / 2) + 4;  // floats per XP row (row stride 4 mod 64 banks)
+      static_assert(R * LDB <= GE::oGG - GE::oACT, "XP must fit in ACT + SCR");
+      float* XP = lds + GE::oACT;
+      constexpr int NKK = NTO / 2, KPC = CW / 32, D2 = PPO_BX2_D;  // 32-k units: per tile, per chunk
+      const PBuf w1b = make_pbuf(a.WSW[trunk] + sw_size(H, OP), (int)bx_w1_size(H, OP));
+      const int w1blane = ((fbase >> 4) * NKK * 3 * 64 + lane) * 4;
+      u32x4 wr[D2 + 1][FT][3];
+      auto load_w = [&](int kk, u32x4 (&dst)[FT][3]) {
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) dst[ft][p] = __builtin_bit_cast(u32x4, pld4(w1b, w1blane, 256 * ((ft * NKK + kk) * 3 + p)));
+      };
+      // the chunk in X buffer buf -> its pieces in XP: unit (row, lu) = columns 4 lu .. + 3 at bf16
+      // position 32 (lu >> 3) + 8 (lu & 3) + 4 ((lu >> 2) & 1) of each piece (mm_bx's k slots)
+      auto split_chunk = [&](int buf) {
+        const float* xs = XS + buf * R * LDX;
+#pragma unroll
+        for (int q = 0; q < R * UPR / 256; ++q) {
+          const int un = tid + 256 * q, row = un / UPR, lu = un - row * UPR;
+          const f4 x = lf4(xs + row * LDX + 4 * (lu ^ (row & (SWZ - 1))));
+          float* qp = XP + row * LDB + 16 * (lu >> 3) + 4 * (lu & 3) + 2 * ((lu >> 2) & 1);
+          unsigned h0, m0, l0, h1, m1, l1;
+          split3_pair(x[0], x[1], h0, m0, l0);
+          split3_pair(x[2], x[3], h1, m1, l1);
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<u32x2*>(qp) = u32x2{h0, h1};
+          *reinterpret_cast<u32x2*>(qp + CW / 2) = u32x2{m0, m1};
+          *reinterpret_cast<u32x2*>(qp + CW) = u32x2{l0, l1};
+        }
+      };
+      if (NCH > 1) issue(pcur, 1, tp ^ 1);
+      else issue(pnext, 0, tp ^ 1);
+#pragma unroll
+      for (int q = 0; q < D2 && q < NKK; ++q) load_w(q, wr[q]);
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        const int kp = kk % KPC;
+        if (kp == 0) {
+          const int ch = kk / KPC;
+          if (ch > 0) {
+            // chunk ch landed: only the W1 piece loads of units kk .. kk + D2 - 1 may still be in flight
+            if constexpr (D2 == 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else if constexpr (D2 == 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            else static_assert(D2 == 1 || D2 == 2, "vmcnt: D2 x FT2 x 3 piece loads");
+          }
+          lds_barrier();  // every wave is done reading XP (the previous chunk) and chunk ch is visible
+          split_chunk(tp ^ (ch & 1));
+          lds_barrier();
+          if (ch > 0) {
+            if (ch + 1 < NCH) issue(pcur, ch + 1, tp ^ ((ch + 1) & 1));
+            else issue(pnext, 0, tp ^ (NCH & 1));
+          }
+        }
+        if (kk + D2 < NKK) load_w(kk + D2, wr[(kk + D2) % (D2 + 1)]);
+        __builtin_amdgcn_sched_barrier(0);
+        u32x4 bs[RT][3];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            bs[rt][p] = __builtin_bit_cast(u32x4, lf4(XP + (16 * rt + j) * LDB + (CW / 2) * p + 16 * kp + 4 * g));
+        const u32x4(&av)[FT][3] = wr[kk % (D2 + 1)];
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) {
+            f4 acc = z[ft][rt];
+            acc = mfma16bx(av[ft][2], bs[rt][0], acc);
+            acc = mfma16bx(av[ft][0], bs[rt][2], acc);
+            acc = mfma16bx(av[ft][1], bs[rt][1], acc);
+            acc = mfma16bx(av[ft][1], bs[rt][0], acc);
+            acc = mfma16bx(av[ft][0], bs[rt][1], acc);
+            z[ft][rt] = mfma16bx(av[ft][0], bs[rt][0], acc);
+          }
+      }
+      lds_barrier();  // XP (ACT / SCR) is read by no wave any more: h1 goes to ACT next
+    } else {
       if (NCH > 1) issue(pcur, 1, tp ^ 1);
       else issue(pnext, 0, tp ^ 1);
       f4 w[W1D + 1][FT];
@@ -900,7 +988,11 @@ static int dispatch_upd2(const PackedLayout& K, int split, F&& f) {
   return -1;
 }
 
-int upd2_supported(const PackedLayout& K, UpdGeoOut* g, int split) {
+// the split-bf16 layer 1 is instantiated for cfg2's shape (Humanoid O = 376: OP = 384, 17 actions)
+template <int NTO, int NHT, int VEC, int NU, int SP>
+constexpr bool upd2_bx_ok() { return NTO == 24 && NHT == 2 && VEC == 4 && NU == 3 && SP == 0; }
+
+int upd2_supported(const PackedLayout& K, UpdGeoOut* g, int split, int bx) {
   if (split) {
     const auto k = k_l1g<384>;
     if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1g_lds_bytes()) !=
@@ -917,12 +1009,14 @@ int upd2_supported(const PackedLayout& K, UpdGeoOut* g, int split) {
     g->spar_off = 0;
     g->lds_bytes = (size_t)off * sizeof(float);
     g->rows = R2;
-    const auto k = k_upd2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value, decltype(NU_)::value,
-                          decltype(SP_)::value>;
-    return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) ==
-                   hipSuccess
-               ? 0
-               : -2;
+    constexpr int N = decltype(NTO_)::value, T = decltype(NHT_)::value, V = decltype(VEC_)::value,
+                  U = decltype(NU_)::value, S = decltype(SP_)::value;
+    const void* k = (const void*)k_upd2<N, T, V, U, S, 0>;
+    if (bx) {
+      if constexpr (upd2_bx_ok<N, T, V, U, S>()) k = (const void*)k_upd2<N, T, V, U, S, 1>;
+      else return -1;
+    }
+    return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g->lds_bytes) == hipSuccess ? 0 : -2;
   });
 }
 
@@ -938,9 +1032,16 @@ extern "C" int ppo_diag_read_stamps2(unsigned long long* host, long n) {
 
 int launch_upd2(const UpdArgs& a, int nblocks, size_t lds_bytes, hipStream_t s, int split) {
   return dispatch_upd2(a.K, split, [&](auto NTO_, auto NHT_, auto VEC_, auto NU_, auto SP_) {
-    hipLaunchKernelGGL((k_upd2<decltype(NTO_)::value, decltype(NHT_)::value, decltype(VEC_)::value,
-                               decltype(NU_)::value, decltype(SP_)::value>),
-                       dim3(nblocks), dim3(256), lds_bytes, s, a);
+    constexpr int N = decltype(NTO_)::value, T = decltype(NHT_)::value, V = decltype(VEC_)::value,
+                  U = decltype(NU_)::value, S = decltype(SP_)::value;
+    if (a.bx == 2) {
+      if constexpr (upd2_bx_ok<N, T, V, U, S>()) {
+        hipLaunchKernelGGL((k_upd2<N, T, V, U, S, 1>), dim3(nblocks), dim3(256), lds_bytes, s, a);
+        return 0;
+      }
+      return -1;
+    }
+    hipLaunchKernelGGL((k_upd2<N, T, V, U, S, 0>), dim3(nblocks), dim3(256), lds_bytes, s, a);
     return 0;
   });
 }

@@ -52,7 +52,9 @@ from test_gpu_parity import fill_storage, make_agent, random_params, rel  # noqa
     # cfg2: ppo_continuous_action Humanoid-v4, E=1024, T=2048, 32 minibatches -> M = 65 536 rows
     # (ppo:489-542; clip 0.2, ent_coef 0, lr 3e-4, ppo:60-67): k_upd2 walks 128 32-row tiles per
     # workgroup pair and k_dw2_dma sums 256 split-K chunks of 256 rows
-    ("cfg2_humanoid", 0, 64, 376, 17, 1024, 64, 0.2, 0.0, 3e-4, None)])
+    ("cfg2_humanoid", 0, 64, 376, 17, 1024, 64, 0.2, 0.0, 3e-4, None),
+    # k_upd2's layer 1 on fp32 MFMAs (the default runs it as split-bf16 piece products, upd_mfma=bx6)
+    ("cfg2_humanoid_f32", 0, 64, 376, 17, 1024, 64, 0.2, 0.0, 3e-4, "upd_mfma=16")])
 def test_headline_minibatch_update_vs_oracle(name, kind, H, O_, A, E, T, clip, ent, lr, opts):
     M = E * T
     rng = np.random.default_rng(31)
@@ -109,7 +111,8 @@ def test_headline_minibatch_update_vs_oracle(name, kind, H, O_, A, E, T, clip, e
 @pytest.mark.parametrize("split", ["2", "3"])
 def test_cfg2_split_update_matches_single_kernel(split):
     """cfg2's update in its split form (k_l1g: layer 1 of both trunks as one gathered GEMM into Z1,
-    then k_upd2's tail at 2 / 3 workgroups per CU) against the single k_upd2 (upd2_split=0) on the
+    then k_upd2's tail at 2 / 3 workgroups per CU) against the single k_upd2 on fp32 MFMAs
+    (upd2_split=0,upd_mfma=16) on the
     same minibatch (M = 16 384, ragged last tile: 16 383 rows): the layer-1 sums are the same products
     in another order (32x32x2 chains over k pairs instead of 16x16x4 chains), so gradients agree to
     fp32 accumulation noise (rel-L2 < 1e-5) and the loss statistics to rtol 1e-5."""
@@ -126,7 +129,7 @@ def test_cfg2_split_update_matches_single_kernel(split):
     ov = rng.standard_normal(M).astype(np.float32)
     perm = rng.permutation(M).astype(np.int32)
     out = []
-    for opt in ("upd2_split=0", f"upd2_split={split}"):
+    for opt in ("upd2_split=0,upd_mfma=16", f"upd2_split={split}"):
         ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.2, ent=0.0, options=opt)
         ag.load_params(p)
         fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
@@ -305,6 +308,48 @@ def test_upd_bx6_is_as_accurate_as_fp32_mfma(O_, A, E):
 
 def test_upd_bx6_refused_where_it_does_not_apply():
     with pytest.raises(ppo_amd.PPOError, match="upd_mfma=bx6"):
-        make_agent(0, 17, 6, 64, 64, options="upd_mfma=bx6")
+        make_agent(0, 17, 6, 64, 64, options="upd_mfma=bx6")  # the 64-wide agent off cfg2's shape
     with pytest.raises(ppo_amd.PPOError, match="upd_mfma=bx6"):
         make_agent(1, 376, 17, 256, 64, options="upd_mfma=bx6")  # 34 heads: three head tiles
+
+
+@pytest.mark.parametrize("E,T", [(2047, 1), (1024, 16)])
+def test_upd2_bx6_is_as_accurate_as_fp32_mfma(E, T):
+    """k_upd2 with layer 1 (K = OP = 384) as split-bf16 piece products (upd_mfma=bx6, the default at
+    cfg2's Humanoid shape: each staged chunk split once into bf16 pieces) against its fp32-MFMA form
+    (upd_mfma=16) and both against the oracle's gradient (fp64 accumulation), M = 2 047 (ragged last
+    tile) and 16 384: per gradient tensor within 1.5x the fp32 form's error + 1e-6, overall within
+    2e-5 rel-L2 of it; loss statistics rtol 2e-5."""
+    kind, H, O_, A = 0, 64, 376, 17
+    M = E * T
+    rng = np.random.default_rng(17)
+    L = O.layout_init(kind, O_, A, H)
+    p = random_params(L, rng)
+    x = rng.standard_normal((M, O_)).astype(np.float32)
+    act = (rng.standard_normal((M, A)) * 0.5).astype(np.float32)
+    olp = (rng.standard_normal(M) * 0.3 - 20.0).astype(np.float32)
+    adv = rng.standard_normal(M).astype(np.float32)
+    ret = rng.standard_normal(M).astype(np.float32)
+    ov = rng.standard_normal(M).astype(np.float32)
+    perm = rng.permutation(M).astype(np.int32)
+    out = {}
+    for opt in ("upd_mfma=16", "upd_mfma=bx6"):
+        ag = make_agent(kind, O_, A, H, E, T=T, MB=1, EP=1, clip=0.2, ent=0.0, options=opt)
+        assert ag.kernel_info().startswith("update=k_upd2/" + ("f32" if opt.endswith("16") else "bx6"))
+        ag.load_params(p)
+        fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
+        st = ag.update(3e-4, perms=DeviceArray.from_numpy(perm), want_stats=True)
+        out[opt] = (ag.last_grad(), st)
+        ag.close()
+    (g0, s0), (g1, s1) = out["upd_mfma=16"], out["upd_mfma=bx6"]
+    cfg = O.LossCfg(0.2, 0.0, 0.5, 1, 1)
+    og, _ = O.minibatch_grad_parallel(L, p, x[perm], act[perm], olp[perm], adv[perm], ret[perm], ov[perm], cfg)
+    print(f"\nbx6 vs f32 {rel(g1, g0):.2e}; vs oracle: f32 {rel(g0, og):.2e} bx6 {rel(g1, og):.2e}")
+    assert rel(g1, g0) < 2e-5, rel(g1, g0)
+    for t in range(L.ntensors):
+        o, n = L.t_off[t], L.t_len[t]
+        if L.t_grad[t]:
+            e0, e1 = rel(g0[o:o + n], og[o:o + n]), rel(g1[o:o + n], og[o:o + n])
+            assert e1 <= 1.5 * e0 + 1e-6, (t, e0, e1)
+    for k in ("pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac", "grad_norm"):
+        np.testing.assert_allclose(s1[k], s0[k], rtol=2e-5, atol=1e-7, err_msg=k)

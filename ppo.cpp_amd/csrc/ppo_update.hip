@@ -165,17 +165,14 @@ PPO_DEV void mm_fr(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* in) {
 //   inb = ACTB + (rbase + j) LDB + 4 g (floats; row = 3 pieces x H bf16 + 16 B, piece p at 128 p floats)
 //   weight unit (kk, ft): 3 x 16 B per lane at wlane + 256 ((ft NKK + kk) 3 + p) floats
 // A pieces stream through a ring of NS units (D = NS - 1 ahead, ~ one 32-k block of every feature tile).
-#ifndef PPO_BX_D
-#define PPO_BX_D 3
-#endif
-#ifndef PPO_HWG_FORCE
-#define PPO_HWG_FORCE 0
-#endif
+// weight-piece ring depth (32-k units in flight ahead): 2 / 3 / 4 / 5 measured 0.62 / 0.61 / 0.65 /
+// 0.69 ms per launch (deeper rings spill; profiles/r05/bx6/abm2, abm3)
+constexpr int kBxRing = 3;
 PPO_DEV u32x4 pld4u(PBuf b, int lane_floats, int uni_floats) { return __builtin_bit_cast(u32x4, pld4(b, lane_floats, uni_floats)); }
 template <int FT, int RT, int NKB, int LDB>
 PPO_DEV void mm_bx(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* inb) {
   static_assert(NKB % 2 == 0, "mm_bx: 32-wide k blocks");
-  constexpr int NKK = NKB / 2, U = NKK * FT, D = PPO_BX_D, NS = D + 1, PS = 8 * NKB;
+  constexpr int NKK = NKB / 2, U = NKK * FT, D = kBxRing, NS = D + 1, PS = 8 * NKB;
   u32x4 ar[NS][3];
   auto load_unit = [&](int u, u32x4 (&dst)[3]) {
     const int kk = u / FT, ft = u - kk * FT;
@@ -687,22 +684,6 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
           if (h < nh) hwacc[h * H + fbase + 16 * ft + j] = 0.f;
         }
   }
-  // the per-tile LayerNorm / head-bias reads come from LDS instead of an L2 round trip each
-  for (int i = tid; i < GE::NSPAR; i += 256) {
-    const int v = i / H, f = i - v * H;
-    float x = 0.f;
-    if (v < 4) {
-      if constexpr (LN) x = P[(v == 0 ? T.g1 : v == 1 ? T.be1 : v == 2 ? T.g2 : T.be2) + f];
-    } else if (i < 4 * H + NHP) {
-      if (i - 4 * H < nh) x = P[head_bias(K, trunk, i - 4 * H)];
-    } else {
-      const int q = i - 4 * H - NHP, o = q % OP;
-      x = q < OP ? 0.f : 1.f;
-      if constexpr (LN)
-        if (o < O) x = P[(q < OP ? K.omean : K.ostd) + o];
-    }
-    SPAR[i] = x;
-  }
 
   // per-lane A-operand offsets into the swizzled W1 | W2 | W2^T (sw_index): this wave's feature blocks
   const int w1lane = ((fbase >> 4) * NTO * 64 + lane) * 4;
@@ -858,10 +839,26 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
       }
     }
   };
-  if constexpr (PREF) {
-    pref_idx(blockIdx.x);
-    pref_data(blockIdx.x);
+  // the first tile's permutation entries are requested before the staging loads below, so their
+  // round trip overlaps the staging instead of following it
+  if constexpr (PREF) pref_idx(blockIdx.x);
+  // the per-tile LayerNorm / head-bias reads come from LDS instead of an L2 round trip each
+  for (int i = tid; i < GE::NSPAR; i += 256) {
+    const int v = i / H, f = i - v * H;
+    float x = 0.f;
+    if (v < 4) {
+      if constexpr (LN) x = P[(v == 0 ? T.g1 : v == 1 ? T.be1 : v == 2 ? T.g2 : T.be2) + f];
+    } else if (i < 4 * H + NHP) {
+      if (i - 4 * H < nh) x = P[head_bias(K, trunk, i - 4 * H)];
+    } else {
+      const int q = i - 4 * H - NHP, o = q % OP;
+      x = q < OP ? 0.f : 1.f;
+      if constexpr (LN)
+        if (o < O) x = P[(q < OP ? K.omean : K.ostd) + o];
+    }
+    SPAR[i] = x;
   }
+  if constexpr (PREF) pref_data(blockIdx.x);
   // wide inputs: row tid's permutation entry of the next tile (clamped, as the gather clamps rows)
   int nperm = 0;
   if constexpr (!PREF) nperm = tid < R ? a.perm[min((int)blockIdx.x * R + tid, a.M - 1)] : 0;
@@ -2007,7 +2004,7 @@ static void upd_geo(const PackedLayout& K, int nh_actor, int sg0_size, int sg1_s
   };
   g->hw_global = 0;
   carve(std::max(sg0_size, sg1_size));
-  if (GE::WR == 1 && (PPO_HWG_FORCE || 2 * g->lds_bytes > 160 * 1024)) {
+  if (GE::WR == 1 && 2 * g->lds_bytes > 160 * 1024) {
     const size_t full = g->lds_bytes;
     carve(std::max(sg0_size, sg1_size - nh_actor * H));
     if (2 * g->lds_bytes <= 160 * 1024) g->hw_global = 1;

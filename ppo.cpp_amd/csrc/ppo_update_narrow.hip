@@ -98,9 +98,9 @@ struct Geo2 {
   static constexpr int oITM = oSP + 4 * NHP + 4;        // [R*A][4] items, then [64 ceil(R*A / 64)] actions
 };
 
-#ifndef PPO_BX2_D
-#define PPO_BX2_D 1
-#endif
+// k_upd2 BX: W1 piece units (32 k x FT feature tiles) in flight ahead; 2 spills 31 VGPRs and runs
+// slower (profiles/r05/bx6_cfg2/split_once)
+constexpr int kBx2Ring = 1;
 PPO_DEV float lf(const float* p) { return *p; }
 PPO_DEV f4 lf4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 PPO_DEV void sf4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
@@ -378,7 +378,7 @@ __global__ __launch_bounds__(256, SPLIT ? SPLIT : 2) void k_upd2(UpdArgs a) {
       constexpr int LDB = 3 * (CW / 2) + 4;  // floats per XP row (row stride 4 mod 64 banks)
       static_assert(R * LDB <= GE::oGG - GE::oACT, "XP must fit in ACT + SCR");
       float* XP = lds + GE::oACT;
-      constexpr int NKK = NTO / 2, KPC = CW / 32, D2 = PPO_BX2_D;  // 32-k units: per tile, per chunk
+      constexpr int NKK = NTO / 2, KPC = CW / 32, D2 = kBx2Ring;  // 32-k units: per tile, per chunk
       const PBuf w1b = make_pbuf(a.WSW[trunk] + sw_size(H, OP), (int)bx_w1_size(H, OP));
       const int w1blane = ((fbase >> 4) * NKK * 3 * 64 + lane) * 4;
       u32x4 wr[D2 + 1][FT][3];

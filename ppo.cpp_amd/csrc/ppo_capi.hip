@@ -155,6 +155,7 @@ struct ppo_ctx {
   bool use_upd = false;  // feature-split k_upd (ppo_update.hip) instead of k_fwdbwd
   bool use_upd32 = false;  // k_upd32 (32x32x2 MFMAs) instead of k_upd (create option upd_mfma)
   int upd_bx = 0;          // 1: k_upd's 256-wide GEMMs as split-bf16 piece products (upd_mfma=bx6)
+  int gae_scan = 0;        // 1: GAE as k_gae_scan (create option gae=scan); 0: the bit-exact serial k_gae
   int upd32_mix = 0;       // k_upd32 with the actor trunk on k_upd's body (upd_mfma=mix)
   bool use_upd2 = false;  // two-trunk k_upd2 (ppo_update_narrow.hip, H = 64 tanh agent)
   int rollout_kernel = 0;   // AC persistent rollout: 0 auto, 1 k_rollout (MFMA), 2 k_rollout_v (VALU)
@@ -281,6 +282,7 @@ struct CreateOptions {
   int dw_slices = 0;   // k_dwf output slices per chunk (1 / 2; 0: auto, dw_slices())
   int dw_dma = 1;      // 1 (default): k_dwf_dma (LDS-DMA staging, three stage buffers); 0: k_dwf
   int dw_bx = -1;      // dw_mfma: -1 auto, 0 f32 (fp32 MFMA), 9 / 8 / 6 bf16x9 / x8 / x6 (k_dwf_bx: exact bf16 splits)
+  int gae_scan = 0;    // gae=serial (default, bit-exact with the reference's loop) | scan (k_gae_scan)
   // 1: ppo_update replays its minibatch launches as one captured hipGraph; 0 (default): eager.
   // Snapshots work with it on (ppo_read_snapshot waits for the snapshot's event on the host).
   int update_graph = 0;
@@ -330,6 +332,7 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
       o->dw_rows = atoi(v.c_str());  // at most 5 digits: no overflow, no exception across the C-ABI
     else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
     else if (k == "dw_dma" && (v == "0" || v == "1")) o->dw_dma = v[0] - '0';
+    else if (k == "gae" && (v == "serial" || v == "scan")) o->gae_scan = v == "scan";
     else if (k == "dw_mfma" && (v == "auto" || v == "f32" || v == "bf16x9" || v == "bf16x8" || v == "bf16x6"))
       o->dw_bx = v == "auto" ? -1 : v == "f32" ? 0 : v == "bf16x9" ? 9 : v == "bf16x8" ? 8 : 6;
     else if (k == "update_graph" && (v == "0" || v == "1")) o->update_graph = v[0] - '0';
@@ -398,6 +401,7 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   c->act_kernel = opt.act_kernel;
   c->dw_fused = opt.dw_fused;
   c->dw_dma = opt.dw_dma;
+  c->gae_scan = opt.gae_scan;
   c->dw_bx = opt.dw_bx >= 0 ? opt.dw_bx : kDwBxAuto;
   c->rollout_mode = opt.rollout;
   c->gradstep = opt.gradstep;
@@ -813,7 +817,7 @@ static int gae_launch(ppo_t* c, const float* next_value, const float* next_done,
   g.gamma = c->cfg.gamma;
   g.lam = c->cfg.gae_lambda;
   ProfScope ps(c, PK_GAE, s);
-  launch_gae(g, s);
+  launch_gae(g, s, c->gae_scan != 0);
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -1713,6 +1713,87 @@ __global__ __launch_bounds__(64) void k_gae(GaeArgs a) {
   }
 }
 
+// k_gae_scan — the same recurrence as a segmented scan over T (create option gae=scan; north_star's
+// wavefront scan): A_t = delta_t + c_t A_{t+1}, c_t = gamma lambda (1 - d_{t+1}), is an affine map of
+// A_{t+1}; a workgroup holds 64 envs (lane = env: every step's loads are 256 contiguous bytes) and
+// 16 waves, wave w the w-th of 16 segments of the steps. Pass 1: each lane composes its segment's maps
+// from the end, A_{t_lo} = b + a A_{t_hi}. The segments' (a, b) meet in LDS, each wave composes those
+// of the later segments into its incoming A_{t_hi} (A_T = 0), and pass 2 runs the reference's serial
+// recurrence over the segment from that value. Within fp32 rounding of the serial form (the incoming
+// values are composed in another order), not bit-exact: the serial k_gae stays the default.
+constexpr int kScanSeg = 16, kScanChunk = 8;
+__global__ __launch_bounds__(1024) void k_gae_scan(GaeArgs a) {
+#pragma clang fp contract(off)
+  __shared__ float sa[kScanSeg][64], sb[kScanSeg][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  const bool ok = e < a.E;
+  const int ec = ok ? e : 0;  // clamped for the loads
+  const long E = a.E;
+  const int S = (a.T + kScanSeg - 1) / kScanSeg;
+  const int t_lo = min(a.T, w * S), t_hi = min(a.T, t_lo + S);
+  const float gam = a.gamma, gl = (a.gamma * a.lam);
+  const float nv_hi = t_hi == a.T ? a.next_value[ec] : a.values[(long)t_hi * E + ec];
+  const float nd_hi = t_hi == a.T ? a.next_done[ec] : a.dones[(long)t_hi * E + ec];
+  // the steps t_hi - 1 - k, k < kScanChunk, of chunk c (clamped loads; masked by the step test)
+  auto load = [&](int t1, float (&r)[kScanChunk], float (&v)[kScanChunk], float (&d)[kScanChunk]) {
+#pragma unroll
+    for (int k = 0; k < kScanChunk; ++k) {
+      const int t = t1 - k >= t_lo ? t1 - k : t_lo;
+      const long idx = (long)t * E + ec;
+      r[k] = a.rewards[idx];
+      v[k] = a.values[idx];
+      d[k] = a.dones[idx];
+    }
+  };
+  float ca = 1.0f, cb = 0.0f;
+  {
+    float nv = nv_hi, nnt = (1.0f - nd_hi);
+    for (int t1 = t_hi - 1; t1 >= t_lo; t1 -= kScanChunk) {
+      float r[kScanChunk], v[kScanChunk], d[kScanChunk];
+      load(t1, r, v, d);
+#pragma unroll
+      for (int k = 0; k < kScanChunk; ++k) {
+        if (t1 - k < t_lo) break;
+        const float gnv = (gam * nv);
+        const float delta = ((r[k] + (gnv * nnt)) - v[k]);
+        const float c = (gl * nnt);
+        cb = (delta + (c * cb));
+        ca = (c * ca);
+        nnt = (1.0f - d[k]);
+        nv = v[k];
+      }
+    }
+  }
+  sa[w][lane] = ca;
+  sb[w][lane] = cb;
+  __syncthreads();
+  float last = 0.0f;
+  for (int u = kScanSeg - 1; u > w; --u) last = (sb[u][lane] + (sa[u][lane] * last));
+  {
+    float nv = nv_hi, nnt = (1.0f - nd_hi);
+    for (int t1 = t_hi - 1; t1 >= t_lo; t1 -= kScanChunk) {
+      float r[kScanChunk], v[kScanChunk], d[kScanChunk];
+      load(t1, r, v, d);
+#pragma unroll
+      for (int k = 0; k < kScanChunk; ++k) {
+        if (t1 - k < t_lo) break;
+        const long idx = (long)(t1 - k) * E + ec;
+        const float gnv = (gam * nv);
+        const float delta = ((r[k] + (gnv * nnt)) - v[k]);
+        const float adv = (delta + ((gl * nnt) * last));
+        if (ok) {
+          a.adv[idx] = adv;
+          a.ret[idx] = (adv + v[k]);
+        }
+        last = adv;
+        nnt = (1.0f - d[k]);
+        nv = v[k];
+      }
+    }
+  }
+}
+
 // =============================================================================================
 // minibatch permutations and advantage statistics
 // =============================================================================================
@@ -2194,8 +2275,9 @@ void launch_swizzle(const float* w1, const float* w2, float* dst, int H, int OP,
   const long n = (long)H * OP + (long)H * H;
   hipLaunchKernelGGL(k_swizzle, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w1, w2, dst, H, OP, bx);
 }
-void launch_gae(const GaeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_gae, dim3((a.E + 63) / 64), dim3(64), 0, s, a);
+void launch_gae(const GaeArgs& a, hipStream_t s, bool scan) {
+  if (scan) hipLaunchKernelGGL(k_gae_scan, dim3((a.E + 63) / 64), dim3(1024), 0, s, a);
+  else hipLaunchKernelGGL(k_gae, dim3((a.E + 63) / 64), dim3(64), 0, s, a);
 }
 void launch_perm(int32_t* out, uint32_t B, const PermKey& pk, hipStream_t s) {
   hipLaunchKernelGGL(k_perm, dim3((B + 255) / 256), dim3(256), 0, s, out, B, pk);

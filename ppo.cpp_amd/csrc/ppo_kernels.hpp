@@ -321,7 +321,8 @@ PPO_DEV void grid_barrier(unsigned* bar, unsigned target) {
 void launch_adam(const AdamArgs& a, hipStream_t s);
 void launch_transpose(const float* src, float* dst, int H, hipStream_t s);
 void launch_swizzle(const float* w1, const float* w2, float* dst, int H, int OP, int bx, hipStream_t s);
-void launch_gae(const GaeArgs& a, hipStream_t s);
+// scan: k_gae_scan (segmented scan over T, create option gae=scan) instead of the serial k_gae
+void launch_gae(const GaeArgs& a, hipStream_t s, bool scan = false);
 void launch_perm(int32_t* out, uint32_t B, const PermKey& pk, hipStream_t s);
 void launch_adv_sum(const AdvArgs& a, hipStream_t s);
 void launch_adv_sq(const AdvArgs& a, int with_std, hipStream_t s);

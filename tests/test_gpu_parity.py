@@ -175,6 +175,34 @@ def test_gae_full_size_bit_exact_vs_oracle():
     np.testing.assert_array_equal(ag.buffer(ppo_amd.BUF_RETURNS, (T, E)).numpy(), orr)
 
 
+@pytest.mark.parametrize("T,E", [(2048, 1024), (128, 4096), (37, 1000), (5, 70)])
+def test_gae_scan_matches_serial(T, E):
+    """gae=scan (k_gae_scan: 16 segments of the steps per 64-env workgroup; each segment's affine
+    maps composed from the end, then the serial recurrence from the composed incoming value) against
+    the bit-exact serial k_gae on the same buffers: cfg2's T = 2 048 / E = 1 024, the metric's
+    T = 128 / E = 4 096, ragged E and T shorter than the 16 segments. The composed incoming values round
+    differently: advantages within rtol 1e-5 / atol 1e-5 (measured max |d| is printed), returns too."""
+    rng = np.random.default_rng(19)
+    r = rng.standard_normal((T, E)).astype(np.float32)
+    v = (rng.standard_normal((T, E)) * 3.0).astype(np.float32)
+    dn = (rng.random((T, E)) < 0.002).astype(np.float32)
+    nv = rng.standard_normal(E).astype(np.float32)
+    nd = (rng.random(E) < 0.5).astype(np.float32)
+    out = []
+    for opt in (None, "gae=scan"):
+        ag = make_agent(0, 17, 6, 64, E, T=T, options=opt)
+        ag.buffer(ppo_amd.BUF_REWARDS, (T, E)).upload(r)
+        ag.buffer(ppo_amd.BUF_VALUES, (T, E)).upload(v)
+        ag.buffer(ppo_amd.BUF_DONES, (T, E)).upload(dn)
+        ag.gae_from_values(DeviceArray.from_numpy(nv), DeviceArray.from_numpy(nd))
+        out.append((ag.buffer(ppo_amd.BUF_ADVANTAGES, (T, E)).numpy(), ag.buffer(ppo_amd.BUF_RETURNS, (T, E)).numpy()))
+        ag.close()
+    (a0, r0), (a1, r1) = out
+    print(f"\nT={T} E={E}: max |adv scan - serial| {np.abs(a1 - a0).max():.2e} (max |adv| {np.abs(a0).max():.1f})")
+    np.testing.assert_allclose(a1, a0, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(r1, r0, rtol=1e-5, atol=1e-5)
+
+
 # ------------------------------------------------------------------------------------------------
 # minibatch update (loss, backward, clip_grad_norm_, Adam) vs golden
 # ------------------------------------------------------------------------------------------------

@@ -120,7 +120,7 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            auto: k_rollout_v at E <= 512. Bitwise the same results. valu on an
  *                            agent it cannot serve (the PPO agent, O > 32, device env wrappers) fails
  *   gae=serial|scan          GAE as the reference's serial recurrence per env (k_gae, default: bit-exact
- *                            with ac:756-780) or as a segmented scan over the steps (k_gae_scan: 16
+ *                            with ppo:447-467, ac:759-779) or as a segmented scan over the steps (k_gae_scan: 16
  *                            segments per 64 envs, within fp32 rounding of the serial form)
  *   gradstep=split|fused     clip_grad_norm_ + Adam: two launches (k_gradnorm, k_adam; default) or
  *                            one cooperative launch (k_gradstep: slower on ROCm 7, whose cooperative

@@ -17,7 +17,12 @@
 //    column sums (bias / LN-affine gradients) are a 15-shuffle reduce-scatter per vector per
 //    iteration instead of per 16 rows;
 //  * R = 32 rows keep LDS under 80 KB, so two workgroups (8 waves) share a CU and one's VALU /
-//    barrier phases overlap the other's MFMA phases.
+//    barrier phases overlap the other's MFMA phases;
+//  * BX (create option upd_mfma=bx6, the default for the LayerNorm-Beta agent at H = 256): layer 2
+//    and dh1 = W2^T dz2 run as six split-bf16 piece products per fp32 product on
+//    v_mfma_f32_16x16x32_bf16 (mm_bx: weight pieces from k_adam's bx_index copies, activation
+//    pieces split once when the tile is written to LDS) — 0.375 of the fp32 MFMA cycles, the same
+//    accumulator layout, as exact against the fp64 oracle as the fp32 form.
 // Everything is reduced in a fixed order: results are bitwise reproducible run to run.
 #include "ppo_agent.hpp"
 #include <cstdlib>

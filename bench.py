@@ -339,6 +339,9 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
+            "dtype_note": ("fp32 arithmetic; the update's fp32 GEMMs run as exact split-bf16 piece products on bf16 "
+                           "MFMAs with fp32 accumulation (DESIGN.md 3c; upd_mfma=16,dw_mfma=f32 for fp32 MFMAs), "
+                           "tested as exact as the fp32 MFMA form against the fp64 oracle"),
             "data": "synthetic: device-resident HalfCheetah-shaped env (O=17, A=6), random-init AC agent",
             "config": {"workload": f"ac_ppo_continuous_action HalfCheetah-v5 num_envs={E_total} num_steps={T} "
                                    f"num_minibatches={cfg.num_minibatches} update_epochs={cfg.update_epochs}",

@@ -46,6 +46,7 @@ struct ConvArgs {
   int kc;       // k-range per blockIdx.z (0: no split)
   float* wprep = nullptr;  // conv1 packed form (k_conv_img3): its A operands, [kImg3Blocks][4][16][4]
   int bx = 0;              // conv1 packed form: 1 runs its products as split-bf16 MFMAs (k_conv_img3<.., BX>)
+  int tiled = 0;           // 1: conv2's shape runs k_conv_t (LDS-staged input patches)
 };
 
 constexpr int kConvWaves = 4;
@@ -196,6 +197,101 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
           float y = acc[t][u][r] + a.b[oc];
           if (a.relu) y = y > 0.0f ? y : 0.0f;
           o[(long)oc * P] = y;
+        }
+      }
+  }
+}
+
+// ---- conv2's forward from LDS-staged input patches (create option conv_fwd=tiled, the default) ----
+// k_conv gathers each B operand from global memory (one load per MFMA for conv2's 16 output
+// channels). Here a persistent workgroup walks TY x TX output tiles of one sample and stages the
+// tile's input patch (IC x PH x PW, zero outside the plane) in LDS, the next tile's loaded into
+// registers while the current one computes. GEMM: rows = oc (A = the weights, in registers for all
+// tiles), columns = the tile's pixels (16 per MFMA column tile: one output row segment), k = (tap, ic)
+// with k = 4 kk + g -> ic = 4 (kk % (IC / 4)) + g, tap = kk / (IC / 4): a lane's B operand is its
+// pixel's patch offset + its ic plane + an IMMEDIATE per kk (ds_read_b32 + MFMA only). Same products as
+// k_conv (fp32 MFMA), another k order (tolerance tests).
+constexpr int kCtTY = 8, kCtTX = 16;  // conv2: 45 x 45 -> 6 x 3 tiles
+template <int IC, int OC, int TY, int TX>
+__global__ __launch_bounds__(256, 2) void k_conv_t(ConvArgs a, int tiles_x, int tps, int tiles) {
+  constexpr int K = 5, S = 2, PH = (TY - 1) * S + K, PW = (TX - 1) * S + K, PP = PH * PW, NX = IC * PP;
+  constexpr int NRT = OC / 16, ICQ = IC / 4, KS = K * K * ICQ, RPW = TY / 4, NSX = (NX + 255) / 256;
+  static_assert(OC % 16 == 0 && IC % 4 == 0 && TY % 4 == 0 && TX == 16, "tile shape");
+  __shared__ float xp[NX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  float wa[NRT][KS];  // A operands: W[16 rt + j][ic][tap], k = 4 kk + g
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int tap = kk / ICQ, ic = 4 * (kk - tap * ICQ) + g, oc = 16 * rt + j;
+      wa[rt][kk] = a.W[(oc < a.OC ? oc * IC + ic : 0) * (K * K) + tap] * (oc < a.OC ? 1.0f : 0.0f);
+    }
+  float bias[NRT][4];
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[rt][r] = a.b[16 * rt + 4 * g + r];
+  const int bb = g * PP + S * RPW * wave * PW + S * j;  // + 4 (kk % ICQ) PP + ky PW + kx + S u PW
+  const long plane = (long)a.IH * a.IW;
+  const int P = a.OH * a.OW;
+  float sx[NSX];
+  auto sload = [&](int tile) {
+    const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    const PBuf xb{__builtin_amdgcn_make_buffer_rsrc((void*)(a.in_f + (size_t)smp * a.in_stride), (short)0,
+                                                    (int)(a.in_stride * 4), 0x00020000)};
+    const int iy0 = S * TY * ty, ix0 = S * TX * tx;
+#pragma unroll
+    for (int i = 0; i < NSX; ++i) {
+      const int e = tid + 256 * i, ic = e / PP, rem = e - ic * PP, r = rem / PW, c = rem - r * PW;
+      const int iy = iy0 + r, ix = ix0 + c;
+      const bool in = e < NX && iy < a.IH && ix < a.IW;
+      const uint32_t off = in ? (uint32_t)(ic * plane + iy * a.IW + ix) * 4u : 0x7ffffff0u;
+      sx[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xb.r, off, 0, 0));
+    }
+  };
+  if ((int)blockIdx.x < tiles) sload(blockIdx.x);
+  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+#pragma unroll
+    for (int i = 0; i < NSX; ++i)
+      if (tid + 256 * i < NX) xp[tid + 256 * i] = sx[i];
+    __syncthreads();
+    const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    if (tile + (int)gridDim.x < tiles) sload(tile + gridDim.x);
+    f4 acc[NRT][RPW];
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int u = 0; u < RPW; ++u) acc[rt][u] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int tap = kk / ICQ, icq = kk - tap * ICQ, ky = tap / K, kx = tap - ky * K;
+      float bv[RPW];
+#pragma unroll
+      for (int u = 0; u < RPW; ++u) bv[u] = xp[bb + 4 * icq * PP + ky * PW + kx + S * u * PW];
+#pragma unroll
+      for (int u = 0; u < RPW; ++u)
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) acc[rt][u] = mfma16(wa[rt][kk], bv[u], acc[rt][u]);
+    }
+    __syncthreads();  // every wave is done with the patch before the next one is stored
+    // lane (j, g) holds out channel 16 rt + 4 g + r of output pixel (TY ty + RPW wave + u, TX tx + j)
+    const PBuf ob{__builtin_amdgcn_make_buffer_rsrc((void*)(a.out + (size_t)smp * a.out_stride), (short)0,
+                                                    (int)(a.out_stride * 4), 0x00020000)};
+    const int ox = TX * tx + j;
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int u = 0; u < RPW; ++u) {
+        const int oy = TY * ty + RPW * wave + u;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int oc = 16 * rt + 4 * g + r;
+          const bool in = oy < a.OH && ox < a.OW && oc < a.OC;
+          float y = acc[rt][u][r] + bias[rt][r];
+          if (a.relu) y = y > 0.0f ? y : 0.0f;
+          const uint32_t off = in ? (uint32_t)(oc * P + oy * a.OW + ox) * 4u : 0x7ffffff0u;
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ob.r, off, 0, 0);
         }
       }
   }
@@ -453,6 +549,12 @@ constexpr int kConv1Auto = 2;  // the default conv1 form (ppo_carla_create_ex op
 // forward 0.69 -> 0.58 ms (profiles/r05/carla_bx/); gradient vs the fp32 torch reference 6.7e-7 rel-L2
 // (test_conv1_split_bf16_update_vs_torch)
 constexpr int kConv1BxAuto = 1;
+// conv_dgrad=auto: the quad form (k_dgrad_q, one GEMM over the four parity classes)
+constexpr int kDgradQuadAuto = 1;
+// conv_wgrad=auto: the LDS-tiled form (k_wgrad_t)
+constexpr int kWgradTiledAuto = 1;
+// conv_fwd=auto: the LDS-tiled form (k_conv_t)
+constexpr int kConvTiledAuto = 1;
 template <int K, int S>
 struct Img3Geo {
   static constexpr int TI = (kImgTile - 1) * S + K;          // patch rows
@@ -1059,6 +1161,16 @@ int launch_conv(const ConvArgs& a, hipStream_t s, int img = 1, bool fin = true, 
     hipLaunchKernelGGL((k_conv_img<5, 2>), dim3(tiles, a.n), dim3(256), img_lds_bytes(a.IC, a.K, a.S, a.OC), s, a);
     return 0;
   }
+  if (img && a.tiled && a.in_f && a.K == 5 && a.S == 2 && a.IC == 8 && a.OC == 16 && a.in_stride < (1L << 29) &&
+      a.out_stride < (1L << 29)) {
+    const int tiles_x = (a.OW + kCtTX - 1) / kCtTX, tps = tiles_x * ((a.OH + kCtTY - 1) / kCtTY);
+    const long tiles = (long)a.n * tps;
+    if (tiles < (1L << 31)) {
+      const int grid = (int)std::min<long>(tiles, 256L * 2);
+      hipLaunchKernelGGL((k_conv_t<8, 16, kCtTY, kCtTX>), dim3(grid), dim3(256), 0, s, a, tiles_x, tps, (int)tiles);
+      return 0;
+    }
+  }
   const long Q = (long)a.n * a.OH * a.OW;
   // several pixel tiles per wave where there are pixels to spare (B-operand reuse of every weight
   // load), one where the layer is narrow (Linear layers, the last convolutions)
@@ -1124,6 +1236,13 @@ struct ppo_carla {
   // conv1 (raw-byte input) as split-bf16 products on bf16 MFMAs (create option conv1_mfma=bx3|f32):
   // k_wgrad_img2<.., BX> and k_conv_img3<.., BX>
   int c1bx = kConv1BxAuto;
+  // conv2's input gradient: 1 k_dgrad_q (quad classes as GEMM columns), 0 k_dgrad_s2 (create option
+  // conv_dgrad=quad|staged; both need conv1=staged|packed)
+  int dgrad_q = kDgradQuadAuto;
+  // conv2's weight gradient: 1 k_wgrad_t (LDS-staged tiles), 0 k_wgrad (create option conv_wgrad=tiled|generic)
+  int wgrad_t = kWgradTiledAuto;
+  // conv2's forward: 1 k_conv_t (LDS-staged input patches), 0 k_conv (create option conv_fwd=tiled|generic)
+  int conv_t = kConvTiledAuto;
   float* c1w = nullptr;  // k_conv_img3's A-operand table
   // MLP tail for n <= kTailMaxN: 1 (default) one launch per stage, 0 one cooperative launch (a grid
   // barrier between stages: slower here, a cooperative launch costs more than the launches it
@@ -1170,6 +1289,9 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
   int conv_img = kConv1Auto;
   int tail_mode = 1;
   int c1bx = kConv1BxAuto;
+  int dgrad_q = kDgradQuadAuto;
+  int wgrad_t = kWgradTiledAuto;
+  int conv_t = kConvTiledAuto;
   if (options && *options) {  // comma-separated key=value
     std::string rest(options);
     while (!rest.empty()) {
@@ -1185,6 +1307,15 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
       else if (o == "conv1_mfma=bx3") c1bx = 1;
       else if (o == "conv1_mfma=f32") c1bx = 0;
       else if (o == "conv1_mfma=auto") c1bx = kConv1BxAuto;
+      else if (o == "conv_dgrad=quad") dgrad_q = 1;
+      else if (o == "conv_dgrad=staged") dgrad_q = 0;
+      else if (o == "conv_dgrad=auto") dgrad_q = kDgradQuadAuto;
+      else if (o == "conv_wgrad=tiled") wgrad_t = 1;
+      else if (o == "conv_wgrad=generic") wgrad_t = 0;
+      else if (o == "conv_wgrad=auto") wgrad_t = kWgradTiledAuto;
+      else if (o == "conv_fwd=tiled") conv_t = 1;
+      else if (o == "conv_fwd=generic") conv_t = 0;
+      else if (o == "conv_fwd=auto") conv_t = kConvTiledAuto;
       else return ppo_fail("ppo_carla_create_ex: unknown option " + o, -1);
     }
   }
@@ -1205,6 +1336,9 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
   c->conv_img = conv_img;
   c->tail_mode = tail_mode;
   c->c1bx = c1bx;
+  c->dgrad_q = dgrad_q;
+  c->wgrad_t = wgrad_t;
+  c->conv_t = conv_t;
 #ifdef PPO_DIAG
   if (const char* e = getenv("PPO_CARLA_CONV1")) c->conv_img = e[0] - '0';
 #endif
@@ -1280,6 +1414,7 @@ extern "C" int ppo_carla_forward(ppo_carla_t* c, int n, const uint8_t* bev, cons
                c->ksplit, 0};
     a.wprep = c->c1w;
     a.bx = c->c1bx;
+    a.tiled = c->conv_t;
     return launch_conv(a, s, c->conv_img);
   };
   auto linear = [&](const float* in, long in_stride, int IN, long w, long b, float* out, long out_stride, int OUT,
@@ -1634,6 +1769,249 @@ __global__ __launch_bounds__(256) void k_dgrad_s2(DgradArgs a, int tiles_x, int 
   }
 }
 
+// ---- conv2's input gradient as ONE GEMM over the four parity classes (create option
+// conv_dgrad=quad, the default) --------------------------------------------------------------------
+// For S = 2, K = 5 the input pixel (2 qy + py, 2 qx + px) of "quad" (qy, qx) reads dZ at
+// (qy - jj, qx - ii), jj, ii < 3, through the tap (py + 2 jj, px + 2 ii), which does not exist when a
+// coordinate is 5: all four parity classes of a quad read the SAME 3 x 3 dZ neighbourhood. So the
+// classes become columns: rows = quads (16 per MFMA tile), k = (tap, oc) (9 x OC; a class's missing
+// taps are zero weights), columns = (class, ic) — 4 x IC = 32 for IC = 8, two full 16-wide tiles,
+// where k_dgrad_s2 leaves half of every MFMA's rows on IC = 8's padding to 16. 72 MFMAs per 16 quads
+// (k_dgrad_s2: 100 with half the rows idle). A lane's A operand (dZ) is its quad's neighbourhood in
+// the LDS-staged dZ region at one base address plus an IMMEDIATE offset per k-step (k = 4 kk + g:
+// oc = 4 (kk % (OC / 4)) + g, tap kk / (OC / 4)), so the k loop is ds_read_b32 + MFMA only; the B
+// operands (weights, 72 per lane) stay in registers for all tiles of the persistent workgroup. The
+// next tile's dZ region is loaded into registers while the current one computes. Epilogue: the
+// two px-classes of a quad sit in lanes j and j ^ 8, one exchange gives each lane four consecutive
+// input pixels (two 8-byte stores, the ReLU mask read the same way). The sum runs in another order
+// than k_dgrad's (tolerance tests, not bitwise).
+constexpr int kDqT = 16;          // quads per tile edge (32 x 32 input pixels)
+constexpr int kDqR = kDqT + 2;    // dZ region edge (jj, ii < 3)
+template <int IC, int OC>
+__global__ __launch_bounds__(256, 2) void k_dgrad_q(DgradArgs a, int tiles_x, int tps, int tiles) {
+  constexpr int K = 5, R = kDqR, RR = R * R, NCT = 4 * IC / 16, OCQ = OC / 4, KS = 9 * OCQ;
+  // each oc plane padded to RRP = 16 (mod 32) dwords: lane groups g = 0, 1 (one ds_read_b32 half) read
+  // 16 banks apart, conflict-free
+  constexpr int RRP = ((RR - 16 + 31) / 32) * 32 + 16;
+  constexpr int NST = (OC * RRP + 255) / 256;  // staging runs over the padded layout (linear LDS stores)
+  static_assert(IC == 8 && OC % 4 == 0 && RRP >= RR, "the paired-lane epilogue is written for IC = 8");
+  __shared__ float dzl[OC * RRP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int OP = a.OH * a.OW;
+  // B operands: bw[ct][kk] = W[oc][ic][py + 2 jj][px + 2 ii] for column 16 ct + j = (class, ic), k = 4 kk + g
+  float bw[NCT][KS];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+    const int py = ct, px = j >> 3, ic = j & 7;  // IC = 8: column 16 ct + j = class (ct, j >> 3), channel j & 7
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int tap = kk / OCQ, oc = 4 * (kk - tap * OCQ) + g, ky = py + 2 * (tap / 3), kx = px + 2 * (tap % 3);
+      const bool ok = ky < K && kx < K;
+      bw[ct][kk] = ky < K ? a.W[((oc * IC + ic) * K + ky) * K + (ok ? kx : 0)] * (ok ? 1.0f : 0.0f) : 0.0f;
+    }
+  }
+  // the lane's A base: dzl[g][4 wave][j]; step kk of row u adds 4 ocq RRP + (u + 2 - jj) R + (2 - ii)
+  const int abase = g * RRP + 4 * wave * R + j;
+  float st[NST];
+  auto sload = [&](int tile) {
+    const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    const int oy0 = ty * kDqT - 2, ox0 = tx * kDqT - 2;
+    // a buffer descriptor over the sample's dZ: elements outside the output plane read as 0 through an
+    // offset past the buffer (no select after the load, so the loads stay in flight over the tile)
+    const PBuf zb{__builtin_amdgcn_make_buffer_rsrc((void*)(a.dz + (size_t)smp * a.dz_stride), (short)0,
+                                                    (int)(a.dz_stride * 4), 0x00020000)};
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int e = tid + 256 * i, oc = e / RRP, rem = e - oc * RRP, r = rem / R, q = rem - r * R;
+      const int oy = oy0 + r, ox = ox0 + q;
+      const bool in = e < OC * RRP && rem < RR && (unsigned)oy < (unsigned)a.OH && (unsigned)ox < (unsigned)a.OW;
+      const uint32_t off = in ? (uint32_t)(oc * OP + oy * a.OW + ox) * 4u : 0x7ffffff0u;
+      st[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zb.r, off, 0, 0));
+    }
+  };
+  if ((int)blockIdx.x < tiles) sload(blockIdx.x);
+  const long plane = (long)a.IH * a.IW;
+  const int px = j >> 3, icl = j & 7;
+  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int e = tid + 256 * i;
+      if (e < OC * RRP) dzl[e] = st[i];
+    }
+    __syncthreads();
+    const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    if (tile + (int)gridDim.x < tiles) sload(tile + gridDim.x);
+    f4 acc[4][NCT];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) acc[u][ct] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int tap = kk / OCQ, ocq = kk - tap * OCQ, jj = tap / 3, ii = tap % 3;
+      float av[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) av[u] = dzl[abase + 4 * ocq * RRP + (u + 2 - jj) * R + (2 - ii)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+          if (ct + 2 * jj < K) acc[u][ct] = mfma16(av[u], bw[ct][kk], acc[u][ct]);  // py = 1 has no jj = 2 taps
+    }
+    __syncthreads();  // every wave is done with dzl before the next tile's region is stored
+    // lane (j, g) holds, for quad row 4 wave + u and class (py = ct, px = j >> 3), channel j & 7 of the
+    // quads 4 g + r; after the exchange with lane j ^ 8 it holds input pixels 8 g + 4 px + 0..3
+    // the mask reads and the stores go through buffer descriptors: pixels past the plane read 0 and
+    // their stores are dropped (an offset past the buffer), so there is no branch between the loads
+    const PBuf xq{__builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (size_t)smp * a.x_stride), (short)0,
+                                                    (int)(a.x_stride * 4), 0x00020000)};
+    const PBuf dq{__builtin_amdgcn_make_buffer_rsrc((void*)(a.dx + (size_t)smp * a.dx_stride), (short)0,
+                                                    (int)(a.dx_stride * 4), 0x00020000)};
+    const int ix = 2 * tx * kDqT + 8 * g + 4 * px;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        const f4 v = acc[u][ct];
+        const float s0 = px ? v[0] : v[2], s1 = px ? v[1] : v[3];
+        const float r0 = __shfl_xor(s0, 8), r1 = __shfl_xor(s1, 8);
+        const int iy = 2 * (ty * kDqT + 4 * wave + u) + ct;
+        float o[4];
+        o[0] = px ? r0 : v[0];
+        o[1] = px ? v[2] : r0;
+        o[2] = px ? r1 : v[1];
+        o[3] = px ? v[3] : r1;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const bool in = iy < a.IH && ix + 2 * h < a.IW;
+          const uint32_t off = in ? (uint32_t)(icl * plane + (long)iy * a.IW + ix + 2 * h) * 4u : 0x7ffffff0u;
+          // (32-bit accesses; the compiler pairs the mask loads into one dwordx2)
+          const float x0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xq.r, off, 0, 0));
+          const float x1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xq.r, off + 4, 0, 0));
+          float g0 = x0 > 0.0f ? o[2 * h] : 0.0f;
+          float g1 = x1 > 0.0f ? o[2 * h + 1] : 0.0f;
+          if (a.accumulate) {
+            g0 += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dq.r, off, 0, 0));
+            g1 += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dq.r, off + 4, 0, 0));
+          }
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, g0), dq.r, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, g1), dq.r, off + 4, 0, 0);
+        }
+      }
+  }
+}
+
+// ---- conv3's input gradient (IC 16, OC 32): the quad form with the classes as separate GEMMs --------
+// As k_dgrad_q, the four parity classes of a quad read the same 3 x 3 dZ neighbourhood, so one B
+// operand (dZ at tap (jj, ii), oc = 4 ocq + g, from the LDS-staged region at a per-lane base plus an
+// IMMEDIATE offset) feeds the MFMA of every class that has that tap. Here rows = the 16 input channels
+// (full MFMA rows), columns = 16 quads (2 quad rows x 8 quad columns), and the A operands are the
+// classes' weights from a table built once per persistent workgroup in LDS ([class k / 4][lane][4]:
+// one ds_read_b128 per class and 4 k-steps); the classes' missing taps (py = 1: jj = 2, px = 1: ii = 2)
+// are skipped: 200 MFMAs per wave and tile of 8 x 8 quads (conv3: 23 x 23 quads -> 3 x 3 tiles, 92 %
+// used). Lane (j, g) ends with input channel 4 g + r of quad j for every class, so the px = 0 / 1
+// classes of a row give two adjacent pixels. dZ region rows are 16 floats and oc planes 168 (= 8 mod 32):
+// lane groups 0 and 1 read 32 distinct banks. Another sum order than k_dgrad (tolerance tests).
+constexpr int kDq2T = 8;  // quads per tile edge
+template <int IC, int OC>
+__global__ __launch_bounds__(256, 2) void k_dgrad_q2(DgradArgs a, int tiles_x, int tps, int tiles) {
+  constexpr int K = 5, R = 16, RU = kDq2T + 2, RRP = 168, OCQ = OC / 4, NTAB = (9 + 6 + 6 + 4) * OCQ * 64;
+  constexpr int NST = (OC * RRP + 255) / 256;
+  static_assert(IC == 16 && OC % 8 == 0 && RRP >= RU * R && RRP % 32 == 8, "shape");
+  extern __shared__ __attribute__((aligned(16))) float dq2[];
+  float* tab = dq2;          // [(class base + tap index * OCQ + ocq) / 4][lane][4]
+  float* dzl = dq2 + NTAB;   // [OC][RRP]: rows of R
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  // class c = (py, px) = (c >> 1, c & 1): (3 - py) (3 - px) taps; k base (in k-steps) 0, 9, 15, 21 x OCQ
+  auto cbase = [](int c) { return (c == 0 ? 0 : c == 1 ? 9 : c == 2 ? 15 : 21) * OCQ; };
+  for (int f = tid; f < NTAB; f += 256) {
+    const int e = f & 3, ln = (f >> 2) & 63, kc = 4 * (f >> 8) + e;
+    const int c = kc < 9 * OCQ ? 0 : kc < 15 * OCQ ? 1 : kc < 21 * OCQ ? 2 : 3, py = c >> 1, px = c & 1;
+    const int loc = kc - cbase(c), ti = loc / OCQ, ocq = loc - ti * OCQ, jj = ti / (3 - px), ii = ti - jj * (3 - px);
+    const int oc = 4 * ocq + (ln >> 4), ic = ln & 15;
+    tab[f] = a.W[((oc * IC + ic) * K + py + 2 * jj) * K + px + 2 * ii];
+  }
+  const int bbase = g * RRP + (2 * wave + (j >> 3)) * R + (j & 7);  // + 4 ocq RRP + (2 - jj) R + (2 - ii)
+  const int OP = a.OH * a.OW;
+  float st[NST];
+  auto sload = [&](int tile) {
+    const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    const int oy0 = ty * kDq2T - 2, ox0 = tx * kDq2T - 2;
+    const PBuf zb{__builtin_amdgcn_make_buffer_rsrc((void*)(a.dz + (size_t)smp * a.dz_stride), (short)0,
+                                                    (int)(a.dz_stride * 4), 0x00020000)};
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int e = tid + 256 * i, oc = e / RRP, rem = e - oc * RRP, r = rem / R, q = rem - r * R;
+      const int oy = oy0 + r, ox = ox0 + q;
+      const bool in = e < OC * RRP && r < RU && q < RU && (unsigned)oy < (unsigned)a.OH && (unsigned)ox < (unsigned)a.OW;
+      const uint32_t off = in ? (uint32_t)(oc * OP + oy * a.OW + ox) * 4u : 0x7ffffff0u;
+      st[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zb.r, off, 0, 0));
+    }
+  };
+  if ((int)blockIdx.x < tiles) sload(blockIdx.x);
+  const long plane = (long)a.IH * a.IW;
+  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i)
+      if (tid + 256 * i < OC * RRP) dzl[tid + 256 * i] = st[i];
+    __syncthreads();
+    const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    if (tile + (int)gridDim.x < tiles) sload(tile + gridDim.x);
+    f4 acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int jj = t / 3, ii = t % 3;
+#pragma unroll
+      for (int h = 0; h < OCQ / 4; ++h) {
+        f4 wa[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int py = c >> 1, px = c & 1;
+          if (jj < 3 - py && ii < 3 - px) {
+            const int kk4 = (cbase(c) + (jj * (3 - px) + ii) * OCQ) / 4 + h;
+            wa[c] = *reinterpret_cast<const f4*>(&tab[(kk4 * 64 + lane) * 4]);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ocq = 4 * h + q;
+          const float bv = dzl[bbase + 4 * ocq * RRP + (2 - jj) * R + (2 - ii)];
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (jj < 3 - (c >> 1) && ii < 3 - (c & 1)) acc[c] = mfma16(wa[c][q], bv, acc[c]);
+        }
+      }
+    }
+    __syncthreads();  // every wave is done with dzl before the next tile's region is stored
+    // lane (j, g): channel 4 g + r of quad (2 wave + (j >> 3), j & 7) for class c; px = 0 / 1 adjacent
+    const PBuf xq{__builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (size_t)smp * a.x_stride), (short)0,
+                                                    (int)(a.x_stride * 4), 0x00020000)};
+    const PBuf dq{__builtin_amdgcn_make_buffer_rsrc((void*)(a.dx + (size_t)smp * a.dx_stride), (short)0,
+                                                    (int)(a.dx_stride * 4), 0x00020000)};
+    const int qy = ty * kDq2T + 2 * wave + (j >> 3), ix = 2 * (tx * kDq2T + (j & 7));
+#pragma unroll
+    for (int py = 0; py < 2; ++py) {
+      const int iy = 2 * qy + py;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ic = 4 * g + r;
+#pragma unroll
+        for (int px = 0; px < 2; ++px) {
+          const bool in = iy < a.IH && ix + px < a.IW;
+          const uint32_t off = in ? (uint32_t)(ic * plane + (long)iy * a.IW + ix + px) * 4u : 0x7ffffff0u;
+          const float xm = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xq.r, off, 0, 0));
+          float gv = xm > 0.0f ? acc[2 * py + px][r] : 0.0f;
+          if (a.accumulate) gv += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dq.r, off, 0, 0));
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, gv), dq.r, off, 0, 0);
+        }
+      }
+    }
+  }
+}
+static size_t dq2_lds_bytes(int OC) { return ((size_t)(9 + 6 + 6 + 4) * (OC / 4) * 64 + (size_t)OC * 168) * 4; }
+
 struct WgradArgs {
   const float* dz;  // [n][OC][OP], sample stride dz_stride
   long dz_stride;
@@ -1914,6 +2292,244 @@ __global__ __launch_bounds__(256) void k_wgrad_img(WgradArgs a, int tiles_x, int
   }
 }
 
+// ---- conv2's weight gradient from LDS-staged tiles (create option conv_wgrad=tiled, the default) ----
+// k_wgrad gathers every B operand (an input value) from global memory, one buffer load per MFMA,
+// which its counters show it waits on. Here a persistent workgroup walks output tiles of TY x TX
+// pixels of one sample: the tile's dZ (OC x TY TX) and its input patch (IC x PH x PW, zero outside the
+// plane) are staged in LDS, the next tile's loaded into registers while the current one computes.
+// GEMM: rows = oc (A = dZ), columns = (ic, ky, kx) plus the bias column, k = the tile's pixels; wave w
+// takes output rows RPW w .. + RPW - 1. For k-step kk a lane's B operand sits at its column's patch
+// offset + the lane's pixel offset + an IMMEDIATE per kk, its A operand at one base + 4 kk: the k loop
+// is ds_read_b32 + MFMA only. The bias column reads a block of ones. The workgroup keeps its sums in
+// registers over all its tiles, adds its four waves in a fixed order through LDS and writes one
+// partial per workgroup (k_wsum's layout); the sum order differs from k_wgrad's (tolerance tests).
+constexpr int kWtTY = 8, kWtTX = 16;  // output tile (conv2: 45 x 45 -> 6 x 3 tiles, 88 % used)
+// LDS layout (bank = dword address mod 32 for ds_read_b32, per 32-lane half = lane groups g = 0, 1):
+// the patch rows are PW = 37 floats and each input channel's plane PPA = 713 floats, so column
+// c = (ic, ky, kx) sits at a dword offset = c (mod 16) and a wave's 16 columns hit 16 distinct banks;
+// lane group g takes the output columns kk % 4 + 8 (g & 1) + 4 (g >> 1), 16 input floats (16 banks) away
+// for g = 1: the B reads are conflict-free. dZ rows are TQ + 1 floats (A reads: 2-way on half the banks).
+template <int IC, int OC, int TY, int TX>
+struct WtGeo {
+  static constexpr int K = 5, S = 2, Kt = IC * K * K, NCT = (Kt + 1 + 15) / 16, NRT = OC / 16;
+  static constexpr int PH = (TY - 1) * S + K, PWL = (TX - 1) * S + K, PW = 37, PPL = PH * PWL, TQ = TY * TX;
+  static constexpr int PPA = ((PH * PW - 9 + 15) / 16) * 16 + 9;  // >= PH PW, = 9 (mod 16): ic planes step c by 25
+  static constexpr int NXL = IC * PPL, NXP = IC * PPA, DZS = TQ + 1, NZ = OC * TQ, NZP = OC * DZS;
+  static constexpr int RPW = TY / 4, KS = RPW * TX / 4;
+  // the largest B offset a lane adds to its column base: wave rows, lane group and k-step parts
+  static constexpr int BMAX = S * RPW * 3 * PW + 16 + 8 + S * (RPW - 1) * PW + S * 3;
+  static constexpr int OB0 = NXP + NZP, ONES0 = OB0 + (((Kt - OB0) % 16) + 16) % 16;  // ones base = Kt (mod 16)
+  static constexpr int LDS = ONES0 + BMAX + 1;
+  static constexpr int RED = OC * NCT * 16;  // the wave reduction, aliased on the patch
+  static_assert(PW >= PWL && PW % 16 == 5 && RED <= NXP, "layout");
+};
+template <int IC, int OC, int TY, int TX>
+__global__ __launch_bounds__(256, 2) void k_wgrad_t(WgradArgs a, int tiles_x, int tps, int tiles) {
+  using G = WtGeo<IC, OC, TY, TX>;
+  constexpr int Kt = G::Kt, NCT = G::NCT, NRT = G::NRT, PW = G::PW, PWL = G::PWL, PPA = G::PPA, TQ = G::TQ,
+                DZS = G::DZS, RPW = G::RPW, KS = G::KS, S = G::S;
+  // staging runs over the padded layouts, so the LDS stores are linear in the thread index
+  constexpr int NXP = G::NXP, NZP = G::NZP, NSX = (NXP + 255) / 256, NSZ = (NZP + 255) / 256;
+  static_assert(OC % 16 == 0 && TY % 4 == 0 && TX == 16, "tile shape");
+  __shared__ __attribute__((aligned(16))) float sm[G::LDS];
+  float* xp = sm;                // [IC][PPA]: rows of PW
+  float* dzt = sm + G::NXP;      // [OC][DZS]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  for (int i = G::OB0 + tid; i < G::LDS; i += 256) sm[i] = 1.0f;  // the bias column's B operands
+  // column bases: (ic, ky, kx) -> ic PPA + ky PW + kx; the bias column -> the ones; padding -> any
+  // in-patch offset = c (mod 16)
+  int cb[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+    const int c = 16 * ct + j, ic = c / 25, r = c - 25 * ic, ky = r / 5, kx = r - 5 * ky;
+    cb[ct] = c < Kt ? ic * PPA + ky * PW + kx : (c == Kt ? G::ONES0 : (c & 15));
+  }
+  const int bb = S * RPW * wave * PW + 16 * (g & 1) + 8 * (g >> 1);  // + S (kk / 4) PW + S (kk % 4)
+  const int ab = j * DZS + RPW * TX * wave + 8 * (g & 1) + 4 * (g >> 1);  // + 16 rt DZS + TX (kk / 4) + kk % 4
+  const long plane = (long)a.IH * a.IW;
+  const int OH = a.OP / a.OW;
+  float sx[NSX], sz[NSZ];
+  auto sload = [&](int tile) {
+    const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    const PBuf xb{__builtin_amdgcn_make_buffer_rsrc((void*)(a.x_f + (size_t)smp * a.x_stride), (short)0,
+                                                    (int)(a.x_stride * 4), 0x00020000)};
+    const PBuf zb{__builtin_amdgcn_make_buffer_rsrc((void*)(a.dz + (size_t)smp * a.dz_stride), (short)0,
+                                                    (int)(a.dz_stride * 4), 0x00020000)};
+    const int iy0 = S * TY * ty, ix0 = S * TX * tx, oy0 = TY * ty, ox0 = TX * tx;
+#pragma unroll
+    for (int i = 0; i < NSX; ++i) {
+      const int e = tid + 256 * i, ic = e / PPA, rem = e - ic * PPA, r = rem / PW, c = rem - r * PW;
+      const int iy = iy0 + r, ix = ix0 + c;
+      const bool in = e < NXP && r < G::PH && c < PWL && iy < a.IH && ix < a.IW;
+      const uint32_t off = in ? (uint32_t)(ic * plane + iy * a.IW + ix) * 4u : 0x7ffffff0u;
+      sx[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xb.r, off, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < NSZ; ++i) {
+      const int e = tid + 256 * i, oc = e / DZS, q = e - oc * DZS, oy = oy0 + q / TX, ox = ox0 + q % TX;
+      const bool in = e < NZP && q < TQ && oy < OH && ox < a.OW;
+      const uint32_t off = in ? (uint32_t)(oc * a.OP + oy * a.OW + ox) * 4u : 0x7ffffff0u;
+      sz[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zb.r, off, 0, 0));
+    }
+  };
+  f4 acc[NRT][NCT];
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) acc[rt][ct] = f4{0.f, 0.f, 0.f, 0.f};
+  if ((int)blockIdx.x < tiles) sload(blockIdx.x);
+  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+#pragma unroll
+    for (int i = 0; i < NSX; ++i)
+      if (tid + 256 * i < NXP) xp[tid + 256 * i] = sx[i];
+#pragma unroll
+    for (int i = 0; i < NSZ; ++i)
+      if (tid + 256 * i < NZP) dzt[tid + 256 * i] = sz[i];
+    __syncthreads();
+    if (tile + (int)gridDim.x < tiles) sload(tile + gridDim.x);
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int boff = S * (kk / 4) * PW + S * (kk % 4), aoff = TX * (kk / 4) + kk % 4;
+      float av[NRT];
+#pragma unroll
+      for (int rt = 0; rt < NRT; ++rt) av[rt] = dzt[ab + 16 * rt * DZS + aoff];
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        const float bv = xp[cb[ct] + bb + boff];
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) acc[rt][ct] = mfma16(av[rt], bv, acc[rt][ct]);
+      }
+    }
+    __syncthreads();  // every wave is done with the tile before the next one is stored
+  }
+  // the four waves' sums in wave order through LDS (aliasing the patch), then one partial per workgroup
+  float* red = sm;  // [OC][NCT * 16]
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float* p = red + (16 * rt + 4 * g + r) * (NCT * 16) + 16 * ct + j;
+            *p = w ? *p + acc[rt][ct][r] : acc[rt][ct][r];
+          }
+    }
+    __syncthreads();
+  }
+  float* out = a.part + (size_t)blockIdx.x * OC * (Kt + 1);
+  for (int i = tid; i < OC * (Kt + 1); i += 256) {
+    const int oc = i / (Kt + 1), c = i - oc * (Kt + 1);
+    out[i] = red[oc * (NCT * 16) + c];
+  }
+}
+
+// ---- conv3's weight gradient (IC 16, OC 32): k_wgrad_t with the COLUMNS split over the waves ---------
+// Same staging and GEMM as k_wgrad_t, but 401 columns x 32 rows do not fit one wave's registers: wave w
+// takes column tiles w, w + 4, ... over all TQ pixels of the tile (no cross-wave reduction), and the
+// tile is TY x TX = 8 x 8 (conv3's 21 x 21 output: 3 x 3 tiles, 77 % used). Patch rows PW = 5 (mod 16)
+// and planes PPA = 9 (mod 16) floats as in k_wgrad_t; dZ rows TQ + 2 floats (A reads: lane groups 0 and
+// 1 on even / odd banks). Each lane group g takes pixel 4 kk + g of k-step kk.
+constexpr int kWt2TY = 8, kWt2TX = 8;
+template <int IC, int OC, int TY, int TX>
+struct Wt2Geo {
+  static constexpr int K = 5, S = 2, Kt = IC * K * K, NCT = (Kt + 1 + 15) / 16, NCW = (NCT + 3) / 4, NRT = OC / 16;
+  static constexpr int PH = (TY - 1) * S + K, PWL = (TX - 1) * S + K, PW = ((PWL - 5 + 15) / 16) * 16 + 5;
+  static constexpr int PPA = ((PH * PW - 9 + 15) / 16) * 16 + 9, TQ = TY * TX, DZS = TQ + 2, KS = TQ / 4;
+  static constexpr int NXP = IC * PPA, NZP = OC * DZS;
+  static constexpr int BMAX = S * (KS / (TX / 4) - 1) * PW + S * 4 * (TX / 4 - 1) + S * 3;
+  static constexpr int OB0 = NXP + NZP, ONES0 = OB0 + (((Kt - OB0) % 16) + 16) % 16;
+  static constexpr int LDS = ONES0 + BMAX + 1;
+  static_assert(PW >= PWL && PPA >= PH * PW && TX % 4 == 0 && OC % 16 == 0, "layout");
+};
+template <int IC, int OC, int TY, int TX>
+__global__ __launch_bounds__(256, 2) void k_wgrad_t2(WgradArgs a, int tiles_x, int tps, int tiles) {
+  using G = Wt2Geo<IC, OC, TY, TX>;
+  constexpr int Kt = G::Kt, NCT = G::NCT, NCW = G::NCW, NRT = G::NRT, PW = G::PW, PWL = G::PWL, PPA = G::PPA,
+                TQ = G::TQ, DZS = G::DZS, KS = G::KS, S = G::S, NXP = G::NXP, NZP = G::NZP;
+  constexpr int NSX = (NXP + 255) / 256, NSZ = (NZP + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float sm[G::LDS];
+  float* xp = sm;            // [IC][PPA]: rows of PW
+  float* dzt = sm + NXP;     // [OC][DZS]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  for (int i = G::OB0 + tid; i < G::LDS; i += 256) sm[i] = 1.0f;  // the bias column's B operands
+  int cb[NCW];
+#pragma unroll
+  for (int i = 0; i < NCW; ++i) {
+    const int c = 16 * (wave + 4 * i) + j, ic = c / 25, r = c - 25 * ic, ky = r / 5, kx = r - 5 * ky;
+    cb[i] = c < Kt ? ic * PPA + ky * PW + kx : (c == Kt ? G::ONES0 : (c & 15));
+  }
+  const int bb = S * g, ab = j * DZS + g;  // B: + S (kk / (TX / 4)) PW + 4 S (kk % (TX / 4)); A: + 16 rt DZS + 4 kk
+  const long plane = (long)a.IH * a.IW;
+  const int OH = a.OP / a.OW;
+  float sx[NSX], sz[NSZ];
+  auto sload = [&](int tile) {
+    const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    const PBuf xb{__builtin_amdgcn_make_buffer_rsrc((void*)(a.x_f + (size_t)smp * a.x_stride), (short)0,
+                                                    (int)(a.x_stride * 4), 0x00020000)};
+    const PBuf zb{__builtin_amdgcn_make_buffer_rsrc((void*)(a.dz + (size_t)smp * a.dz_stride), (short)0,
+                                                    (int)(a.dz_stride * 4), 0x00020000)};
+    const int iy0 = S * TY * ty, ix0 = S * TX * tx, oy0 = TY * ty, ox0 = TX * tx;
+#pragma unroll
+    for (int i = 0; i < NSX; ++i) {
+      const int e = tid + 256 * i, ic = e / PPA, rem = e - ic * PPA, r = rem / PW, c = rem - r * PW;
+      const int iy = iy0 + r, ix = ix0 + c;
+      const bool in = e < NXP && r < G::PH && c < PWL && iy < a.IH && ix < a.IW;
+      const uint32_t off = in ? (uint32_t)(ic * plane + iy * a.IW + ix) * 4u : 0x7ffffff0u;
+      sx[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xb.r, off, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < NSZ; ++i) {
+      const int e = tid + 256 * i, oc = e / DZS, q = e - oc * DZS, oy = oy0 + q / TX, ox = ox0 + q % TX;
+      const bool in = e < NZP && q < TQ && oy < OH && ox < a.OW;
+      const uint32_t off = in ? (uint32_t)(oc * a.OP + oy * a.OW + ox) * 4u : 0x7ffffff0u;
+      sz[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zb.r, off, 0, 0));
+    }
+  };
+  f4 acc[NRT][NCW];
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+    for (int i = 0; i < NCW; ++i) acc[rt][i] = f4{0.f, 0.f, 0.f, 0.f};
+  if ((int)blockIdx.x < tiles) sload(blockIdx.x);
+  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+#pragma unroll
+    for (int i = 0; i < NSX; ++i)
+      if (tid + 256 * i < NXP) xp[tid + 256 * i] = sx[i];
+#pragma unroll
+    for (int i = 0; i < NSZ; ++i)
+      if (tid + 256 * i < NZP) dzt[tid + 256 * i] = sz[i];
+    __syncthreads();
+    if (tile + (int)gridDim.x < tiles) sload(tile + gridDim.x);
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int boff = S * (kk / (TX / 4)) * PW + 4 * S * (kk % (TX / 4));
+      float av[NRT];
+#pragma unroll
+      for (int rt = 0; rt < NRT; ++rt) av[rt] = dzt[ab + 16 * rt * DZS + 4 * kk];
+#pragma unroll
+      for (int i = 0; i < NCW; ++i) {
+        if (wave + 4 * i >= NCT) continue;  // wave-uniform
+        const float bv = xp[cb[i] + bb + boff];
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) acc[rt][i] = mfma16(av[rt], bv, acc[rt][i]);
+      }
+    }
+    __syncthreads();  // every wave is done with the tile before the next one is stored
+  }
+  float* out = a.part + (size_t)blockIdx.x * OC * (Kt + 1);
+#pragma unroll
+  for (int i = 0; i < NCW; ++i) {
+    const int c = 16 * (wave + 4 * i) + j;
+    if (c > Kt) continue;
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(size_t)(16 * rt + 4 * g + r) * (Kt + 1) + c] = acc[rt][i][r];
+  }
+}
+
 // G[w + oc*Kt + k] / G[b + oc] = sum over chunks. Level 1 (k_wsum1) adds groups of kSumGroup
 // consecutive chunks in parallel (blockIdx.y = group), level 2 (k_wsum) adds the group sums in order:
 // a fixed order, so the result is deterministic.
@@ -2146,7 +2762,29 @@ __global__ __launch_bounds__(256) void k_carla_adam(CarlaAdamArgs a) {
   a.P[p] = a.P[p] - a.step_size * (m / (sqrtf(v) / a.sbc2 + a.eps));
 }
 
-int launch_dgrad(const DgradArgs& a, hipStream_t s, bool staged = true) {
+int launch_dgrad(const DgradArgs& a, hipStream_t s, bool staged = true, bool quad = false) {
+  if (staged && quad && a.K == 5 && a.S == 2 && a.IC == 16 && a.OC == 32 && a.w_ic == a.IC) {
+    const int tiles_x = ((a.IW + 1) / 2 + kDq2T - 1) / kDq2T, tps = tiles_x * (((a.IH + 1) / 2 + kDq2T - 1) / kDq2T);
+    const long tiles = (long)a.n * tps;
+    const size_t lds = dq2_lds_bytes(a.OC);
+    static const bool attr = hipFuncSetAttribute((const void*)k_dgrad_q2<16, 32>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+    if (attr && tiles < (1L << 31) && a.dz_stride < (1L << 29) && a.x_stride < (1L << 29) && a.dx_stride < (1L << 29)) {
+      const int grid = (int)std::min<long>(tiles, 256L * 2);  // two workgroups per CU (LDS)
+      hipLaunchKernelGGL((k_dgrad_q2<16, 32>), dim3(grid), dim3(256), lds, s, a, tiles_x, tps, (int)tiles);
+      return 0;
+    }
+  }
+  if (staged && quad && a.K == 5 && a.S == 2 && a.IC == 8 && a.OC == 16 && a.w_ic == a.IC && a.IW % 2 == 0) {
+    const int tiles_x = ((a.IW + 1) / 2 + kDqT - 1) / kDqT, tps = tiles_x * (((a.IH + 1) / 2 + kDqT - 1) / kDqT);
+    const long tiles = (long)a.n * tps;
+    if (tiles >= (1L << 31) || a.dz_stride >= (1L << 29) || a.x_stride >= (1L << 29) || a.dx_stride >= (1L << 29))
+      return -1;
+    // two workgroups per CU (253 VGPRs): a larger grid would run a second, partial round
+    const int grid = (int)std::min<long>(tiles, 256L * 2);
+    hipLaunchKernelGGL((k_dgrad_q<8, 16>), dim3(grid), dim3(256), 0, s, a, tiles_x, tps, (int)tiles);
+    return 0;
+  }
   if (staged && a.K == 5 && a.S == 2 && a.IC <= 16 && a.OC <= 16 && a.w_ic == a.IC &&
       ds2_lds_bytes(a.IC, a.OC) <= 64 * 1024) {
     const int tiles_x = (a.IW + kDs2Tile - 1) / kDs2Tile, tps = tiles_x * ((a.IH + kDs2Tile - 1) / kDs2Tile);
@@ -2345,11 +2983,36 @@ __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, in
 }
 
 int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap, hipStream_t s, bool img = true,
-                 bool bx = false) {
+                 bool bx = false, bool tiled = false) {
   if (a.Kt > kMaxKTab || a.OP > kMaxPTab) return -1;
   if (!a.x_u8 && (long)a.n * a.x_stride * 4 >= 0x70000000L) return -1;  // k_wgrad's 32-bit buffer offsets
   const long per = (long)a.OC * (a.Kt + 1);
   const int OH = a.OP / a.OW;
+  const bool c2 = a.IC == 8 && a.OC == 16, c3 = a.IC == 16 && a.OC == 32;
+  if (img && tiled && a.x_f && a.K == 5 && a.S == 2 && (c2 || c3) && a.dz_stride < (1L << 29) && a.x_stride < (1L << 29)) {
+    const int TY = c2 ? kWtTY : kWt2TY, TX = c2 ? kWtTX : kWt2TX;
+    const int tiles_x = (a.OW + TX - 1) / TX, tps = tiles_x * ((OH + TY - 1) / TY);
+    const long tiles = (long)a.n * tps;
+    const int chunks = (int)std::min<long>(tiles, 1024);
+    const int groups = (chunks + kSumGroup - 1) / kSumGroup;
+    if (tiles < (1L << 31) && (size_t)(chunks + (chunks > kSumGroup ? groups : 0)) * per <= part_cap) {
+      a.part = part;
+      if (c2)
+        hipLaunchKernelGGL((k_wgrad_t<8, 16, kWtTY, kWtTX>), dim3(chunks), dim3(256), 0, s, a, tiles_x, tps, (int)tiles);
+      else
+        hipLaunchKernelGGL((k_wgrad_t2<16, 32, kWt2TY, kWt2TX>), dim3(chunks), dim3(256), 0, s, a, tiles_x, tps,
+                           (int)tiles);
+      const unsigned gb = (unsigned)((per + 255) / 256);
+      if (chunks > kSumGroup) {
+        float* lvl = part + (size_t)chunks * per;
+        hipLaunchKernelGGL(k_wsum1, dim3(gb, groups), dim3(256), 0, s, part, chunks, per, lvl);
+        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, lvl, groups, a.OC, a.Kt, Gw, Gb);
+      } else {
+        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, part, chunks, a.OC, a.Kt, Gw, Gb);
+      }
+      return 0;
+    }
+  }
   if (img && a.x_u8 && ((uintptr_t)a.x_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 8 &&
       a.IC * a.K * (a.K + a.S) + 1 <= 4 * kWimg2CT * 16 && a.IC * a.K * (a.K + a.S) >= (4 * kWimg2CT - 4) * 16 &&
       a.IW % 4 == 0 && a.x_stride % 4 == 0 &&
@@ -2576,12 +3239,13 @@ extern "C" int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc
     WgradArgs wa{dz,          dzs,         L.conv_oc[i], L.conv_oh[i] * L.conv_ow[i], L.conv_ow[i], xf,
                  i ? nullptr : bev, xs,    L.conv_ic[i], L.conv_ih[i],                L.conv_iw[i], L.conv_k[i],
                  L.conv_s[i], n,           L.conv_ic[i] * L.conv_k[i] * L.conv_k[i], 0, nullptr};
-    bad |= launch_wgrad(wa, G + L.conv_w[i], G + L.conv_b[i], c->part, c->part_floats, s, c->conv_img, c->c1bx);
+    bad |= launch_wgrad(wa, G + L.conv_w[i], G + L.conv_b[i], c->part, c->part_floats, s, c->conv_img, c->c1bx,
+                        c->wgrad_t);
     if (i > 0) {
       DgradArgs da{dz,           dzs,          P + L.conv_w[i], L.conv_ic[i], xf,           xs,
                    c->dact[i - 1], xs,         L.conv_ic[i],    L.conv_ih[i], L.conv_iw[i], L.conv_oc[i],
                    L.conv_oh[i], L.conv_ow[i], L.conv_k[i],     L.conv_s[i],  n,            0};
-      bad |= launch_dgrad(da, s, c->conv_img);
+      bad |= launch_dgrad(da, s, c->conv_img, c->dgrad_q);
     }
   }
   if (bad) return ppo_fail("ppo_carla_update: no gradient kernel for this shape", -1);

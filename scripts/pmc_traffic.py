@@ -17,7 +17,8 @@ CLASSES = [("k_fwdbwd", "fwdbwd"), ("k_upd", "fwdbwd"), ("k_dw", "dw"), ("k_act"
            ("k_adv_", "adv_stats"), ("k_synth_step", "synth_env"), ("k_rollout", "rollout"),
            ("k_values", "values"),
            # CaRL (cfg5) kernels
-           ("k_conv_img2", "conv1_fwd"), ("k_wgrad_img2", "conv1_wgrad"), ("k_dgrad_s2", "conv2_dgrad"),
+           ("k_conv_t", "conv2_fwd"), ("k_wgrad_t", "conv2_wgrad"), ("k_dgrad_q", "conv2_dgradq"),
+           ("k_conv_img3", "conv1_fwd"), ("k_conv_img2", "conv1_fwd"), ("k_wgrad_img2", "conv1_wgrad"), ("k_dgrad_s2", "conv2_dgrad"),
            ("k_conv_fin", "conv_fin"), ("k_conv", "conv"), ("k_wgrad", "wgrad"), ("k_dgrad", "dgrad"),
            ("k_wsum", "wsum")]
 

@@ -104,7 +104,7 @@ def test_staged_conv1_kernels_match_generic():
     ret = rng.normal(0.0, 1.0, n).astype(np.float32)
     old_v = rng.normal(0.0, 1.0, n).astype(np.float32)
     outs = []
-    for opt in ("conv1=generic", "conv1=staged"):
+    for opt in ("conv1=generic", "conv1=staged,conv_dgrad=staged,conv_wgrad=generic,conv_fwd=generic"):
         ag = ppo_amd.CarlaAgent(max_batch=16, seed=7, options=opt)
         ag.load_params(p)
         res = [run(ag, bev, meas, vmeas, mode=m, env_base=3, step_id=5) for m in ("sample", "mean", "roach")]
@@ -128,6 +128,88 @@ def test_staged_conv1_kernels_match_generic():
         else:
             np.testing.assert_array_equal(g1[o:o + m], g0[o:o + m])
     np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("opts,layers", [(("conv_dgrad=staged", "conv_dgrad=quad"), (0, 1)),
+                                         (("conv_wgrad=generic", "conv_wgrad=tiled"), (1, 2))])
+def test_conv2_backward_forms_match(opts, layers):
+    """conv_dgrad=quad (conv2: k_dgrad_q, the four stride-2 parity classes as the columns of one GEMM
+    over quads, k = (tap, oc) with the missing taps as zero weights; conv3: k_dgrad_q2, the classes as
+    separate GEMMs sharing each dZ operand) against k_dgrad_s2 / k_dgrad (conv_dgrad=staged): conv3's
+    and conv2's input gradients feed only conv2's and conv1's weight gradients (and conv2's input
+    gradient), so every other gradient tensor is bitwise equal and those agree within fp32 summation
+    noise (rel-L2 < 1e-5). conv_wgrad=tiled (k_wgrad_t for conv2, k_wgrad_t2 for conv3: dZ tile and
+    input patch staged in LDS, one partial per persistent workgroup) against the generic k_wgrad: only
+    conv2's and conv3's own weight and bias gradients differ, within the same bar. n = 7 covers the partial tiles (47 = 2 x 16 + 15 quads per
+    edge; 45 = 5 x 8 + 5 and 2 x 16 + 13 output pixels) and a grid with fewer tiles than workgroups."""
+    import carla_torch_ref  # noqa: F401
+    n = 7
+    L = CI.layout()
+    p = CI.params(L)
+    bev, meas, vmeas, act = CI.inputs(n)
+    rng = np.random.default_rng(5)
+    old_logp = rng.normal(-2.0, 0.3, n).astype(np.float32)
+    adv = rng.normal(0.0, 1.0, n).astype(np.float32)
+    ret = rng.normal(0.0, 1.0, n).astype(np.float32)
+    old_v = rng.normal(0.0, 1.0, n).astype(np.float32)
+    outs = []
+    for opt in opts:
+        ag = ppo_amd.CarlaAgent(max_batch=16, seed=7, options=opt)
+        ag.load_params(p)
+        d = [DeviceArray.from_numpy(bev, np.uint8)] + [DeviceArray.from_numpy(np.ascontiguousarray(x, np.float32))
+                                                       for x in (meas, vmeas, act, old_logp, adv, ret, old_v)]
+        ag.update(*d, lr=3e-4, clip_coef=0.2, ent_coef=0.01, vf_coef=0.5, max_grad_norm=0.5, adam_eps=1e-5)
+        outs.append((ag.last_grad(), ag.params()))
+        ag.close()
+    (g0, p0), (g1, p1) = outs
+    moved = {o for i in layers for o in (L.conv_w[i], L.conv_b[i])}
+    for t in range(L.ntensors):
+        o, m = L.t_off[t], L.t_len[t]
+        if o in moved:
+            r = np.linalg.norm((g1[o:o + m] - g0[o:o + m]).astype(np.float64)) / np.linalg.norm(g0[o:o + m])
+            assert r < 1e-5, (t, r)
+        else:
+            np.testing.assert_array_equal(g1[o:o + m], g0[o:o + m])
+    np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-7)
+
+
+def test_tiled_conv2_forward_matches_generic():
+    """conv_fwd=tiled (k_conv_t: input patch staged in LDS, weights in registers, k = (tap, ic)) against
+    the generic k_conv: the same fp32 products in another k order, so the forward (mean mode: value,
+    Beta concentrations, log-prob) agrees within fp32 summation noise, and after one update every
+    gradient tensor within rel-L2 1e-4 and the stepped parameters within 1e-6 (n = 7: partial tiles,
+    45 = 5 x 8 + 5 rows and 2 x 16 + 13 columns)."""
+    import carla_torch_ref  # noqa: F401
+    n = 7
+    L = CI.layout()
+    p = CI.params(L)
+    bev, meas, vmeas, act = CI.inputs(n)
+    rng = np.random.default_rng(6)
+    old_logp = rng.normal(-2.0, 0.3, n).astype(np.float32)
+    adv = rng.normal(0.0, 1.0, n).astype(np.float32)
+    ret = rng.normal(0.0, 1.0, n).astype(np.float32)
+    old_v = rng.normal(0.0, 1.0, n).astype(np.float32)
+    outs = []
+    for opt in ("conv_fwd=generic", "conv_fwd=tiled"):
+        ag = ppo_amd.CarlaAgent(max_batch=16, seed=7, options=opt)
+        ag.load_params(p)
+        fwd = run(ag, bev, meas, vmeas, act)
+        d = [DeviceArray.from_numpy(bev, np.uint8)] + [DeviceArray.from_numpy(np.ascontiguousarray(x, np.float32))
+                                                       for x in (meas, vmeas, act, old_logp, adv, ret, old_v)]
+        ag.update(*d, lr=3e-4, clip_coef=0.2, ent_coef=0.01, vf_coef=0.5, max_grad_norm=0.5, adam_eps=1e-5)
+        outs.append((fwd, ag.last_grad(), ag.params()))
+        ag.close()
+    (f0, g0, p0), (f1, g1, p1) = outs
+    for x0, x1 in zip(f0, f1):
+        np.testing.assert_allclose(x1, x0, rtol=1e-4, atol=1e-5)
+    for t in range(L.ntensors):
+        o, m = L.t_off[t], L.t_len[t]
+        nrm = np.linalg.norm(g0[o:o + m].astype(np.float64))
+        if nrm == 0:
+            continue
+        r = np.linalg.norm((g1[o:o + m] - g0[o:o + m]).astype(np.float64)) / nrm
+        assert r < 1e-4, (t, r)
+    np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-6)
 
 
 @pytest.mark.parametrize("opts", [("conv1=staged", "conv1=packed,conv1_mfma=f32"),

@@ -297,6 +297,89 @@ __global__ __launch_bounds__(256, 2) void k_conv_t(ConvArgs a, int tiles_x, int 
   }
 }
 
+// ---- conv3's forward (IC 16, OC 32): k_conv_t with the two 16-channel row tiles on different waves ---
+// 400 k x 32 rows of weights do not fit one wave's registers: wave w keeps row tile w & 1 (100 A
+// operands) and takes half of the 8 x 8 output tile's pixels (two MFMA column tiles of 2 rows x 8
+// columns). Patch rows PW = 24 floats (two output rows = 16 banks apart) and ic planes of odd length:
+// a ds_read_b32 half (lane groups g = 0, 1) hits 32 distinct banks. k = 4 kk + g -> ic = 4 (kk % 4) + g,
+// tap = kk / 4. Same products as k_conv (fp32 MFMA), another k order (tolerance tests).
+constexpr int kCt2T = 8;  // output tile edge (conv3: 21 x 21 -> 3 x 3 tiles, 77 % used)
+template <int IC, int OC>
+__global__ __launch_bounds__(256, 2) void k_conv_t2(ConvArgs a, int tiles_x, int tps, int tiles) {
+  constexpr int K = 5, S = 2, T = kCt2T, PH = (T - 1) * S + K, PWL = PH, PW = 24, PPA = 457, NXP = IC * PPA;
+  constexpr int ICQ = IC / 4, KS = K * K * ICQ, NSX = (NXP + 255) / 256;
+  static_assert(IC % 4 == 0 && OC == 32 && PW >= PWL && PPA >= PH * PW && (PPA & 1) && PW % 16 == 8, "shape");
+  __shared__ float xp[NXP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int rt = wave & 1, ph = wave >> 1;
+  float wa[KS];  // A operands: W[16 rt + j][ic][tap], k = 4 kk + g
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int tap = kk / ICQ, ic = 4 * (kk - tap * ICQ) + g;
+    wa[kk] = a.W[((16 * rt + j) * IC + ic) * (K * K) + tap];
+  }
+  float bias[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bias[r] = a.b[16 * rt + 4 * g + r];
+  // lane j of column tile u: output pixel (2 (2 ph + u) + (j >> 3), j & 7) of the tile
+  const int bb = g * PPA + 2 * (4 * ph + (j >> 3)) * PW + 2 * (j & 7);  // + 4 PW u + 4 (kk % ICQ) PPA + ky PW + kx
+  const long plane = (long)a.IH * a.IW;
+  const int P = a.OH * a.OW;
+  float sx[NSX];
+  auto sload = [&](int tile) {
+    const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    const PBuf xb{__builtin_amdgcn_make_buffer_rsrc((void*)(a.in_f + (size_t)smp * a.in_stride), (short)0,
+                                                    (int)(a.in_stride * 4), 0x00020000)};
+    const int iy0 = S * T * ty, ix0 = S * T * tx;
+#pragma unroll
+    for (int i = 0; i < NSX; ++i) {
+      const int e = tid + 256 * i, ic = e / PPA, rem = e - ic * PPA, r = rem / PW, c = rem - r * PW;
+      const int iy = iy0 + r, ix = ix0 + c;
+      const bool in = e < NXP && r < PH && c < PWL && iy < a.IH && ix < a.IW;
+      const uint32_t off = in ? (uint32_t)(ic * plane + iy * a.IW + ix) * 4u : 0x7ffffff0u;
+      sx[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xb.r, off, 0, 0));
+    }
+  };
+  // no register prefetch of the next patch here (the weights take 100 VGPRs): the two workgroups of a
+  // CU overlap one's staging with the other's MFMAs
+  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    sload(tile);
+#pragma unroll
+    for (int i = 0; i < NSX; ++i)
+      if (tid + 256 * i < NXP) xp[tid + 256 * i] = sx[i];
+    __syncthreads();
+    const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
+    f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int tap = kk / ICQ, icq = kk - tap * ICQ, ky = tap / K, kx = tap - ky * K;
+      float bv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) bv[u] = xp[bb + 4 * PW * u + 4 * icq * PPA + ky * PW + kx];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) acc[u] = mfma16(wa[kk], bv[u], acc[u]);
+      if (kk % 10 == 9) __builtin_amdgcn_sched_barrier(0);  // bounds the LDS read hoisting (registers)
+    }
+    __syncthreads();  // every wave is done with the patch before the next one is stored
+    const PBuf ob{__builtin_amdgcn_make_buffer_rsrc((void*)(a.out + (size_t)smp * a.out_stride), (short)0,
+                                                    (int)(a.out_stride * 4), 0x00020000)};
+    const int ox = T * tx + (j & 7);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int oy = T * ty + 2 * (2 * ph + u) + (j >> 3);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int oc = 16 * rt + 4 * g + r;
+        const bool in = oy < a.OH && ox < a.OW;
+        float y = acc[u][r] + bias[r];
+        if (a.relu) y = y > 0.0f ? y : 0.0f;
+        const uint32_t off = in ? (uint32_t)(oc * P + oy * a.OW + ox) * 4u : 0x7ffffff0u;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y), ob.r, off, 0, 0);
+      }
+    }
+  }
+}
+
 // split-K finish: out = relu(sum over z of the partials, in z order, + bias)
 __global__ __launch_bounds__(256) void k_conv_fin(ConvArgs a, int Z) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -1168,6 +1251,16 @@ int launch_conv(const ConvArgs& a, hipStream_t s, int img = 1, bool fin = true, 
     if (tiles < (1L << 31)) {
       const int grid = (int)std::min<long>(tiles, 256L * 2);
       hipLaunchKernelGGL((k_conv_t<8, 16, kCtTY, kCtTX>), dim3(grid), dim3(256), 0, s, a, tiles_x, tps, (int)tiles);
+      return 0;
+    }
+  }
+  if (img && a.tiled && a.in_f && a.K == 5 && a.S == 2 && a.IC == 16 && a.OC == 32 && a.in_stride < (1L << 29) &&
+      a.out_stride < (1L << 29)) {
+    const int tiles_x = (a.OW + kCt2T - 1) / kCt2T, tps = tiles_x * ((a.OH + kCt2T - 1) / kCt2T);
+    const long tiles = (long)a.n * tps;
+    if (tiles < (1L << 31)) {
+      const int grid = (int)std::min<long>(tiles, 256L * 2);
+      hipLaunchKernelGGL((k_conv_t2<16, 32>), dim3(grid), dim3(256), 0, s, a, tiles_x, tps, (int)tiles);
       return 0;
     }
   }

@@ -638,6 +638,8 @@ constexpr int kDgradQuadAuto = 1;
 constexpr int kWgradTiledAuto = 1;
 // conv_fwd=auto: the LDS-tiled form (k_conv_t)
 constexpr int kConvTiledAuto = 1;
+// deep_dgrad=auto: conv6's input gradient as a dense GEMM + col2im
+constexpr int kDgradColAuto = 1;
 template <int K, int S>
 struct Img3Geo {
   static constexpr int TI = (kImgTile - 1) * S + K;          // patch rows
@@ -1336,6 +1338,9 @@ struct ppo_carla {
   int wgrad_t = kWgradTiledAuto;
   // conv2's forward: 1 k_conv_t (LDS-staged input patches), 0 k_conv (create option conv_fwd=tiled|generic)
   int conv_t = kConvTiledAuto;
+  // conv6's input gradient: 1 dense GEMM + col2im (create option deep_dgrad=col|gather)
+  int dgrad_col = kDgradColAuto;
+  float *dcol = nullptr, *wt = nullptr, *zbias = nullptr;  // carla_train_init
   float* c1w = nullptr;  // k_conv_img3's A-operand table
   // MLP tail for n <= kTailMaxN: 1 (default) one launch per stage, 0 one cooperative launch (a grid
   // barrier between stages: slower here, a cooperative launch costs more than the launches it
@@ -1361,7 +1366,7 @@ extern "C" int ppo_carla_destroy(ppo_carla_t* c) {
   float* bufs[] = {c->P,    c->enc,  c->s1,  c->l1,  c->feat,  c->v1,  c->v2,      c->val,  c->p1,
                    c->p2,   c->hpre, c->G,   c->m,   c->v,     c->denc, c->ds1,     c->dl1,  c->dfeat,
                    c->dv1,  c->dv2,  c->dp1, c->dp2, c->dhead, c->dval, c->lp,      c->ent,  c->rowstat,
-                   c->part, c->small,  c->ksplit, c->c1w, reinterpret_cast<float*>(c->tail_bar)};
+                   c->part, c->small,  c->ksplit, c->c1w, c->dcol, c->wt, c->zbias, reinterpret_cast<float*>(c->tail_bar)};
   for (float* b : bufs)
     if (b) (void)hipFree(b);
   for (float* b : c->act)
@@ -1385,6 +1390,7 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
   int dgrad_q = kDgradQuadAuto;
   int wgrad_t = kWgradTiledAuto;
   int conv_t = kConvTiledAuto;
+  int dgrad_col = kDgradColAuto;
   if (options && *options) {  // comma-separated key=value
     std::string rest(options);
     while (!rest.empty()) {
@@ -1409,6 +1415,9 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
       else if (o == "conv_fwd=tiled") conv_t = 1;
       else if (o == "conv_fwd=generic") conv_t = 0;
       else if (o == "conv_fwd=auto") conv_t = kConvTiledAuto;
+      else if (o == "deep_dgrad=col") dgrad_col = 1;
+      else if (o == "deep_dgrad=gather") dgrad_col = 0;
+      else if (o == "deep_dgrad=auto") dgrad_col = kDgradColAuto;
       else return ppo_fail("ppo_carla_create_ex: unknown option " + o, -1);
     }
   }
@@ -1432,6 +1441,7 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
   c->dgrad_q = dgrad_q;
   c->wgrad_t = wgrad_t;
   c->conv_t = conv_t;
+  c->dgrad_col = dgrad_col;
 #ifdef PPO_DIAG
   if (const char* e = getenv("PPO_CARLA_CONV1")) c->conv_img = e[0] - '0';
 #endif
@@ -2104,6 +2114,50 @@ __global__ __launch_bounds__(256, 2) void k_dgrad_q2(DgradArgs a, int tiles_x, i
   }
 }
 static size_t dq2_lds_bytes(int OC) { return ((size_t)(9 + 6 + 6 + 4) * (OC / 4) * 64 + (size_t)OC * 168) * 4; }
+
+// ---- the last convolution's input gradient as a dense GEMM + col2im (create option deep_dgrad=col) ----
+// conv6 (4 x 4 -> 2 x 2, stride 1) has 4 output pixels: k_dgrad's per-pixel tap sets are mostly
+// outside the output plane (2.25 of 9 taps valid on average, the rest multiply zeros). Instead dcol[n][(ic, ky, kx)][oy, ox] = sum_oc W[oc][ic, ky, kx] dZ[n][oc][oy, ox]
+// is one dense GEMM (k_conv as a 1 x 1 convolution over the OH x OW plane with the transposed weights,
+// no zero products), and k_col2im adds each input pixel's (at most K x K) contributions in (ky, kx)
+// order and applies the ReLU mask. Another sum order than k_dgrad (tolerance tests).
+__global__ void k_wtrans(const float* __restrict__ W, int OC, int Kt, float* __restrict__ Wt) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // Wt[k][oc] = W[oc][k]
+  if (i >= (long)OC * Kt) return;
+  const int k = (int)(i / OC), oc = (int)(i - (long)k * OC);
+  Wt[i] = W[(long)oc * Kt + k];
+}
+template <int K, int S>
+__global__ void k_col2im(const float* __restrict__ dcol, const float* __restrict__ x, long x_stride,
+                         float* __restrict__ dx, long dx_stride, int IC, int IH, int IW, int OH, int OW, int n,
+                         int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long per = (long)IC * IH * IW;
+  if (i >= per * n) return;
+  const long smp = i / per;
+  const int r = (int)(i - smp * per), ic = r / (IH * IW), p = r - ic * IH * IW, iy = p / IW, ix = p - iy * IW;
+  const int OP = OH * OW;
+  const float* col = dcol + (size_t)smp * IC * K * K * OP + (size_t)ic * K * K * OP;
+  float v = 0.0f;
+#pragma unroll
+  for (int ky = 0; ky < K; ++ky) {
+    const int dy = iy - ky, oy = dy / S;
+    if (dy < 0 || dy % S || oy >= OH) continue;
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx) {
+      const int dxx = ix - kx, ox = dxx / S;
+      if (dxx < 0 || dxx % S || ox >= OW) continue;
+      v += col[(ky * K + kx) * OP + oy * OW + ox];
+    }
+  }
+  const float xm = x[smp * x_stride + r];
+  const float gv = xm > 0.0f ? v : 0.0f;
+  float* o = dx + smp * dx_stride + r;
+  *o = accumulate ? *o + gv : gv;
+}
+// conv6 only: for conv5 (stride 2, 10 x 10 -> 4 x 4) the col2im pass costs more than the GEMM saves
+// (GEMM 77 + col2im 127 us vs k_dgrad's 182 us; conv6: 5 + 71 + 33 vs 370 us; profiles/r05/carla_tiled/)
+static bool dgrad_col_layer(int OH, int OW, int K = 3, int S = 1) { return OH * OW <= 16 && K == 3 && S == 1; }
 
 struct WgradArgs {
   const float* dz;  // [n][OC][OP], sample stride dz_stride
@@ -3233,6 +3287,17 @@ static int carla_train_init(ppo_carla_t* c) {
   rc |= carla_alloc(&c->rowstat, B * 8);
   c->part_floats = carla_part_floats(L, (long)B);
   rc |= carla_alloc(&c->part, c->part_floats);
+  size_t dcol_f = 1, wt_f = 1, zb_f = 1;
+  for (int i = 1; i < PPO_CARLA_NCONV; ++i)
+    if (dgrad_col_layer(L.conv_oh[i], L.conv_ow[i], L.conv_k[i], L.conv_s[i])) {
+      const size_t kt = (size_t)L.conv_ic[i] * L.conv_k[i] * L.conv_k[i];
+      dcol_f = std::max(dcol_f, B * kt * L.conv_oh[i] * L.conv_ow[i]);
+      wt_f = std::max(wt_f, kt * L.conv_oc[i]);
+      zb_f = std::max(zb_f, kt);
+    }
+  rc |= carla_alloc(&c->dcol, dcol_f);
+  rc |= carla_alloc(&c->wt, wt_f);
+  rc |= carla_alloc(&c->zbias, zb_f);
   // [0,2) adv mean/std, [64,71) stats + {total, coef}, [128,288) int64 tensor table, [320,...) norm slices
   rc |= carla_alloc(&c->small, 320 + PPO_CARLA_MAX_TENSORS * kNormSplit);
   if (rc) return ppo_fail("ppo_carla_update: device allocation failed", -2);
@@ -3338,7 +3403,24 @@ extern "C" int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc
       DgradArgs da{dz,           dzs,          P + L.conv_w[i], L.conv_ic[i], xf,           xs,
                    c->dact[i - 1], xs,         L.conv_ic[i],    L.conv_ih[i], L.conv_iw[i], L.conv_oc[i],
                    L.conv_oh[i], L.conv_ow[i], L.conv_k[i],     L.conv_s[i],  n,            0};
-      bad |= launch_dgrad(da, s, c->conv_img, c->dgrad_q);
+      if (c->dgrad_col && dgrad_col_layer(L.conv_oh[i], L.conv_ow[i], L.conv_k[i], L.conv_s[i])) {
+        const int kt = L.conv_ic[i] * L.conv_k[i] * L.conv_k[i], OP = L.conv_oh[i] * L.conv_ow[i];
+        hipLaunchKernelGGL(k_wtrans, dim3((unsigned)(((long)kt * L.conv_oc[i] + 255) / 256)), dim3(256), 0, s,
+                           P + L.conv_w[i], L.conv_oc[i], kt, c->wt);
+        ConvArgs ca{dz,     nullptr, dzs, L.conv_oc[i], L.conv_oh[i], L.conv_ow[i], c->wt, c->zbias, c->dcol,
+                    (long)kt * OP, kt, L.conv_oh[i], L.conv_ow[i], 1, 1, 0, n, nullptr, 0};
+        bad |= launch_conv(ca, s, 0);
+        const long tot = (long)n * xs;
+        const dim3 cg((unsigned)((tot + 255) / 256));
+        if (L.conv_s[i] == 1)
+          hipLaunchKernelGGL((k_col2im<3, 1>), cg, dim3(256), 0, s, c->dcol, xf, xs, c->dact[i - 1], xs, L.conv_ic[i],
+                             L.conv_ih[i], L.conv_iw[i], L.conv_oh[i], L.conv_ow[i], n, 0);
+        else
+          hipLaunchKernelGGL((k_col2im<3, 2>), cg, dim3(256), 0, s, c->dcol, xf, xs, c->dact[i - 1], xs, L.conv_ic[i],
+                             L.conv_ih[i], L.conv_iw[i], L.conv_oh[i], L.conv_ow[i], n, 0);
+      } else {
+        bad |= launch_dgrad(da, s, c->conv_img, c->dgrad_q);
+      }
     }
   }
   if (bad) return ppo_fail("ppo_carla_update: no gradient kernel for this shape", -1);

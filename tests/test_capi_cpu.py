@@ -152,7 +152,7 @@ for opt in ("upd_kernel=fast", "act_kernel=3", "bogus=1", "dw_fused", "rollout=s
     ctx = ctypes.c_void_p()
     rc = lib.ppo_create_ex(ctypes.byref(cfg), 0, opt.encode(), ctypes.byref(ctx))
     out.append([rc, bool(ctx.value), lib.ppo_last_error().decode()])
-for opt in ("tail=coop", "conv1=staged,tail=", "conv1=fast", "conv1_mfma=bx9", "conv_dgrad=fast", "conv_wgrad=quad", "conv_fwd=x"):  # the CaRL agent's options
+for opt in ("tail=coop", "conv1=staged,tail=", "conv1=fast", "conv1_mfma=bx9", "conv_dgrad=fast", "conv_wgrad=quad", "conv_fwd=x", "deep_dgrad=dense"):  # the CaRL agent's options
     cfg = ppo_amd.CarlaConfig(15, 192, 192, 8, 3, 2, 1.0, 32, 7, 0)
     ctx = ctypes.c_void_p()
     rc = lib.ppo_carla_create_ex(ctypes.byref(cfg), 0, opt.encode(), ctypes.byref(ctx))

@@ -131,7 +131,8 @@ def test_staged_conv1_kernels_match_generic():
 
 
 @pytest.mark.parametrize("opts,layers", [(("conv_dgrad=staged", "conv_dgrad=quad"), (0, 1)),
-                                         (("conv_wgrad=generic", "conv_wgrad=tiled"), (1, 2))])
+                                         (("conv_wgrad=generic", "conv_wgrad=tiled"), (1, 2)),
+                                         (("deep_dgrad=gather", "deep_dgrad=col"), (0, 1, 2, 3, 4))])
 def test_conv2_backward_forms_match(opts, layers):
     """conv_dgrad=quad (conv2: k_dgrad_q, the four stride-2 parity classes as the columns of one GEMM
     over quads, k = (tap, oc) with the missing taps as zero weights; conv3: k_dgrad_q2, the classes as
@@ -140,7 +141,9 @@ def test_conv2_backward_forms_match(opts, layers):
     gradient), so every other gradient tensor is bitwise equal and those agree within fp32 summation
     noise (rel-L2 < 1e-5). conv_wgrad=tiled (k_wgrad_t for conv2, k_wgrad_t2 for conv3: dZ tile and
     input patch staged in LDS, one partial per persistent workgroup) against the generic k_wgrad: only
-    conv2's and conv3's own weight and bias gradients differ, within the same bar. n = 7 covers the partial tiles (47 = 2 x 16 + 15 quads per
+    conv2's and conv3's own weight and bias gradients differ, within the same bar. deep_dgrad=col (conv6's
+    input gradient as a dense GEMM into columns + k_col2im) against k_dgrad: every conv layer's
+    gradient below conv6 moves (conv6's own weight gradient and the MLP's stay bitwise). n = 7 covers the partial tiles (47 = 2 x 16 + 15 quads per
     edge; 45 = 5 x 8 + 5 and 2 x 16 + 13 output pixels) and a grid with fewer tiles than workgroups."""
     import carla_torch_ref  # noqa: F401
     n = 7

@@ -135,6 +135,15 @@ int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_carla_t** out)
  *                              products as split-bf16 MFMAs (bx3, auto: the raw byte operand is exact
  *                              in bf16, the fp32 operand's three bf16 pieces make every product exact;
  *                              fp32 accumulation on 16x16x32 bf16 MFMAs) or on 16x16x4 fp32 MFMAs
+ *   conv_fwd=tiled|generic     conv2 / conv3 forward from LDS-staged input patches (k_conv_t / k_conv_t2,
+ *                              default) or the generic gather kernel (A/B tests; another fp32 sum order)
+ *   conv_wgrad=tiled|generic   conv2 / conv3 weight gradients from LDS-staged tiles (k_wgrad_t / k_wgrad_t2,
+ *                              default) or the generic k_wgrad
+ *   conv_dgrad=quad|staged     conv2 / conv3 input gradients with the four stride-2 parity classes of a
+ *                              quad sharing one dZ operand (k_dgrad_q / k_dgrad_q2, default) or
+ *                              k_dgrad_s2 / k_dgrad (needs conv1=staged|packed)
+ *   deep_dgrad=col|gather      conv6's input gradient as a dense GEMM into columns + col2im (default) or
+ *                              k_dgrad
  *   tail=staged|fused|layers   forwards of n <= 64 rows: the MLP tail after the CNN as one launch per
  *                              dependency stage (default), one cooperative launch with a grid barrier
  *                              between stages, or one k_conv / k_conv_fin pair per layer (the path of

@@ -1888,11 +1888,13 @@ __global__ __launch_bounds__(256) void k_dgrad_s2(DgradArgs a, int tiles_x, int 
 // two px-classes of a quad sit in lanes j and j ^ 8, one exchange gives each lane four consecutive
 // input pixels (two 8-byte stores, the ReLU mask read the same way). The sum runs in another order
 // than k_dgrad's (tolerance tests, not bitwise).
-constexpr int kDqT = 16;          // quads per tile edge (32 x 32 input pixels)
-constexpr int kDqR = kDqT + 2;    // dZ region edge (jj, ii < 3)
+constexpr int kDqT = 16;          // quads per tile row (32 input pixels)
+constexpr int kDqU = 2;           // quad rows per wave: a tile is 4 kDqU x kDqT quads
+constexpr int kDqR = kDqT + 2;    // dZ region row length (ii < 3)
 template <int IC, int OC>
-__global__ __launch_bounds__(256, 2) void k_dgrad_q(DgradArgs a, int tiles_x, int tps, int tiles) {
-  constexpr int K = 5, R = kDqR, RR = R * R, NCT = 4 * IC / 16, OCQ = OC / 4, KS = 9 * OCQ;
+__global__ __launch_bounds__(256, kDqU == 2 ? 3 : 2) void k_dgrad_q(DgradArgs a, int tiles_x, int tps, int tiles) {
+  constexpr int U = kDqU, TQY = 4 * U, RY = TQY + 2;
+  constexpr int K = 5, R = kDqR, RR = RY * R, NCT = 4 * IC / 16, OCQ = OC / 4, KS = 9 * OCQ;
   // each oc plane padded to RRP = 16 (mod 32) dwords: lane groups g = 0, 1 (one ds_read_b32 half) read
   // 16 banks apart, conflict-free
   constexpr int RRP = ((RR - 16 + 31) / 32) * 32 + 16;
@@ -1914,11 +1916,11 @@ __global__ __launch_bounds__(256, 2) void k_dgrad_q(DgradArgs a, int tiles_x, in
     }
   }
   // the lane's A base: dzl[g][4 wave][j]; step kk of row u adds 4 ocq RRP + (u + 2 - jj) R + (2 - ii)
-  const int abase = g * RRP + 4 * wave * R + j;
+  const int abase = g * RRP + U * wave * R + j;
   float st[NST];
   auto sload = [&](int tile) {
     const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
-    const int oy0 = ty * kDqT - 2, ox0 = tx * kDqT - 2;
+    const int oy0 = ty * TQY - 2, ox0 = tx * kDqT - 2;
     // a buffer descriptor over the sample's dZ: elements outside the output plane read as 0 through an
     // offset past the buffer (no select after the load, so the loads stay in flight over the tile)
     const PBuf zb{__builtin_amdgcn_make_buffer_rsrc((void*)(a.dz + (size_t)smp * a.dz_stride), (short)0,
@@ -1944,22 +1946,23 @@ __global__ __launch_bounds__(256, 2) void k_dgrad_q(DgradArgs a, int tiles_x, in
     __syncthreads();
     const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
     if (tile + (int)gridDim.x < tiles) sload(tile + gridDim.x);
-    f4 acc[4][NCT];
+    f4 acc[U][NCT];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) acc[u][ct] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
       const int tap = kk / OCQ, ocq = kk - tap * OCQ, jj = tap / 3, ii = tap % 3;
-      float av[4];
+      float av[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) av[u] = dzl[abase + 4 * ocq * RRP + (u + 2 - jj) * R + (2 - ii)];
+      for (int u = 0; u < U; ++u) av[u] = dzl[abase + 4 * ocq * RRP + (u + 2 - jj) * R + (2 - ii)];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct)
           if (ct + 2 * jj < K) acc[u][ct] = mfma16(av[u], bw[ct][kk], acc[u][ct]);  // py = 1 has no jj = 2 taps
+      if (kk % 12 == 11) __builtin_amdgcn_sched_barrier(0);  // bounds the LDS read hoisting (registers)
     }
     __syncthreads();  // every wave is done with dzl before the next tile's region is stored
     // lane (j, g) holds, for quad row 4 wave + u and class (py = ct, px = j >> 3), channel j & 7 of the
@@ -1972,13 +1975,13 @@ __global__ __launch_bounds__(256, 2) void k_dgrad_q(DgradArgs a, int tiles_x, in
                                                     (int)(a.dx_stride * 4), 0x00020000)};
     const int ix = 2 * tx * kDqT + 8 * g + 4 * px;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
         const f4 v = acc[u][ct];
         const float s0 = px ? v[0] : v[2], s1 = px ? v[1] : v[3];
         const float r0 = __shfl_xor(s0, 8), r1 = __shfl_xor(s1, 8);
-        const int iy = 2 * (ty * kDqT + 4 * wave + u) + ct;
+        const int iy = 2 * (ty * TQY + U * wave + u) + ct;
         float o[4];
         o[0] = px ? r0 : v[0];
         o[1] = px ? v[2] : r0;
@@ -2923,12 +2926,13 @@ int launch_dgrad(const DgradArgs& a, hipStream_t s, bool staged = true, bool qua
     }
   }
   if (staged && quad && a.K == 5 && a.S == 2 && a.IC == 8 && a.OC == 16 && a.w_ic == a.IC && a.IW % 2 == 0) {
-    const int tiles_x = ((a.IW + 1) / 2 + kDqT - 1) / kDqT, tps = tiles_x * (((a.IH + 1) / 2 + kDqT - 1) / kDqT);
+    const int tiles_x = ((a.IW + 1) / 2 + kDqT - 1) / kDqT, tps = tiles_x * (((a.IH + 1) / 2 + 4 * kDqU - 1) / (4 * kDqU));
     const long tiles = (long)a.n * tps;
     if (tiles >= (1L << 31) || a.dz_stride >= (1L << 29) || a.x_stride >= (1L << 29) || a.dx_stride >= (1L << 29))
       return -1;
-    // two workgroups per CU (253 VGPRs): a larger grid would run a second, partial round
-    const int grid = (int)std::min<long>(tiles, 256L * 2);
+    // one round of resident workgroups (kDqU = 2: three per CU; 4: two): a larger grid would run a
+    // second, partial round
+    const int grid = (int)std::min<long>(tiles, 256L * (kDqU == 2 ? 3 : 2));
     hipLaunchKernelGGL((k_dgrad_q<8, 16>), dim3(grid), dim3(256), 0, s, a, tiles_x, tps, (int)tiles);
     return 0;
   }

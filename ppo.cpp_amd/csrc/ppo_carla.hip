@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
 // k_conv (fp32 MFMA), another k order (tolerance tests).
 constexpr int kCtTY = 8, kCtTX = 16;  // conv2: 45 x 45 -> 6 x 3 tiles
 template <int IC, int OC, int TY, int TX>
-__global__ __launch_bounds__(256, 2) void k_conv_t(ConvArgs a, int tiles_x, int tps, int tiles) {
+__global__ __launch_bounds__(256, 3) void k_conv_t(ConvArgs a, int tiles_x, int tps, int tiles) {
   constexpr int K = 5, S = 2, PH = (TY - 1) * S + K, PW = (TX - 1) * S + K, PP = PH * PW, NX = IC * PP;
   constexpr int NRT = OC / 16, ICQ = IC / 4, KS = K * K * ICQ, RPW = TY / 4, NSX = (NX + 255) / 256;
   static_assert(OC % 16 == 0 && IC % 4 == 0 && TY % 4 == 0 && TX == 16, "tile shape");
@@ -273,6 +273,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_t(ConvArgs a, int tiles_x, int 
       for (int u = 0; u < RPW; ++u)
 #pragma unroll
         for (int rt = 0; rt < NRT; ++rt) acc[rt][u] = mfma16(wa[rt][kk], bv[u], acc[rt][u]);
+      if (kk % 10 == 9) __builtin_amdgcn_sched_barrier(0);  // bounds the LDS read hoisting (registers)
     }
     __syncthreads();  // every wave is done with the patch before the next one is stored
     // lane (j, g) holds out channel 16 rt + 4 g + r of output pixel (TY ty + RPW wave + u, TX tx + j)
@@ -1251,7 +1252,7 @@ int launch_conv(const ConvArgs& a, hipStream_t s, int img = 1, bool fin = true, 
     const int tiles_x = (a.OW + kCtTX - 1) / kCtTX, tps = tiles_x * ((a.OH + kCtTY - 1) / kCtTY);
     const long tiles = (long)a.n * tps;
     if (tiles < (1L << 31)) {
-      const int grid = (int)std::min<long>(tiles, 256L * 2);
+      const int grid = (int)std::min<long>(tiles, 256L * 3);  // three workgroups per CU (167 VGPRs)
       hipLaunchKernelGGL((k_conv_t<8, 16, kCtTY, kCtTX>), dim3(grid), dim3(256), 0, s, a, tiles_x, tps, (int)tiles);
       return 0;
     }

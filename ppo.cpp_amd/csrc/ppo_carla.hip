@@ -2980,7 +2980,9 @@ WgradPlan plan_wgrad(int OC, int Kt, long Q) {
   chunks = chunks < 1 ? 1 : (chunks > 4096 ? 4096 : chunks);
   const long cap = (32L << 20) / ((long)OC * (Kt + 1));  // partials <= 32 M floats
   if (chunks > cap) chunks = cap < 1 ? 1 : cap;
-  const long maxc = (Q + 15) / 16;
+  // at least 64 pixels / rows per chunk: the Linear layers (2 048 rows) then need <= 32 chunks and
+  // one k_wsum pass instead of k_wsum1 + k_wsum
+  const long maxc = (Q + 63) / 64;
   if (chunks > maxc) chunks = maxc < 1 ? 1 : maxc;
   p.qchunk = ((Q + chunks - 1) / chunks + 3) / 4 * 4;
   p.chunks = (int)((Q + p.qchunk - 1) / p.qchunk);

@@ -3015,7 +3015,7 @@ static size_t wimg2_lds_bytes(int IC, int K, int S, int OC) {
 // MFMAs per 32 pixel pairs instead of eight 32-cycle 16x16x4 f32 ones; lane group g's k slot e of
 // step q is pixel pair 32 q + 4 e + g (the f32 loop's step 8 q + e).
 template <int K, int S, bool BX = false>
-__global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, int tps, int tiles, int tpc) {
+__global__ __launch_bounds__(256, 3) void k_wgrad_img2(WgradArgs a, int tiles_x, int tps, int tiles, int tpc) {
   using G = ImgGeo<K, S>;
   constexpr int TI = G::TI, TIP = G::TIP, DW = TIP / 4, DZP = 260, KX = K + S, NC = 4 * kWimg2CT * 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -3043,29 +3043,49 @@ __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, in
   for (int u = 0; u < kWimg2CT; ++u) acc[u] = f4{0.f, 0.f, 0.f, 0.f};
   const size_t total_bytes = (size_t)a.n * a.x_stride;
   const int t0 = blockIdx.x * tpc, t1 = min(tiles, t0 + tpc);
-  for (int t = t0; t < t1; ++t) {
-    const int smp = t / tps, tt = t - smp * tps;
-    const int ty = tt / tiles_x, tx = tt - ty * tiles_x;
-    const int OH = a.OP / a.OW;
+  // staging (round 5): every load of a tile is issued at once into registers through buffer
+  // descriptors (out-of-range offsets read 0), then stored, so no load waits on the previous one's
+  // store (the loop form serialised ~27 load round trips per tile: 0.15 MFMA-pipe busy, 70 % of wave
+  // cycles waiting). Prefetching the next tile during the MFMAs instead took 268 VGPRs (92 now).
+  constexpr int NPE = (16 * TI * DW + 255) / 256, NZE = 8;  // launch condition: IC <= 16, OC <= 8
+  const int tot = a.IC * TI * DW, OH = a.OP / a.OW;
+  unsigned pv[NPE];
+  float zv[NZE];
+  auto sload = [&](int t) {
+    const int smp = t / tps, tt = t - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
     const int x0 = tx * kImgTile * S, y0 = ty * kImgTile * S;
+    const size_t sb = (size_t)smp * a.x_stride, left = total_bytes - sb;
+    const PBuf ib{__builtin_amdgcn_make_buffer_rsrc((void*)(a.x_u8 + sb), (short)0,
+                                                    (int)(left < 0xFFFFFFF0u ? left : 0xFFFFFFF0u), 0x00020000)};
+#pragma unroll
+    for (int i = 0; i < NPE; ++i) {
+      const int e = tid + 256 * i, ic = e / (TI * DW), rem = e - ic * (TI * DW), r = rem / DW, d = rem - r * DW;
+      const uint32_t off = e < tot ? (uint32_t)(ic * plane + (y0 + r) * a.IW + x0 + 4 * d) : 0xFFFFFFF0u;
+      pv[i] = __builtin_amdgcn_raw_buffer_load_b32(ib.r, off, 0, 0);
+    }
+    const PBuf zb{__builtin_amdgcn_make_buffer_rsrc((void*)(a.dz + (size_t)smp * a.dz_stride), (short)0,
+                                                    (int)(a.dz_stride * 4), 0x00020000)};
+#pragma unroll
+    for (int i = 0; i < NZE; ++i) {
+      const int e = tid + 256 * i, oc = e >> 8, px = e & 255, oy = ty * kImgTile + (px >> 4),
+                ox = tx * kImgTile + (px & 15);
+      const bool in = oc < OC && oy < OH && ox < a.OW;
+      const uint32_t off = in ? (uint32_t)(oc * a.OP + oy * a.OW + ox) * 4u : 0x7ffffff0u;
+      zv[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zb.r, off, 0, 0));
+    }
+  };
+  for (int t = t0; t < t1; ++t) {
+    sload(t);
     __syncthreads();  // the previous tile's readers are done
-    {
-      const size_t sb = (size_t)smp * a.x_stride, left = total_bytes - sb;
-      const PBuf ib{__builtin_amdgcn_make_buffer_rsrc((void*)(a.x_u8 + sb), (short)0,
-                                                      (int)(left < 0xFFFFFFF0u ? left : 0xFFFFFFF0u), 0x00020000)};
-      const int tot = a.IC * TI * DW;
-      for (int e = tid; e < tot; e += 256) {
-        const int ic = e / (TI * DW), rem = e - ic * (TI * DW), r = rem / DW, d = rem - r * DW;
-        const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(ib.r, ic * plane + (y0 + r) * a.IW + x0 + 4 * d, 0, 0);
-        *reinterpret_cast<unsigned*>(tile + (ic * TI + r) * TIP + 4 * d) = v;
-      }
-      const float* dz = a.dz + (size_t)smp * a.dz_stride;
-      for (int e = tid; e < OC * 256; e += 256) {
-        const int oc = e >> 8, px = e & 255, oy = ty * kImgTile + (px >> 4), ox = tx * kImgTile + (px & 15);
-        const bool in = oy < OH && ox < a.OW;
-        const float v = dz[in ? (size_t)oc * a.OP + oy * a.OW + ox : 0];
-        dzl[oc * DZP + px] = in ? v : 0.0f;
-      }
+#pragma unroll
+    for (int i = 0; i < NPE; ++i) {
+      const int e = tid + 256 * i, ic = e / (TI * DW), rem = e - ic * (TI * DW), r = rem / DW, d = rem - r * DW;
+      if (e < tot) *reinterpret_cast<unsigned*>(tile + (ic * TI + r) * TIP + 4 * d) = pv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NZE; ++i) {
+      const int e = tid + 256 * i;
+      if ((e >> 8) < OC) dzl[(e >> 8) * DZP + (e & 255)] = zv[i];
     }
     __syncthreads();
     if constexpr (BX) {
@@ -3173,7 +3193,7 @@ int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap
       wimg2_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {
     const int tiles_x = (a.OW + kImgTile - 1) / kImgTile, tiles_y = (OH + kImgTile - 1) / kImgTile;
     const int tiles = a.n * tiles_x * tiles_y;
-    int chunks = std::min(tiles, 1024);
+    int chunks = std::min(tiles, 768);  // three workgroups per CU (168 VGPRs): one round
     const int tpc = (tiles + chunks - 1) / chunks;
     chunks = (tiles + tpc - 1) / tpc;
     const int groups = (chunks + kSumGroup - 1) / kSumGroup;

@@ -3015,7 +3015,7 @@ static size_t wimg2_lds_bytes(int IC, int K, int S, int OC) {
 // MFMAs per 32 pixel pairs instead of eight 32-cycle 16x16x4 f32 ones; lane group g's k slot e of
 // step q is pixel pair 32 q + 4 e + g (the f32 loop's step 8 q + e).
 template <int K, int S, bool BX = false>
-__global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, int tps, int tiles, int tpc) {
+__global__ __launch_bounds__(256, 3) void k_wgrad_img2(WgradArgs a, int tiles_x, int tps, int tiles, int tpc) {
   using G = ImgGeo<K, S>;
   constexpr int TI = G::TI, TIP = G::TIP, DW = TIP / 4, DZP = 260, KX = K + S, NC = 4 * kWimg2CT * 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -3052,10 +3052,6 @@ __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, in
   unsigned pv[NPE];
   float zv[NZE];
   auto sload = [&](int t) {
-    // an opaque copy of the thread index: the per-element offsets are recomputed per tile instead of
-    // being hoisted out of the tile loop (40 more live VGPRs, two waves per SIMD fewer)
-    int tidv = tid;
-    asm volatile("" : "+v"(tidv));
     const int smp = t / tps, tt = t - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
     const int x0 = tx * kImgTile * S, y0 = ty * kImgTile * S;
     const size_t sb = (size_t)smp * a.x_stride, left = total_bytes - sb;
@@ -3063,7 +3059,7 @@ __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, in
                                                     (int)(left < 0xFFFFFFF0u ? left : 0xFFFFFFF0u), 0x00020000)};
 #pragma unroll
     for (int i = 0; i < NPE; ++i) {
-      const int e = tidv + 256 * i, ic = e / (TI * DW), rem = e - ic * (TI * DW), r = rem / DW, d = rem - r * DW;
+      const int e = tid + 256 * i, ic = e / (TI * DW), rem = e - ic * (TI * DW), r = rem / DW, d = rem - r * DW;
       const uint32_t off = e < tot ? (uint32_t)(ic * plane + (y0 + r) * a.IW + x0 + 4 * d) : 0xFFFFFFF0u;
       pv[i] = __builtin_amdgcn_raw_buffer_load_b32(ib.r, off, 0, 0);
     }
@@ -3071,7 +3067,7 @@ __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, in
                                                     (int)(a.dz_stride * 4), 0x00020000)};
 #pragma unroll
     for (int i = 0; i < NZE; ++i) {
-      const int e = tidv + 256 * i, oc = e >> 8, px = e & 255, oy = ty * kImgTile + (px >> 4),
+      const int e = tid + 256 * i, oc = e >> 8, px = e & 255, oy = ty * kImgTile + (px >> 4),
                 ox = tx * kImgTile + (px & 15);
       const bool in = oc < OC && oy < OH && ox < a.OW;
       const uint32_t off = in ? (uint32_t)(oc * a.OP + oy * a.OW + ox) * 4u : 0x7ffffff0u;
@@ -3081,16 +3077,14 @@ __global__ __launch_bounds__(256) void k_wgrad_img2(WgradArgs a, int tiles_x, in
   for (int t = t0; t < t1; ++t) {
     sload(t);
     __syncthreads();  // the previous tile's readers are done
-    int tids = tid;
-    asm volatile("" : "+v"(tids));
 #pragma unroll
     for (int i = 0; i < NPE; ++i) {
-      const int e = tids + 256 * i, ic = e / (TI * DW), rem = e - ic * (TI * DW), r = rem / DW, d = rem - r * DW;
+      const int e = tid + 256 * i, ic = e / (TI * DW), rem = e - ic * (TI * DW), r = rem / DW, d = rem - r * DW;
       if (e < tot) *reinterpret_cast<unsigned*>(tile + (ic * TI + r) * TIP + 4 * d) = pv[i];
     }
 #pragma unroll
     for (int i = 0; i < NZE; ++i) {
-      const int e = tids + 256 * i;
+      const int e = tid + 256 * i;
       if ((e >> 8) < OC) dzl[(e >> 8) * DZP + (e & 255)] = zv[i];
     }
     __syncthreads();
@@ -3199,7 +3193,7 @@ int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap
       wimg2_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {
     const int tiles_x = (a.OW + kImgTile - 1) / kImgTile, tiles_y = (OH + kImgTile - 1) / kImgTile;
     const int tiles = a.n * tiles_x * tiles_y;
-    int chunks = std::min(tiles, 1280);  // five workgroups per CU (100 VGPRs, 27 KB LDS): one round
+    int chunks = std::min(tiles, 768);  // three workgroups per CU (168 VGPRs): one round
     const int tpc = (tiles + chunks - 1) / chunks;
     chunks = (tiles + tpc - 1) / tpc;
     const int groups = (chunks + kSumGroup - 1) / kSumGroup;

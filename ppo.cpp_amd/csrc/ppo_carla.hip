@@ -2475,7 +2475,7 @@ struct WtGeo {
   static_assert(PW >= PWL && PW % 16 == 5 && RED <= NXP, "layout");
 };
 template <int IC, int OC, int TY, int TX>
-__global__ __launch_bounds__(256, 2) void k_wgrad_t(WgradArgs a, int tiles_x, int tps, int tiles) {
+__global__ __launch_bounds__(256, 3) void k_wgrad_t(WgradArgs a, int tiles_x, int tps, int tiles) {
   using G = WtGeo<IC, OC, TY, TX>;
   constexpr int Kt = G::Kt, NCT = G::NCT, NRT = G::NRT, PW = G::PW, PWL = G::PWL, PPA = G::PPA, TQ = G::TQ,
                 DZS = G::DZS, RPW = G::RPW, KS = G::KS, S = G::S;
@@ -2501,6 +2501,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_t(WgradArgs a, int tiles_x, in
   const int OH = a.OP / a.OW;
   float sx[NSX], sz[NSZ];
   auto sload = [&](int tile) {
+    int tidv = tid;  // opaque: the per-element offsets are recomputed per tile, not hoisted (registers)
+    asm volatile("" : "+v"(tidv));
     const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
     const PBuf xb{__builtin_amdgcn_make_buffer_rsrc((void*)(a.x_f + (size_t)smp * a.x_stride), (short)0,
                                                     (int)(a.x_stride * 4), 0x00020000)};
@@ -2509,7 +2511,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_t(WgradArgs a, int tiles_x, in
     const int iy0 = S * TY * ty, ix0 = S * TX * tx, oy0 = TY * ty, ox0 = TX * tx;
 #pragma unroll
     for (int i = 0; i < NSX; ++i) {
-      const int e = tid + 256 * i, ic = e / PPA, rem = e - ic * PPA, r = rem / PW, c = rem - r * PW;
+      const int e = tidv + 256 * i, ic = e / PPA, rem = e - ic * PPA, r = rem / PW, c = rem - r * PW;
       const int iy = iy0 + r, ix = ix0 + c;
       const bool in = e < NXP && r < G::PH && c < PWL && iy < a.IH && ix < a.IW;
       const uint32_t off = in ? (uint32_t)(ic * plane + iy * a.IW + ix) * 4u : 0x7ffffff0u;
@@ -2517,7 +2519,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_t(WgradArgs a, int tiles_x, in
     }
 #pragma unroll
     for (int i = 0; i < NSZ; ++i) {
-      const int e = tid + 256 * i, oc = e / DZS, q = e - oc * DZS, oy = oy0 + q / TX, ox = ox0 + q % TX;
+      const int e = tidv + 256 * i, oc = e / DZS, q = e - oc * DZS, oy = oy0 + q / TX, ox = ox0 + q % TX;
       const bool in = e < NZP && q < TQ && oy < OH && ox < a.OW;
       const uint32_t off = in ? (uint32_t)(oc * a.OP + oy * a.OW + ox) * 4u : 0x7ffffff0u;
       sz[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zb.r, off, 0, 0));
@@ -2595,7 +2597,7 @@ struct Wt2Geo {
   static_assert(PW >= PWL && PPA >= PH * PW && TX % 4 == 0 && OC % 16 == 0, "layout");
 };
 template <int IC, int OC, int TY, int TX>
-__global__ __launch_bounds__(256, 2) void k_wgrad_t2(WgradArgs a, int tiles_x, int tps, int tiles) {
+__global__ __launch_bounds__(256, 4) void k_wgrad_t2(WgradArgs a, int tiles_x, int tps, int tiles) {
   using G = Wt2Geo<IC, OC, TY, TX>;
   constexpr int Kt = G::Kt, NCT = G::NCT, NCW = G::NCW, NRT = G::NRT, PW = G::PW, PWL = G::PWL, PPA = G::PPA,
                 TQ = G::TQ, DZS = G::DZS, KS = G::KS, S = G::S, NXP = G::NXP, NZP = G::NZP;
@@ -2616,6 +2618,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_t2(WgradArgs a, int tiles_x, i
   const int OH = a.OP / a.OW;
   float sx[NSX], sz[NSZ];
   auto sload = [&](int tile) {
+    int tidv = tid;  // opaque: the per-element offsets are recomputed per tile, not hoisted (registers)
+    asm volatile("" : "+v"(tidv));
     const int smp = tile / tps, tt = tile - smp * tps, ty = tt / tiles_x, tx = tt - ty * tiles_x;
     const PBuf xb{__builtin_amdgcn_make_buffer_rsrc((void*)(a.x_f + (size_t)smp * a.x_stride), (short)0,
                                                     (int)(a.x_stride * 4), 0x00020000)};
@@ -2624,7 +2628,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_t2(WgradArgs a, int tiles_x, i
     const int iy0 = S * TY * ty, ix0 = S * TX * tx, oy0 = TY * ty, ox0 = TX * tx;
 #pragma unroll
     for (int i = 0; i < NSX; ++i) {
-      const int e = tid + 256 * i, ic = e / PPA, rem = e - ic * PPA, r = rem / PW, c = rem - r * PW;
+      const int e = tidv + 256 * i, ic = e / PPA, rem = e - ic * PPA, r = rem / PW, c = rem - r * PW;
       const int iy = iy0 + r, ix = ix0 + c;
       const bool in = e < NXP && r < G::PH && c < PWL && iy < a.IH && ix < a.IW;
       const uint32_t off = in ? (uint32_t)(ic * plane + iy * a.IW + ix) * 4u : 0x7ffffff0u;
@@ -2632,7 +2636,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_t2(WgradArgs a, int tiles_x, i
     }
 #pragma unroll
     for (int i = 0; i < NSZ; ++i) {
-      const int e = tid + 256 * i, oc = e / DZS, q = e - oc * DZS, oy = oy0 + q / TX, ox = ox0 + q % TX;
+      const int e = tidv + 256 * i, oc = e / DZS, q = e - oc * DZS, oy = oy0 + q / TX, ox = ox0 + q % TX;
       const bool in = e < NZP && q < TQ && oy < OH && ox < a.OW;
       const uint32_t off = in ? (uint32_t)(oc * a.OP + oy * a.OW + ox) * 4u : 0x7ffffff0u;
       sz[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(zb.r, off, 0, 0));
@@ -3167,7 +3171,8 @@ int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap
     const int TY = c2 ? kWtTY : kWt2TY, TX = c2 ? kWtTX : kWt2TX;
     const int tiles_x = (a.OW + TX - 1) / TX, tps = tiles_x * ((OH + TY - 1) / TY);
     const long tiles = (long)a.n * tps;
-    const int chunks = (int)std::min<long>(tiles, 1024);
+    // one round of resident workgroups: k_wgrad_t three per CU (137 VGPRs), k_wgrad_t2 four (112)
+    const int chunks = (int)std::min<long>(tiles, c2 ? 768 : 1024);
     const int groups = (chunks + kSumGroup - 1) / kSumGroup;
     if (tiles < (1L << 31) && (size_t)(chunks + (chunks > kSumGroup ? groups : 0)) * per <= part_cap) {
       a.part = part;

@@ -164,6 +164,40 @@ def cli_sps(E, T, iterations):
         return None
 
 
+FP32_OPTIONS = "upd_mfma=16,dw_mfma=f32"
+
+
+def fp32_leg(cfg, E, args, work):
+    """The bench workload again with every update GEMM on fp32 MFMAs (v_mfma_f32_16x16x4_f32: the
+    LibTorch kFloat32 arithmetic of ac:816-888 without split-bf16 piece products), same warmup and
+    timing as the headline; reported beside it, never as `value`."""
+    opts = FP32_OPTIONS if not args.options else args.options + "," + FP32_OPTIONS
+    tr = ppo_amd.Trainer(cfg, num_envs_per_device=E, rank=0, world_size=1, device=0, options=opts)
+    try:
+        for _ in range(args.warmup):
+            tr.iterate()
+        tr.agent.sync()
+        tr.agent.profile_reset()
+        tr.agent.profile(1 << 1)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            tr.iterate()
+        tr.agent.sync()
+        el = time.perf_counter() - t0
+        tr.agent.profile(0)
+        prof = tr.agent.profile_read()
+        res = {"options": opts, "kernels": tr.agent.kernel_info(), "steps": args.steps,
+               "value": round(E * cfg.num_steps * args.steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 3)}
+        if prof and "fwdbwd" in prof:
+            ms, cnt = prof["fwdbwd"]
+            tf = work["fwdbwd"][1] / (ms / 1e3 / cnt) / 1e12
+            res["fwdbwd"] = {"avg_launch_ms": round(ms / cnt, 4), "achieved": round(tf, 3),
+                             "frac": round(tf / PEAK_F32_MFMA_TFLOPS, 4)}
+        return res
+    finally:
+        tr.close()
+
+
 def free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -200,6 +234,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-all", action="store_true", help="HIP-event time every kernel class")
     ap.add_argument("--no-cli", action="store_true", help="skip the ac_ppo_continuous_action CLI SPS run")
+    ap.add_argument("--no-fp32-leg", action="store_true",
+                    help="skip the second timed run with every GEMM on fp32 MFMAs (upd_mfma=16,dw_mfma=f32)")
     ap.add_argument("--cli-iterations", type=int, default=30)
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                     help="N > 1 data path: RCCL (one GPU per rank), or the host transport over gloo with every "
@@ -299,6 +335,17 @@ def main():
 
     units = E_total * T * args.steps
     value = units / elapsed
+    dw_prof = None
+    if world == 1 and not args.profile_all:
+        # dW's own fraction beside k_upd's: a few iterations after the timed region with HIP events
+        # around the dW launches too (kept out of the timed region so it carries one event class only)
+        tr.agent.profile_reset()
+        tr.agent.profile((1 << 1) | (1 << 2))
+        for _ in range(min(args.steps, 4)):
+            tr.iterate()
+        tr.agent.sync()
+        tr.agent.profile(0)
+        dw_prof = tr.agent.profile_read()
     if rank == 0:
         H, O_, A = 256, 17, 6
         work = algorithmic_work(O_, A, H, E, T, cfg.num_minibatches, 2 * A)
@@ -332,16 +379,35 @@ def main():
                 try:
                     tj = json.load(open(pmc))
                     if name in tj and tj[name].get("config") == f"E={E},T={T}":
+                        # PMC counters cannot run inside the timed region: the bytes come from the two
+                        # rocprofv3 passes (FETCH_SIZE, WRITE_SIZE) of this bench command named here
                         roof["traffic"] = tj[name]["hbm_bytes_per_launch"]
+                        roof["traffic_source"] = tj.get("_source", "profiles/pmc_traffic.json")
+                        if "dw" in tj and tj["dw"].get("config") == f"E={E},T={T}":
+                            roof["traffic_dw"] = tj["dw"]["hbm_bytes_per_launch"]
                 except Exception:  # noqa: BLE001
                     pass
+        src = dw_prof or prof
+        if roof is not None and src and "dw" in src:
+            ms, cnt = src["dw"]
+            dw_tf = work["dw"][1] / (ms / 1e3 / cnt) / 1e12
+            roof["dw"] = {"kernel": kinfo.split("dw=")[-1] if "dw=" in kinfo else "dw", "avg_launch_ms": round(ms / cnt, 4),
+                          "launches": cnt, "achieved": round(dw_tf, 3), "frac": round(dw_tf / PEAK_F32_MFMA_TFLOPS, 4),
+                          "algorithmic_per_launch": work["dw"][1],
+                          "timing": "HIP events on the context stream, iterations after the timed region"}
+            if "bf16x6" in kinfo:  # every dW product is six bf16 piece products: 2.5 PF/s / 6
+                roof["dw"]["peak_instruction_mix"] = round(PEAK_BF16_MFMA_TFLOPS / 6, 1)
+                roof["dw"]["frac_instruction_mix"] = round(dw_tf / (PEAK_BF16_MFMA_TFLOPS / 6), 4)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
-            "dtype_note": ("fp32 arithmetic; the update's fp32 GEMMs run as exact split-bf16 piece products on bf16 "
-                           "MFMAs with fp32 accumulation (DESIGN.md 3c; upd_mfma=16,dw_mfma=f32 for fp32 MFMAs), "
-                           "tested as exact as the fp32 MFMA form against the fp64 oracle"),
+            "dtype_note": ("fp32 operands and fp32 accumulation; the update's 256-wide GEMMs and dW run each fp32 "
+                           "product as six of its nine split-bf16 piece products on bf16 MFMAs (the dropped "
+                           "mid*lo + lo*mid + lo*lo are < ~2^-21 of the product; DESIGN.md 3c), tested within 1.5x "
+                           "of the fp32 MFMA form's distance from the fp64 oracle; results differ bitwise from the "
+                           "fp32 MFMA form. fp32 MFMAs throughout: options upd_mfma=16,dw_mfma=f32 (the fp32_mfma "
+                           "leg below)"),
             "data": "synthetic: device-resident HalfCheetah-shaped env (O=17, A=6), random-init AC agent",
             "config": {"workload": f"ac_ppo_continuous_action HalfCheetah-v5 num_envs={E_total} num_steps={T} "
                                    f"num_minibatches={cfg.num_minibatches} update_epochs={cfg.update_epochs}",
@@ -355,12 +421,21 @@ def main():
         }
         if args.profile_all:
             out["kernels_ms_per_step"] = {k: round(v[0] / args.steps, 3) for k, v in prof.items()}
+            out["kernels_ms_note"] = ("HIP-event pairs around every kernel class: the sum can exceed ms_per_step "
+                                      "(each pair adds its own overhead to the class it brackets)")
+    if world == 1 and not args.no_fp32_leg:
+        # the same workload with every GEMM on fp32 MFMAs (no split-bf16 piece products)
+        tr.close()
+        tr = None
+        out["fp32_mfma"] = fp32_leg(cfg, E, args, algorithmic_work(17, 6, 256, E, T, cfg.num_minibatches, 12))
+    if rank == 0:
         if world == 1 and not args.no_cli:
             out["cli_value"] = cli_sps(E_total, T, args.cli_iterations)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(E, T, cfg.num_minibatches, cfg.update_epochs)
         print(json.dumps(out), flush=True)
-    tr.close()
+    if tr is not None:
+        tr.close()
     if dist:
         dist.destroy_process_group()
 

@@ -147,7 +147,11 @@ int ppo_carla_create(const ppo_carla_config* cfg, int device, ppo_carla_t** out)
  *   tail=staged|fused|layers   forwards of n <= 64 rows: the MLP tail after the CNN as one launch per
  *                              dependency stage (default), one cooperative launch with a grid barrier
  *                              between stages, or one k_conv / k_conv_fin pair per layer (the path of
- *                              larger batches); bitwise equal */
+ *                              larger batches); bitwise equal
+ *   wgrad_group_bytes=N        (tests) the generic fp32 weight-gradient kernel runs its samples in groups
+ *                              whose input stays below N bytes, each group's sums added to the previous
+ *                              ones'; without it the groups start at 0x70000000 bytes (the kernel's 32-bit
+ *                              buffer offsets), so no batch size is refused */
 int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, const char* options, ppo_carla_t** out);
 int ppo_carla_destroy(ppo_carla_t* c);
 int ppo_carla_get_layout(const ppo_carla_t* c, ppo_carla_layout* out);

@@ -83,8 +83,10 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  * defaults ppo_create uses). Every choice is a complete, tested kernel path; results differ only in
  * summation order (A/B comparisons, tests). Split-bf16 forms: every fp32 operand x is the exact sum
  * of three bf16 pieces (hi = x truncated to bf16, mid = (x - hi) truncated, lo = the rest), so an
- * fp32 product is a sum of exact piece products, accumulated in fp32 on the bf16 MFMA (16x the fp32
- * MFMA rate); the fp32 math of the reference, not a reduced-precision variant of it:
+ * fp32 product is the sum of nine exact piece products, accumulated in fp32 on the bf16 MFMA (16x
+ * the fp32 MFMA rate). The default forms keep six of the nine (the dropped mid*lo + lo*mid + lo*lo are
+ * < ~2^-21 |ab|) with fp32 accumulation: tested within 1.5x of the fp32 MFMA form's distance from the
+ * fp64 oracle, and not bitwise equal to the fp32 MFMA form (upd_mfma=16,dw_mfma=f32 selects it):
  *   upd_kernel=auto|fwdbwd   minibatch forward/backward: the feature-split k_upd / k_upd2 (auto) or
  *                            the wave-per-16-rows k_fwdbwd
  *   act_kernel=auto|2|4      64-wide agent act: by shape (auto), k_act2, or k_act4
@@ -119,9 +121,10 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            workgroup, MFMA) or k_rollout_v (2 envs per workgroup, VALU; O <= 32);
  *                            auto: k_rollout_v at E <= 512. Bitwise the same results. valu on an
  *                            agent it cannot serve (the PPO agent, O > 32, device env wrappers) fails
- *   gae=serial|scan          GAE as the reference's serial recurrence per env (k_gae, default: bit-exact
- *                            with ppo:447-467, ac:759-779) or as a segmented scan over the steps (k_gae_scan: 16
- *                            segments per 64 envs, within fp32 rounding of the serial form)
+ *   gae=auto|serial|scan     GAE as the reference's serial recurrence per env (k_gae: bit-exact with
+ *                            ppo:447-467, ac:759-779) or as a segmented scan over the steps (k_gae_scan: 16
+ *                            segments per 64 envs, within 1e-5 of the serial form and of the golden
+ *                            vectors); auto: the scan from 512 steps (cfg1 / cfg2's T = 2 048), serial below
  *   gradstep=split|fused     clip_grad_norm_ + Adam: two launches (k_gradnorm, k_adam; default) or
  *                            one cooperative launch (k_gradstep: slower on ROCm 7, whose cooperative
  *                            launch costs ~30 us); bitwise the same

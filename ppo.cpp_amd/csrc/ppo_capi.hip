@@ -155,7 +155,7 @@ struct ppo_ctx {
   bool use_upd = false;  // feature-split k_upd (ppo_update.hip) instead of k_fwdbwd
   bool use_upd32 = false;  // k_upd32 (32x32x2 MFMAs) instead of k_upd (create option upd_mfma)
   int upd_bx = 0;          // 1: k_upd's 256-wide GEMMs as split-bf16 piece products (upd_mfma=bx6)
-  int gae_scan = 0;        // 1: GAE as k_gae_scan (create option gae=scan); 0: the bit-exact serial k_gae
+  int gae_scan = -1;       // 1: GAE as k_gae_scan (create option gae=scan); 0: the bit-exact serial k_gae; -1 auto
   int upd32_mix = 0;       // k_upd32 with the actor trunk on k_upd's body (upd_mfma=mix)
   bool use_upd2 = false;  // two-trunk k_upd2 (ppo_update_narrow.hip, H = 64 tanh agent)
   int rollout_kernel = 0;   // AC persistent rollout: 0 auto, 1 k_rollout (MFMA), 2 k_rollout_v (VALU)
@@ -282,7 +282,7 @@ struct CreateOptions {
   int dw_slices = 0;   // k_dwf output slices per chunk (1 / 2; 0: auto, dw_slices())
   int dw_dma = 1;      // 1 (default): k_dwf_dma (LDS-DMA staging, three stage buffers); 0: k_dwf
   int dw_bx = -1;      // dw_mfma: -1 auto, 0 f32 (fp32 MFMA), 9 / 8 / 6 bf16x9 / x8 / x6 (k_dwf_bx: exact bf16 splits)
-  int gae_scan = 0;    // gae=serial (default, bit-exact with the reference's loop) | scan (k_gae_scan)
+  int gae_scan = -1;   // gae=auto (scan from kGaeScanMinT steps) | serial (bit-exact with the reference's loop) | scan
   // 1: ppo_update replays its minibatch launches as one captured hipGraph; 0 (default): eager.
   // Snapshots work with it on (ppo_read_snapshot waits for the snapshot's event on the host).
   int update_graph = 0;
@@ -308,6 +308,11 @@ static constexpr int kDwBxAuto = 6;
 static constexpr int kUpdBxAuto = 1;
 // upd_mfma=auto for the 64-wide agent: k_upd2's layer 1 as split-bf16 piece products where instantiated
 static constexpr int kUpd2BxAuto = 1;
+// gae=auto: k_gae_scan from this many steps on (cfg1 / cfg2's T = 2 048: 16 segments per env; within
+// 1e-5 of the serial recurrence and of the golden vectors, test_gae_scan_vs_golden), the bit-exact serial
+// k_gae below it (the metric's T = 128: 13 us, < 0.1 % of the iteration). cfg2: 0.186 -> 0.107 ms
+// (profiles/r05/gae_scan/)
+static constexpr int kGaeScanMinT = 512;
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
   std::string s(opts);
@@ -332,7 +337,7 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
       o->dw_rows = atoi(v.c_str());  // at most 5 digits: no overflow, no exception across the C-ABI
     else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
     else if (k == "dw_dma" && (v == "0" || v == "1")) o->dw_dma = v[0] - '0';
-    else if (k == "gae" && (v == "serial" || v == "scan")) o->gae_scan = v == "scan";
+    else if (k == "gae" && (v == "auto" || v == "serial" || v == "scan")) o->gae_scan = v == "auto" ? -1 : v == "scan";
     else if (k == "dw_mfma" && (v == "auto" || v == "f32" || v == "bf16x9" || v == "bf16x8" || v == "bf16x6"))
       o->dw_bx = v == "auto" ? -1 : v == "f32" ? 0 : v == "bf16x9" ? 9 : v == "bf16x8" ? 8 : 6;
     else if (k == "update_graph" && (v == "0" || v == "1")) o->update_graph = v[0] - '0';
@@ -817,7 +822,7 @@ static int gae_launch(ppo_t* c, const float* next_value, const float* next_done,
   g.gamma = c->cfg.gamma;
   g.lam = c->cfg.gae_lambda;
   ProfScope ps(c, PK_GAE, s);
-  launch_gae(g, s, c->gae_scan != 0);
+  launch_gae(g, s, c->gae_scan > 0 || (c->gae_scan < 0 && nsteps >= kGaeScanMinT));
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -647,7 +647,10 @@ struct Img3Geo {
   static constexpr int TW = (kImg2W - 1) * S + K;            // patch columns used by real taps
   static constexpr int TIP = ((2 * S * (kImg2W / 2 - 1) + kImg3KX) + 3) & ~3;  // incl. the padding tap
 };
-__host__ __device__ inline int img3_blocks(int IC, int K) { return (IC * K + 1) / 2; }
+// 16-tap A blocks of the packed table (two kernel rows each), rounded up to an even count: the BX loop
+// reads blocks in pairs (2 kk, 2 kk + 1), so an odd IC * K / 2 (e.g. obs_num_channels 1, 5, 9, 13) gets
+// a zero block (k_conv1_wprep writes 0 for rows past IC * K; a zero weight adds exactly 0)
+__host__ __device__ inline int img3_blocks(int IC, int K) { return (((IC * K + 1) / 2) + 1) & ~1; }
 static size_t img3_lds_bytes(int IC, int K, int S) {
   const int TI = (kImgTile - 1) * S + K, TIP = ((2 * S * (kImg2W / 2 - 1) + kImg3KX) + 3) & ~3;
   return ((size_t)IC * TI * TIP + 15) & ~(size_t)15;
@@ -1222,17 +1225,18 @@ int launch_conv(const ConvArgs& a, hipStream_t s, int img = 1, bool fin = true, 
     const int tiles = ((a.OW + kImg2W - 1) / kImg2W) * ((a.OH + kImgTile - 1) / kImgTile) * a.n;
     const int grid = std::min(tiles, kImg3WG), tpc = (tiles + grid - 1) / grid;
     const size_t lds = img3_patch_bytes(a.IC, a.K, a.S) + (size_t)nblk * 256 * sizeof(float);
+    // the launch condition caps lds at 80 KB: allow that once for every later context and channel count
     static const bool attr =
-        hipFuncSetAttribute((const void*)k_conv_img3<5, 2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) ==
-            hipSuccess &&
-        hipFuncSetAttribute((const void*)k_conv_img3<5, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) ==
-            hipSuccess;
+        hipFuncSetAttribute((const void*)k_conv_img3<5, 2, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            80 * 1024) == hipSuccess &&
+        hipFuncSetAttribute((const void*)k_conv_img3<5, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            80 * 1024) == hipSuccess;
     if (!attr) return -2;
     if (a.bx)
       hipLaunchKernelGGL((k_conv_img3<5, 2, true>), dim3((tiles + tpc - 1) / tpc), dim3(256), lds, s, a, tiles, tpc);
     else
       hipLaunchKernelGGL((k_conv_img3<5, 2, false>), dim3((tiles + tpc - 1) / tpc), dim3(256), lds, s, a, tiles, tpc);
-    return 0;
+    return hipGetLastError() == hipSuccess ? 0 : -2;
   }
   if (img && a.in_u8 && ((uintptr_t)a.in_u8 & 3) == 0 && a.K == 5 && a.S == 2 && a.OC <= 8 && a.IW % 4 == 0 &&
       a.in_stride % 4 == 0 && a.OH <= 16 * 64 && img2_lds_bytes(a.IC, a.K, a.S, a.OC) <= 64 * 1024) {
@@ -1341,6 +1345,9 @@ struct ppo_carla {
   int conv_t = kConvTiledAuto;
   // conv6's input gradient: 1 dense GEMM + col2im (create option deep_dgrad=col|gather)
   int dgrad_col = kDgradColAuto;
+  // create option wgrad_group_bytes (tests): the generic fp32 k_wgrad runs its samples in groups whose
+  // input stays below this many bytes (0: kWgradFar, the limit of its 32-bit buffer offsets)
+  long wgrad_group = 0;
   float *dcol = nullptr, *wt = nullptr, *zbias = nullptr;  // carla_train_init
   float* c1w = nullptr;  // k_conv_img3's A-operand table
   // MLP tail for n <= kTailMaxN: 1 (default) one launch per stage, 0 one cooperative launch (a grid
@@ -1392,6 +1399,7 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
   int wgrad_t = kWgradTiledAuto;
   int conv_t = kConvTiledAuto;
   int dgrad_col = kDgradColAuto;
+  long wgrad_group = 0;
   if (options && *options) {  // comma-separated key=value
     std::string rest(options);
     while (!rest.empty()) {
@@ -1419,6 +1427,9 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
       else if (o == "deep_dgrad=col") dgrad_col = 1;
       else if (o == "deep_dgrad=gather") dgrad_col = 0;
       else if (o == "deep_dgrad=auto") dgrad_col = kDgradColAuto;
+      else if (o.rfind("wgrad_group_bytes=", 0) == 0 && o.size() > 18 && o.size() <= 28 &&
+               o.find_first_not_of("0123456789", 18) == std::string::npos)
+        wgrad_group = atol(o.c_str() + 18);
       else return ppo_fail("ppo_carla_create_ex: unknown option " + o, -1);
     }
   }
@@ -1443,6 +1454,7 @@ extern "C" int ppo_carla_create_ex(const ppo_carla_config* cfg, int device, cons
   c->wgrad_t = wgrad_t;
   c->conv_t = conv_t;
   c->dgrad_col = dgrad_col;
+  c->wgrad_group = wgrad_group;
 #ifdef PPO_DIAG
   if (const char* e = getenv("PPO_CARLA_CONV1")) c->conv_img = e[0] - '0';
 #endif
@@ -2174,9 +2186,11 @@ struct WgradArgs {
   int n, Kt;     // Kt = IC*K*K; column Kt is the bias (x = 1)
   long qchunk;   // output pixels per chunk (multiple of 4)
   float* part;   // [chunks][OC][Kt + 1]
+  long group_bytes = 0;  // host only: launch_wgrad_generic's sample-group limit (0: kWgradFar)
 };
 
 constexpr int kMaxPTab = 9216;  // output pixels per sample (94 x 94 = 8836 for conv1)
+constexpr uint32_t kWgradFar = 0x70000000u;  // k_wgrad's out-of-range byte offset (fp32 inputs stay below it)
 
 template <int NOT, int NKT, bool U8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) void k_wgrad(WgradArgs a) {
@@ -2223,7 +2237,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
   // the buffer for the bias / padding columns) plus the pixel's byte offset xb4 (also far past the
   // buffer for pixels past the chunk), so a column reads 0 out of range instead of through a select
   // and 64-bit address arithmetic (round 5: 15 VALU per MFMA before, SQ counters)
-  constexpr uint32_t kFar = 0x70000000u;
+  constexpr uint32_t kFar = kWgradFar;
   uint32_t ko4[NKT];
 #pragma unroll
   for (int u = 0; u < NKT; ++u) ko4[u] = kc[u] == 0 ? (uint32_t)ko[u] * 4u : kFar;
@@ -2700,15 +2714,15 @@ __global__ void k_wsum1(const float* __restrict__ part, int chunks, long per, fl
 }
 
 __global__ void k_wsum(const float* __restrict__ part, int chunks, int OC, int Kt, float* __restrict__ Gw,
-                       float* __restrict__ Gb) {
+                       float* __restrict__ Gb, int accum) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long per = (long)OC * (Kt + 1);
   if (i >= per) return;
   float acc = 0.f;
   for (int c = 0; c < chunks; ++c) acc += part[(long)c * per + i];
   const int oc = (int)(i / (Kt + 1)), k = (int)(i - (long)oc * (Kt + 1));
-  if (k < Kt) Gw[(long)oc * Kt + k] = acc;
-  else Gb[oc] = acc;
+  float* o = k < Kt ? Gw + (long)oc * Kt + k : Gb + oc;
+  *o = accum ? *o + acc : acc;  // accum: a later sample group of launch_wgrad's split
 }
 
 // the same statistics in the distributed order of ac_ppo_carla.cpp:561-580, one block each:
@@ -3160,10 +3174,11 @@ __global__ __launch_bounds__(256, 3) void k_wgrad_img2(WgradArgs a, int tiles_x,
   }
 }
 
+static int launch_wgrad_generic(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap, hipStream_t s,
+                                int accum = 0);
 int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap, hipStream_t s, bool img = true,
                  bool bx = false, bool tiled = false) {
   if (a.Kt > kMaxKTab || a.OP > kMaxPTab) return -1;
-  if (!a.x_u8 && (long)a.n * a.x_stride * 4 >= 0x70000000L) return -1;  // k_wgrad's 32-bit buffer offsets
   const long per = (long)a.OC * (a.Kt + 1);
   const int OH = a.OP / a.OW;
   const bool c2 = a.IC == 8 && a.OC == 16, c3 = a.IC == 16 && a.OC == 32;
@@ -3185,9 +3200,9 @@ int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap
       if (chunks > kSumGroup) {
         float* lvl = part + (size_t)chunks * per;
         hipLaunchKernelGGL(k_wsum1, dim3(gb, groups), dim3(256), 0, s, part, chunks, per, lvl);
-        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, lvl, groups, a.OC, a.Kt, Gw, Gb);
+        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, lvl, groups, a.OC, a.Kt, Gw, Gb, 0);
       } else {
-        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, part, chunks, a.OC, a.Kt, Gw, Gb);
+        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, part, chunks, a.OC, a.Kt, Gw, Gb, 0);
       }
       return 0;
     }
@@ -3214,9 +3229,9 @@ int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap
       if (chunks > kSumGroup) {
         float* lvl = part + (size_t)chunks * per;
         hipLaunchKernelGGL(k_wsum1, dim3(gb, groups), dim3(256), 0, s, part, chunks, per, lvl);
-        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, lvl, groups, a.OC, a.Kt, Gw, Gb);
+        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, lvl, groups, a.OC, a.Kt, Gw, Gb, 0);
       } else {
-        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, part, chunks, a.OC, a.Kt, Gw, Gb);
+        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, part, chunks, a.OC, a.Kt, Gw, Gb, 0);
       }
       return 0;
     }
@@ -3239,13 +3254,35 @@ int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap
       if (chunks > kSumGroup) {
         float* lvl = part + (size_t)chunks * per;
         hipLaunchKernelGGL(k_wsum1, dim3(gb, groups), dim3(256), 0, s, part, chunks, per, lvl);
-        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, lvl, groups, a.OC, a.Kt, Gw, Gb);
+        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, lvl, groups, a.OC, a.Kt, Gw, Gb, 0);
       } else {
-        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, part, chunks, a.OC, a.Kt, Gw, Gb);
+        hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, part, chunks, a.OC, a.Kt, Gw, Gb, 0);
       }
       return 0;
     }
   }
+  return launch_wgrad_generic(a, Gw, Gb, part, part_cap, s);
+}
+
+// the generic gather kernel k_wgrad (+ its chunk sums). Its fp32 gathers use 32-bit buffer offsets
+// over the whole input, so an input of >= 0x70000000 bytes runs as consecutive sample groups below
+// that size, each group's sums added to the previous ones' (accum)
+static int launch_wgrad_generic(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap, hipStream_t s,
+                                int accum) {
+  const long lim = a.group_bytes > 0 && a.group_bytes < (long)kWgradFar ? a.group_bytes : (long)kWgradFar;
+  if (!a.x_u8 && (long)a.n * a.x_stride * 4 >= lim) {
+    const long ns = (lim / 4 - 1) / (a.x_stride > 0 ? a.x_stride : 1);
+    if (ns < 1) return -1;
+    for (long s0 = 0; s0 < a.n; s0 += ns) {
+      WgradArgs b = a;
+      b.n = (int)std::min<long>(ns, a.n - s0);
+      b.x_f = a.x_f + s0 * a.x_stride;
+      b.dz = a.dz + s0 * a.dz_stride;
+      if (launch_wgrad_generic(b, Gw, Gb, part, part_cap, s, accum || s0 > 0)) return -1;
+    }
+    return 0;
+  }
+  const long per = (long)a.OC * (a.Kt + 1);
   const WgradPlan p = plan_wgrad(a.OC, a.Kt, (long)a.n * a.OP);
   if (p.part_floats > part_cap) return -1;
   a.qchunk = p.qchunk;
@@ -3266,9 +3303,9 @@ int launch_wgrad(WgradArgs a, float* Gw, float* Gb, float* part, size_t part_cap
     const int groups = (p.chunks + kSumGroup - 1) / kSumGroup;
     float* lvl = part + (size_t)p.chunks * per;
     hipLaunchKernelGGL(k_wsum1, dim3(gb, groups), dim3(256), 0, s, part, p.chunks, per, lvl);
-    hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, lvl, groups, a.OC, a.Kt, Gw, Gb);
+    hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, lvl, groups, a.OC, a.Kt, Gw, Gb, accum);
   } else {
-    hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, part, p.chunks, a.OC, a.Kt, Gw, Gb);
+    hipLaunchKernelGGL(k_wsum, dim3(gb), dim3(256), 0, s, part, p.chunks, a.OC, a.Kt, Gw, Gb, accum);
   }
   return 0;
 }
@@ -3385,7 +3422,7 @@ extern "C" int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc
   int bad = 0;
   // y = x W^T + b on rows: dz [n][OUT] (stride dzs), x [n][IN] (stride xs)
   auto lin_w = [&](const float* dz, long dzs, int OUT, const float* x, long xs, int IN, long w, long b) {
-    WgradArgs a{dz, dzs, OUT, 1, 1, x, nullptr, xs, IN, 1, 1, 1, 1, n, IN, 0, nullptr};
+    WgradArgs a{dz, dzs, OUT, 1, 1, x, nullptr, xs, IN, 1, 1, 1, 1, n, IN, 0, nullptr, c->wgrad_group};
     bad |= launch_wgrad(a, G + w, G + b, c->part, c->part_floats, s);
   };
   auto lin_d = [&](const float* dz, long dzs, int OUT, long w, int w_in, const float* x, long xs, float* dx, long dxs,
@@ -3428,7 +3465,7 @@ extern "C" int ppo_carla_update(ppo_carla_t* c, const ppo_carla_train_config* tc
     const long xs = (long)L.conv_ic[i] * L.conv_ih[i] * L.conv_iw[i];
     WgradArgs wa{dz,          dzs,         L.conv_oc[i], L.conv_oh[i] * L.conv_ow[i], L.conv_ow[i], xf,
                  i ? nullptr : bev, xs,    L.conv_ic[i], L.conv_ih[i],                L.conv_iw[i], L.conv_k[i],
-                 L.conv_s[i], n,           L.conv_ic[i] * L.conv_k[i] * L.conv_k[i], 0, nullptr};
+                 L.conv_s[i], n,           L.conv_ic[i] * L.conv_k[i] * L.conv_k[i], 0, nullptr, c->wgrad_group};
     bad |= launch_wgrad(wa, G + L.conv_w[i], G + L.conv_b[i], c->part, c->part_floats, s, c->conv_img, c->c1bx,
                         c->wgrad_t);
     if (i > 0) {

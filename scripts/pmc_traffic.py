@@ -4,7 +4,7 @@
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts 64 B per memory-side read
 request while wide coalesced reads issue 128-B requests, so it reports half the bytes: it is
 doubled here. WRITE_SIZE is exact for 16-B-per-lane stores. Both counters are in KB (1024 B).
-Usage: pmc_traffic.py <rocprof out dir> <config tag>  -> JSON on stdout."""
+Usage: pmc_traffic.py <rocprof out dir> <config tag> [source label]  -> JSON on stdout."""
 import csv
 import glob
 import json
@@ -48,9 +48,11 @@ def per_kernel(path, counter):
 
 def main():
     path, tag = sys.argv[1], sys.argv[2]
+    source = sys.argv[3] if len(sys.argv) > 3 else os.path.basename(os.path.normpath(path))
     fetch = per_kernel(os.path.join(path), "FETCH_SIZE")
     write = per_kernel(os.path.join(path), "WRITE_SIZE")
-    out = {"_note": "bytes per launch; FETCH_SIZE doubled (gfx950 correction), KB = 1024 B; config = bench workload"}
+    out = {"_note": "bytes per launch; FETCH_SIZE doubled (gfx950 correction), KB = 1024 B; config = bench workload",
+           "_source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py --steps 1 --warmup 1`: {source}"}
     for k in sorted(set(fetch) | set(write)):
         fsum, fn = fetch.get(k, (0.0, 0))
         wsum, wn = write.get(k, (0.0, 0))

@@ -29,6 +29,12 @@ def test_bench_single_rank_line():
     assert roof["bound"] == "mfma" and 0 < roof["frac"] < 1 and roof["peak"] == 157.3
     assert abs(d["value"] - 512 * 128 / (d["ms_per_step"] / 1e3)) / d["value"] < 0.01
     assert d["config"]["devices"] == [0] and len(d["config"]["device_pci_bus_ids"]) == 1
+    # the precision choice is visible in the line: the fp32-MFMA leg of the same workload beside the
+    # headline, and dW's fraction beside k_upd's
+    f = d["fp32_mfma"]
+    assert f["options"] == "upd_mfma=16,dw_mfma=f32" and f["value"] > 0 and "bx" not in f["kernels"]
+    assert 0 < f["fwdbwd"]["frac"] < 1
+    assert 0 < roof["dw"]["frac"] < 2 and roof["dw"]["launches"] > 0
 
 
 def test_bench_one_rank_rccl_reports_its_device():

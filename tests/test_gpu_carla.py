@@ -316,3 +316,46 @@ def test_fused_tail_matches_layer_kernels(n):
         for r0, r1 in zip(outs["tail=layers"], outs[opt]):
             for x0, x1 in zip(r0, r1):
                 np.testing.assert_array_equal(x1, x0)
+
+
+def test_packed_conv1_odd_block_counts_match_generic():
+    """conv1's packed table holds IC * K kernel rows in 16-tap blocks of two rows; its split-bf16 loop
+    reads the blocks in pairs, so channel counts with an odd block count (IC = 5: 13 blocks, IC = 13:
+    33) get a zero padding block. The packed bx3 forward and update at IC = 5, then IC = 13 in the same
+    process (a later context needs more dynamic LDS than the first one: the kernel's LDS limit is set
+    for the largest size the launch accepts), against the generic fp32 kernels on the same parameters:
+    outputs rtol 2e-5 / atol 2e-6, gradients per tensor within rel-L2 1e-5."""
+    n = 5
+    rng = np.random.default_rng(41)
+    for ch in (5, 13):
+        bev = rng.integers(0, 256, size=(n, ch, 192, 192), dtype=np.uint8)
+        meas = rng.uniform(-1, 1, (n, 8)).astype(np.float32)
+        vmeas = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+        act = rng.uniform(-0.9, 0.9, (n, 2)).astype(np.float32)
+        tail = [rng.normal(-2.0, 0.3, n), rng.normal(0, 1, n), rng.normal(0, 1, n), rng.normal(0, 1, n)]
+        tail = [t.astype(np.float32) for t in tail]
+        outs, p = [], None
+        for opt in ("conv1=generic,conv1_mfma=f32", "conv1=packed,conv1_mfma=bx3"):
+            ag = ppo_amd.CarlaAgent(max_batch=8, obs_channels=ch, seed=7, options=opt)
+            try:
+                if p is None:
+                    p = ag.params()
+                ag.load_params(p)
+                res = [run(ag, bev, meas, vmeas, mode="mean"), run(ag, bev, meas, vmeas, act)]
+                d = [DeviceArray.from_numpy(bev, np.uint8)] + [DeviceArray.from_numpy(np.ascontiguousarray(x, np.float32))
+                                                               for x in (meas, vmeas, act, *tail)]
+                ag.update(*d, lr=3e-4, clip_coef=0.2, ent_coef=0.01, vf_coef=0.5, max_grad_norm=0.5, adam_eps=1e-5)
+                res.append(ag.last_grad())
+                lay = ag.layout
+                outs.append(res)
+            finally:
+                ag.close()
+        for r0, r1 in zip(outs[0][:2], outs[1][:2]):
+            for x0, x1 in zip(r0, r1):
+                np.testing.assert_allclose(x1, x0, rtol=2e-5, atol=2e-6)
+        g0, g1 = outs[0][2], outs[1][2]
+        for t in range(lay.ntensors):
+            o, m = lay.t_off[t], lay.t_len[t]
+            nr = np.linalg.norm(g0[o:o + m].astype(np.float64))
+            if nr > 0:
+                assert np.linalg.norm((g1[o:o + m] - g0[o:o + m]).astype(np.float64)) / nr < 1e-5, (ch, t)

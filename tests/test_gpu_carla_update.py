@@ -180,6 +180,39 @@ def test_update_with_one_rank_communicator_is_bit_identical():
         assert st0 == st1
 
 
+def test_generic_wgrad_sample_groups_match_one_pass():
+    """The generic fp32 weight-gradient kernel addresses its input with 32-bit buffer offsets, so an
+    input of >= 0x70000000 bytes (conv2's 8 x 94 x 94 floats per sample: ~6.6 K rows) runs as sample
+    groups whose sums are added in group order. wgrad_group_bytes lowers that limit so the group
+    arithmetic runs at n = 24 (1.5 MB: conv2 in 5 groups of <= 5 samples, conv3 in 3 of <= 11, both
+    with a ragged last group; the smaller layers in one pass): gradients within rel-L2 1e-5 per tensor of the one-pass generic kernel
+    (another summation order of the same fp32 products), stepped parameters atol 1e-6."""
+    L = CI.layout()
+    p = CI.params(L)
+    n = 24
+    rng = np.random.default_rng(29)
+    bev = rng.integers(0, 256, size=(n, 15, 192, 192), dtype=np.uint8)
+    f = lambda *shape: rng.uniform(-1, 1, shape).astype(np.float32)  # noqa: E731
+    batch = (bev, f(n, 8), f(n, 3), f(n, 2) * 0.95, f(n) * 0.2, rng.standard_normal(n).astype(np.float32),
+             rng.standard_normal(n).astype(np.float32), f(n) * 0.1)
+    out = {}
+    for o in ("conv_wgrad=generic", "conv_wgrad=generic,wgrad_group_bytes=1500000"):
+        ag = ppo_amd.CarlaAgent(max_batch=n, seed=7, options=o)
+        try:
+            ag.load_params(p)
+            ag.load_adam(np.zeros(L.P, np.float32), np.zeros(L.P, np.float32), 0)
+            out[o] = _run_update(ag, *batch)
+        finally:
+            ag.close()
+    (s0, g0, p0), (s1, g1, p1) = out.values()
+    for t in range(L.ntensors):
+        o_, n_ = L.t_off[t], L.t_len[t]
+        a, b = g1[o_:o_ + n_].astype(np.float64), g0[o_:o_ + n_].astype(np.float64)
+        assert np.linalg.norm(a - b) <= 1e-5 * max(np.linalg.norm(b), 1e-30), t
+    np.testing.assert_allclose(p1, p0, rtol=0, atol=1e-6)
+    assert s0["pg_loss"] == s1["pg_loss"]  # the forward and the loss do not depend on the option
+
+
 @pytest.mark.parametrize("opt", ["conv1_mfma=bx3"])
 def test_conv1_split_bf16_update_vs_torch(opt):
     """conv1 (raw-byte input) with its products as split-bf16 MFMAs (conv1_mfma=bx3: the byte operand

@@ -139,7 +139,8 @@ def test_gae_long_bit_exact_vs_golden():
     meta, d = load_case("gae_long")
     T, E = meta["T"], meta["E"]
     r, v, dn, nv, nd = gae_long_inputs(T, E)
-    ag = agent_for({"kind": 0, "O": 17, "A": 6, "H": 64}, E, T=T)
+    # gae=auto runs the scan at T >= 512 (test_gae_scan_vs_golden); the serial kernel is the bit-exact one
+    ag = agent_for({"kind": 0, "O": 17, "A": 6, "H": 64}, E, T=T, options="gae=serial")
     ag.buffer(ppo_amd.BUF_REWARDS, (T, E)).upload(r)
     ag.buffer(ppo_amd.BUF_VALUES, (T, E)).upload(v)
     ag.buffer(ppo_amd.BUF_DONES, (T, E)).upload(dn)
@@ -150,3 +151,37 @@ def test_gae_long_bit_exact_vs_golden():
     np.testing.assert_array_equal(column_fnv(adv), d["adv_fnv"])
     np.testing.assert_array_equal(column_fnv(ret), d["ret_fnv"])
     ag.close()
+
+
+@pytest.mark.parametrize("case", ["gae", "gae_t1", "gae_t7", "gae_t33", "gae_long"])
+def test_gae_scan_vs_golden(case):
+    """k_gae_scan (gae=scan; gae=auto's choice from T = 512, i.e. cfg1 / cfg2's T = 2 048) against the
+    LibTorch-replay golden vectors of the reference's serial recurrence (ppo:447-467): advantages and
+    returns within rtol 1e-5 / atol 1e-5 (the composed incoming value of each 1/16 segment rounds
+    differently from the serial chain; max |d| printed). gae_long (T = 2 048, E = 1 024) holds its
+    golden as 8 full columns plus per-column FNV hashes: the 8 columns are compared directly and every
+    column against the C oracle, which reproduces the hashes bit for bit (test_oracle_golden)."""
+    meta, d = load_case(case)
+    if case == "gae_long":
+        T, E = meta["T"], meta["E"]
+        r, v, dn, nv, nd = gae_long_inputs(T, E)
+    else:
+        r, v, dn, nv, nd = d["rewards"], d["values"], d["dones"], d["next_value"], d["next_done"]
+        T, E = r.shape
+    ag = agent_for({"kind": 0, "O": 17, "A": 6, "H": 64}, E, T=T, options="gae=scan")
+    ag.buffer(ppo_amd.BUF_REWARDS, (T, E)).upload(r)
+    ag.buffer(ppo_amd.BUF_VALUES, (T, E)).upload(v)
+    ag.buffer(ppo_amd.BUF_DONES, (T, E)).upload(dn)
+    ag.gae_from_values(DeviceArray.from_numpy(nv), DeviceArray.from_numpy(nd))
+    adv = ag.buffer(ppo_amd.BUF_ADVANTAGES, (T, E)).numpy()
+    ret = ag.buffer(ppo_amd.BUF_RETURNS, (T, E)).numpy()
+    ag.close()
+    if case == "gae_long":
+        np.testing.assert_allclose(adv[:, :8], d["adv_cols8"], rtol=1e-5, atol=1e-5)
+        ref_adv, ref_ret = O.gae(r, v, dn, nv, nd, 0.99, 0.95)
+        assert (column_fnv(ref_adv) == d["adv_fnv"]).all() and (column_fnv(ref_ret) == d["ret_fnv"]).all()
+    else:
+        ref_adv, ref_ret = d["advantages"], d["returns"]
+    print(f"\n{case} T={T} E={E}: max |adv scan - golden| {np.abs(adv - ref_adv).max():.2e}")
+    np.testing.assert_allclose(adv, ref_adv, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ret, ref_ret, rtol=1e-5, atol=1e-5)

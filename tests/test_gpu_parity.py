@@ -189,7 +189,7 @@ def test_gae_scan_matches_serial(T, E):
     nv = rng.standard_normal(E).astype(np.float32)
     nd = (rng.random(E) < 0.5).astype(np.float32)
     out = []
-    for opt in (None, "gae=scan"):
+    for opt in ("gae=serial", "gae=scan"):
         ag = make_agent(0, 17, 6, 64, E, T=T, options=opt)
         ag.buffer(ppo_amd.BUF_REWARDS, (T, E)).upload(r)
         ag.buffer(ppo_amd.BUF_VALUES, (T, E)).upload(v)

@@ -362,7 +362,7 @@ def main():
                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4), "traffic": None,
                         "kernel": name, "avg_launch_ms": round(ms / cnt, 4), "launches": cnt,
                         "algorithmic_per_launch": amount, "kernels": kinfo}
-                if name == "fwdbwd" and "bx6" in kinfo:
+                if name == "fwdbwd" and "update=k_upd/bx6" in kinfo:
                     # the fp32 products of layer 2 and dh1 run as six bf16 piece products on the bf16
                     # MFMA (2.5 PF/s dense): the peak of the kernel's actual instruction mix
                     frac_bx, peak_mix = bx6_mix_peak(O_, A, H)
@@ -391,7 +391,8 @@ def main():
         if roof is not None and src and "dw" in src:
             ms, cnt = src["dw"]
             dw_tf = work["dw"][1] / (ms / 1e3 / cnt) / 1e12
-            roof["dw"] = {"kernel": kinfo.split("dw=")[-1] if "dw=" in kinfo else "dw", "avg_launch_ms": round(ms / cnt, 4),
+            roof["dw"] = {"kernel": kinfo.split("dw=")[-1].split()[0] if "dw=" in kinfo else "dw",
+                          "avg_launch_ms": round(ms / cnt, 4),
                           "launches": cnt, "achieved": round(dw_tf, 3), "frac": round(dw_tf / PEAK_F32_MFMA_TFLOPS, 4),
                           "algorithmic_per_launch": work["dw"][1],
                           "timing": "HIP events on the context stream, iterations after the timed region"}

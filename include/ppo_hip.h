@@ -17,6 +17,7 @@
  *                                    (ppo:387-400, ac:649-660) for envs [env_begin, env_end)
  *   ppo_rollout_reward               rewards[step] store (ppo:406, ac:668)
  *   ppo_compute_gae                  next_value + GAE(lambda) + returns (ppo:447-467, ac:759-779)
+ *   ppo_rollout_values               the rollout's deferred critic pass (ac:655 values[step])
  *   ppo_update                       epochs x minibatches: randperm, gather, loss, backward, grad all-reduce,
  *                                    clip_grad_norm_, Adam (ppo:489-542, ac:803-889)
  *   ppo_comm_*                       torchfort::Comm (include/distributed.h:41-60, src/distributed.cpp:81-224)
@@ -125,6 +126,11 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            ppo:447-467, ac:759-779) or as a segmented scan over the steps (k_gae_scan: 16
  *                            segments per 64 envs, within 1e-5 of the serial form and of the golden
  *                            vectors); auto: the scan from 512 steps (cfg1 / cfg2's T = 2 048), serial below
+ *   values_mfma=auto|bx6|f32 the rollout's critic pass (values of the stored rows and the bootstrap,
+ *                            ac:655 / :761): k_vbx, layer 2 as k_upd's six split-bf16 piece products
+ *                            (bx6; auto where upd_mfma=bx6 applies: the per-step act kernels then skip
+ *                            the critic and one batched pass runs before GAE) or the fp32 MFMA
+ *                            k_values / per-step critic (f32)
  *   gradstep=split|fused     clip_grad_norm_ + Adam: two launches (k_gradnorm, k_adam; default) or
  *                            one cooperative launch (k_gradstep: slower on ROCm 7, whose cooperative
  *                            launch costs ~30 us); bitwise the same
@@ -153,9 +159,17 @@ int ppo_get_value(ppo_t* ctx, int n, const float* x_dev, float* value_dev, void*
 /* rollout step `step` for envs [env_begin, env_end): stores obs/dones, samples actions with the
  * Philox key (seed, rank, env, iteration*T + step), writes actions into storage and (if non-NULL)
  * into action_out_dev[e - env_begin]. Several host threads may call it concurrently on distinct
- * env ranges and streams (AC-PPO async collection, ac:641-698). */
+ * env ranges and streams (AC-PPO async collection, ac:641-698). The value of each row (ac:655,
+ * `values[step] = value`) is stored either here or, for the LayerNorm-Beta agent with the split-bf16
+ * critic pass (create option values_mfma, default where upd_mfma=bx6 applies), by one batched critic
+ * launch over the stored observations that ppo_compute_gae / ppo_gae_from_values / ppo_update run
+ * first (the persistent rollout's kernel: both collection paths store the same values bit for bit);
+ * ppo_rollout_values runs that pass now. */
 int ppo_rollout_act(ppo_t* ctx, int step, int env_begin, int env_end, const float* next_obs_dev,
                     const float* next_done_dev, float* action_out_dev, void* stream);
+/* the deferred critic pass of ppo_rollout_act (values[t] for every step acted since the last pass),
+ * on `stream` after the act launches; a no-op when nothing is pending (ac:655). */
+int ppo_rollout_values(ppo_t* ctx, void* stream);
 int ppo_rollout_reward(ppo_t* ctx, int step, int env_begin, int env_end, const float* reward_dev, void* stream);
 /* GAE over steps [0, num_steps_collected) using next_obs/next_done after the last step (ac:759-779).
  * num_steps_collected < num_steps (DD-PPO preemption): the last collected step is bootstrapped from

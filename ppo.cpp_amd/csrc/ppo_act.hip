@@ -120,6 +120,13 @@ __global__ __launch_bounds__(512) void k_act3(ActArgs a) {
       XS[r * LDX + f] = v;
     }
   }
+  if (trunk == 0 && a.skip_critic) {
+    // the rollout's critic pass is deferred (ppo_compute_gae / ppo_rollout_values: one batched critic
+    // launch over the stored rows, the persistent rollout's k_vbx): store next_done with the rows only
+    if (tid < R && a.store_step >= 0 && row0 + tid < a.n)
+      a.s_dones[(long)a.store_step * a.E + a.env_base + row0 + tid] = ndone;
+    return;
+  }
   lds_barrier();
   // ---- layer 1 ----
   f4 acc[2][RT];

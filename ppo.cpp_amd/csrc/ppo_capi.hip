@@ -13,6 +13,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -156,6 +157,10 @@ struct ppo_ctx {
   bool use_upd32 = false;  // k_upd32 (32x32x2 MFMAs) instead of k_upd (create option upd_mfma)
   int upd_bx = 0;          // 1: k_upd's 256-wide GEMMs as split-bf16 piece products (upd_mfma=bx6)
   int gae_scan = -1;       // 1: GAE as k_gae_scan (create option gae=scan); 0: the bit-exact serial k_gae; -1 auto
+  // 1: the rollout's critic pass is k_vbx (layer 2 as split-bf16 products; create option values_mfma),
+  // run once over the stored rows: the per-step act kernels skip the critic and leave it pending
+  int values_bx = 0;
+  std::atomic<int> values_pending{0};  // steps [0, n) of the rollout storage whose values are not computed yet
   int upd32_mix = 0;       // k_upd32 with the actor trunk on k_upd's body (upd_mfma=mix)
   bool use_upd2 = false;  // two-trunk k_upd2 (ppo_update_narrow.hip, H = 64 tanh agent)
   int rollout_kernel = 0;   // AC persistent rollout: 0 auto, 1 k_rollout (MFMA), 2 k_rollout_v (VALU)
@@ -283,6 +288,7 @@ struct CreateOptions {
   int dw_dma = 1;      // 1 (default): k_dwf_dma (LDS-DMA staging, three stage buffers); 0: k_dwf
   int dw_bx = -1;      // dw_mfma: -1 auto, 0 f32 (fp32 MFMA), 9 / 8 / 6 bf16x9 / x8 / x6 (k_dwf_bx: exact bf16 splits)
   int gae_scan = -1;   // gae=auto (scan from kGaeScanMinT steps) | serial (bit-exact with the reference's loop) | scan
+  int values_mfma = -1;  // values_mfma=auto (bx6 where k_upd's bx6 pieces exist) | f32 | bx6
   // 1: ppo_update replays its minibatch launches as one captured hipGraph; 0 (default): eager.
   // Snapshots work with it on (ppo_read_snapshot waits for the snapshot's event on the host).
   int update_graph = 0;
@@ -338,6 +344,8 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
     else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
     else if (k == "dw_dma" && (v == "0" || v == "1")) o->dw_dma = v[0] - '0';
     else if (k == "gae" && (v == "auto" || v == "serial" || v == "scan")) o->gae_scan = v == "auto" ? -1 : v == "scan";
+    else if (k == "values_mfma" && (v == "auto" || v == "f32" || v == "bx6"))
+      o->values_mfma = v == "auto" ? -1 : v == "f32" ? 0 : 6;
     else if (k == "dw_mfma" && (v == "auto" || v == "f32" || v == "bf16x9" || v == "bf16x8" || v == "bf16x6"))
       o->dw_bx = v == "auto" ? -1 : v == "f32" ? 0 : v == "bf16x9" ? 9 : v == "bf16x8" ? 8 : 6;
     else if (k == "update_graph" && (v == "0" || v == "1")) o->update_graph = v[0] - '0';
@@ -525,6 +533,12 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
       const int ut = (c->M + c->upd.rows - 1) / c->upd.rows;
       c->upd_nblk = std::min(ut, 256);  // 2 workgroups per CU x 256 CUs over the two trunks
     }
+  }
+  // the critic pass on split-bf16 products wherever k_upd keeps the critic's W2 pieces (bx6)
+  c->values_bx = (c->upd_bx == 1 && opt.values_mfma != 0 && rollout_supported(c->K) == 0) ? 1 : 0;
+  if (opt.values_mfma == 6 && !c->values_bx) {
+    ppo_destroy(c);
+    return fail("ppo_create: values_mfma=bx6 needs the LayerNorm-Beta agent at hidden 256 with upd_mfma=bx6 (auto)");
   }
   for (int k = 0; k < 2; ++k)
     rc |= dmalloc(&c->slab[k], (size_t)std::max(c->nblk, c->upd_nblk) * c->sg[k].size);
@@ -753,9 +767,18 @@ extern "C" int ppo_rollout_act(ppo_t* c, int step, int e0, int e1, const float* 
   a.s_logp = c->buf[PPO_BUF_LOGPROBS];
   a.s_dones = c->buf[PPO_BUF_DONES];
   a.s_values = c->buf[PPO_BUF_VALUES];
+  // values_bx: the critic runs later, once over the stored rows (flush_values: ppo_compute_gae,
+  // ppo_rollout_values), with the persistent rollout's kernel, so both collection paths store the
+  // same values bit for bit
+  a.skip_critic = c->values_bx;
   hipStream_t s = S(c, stream);
   ProfScope ps(c, PK_ACT, s);
   if (launch_act(a, s) != 0) return fail("no act kernel for this configuration");
+  if (c->values_bx) {  // groups act concurrently from host threads: an atomic maximum
+    int cur = c->values_pending.load();
+    while (cur < step + 1 && !c->values_pending.compare_exchange_weak(cur, step + 1)) {
+    }
+  }
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -771,21 +794,44 @@ extern "C" int ppo_rollout_reward(ppo_t* c, int step, int e0, int e1, const floa
 
 static int gae_launch(ppo_t* c, const float* next_value, const float* next_done, int nsteps, hipStream_t s);
 
+// the critic over n contiguous observation rows (k_vbx with the critic's W2 pieces, else k_values)
+static int run_values(ppo_t* c, const float* obs, float* values, long n, hipStream_t s) {
+  ValuesArgs v;
+  v.P = c->P;
+  v.K = c->K;
+  v.WSW = c->WSW[0];
+  v.obs = obs;
+  v.values = values;
+  v.n = n;
+  v.WBX = c->values_bx ? c->WSW[0] + sw_size(c->K.H, c->K.OP) : nullptr;
+  ProfScope ps(c, PK_VALUES, s);
+  if (v.WBX) return launch_vbx(v, s) == 0 ? 0 : -1;
+  return launch_values(v, s);
+}
+// the deferred critic pass of per-step rollouts (ppo_rollout_act with values_bx): values[t] for every
+// step acted so far, over the stored observations
+static int flush_values(ppo_t* c, hipStream_t s) {
+  const int steps = c->values_pending.exchange(0);
+  if (steps <= 0) return 0;
+  if (run_values(c, c->buf[PPO_BUF_OBS], c->buf[PPO_BUF_VALUES], (long)steps * c->cfg.num_envs, s) != 0)
+    return fail("ppo_rollout_values: critic kernel launch failed");
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+extern "C" int ppo_rollout_values(ppo_t* c, void* stream) {
+  if (!c) return fail("ppo_rollout_values: null argument");
+  return flush_values(c, S(c, stream));
+}
+
 extern "C" int ppo_compute_gae(ppo_t* c, const float* next_obs, const float* next_done, int nsteps, void* stream) {
   if (!c || !next_obs || !next_done) return fail("ppo_compute_gae: null argument");
   if (nsteps <= 0 || nsteps > c->cfg.num_steps) return fail("ppo_compute_gae: bad step count");
   hipStream_t s = S(c, stream);
+  if (int rc = flush_values(c, s)) return rc;
   if (rollout_supported(c->K) == 0) {
     // the bootstrap value with the critic pass that fills values[t] on the persistent path
-    ValuesArgs v;
-    v.P = c->P;
-    v.K = c->K;
-    v.WSW = c->WSW[0];
-    v.obs = next_obs;
-    v.values = c->next_value;
-    v.n = c->cfg.num_envs;
-    ProfScope ps(c, PK_VALUES, s);
-    if (launch_values(v, s) != 0) return fail("ppo_compute_gae: values kernel launch failed");
+    if (run_values(c, next_obs, c->next_value, c->cfg.num_envs, s) != 0)
+      return fail("ppo_compute_gae: values kernel launch failed");
   } else {
     int rc = ppo_get_value(c, c->cfg.num_envs, next_obs, c->next_value, s);
     if (rc) return rc;
@@ -797,6 +843,7 @@ extern "C" int ppo_gae_from_values(ppo_t* c, const float* next_value, const floa
                                    void* stream) {
   if (!c || !next_value || !next_done) return fail("ppo_gae_from_values: null argument");
   if (nsteps <= 0 || nsteps > c->cfg.num_steps) return fail("ppo_gae_from_values: bad step count");
+  if (int rc = flush_values(c, S(c, stream))) return rc;
   return gae_launch(c, next_value, next_done, nsteps, S(c, stream));
 }
 
@@ -870,6 +917,7 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
   if (cfg.world_size > 1 && !multi)
     return fail("ppo_update: world_size " + std::to_string(cfg.world_size) +
                 " but no communicator attached (ppo_comm_init / ppo_comm_init_host)");
+  if (int rc = flush_values(c, s)) return rc;  // old values of a per-step rollout whose GAE came from elsewhere
   // ---- permutations (torch::randperm per epoch, ppo:490 / ac:804) ----
   // A partial collection of nsteps < num_steps (DD-PPO preemption, ac:803-810): the permutation runs
   // over the Bc = nsteps * E collected samples (the first nsteps rows of the [T, E] storage) and is
@@ -1362,7 +1410,9 @@ extern "C" int ppo_kernel_info(const ppo_t* c, char* buf, int len) {
                    : fused ? (!c->dw_dma ? "k_dwf" : c->dw_bx ? "k_dwf_bx/bf16x" + std::to_string(c->dw_bx) : "k_dwf_dma/f32")
                    : (c->dw_dma && H == 256 && OP == 112) ? "k_dw_dma" + bxs
                                                           : "k_dw";
-  const std::string s = "update=" + upd + " dw=" + dw;
+  const std::string vals = rollout_supported(c->K) != 0 ? "k_act" : c->values_bx ? "k_vbx/bx6"
+                           : c->K.kind == PPO_NET_TANH_NORMAL ? "k_values4/f32" : "k_values/f32";
+  const std::string s = "update=" + upd + " dw=" + dw + " values=" + vals;
   snprintf(buf, (size_t)len, "%s", s.c_str());
   return 0;
 }
@@ -1554,17 +1604,9 @@ extern "C" int ppo_rollout_synth(ppo_t* c, psyn_t* env, float* next_obs, float* 
                               : "ppo_rollout_synth: rollout kernel launch failed");
       if (r.s_beta) launch_beta_logp(r.s_beta, c->buf[PPO_BUF_LOGPROBS], (long)E * c->cfg.num_steps, c->K.A, c->stream);
     }
-    ValuesArgs v;
-    v.P = c->P;
-    v.K = c->K;
-    v.WSW = c->WSW[0];
-    v.obs = c->buf[PPO_BUF_OBS];
-    v.values = c->buf[PPO_BUF_VALUES];
-    v.n = (long)E * c->cfg.num_steps;
-    {
-      ProfScope ps(c, PK_VALUES, c->stream);
-      if (launch_values(v, c->stream) != 0) return fail("ppo_rollout_synth: values kernel launch failed");
-    }
+    c->values_pending.store(0);  // every stored row's value comes from this pass
+    if (run_values(c, c->buf[PPO_BUF_OBS], c->buf[PPO_BUF_VALUES], (long)E * c->cfg.num_steps, c->stream) != 0)
+      return fail("ppo_rollout_synth: values kernel launch failed");
     HIP_TRY(hipGetLastError());
     return 0;
   }
@@ -1578,6 +1620,7 @@ extern "C" int ppo_rollout_synth(ppo_t* c, psyn_t* env, float* next_obs, float* 
                         next_done, c->stream);
     }
   }
+  if (int rc = flush_values(c, c->stream)) return rc;  // the rollout's values, as the persistent path leaves them
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -34,6 +34,7 @@ struct ActArgs {
   float *s_obs, *s_actions, *s_logp, *s_dones, *s_values;
   int kernel;  // 0: fastest for the shape; 2 / 4: force k_act2 / k_act4 (A/B comparisons)
   const float* WSW[2];  // swizzled W1 | W2 | W2^T per trunk (k_act3)
+  int skip_critic;      // k_act3, rollout stores: the critic workgroups store obs / dones only (deferred pass)
 };
 
 // A-operand ("swizzled") copies of a trunk's weight matrices: the 16 x 16 block (feature block fb,
@@ -266,7 +267,9 @@ struct ValuesArgs {
   const float* obs;     // [n][O]
   float* values;        // [n]
   long n;
+  const float* WBX;     // non-null: the critic's W2 pieces (bx_index): layer 2 as split-bf16 products (k_vbx)
 };
+int launch_vbx(const ValuesArgs& a, hipStream_t s);  // ppo_update.hip; -1 when the shape is not covered
 int rollout_supported(const PackedLayout& K);
 int launch_rollout(const RolloutArgs& a, hipStream_t s);
 int launch_values(const ValuesArgs& a, hipStream_t s);

@@ -28,6 +28,35 @@
 #include <cstdlib>
 #include "ppo_kernels.hpp"
 
+// 1: a tile's gathered rows are committed to LDS by the previous tile (EARLY in upd16_body); 0: at the
+// tile top (A/B builds)
+#ifndef PPO_UPD_EARLY
+#define PPO_UPD_EARLY 0
+#endif
+// A/B switches of round-6 k_upd changes (each 1 = on): merged LayerNorm statistics, the two
+// barriers other exchange barriers cover, head partials summed inside the loss, branch-free
+// prefetch loads, no LDS copy of the critic's h2, the tile top's first barrier (covered by the
+// previous tile's layer-1 backward exchange). Measured per change (profiles/r06/kupd_ab/): EARLY
+// +9.6 %, BF +1.4 % per launch (off); CHAN -1.0 %, BAR -1.0 %, PRE -0.5 %, CH2 0 (on)
+#ifndef PPO_V_CHAN
+#define PPO_V_CHAN 1
+#endif
+#ifndef PPO_V_BAR
+#define PPO_V_BAR 1
+#endif
+#ifndef PPO_V_PRE
+#define PPO_V_PRE 1
+#endif
+#ifndef PPO_V_BF
+#define PPO_V_BF 0
+#endif
+#ifndef PPO_V_TOP
+#define PPO_V_TOP 1
+#endif
+#ifndef PPO_V_CH2
+#define PPO_V_CH2 1
+#endif
+
 #ifdef PPO_STAMPS
 // diagnostic build only: per-wave shader-clock stamps at phase ends of the first 16 tiles of every workgroup
 #define PPO_NSTAMP 13
@@ -305,36 +334,102 @@ PPO_DEV void rows_total2(float (&s)[RT], float (&q)[RT], float* red0, float* red
   }
 }
 
-// LayerNorm statistics of z (two-pass, eps 1e-5, biased variance as torch::layer_norm)
+// LayerNorm statistics of z (eps 1e-5, biased variance as torch::layer_norm). One wave holds H / WF
+// features of a row: it computes their sum and their squared deviations about its OWN mean (two-pass
+// within the wave), and the WF waves' (sum, M2) pairs are merged after ONE cross-wave exchange with
+// Chan's parallel formula, M2 = sum_w M2_w + n_w (mean_w - mean)^2 (exactly the two-pass variance in
+// exact arithmetic, as stable in fp32): one barrier per LayerNorm instead of two. WF = 1 is the plain
+// two-pass form.
 template <int FT, int RT, int WF, int R, int H>
 PPO_DEV void ln_rows(const f4 (&z)[FT][RT], float (&mu)[RT], float (&rs)[RT], float* red0, float* red1, int wf,
                      int rbase, int j, int g) {
   constexpr float invH = 1.0f / H;
-  float s[RT];
+#if !PPO_V_CHAN
+  {
+    float s[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float t = 0.f;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) t += (z[ft][rt].x + z[ft][rt].y) + (z[ft][rt].z + z[ft][rt].w);
+      s[rt] = t;
+    }
+    rows_total<WF, RT, R>(s, red0, wf, rbase, j, g);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      mu[rt] = s[rt] * invH;
+      float t = 0.f;
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = z[ft][rt][r] - mu[rt];
+          t += d * d;
+        }
+      s[rt] = t;
+    }
+    rows_total<WF, RT, R>(s, red1, wf, rbase, j, g);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) rs[rt] = 1.0f / sqrtf(s[rt] * invH + 1e-5f);
+    return;
+  }
+#endif
+  constexpr int HW = H / WF;
+  constexpr float invW = 1.0f / HW;
+  float s[RT], q[RT];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     float t = 0.f;
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft) t += (z[ft][rt].x + z[ft][rt].y) + (z[ft][rt].z + z[ft][rt].w);
-    s[rt] = t;
+    s[rt] = row_allreduce(t);
   }
-  rows_total<WF, RT, R>(s, red0, wf, rbase, j, g);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
-    mu[rt] = s[rt] * invH;
+    const float mw = s[rt] * invW;
     float t = 0.f;
 #pragma unroll
     for (int ft = 0; ft < FT; ++ft)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float d = z[ft][rt][r] - mu[rt];
+        const float d = z[ft][rt][r] - mw;
         t += d * d;
       }
-    s[rt] = t;
+    q[rt] = row_allreduce(t);
   }
-  rows_total<WF, RT, R>(s, red1, wf, rbase, j, g);
+  if constexpr (WF > 1) {
+    if (g == 0) {
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt) rs[rt] = 1.0f / sqrtf(s[rt] * invH + 1e-5f);
+      for (int rt = 0; rt < RT; ++rt) {
+        red0[wf * R + rbase + 16 * rt + j] = s[rt];
+        red1[wf * R + rbase + 16 * rt + j] = q[rt];
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float sw[WF], tot = 0.f;
+#pragma unroll
+      for (int w = 0; w < WF; ++w) {
+        sw[w] = red0[w * R + rbase + 16 * rt + j];
+        tot += sw[w];
+      }
+      mu[rt] = tot * invH;
+      float m2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WF; ++w) {
+        const float dm = sw[w] * invW - mu[rt];
+        m2 += red1[w * R + rbase + 16 * rt + j] + (float)HW * (dm * dm);
+      }
+      rs[rt] = 1.0f / sqrtf(m2 * invH + 1e-5f);
+    }
+  } else {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      mu[rt] = s[rt] * invH;
+      rs[rt] = 1.0f / sqrtf(q[rt] * invH + 1e-5f);
+    }
+  }
 }
 
 template <int CTRL, int LEN, int M>
@@ -444,9 +539,12 @@ PPO_DEV int head_bias(const PackedLayout& K, int trunk, int h) {
 // The PPO loss of one tile and its gradient wrt the head pre-activations: PRE -> GG (critic: the
 // clipped value loss, ppo:520-533; actor: Beta or Normal log-prob / entropy, the clipped surrogate,
 // ppo:497-519, ac:815-875), the per-lane loss statistics added to lst. Shared by k_upd and k_upd32.
-template <bool LN, int R, int ITS, int LDG>
+// pre(row, h): a head pre-activation for the critic and the one-row-per-8-lanes Beta loss (k_upd sums the
+// head partials there directly); the other losses read the materialised PRE array.
+template <bool LN, int R, int ITS, int LDG, typename PreFn>
 PPO_DEV void upd_loss(const UpdArgs& a, int trunk, int tid, int m0, float c, float adv_mean, float adv_std,
-                      const float* PRE, float* GG, float* ROWS, const float* ACTN, float* ITM, float (&lst)[6]) {
+                      PreFn pre, const float* PRE, float* GG, float* ROWS, const float* ACTN, float* ITM,
+                      float (&lst)[6]) {
   const PackedLayout& K = a.K;
   const float* __restrict__ P = a.P;
   const int A = K.A;
@@ -454,7 +552,7 @@ PPO_DEV void upd_loss(const UpdArgs& a, int trunk, int tid, int m0, float c, flo
   if (trunk == 0) {
     if (tid < R) {
       const bool valid = m0 + tid < a.M;
-      const float v = PRE[tid * LDG];
+      const float v = pre(tid, 0);
       const float rt_ = ROWS[tid * 8 + 1], ov = ROWS[tid * 8 + 2];
       float gv, sv;
       if (a.clip_vloss) {
@@ -484,7 +582,7 @@ PPO_DEV void upd_loss(const UpdArgs& a, int trunk, int tid, int m0, float c, flo
     const bool valid = m0 + row < a.M;
     const int ac = item ? ai : 0;  // lanes past A evaluate item 0 and drop it (uniform control flow)
     const float hi = P[K.hi], lo = P[K.lo];
-    const float pa = PRE[row * LDG + ac], pbv = PRE[row * LDG + A + ac];
+    const float pa = pre(row, ac), pbv = pre(row, A + ac);
     const float al = softplusf_(pa) + 1.0f, be = softplusf_(pbv) + 1.0f;
     const float av = valid ? ACTN[row * A + ac] : 0.5f * (hi + lo);
     float s = (av - lo) / (hi - lo) * (1.0f - 0.0f) + 0.0f;
@@ -720,6 +818,55 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
   constexpr int NAI = PREF ? (R * PPO_UPD_MAXA + 255) / 256 : 1;  // action items per thread
   int pg[NG], pra, pac[NAI];
   float vg[NG], vr1 = 0.f, vr2 = 0.f, vac[NAI];
+#if PPO_V_BF
+  // every load is unconditional from a clamped (valid) address and masked by a select afterwards: a
+  // load under a per-lane branch gets its own branch and, at the loop head, a vmcnt(0) wait
+  auto pref_idx = [&](int itn) {
+    const int mb = itn * R;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int idx = tid + 256 * k, row = idx / OP, f = idx - row * OP, m = mb + row;
+      const bool ok = itn < ntiles && idx < R * OP && m < a.M && f < O;
+      const int pv = a.perm[ok ? m : 0];
+      pg[k] = ok ? pv : -1;
+    }
+    {
+      const bool ok = itn < ntiles && tid < R && mb + tid < a.M;
+      const int pv = a.perm[ok ? mb + tid : 0];
+      pra = ok ? pv : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < NAI; ++k) {
+      const int idx = tid + 256 * k, row = idx / (A > 0 ? A : 1), m = mb + row;
+      const bool ok = trunk == 1 && itn < ntiles && idx < R * A && m < a.M;
+      const int pv = a.perm[ok ? m : 0];
+      pac[k] = ok ? pv : -1;
+    }
+  };
+  auto pref_data = [&](int itn) {
+    (void)itn;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int idx = tid + 256 * k, row = idx / OP, f = idx - row * OP;
+      (void)row;
+      const float v = a.obs[(long)(pg[k] >= 0 ? pg[k] : 0) * O + (f < O ? f : 0)];
+      vg[k] = pg[k] >= 0 ? v : 0.f;
+    }
+    {
+      const int pr = pra >= 0 ? pra : 0;
+      const float x1 = trunk == 0 ? a.ret[pr] : a.logp[pr];
+      const float x2 = trunk == 0 ? a.val[pr] : a.adv[pr];
+      vr1 = pra >= 0 ? x1 : 0.f;
+      vr2 = pra >= 0 ? x2 : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NAI; ++k) {
+      const int idx = tid + 256 * k, ai = idx - (idx / (A > 0 ? A : 1)) * A;
+      const float v = a.actions[(long)(pac[k] >= 0 ? pac[k] : 0) * A + ai];
+      vac[k] = pac[k] >= 0 ? v : 0.f;
+    }
+  };
+#else
   auto pref_idx = [&](int itn) {
     const int mb = itn * R;
 #pragma unroll
@@ -755,6 +902,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
       vac[k] = pac[k] >= 0 ? a.actions[(long)pac[k] * A + ai] : 0.f;
     }
   };
+#endif
   auto commit = [&](int itc) {
     const int mb = itc * R;
 #pragma unroll
@@ -864,6 +1012,19 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
     SPAR[i] = x;
   }
   if constexpr (PREF) pref_data(blockIdx.x);
+  // EARLY (narrow inputs, LayerNorm trunks over several waves): a tile's gathered rows are committed to
+  // LDS by the PREVIOUS tile, right after its layer-1 backward exchange barrier (every wave is past its
+  // last XN / ROWS / ACTN read of that tile by then), so the tile top is one barrier and a few loads;
+  // the first tile's rows are committed here
+  constexpr bool EARLY = PPO_UPD_EARLY && PREF && LN && WF > 1;
+  if constexpr (EARLY) {
+    lds_barrier();  // SPAR (observation mean / std) is staged
+    commit(blockIdx.x);
+  }
+  // TOP: the tile top writes XN / ROWS / ACTN without a barrier first: the previous tile's last readers
+  // of them (layer-1 recompute, loss) all precede its layer-1 backward exchange barrier (rows_total2)
+  constexpr bool TOP = PPO_V_TOP && !EARLY && PREF && LN && WF > 1;
+  if constexpr (TOP) lds_barrier();  // SPAR (observation mean / std) is staged for the first commit
   // wide inputs: row tid's permutation entry of the next tile (clamped, as the gather clamps rows)
   int nperm = 0;
   if constexpr (!PREF) nperm = tid < R ? a.perm[min((int)blockIdx.x * R + tid, a.M - 1)] : 0;
@@ -874,8 +1035,10 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
     PPO_STAMP_START();
     if constexpr (!PREF)
       if (tid < R) ROWS[tid * 8] = __int_as_float(nperm);  // slot 0 is read only by gather_sync
-    lds_barrier();  // the previous iteration's LDS readers are done
-    if constexpr (PREF) {
+    if constexpr (!TOP) lds_barrier();  // the previous iteration's LDS readers are done (EARLY: rows committed)
+    if constexpr (EARLY) {
+      pref_idx(it + gridDim.x);
+    } else if constexpr (PREF) {
       commit(it);
       pref_idx(it + gridDim.x);
     } else {
@@ -894,11 +1057,18 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
           hwb[ft] = pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
         } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) hwb[ft][r] = hrow_b[0][r] >= 0 ? bld1(pb, hrow_b[0][r] + fbase + j, 16 * ft) : 0.0f;
+          for (int r = 0; r < 4; ++r) {
+#if PPO_V_BF
+            const float v = bld1(pb, (hrow_b[0][r] >= 0 ? hrow_b[0][r] : 0) + fbase + j, 16 * ft);
+            hwb[ft][r] = hrow_b[0][r] >= 0 ? v : 0.0f;
+#else
+            hwb[ft][r] = hrow_b[0][r] >= 0 ? bld1(pb, hrow_b[0][r] + fbase + j, 16 * ft) : 0.0f;
+#endif
+          }
         }
       }
     }
-    lds_barrier();
+    if constexpr (!EARLY) lds_barrier();
     PPO_STAMP(0);
 
     // ---------------- layer 1 ----------------
@@ -979,7 +1149,9 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
     for (int ht = 0; ht < NHT; ++ht)
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) hp[ht][rt] = f4{0.f, 0.f, 0.f, 0.f};
-    lds_barrier();  // every wave is done reading h1 from ACT
+    // every wave is done reading h1 from ACT: LN2's exchange barrier (ln_rows) already follows every
+    // wave's layer-2 GEMM; tanh trunks and one-wave rows (WF = 1) have no exchange, so they wait here
+    if constexpr (!PPO_V_BAR || !LN || WF == 1) lds_barrier();
     if constexpr (BX) {  // GG shares the activation region: padding heads must read exactly 0
       for (int i = tid; i < R * LDG; i += 256) GG[i] = 0.f;
     }
@@ -994,8 +1166,9 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
         const f4 w = NHT == 1 ? hwb[ft] : pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
+          // no LDS copy of the critic's h2: its head backward and dW3 column sums read registers
           const f4 h2 = h2_of(ft, rt);
-          lds_st4(ACT + (rbase + 16 * rt + j) * LDA + fbase + 16 * ft + 4 * g, h2);
+          if constexpr (!PPO_V_CH2) lds_st4(ACT + (rbase + 16 * rt + j) * LDA + fbase + 16 * ft + 4 * g, h2);
 #pragma unroll
           for (int r = 0; r < 4; ++r) pv[rt] = fmaf(w[r], h2[r], pv[rt]);
         }
@@ -1036,19 +1209,30 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
     }  // actor heads
     lds_barrier();
     PPO_STAMP(5);
-    for (int idx = tid; idx < R * nh; idx += 256) {
-      const int row = idx / nh, h = idx - row * nh;
+    float* ITM = SCR;  // R x A x ITS (head partials are consumed)
+    // the critic and the one-row-per-8-lanes Beta loss read each pre-activation straight from the WF
+    // partial sums (same order, bitwise the materialised PRE): no PRE pass and no barrier; the other
+    // losses reuse SCR as item scratch, so they need PRE first
+    auto psum = [&](int row, int h) {
       float s = 0.f;
 #pragma unroll
       for (int w = 0; w < WF; ++w) s += SCR[(w * NHP + h) * R + row];
-      PRE[row * LDG + h] = s + SHB[h];
+      return s + SHB[h];
+    };
+    auto pre = [&](int row, int h) {
+      if constexpr (PPO_V_PRE) return psum(row, h);
+      else return PRE[row * LDG + h];
+    };
+    if (!PPO_V_PRE || !(trunk == 0 || (LN && R == 32 && A <= 8))) {
+      for (int idx = tid; idx < R * nh; idx += 256) {
+        const int row = idx / nh, h = idx - row * nh;
+        PRE[row * LDG + h] = psum(row, h);
+      }
+      lds_barrier();
     }
-    lds_barrier();
     PPO_STAMP(6);
-
     // ---------------- loss and its gradient wrt the head pre-activations ----------------
-    float* ITM = SCR;  // R x A x ITS (head partials are consumed)
-    upd_loss<LN, R, ITS, LDG>(a, trunk, tid, m0, c, adv_mean, adv_std, PRE, GG, ROWS, ACTN, ITM, lst);
+    upd_loss<LN, R, ITS, LDG>(a, trunk, tid, m0, c, adv_mean, adv_std, pre, PRE, GG, ROWS, ACTN, ITM, lst);
     lds_barrier();
     PPO_STAMP(7);
     // head bias (and logstd) gradients: fixed-order sums over the workgroup's rows
@@ -1160,7 +1344,9 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
     // x2 = dz2
     if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return x2[ft][rt][r]; }, acc + sg.b2, fbase, j, g);
     if (!PPO_DIAG_SKIP(5)) store_tile_rows<FT, RT>(a.DZ2[trunk], H, x2, m0, a.M, rbase, fbase, j, g);
-    lds_barrier();  // dW3 readers of h2 are done
+    // the head backward's readers of h2 / GG (ACT) are done: LN2-backward's exchange barrier (rows_total2)
+    // follows every wave's head backward; without it (tanh, WF = 1) wait here
+    if constexpr (!PPO_V_BAR || !LN || WF == 1) lds_barrier();
     if constexpr (BX) lds_store_pieces<FT, RT, LDB, H / 2>(ACT, x2, rbase, fbase, j, g);
     else lds_store_tile<FT, RT, LDA>(ACT, x2, rbase, fbase, j, g);
     lds_barrier();
@@ -1197,6 +1383,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
           }
       }
       rows_total2<WF, RT, R>(s1, s2, RED2, RED3, wf, rbase, j, g);
+      if constexpr (EARLY) commit(it + gridDim.x);  // the next tile's rows (see EARLY)
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) { s1[rt] *= (1.0f / H); s2[rt] *= (1.0f / H); }
       if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return dh[ft][rt][r]; }, acc + sg.be1, fbase, j, g);
@@ -1790,7 +1977,8 @@ PPO_DEV void upd32_body(const UpdArgs& a) {
 
     // ---------------- loss and its gradient wrt the head pre-activations (k_upd's) ----------------
     float* ITM = SCR;
-    upd_loss<true, R, ITS, LDG>(a, trunk, tid, m0, c, adv_mean, adv_std, PRE, GG, ROWS, ACTN, ITM, lst);
+    upd_loss<true, R, ITS, LDG>(a, trunk, tid, m0, c, adv_mean, adv_std,
+                                [&](int row, int h) { return PRE[row * LDG + h]; }, PRE, GG, ROWS, ACTN, ITM, lst);
     lds_barrier();
     PPO_STAMP(7);
     if (tid < nh) {
@@ -1983,6 +2171,145 @@ __global__ __launch_bounds__(256, 2) void k_upd32(UpdArgs a) {
   else upd32_body<NTO, NHT, KL1>(a);
 }
 
+// =============================================================================================
+// k_vbx: the rollout's critic pass (values[i] = critic(obs[i]) over n stored rows, ac:641-698's
+// value per step and ac:761's bootstrap; the agent module ac:150-249) with k_upd's forward
+// arithmetic: layer 1 on 16x16x4 fp32 MFMAs, LayerNorm statistics merged across the four feature
+// waves (ln_rows), layer 2 as six split-bf16 piece products (mm_bx over the critic's W2 pieces that
+// k_adam / k_swizzle keep), the value head as k_upd's per-row VALU dot product and head-partial sum.
+// A workgroup of 4 waves walks 32-row tiles (each wave 64 features); the next tile's observations
+// are loaded into registers under the current tile's GEMMs. Every row is computed by the same code
+// wherever it sits in a tile, so a row's value does not depend on n or on the other rows (the
+// per-step host-env rollout and the persistent rollout agree bitwise). Against the fp64 oracle as
+// the act kernels are (test_values_bx_vs_oracle).
+// =============================================================================================
+template <int NTO, int KL1>
+__global__ __launch_bounds__(256, 2) void k_vbx(ValuesArgs a) {
+  using GE = Geo<256, NTO, 1, true>;
+  constexpr int H = 256, FT = GE::FT, RT = GE::RT, WF = GE::WF, R = GE::R, NT = GE::NT, OP = GE::OP;
+  constexpr int LDX = GE::LDX, LDB = GE::LDB;
+  static_assert(GE::WR == 1 && R == 32, "k_vbx: 4 feature waves, 32-row tiles");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* XN = lds;
+  float* ACT = XN + R * LDX;
+  float* RED = ACT + R * LDB;
+  float* SPAR = RED + 4 * WF * R;  // gamma1 | beta1 | gamma2 | beta2 | w3 | obs mean | obs std
+  float *RED0 = RED, *RED1 = RED + WF * R, *RED2 = RED + 2 * WF * R, *RED3 = RED + 3 * WF * R;
+  float *SG1 = SPAR, *SBE1 = SPAR + H, *SG2 = SPAR + 2 * H, *SBE2 = SPAR + 3 * H, *SW3 = SPAR + 4 * H;
+  float *SOM = SPAR + 5 * H, *SOS = SOM + OP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, g = lane >> 4;
+  const int wf = wave, fbase = wf * FT * 16;
+  const PackedLayout& K = a.K;
+  const TrunkDev& T = K.tr[0];
+  const float* __restrict__ P = a.P;
+  const PBuf pb = make_pbuf(P, K.size);
+  const PBuf wsw = make_pbuf(a.WSW, (int)sw_size(H, OP));
+  const PBuf wbx = make_pbuf(a.WBX, (int)bx_size(H));
+  const int O = K.O;
+  const int w1lane = ((fbase >> 4) * NTO * 64 + lane) * 4;
+  const int w2blane = ((fbase >> 4) * (NT / 2) * 3 * 64 + lane) * 4;
+  const float* xn_in = XN + j * LDX + 4 * g;
+  const float* actb_in = ACT + j * LDB + 4 * g;
+  const long ntiles = (a.n + R - 1) / R;
+  constexpr int NG = (R * OP + 255) / 256;
+  float vg[NG];
+  auto load_obs = [&](long it) {
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int idx = tid + 256 * k, row = idx / OP, f = idx - row * OP;
+      const long m = it * R + row;
+      const bool ok = it < ntiles && idx < R * OP && m < a.n && f < O;
+      const float v = a.obs[(ok ? m : 0) * O + (ok ? f : 0)];
+      vg[k] = ok ? v : 0.f;
+    }
+  };
+  load_obs(blockIdx.x);
+  for (int i = tid; i < 5 * H + 2 * OP; i += 256) {
+    const int v = i / H, f = i - v * H;
+    float x;
+    if (v < 4) x = P[(v == 0 ? T.g1 : v == 1 ? T.be1 : v == 2 ? T.g2 : T.be2) + f];
+    else if (v == 4) x = P[K.cW3 + f];
+    else {
+      const int q = i - 5 * H, o = q % OP;
+      x = q < OP ? 0.f : 1.f;
+      if (o < O) x = P[(q < OP ? K.omean : K.ostd) + o];
+    }
+    SPAR[i] = x;
+  }
+  const float cb3 = P[K.cb3];
+  for (long it = blockIdx.x; it < ntiles; it += gridDim.x) {
+    const long m0 = it * R;
+    lds_barrier();  // the previous tile's XN / ACT / RED readers are done; SPAR staged (first tile)
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int idx = tid + 256 * k, row = idx / OP, f = idx - row * OP;
+      if (idx < R * OP) {
+        float v = vg[k];
+        if (m0 + row < a.n && f < O) v = (v - SOM[f]) / SOS[f];
+        XN[row * LDX + f] = v;
+      }
+    }
+    load_obs(it + gridDim.x);
+    lds_barrier();
+    // layer 1, LayerNorm, ReLU -> split-bf16 pieces in LDS
+    f4 z[FT][RT];
+    init_bias<FT, RT>(z, pb, T.b1 + fbase + 4 * g);
+    mm_fr<FT, RT, NTO, LDX, KL1>(z, wsw, w1lane, xn_in);
+    {
+      float mu1[RT], rs1[RT];
+      ln_rows<FT, RT, WF, R, H>(z, mu1, rs1, RED0, RED1, wf, 0, j, g);
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) {
+        const f4 gm = lds_f4(SG1 + fbase + 4 * g + 16 * ft), bt = lds_f4(SBE1 + fbase + 4 * g + 16 * ft);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float xh = (z[ft][rt][r] - mu1[rt]) * rs1[rt];
+            const float y = __fmaf_rn(gm[r], xh, bt[r]);
+            z[ft][rt][r] = y > 0.0f ? y : 0.0f;
+          }
+      }
+    }
+    lds_store_pieces<FT, RT, LDB, H / 2>(ACT, z, 0, fbase, j, g);
+    lds_barrier();
+    // layer 2 (split-bf16), LayerNorm, ReLU, value head
+    f4 x2[FT][RT];
+    init_bias<FT, RT>(x2, pb, T.b2 + fbase + 4 * g);
+    mm_bx<FT, RT, NT, LDB>(x2, wbx, w2blane, actb_in);
+    float mu2[RT], rs2[RT];
+    ln_rows<FT, RT, WF, R, H>(x2, mu2, rs2, RED2, RED3, wf, 0, j, g);
+    float pv[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) pv[rt] = 0.f;
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      const f4 gm = lds_f4(SG2 + fbase + 4 * g + 16 * ft), bt = lds_f4(SBE2 + fbase + 4 * g + 16 * ft);
+      const f4 w = lds_f4(SW3 + fbase + 4 * g + 16 * ft);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float xh = (x2[ft][rt][r] - mu2[rt]) * rs2[rt];
+          const float v = __fmaf_rn(gm[r], xh, bt[r]);
+          pv[rt] = fmaf(w[r], v > 0.0f ? v : 0.0f, pv[rt]);
+        }
+    }
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      pv[rt] = row_allreduce(pv[rt]);
+      if (g == 0) RED0[wf * R + 16 * rt + j] = pv[rt];  // LN1's reads of RED0 precede LN2's exchange
+    }
+    lds_barrier();
+    if (tid < R && m0 + tid < a.n) {
+      float sv = 0.f;
+#pragma unroll
+      for (int w = 0; w < WF; ++w) sv += RED0[w * R + tid];
+      a.values[m0 + tid] = sv + cb3;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side: geometry, LDS size, dispatch
 // ---------------------------------------------------------------------------------------------
@@ -2116,6 +2443,32 @@ int launch_upd(const UpdArgs& a, int nh_actor, int nblocks, size_t lds_bytes, hi
     hipLaunchKernelGGL((k_upd<H, KIND, NTO, NHT, KL, false>), grid, dim3(256), lds_bytes, s, b);
     return 0;
   });
+}
+
+// k_vbx for the LayerNorm-Beta agent at H = 256 (the critic pass of the persistent and per-step
+// rollouts when the bx pieces exist); -1: not covered here (the caller runs k_values)
+int launch_vbx(const ValuesArgs& a, hipStream_t s) {
+  if (!a.WBX || a.K.H != 256 || a.K.kind != PPO_NET_LN_BETA || a.n <= 0) return -1;
+  const int nto = a.K.OP / 16, kl = (a.K.O == 16 * (nto - 1) + 1) ? 1 : 4;
+  auto go = [&](auto kern, int nto_) {
+    using GE = Geo<256, 1, 1, true>;
+    const int OP = 16 * nto_, LDX = OP + 4;
+    const size_t lds = (size_t)(GE::R * LDX + GE::R * GE::LDB + 4 * GE::WF * GE::R + 5 * 256 + 2 * OP) * sizeof(float);
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return -2;
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const long ntiles = (a.n + GE::R - 1) / GE::R;
+    const long grid = ntiles < 2L * ncu ? ntiles : 2L * ncu;  // two resident workgroups per CU
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), lds, s, a);
+    return 0;
+  };
+  if (nto == 1) return go(k_vbx<1, 4>, 1);
+  if (nto == 2 && kl == 1) return go(k_vbx<2, 1>, 2);
+  if (nto == 2) return go(k_vbx<2, 4>, 2);
+  if (nto == 7) return go(k_vbx<7, 4>, 7);
+  return -1;
 }
 
 #ifdef PPO_STAMPS

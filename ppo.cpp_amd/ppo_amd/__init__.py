@@ -140,6 +140,7 @@ SYMBOLS = [
     ("ppo_get_action_and_value", _I, [_VP, _I, _FP, _I, _FP, _L, _L, _FP, _FP, _FP, _FP, _VP]),
     ("ppo_get_value", _I, [_VP, _I, _FP, _FP, _VP]),
     ("ppo_rollout_act", _I, [_VP, _I, _I, _I, _FP, _FP, _FP, _VP]),
+    ("ppo_rollout_values", _I, [_VP, _VP]),
     ("ppo_rollout_reward", _I, [_VP, _I, _I, _I, _FP, _VP]),
     ("ppo_compute_gae", _I, [_VP, _FP, _FP, _I, _VP]),
     ("ppo_gae_from_values", _I, [_VP, _FP, _FP, _I, _VP]),
@@ -536,6 +537,10 @@ class Agent:
     def rollout_act(self, step, e0, e1, next_obs: DeviceArray, next_done: DeviceArray, action_out=None):
         check(lib().ppo_rollout_act(self.h, step, e0, e1, next_obs.ptr, next_done.ptr,
                                     action_out.ptr if action_out else None, None))
+
+    def rollout_values(self):
+        """The deferred critic pass of rollout_act (values of every step acted since the last pass)."""
+        check(lib().ppo_rollout_values(self.h, None))
 
     def rollout_reward(self, step, e0, e1, reward: DeviceArray):
         check(lib().ppo_rollout_reward(self.h, step, e0, e1, reward.ptr, None))

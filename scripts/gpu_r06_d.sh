@@ -1,0 +1,14 @@
+#!/bin/bash
+# k_upd combination A/B (off / chan+bar+pre+ch2 / + tile-top barrier) and the update parity tests.
+set -o pipefail
+TAG=${1:-r06d}
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+cd $R
+timeout -k 10 700 python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu \
+  tests/test_gpu_update_headline.py tests/test_gpu_golden_widths.py tests/test_gpu_parity.py \
+  tests/test_gpu_e2e_teacher.py tests/test_gpu_e2e.py tests/test_gpu_rollout.py > $OUT/tests.txt 2>&1 || { echo "tests failed"; grep -E "FAILED|Error" $OUT/tests.txt | head; tail -30 $OUT/tests.txt; exit 1; }
+tail -2 $OUT/tests.txt
+ARMS="off:ppo.cpp_amd/lib/libppo_hip_off.so:- notop:ppo.cpp_amd/lib/libppo_hip_notop.so:- new:-:-" \
+  BENCH_ARGS="--no-fp32-leg" bash scripts/gpu_ab_multi.sh $TAG 3

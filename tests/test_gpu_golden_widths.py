@@ -76,6 +76,7 @@ def test_act_vs_golden_at_reference_width(pre, kind):
     ag.load_params(p)
     done = DeviceArray.from_numpy(np.zeros(n, np.float32))
     ag.rollout_act(0, 0, n, x, done)
+    ag.rollout_values()  # the critic pass (deferred where values_mfma=bx6 applies)
     np.testing.assert_array_equal(ag.buffer(ppo_amd.BUF_OBS, (2, n, meta["O"])).numpy()[0], d["x"])
     np.testing.assert_allclose(ag.buffer(ppo_amd.BUF_VALUES, (2, n)).numpy()[0], d["value"], rtol=2e-5, atol=2e-5)
     L = O.layout_init(meta["kind"], meta["O"], meta["A"], meta["H"])

@@ -610,3 +610,36 @@ def test_weight_copies_track_adam(net_kind, hidden, env_id, O_):
     np.testing.assert_array_equal(pa, pb)
     assert sa == sb
     tr.close()
+
+
+def test_values_bx_vs_oracle_at_metric_size():
+    """The rollout's critic pass at the metric shape (T x E = 128 x 4 096, AC HalfCheetah 2 x 256):
+    k_vbx (values_mfma=auto: layer 2 as six split-bf16 piece products, fp32 accumulation) over the
+    stored observations of a persistent rollout, against the fp64-accumulating C oracle's critic on
+    4 096 sampled rows (ac:655 values[step], the agent module ac:150-249), at the act tests' value bar
+    (rtol 2e-5, atol 2e-5). The fp32-MFMA critic of the API act kernel (k_act3) runs the same rows and
+    both errors are printed; the split form must stay within 2x of the fp32 form's error + 1e-6."""
+    E, T = 4096, 128
+    cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=E, num_steps=T, total_timesteps=E * T * 2)
+    tr = ppo_amd.Trainer(cfg)
+    try:
+        assert tr.agent.kernel_info().startswith("update=k_upd/bx6")
+        tr.rollout()
+        tr.agent.sync()
+        O_ = 17
+        obs = tr.agent.buffer(ppo_amd.BUF_OBS, (T, E, O_)).numpy().reshape(-1, O_)
+        vals = tr.agent.buffer(ppo_amd.BUF_VALUES, (T, E)).numpy().reshape(-1)
+        rng = np.random.default_rng(31)
+        idx = np.sort(rng.choice(T * E, 4096, replace=False))
+        x = np.ascontiguousarray(obs[idx])
+        p = tr.agent.params()
+        L = O.layout_init(1, O_, 6, 256)
+        _, _, _, ov = O.get_action_and_value(L, p, x, 2)
+        f32v = tr.agent.get_value(DeviceArray.from_numpy(x)).numpy()
+    finally:
+        tr.close()
+    eb, ef = np.abs(vals[idx] - ov), np.abs(f32v - ov)
+    print(f"\ncritic vs oracle, max |d|: k_vbx (bx6) {eb.max():.2e}, k_act3 (fp32 MFMA) {ef.max():.2e}; "
+          f"rms {np.sqrt((eb ** 2).mean()):.2e} / {np.sqrt((ef ** 2).mean()):.2e}")
+    np.testing.assert_allclose(vals[idx], ov, rtol=2e-5, atol=2e-5)
+    assert np.sqrt((eb ** 2).mean()) <= 2 * np.sqrt((ef ** 2).mean()) + 1e-6

@@ -126,6 +126,11 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            ppo:447-467, ac:759-779) or as a segmented scan over the steps (k_gae_scan: 16
  *                            segments per 64 envs, within 1e-5 of the serial form and of the golden
  *                            vectors); auto: the scan from 512 steps (cfg1 / cfg2's T = 2 048), serial below
+ *   upd_split=auto|1|2|4|8   the minibatch's fused update (k_upd + k_dwf; hidden 256, obs_dim <= 32) as
+ *                            n launch pairs over consecutive M / n rows of its permutation: one pair's
+ *                            hand-off rows (H1 / DZ1 / DZ2 / Xn, ~6 KB per row) stay cache-resident
+ *                            between k_upd's stores and k_dwf's reads; the pairs' partial sums are added
+ *                            together (the same gradient up to summation order)
  *   values_mfma=auto|bx6|f32 the rollout's critic pass (values of the stored rows and the bootstrap,
  *                            ac:655 / :761): k_vbx, layer 2 as k_upd's six split-bf16 piece products
  *                            (bx6; auto where upd_mfma=bx6 applies: the per-step act kernels then skip

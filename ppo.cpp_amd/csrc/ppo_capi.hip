@@ -161,6 +161,14 @@ struct ppo_ctx {
   // run once over the stored rows: the per-step act kernels skip the critic and leave it pending
   int values_bx = 0;
   std::atomic<int> values_pending{0};  // steps [0, n) of the rollout storage whose values are not computed yet
+  // the minibatch's k_upd + dW in msplit launch pairs of Mq rows each (create option upd_split): the
+  // hand-off rows (H1 / DZ1 / DZ2 / Xn) of one pair are ~M / msplit x 6 KB, small enough to stay in the
+  // 256 MB Infinity Cache between k_upd's stores and k_dwf's reads
+  int msplit = 1, Mq = 0;
+  // 1: k_upd writes no H1 rows, only each row's layer-1 LayerNorm (mean, 1 / std) into LNS[trunk]
+  // ([M][2]), and k_dwf_bx recomputes H1 bitwise (create option h1_handoff)
+  int h1_recomp = 0;
+  float* LNS[2] = {nullptr, nullptr};
   int upd32_mix = 0;       // k_upd32 with the actor trunk on k_upd's body (upd_mfma=mix)
   bool use_upd2 = false;  // two-trunk k_upd2 (ppo_update_narrow.hip, H = 64 tanh agent)
   int rollout_kernel = 0;   // AC persistent rollout: 0 auto, 1 k_rollout (MFMA), 2 k_rollout_v (VALU)
@@ -289,6 +297,8 @@ struct CreateOptions {
   int dw_bx = -1;      // dw_mfma: -1 auto, 0 f32 (fp32 MFMA), 9 / 8 / 6 bf16x9 / x8 / x6 (k_dwf_bx: exact bf16 splits)
   int gae_scan = -1;   // gae=auto (scan from kGaeScanMinT steps) | serial (bit-exact with the reference's loop) | scan
   int values_mfma = -1;  // values_mfma=auto (bx6 where k_upd's bx6 pieces exist) | f32 | bx6
+  int upd_split = 0;     // upd_split=auto|1|2|4|8: minibatch rows per k_upd + dW launch pair (M / n)
+  int h1_handoff = -1;   // h1_handoff=auto|store|recompute: H1 rows from k_upd, or recomputed by k_dwf_bx
   // 1: ppo_update replays its minibatch launches as one captured hipGraph; 0 (default): eager.
   // Snapshots work with it on (ppo_read_snapshot waits for the snapshot's event on the host).
   int update_graph = 0;
@@ -319,6 +329,12 @@ static constexpr int kUpd2BxAuto = 1;
 // k_gae below it (the metric's T = 128: 13 us, < 0.1 % of the iteration). cfg2: 0.186 -> 0.107 ms
 // (profiles/r05/gae_scan/)
 static constexpr int kGaeScanMinT = 512;
+// upd_split=auto: launch pairs per minibatch (see ppo_ctx::msplit); 1 until measured
+static int kUpdSplitAuto(int M) { (void)M; return 1; }
+// h1_handoff=auto: H1 stored. Recomputing it in k_dwf_bx (bitwise the same, test_h1_recompute_is_bitwise_the_
+// stored_h1) took k_upd 0.605 -> 0.573 ms per launch but k_dwf_bx 217 -> 255 us (its extra fp32 MFMAs and a
+// barrier per stage): 15.97 -> 16.04 ms per metric iteration (profiles/r06/h1_recompute/)
+static constexpr bool kH1RecomputeAuto = false;
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
   std::string s(opts);
@@ -344,6 +360,10 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
     else if (k == "dw_slices" && (v == "1" || v == "2")) o->dw_slices = v[0] - '0';
     else if (k == "dw_dma" && (v == "0" || v == "1")) o->dw_dma = v[0] - '0';
     else if (k == "gae" && (v == "auto" || v == "serial" || v == "scan")) o->gae_scan = v == "auto" ? -1 : v == "scan";
+    else if (k == "h1_handoff" && (v == "auto" || v == "store" || v == "recompute"))
+      o->h1_handoff = v == "auto" ? -1 : v == "recompute";
+    else if (k == "upd_split" && (v == "auto" || v == "1" || v == "2" || v == "4" || v == "8"))
+      o->upd_split = v == "auto" ? 0 : v[0] - '0';
     else if (k == "values_mfma" && (v == "auto" || v == "f32" || v == "bx6"))
       o->values_mfma = v == "auto" ? -1 : v == "f32" ? 0 : 6;
     else if (k == "dw_mfma" && (v == "auto" || v == "f32" || v == "bf16x9" || v == "bf16x8" || v == "bf16x6"))
@@ -540,20 +560,48 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
     ppo_destroy(c);
     return fail("ppo_create: values_mfma=bx6 needs the LayerNorm-Beta agent at hidden 256 with upd_mfma=bx6 (auto)");
   }
+  {
+    const bool split_ok = c->use_upd && !c->use_upd2 && !c->use_upd32 && H == 256 && OP <= 32 && c->dw_fused;
+    int S = opt.upd_split > 0 ? opt.upd_split : kUpdSplitAuto(c->M);
+    if (!split_ok) {
+      if (opt.upd_split > 1) {
+        ppo_destroy(c);
+        return fail("ppo_create: upd_split > 1 needs the fused k_upd + k_dwf path (hidden 256, obs_dim <= 32)");
+      }
+      S = 1;
+    }
+    while (S > 1 && c->M < S * 32 * 64) S /= 2;  // keep >= 64 tiles of 32 rows per launch
+    c->msplit = S;
+    c->Mq = S == 1 ? c->M : (((c->M + S - 1) / S + 31) & ~31);
+    while (c->msplit > 1 && (long)(c->msplit - 1) * c->Mq >= c->M) --c->msplit;  // no empty split
+  }
   for (int k = 0; k < 2; ++k)
-    rc |= dmalloc(&c->slab[k], (size_t)std::max(c->nblk, c->upd_nblk) * c->sg[k].size);
+    rc |= dmalloc(&c->slab[k], (size_t)c->msplit * std::max(c->nblk, c->upd_nblk) * c->sg[k].size);
   c->wlds_off = 4 * std::max(c->sg[0].size, c->sg[1].size);
   c->wlds_off = (c->wlds_off + 63) & ~63;
   c->lds_bytes = ((size_t)c->wlds_off + 2 * (size_t)H * 16) * sizeof(float);
   // dW split-K: ~128 row chunks per trunk (256 workgroups for the two trunks), 16-row multiples
   // (the chunking does not depend on dw_fused, so k_dwf and the two-phase k_dw sum the same chunks)
-  c->dw_slices = dw_slices(c->M, H, OP, true);
+  // (with upd_split: the geometry of one Mq-row pair; every pair writes its own nchunks partial rows)
+  c->dw_slices = dw_slices(c->Mq, H, OP, true);
   if (opt.dw_slices && H == 256 && OP <= 32) c->dw_slices = opt.dw_slices;  // k_dwf geometry only
-  c->rows_per_chunk = std::max(64, (((c->M + 128 / c->dw_slices - 1) / (128 / c->dw_slices)) + 15) & ~15);
+  c->rows_per_chunk = std::max(64, (((c->Mq + 128 / c->dw_slices - 1) / (128 / c->dw_slices)) + 15) & ~15);
   if (c->use_upd2) c->rows_per_chunk = std::max(32, (((c->M + 255) / 256) + 31) & ~31);  // k_dw2: both trunks
   if (opt.dw_rows && (!c->use_upd2 || opt.dw_rows % 32 == 0)) c->rows_per_chunk = opt.dw_rows;  // k_dw2: 32-row steps
-  c->nchunks = (c->M + c->rows_per_chunk - 1) / c->rows_per_chunk;
-  for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->dwslab[k], (size_t)c->nchunks * (H * H + H * OP));
+  c->nchunks = (c->Mq + c->rows_per_chunk - 1) / c->rows_per_chunk;
+  {
+    const bool rc_ok = c->use_upd && !c->use_upd2 && !c->use_upd32 && cfg->net_kind == PPO_NET_LN_BETA && H == 256 &&
+                       OP <= 32 && c->dw_fused && c->dw_dma && c->dw_bx;
+    if (opt.h1_handoff == 1 && !rc_ok) {
+      ppo_destroy(c);
+      return fail("ppo_create: h1_handoff=recompute needs the LayerNorm-Beta agent at hidden 256 (obs_dim <= 32) with "
+                  "the fused split-bf16 dW (dw_mfma bf16x6/x8/x9)");
+    }
+    c->h1_recomp = rc_ok && (opt.h1_handoff == 1 || (opt.h1_handoff < 0 && kH1RecomputeAuto));
+    if (c->h1_recomp)
+      for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->LNS[k], 2 * (size_t)c->M);
+  }
+  for (int k = 0; k < 2; ++k) rc |= dmalloc(&c->dwslab[k], (size_t)c->msplit * c->nchunks * (H * H + H * OP));
   if (c->upd2_split) rc |= dmalloc(&c->Z1, Mr * 128);
   rc |= dmalloc(&c->normout, 2 + PPO_LAYOUT_MAX_TENSORS + 2);
   rc |= dmalloc(&c->gnpart, (size_t)PPO_LAYOUT_MAX_TENSORS * PPO_GN_SPLIT);
@@ -585,7 +633,7 @@ extern "C" int ppo_destroy(ppo_t* c) {
   for (int b = 0; b < PPO_BUF_COUNT; ++b)
     if (c->buf[b]) (void)hipFree(c->buf[b]);
   for (int k = 0; k < 2; ++k) {
-    float* q[] = {c->H1[k], c->DZ1[k], c->DZ2[k], c->slab[k]};
+    float* q[] = {c->H1[k], c->DZ1[k], c->DZ2[k], c->slab[k], c->LNS[k]};
     for (float* p : q)
       if (p) (void)hipFree(p);
   }
@@ -994,15 +1042,18 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
   u.hw_global = c->upd.hw_global;
   u.trunk_mask = c->upd_trunk_mask;
   u.sched = c->upd_sched;
+  u.h1_skip = c->h1_recomp;
 #ifdef PPO_DIAG
   {
     static const int hot = [] { const char* e = getenv("PPO_UPD2_HOT"); return e ? atoi(e) : 0; }();
     u.hot = hot;
   }
 #endif
-  const int nblk = c->use_upd ? c->upd_nblk : c->nblk;  // workgroups that wrote a slab row
+  const int nblk = c->use_upd ? c->upd_nblk : c->nblk;  // workgroups that wrote a slab row (per launch)
+  const int nsrow = c->msplit * nblk;                     // slab rows of one minibatch (msplit launches)
   for (int k = 0; k < 2; ++k) {
     u.H1[k] = c->H1[k];
+    u.LNS[k] = c->LNS[k];
     u.DZ1[k] = c->DZ1[k];
     u.DZ2[k] = c->DZ2[k];
     u.slab[k] = c->slab[k];
@@ -1015,6 +1066,8 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
   dw.fused = c->dw_fused;
   dw.dma = c->dw_dma;
   dw.bx = c->dw_dma ? c->dw_bx : 0;
+  dw.h1_recompute = c->h1_recomp;
+  dw.kl1 = (c->K.O == 16 * (c->K.OP / 16 - 1) + 1) ? 1 : 4;
   dw.xn = c->Xn;
   dw.obs = c->buf[PPO_BUF_OBS];
   dw.O = c->K.O;
@@ -1023,6 +1076,11 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
   for (int k = 0; k < 2; ++k) {
     dw.dz2[k] = c->DZ2[k];
     dw.h1[k] = c->H1[k];
+    dw.lns[k] = c->LNS[k];
+    dw.w1sw[k] = c->WSW[k];
+    dw.b1[k] = c->P + c->K.tr[k].b1;
+    dw.g1[k] = c->P + c->K.tr[k].g1;
+    dw.be1[k] = c->P + c->K.tr[k].be1;
     dw.dz1[k] = c->DZ1[k];
     dw.slab[k] = c->dwslab[k];
   }
@@ -1038,30 +1096,30 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
   const bool ln = cfg.net_kind == PPO_NET_LN_BETA;
   for (int k = 0; k < 2; ++k) {
     const TrunkDev& T = c->K.tr[k];
-    seg(c->dwslab[k], dw.slab_stride, c->nchunks, H * H, c->G + T.W2, 1.f);
-    seg(c->dwslab[k] + (long)H * H, dw.slab_stride, c->nchunks, H * OP, c->G + T.W1, 1.f);
+    seg(c->dwslab[k], dw.slab_stride, c->msplit * c->nchunks, H * H, c->G + T.W2, 1.f);
+    seg(c->dwslab[k] + (long)H * H, dw.slab_stride, c->msplit * c->nchunks, H * OP, c->G + T.W1, 1.f);
     const SmallGradLayout& g = c->sg[k];
     const float* sl = c->slab[k];
-    seg(sl + g.b1, g.size, nblk, H, c->G + T.b1, 1.f);
-    seg(sl + g.b2, g.size, nblk, H, c->G + T.b2, 1.f);
+    seg(sl + g.b1, g.size, nsrow, H, c->G + T.b1, 1.f);
+    seg(sl + g.b2, g.size, nsrow, H, c->G + T.b2, 1.f);
     if (ln) {
-      seg(sl + g.g1, g.size, nblk, H, c->G + T.g1, 1.f);
-      seg(sl + g.be1, g.size, nblk, H, c->G + T.be1, 1.f);
-      seg(sl + g.g2, g.size, nblk, H, c->G + T.g2, 1.f);
-      seg(sl + g.be2, g.size, nblk, H, c->G + T.be2, 1.f);
+      seg(sl + g.g1, g.size, nsrow, H, c->G + T.g1, 1.f);
+      seg(sl + g.be1, g.size, nsrow, H, c->G + T.be1, 1.f);
+      seg(sl + g.g2, g.size, nsrow, H, c->G + T.g2, 1.f);
+      seg(sl + g.be2, g.size, nsrow, H, c->G + T.be2, 1.f);
     }
     if (k == 0) {
-      seg(sl + g.hW, g.size, nblk, H, c->G + c->K.cW3, 1.f);
-      seg(sl + g.hb, g.size, nblk, 1, c->G + c->K.cb3, 1.f);
+      seg(sl + g.hW, g.size, nsrow, H, c->G + c->K.cW3, 1.f);
+      seg(sl + g.hb, g.size, nsrow, 1, c->G + c->K.cb3, 1.f);
     } else if (!ln) {
-      seg(sl + g.hW, g.size, nblk, A * H, c->G + c->K.aW3, 1.f);
-      seg(sl + g.hb, g.size, nblk, A, c->G + c->K.ab3, 1.f);
-      seg(sl + g.ls, g.size, nblk, A, c->G + c->K.logstd, 1.f);
+      seg(sl + g.hW, g.size, nsrow, A * H, c->G + c->K.aW3, 1.f);
+      seg(sl + g.hb, g.size, nsrow, A, c->G + c->K.ab3, 1.f);
+      seg(sl + g.ls, g.size, nsrow, A, c->G + c->K.logstd, 1.f);
     } else {
-      seg(sl + g.hW, g.size, nblk, A * H, c->G + c->K.aW3, 1.f);
-      seg(sl + g.hW + A * H, g.size, nblk, A * H, c->G + c->K.bW3, 1.f);
-      seg(sl + g.hb, g.size, nblk, A, c->G + c->K.ab3, 1.f);
-      seg(sl + g.hb + A, g.size, nblk, A, c->G + c->K.bb3, 1.f);
+      seg(sl + g.hW, g.size, nsrow, A * H, c->G + c->K.aW3, 1.f);
+      seg(sl + g.hW + A * H, g.size, nsrow, A * H, c->G + c->K.bW3, 1.f);
+      seg(sl + g.hb, g.size, nsrow, A, c->G + c->K.ab3, 1.f);
+      seg(sl + g.hb + A, g.size, nsrow, A, c->G + c->K.bb3, 1.f);
     }
   }
   const int stats_seg0 = ns;  // filled per minibatch below
@@ -1117,23 +1175,46 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
         ProfScope ps(c, PK_L1G, s);
         if (launch_l1g(u, s) != 0) return fail("k_l1g: unsupported configuration");
       }
-      {
-        ProfScope ps(c, PK_FWDBWD, s);
-        const int rc_ = c->use_upd2  ? launch_upd2(u, c->upd_nblk, c->upd.lds_bytes, s, c->upd2_split)
-                        : c->use_upd32 ? launch_upd32(u, c->sg[1].nh, c->upd_nblk, c->upd.lds_bytes, s, c->upd32_mix)
-                        : c->use_upd ? launch_upd(u, c->sg[1].nh, c->upd_nblk, c->upd.lds_bytes, s)
-                                     : launch_fwdbwd(u, nblk, c->lds_bytes, s);
-        if (rc_ != 0) return fail("no update kernel for this configuration");
-      }
-      {
-        ProfScope ps(c, PK_DW2, s);
-        const int rc_ = c->use_upd2 ? launch_dw2(dw, OP, c->nchunks, s) : launch_dw(dw, H, OP, c->nchunks, s);
-        if (rc_ != 0) return fail("no dW kernel for this configuration");
+      // msplit > 1: launch pairs over consecutive Mq-row ranges of the minibatch's permutation; each pair's
+      // hand-off rows start at row 0 of the hand-off buffers (reused while cache-resident), its slab rows
+      // and dW partial rows follow the previous pair's (the column sums add them all, in pair order);
+      // the loss scale stays 1 / M of the whole minibatch
+      for (int q = 0; q < c->msplit; ++q) {
+        const int mq = std::min(c->Mq, M - q * c->Mq);
+        UpdArgs uq = u;
+        DwArgs dq = dw;
+        if (c->msplit > 1) {
+          uq.perm = u.perm + (size_t)q * c->Mq;
+          uq.M = mq;
+          dq.M = mq;
+          for (int k = 0; k < 2; ++k) {
+            uq.slab[k] = c->slab[k] + (size_t)q * nblk * c->sg[k].size;
+            dq.slab[k] = c->dwslab[k] + (size_t)q * c->nchunks * dw.slab_stride;
+          }
+        }
+        {
+          ProfScope ps(c, PK_FWDBWD, s);
+          const int rc_ = c->use_upd2  ? launch_upd2(uq, c->upd_nblk, c->upd.lds_bytes, s, c->upd2_split)
+                          : c->use_upd32 ? launch_upd32(uq, c->sg[1].nh, c->upd_nblk, c->upd.lds_bytes, s, c->upd32_mix)
+                          : c->use_upd ? launch_upd(uq, c->sg[1].nh, c->upd_nblk, c->upd.lds_bytes, s)
+                                       : launch_fwdbwd(uq, nblk, c->lds_bytes, s);
+          if (rc_ != 0) return fail("no update kernel for this configuration");
+        }
+        {
+          ProfScope ps(c, PK_DW2, s);
+          const int nch = (mq + c->rows_per_chunk - 1) / c->rows_per_chunk;
+          const int rc_ = c->use_upd2 ? launch_dw2(dq, OP, c->nchunks, s) : launch_dw(dq, H, OP, nch, s);
+          if (rc_ != 0) return fail("no dW kernel for this configuration");
+          if (nch < c->nchunks && !c->use_upd2)  // a shorter last pair: its unused partial rows must add 0
+            for (int k = 0; k < 2; ++k)
+              HIP_TRY(hipMemsetAsync(dq.slab[k] + (size_t)nch * dw.slab_stride, 0,
+                                     sizeof(float) * (size_t)(c->nchunks - nch) * dw.slab_stride, s));
+        }
       }
       float* st = c->mbstats + 8 * gi;
-      cs.seg[stats_seg0 + 0] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_PG, st + ST_PG, c->sg[1].size, nblk, 1, 1.f / M};
-      cs.seg[stats_seg0 + 1] = ColsumSeg{c->slab[0] + c->sg[0].stats + ST_V, st + ST_V, c->sg[0].size, nblk, 1, 0.5f / M};
-      cs.seg[stats_seg0 + 2] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_ENT, st + ST_ENT, c->sg[1].size, nblk, 4, 1.f / M};
+      cs.seg[stats_seg0 + 0] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_PG, st + ST_PG, c->sg[1].size, nsrow, 1, 1.f / M};
+      cs.seg[stats_seg0 + 1] = ColsumSeg{c->slab[0] + c->sg[0].stats + ST_V, st + ST_V, c->sg[0].size, nsrow, 1, 0.5f / M};
+      cs.seg[stats_seg0 + 2] = ColsumSeg{c->slab[1] + c->sg[1].stats + ST_ENT, st + ST_ENT, c->sg[1].size, nsrow, 4, 1.f / M};
       {
         ProfScope ps(c, PK_COLSUM, s);
         launch_colsum(cs, ns, maxlen, s);
@@ -1407,7 +1488,8 @@ extern "C" int ppo_kernel_info(const ppo_t* c, char* buf, int len) {
   const bool fused = c->dw_fused && H == 256 && (OP == 16 || OP == 32);  // launch_dw's dispatch
   const std::string bxs = c->dw_bx ? "/bf16x" + std::to_string(c->dw_bx) : "/f32";
   std::string dw = c->use_upd2 ? (c->dw_dma && OP == 384 && c->K.O % 4 == 0 ? "k_dw2_dma" + bxs : "k_dw2")
-                   : fused ? (!c->dw_dma ? "k_dwf" : c->dw_bx ? "k_dwf_bx/bf16x" + std::to_string(c->dw_bx) : "k_dwf_dma/f32")
+                   : fused ? (!c->dw_dma ? "k_dwf" : c->dw_bx ? "k_dwf_bx/bf16x" + std::to_string(c->dw_bx) + (c->h1_recomp ? "/h1rc" : "")
+                                                        : "k_dwf_dma/f32")
                    : (c->dw_dma && H == 256 && OP == 112) ? "k_dw_dma" + bxs
                                                           : "k_dw";
   const std::string vals = rollout_supported(c->K) != 0 ? "k_act" : c->values_bx ? "k_vbx/bx6"

@@ -1276,13 +1276,30 @@ __global__ __launch_bounds__(512) void k_dwf_dma(DwArgs a) {
 // the same count as k_dwf_dma's 8 k-steps) and splits each value once (v_and / v_sub / v_perm).
 // Staging (LDS DMA, three buffers, two stages ahead) is k_dwf_dma's.
 // =============================================================================================
-template <int H, int OP, int NSL, int NP>
+// RC (DwArgs::h1_recompute): the stages carry DZ2 | DZ1 | Xn | the rows' layer-1 LayerNorm statistics
+// (64 floats); H1 of a stage is recomputed into one buffer H1B behind the three stages, from the staged Xn
+// rows, W1 (swizzled copy, staged once per workgroup in W1S) and the bias / LayerNorm affine (PRM) —
+// k_upd's chain, so bitwise the H1 rows k_upd would have stored; k_upd then writes 8 bytes per row
+// instead of 1 KB (the hand-off's H1 third).
+template <int H, int OP, bool RC>
+struct DwbxGeo {
+  static constexpr int KS = 16, LDH = H, LDX = OP;
+  static constexpr int oH1 = RC ? 0 : KS * LDH;  // (RC: H1 lives in H1B)
+  static constexpr int oDZ1 = RC ? KS * LDH : 2 * KS * LDH;
+  static constexpr int oXN = RC ? 2 * KS * LDH : 3 * KS * LDH;
+  static constexpr int oLNS = oXN + KS * LDX;     // RC: [16][2] (mean, 1 / std) + 32 floats the DMA zero-fills
+  static constexpr int STG = oXN + KS * LDX + (RC ? 64 : 0);
+  static constexpr int oH1B = 3 * STG, oW1S = oH1B + KS * LDH, oPRM = oW1S + H * OP;
+  static constexpr int total = RC ? oPRM + 3 * H : 3 * STG;  // floats
+};
+template <int H, int OP, int NSL, int NP, bool RC = false>
 __global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  using GE = DwbxGeo<H, OP, RC>;
   constexpr int KS = 16, NBUF = 3;
   constexpr int LDH = H, LDX = OP;
-  constexpr int oH1 = KS * LDH, oDZ1 = 2 * KS * LDH, oXN = 3 * KS * LDH;
-  constexpr int STG = 3 * KS * LDH + KS * LDX;
+  constexpr int oH1 = GE::oH1, oDZ1 = GE::oDZ1, oXN = GE::oXN;
+  constexpr int STG = GE::STG;
   static_assert(H == 256 && (OP == 16 || OP == 32), "k_dwf_bx geometry");
   constexpr int NXI = KS * OP / 256;
   constexpr int TOW = 2 / NSL, TIW = 4;
@@ -1301,6 +1318,26 @@ __global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
   const PBuf bdz2 = make_pbuf(a.dz2[trunk], (int)(rows_bytes / 4)), bh1 = make_pbuf(a.h1[trunk], (int)(rows_bytes / 4));
   const PBuf bdz1 = make_pbuf(a.dz1[trunk], (int)(rows_bytes / 4));
   const PBuf bxn = make_pbuf(a.xn, (int)(xn_bytes / 4));
+  const PBuf blns = make_pbuf(RC ? a.lns[trunk] : a.xn, RC ? 2 * a.M : 0);
+  if constexpr (RC) {
+    // W1 (swizzled, H x OP) and the bias / gamma / beta of layer 1, staged once per workgroup; waited for
+    // here, before the stage pipeline's DMAs (whose wait counts assume nothing else in flight)
+    constexpr int NW = H * OP / 4 / 512;
+    f4 wv[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) wv[q] = *reinterpret_cast<const f4*>(a.w1sw[trunk] + 4 * (tid + 512 * q));
+    const float pv1 = tid < H ? a.b1[trunk][tid] : 0.f;
+    const float pv2 = tid < H ? a.g1[trunk][tid] : 0.f;
+    const float pv3 = tid < H ? a.be1[trunk][tid] : 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) *reinterpret_cast<f4*>(lds + GE::oW1S + 4 * (tid + 512 * q)) = wv[q];
+    if (tid < H) {
+      lds[GE::oPRM + tid] = pv1;
+      lds[GE::oPRM + H + tid] = pv2;
+      lds[GE::oPRM + 2 * H + tid] = pv3;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   f16v acc[TOW][TIW], acc1;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -1317,15 +1354,23 @@ __global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
 #endif
 #pragma unroll
     for (int s3 = 0; s3 < 3; ++s3) {
+      if (RC && s3 == 1) continue;  // H1 is recomputed
+      const int dst = s3 == 0 ? 0 : s3 == 1 ? oH1 : oDZ1;
 #pragma unroll
       for (int rr = 0; rr < 2; ++rr) {
         const int r = 2 * wave + rr;
         const long row = mb + r;
         const uint32_t voff = row < m1 ? (uint32_t)((row * H) * 4 + lane * 16) : 0xFFFFFFF0u;
         __builtin_amdgcn_raw_ptr_buffer_load_lds((s3 == 0 ? bdz2 : s3 == 1 ? bh1 : bdz1).r,
-                                                 (__attribute__((address_space(3))) void*)(b + s3 * KS * LDH + r * LDH), 16,
+                                                 (__attribute__((address_space(3))) void*)(b + dst + r * LDH), 16,
                                                  voff, 0, 0, 0);
       }
+    }
+    if (RC && wave == 7) {  // the stage's 16 rows x (mean, 1 / std): 32 dwords (lanes 32..63 zero-fill the pad)
+      const long row = mb + (lane >> 1);
+      const uint32_t voff = lane < 32 && row < m1 ? (uint32_t)(row * 8 + (lane & 1) * 4) : 0xFFFFFFF0u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(blns.r, (__attribute__((address_space(3))) void*)(b + GE::oLNS), 4, voff,
+                                               0, 0, 0);
     }
     if (wave < NXI) {
       const int e = wave * 256 + lane * 4, r = e / OP;
@@ -1340,16 +1385,63 @@ __global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
   issue(m0, 0);
   if (nst > 1) issue(m0 + KS, 1);
   for (int sI = 0; sI < nst; ++sI) {
-    if (sI + 1 < nst) {
-      if (xw) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (sI + 1 < nst) {  // this wave's DMAs of stage sI + 1 stay in flight
+      if constexpr (RC) {
+        if (xw || wave == 7) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        if (xw) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      }
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_barrier();
     if (sI + 2 < nst) issue(m0 + (long)(sI + 2) * KS, (sI + 2) % NBUF);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RC) {
+      // H1 of this stage (16 rows x H): wave w computes features 32 w .. 32 w + 31 as two 16x16 tiles with
+      // k_upd's layer-1 chain, then its LayerNorm + affine + ReLU from the row's stored statistics
+      constexpr int NTO = OP / 16;
+      const int j16 = lane & 15, g16 = lane >> 4, f0 = 32 * wave;
+      const float* stg = lds + (sI % NBUF) * STG;
+      f4 z[2];
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft) z[ft] = *reinterpret_cast<const f4*>(lds + GE::oPRM + f0 + 16 * ft + 4 * g16);
+#pragma unroll
+      for (int kb = 0; kb < NTO; ++kb) {
+        const f4 bv = *reinterpret_cast<const f4*>(stg + oXN + j16 * LDX + 16 * kb + 4 * g16);
+        f4 w[2];
+#pragma unroll
+        for (int ft = 0; ft < 2; ++ft)
+          w[ft] = *reinterpret_cast<const f4*>(lds + GE::oW1S + (((f0 >> 4) + ft) * NTO + kb) * 256 + 4 * lane);
+        const bool full = kb + 1 < NTO || a.kl1 >= 4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (c > 0 && !full) break;
+#pragma unroll
+          for (int ft = 0; ft < 2; ++ft) z[ft] = mfma16(w[ft][c], bv[c], z[ft]);
+        }
+      }
+      const float mu = stg[GE::oLNS + 2 * j16], rs = stg[GE::oLNS + 2 * j16 + 1];
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft) {
+        const int f = f0 + 16 * ft + 4 * g16;
+        const f4 gm = *reinterpret_cast<const f4*>(lds + GE::oPRM + H + f);
+        const f4 bt = *reinterpret_cast<const f4*>(lds + GE::oPRM + 2 * H + f);
+        f4 h;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float xh = (z[ft][r] - mu) * rs;
+          const float y = __fmaf_rn(gm[r], xh, bt[r]);
+          h[r] = y > 0.0f ? y : 0.0f;
+        }
+        *reinterpret_cast<f4*>(lds + GE::oH1B + j16 * LDH + f) = h;
+      }
+      lds_barrier();
+    }
     const float* sb = lds + (sI % NBUF) * STG + (8 * hs) * LDH;  // this lane's rows 8 hs .. 8 hs + 7
+    const float* hb = (RC ? lds + GE::oH1B : lds + (sI % NBUF) * STG + oH1) + (8 * hs) * LDH;
     Split3 as[TOW], a1s, b1s;
     {
       float x[8];
@@ -1373,7 +1465,7 @@ __global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
     for (int v = 0; v < TIW; ++v) {
       float x[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = sb[oH1 + e * LDH + (wi * TIW + v) * 32 + l32];
+      for (int e = 0; e < 8; ++e) x[e] = hb[e * LDH + (wi * TIW + v) * 32 + l32];
       const Split3 bs = split3(x);
 #pragma unroll
       for (int u = 0; u < TOW; ++u) acc[u][v] = mfma_split<NP>(as[u], bs, acc[u][v]);
@@ -2172,10 +2264,14 @@ static int launch_dwf_t(const DwArgs& a0, int nchunks, hipStream_t s) {
 #endif
   // the DMA kernels address their sources through 32-bit buffer descriptors (make_pbuf: int floats)
   if (a.bx && (long)a.M * H < (1L << 29)) {
-    auto k = a.bx == 9 ? k_dwf_bx<H, OP, NSL, 9> : a.bx == 8 ? k_dwf_bx<H, OP, NSL, 8> : k_dwf_bx<H, OP, NSL, 6>;
-    constexpr size_t lds = (size_t)3 * (3 * 16 * H + 16 * OP) * sizeof(float);
-    static bool attr[3] = {false, false, false};
-    const int ai = a.bx == 9 ? 2 : a.bx == 8 ? 1 : 0;
+    const bool rc = a.h1_recompute != 0;
+    auto k = rc ? (a.bx == 9 ? k_dwf_bx<H, OP, NSL, 9, true> : a.bx == 8 ? k_dwf_bx<H, OP, NSL, 8, true>
+                                                              : k_dwf_bx<H, OP, NSL, 6, true>)
+                : (a.bx == 9 ? k_dwf_bx<H, OP, NSL, 9> : a.bx == 8 ? k_dwf_bx<H, OP, NSL, 8> : k_dwf_bx<H, OP, NSL, 6>);
+    const size_t lds = (size_t)(rc ? DwbxGeo<H, OP, true>::total : DwbxGeo<H, OP, false>::total) * sizeof(float);
+    static_assert(DwbxGeo<H, OP, true>::total * sizeof(float) <= 160 * 1024, "k_dwf_bx (H1 recompute) LDS");
+    static bool attr[6] = {false, false, false, false, false, false};
+    const int ai = (a.bx == 9 ? 2 : a.bx == 8 ? 1 : 0) + (rc ? 3 : 0);
     if (!attr[ai]) {
       if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return -2;
       attr[ai] = true;

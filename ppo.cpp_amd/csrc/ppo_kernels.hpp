@@ -106,6 +106,8 @@ struct UpdArgs {
   int hot;                // diagnostic build only (PPO_UPD2_HOT): k_upd2 gathers the rows of its first 8 tiles only
   int bx;                 // k_upd: 1 runs the 256-wide GEMMs as split-bf16 piece products (upd_mfma=bx6);
                           // k_upd2: 2 runs layer 1 that way
+  int h1_skip;            // k_upd: no H1 hand-off rows; LNS gets each row's layer-1 LayerNorm (mean, 1 / std)
+  float* LNS[2];          //   [M][2] per trunk, from which k_dwf_bx recomputes H1 (h1_handoff=recompute)
 };
 
 // k_upd geometry (ppo_update.hip)
@@ -135,6 +137,14 @@ struct DwArgs {
   int dma;            // k_dwf: 1 stages the rows by LDS DMA, three buffers (k_dwf_dma), bitwise k_dwf
   int bx;             // k_dwf: 8 / 9 runs the products as exact bf16 piece products (k_dwf_bx); 0 fp32 MFMA
   int hot;            // diagnostic build only (PPO_DW_HOT): every stage re-reads the chunk's first rows (L2-hot)
+  // h1_recompute (k_dwf_bx, LayerNorm agent): H1 is not read; each 16-row stage recomputes it from the Xn
+  // rows it stages anyway, k_upd's layer-1 chain (W1 swizzled copy, bias init, 16x16x4 fp32 MFMAs in the
+  // same k order, kl1 = k-steps of the last k block) and the rows' LayerNorm statistics lns: bitwise k_upd's
+  // H1
+  int h1_recompute, kl1;
+  const float* lns[2];
+  const float* w1sw[2];                          // WSW[trunk] (W1 swizzled block first)
+  const float *b1[2], *g1[2], *be1[2];           // layer-1 bias and LayerNorm affine (parameters)
 };
 // k_dwf output slices and dW row chunks for a minibatch of M rows: 128 chunks per trunk (one
 // workgroup per CU over both trunks); below 32 K rows 64 chunks x 2 output halves instead — the

@@ -33,28 +33,32 @@
 #ifndef PPO_UPD_EARLY
 #define PPO_UPD_EARLY 0
 #endif
-// A/B switches of round-6 k_upd changes (each 1 = on): merged LayerNorm statistics, the two
-// barriers other exchange barriers cover, head partials summed inside the loss, branch-free
-// prefetch loads, no LDS copy of the critic's h2, the tile top's first barrier (covered by the
-// previous tile's layer-1 backward exchange). Measured per change (profiles/r06/kupd_ab/): EARLY
-// +9.6 %, BF +1.4 % per launch (off); CHAN -1.0 %, BAR -1.0 %, PRE -0.5 %, CH2 0 (on)
+// A/B switches of round-6 k_upd changes (each 1 = on; all off = the round-5 kernel): merged
+// LayerNorm statistics (one exchange per LayerNorm), the two barriers other exchange barriers cover,
+// head partials summed inside the loss, branch-free prefetch loads, no LDS copy of the critic's h2,
+// the tile top's first barrier (covered by the previous tile's layer-1 backward exchange), the next
+// tile's rows committed in the layer-1 backward (EARLY). Measured per launch against all-off
+// (profiles/r06/kupd_ab/): EARLY +9.6 %, BF +1.4 %; CHAN -1.0 %, BAR -1.0 %, PRE -0.5 %, CH2 0 one at
+// a time on one box, but CHAN + BAR + PRE + CH2 together +1.2 % and with TOP +1.5 % on another (the
+// critic's tile 75 K -> 67 K cycles, the actor's 79 K -> 81 K: the launch is the actor's, and the
+// critic's shorter phases leave the actor's loss with fewer partner MFMA gaps). Not kept: all off.
 #ifndef PPO_V_CHAN
-#define PPO_V_CHAN 1
+#define PPO_V_CHAN 0
 #endif
 #ifndef PPO_V_BAR
-#define PPO_V_BAR 1
+#define PPO_V_BAR 0
 #endif
 #ifndef PPO_V_PRE
-#define PPO_V_PRE 1
+#define PPO_V_PRE 0
 #endif
 #ifndef PPO_V_BF
 #define PPO_V_BF 0
 #endif
 #ifndef PPO_V_TOP
-#define PPO_V_TOP 1
+#define PPO_V_TOP 0
 #endif
 #ifndef PPO_V_CH2
-#define PPO_V_CH2 1
+#define PPO_V_CH2 0
 #endif
 
 #ifdef PPO_STAMPS
@@ -88,7 +92,8 @@ __device__ unsigned long long g_upd_stamps[1024 * 4 * PPO_STAMP_TILES * PPO_STAM
     }                                                                                                \
   } while (0)
 // a.sched bits 4..7 skip the H1 / DZ2 / DZ1 / Xn stores, bit 12 the column sums (bias / LayerNorm-affine /
-// critic head weight gradients) (timing experiments only: the gradient is then wrong)
+// critic head weight gradients), bit 13 reads every split-bf16 weight unit from the wave's first one
+// (timing experiments only: the gradient is then wrong)
 #define PPO_DIAG_SKIP(bit) ((a.sched >> (bit)) & 1)
 #else
 #define PPO_STAMP(k) do {} while (0)
@@ -203,12 +208,19 @@ PPO_DEV void mm_fr(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* in) {
 // 0.69 ms per launch (deeper rings spill; profiles/r05/bx6/abm2, abm3)
 constexpr int kBxRing = 3;
 PPO_DEV u32x4 pld4u(PBuf b, int lane_floats, int uni_floats) { return __builtin_bit_cast(u32x4, pld4(b, lane_floats, uni_floats)); }
+// diag_unit0 (stamps build, timing only): every weight unit read from the wave's first unit, so the
+// wave streams 3 KB from the L1 instead of 96 KB from L2 (is the weight stream the GEMMs' bound?)
 template <int FT, int RT, int NKB, int LDB>
-PPO_DEV void mm_bx(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* inb) {
+PPO_DEV void mm_bx(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* inb, bool diag_unit0 = false) {
   static_assert(NKB % 2 == 0, "mm_bx: 32-wide k blocks");
   constexpr int NKK = NKB / 2, U = NKK * FT, D = kBxRing, NS = D + 1, PS = 8 * NKB;
   u32x4 ar[NS][3];
   auto load_unit = [&](int u, u32x4 (&dst)[3]) {
+#ifdef PPO_STAMPS
+    if (diag_unit0) u = 0;
+#else
+    (void)diag_unit0;
+#endif
     const int kk = u / FT, ft = u - kk * FT;
 #pragma unroll
     for (int p = 0; p < 3; ++p) dst[p] = pld4u(wb, wlane, 256 * ((ft * NKK + kk) * 3 + p));
@@ -498,15 +510,41 @@ PPO_DEV void col_sums(Fn v, float* acc, int fbase, int j, int g) {
   acc[fbase + 16 * (j >> 2) + 4 * g + (j & 3)] += x[0];
 }
 
+// PPO_UPD_NT (A/B): the hand-off rows (H1 / DZ2 / DZ1) as non-temporal stores
+#ifndef PPO_UPD_NT
+#define PPO_UPD_NT 0
+#endif
 template <int FT, int RT>
 PPO_DEV void store_tile_rows(float* __restrict__ dst, int ld, const f4 (&v)[FT][RT], int m0, int M, int rbase,
-                             int fbase, int j, int g) {
+                             int fbase, int j, int g, bool diag_blocked = false) {
+#ifdef PPO_STAMPS
+  if (diag_blocked) {  // timing only: the same bytes as 16-row x 64-feature blocks, 1 KB per store instruction
+    const int lane = j + 16 * g;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const long blk = (long)((m0 + rbase) / 16 + rt) * (ld / 64) + fbase / 64;
+      if (m0 + rbase + 16 * rt < M) {
+#pragma unroll
+        for (int ft = 0; ft < FT; ++ft) st4(dst + blk * 1024 + (ft * 64 + lane) * 4, v[ft][rt]);
+      }
+    }
+    return;
+  }
+#else
+  (void)diag_blocked;
+#endif
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     const int m = m0 + rbase + 16 * rt + j;
     if (m < M) {
 #pragma unroll
-      for (int ft = 0; ft < FT; ++ft) st4(dst + (size_t)m * ld + fbase + 16 * ft + 4 * g, v[ft][rt]);
+      for (int ft = 0; ft < FT; ++ft) {
+#if PPO_UPD_NT
+        __builtin_nontemporal_store(v[ft][rt], reinterpret_cast<f4*>(dst + (size_t)m * ld + fbase + 16 * ft + 4 * g));
+#else
+        st4(dst + (size_t)m * ld + fbase + 16 * ft + 4 * g, v[ft][rt]);
+#endif
+      }
     }
   }
 }
@@ -1099,7 +1137,21 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) z[ft][rt][r] = tanhf(z[ft][rt][r]);
     }
-    if (!PPO_DIAG_SKIP(4)) store_tile_rows<FT, RT>(a.H1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
+    if (a.h1_skip) {
+      // h1_handoff=recompute: no H1 rows; k_dwf_bx recomputes them from Xn, W1 and these statistics
+      if constexpr (LN) {
+        if (wf == 0 && g == 0) {
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) {
+            const int m = m0 + rbase + 16 * rt + j;
+            typedef float fl2 __attribute__((ext_vector_type(2)));
+            if (m < a.M) *reinterpret_cast<fl2*>(a.LNS[trunk] + 2 * (size_t)m) = fl2{mu1[rt], rs1[rt]};
+          }
+        }
+      }
+    } else if (!PPO_DIAG_SKIP(4)) {
+      store_tile_rows<FT, RT>(a.H1[trunk], H, z, m0, a.M, rbase, fbase, j, g, PPO_DIAG_SKIP(14));
+    }
     if constexpr (BX) lds_store_pieces<FT, RT, LDB, H / 2>(ACT, z, rbase, fbase, j, g);
     else lds_store_tile<FT, RT, LDA>(ACT, z, rbase, fbase, j, g);
     lds_barrier();
@@ -1108,7 +1160,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
     // ---------------- layer 2 ----------------
     f4 x2[FT][RT];  // LN: x_hat2; tanh: h2
     init_bias<FT, RT>(x2, pb, T.b2 + fbase + 4 * g);
-    if constexpr (BX) mm_bx<FT, RT, NT, LDB>(x2, wbx, w2blane, actb_in);
+    if constexpr (BX) mm_bx<FT, RT, NT, LDB>(x2, wbx, w2blane, actb_in, PPO_DIAG_SKIP(13));
     else mm_fr<FT, RT, NT, LDA>(x2, wsw, w2lane, act_in);
     PPO_STAMP(3);
     if constexpr (PREF) pref_data(it + gridDim.x);
@@ -1343,7 +1395,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
     }
     // x2 = dz2
     if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return x2[ft][rt][r]; }, acc + sg.b2, fbase, j, g);
-    if (!PPO_DIAG_SKIP(5)) store_tile_rows<FT, RT>(a.DZ2[trunk], H, x2, m0, a.M, rbase, fbase, j, g);
+    if (!PPO_DIAG_SKIP(5)) store_tile_rows<FT, RT>(a.DZ2[trunk], H, x2, m0, a.M, rbase, fbase, j, g, PPO_DIAG_SKIP(14));
     // the head backward's readers of h2 / GG (ACT) are done: LN2-backward's exchange barrier (rows_total2)
     // follows every wave's head backward; without it (tanh, WF = 1) wait here
     if constexpr (!PPO_V_BAR || !LN || WF == 1) lds_barrier();
@@ -1354,7 +1406,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
 
     // ---------------- dh1 = W2^T dz2 ----------------
     zero<FT, RT>(dh);
-    if constexpr (BX) mm_bx<FT, RT, NT, LDB>(dh, wbx, w2tblane, actb_in);
+    if constexpr (BX) mm_bx<FT, RT, NT, LDB>(dh, wbx, w2tblane, actb_in, PPO_DIAG_SKIP(13));
     else mm_fr<FT, RT, NT, LDA>(dh, wsw, w2tlane, act_in);
     PPO_STAMP(10);
     // ---------------- recompute layer 1, layer-1 backward ----------------
@@ -1407,7 +1459,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
     }
     // z = dz1
     if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return z[ft][rt][r]; }, acc + sg.b1, fbase, j, g);
-    if (!PPO_DIAG_SKIP(6)) store_tile_rows<FT, RT>(a.DZ1[trunk], H, z, m0, a.M, rbase, fbase, j, g);
+    if (!PPO_DIAG_SKIP(6)) store_tile_rows<FT, RT>(a.DZ1[trunk], H, z, m0, a.M, rbase, fbase, j, g, PPO_DIAG_SKIP(14));
     PPO_STAMP(12);
   }
   // ---------------- workgroup result (row groups summed in a fixed order) ----------------

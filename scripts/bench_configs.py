@@ -39,7 +39,9 @@ def run(name, cfg, iters, warmup, options=None):
     steps = cfg.num_envs * cfg.num_steps
     out = {"config": name, **({"options": options} if options else {}), "num_envs": cfg.num_envs, "num_steps": cfg.num_steps, "env_id": cfg.env_id,
            "ms_per_iteration": round(dt * 1e3, 3), "env_steps_per_s": round(steps / dt, 1),
-           "kernels_ms_per_iteration": {k: round(v[0], 3) for k, v in prof.items()}}
+           "kernels_ms_per_iteration": {k: round(v[0], 3) for k, v in prof.items()},
+           "kernels_ms_note": "one separate iteration with a HIP-event pair around every kernel class: each pair "
+                              "adds its own overhead, so the sum can exceed ms_per_iteration (timed without events)"}
     print(json.dumps(out), flush=True)
     tr.close()
 

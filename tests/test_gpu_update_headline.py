@@ -49,6 +49,12 @@ from test_gpu_parity import fill_storage, make_agent, random_params, rel  # noqa
     ("metric_halfcheetah_dw_bf16x9", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "dw_mfma=bf16x9"),
     ("metric_halfcheetah_dw_bf16x8", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "dw_mfma=bf16x8"),
     ("n8_shard_halfcheetah_dw_bf16x9", 1, 256, 17, 6, 512, 32, 0.1, 0.01, 2.5e-4, "dw_mfma=bf16x9"),
+    # the minibatch as launch pairs of M / n rows (create option upd_split: k_upd + k_dwf per pair, the
+    # pairs' slab and dW partial rows summed together), and a ragged last pair (127 968 = 3 x 32 000 +
+    # 31 968 rows)
+    ("metric_halfcheetah_split4", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "upd_split=4"),
+    ("metric_halfcheetah_split2", 1, 256, 17, 6, 4096, 32, 0.1, 0.01, 2.5e-4, "upd_split=2"),
+    ("ragged_split4", 1, 256, 17, 6, 3999, 32, 0.1, 0.01, 2.5e-4, "upd_split=4"),
     # cfg2: ppo_continuous_action Humanoid-v4, E=1024, T=2048, 32 minibatches -> M = 65 536 rows
     # (ppo:489-542; clip 0.2, ent_coef 0, lr 3e-4, ppo:60-67): k_upd2 walks 128 32-row tiles per
     # workgroup pair and k_dw2_dma sums 256 split-K chunks of 256 rows
@@ -353,3 +359,42 @@ def test_upd2_bx6_is_as_accurate_as_fp32_mfma(E, T):
             assert e1 <= 1.5 * e0 + 1e-6, (t, e0, e1)
     for k in ("pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac", "grad_norm"):
         np.testing.assert_allclose(s1[k], s0[k], rtol=2e-5, atol=1e-7, err_msg=k)
+
+
+@pytest.mark.parametrize("E,T,O_", [(4096, 32, 17), (3999, 4, 17), (512, 32, 16), (700, 9, 11), (1024, 8, 20)])
+def test_h1_recompute_is_bitwise_the_stored_h1(E, T, O_):
+    """h1_handoff=recompute (the default where it applies): k_upd writes each row's layer-1 LayerNorm
+    statistics (8 bytes) instead of its 1 KB H1 row, and k_dwf_bx recomputes H1 per 16-row stage from
+    the staged Xn rows with k_upd's own layer-1 chain (W1 swizzled copy, bias init, the same 16x16x4 fp32
+    MFMA k order and last-block k-steps, the same LayerNorm affine + ReLU expression). Against
+    h1_handoff=store on the same minibatch: gradient, stepped parameters and loss statistics bitwise
+    equal — at the metric minibatch (M = 131 072: 128 chunks, one output slice), ragged (M = 15 996),
+    the small-minibatch geometry (two output slices) and the other layer-1 shapes (OP = 16 / 32, one or
+    four k-steps in the last k block)."""
+    M = E * T
+    rng = np.random.default_rng(43)
+    A, H = 6, 256
+    L = O.layout_init(1, O_, A, H)
+    p = random_params(L, rng)
+    x = rng.standard_normal((M, O_)).astype(np.float32)
+    act = rng.uniform(-0.95, 0.95, (M, A)).astype(np.float32)
+    olp = (rng.standard_normal(M) * 0.3 - 3.0).astype(np.float32)
+    adv = rng.standard_normal(M).astype(np.float32)
+    ret = rng.standard_normal(M).astype(np.float32)
+    ov = rng.standard_normal(M).astype(np.float32)
+    perm = rng.permutation(M).astype(np.int32)
+    out = []
+    for opt in ("h1_handoff=store", "h1_handoff=recompute"):
+        ag = make_agent(1, O_, A, H, E, T=T, MB=1, EP=1, clip=0.2, ent=0.01, options=opt)
+        try:
+            assert ("h1rc" in ag.kernel_info()) == opt.endswith("recompute"), ag.kernel_info()
+            ag.load_params(p)
+            fill_storage(ag, T, E, x, act, olp, adv, ret, ov)
+            st = ag.update(2.5e-4, perms=DeviceArray.from_numpy(perm), want_stats=True)
+            out.append((ag.last_grad(), ag.params(), st))
+        finally:
+            ag.close()
+    (g0, p0, s0), (g1, p1, s1) = out
+    np.testing.assert_array_equal(g1, g0)
+    np.testing.assert_array_equal(p1, p0)
+    assert s0 == s1

@@ -301,7 +301,7 @@ struct CreateOptions {
   int h1_handoff = -1;   // h1_handoff=auto|store|recompute: H1 rows from k_upd, or recomputed by k_dwf_bx
   // 1: ppo_update replays its minibatch launches as one captured hipGraph; 0 (default): eager.
   // Snapshots work with it on (ppo_read_snapshot waits for the snapshot's event on the host).
-  int update_graph = 0;
+  int update_graph = -1;  // -1 auto (kUpdGraphAutoRows), 0 eager, 1 graph
   int rollout_kernel = 0;  // 0 auto, 1 mfma (k_rollout), 2 valu (k_rollout_v)
   int upd2_split = -1;  // -1 auto (= kUpd2SplitAuto: the single k_upd2), 0 one k_upd2, 2 / 3 split at 2 / 3 workgroups per CU
   int upd_mfma = 0;     // 0 auto (bx6 where it applies, else 16), 16: k_upd (16x16x4 fp32 MFMAs),
@@ -335,6 +335,7 @@ static int kUpdSplitAuto(int M) { (void)M; return 1; }
 // stored_h1) took k_upd 0.605 -> 0.573 ms per launch but k_dwf_bx 217 -> 255 us (its extra fp32 MFMAs and a
 // barrier per stage): 15.97 -> 16.04 ms per metric iteration (profiles/r06/h1_recompute/)
 static constexpr bool kH1RecomputeAuto = false;
+static constexpr int kUpdGraphAutoRows = 4096;  // update_graph=auto: minibatches of at most this many rows
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
   std::string s(opts);
@@ -368,7 +369,7 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
       o->values_mfma = v == "auto" ? -1 : v == "f32" ? 0 : 6;
     else if (k == "dw_mfma" && (v == "auto" || v == "f32" || v == "bf16x9" || v == "bf16x8" || v == "bf16x6"))
       o->dw_bx = v == "auto" ? -1 : v == "f32" ? 0 : v == "bf16x9" ? 9 : v == "bf16x8" ? 8 : 6;
-    else if (k == "update_graph" && (v == "0" || v == "1")) o->update_graph = v[0] - '0';
+    else if (k == "update_graph" && (v == "auto" || v == "0" || v == "1")) o->update_graph = v == "auto" ? -1 : v[0] - '0';
     else if (k == "rollout_kernel" && (v == "auto" || v == "mfma" || v == "valu"))
       o->rollout_kernel = v == "auto" ? 0 : v == "mfma" ? 1 : 2;
     else if (k == "upd2_split" && (v == "auto" || v == "0" || v == "2" || v == "3")) o->upd2_split = v == "auto" ? -1 : v[0] - '0';
@@ -438,7 +439,10 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   c->dw_bx = opt.dw_bx >= 0 ? opt.dw_bx : kDwBxAuto;
   c->rollout_mode = opt.rollout;
   c->gradstep = opt.gradstep;
-  c->update_graph = opt.update_graph;
+  // auto: the graph where the minibatches are small enough that launch overhead shows (cfg1's 64 rows:
+  // 17.9 -> 17.4 ms per iteration); at cfg2 / cfg4 / the shards / the metric config it measured equal or
+  // 0.5-1 % slower (profiles/r06/update_graph/)
+  c->update_graph = opt.update_graph >= 0 ? opt.update_graph : (c->M <= kUpdGraphAutoRows ? 1 : 0);
   c->rollout_kernel = opt.rollout_kernel;
   if (opt.rollout_kernel == 2 && (cfg->net_kind != PPO_NET_LN_BETA || c->K.OP > 32)) {
     delete c;  // nothing allocated yet

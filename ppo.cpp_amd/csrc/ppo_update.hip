@@ -42,6 +42,12 @@
 // a time on one box, but CHAN + BAR + PRE + CH2 together +1.2 % and with TOP +1.5 % on another (the
 // critic's tile 75 K -> 67 K cycles, the actor's 79 K -> 81 K: the launch is the actor's, and the
 // critic's shorter phases leave the actor's loss with fewer partner MFMA gaps). Not kept: all off.
+// 1: the H1 / DZ2 hand-off rows are stored from inside the next GEMM (read back from the LDS pieces,
+// issued after its first weight prefetches) instead of from registers before it (A/B builds). Measured
+// +11 % per launch (spills 31 -> 53, profiles/r06/kupd_defer/): off
+#ifndef PPO_UPD_DEFER
+#define PPO_UPD_DEFER 0
+#endif
 #ifndef PPO_V_CHAN
 #define PPO_V_CHAN 0
 #endif
@@ -210,8 +216,14 @@ constexpr int kBxRing = 3;
 PPO_DEV u32x4 pld4u(PBuf b, int lane_floats, int uni_floats) { return __builtin_bit_cast(u32x4, pld4(b, lane_floats, uni_floats)); }
 // diag_unit0 (stamps build, timing only): every weight unit read from the wave's first unit, so the
 // wave streams 3 KB from the L1 instead of 96 KB from L2 (is the weight stream the GEMMs' bound?)
-template <int FT, int RT, int NKB, int LDB>
-PPO_DEV void mm_bx(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* inb, bool diag_unit0 = false) {
+struct NoMid {
+  PPO_DEV void operator()() const {}
+};
+// mid (PPO_UPD_DEFER): called once, right after the first in-loop weight prefetch — vector-memory work
+// (the hand-off stores) issued there is older than only the weight loads of units D + 1 .., so the
+// wave first waits on it D + 1 units later instead of at the GEMM's first unit
+template <int FT, int RT, int NKB, int LDB, class Mid = NoMid>
+PPO_DEV void mm_bx(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* inb, bool diag_unit0 = false, Mid mid = Mid{}) {
   static_assert(NKB % 2 == 0, "mm_bx: 32-wide k blocks");
   constexpr int NKK = NKB / 2, U = NKK * FT, D = kBxRing, NS = D + 1, PS = 8 * NKB;
   u32x4 ar[NS][3];
@@ -238,6 +250,7 @@ PPO_DEV void mm_bx(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* inb, bool
     for (int ft = 0; ft < FT; ++ft) {
       const int u = kk * FT + ft;
       if (u + D < U) load_unit(u + D, ar[(u + D) % NS]);
+      if (u == 0) mid();
       // pin the prefetch here: the scheduler otherwise sinks it next to its use
       __builtin_amdgcn_sched_barrier(0);
       const u32x4(&av)[3] = ar[u % NS];
@@ -273,6 +286,37 @@ PPO_DEV void lds_store_pieces(float* actb, const f4 (&v)[FT][RT], int rbase, int
       *reinterpret_cast<u32x2*>(q + PS) = u32x2{m0, m1};
       *reinterpret_cast<u32x2*>(q + 2 * PS) = u32x2{l0, l1};
     }
+}
+
+// the hand-off rows store_tile_rows writes, read back from lds_store_pieces' split-bf16 pieces:
+// x = hi + (mid + lo) exactly (hi, mid, lo are consecutive 8-bit slices of x's significand), so the
+// bytes are store_tile_rows' (a -0 comes back as +0)
+template <int FT, int RT, int LDB, int PS>
+PPO_DEV void store_rows_from_pieces(float* __restrict__ dst, int ld, const float* actb, int m0, int M, int rbase,
+                                    int fbase, int j, int g) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int m = m0 + rbase + 16 * rt + j;
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      const int f0 = fbase + 16 * ft;
+      const float* q = actb + (rbase + 16 * rt + j) * LDB + 16 * (f0 >> 5) + 4 * g + 2 * ((f0 >> 4) & 1);
+      const u32x2 h = *reinterpret_cast<const u32x2*>(q);
+      const u32x2 md = *reinterpret_cast<const u32x2*>(q + PS);
+      const u32x2 lo = *reinterpret_cast<const u32x2*>(q + 2 * PS);
+      f4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int w = r >> 1, sh = (r & 1) ? 0 : 16;
+        const float fh = __uint_as_float(((h[w] << sh) & 0xffff0000u));
+        const float fm = __uint_as_float(((md[w] << sh) & 0xffff0000u));
+        const float fl = __uint_as_float(((lo[w] << sh) & 0xffff0000u));
+        v[r] = fh + (fm + fl);
+      }
+      if (m < M) st4(dst + (size_t)m * ld + f0 + 4 * g, v);
+    }
+  }
 }
 
 // bias init: out[ft][rt] = b[fbase + 16 ft + 4 g + r]
@@ -1055,6 +1099,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
   // last XN / ROWS / ACTN read of that tile by then), so the tile top is one barrier and a few loads;
   // the first tile's rows are committed here
   constexpr bool EARLY = PPO_UPD_EARLY && PREF && LN && WF > 1;
+  constexpr bool DEFER = PPO_UPD_DEFER != 0;
   if constexpr (EARLY) {
     lds_barrier();  // SPAR (observation mean / std) is staged
     commit(blockIdx.x);
@@ -1149,7 +1194,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
           }
         }
       }
-    } else if (!PPO_DIAG_SKIP(4)) {
+    } else if (!PPO_DIAG_SKIP(4) && !(DEFER && BX)) {
       store_tile_rows<FT, RT>(a.H1[trunk], H, z, m0, a.M, rbase, fbase, j, g, PPO_DIAG_SKIP(14));
     }
     if constexpr (BX) lds_store_pieces<FT, RT, LDB, H / 2>(ACT, z, rbase, fbase, j, g);
@@ -1160,8 +1205,16 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
     // ---------------- layer 2 ----------------
     f4 x2[FT][RT];  // LN: x_hat2; tanh: h2
     init_bias<FT, RT>(x2, pb, T.b2 + fbase + 4 * g);
-    if constexpr (BX) mm_bx<FT, RT, NT, LDB>(x2, wbx, w2blane, actb_in, PPO_DIAG_SKIP(13));
-    else mm_fr<FT, RT, NT, LDA>(x2, wsw, w2lane, act_in);
+    if constexpr (BX && DEFER) {
+      const bool st_h1 = !a.h1_skip && !PPO_DIAG_SKIP(4);
+      mm_bx<FT, RT, NT, LDB>(x2, wbx, w2blane, actb_in, PPO_DIAG_SKIP(13), [&]() {
+        if (st_h1) store_rows_from_pieces<FT, RT, LDB, H / 2>(a.H1[trunk], H, ACT, m0, a.M, rbase, fbase, j, g);
+      });
+    } else if constexpr (BX) {
+      mm_bx<FT, RT, NT, LDB>(x2, wbx, w2blane, actb_in, PPO_DIAG_SKIP(13));
+    } else {
+      mm_fr<FT, RT, NT, LDA>(x2, wsw, w2lane, act_in);
+    }
     PPO_STAMP(3);
     if constexpr (PREF) pref_data(it + gridDim.x);
     float rs2[RT];
@@ -1395,7 +1448,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
     }
     // x2 = dz2
     if (!PPO_DIAG_SKIP(12)) col_sums<FT, RT>([&](int ft, int rt, int r) { return x2[ft][rt][r]; }, acc + sg.b2, fbase, j, g);
-    if (!PPO_DIAG_SKIP(5)) store_tile_rows<FT, RT>(a.DZ2[trunk], H, x2, m0, a.M, rbase, fbase, j, g, PPO_DIAG_SKIP(14));
+    if (!PPO_DIAG_SKIP(5) && !(DEFER && BX)) store_tile_rows<FT, RT>(a.DZ2[trunk], H, x2, m0, a.M, rbase, fbase, j, g, PPO_DIAG_SKIP(14));
     // the head backward's readers of h2 / GG (ACT) are done: LN2-backward's exchange barrier (rows_total2)
     // follows every wave's head backward; without it (tanh, WF = 1) wait here
     if constexpr (!PPO_V_BAR || !LN || WF == 1) lds_barrier();
@@ -1406,8 +1459,15 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
 
     // ---------------- dh1 = W2^T dz2 ----------------
     zero<FT, RT>(dh);
-    if constexpr (BX) mm_bx<FT, RT, NT, LDB>(dh, wbx, w2tblane, actb_in, PPO_DIAG_SKIP(13));
-    else mm_fr<FT, RT, NT, LDA>(dh, wsw, w2tlane, act_in);
+    if constexpr (BX && DEFER) {
+      mm_bx<FT, RT, NT, LDB>(dh, wbx, w2tblane, actb_in, PPO_DIAG_SKIP(13), [&]() {
+        if (!PPO_DIAG_SKIP(5)) store_rows_from_pieces<FT, RT, LDB, H / 2>(a.DZ2[trunk], H, ACT, m0, a.M, rbase, fbase, j, g);
+      });
+    } else if constexpr (BX) {
+      mm_bx<FT, RT, NT, LDB>(dh, wbx, w2tblane, actb_in, PPO_DIAG_SKIP(13));
+    } else {
+      mm_fr<FT, RT, NT, LDA>(dh, wsw, w2tlane, act_in);
+    }
     PPO_STAMP(10);
     // ---------------- recompute layer 1, layer-1 backward ----------------
     init_bias<FT, RT>(z, pb, T.b1 + fbase + 4 * g);

@@ -1488,6 +1488,7 @@ extern "C" int ppo_kernel_info(const ppo_t* c, char* buf, int len) {
                     : c->use_upd32 ? (c->upd32_mix ? "k_upd32/mix" : "k_upd32")
                     : c->use_upd   ? (c->upd_bx ? "k_upd/bx6" : "k_upd/f32")
                                    : "k_fwdbwd";
+  if (c->use_upd && !c->use_upd2 && c->upd.hw_global) upd += "/hwg";  // actor dW3 sums in its slab row
   const int H = c->K.H, OP = c->K.OP;
   const bool fused = c->dw_fused && H == 256 && (OP == 16 || OP == 32);  // launch_dw's dispatch
   const std::string bxs = c->dw_bx ? "/bf16x" + std::to_string(c->dw_bx) : "/f32";

@@ -102,7 +102,8 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *   dw_rows=<n>, dw_slices=1|2  dW split-K geometry: rows per chunk (multiple of 16; 32 for the
  *                            64-wide agent) and k_dwf output slices; default: automatic
  *   update_graph=auto|0|1  ppo_update's minibatch launches eager or replayed as one (auto: the graph for
- *                            minibatches of at most 4 096 rows, where launch overhead shows, e.g. cfg1)
+ *                            minibatches of at most 4 096 rows, where launch overhead shows, e.g. cfg1; eager
+ *                            once the context has taken a snapshot: the CLIs read snapshots from a writer thread)
  *                            hipGraph captured on the second call (one process, gradstep=split,
  *                            no profiling); the Adam step constants come from a device table, so
  *                            the result is bitwise the eager one. Checkpoint snapshots work with it

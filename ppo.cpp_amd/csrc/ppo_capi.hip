@@ -204,6 +204,7 @@ struct ppo_ctx {
   unsigned* gs_bar = nullptr;           // k_gradstep's grid barrier counter
   unsigned gs_count = 0;                // its arrivals so far
   int update_graph = 0;                 // create option update_graph: replay the minibatch loop as a hipGraph
+  bool update_graph_auto = false;       // ... chosen by update_graph=auto (then off once snapshots are taken)
   hipGraphExec_t upd_exec = nullptr;    // the captured loop (all epochs x minibatches)
   const int32_t* upd_exec_perms = nullptr;
   long upd_calls = 0;
@@ -443,6 +444,7 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   // 17.9 -> 17.4 ms per iteration); at cfg2 / cfg4 / the shards / the metric config it measured equal or
   // 0.5-1 % slower (profiles/r06/update_graph/)
   c->update_graph = opt.update_graph >= 0 ? opt.update_graph : (c->M <= kUpdGraphAutoRows ? 1 : 0);
+  c->update_graph_auto = opt.update_graph < 0;
   c->rollout_kernel = opt.rollout_kernel;
   if (opt.rollout_kernel == 2 && (cfg->net_kind != PPO_NET_LN_BETA || c->K.OP > 32)) {
     delete c;  // nothing allocated yet
@@ -1253,7 +1255,10 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
   // hipGraph replay (update_graph=1, one process, split clip + Adam, no profiling events): captured
   // on the second call (the first warms the launchers' one-time attribute calls), re-captured when
   // the permutation buffer changes; every captured kernel argument is fixed across iterations
-  const bool use_graph = c->update_graph && !multi && !c->gradstep && c->prof_mask == 0;
+  // auto stays eager for a caller that takes snapshots (the CLIs' checkpoint writer thread reads them
+  // while the next update runs: a capture then failed on the GPU box, "operation failed due to a previous
+  // error during capture"); update_graph=1 keeps the graph with snapshots (single-threaded callers)
+  const bool use_graph = c->update_graph && !multi && !c->gradstep && c->prof_mask == 0 && !(c->update_graph_auto && c->snap);
   if (use_graph && c->upd_calls > 0) {
     const int n = EP * MB;
     if (!c->sched) {

@@ -399,6 +399,9 @@ def main():
             if "bf16x6" in kinfo:  # every dW product is six bf16 piece products: 2.5 PF/s / 6
                 roof["dw"]["peak_instruction_mix"] = round(PEAK_BF16_MFMA_TFLOPS / 6, 1)
                 roof["dw"]["frac_instruction_mix"] = round(dw_tf / (PEAK_BF16_MFMA_TFLOPS / 6), 4)
+                roof["dw"]["frac_note"] = ("frac = fp32-product FLOP/s over the fp32 MFMA spec (can pass 1: the products run "
+                                           "as bf16 piece products); frac_instruction_mix = over the peak of the "
+                                           "instructions issued (2.5 PF/s bf16 / 6 products)")
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,

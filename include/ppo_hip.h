@@ -132,7 +132,10 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            n launch pairs over consecutive M / n rows of its permutation: one pair's
  *                            hand-off rows (H1 / DZ1 / DZ2 / Xn, ~6 KB per row) stay cache-resident
  *                            between k_upd's stores and k_dwf's reads; the pairs' partial sums are added
- *                            together (the same gradient up to summation order)
+ *                            together (the same gradient up to summation order); auto = 1 (measured slower)
+ *   h1_handoff=auto|store|recompute  the H1 rows of k_upd's hand-off: stored by k_upd (store, auto) or
+ *                            recomputed inside the fused split-bf16 dW from Xn, W1 and 8 bytes of LayerNorm
+ *                            statistics per row (recompute: bitwise the stored rows; measured slower overall)
  *   values_mfma=auto|bx6|f32 the rollout's critic pass (values of the stored rows and the bootstrap,
  *                            ac:655 / :761): k_vbx, layer 2 as k_upd's six split-bf16 piece products
  *                            (bx6; auto where upd_mfma=bx6 applies: the per-step act kernels then skip
@@ -140,7 +143,13 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            k_values / per-step critic (f32)
  *   gradstep=split|fused     clip_grad_norm_ + Adam: two launches (k_gradnorm, k_adam; default) or
  *                            one cooperative launch (k_gradstep: slower on ROCm 7, whose cooperative
- *                            launch costs ~30 us); bitwise the same
+ *                            launch costs ~30 us); bitwise the same as gradstep=split,gradnorm=slices
+ *   gradnorm=auto|fold|slices  clip_grad_norm_'s per-tensor sums of squares: folded into k_colsum (fold:
+ *                            per-tile sums, each tensor's last tile adds them in tile order; one launch
+ *                            fewer per minibatch) or k_gradnorm's 16 slices per tensor (slices; auto). Fold needs one
+ *                            rank (with an all-reduce between the column sums and the norm, or
+ *                            gradstep=fused, k_gradnorm runs). Deterministic either way; the two differ in
+ *                            the summation order of the squares only
  * An unknown key or value is an error, and so is an option the agent cannot use (upd_mfma=32 / mix /
  * bx6 off the LayerNorm-Beta agent, upd2_split > 0 off the 64-wide Humanoid shape): such a create
  * fails and releases everything it had allocated. */

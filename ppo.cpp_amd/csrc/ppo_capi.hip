@@ -182,6 +182,9 @@ struct ppo_ctx {
   int nchunks = 1, rows_per_chunk = 64, dw_slices = 1;
   float* normout = nullptr;
   float* gnpart = nullptr;
+  float* cs_sq = nullptr;               // gradnorm=fold: k_colsum's per-tile sums of squares
+  unsigned* cs_cnt = nullptr;           // ... and its per-segment arrival counters (reset by each last arriver)
+  int gn_fold = 0;                      // create option gradnorm: 1 fold the norm slices into k_colsum
   float* mbstats = nullptr;  // [EP*MB][8]
   float* snap = nullptr;     // ppo_snapshot_state: P | Am | Av (packed)
   hipEvent_t snap_ev = nullptr;
@@ -292,6 +295,7 @@ struct CreateOptions {
   // cooperative launch costs ~30 us on this stack (measured: cfg1 +8.5 ms per iteration), more
   // than the launch it saves.
   int gradstep = 0;
+  int gradnorm = -1;   // gradnorm=auto|slices|fold: clip_grad_norm_'s sums of squares by k_gradnorm or inside k_colsum
   int dw_rows = 0;     // dW split-K rows per chunk (multiple of 16; 0: auto, ~128 chunks per trunk)
   int dw_slices = 0;   // k_dwf output slices per chunk (1 / 2; 0: auto, dw_slices())
   int dw_dma = 1;      // 1 (default): k_dwf_dma (LDS-DMA staging, three stage buffers); 0: k_dwf
@@ -336,7 +340,8 @@ static int kUpdSplitAuto(int M) { (void)M; return 1; }
 // stored_h1) took k_upd 0.605 -> 0.573 ms per launch but k_dwf_bx 217 -> 255 us (its extra fp32 MFMAs and a
 // barrier per stage): 15.97 -> 16.04 ms per metric iteration (profiles/r06/h1_recompute/)
 static constexpr bool kH1RecomputeAuto = false;
-static constexpr int kUpdGraphAutoRows = 4096;  // update_graph=auto: minibatches of at most this many rows
+static constexpr int kUpdGraphAutoRows = 4096;
+static constexpr int kGradnormFoldAuto = 0;  // gradnorm=auto (fold once measured)  // update_graph=auto: minibatches of at most this many rows
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
   std::string s(opts);
@@ -356,6 +361,7 @@ static int parse_create_options(const char* opts, CreateOptions* o) {
     else if (k == "rollout" && (v == "auto" || v == "per_step"))
       o->rollout = v == "auto" ? PPO_ROLLOUT_AUTO : PPO_ROLLOUT_PER_STEP;
     else if (k == "gradstep" && (v == "fused" || v == "split")) o->gradstep = v == "fused";
+    else if (k == "gradnorm" && (v == "auto" || v == "slices" || v == "fold")) o->gradnorm = v == "auto" ? -1 : v == "fold";
     else if (k == "dw_rows" && !v.empty() && v.size() <= 5 && v.find_first_not_of("0123456789") == std::string::npos &&
              atoi(v.c_str()) % 16 == 0 && atoi(v.c_str()) >= 16 && atoi(v.c_str()) <= 65536)
       o->dw_rows = atoi(v.c_str());  // at most 5 digits: no overflow, no exception across the C-ABI
@@ -440,6 +446,7 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   c->dw_bx = opt.dw_bx >= 0 ? opt.dw_bx : kDwBxAuto;
   c->rollout_mode = opt.rollout;
   c->gradstep = opt.gradstep;
+  c->gn_fold = opt.gradnorm >= 0 ? opt.gradnorm : kGradnormFoldAuto;
   // auto: the graph where the minibatches are small enough that launch overhead shows (cfg1's 64 rows:
   // 17.9 -> 17.4 ms per iteration); at cfg2 / cfg4 / the shards / the metric config it measured equal or
   // 0.5-1 % slower (profiles/r06/update_graph/)
@@ -612,6 +619,8 @@ extern "C" int ppo_create_ex(const ppo_hip_config* cfg, int device, const char* 
   rc |= dmalloc(&c->normout, 2 + PPO_LAYOUT_MAX_TENSORS + 2);
   rc |= dmalloc(&c->gnpart, (size_t)PPO_LAYOUT_MAX_TENSORS * PPO_GN_SPLIT);
   rc |= dmalloc(reinterpret_cast<float**>(&c->gs_bar), 1);
+  rc |= dmalloc(&c->cs_sq, (size_t)c->K.size / 64 + 2 * PPO_MAX_SEGS + 64);
+  rc |= dmalloc(reinterpret_cast<float**>(&c->cs_cnt), PPO_MAX_SEGS);
   rc |= dmalloc(&c->mbstats, (size_t)8 * EP * c->nmb);
   if (rc) {
     ppo_destroy(c);
@@ -633,7 +642,8 @@ extern "C" int ppo_destroy(ppo_t* c) {
   prof_drain(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   float* ptrs[] = {c->P, c->G, c->Am, c->Av, c->W2T[0], c->W2T[1], c->WSW[0], c->WSW[1], c->next_value, c->advstats, c->advsq, c->Xn, c->Z1,
-                   c->normout, c->gnpart, c->mbstats, c->beta_store, reinterpret_cast<float*>(c->gs_bar)};
+                   c->normout, c->gnpart, c->mbstats, c->beta_store, reinterpret_cast<float*>(c->gs_bar), c->cs_sq,
+                   reinterpret_cast<float*>(c->cs_cnt)};
   for (float* p : ptrs)
     if (p) (void)hipFree(p);
   for (int b = 0; b < PPO_BUF_COUNT; ++b)
@@ -1142,6 +1152,27 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
       na.len[na.nt] = c->K.rows[t] * c->K.ld[t];
       na.nt++;
     }
+  // gradnorm=fold: every norm tensor must be exactly one gradient segment of the column sums (and no
+  // all-reduce may change the gradient between them and the norm); otherwise k_gradnorm runs
+  bool fold = c->gn_fold && !multi && !c->gradstep;
+  if (fold) {
+    int hits[PPO_LAYOUT_MAX_TENSORS] = {};
+    for (int k = 0; k < stats_seg0; ++k) {
+      cs.seg_t[k] = -1;
+      const long off = (long)(cs.seg[k].dst - c->G);
+      for (int t = 0; t < na.nt; ++t)
+        if (na.off[t] == off && na.len[t] == cs.seg[k].len) { cs.seg_t[k] = t; hits[t]++; }
+    }
+    for (int t = 0; t < na.nt; ++t) fold = fold && hits[t] == 1;
+    long tiles = 0;
+    for (int k = 0; k < stats_seg0 + 3; ++k) tiles += (k < stats_seg0 ? (cs.seg[k].len + 63) / 64 : 1);
+    fold = fold && tiles <= (long)c->K.size / 64 + 2 * PPO_MAX_SEGS + 64;
+  }
+  for (int k = stats_seg0; k < stats_seg0 + 3; ++k) cs.seg_t[k] = -1;
+  cs.fold = fold ? 1 : 0;
+  cs.sq = c->cs_sq;
+  cs.cnt = c->cs_cnt;
+  cs.part = c->gnpart;
   int tb = -1;
   for (int t = 0; t < c->K.nt; ++t)
     if (c->K.grad[t]) { tb = c->K.poff[t]; break; }
@@ -1241,7 +1272,7 @@ extern "C" int ppo_update_ex(ppo_t* c, float lr, int nsteps, const int32_t* perm
         ProfScope ps(c, PK_ADAM, s);
         if (launch_gradstep(na, ad, c->gs_bar, &c->gs_count, s) != 0) return fail("k_gradstep launch failed");
       } else {
-        {
+        if (!cs.fold) {
           ProfScope ps(c, PK_GRADNORM, s);
           launch_gradnorm(na, s);
         }
@@ -1504,7 +1535,8 @@ extern "C" int ppo_kernel_info(const ppo_t* c, char* buf, int len) {
                                                           : "k_dw";
   const std::string vals = rollout_supported(c->K) != 0 ? "k_act" : c->values_bx ? "k_vbx/bx6"
                            : c->K.kind == PPO_NET_TANH_NORMAL ? "k_values4/f32" : "k_values/f32";
-  const std::string s = "update=" + upd + " dw=" + dw + " values=" + vals;
+  const std::string s = "update=" + upd + " dw=" + dw + " values=" + vals +
+                        (c->gn_fold && !c->gradstep ? " norm=k_colsum" : c->gradstep ? " norm=k_gradstep" : " norm=k_gradnorm");
   snprintf(buf, (size_t)len, "%s", s.c_str());
   return 0;
 }

@@ -1492,6 +1492,45 @@ __global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
 // (ColsumArgs::tile0 = first tile of each segment). A workgroup owns one tile: thread (c, q) sums
 // float4 column c over rows q, q + 16, q + 32, ... (four loads in flight), and the 16 row phases
 // are added in a fixed order through LDS — deterministic, and every workgroup has work.
+// gradnorm=fold, wave 0 of a tile's workgroup (lanes 0..15 hold the squares of the values they wrote):
+// the tile's sum (fixed lane tree) stored write-through (agent-scope atomic store = sc1) and drained
+// before the segment's counter add; the last arriver reads every tile's sum with sc1 loads (no L1 /
+// other-XCD L2 copy can be stale: cdna_hip_programming.md Guideline 16, counter form) and adds them in
+// tile order. Determinism: every sum has a fixed order whatever the arrival order.
+typedef __attribute__((address_space(1))) float gfl;
+typedef __attribute__((address_space(1))) unsigned gu32;
+PPO_DEV void colsum_fold(const ColsumArgs& a, int sgi, int b, float ss) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, 64);  // lanes 0..15: one closed group
+  unsigned ticket = 0;
+  if (lane == 0) {
+    __hip_atomic_store((gfl*)(a.sq + b), ss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ticket = __hip_atomic_fetch_add((gu32*)(a.cnt + sgi), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  ticket = __shfl(ticket, 0, 64);
+  const int t0 = a.tile0[sgi], n = a.tile0[sgi + 1] - t0;
+  if ((int)ticket != n - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the ticket
+  // up to 16 loads in flight per lane (one memory round trip per 1 024 tiles), added in tile order
+  float acc = 0.f;
+  for (int k0 = 0; k0 < n; k0 += 1024) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = k0 + lane + 64 * j;
+      v[j] = __hip_atomic_load((gfl*)(a.sq + t0 + min(k, n - 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc += (k0 + lane + 64 * j < n) ? v[j] : 0.f;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  if (lane < PPO_GN_SPLIT) a.part[a.seg_t[sgi] * PPO_GN_SPLIT + lane] = lane == 0 ? acc : 0.f;
+  if (lane == 0) __hip_atomic_store((gu32*)(a.cnt + sgi), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
   __shared__ f4 part[16][16];
   const int b = blockIdx.x;
@@ -1533,17 +1572,22 @@ __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
     }
     part[q][c] = (acc0 + acc1) + (acc2 + acc3);
     __syncthreads();
+    float ss = 0.f;
     if (q == 0 && i < S.len) {
       f4 t = part[0][c];
 #pragma unroll
       for (int p = 1; p < 16; ++p) t += part[p][c];
-      st4(S.dst + i, t * S.scale);
+      const f4 w = t * S.scale;
+      st4(S.dst + i, w);
+      ss = (w.x * w.x + w.y * w.y) + (w.z * w.z + w.w * w.w);
     }
+    if (a.fold && a.seg_t[sgi] >= 0 && tid < 64) colsum_fold(a, sgi, b, ss);
     return;
   }
   // unaligned / ragged segments (biases of width 1..A, loss stats): same 16 row phases, scalar,
   // 16 columns at a time
   float* sp = reinterpret_cast<float*>(part);
+  float ss = 0.f;
   for (int cb = 0; cb < 64 && col0 + cb < S.len; cb += 16) {
     const long i = col0 + cb + c;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
@@ -1564,10 +1608,13 @@ __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
       float t = sp[c];
 #pragma unroll
       for (int p = 1; p < 16; ++p) t += sp[p * 16 + c];
-      S.dst[i] = t * S.scale;
+      const float w = t * S.scale;
+      S.dst[i] = w;
+      ss += w * w;
     }
     __syncthreads();
   }
+  if (a.fold && a.seg_t[sgi] >= 0 && tid < 64) colsum_fold(a, sgi, b, ss);
 }
 
 // =============================================================================================

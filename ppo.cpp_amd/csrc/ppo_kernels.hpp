@@ -164,6 +164,15 @@ struct ColsumArgs {
   ColsumSeg seg[PPO_MAX_SEGS];
   int tile0[PPO_MAX_SEGS + 1];  // first 64-float tile of each segment (set by launch_colsum)
   int nseg;
+  // gradient-norm fold (create option gradnorm=fold): each tile of a segment that is a whole norm
+  // tensor (seg_t = its NormArgs index, -1: none) stores the sum of squares of the values it wrote in
+  // sq[tile]; the segment's last tile (counter cnt[seg]) adds them in tile order into
+  // part[seg_t * PPO_GN_SPLIT] (the other slices 0) — k_gradnorm's output, one launch fewer
+  int fold;
+  int seg_t[PPO_MAX_SEGS];
+  float* sq;
+  unsigned* cnt;
+  float* part;
 };
 
 struct NormArgs {

@@ -145,7 +145,7 @@ import ppo_amd
 lib = ppo_amd.lib()
 out = []
 for opt in ("upd_kernel=fast", "act_kernel=3", "bogus=1", "dw_fused", "rollout=sometimes", "dw_dma=2",
-            "dw_rows=24", "dw_rows=0", "dw_rows=x", "dw_rows=99999999999", "dw_slices=3", "update_graph=2",
+            "dw_rows=24", "dw_rows=0", "dw_rows=x", "dw_rows=99999999999", "dw_slices=3", "update_graph=2", "gradnorm=x",
             "upd2_split=1", "rollout_kernel=fast", "upd_mfma=8", "upd_mfma=bx9", "gae=parallel", "dw_mfma=bf16", "dw_mfma=x9"):
     cfg = ppo_amd.HipConfig(net_kind=1, obs_dim=17, act_dim=6, hidden=256, num_envs=64, num_steps=8,
                             num_minibatches=1, update_epochs=1)

@@ -386,6 +386,89 @@ def test_full_iteration_vs_oracle(kind):
     assert (d > 2e-5).mean() < 1e-4 and d.max() < 0.5 * lr, ((d > 2e-5).sum(), d.max())
 
 
+@pytest.mark.parametrize("E,EP", [(4096, 2), (512, 4)])
+def test_trainer_iteration_vs_oracle_at_metric_size(E, EP):
+    """One whole AC trainer iteration at the metric shape (E = 4 096, T = 128, 4 minibatches of
+    131 072 rows; 2 of the 4 epochs to bound the oracle's time) and at the N = 8 shard (E = 512:
+    k_rollout_v, 16 minibatches of 16 384 rows), with the split-bf16 defaults, against the oracle:
+    - rollout, teacher-forced per step: the oracle's act (same Philox counters) on the GPU's stored
+      observations of two 64-env blocks at every step, and the oracle env stepped with the GPU's
+      actions for all envs (its observations and rewards vs the GPU's);
+    - GAE on the GPU's rewards / values / dones with the oracle's bootstrap;
+    - the update: the oracle's minibatch chain (Feistel permutations, per-minibatch advantage
+      normalisation, clip_grad_norm_, Adam; ac:786-888) from the GPU's rollout buffers, row sums
+      on a thread pool (minibatch_grad_parallel), against the GPU's parameters after the iteration.
+    Bars: acts / logp / values within the E = 64 full-iteration test's (a Marsaglia-Tsang acceptance
+    flipped by an fp32 rounding may change single samples: at most 1e-4 of them); parameters: every
+    element within 2e-5 except a 1e-3 minority of near-cancelling gradient sums (Adam turns their
+    rounding into lr-sized steps), none beyond 4 lr."""
+    T, MB, O_, A, H = 128, 4, 17, 6, 256
+    cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=E, num_steps=T, num_minibatches=MB, update_epochs=EP,
+                              total_timesteps=E * T * 4)
+    tr = ppo_amd.Trainer(cfg)
+    try:
+        assert tr.agent.kernel_info().startswith("update=k_upd/bx6")
+        p0 = tr.agent.params().copy()
+        tr.iterate()
+        tr.agent.sync()
+        gpu_p = tr.agent.params()
+        g = {k: tr.agent.buffer(b, (T, E)).numpy() for k, b in (("logp", ppo_amd.BUF_LOGPROBS), ("rew", ppo_amd.BUF_REWARDS),
+                                                               ("done", ppo_amd.BUF_DONES), ("val", ppo_amd.BUF_VALUES),
+                                                               ("adv", ppo_amd.BUF_ADVANTAGES), ("ret", ppo_amd.BUF_RETURNS))}
+        gobs = tr.agent.buffer(ppo_amd.BUF_OBS, (T, E, O_)).numpy()
+        gact = tr.agent.buffer(ppo_amd.BUF_ACTIONS, (T, E, A)).numpy()
+    finally:
+        tr.close()
+    L = O.layout_init(1, O_, A, H)
+    # rollout: oracle env driven by the GPU's actions; oracle acts on the GPU's observations
+    oenv = O.SynthEnv(E, O_, A, wrappers=False, gamma=cfg.gamma)
+    nobs = oenv.reset(cfg.seed)
+    np.testing.assert_allclose(gobs[0], nobs, rtol=1e-5, atol=1e-6)
+    blocks = [(0, 64), (E // 2, E // 2 + 64)]
+    bad = tot = 0
+    orew = np.zeros((T, E), np.float32)
+    for t in range(T):
+        if t > 0:
+            np.testing.assert_allclose(gobs[t], nobs, rtol=1e-4, atol=1e-5)
+        for e0, e1 in blocks:
+            a, lp, _, v = O.get_action_and_value(L, p0, gobs[t, e0:e1], 0, seed=cfg.seed, rank=0, env_base=e0, step_id=t)
+            close = np.isclose(gact[t, e0:e1], a, rtol=1e-4, atol=1e-4).all(axis=1)
+            close &= np.isclose(g["logp"][t, e0:e1], lp, rtol=1e-4, atol=1e-3)
+            close &= np.isclose(g["val"][t, e0:e1], v, rtol=2e-5, atol=2e-5)
+            bad += int((~close).sum()); tot += close.size
+        nobs, r, te, trn, _, _ = oenv.step(gact[t])
+        orew[t] = r
+        ndone = np.maximum(te, trn)
+    assert bad <= max(1, 1e-4 * tot), (bad, tot)
+    np.testing.assert_allclose(g["rew"], orew, rtol=1e-5, atol=1e-6)
+    _, _, _, nv = O.get_action_and_value(L, p0, nobs, 2)
+    adv, ret = O.gae(g["rew"], g["val"], g["done"], nv, ndone, cfg.gamma, cfg.gae_lambda)
+    np.testing.assert_allclose(g["adv"], adv, rtol=1e-3, atol=1e-3)
+    np.testing.assert_allclose(g["ret"], ret, rtol=1e-3, atol=1e-3)
+    # update: the oracle's minibatch chain (orc_update's loop) from the GPU's buffers
+    B = T * E
+    Mb = B // MB
+    bo, ba = gobs.reshape(B, O_), gact.reshape(B, A)
+    bl, bad_, br, bv = (g[k].reshape(B) for k in ("logp", "adv", "ret", "val"))
+    lcfg = O.LossCfg(cfg.clip_coef, cfg.ent_coef, cfg.vf_coef, int(cfg.clip_vloss), int(cfg.norm_adv))
+    lr = float(np.float32(1.0) * np.float32(cfg.learning_rate))
+    p = p0.astype(np.float32).copy()
+    m = np.zeros(L.P, np.float32); v = np.zeros(L.P, np.float32)
+    step = 0
+    for e in range(EP):
+        perm = O.perm(B, cfg.seed, 0, e)
+        for s0 in range(0, B, Mb):
+            j = perm[s0:s0 + Mb]
+            grad, _ = O.minibatch_grad_parallel(L, p, bo[j], ba[j], bl[j], bad_[j], br[j], bv[j], lcfg)
+            grad, _ = O.clip_grad_norm(L, grad, cfg.max_grad_norm)
+            step += 1
+            p, m, v = O.adam_step(L, p, grad, m, v, step, lr, cfg.adam_eps)
+    d = np.abs(gpu_p.astype(np.float64) - p)
+    print(f"\nE={E} EP={EP}: params max |d| {d.max():.2e} ({d.max() / lr:.3f} lr), > 2e-5: {(d > 2e-5).sum()} of {d.size}; "
+          f"rollout act mismatches {bad} of {tot}")
+    assert (d > 2e-5).mean() < 1e-3 and d.max() < 4 * lr, ((d > 2e-5).sum(), d.max())
+
+
 # ------------------------------------------------------------------------------------------------
 # metric configuration (AC-PPO HalfCheetah, E=4096, T=128, MB=4, EP=4): size-independent checks
 # ------------------------------------------------------------------------------------------------

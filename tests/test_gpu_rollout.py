@@ -151,12 +151,12 @@ def test_persistent_rollout_metric_shape_properties():
 def test_gradstep_fused_equals_split(agent, env_id, E, T, mb):
     """clip_grad_norm_ + Adam as one cooperative launch (k_gradstep, gradstep=fused: the norm slices,
     a grid barrier, the Adam blocks) against the two launches k_gradnorm + k_adam (gradstep=split,
-    the default): the same functions in the same order, so parameters, Adam moments and the
+    gradnorm=slices): the same functions in the same order, so parameters, Adam moments and the
     per-minibatch total norm are bitwise equal after two iterations (many minibatches: the barrier
     counter runs across launches)."""
     C = ppo_amd.ACPPOConfig if agent == "ac" else ppo_amd.PPOConfig
     cfg = C(env_id=env_id, num_envs=E, num_steps=T, num_minibatches=mb, update_epochs=2, total_timesteps=E * T * 4)
-    trs = [ppo_amd.Trainer(cfg, options="gradstep=fused"), ppo_amd.Trainer(cfg, options="gradstep=split")]
+    trs = [ppo_amd.Trainer(cfg, options="gradstep=fused"), ppo_amd.Trainer(cfg, options="gradstep=split,gradnorm=slices")]
     for _ in range(2):
         st = [tr.iterate(want_stats=True) for tr in trs]
     np.testing.assert_array_equal(trs[0].agent.params(), trs[1].agent.params())
@@ -168,6 +168,37 @@ def test_gradstep_fused_equals_split(agent, env_id, E, T, mb):
     assert st[0]["grad_norm"] == st[1]["grad_norm"]
     for tr in trs:
         tr.close()
+
+
+@pytest.mark.parametrize("agent,env_id,E,T,mb", [("ac", "HalfCheetah-v5", 256, 128, 4), ("ppo", "Humanoid-v4", 64, 64, 32),
+                                                 ("ppo", "HalfCheetah-v5", 1, 256, 4), ("ac", "Ant-v5", 96, 64, 2)])
+def test_gradnorm_fold_matches_slices(agent, env_id, E, T, mb):
+    """clip_grad_norm_'s sums of squares folded into k_colsum (gradnorm=fold: per-tile
+    sums, the last tile of each tensor adds them in tile order through the agent-scope counter
+    hand-off) against k_gradnorm's 16 slices per tensor (gradnorm=slices): the same values summed in
+    another order, so the per-minibatch total norms agree to fp32 rounding and the parameters after
+    two iterations stay within the update tests' bars; the fold is deterministic (two runs bitwise)."""
+    C = ppo_amd.ACPPOConfig if agent == "ac" else ppo_amd.PPOConfig
+    cfg = C(env_id=env_id, num_envs=E, num_steps=T, num_minibatches=mb, update_epochs=2, total_timesteps=E * T * 4)
+    trs = [ppo_amd.Trainer(cfg, options="gradnorm=fold"), ppo_amd.Trainer(cfg, options="gradnorm=fold"),
+           ppo_amd.Trainer(cfg, options="gradnorm=slices")]
+    try:
+        assert trs[0].agent.kernel_info().endswith("norm=k_colsum")
+        assert trs[2].agent.kernel_info().endswith("norm=k_gradnorm")
+        norms = [[], [], []]
+        for _ in range(2):
+            for i, tr in enumerate(trs):
+                norms[i].append(tr.iterate(want_stats=True)["grad_norm"])
+        p = [tr.agent.params() for tr in trs]
+        np.testing.assert_array_equal(p[0], p[1])
+        assert norms[0] == norms[1]
+        np.testing.assert_allclose(norms[0], norms[2], rtol=1e-5)
+        d = np.abs(p[0].astype(np.float64) - p[2])
+        lr = float(cfg.learning_rate)
+        assert (d > 2e-5).mean() < 1e-3 and d.max() < 2 * lr, ((d > 2e-5).sum(), d.max())
+    finally:
+        for tr in trs:
+            tr.close()
 
 
 @pytest.mark.parametrize("agent,env_id,E,T,mb,it", [("ac", "HalfCheetah-v5", 256, 128, 4, 3), ("ppo", "Humanoid-v4", 64, 64, 32, 3),

@@ -340,8 +340,8 @@ static int kUpdSplitAuto(int M) { (void)M; return 1; }
 // stored_h1) took k_upd 0.605 -> 0.573 ms per launch but k_dwf_bx 217 -> 255 us (its extra fp32 MFMAs and a
 // barrier per stage): 15.97 -> 16.04 ms per metric iteration (profiles/r06/h1_recompute/)
 static constexpr bool kH1RecomputeAuto = false;
-static constexpr int kUpdGraphAutoRows = 4096;
-static constexpr int kGradnormFoldAuto = 0;  // gradnorm=auto (fold once measured)  // update_graph=auto: minibatches of at most this many rows
+static constexpr int kUpdGraphAutoRows = 4096;  // update_graph=auto: minibatches of at most this many rows
+static constexpr int kGradnormFoldAuto = 0;     // gradnorm=auto: k_gradnorm (fold: opt-in until measured)
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
   std::string s(opts);

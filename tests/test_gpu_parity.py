@@ -7,6 +7,8 @@ Tolerances (fp32 throughout, MFMA f32 = exact fp32 FMA chains, oracle accumulate
   parameters after Adam                     atol 2e-6 per step (lr = 2.5e-4 .. 3e-4)
   GAE, env dynamics, permutations           bit-exact
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -386,8 +388,9 @@ def test_full_iteration_vs_oracle(kind):
     assert (d > 2e-5).mean() < 1e-4 and d.max() < 0.5 * lr, ((d > 2e-5).sum(), d.max())
 
 
-@pytest.mark.parametrize("E,EP", [(4096, 2), (512, 4)])
-def test_trainer_iteration_vs_oracle_at_metric_size(E, EP):
+@pytest.mark.parametrize("E,EP,opts", [(4096, 2, None), (512, 4, None),
+                                        (512, 4, "upd_mfma=16,dw_mfma=f32,values_mfma=f32")])
+def test_trainer_iteration_vs_oracle_at_metric_size(E, EP, opts):
     """One whole AC trainer iteration at the metric shape (E = 4 096, T = 128, 4 minibatches of
     131 072 rows; 2 of the 4 epochs to bound the oracle's time) and at the N = 8 shard (E = 512:
     k_rollout_v, 16 minibatches of 16 384 rows), with the split-bf16 defaults, against the oracle:
@@ -399,15 +402,20 @@ def test_trainer_iteration_vs_oracle_at_metric_size(E, EP):
       normalisation, clip_grad_norm_, Adam; ac:786-888) from the GPU's rollout buffers, row sums
       on a thread pool (minibatch_grad_parallel), against the GPU's parameters after the iteration.
     Bars: acts / logp / values within the E = 64 full-iteration test's (a Marsaglia-Tsang acceptance
-    flipped by an fp32 rounding may change single samples: at most 1e-4 of them); parameters: every
-    element within 2e-5 except a 1e-3 minority of near-cancelling gradient sums (Adam turns their
-    rounding into lr-sized steps), none beyond 4 lr."""
+    flipped by an fp32 rounding may change single samples: at most 1e-4 of them); parameters: the
+    median within 2e-6, 99 % within 5e-5, at most 3 % beyond 2e-5, none beyond lr. The tail is the
+    actor's near-zero gradients: with |g| ~ 1e-6 (Adam's v ~ 1e-12, below eps = 1e-5) the fp32 sums
+    of a minibatch keep a relative rounding error that the fp64 oracle does not, and each Adam step
+    turns it into a fraction of lr. Measured (MI355X): E = 4 096, 2 epochs (8 steps): max 7.0e-6,
+    none beyond 2e-5; E = 512, 4 epochs (16 steps): max 1.26e-4 (0.5 lr), 1.4 % beyond 2e-5 with
+    the split-bf16 defaults and 1.7 % with every GEMM on fp32 MFMAs (same max): the fp32 arithmetic,
+    not the split products; 1 epoch at E = 512: max 7.3e-6."""
     T, MB, O_, A, H = 128, 4, 17, 6, 256
     cfg = ppo_amd.ACPPOConfig(env_id="HalfCheetah-v5", num_envs=E, num_steps=T, num_minibatches=MB, update_epochs=EP,
                               total_timesteps=E * T * 4)
-    tr = ppo_amd.Trainer(cfg)
+    tr = ppo_amd.Trainer(cfg, options=opts)
     try:
-        assert tr.agent.kernel_info().startswith("update=k_upd/bx6")
+        assert tr.agent.kernel_info().startswith("update=k_upd/bx6" if opts is None else "update=k_upd/f32")
         p0 = tr.agent.params().copy()
         tr.iterate()
         tr.agent.sync()
@@ -464,9 +472,21 @@ def test_trainer_iteration_vs_oracle_at_metric_size(E, EP):
             step += 1
             p, m, v = O.adam_step(L, p, grad, m, v, step, lr, cfg.adam_eps)
     d = np.abs(gpu_p.astype(np.float64) - p)
-    print(f"\nE={E} EP={EP}: params max |d| {d.max():.2e} ({d.max() / lr:.3f} lr), > 2e-5: {(d > 2e-5).sum()} of {d.size}; "
+    print(f"\nE={E} EP={EP} {opts}: params max |d| {d.max():.2e} ({d.max() / lr:.3f} lr), > 2e-5: {(d > 2e-5).sum()} of {d.size}; "
           f"rollout act mismatches {bad} of {tot}")
-    assert (d > 2e-5).mean() < 1e-3 and d.max() < 4 * lr, ((d > 2e-5).sum(), d.max())
+    print("|d| quantiles 0.5 / 0.9 / 0.99 / 0.999:", np.quantile(d, [0.5, 0.9, 0.99, 0.999]))
+    if os.environ.get("PPO_TEST_DIAG"):
+        offs = [(int(L.t_off[i]), int(L.t_len[i])) for i in range(L.ntensors)]
+        for k in np.argsort(-d)[:12]:
+            ti = [i for i, (o, n) in enumerate(offs) if o <= k < o + n]
+            print(f"  elem {k} tensor {ti} p0 {p0[k]:+.6e} gpu {gpu_p[k]:+.6e} oracle {p[k]:+.6e} m {m[k]:+.3e} v {v[k]:.3e}")
+        big = d > 2e-5
+        for i, (o, n) in enumerate(offs):
+            nb = int(big[o:o + n].sum())
+            if nb:
+                print(f"  tensor {i} off {o} len {n}: {nb} elements > 2e-5, max {d[o:o + n].max():.2e}")
+    q50, q99 = np.quantile(d, [0.5, 0.99])
+    assert q50 < 2e-6 and q99 < 5e-5 and (d > 2e-5).mean() < 0.03 and d.max() < lr, (q50, q99, (d > 2e-5).sum(), d.max())
 
 
 # ------------------------------------------------------------------------------------------------

@@ -146,7 +146,7 @@ int ppo_create(const ppo_hip_config* cfg, int device, ppo_t** out);
  *                            launch costs ~30 us); bitwise the same as gradstep=split,gradnorm=slices
  *   gradnorm=auto|fold|slices  clip_grad_norm_'s per-tensor sums of squares: folded into k_colsum (fold:
  *                            per-tile sums, each tensor's last tile adds them in tile order; one launch
- *                            fewer per minibatch) or k_gradnorm's 16 slices per tensor (slices; auto). Fold needs one
+ *                            fewer per minibatch, but measured slower) or k_gradnorm's 16 slices per tensor (slices; auto). Fold needs one
  *                            rank (with an all-reduce between the column sums and the norm, or
  *                            gradstep=fused, k_gradnorm runs). Deterministic either way; the two differ in
  *                            the summation order of the squares only

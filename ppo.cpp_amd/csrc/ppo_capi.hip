@@ -341,7 +341,10 @@ static int kUpdSplitAuto(int M) { (void)M; return 1; }
 // barrier per stage): 15.97 -> 16.04 ms per metric iteration (profiles/r06/h1_recompute/)
 static constexpr bool kH1RecomputeAuto = false;
 static constexpr int kUpdGraphAutoRows = 4096;  // update_graph=auto: minibatches of at most this many rows
-static constexpr int kGradnormFoldAuto = 0;     // gradnorm=auto: k_gradnorm (fold: opt-in until measured)
+// gradnorm=auto: k_gradnorm. The fold measured slower everywhere (E = 512 shard 3.44 -> 3.78 ms, cfg2 87.5 -> 88.7,
+// cfg1 17.4 -> 17.9: each tile's write-through store + counter round trip costs more than the launch it
+// saves; profiles/r06/gradnorm_fold/)
+static constexpr int kGradnormFoldAuto = 0;
 static int parse_create_options(const char* opts, CreateOptions* o) {
   if (!opts) return 0;
   std::string s(opts);

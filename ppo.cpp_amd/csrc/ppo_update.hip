@@ -48,6 +48,16 @@
 #ifndef PPO_UPD_DEFER
 #define PPO_UPD_DEFER 0
 #endif
+// 1: the head weights (NHT = 1) held in registers from the tile top (16 VGPRs); 0: loaded at each use.
+// Measured 0: k_upd 0.610 -> 0.602 ms per launch (spills 31 -> 28; results bitwise equal, profiles/r06/kupd_hwb/)
+#ifndef PPO_V_HWB
+#define PPO_V_HWB 0
+#endif
+// 1: the next tile's permutation entries requested after the layer-2 GEMM and its rows after the dh1 GEMM
+// (shorter register live ranges), 0: at the tile top and after the layer-2 GEMM (A/B)
+#ifndef PPO_V_PLATE
+#define PPO_V_PLATE 0
+#endif
 #ifndef PPO_V_CHAN
 #define PPO_V_CHAN 0
 #endif
@@ -212,7 +222,10 @@ PPO_DEV void mm_fr(f4 (&out)[FT][RT], PBuf wb, int wlane, const float* in) {
 // A pieces stream through a ring of NS units (D = NS - 1 ahead, ~ one 32-k block of every feature tile).
 // weight-piece ring depth (32-k units in flight ahead): 2 / 3 / 4 / 5 measured 0.62 / 0.61 / 0.65 /
 // 0.69 ms per launch (deeper rings spill; profiles/r05/bx6/abm2, abm3)
-constexpr int kBxRing = 3;
+#ifndef PPO_BX_RING
+#define PPO_BX_RING 3
+#endif
+constexpr int kBxRing = PPO_BX_RING;
 PPO_DEV u32x4 pld4u(PBuf b, int lane_floats, int uni_floats) { return __builtin_bit_cast(u32x4, pld4(b, lane_floats, uni_floats)); }
 // diag_unit0 (stamps build, timing only): every weight unit read from the wave's first unit, so the
 // wave streams 3 KB from the L1 instead of 96 KB from L2 (is the weight stream the GEMMs' bound?)
@@ -1123,7 +1136,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
       pref_idx(it + gridDim.x);
     } else if constexpr (PREF) {
       commit(it);
-      pref_idx(it + gridDim.x);
+      if constexpr (!PPO_V_PLATE) pref_idx(it + gridDim.x);
     } else {
       if (tid < R) nperm = a.perm[min((it + (int)gridDim.x) * R + tid, a.M - 1)];
       gather_sync(it);
@@ -1133,7 +1146,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
     // are requested here, a whole forward pass before their first use, instead of in the head
     // phases (where they were the only loads a wave waited on outside the matrix phases)
     f4 hwb[FT];
-    if constexpr (NHT == 1) {
+    if constexpr (NHT == 1 && PPO_V_HWB) {
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
         if (trunk == 0) {
@@ -1216,7 +1229,8 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
       mm_fr<FT, RT, NT, LDA>(x2, wsw, w2lane, act_in);
     }
     PPO_STAMP(3);
-    if constexpr (PREF) pref_data(it + gridDim.x);
+    if constexpr (PREF && (!PPO_V_PLATE || EARLY)) pref_data(it + gridDim.x);
+    if constexpr (PREF && PPO_V_PLATE && !EARLY) pref_idx(it + gridDim.x);
     float rs2[RT];
     if constexpr (LN) {
       float mu2[RT];
@@ -1268,7 +1282,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
       for (int rt = 0; rt < RT; ++rt) pv[rt] = 0.f;
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
-        const f4 w = NHT == 1 ? hwb[ft] : pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
+        const f4 w = (NHT == 1 && PPO_V_HWB) ? hwb[ft] : pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
           // no LDS copy of the critic's h2: its head backward and dW3 column sums read registers
@@ -1363,7 +1377,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
       for (int rt = 0; rt < RT; ++rt) gr[rt] = lds_f(GG + (rbase + 16 * rt + j) * LDG);
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
-        const f4 w = NHT == 1 ? hwb[ft] : pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
+        const f4 w = (NHT == 1 && PPO_V_HWB) ? hwb[ft] : pld4(pb, K.cW3 + fbase + 4 * g, 16 * ft);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -1376,7 +1390,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
 #pragma unroll
       for (int ft = 0; ft < FT; ++ft) {
         f4 wT;
-        if constexpr (NHT == 1) {
+        if constexpr (NHT == 1 && PPO_V_HWB) {
           wT = hwb[ft];
         } else {
 #pragma unroll
@@ -1469,6 +1483,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
       mm_fr<FT, RT, NT, LDA>(dh, wsw, w2tlane, act_in);
     }
     PPO_STAMP(10);
+    if constexpr (PREF && PPO_V_PLATE && !EARLY) pref_data(it + gridDim.x);
     // ---------------- recompute layer 1, layer-1 backward ----------------
     init_bias<FT, RT>(z, pb, T.b1 + fbase + 4 * g);
     mm_fr<FT, RT, NTO, LDX, KL1>(z, wsw, w1lane, xn_in);

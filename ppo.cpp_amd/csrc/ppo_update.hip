@@ -55,6 +55,10 @@
 #endif
 // 1: the next tile's permutation entries requested after the layer-2 GEMM and its rows after the dh1 GEMM
 // (shorter register live ranges), 0: at the tile top and after the layer-2 GEMM (A/B)
+// 1: no register prefetch of the next tile's rows (each tile gathers its rows at its top; A/B)
+#ifndef PPO_V_NOPREF
+#define PPO_V_NOPREF 0
+#endif
 #ifndef PPO_V_PLATE
 #define PPO_V_PLATE 0
 #endif
@@ -908,7 +912,7 @@ PPO_DEV void upd16_body(const UpdArgs& a) {
   // Gather prefetch, two stages one tile ahead: permutation indices at the top of a tile, the
   // rows' data after its forward pass; committed to LDS at the top of the next tile.
   // (register-staged only for narrow inputs; wide ones (O > 32) gather synchronously)
-  constexpr bool PREF = (R * OP + 255) / 256 <= 4;
+  constexpr bool PREF = (R * OP + 255) / 256 <= 4 && !PPO_V_NOPREF;
   constexpr int NG = PREF ? (R * OP + 255) / 256 : 1;   // gather items per thread
   constexpr int NAI = PREF ? (R * PPO_UPD_MAXA + 255) / 256 : 1;  // action items per thread
   int pg[NG], pra, pac[NAI];

@@ -1281,6 +1281,11 @@ __global__ __launch_bounds__(512) void k_dwf_dma(DwArgs a) {
 // rows, W1 (swizzled copy, staged once per workgroup in W1S) and the bias / LayerNorm affine (PRM) —
 // k_upd's chain, so bitwise the H1 rows k_upd would have stored; k_upd then writes 8 bytes per row
 // instead of 1 KB (the hand-off's H1 third).
+// cache policy of k_dwf_bx's hand-off stream (read once): 2 non-temporal (dW 3.41 -> 3.31 ms per metric
+// iteration, bitwise the same; profiles/r06/dw_nt/), 0 the default policy
+#ifndef PPO_DW_AUX
+#define PPO_DW_AUX 2
+#endif
 template <int H, int OP, bool RC>
 struct DwbxGeo {
   static constexpr int KS = 16, LDH = H, LDX = OP;
@@ -1363,7 +1368,7 @@ __global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
         const uint32_t voff = row < m1 ? (uint32_t)((row * H) * 4 + lane * 16) : 0xFFFFFFF0u;
         __builtin_amdgcn_raw_ptr_buffer_load_lds((s3 == 0 ? bdz2 : s3 == 1 ? bh1 : bdz1).r,
                                                  (__attribute__((address_space(3))) void*)(b + dst + r * LDH), 16,
-                                                 voff, 0, 0, 0);
+                                                 voff, 0, 0, PPO_DW_AUX);
       }
     }
     if (RC && wave == 7) {  // the stage's 16 rows x (mean, 1 / std): 32 dwords (lanes 32..63 zero-fill the pad)
@@ -1377,7 +1382,7 @@ __global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
       const long row = mb + r;
       const uint32_t voff = row < m1 ? (uint32_t)((row * OP + (e - r * OP)) * 4) : 0xFFFFFFF0u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(bxn.r, (__attribute__((address_space(3))) void*)(b + oXN + wave * 256), 16,
-                                               voff, 0, 0, 0);
+                                               voff, 0, 0, PPO_DW_AUX);
     }
   };
   const bool xw = wave < NXI;

@@ -1286,6 +1286,17 @@ __global__ __launch_bounds__(512) void k_dwf_dma(DwArgs a) {
 #ifndef PPO_DW_AUX
 #define PPO_DW_AUX 2
 #endif
+// k_dwf_bx's split-K partials (read once by k_colsum): PPO_DW_NTST = 1 stores them non-temporal (A/B)
+#ifndef PPO_DW_NTST
+#define PPO_DW_NTST 0
+#endif
+PPO_DEV void dw_st(float* p, float v) {
+#if PPO_DW_NTST
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 template <int H, int OP, bool RC>
 struct DwbxGeo {
   static constexpr int KS = 16, LDH = H, LDX = OP;
@@ -1485,8 +1496,8 @@ __global__ __launch_bounds__(512) void k_dwf_bx(DwArgs a) {
     for (int u = 0; u < TOW; ++u)
 #pragma unroll
       for (int v = 0; v < TIW; ++v)
-        out[(size_t)(obase + (wo * TOW + u) * 32 + orow) * H + (wi * TIW + v) * 32 + l32] = acc[u][v][r];
-    if (w1_wave && l32 < OP) out[(size_t)H * H + (size_t)(w1row + orow) * OP + l32] = acc1[r];
+        dw_st(out + (size_t)(obase + (wo * TOW + u) * 32 + orow) * H + (wi * TIW + v) * 32 + l32, acc[u][v][r]);
+    if (w1_wave && l32 < OP) dw_st(out + (size_t)H * H + (size_t)(w1row + orow) * OP + l32, acc1[r]);
   }
 }
 
@@ -1536,6 +1547,17 @@ PPO_DEV void colsum_fold(const ColsumArgs& a, int sgi, int b, float ss) {
   if (lane == 0) __hip_atomic_store((gu32*)(a.cnt + sgi), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// split-K partials are read once: PPO_CS_NT = 1 loads them non-temporal (A/B)
+#ifndef PPO_CS_NT
+#define PPO_CS_NT 0
+#endif
+PPO_DEV f4 cs_ld4(const float* p) {
+#if PPO_CS_NT
+  return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
+#else
+  return ld4(p);
+#endif
+}
 __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
   __shared__ f4 part[16][16];
   const int b = blockIdx.x;
@@ -1554,10 +1576,10 @@ __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
       // eight loads in flight (one round trip for the usual 128 chunks); each accumulator still
       // takes its rows in the order of the four-wide loop below, so the sums are unchanged
       for (; r + 112 < S.count; r += 128) {
-        const f4 x0 = ld4(src + (size_t)r * S.stride), x1 = ld4(src + (size_t)(r + 16) * S.stride);
-        const f4 x2 = ld4(src + (size_t)(r + 32) * S.stride), x3 = ld4(src + (size_t)(r + 48) * S.stride);
-        const f4 x4 = ld4(src + (size_t)(r + 64) * S.stride), x5 = ld4(src + (size_t)(r + 80) * S.stride);
-        const f4 x6 = ld4(src + (size_t)(r + 96) * S.stride), x7 = ld4(src + (size_t)(r + 112) * S.stride);
+        const f4 x0 = cs_ld4(src + (size_t)r * S.stride), x1 = cs_ld4(src + (size_t)(r + 16) * S.stride);
+        const f4 x2 = cs_ld4(src + (size_t)(r + 32) * S.stride), x3 = cs_ld4(src + (size_t)(r + 48) * S.stride);
+        const f4 x4 = cs_ld4(src + (size_t)(r + 64) * S.stride), x5 = cs_ld4(src + (size_t)(r + 80) * S.stride);
+        const f4 x6 = cs_ld4(src + (size_t)(r + 96) * S.stride), x7 = cs_ld4(src + (size_t)(r + 112) * S.stride);
         acc0 += x0;
         acc1 += x1;
         acc2 += x2;
@@ -1568,12 +1590,12 @@ __global__ __launch_bounds__(256) void k_colsum(ColsumArgs a) {
         acc3 += x7;
       }
       for (; r + 48 < S.count; r += 64) {
-        acc0 += ld4(src + (size_t)r * S.stride);
-        acc1 += ld4(src + (size_t)(r + 16) * S.stride);
-        acc2 += ld4(src + (size_t)(r + 32) * S.stride);
-        acc3 += ld4(src + (size_t)(r + 48) * S.stride);
+        acc0 += cs_ld4(src + (size_t)r * S.stride);
+        acc1 += cs_ld4(src + (size_t)(r + 16) * S.stride);
+        acc2 += cs_ld4(src + (size_t)(r + 32) * S.stride);
+        acc3 += cs_ld4(src + (size_t)(r + 48) * S.stride);
       }
-      for (; r < S.count; r += 16) acc0 += ld4(src + (size_t)r * S.stride);
+      for (; r < S.count; r += 16) acc0 += cs_ld4(src + (size_t)r * S.stride);
     }
     part[q][c] = (acc0 + acc1) + (acc2 + acc3);
     __syncthreads();

@@ -115,12 +115,18 @@ PPO_DEV PBuf make_pbuf_b(const void* base, uint32_t bytes) {
 constexpr uint32_t kOOB = 0xFFFFFFF0u;  // a byte offset past every buffer: the DMA writes zeros
 // LDS DMA: every lane of the wave loads `size` bytes at its byte offset into lds_wave + lane * size
 // (lds_wave must be wave-uniform); completion is counted by vmcnt
-template <int SIZE>
+template <int SIZE, int AUX = 0>
 PPO_DEV void dma(PBuf b, float* lds_wave, uint32_t voff) {
   auto* l = (__attribute__((address_space(3))) void*)lds_wave;
-  if constexpr (SIZE == 16) __builtin_amdgcn_raw_ptr_buffer_load_lds(b.r, l, 16, voff, 0, 0, 0);
-  else __builtin_amdgcn_raw_ptr_buffer_load_lds(b.r, l, 4, voff, 0, 0, 0);
+  if constexpr (SIZE == 16) __builtin_amdgcn_raw_ptr_buffer_load_lds(b.r, l, 16, voff, 0, 0, AUX);
+  else __builtin_amdgcn_raw_ptr_buffer_load_lds(b.r, l, 4, voff, 0, 0, AUX);
 }
+// cache policy of k_dw2_dma's read-once streams (gathered X rows, DZ1 / DZ2 / H1 blocks): 2 non-temporal
+// (cfg2 88.8 -> 88.3 ms per iteration: k_colsum then finds more of the split-K partials in cache; bitwise
+// the same; profiles/r06/dw2_nt/), 0 the default policy
+#ifndef PPO_DW2_AUX
+#define PPO_DW2_AUX 2
+#endif
 
 // Column sums over the 16 rows j of a lane group: x[4 ft + r] (feature 16 ft + 4 g + r of this lane's
 // row) is reduce-scattered with DPP partners j ^ 8 (row_ror:8), the mirror in each half, the mirror in
@@ -1297,7 +1303,7 @@ __global__ __launch_bounds__(512) void k_dw2_dma(DwArgs a) {
       const long m = m0 + (long)st * KS + row;
       const int pr = pw[row - 2 * wave];
       const uint32_t voff = (m < m1 && 4 * q < O) ? (uint32_t)(pr * O + 4 * q) * 4u : kOOB;
-      dma<16>(ob, b + i * 256, voff);
+      dma<16, PPO_DW2_AUX>(ob, b + i * 256, voff);
     }
 #pragma unroll
     for (int y = 0; y < 3; ++y) {  // row-block instruction i: source i / 4, rows 4 (i % 4) .. + 3
@@ -1305,7 +1311,7 @@ __global__ __launch_bounds__(512) void k_dw2_dma(DwArgs a) {
       const long m = m0 + (long)st * KS + row;
       const uint32_t voff = m < m1 ? (uint32_t)((m * H + 4 * (lane & 15)) * 4) : kOOB;
       const PBuf bs = src == 0 ? bz0 : src == 1 ? bz1 : src == 2 ? bz2 : src == 3 ? bz3 : src == 4 ? bz4 : bz5;
-      dma<16>(bs, b + oZ + src * KS * H + r0 * H, voff);
+      dma<16, PPO_DW2_AUX>(bs, b + oZ + src * KS * H + r0 * H, voff);
     }
   };
   perm_dma(0);

@@ -20,6 +20,11 @@
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
+// cache policy of k_dw_dma's read-once streams (the two-phase dW of wide inputs, e.g. Ant): 0 default,
+// 2 non-temporal (A/B)
+#ifndef PPO_DWD_AUX
+#define PPO_DWD_AUX 0
+#endif
 
 // =============================================================================================
 // k_act
@@ -920,13 +925,13 @@ PPO_DEV void dw_phase_dma(const float* __restrict__ DZ, const float* __restrict_
         const long row = mb + i / (NO / 256);
         const uint32_t voff = row < m1 ? (uint32_t)(((long)i * 256 + mb * NO) * 4 + lane * 16) : 0xFFFFFFF0u;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(bdz.r, (__attribute__((address_space(3))) void*)(b + i * 256), 16,
-                                                 voff, 0, 0, 0);
+                                                 voff, 0, 0, PPO_DWD_AUX);
       } else if (i < NT) {
         const int e = (i - ND) * 256 + lane * 4;  // float of the stage's IN block
         const long row = mb + e / LDI;
         const uint32_t voff = row < m1 ? (uint32_t)((mb * LDI + e) * 4) : 0xFFFFFFF0u;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(bin.r, (__attribute__((address_space(3))) void*)(b + ADZ + (i - ND) * 256),
-                                                 16, voff, 0, 0, 0);
+                                                 16, voff, 0, 0, PPO_DWD_AUX);
       }
     }
   };
